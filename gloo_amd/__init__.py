@@ -1,0 +1,32 @@
+"""gloo_amd -- MI355X-native gloo allreduce hot path.
+
+The drop-in surface of liuxiaotiao/gloo for its data-parallel allreduce:
+gloo::Context / rendezvous, gloo::Algorithm with AllreduceRingChunked and
+AllreduceHalvingDoubling, ReductionFunction, and the elementwise reductions
+of gloo/math.h -- executed on MI355X GPUs (HIP kernels for gfx950, chunks
+moved between the GPUs of a node with hipMemcpyPeerAsync over xGMI).
+The native library (libgloo_amd.so, C ABI in include/gloo_amd/glx.h) is
+required; there is no CPU fallback.
+"""
+from . import _lib  # noqa: F401  (raises ImportError if the HIP build is missing)
+from . import math, rendezvous  # noqa: F401
+from .algorithms import (  # noqa: F401
+    AllreduceHalvingDoubling,
+    AllreduceRingChunked,
+    HipAllreduceHalvingDoubling,
+    HipAllreduceRingChunked,
+    ReductionFunction,
+    ReductionType,
+    plan,
+)
+from .errors import EnforceNotMet, Exception, HipError, IoException  # noqa: F401,A004
+
+__version__ = _lib.lib.glx_version().decode()
+LIB_PATH = _lib.LIB_PATH
+
+
+def device_count():
+    import ctypes
+    n = ctypes.c_int(0)
+    _lib.lib.glx_device_count(ctypes.byref(n))
+    return n.value

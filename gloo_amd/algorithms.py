@@ -1,0 +1,175 @@
+"""Class-style allreduce algorithms on device buffers (gloo/algorithm.h).
+
+    alg = AllreduceRingChunked(context, [t0], count, ReductionFunction.sum)
+    alg.run()
+
+Buffers are torch tensors on the context's device (or raw device pointers
+with an explicit dtype).  Constructor shape follows
+CudaAllreduceRingChunked<T>(context, ptrs, count, streams)
+(gloo/cuda_allreduce_ring_chunked.h:22-26).
+"""
+import ctypes
+
+from . import _lib
+from .errors import check, check_handle
+
+lib = _lib.lib
+
+# dtype codes (glx_dtype)
+INT8, UINT8, INT32, INT64, UINT64, FLOAT32, FLOAT64, FLOAT16, BFLOAT16 = range(9)
+
+
+class ReductionType:
+    """gloo::ReductionType (gloo/algorithm.h:49-57)."""
+    SUM = 1
+    PRODUCT = 2
+    MAX = 3
+    MIN = 4
+
+
+class ReductionFunction:
+    """gloo::ReductionFunction<T> singletons (gloo/algorithm.h:59-96).  The
+    element type comes from the buffers, so one object serves every T."""
+
+    def __init__(self, type_):
+        self._type = type_
+
+    def type(self):
+        return self._type
+
+    def __repr__(self):
+        names = {1: "sum", 2: "product", 3: "max", 4: "min"}
+        return "ReductionFunction.%s" % names[self._type]
+
+
+ReductionFunction.sum = ReductionFunction(ReductionType.SUM)
+ReductionFunction.product = ReductionFunction(ReductionType.PRODUCT)
+ReductionFunction.max = ReductionFunction(ReductionType.MAX)
+ReductionFunction.min = ReductionFunction(ReductionType.MIN)
+
+
+def torch_dtype_code(t):
+    import torch
+    table = {
+        torch.int8: INT8, torch.uint8: UINT8, torch.int32: INT32,
+        torch.int64: INT64, torch.float32: FLOAT32, torch.float64: FLOAT64,
+        torch.float16: FLOAT16, torch.bfloat16: BFLOAT16,
+    }
+    if hasattr(torch, "uint64"):
+        table[torch.uint64] = UINT64
+    if t.dtype not in table:
+        raise TypeError("unsupported dtype %s" % t.dtype)
+    return table[t.dtype]
+
+
+def _as_ptrs(bufs, dtype):
+    """tensors or ints -> (list of device pointers, dtype code, min numel)."""
+    ptrs, numel = [], None
+    for b in bufs:
+        if isinstance(b, int):
+            if dtype is None:
+                raise TypeError("raw pointers need an explicit dtype")
+            ptrs.append(b)
+            continue
+        if not b.is_cuda:
+            raise ValueError("buffers must be device tensors (got %s)" % b.device)
+        if not b.is_contiguous():
+            raise ValueError("buffers must be contiguous")
+        code = torch_dtype_code(b)
+        if dtype is None:
+            dtype = code
+        elif dtype != code:
+            raise TypeError("all buffers must share one dtype")
+        ptrs.append(b.data_ptr())
+        numel = b.numel() if numel is None else min(numel, b.numel())
+    return ptrs, dtype, numel
+
+
+def _stream_ptr(s):
+    if s is None:
+        return None
+    if isinstance(s, int):
+        return s
+    return s.cuda_stream  # torch.cuda.Stream
+
+
+class Algorithm:
+    """gloo::Algorithm (gloo/algorithm.h:20-38)."""
+
+    _create = None
+
+    def __init__(self, context, ptrs, count=None, fn=None, streams=None, dtype=None):
+        if fn is None:
+            fn = ReductionFunction.sum
+        if not isinstance(ptrs, (list, tuple)):
+            ptrs = [ptrs]
+        self.context = context
+        self._keep = list(ptrs)  # keep tensors alive for the object's lifetime
+        pp, dt, numel = _as_ptrs(ptrs, dtype)
+        if count is None:
+            if numel is None:
+                raise ValueError("count is required with raw pointers")
+            count = numel
+        if numel is not None and count > numel:
+            raise ValueError("count %d exceeds buffer size %d" % (count, numel))
+        self.count = int(count)
+        self.dtype = dt
+        self.fn = fn
+        arr = (ctypes.c_void_p * len(pp))(*pp)
+        if streams:
+            sp = [_stream_ptr(s) for s in streams]
+            sarr = (ctypes.c_void_p * len(sp))(*sp)
+            ns = len(sp)
+        else:
+            sarr, ns = None, 0
+        self._streams = streams
+        self._h = check_handle(
+            type(self)._create(context.handle, arr, len(pp), self.count, dt, fn.type(),
+                               sarr, ns),
+            type(self).__name__)
+
+    def run(self):
+        check(lib.glx_algorithm_run(self._h), type(self).__name__ + ".run")
+
+    def bytes_sent(self):
+        """Bytes this rank moves over peer links per run()."""
+        return lib.glx_algorithm_bytes_sent(self._h)
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib.glx_algorithm_destroy(h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+class AllreduceRingChunked(Algorithm):
+    """gloo::AllreduceRingChunked<T> (gloo/allreduce_ring_chunked.h:19) on
+    MI355X: xGMI peer copies + HIP reduce kernel, same chunking and order."""
+    _create = lib.glx_allreduce_ring_chunked_create
+
+
+class AllreduceHalvingDoubling(Algorithm):
+    """gloo::AllreduceHalvingDoubling<T> (gloo/allreduce_halving_doubling.h:37)."""
+    _create = lib.glx_allreduce_halving_doubling_create
+
+
+# The device classes under the names the reference's GPU path uses.
+HipAllreduceRingChunked = AllreduceRingChunked
+HipAllreduceHalvingDoubling = AllreduceHalvingDoubling
+
+
+def plan(algo, rank, size, count):
+    """The step program of one rank (host logic, no GPU).  algo: 'ring_chunked'
+    or 'halving_doubling'.  Returns (steps as list of 8-tuples, scratch_elems)."""
+    code = {"ring_chunked": 0, "halving_doubling": 1}[algo]
+    scratch = ctypes.c_int64(0)
+    n = lib.glx_plan(code, rank, size, count, None, 0, ctypes.byref(scratch))
+    if n < 0:
+        check(_lib.ERR_INVALID, "plan")
+    buf = (ctypes.c_int64 * (8 * max(n, 1)))()
+    lib.glx_plan(code, rank, size, count, buf, n, ctypes.byref(scratch))
+    steps = [tuple(buf[8 * i: 8 * i + 8]) for i in range(n)]
+    return steps, scratch.value

@@ -1,0 +1,322 @@
+// capi.cc -- the extern "C" boundary (include/gloo_amd/glx.h).
+// Every entry point catches, records the message for glx_last_error() and
+// returns a GLX_ERR_* code; nothing throws across the ABI.
+#include <hip/hip_runtime_api.h>
+
+#include <cstring>
+#include <memory>
+#include <string>
+
+#include "../../include/gloo_amd/glx.h"
+#include "common.h"
+#include "context.h"
+#include "executor.h"
+#include "kernels.h"
+#include "plan.h"
+#include "store.h"
+
+struct glx_store {
+  std::shared_ptr<gloo::rendezvous::Store> s;
+};
+struct glx_context {
+  std::shared_ptr<gloo::Context> c;
+};
+struct glx_algorithm {
+  std::unique_ptr<gloo::HipPlanExecutor> a;
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+template <typename F>
+int guarded(F&& f) {
+  try {
+    g_last_error.clear();
+    return f();
+  } catch (const gloo::TimeoutException& e) {
+    return fail(GLX_ERR_TIMEOUT, e.what());
+  } catch (const gloo::IoException& e) {
+    return fail(GLX_ERR_IO, e.what());
+  } catch (const gloo::HipError& e) {
+    return fail(GLX_ERR_HIP, e.what());
+  } catch (const gloo::EnforceNotMet& e) {
+    return fail(GLX_ERR_ENFORCE, e.what());
+  } catch (const std::logic_error& e) {
+    return fail(GLX_ERR_INVALID, e.what());
+  } catch (const std::exception& e) {
+    return fail(GLX_ERR_INTERNAL, e.what());
+  } catch (...) {
+    return fail(GLX_ERR_INTERNAL, "unknown exception");
+  }
+}
+
+int hipStatus(hipError_t e, const char* what) {
+  if (e == hipSuccess) return GLX_OK;
+  return fail(GLX_ERR_HIP, std::string(what) + ": " + hipGetErrorName(e) + ": " +
+                               hipGetErrorString(e));
+}
+
+bool validDtype(int d) { return d >= GLX_INT8 && d <= GLX_BFLOAT16; }
+bool validOp(int o) { return o >= GLX_SUM && o <= GLX_MIN; }
+
+glx_algorithm* makeAlgorithm(int algo, glx_context* ctx, void* const* ptrs, int nptrs,
+                             int count, int dtype, int op, const glx_stream_t* streams,
+                             int nstreams) {
+  glx_algorithm* out = nullptr;
+  guarded([&]() -> int {
+    GLX_ENFORCE(ctx != nullptr, "null context");
+    GLX_ENFORCE(ptrs != nullptr && nptrs > 0, "need at least one pointer");
+    GLX_ENFORCE(nstreams == 0 || streams != nullptr, "null streams array");
+    std::vector<void*> p(ptrs, ptrs + nptrs);
+    std::vector<hipStream_t> s;
+    for (int i = 0; i < nstreams; i++) s.push_back((hipStream_t)streams[i]);
+    std::unique_ptr<gloo::HipPlanExecutor> a(
+        new gloo::HipPlanExecutor(ctx->c, algo, p, count, dtype, op, s));
+    out = new glx_algorithm{std::move(a)};
+    return GLX_OK;
+  });
+  return out;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* glx_last_error(void) { return g_last_error.c_str(); }
+
+const char* glx_version(void) { return "0.1.0"; }
+
+size_t glx_dtype_size(int dtype) {
+  static const size_t sz[] = {1, 1, 4, 8, 8, 4, 8, 2, 2};
+  return validDtype(dtype) ? sz[dtype] : 0;
+}
+
+int glx_reduce(int op, int dtype, void* dst, const void* a, const void* b, size_t n,
+               glx_stream_t stream) {
+  if (!validOp(op)) return fail(GLX_ERR_INVALID, "glx_reduce: unknown op");
+  if (!validDtype(dtype)) return fail(GLX_ERR_INVALID, "glx_reduce: unknown dtype");
+  if (n > 0 && (dst == nullptr || a == nullptr || b == nullptr)) {
+    return fail(GLX_ERR_INVALID, "glx_reduce: null pointer");
+  }
+  return hipStatus(glx::launch_reduce(op, dtype, dst, a, b, n, (hipStream_t)stream),
+                   "glx_reduce");
+}
+
+int glx_reduce_n(int op, int dtype, void* dst, const void* const* srcs, int k, size_t n,
+                 glx_stream_t stream) {
+  if (!validOp(op)) return fail(GLX_ERR_INVALID, "glx_reduce_n: unknown op");
+  if (!validDtype(dtype)) return fail(GLX_ERR_INVALID, "glx_reduce_n: unknown dtype");
+  if (k < 2 || k > 8 || srcs == nullptr) {
+    return fail(GLX_ERR_INVALID, "glx_reduce_n: need 2..8 sources");
+  }
+  return hipStatus(glx::launch_reduce_n(op, dtype, dst, srcs, k, n, (hipStream_t)stream),
+                   "glx_reduce_n");
+}
+
+int glx_peer_copy(void* dst, int dst_dev, const void* src, int src_dev, size_t bytes,
+                  glx_stream_t stream) {
+  if (bytes == 0) return GLX_OK;
+  if (dst == nullptr || src == nullptr) return fail(GLX_ERR_INVALID, "glx_peer_copy: null");
+  return hipStatus(hipMemcpyPeerAsync(dst, dst_dev, src, src_dev, bytes, (hipStream_t)stream),
+                   "hipMemcpyPeerAsync");
+}
+
+int glx_enable_peer(int a, int b) {
+  if (a == b) return GLX_OK;
+  int cur = 0;
+  hipGetDevice(&cur);
+  for (int pass = 0; pass < 2; pass++) {
+    int from = pass == 0 ? a : b, to = pass == 0 ? b : a;
+    hipError_t e = hipSetDevice(from);
+    if (e == hipSuccess) e = hipDeviceEnablePeerAccess(to, 0);
+    if (e == hipErrorPeerAccessAlreadyEnabled) {
+      (void)hipGetLastError();
+      e = hipSuccess;
+    }
+    if (e != hipSuccess) {
+      hipSetDevice(cur);
+      return hipStatus(e, "hipDeviceEnablePeerAccess");
+    }
+  }
+  hipSetDevice(cur);
+  return GLX_OK;
+}
+
+int glx_device_count(int* count) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    n = 0;
+  }
+  if (count) *count = n;
+  return GLX_OK;
+}
+
+// ---- stores ----------------------------------------------------------------
+
+glx_store* glx_hash_store_create(void) {
+  return new glx_store{std::make_shared<gloo::rendezvous::HashStore>()};
+}
+
+glx_store* glx_file_store_create(const char* path) {
+  glx_store* out = nullptr;
+  guarded([&]() -> int {
+    GLX_ENFORCE(path != nullptr, "null path");
+    out = new glx_store{std::make_shared<gloo::rendezvous::FileStore>(path)};
+    return GLX_OK;
+  });
+  return out;
+}
+
+glx_store* glx_prefix_store_create(const char* prefix, glx_store* base) {
+  if (prefix == nullptr || base == nullptr) return nullptr;
+  return new glx_store{std::make_shared<gloo::rendezvous::PrefixStore>(prefix, base->s)};
+}
+
+glx_store* glx_callback_store_create(glx_store_set_fn set_fn, glx_store_get_fn get_fn,
+                                     void* user) {
+  if (set_fn == nullptr || get_fn == nullptr) return nullptr;
+  return new glx_store{std::make_shared<gloo::rendezvous::CallbackStore>(set_fn, get_fn, user)};
+}
+
+void glx_store_destroy(glx_store* store) { delete store; }
+
+int glx_store_set(glx_store* store, const char* key, const void* data, size_t len) {
+  return guarded([&]() -> int {
+    GLX_ENFORCE(store != nullptr && key != nullptr, "null store/key");
+    const char* d = static_cast<const char*>(data);
+    store->s->set(key, std::vector<char>(d, d + (d ? len : 0)));
+    return GLX_OK;
+  });
+}
+
+int glx_store_get(glx_store* store, const char* key, void* buf, size_t cap,
+                  size_t* len_out, int64_t timeout_ms) {
+  return guarded([&]() -> int {
+    GLX_ENFORCE(store != nullptr && key != nullptr, "null store/key");
+    auto v = store->s->get(key, std::chrono::milliseconds(timeout_ms));
+    if (buf != nullptr && cap > 0) memcpy(buf, v.data(), std::min(cap, v.size()));
+    if (len_out) *len_out = v.size();
+    return GLX_OK;
+  });
+}
+
+// ---- context -----------------------------------------------------------------
+
+glx_context* glx_context_create(int rank, int size, int device) {
+  glx_context* out = nullptr;
+  guarded([&]() -> int {
+    out = new glx_context{std::make_shared<gloo::Context>(rank, size, device)};
+    return GLX_OK;
+  });
+  return out;
+}
+
+void glx_context_destroy(glx_context* ctx) { delete ctx; }
+
+int glx_context_connect_full_mesh(glx_context* ctx, glx_store* store) {
+  return guarded([&]() -> int {
+    GLX_ENFORCE(ctx != nullptr && store != nullptr, "null context/store");
+    ctx->c->connectFullMesh(store->s);
+    return GLX_OK;
+  });
+}
+
+int glx_context_rank(glx_context* ctx) { return ctx ? ctx->c->rank : -1; }
+int glx_context_size(glx_context* ctx) { return ctx ? ctx->c->size : -1; }
+int glx_context_device(glx_context* ctx) { return ctx ? ctx->c->device() : -1; }
+
+int glx_context_set_timeout(glx_context* ctx, int64_t timeout_ms) {
+  return guarded([&]() -> int {
+    GLX_ENFORCE(ctx != nullptr, "null context");
+    GLX_ENFORCE(timeout_ms >= 0, "negative timeout");
+    ctx->c->setTimeout(std::chrono::milliseconds(timeout_ms));
+    return GLX_OK;
+  });
+}
+
+int64_t glx_context_get_timeout(glx_context* ctx) {
+  return ctx ? (int64_t)ctx->c->getTimeout().count() : -1;
+}
+
+int glx_context_next_slot(glx_context* ctx, int num_to_skip) {
+  int slot = -1;
+  int rc = guarded([&]() -> int {
+    GLX_ENFORCE(ctx != nullptr, "null context");
+    slot = ctx->c->nextSlot(num_to_skip);
+    return GLX_OK;
+  });
+  return rc == GLX_OK ? slot : -1;
+}
+
+// ---- algorithms --------------------------------------------------------------
+
+glx_algorithm* glx_allreduce_ring_chunked_create(glx_context* ctx, void* const* ptrs,
+                                                 int nptrs, int count, int dtype, int op,
+                                                 const glx_stream_t* streams,
+                                                 int nstreams) {
+  return makeAlgorithm(glx::ALGO_RING_CHUNKED, ctx, ptrs, nptrs, count, dtype, op,
+                       streams, nstreams);
+}
+
+glx_algorithm* glx_allreduce_halving_doubling_create(glx_context* ctx, void* const* ptrs,
+                                                     int nptrs, int count, int dtype,
+                                                     int op, const glx_stream_t* streams,
+                                                     int nstreams) {
+  return makeAlgorithm(glx::ALGO_HALVING_DOUBLING, ctx, ptrs, nptrs, count, dtype, op,
+                       streams, nstreams);
+}
+
+int glx_algorithm_run(glx_algorithm* alg) {
+  return guarded([&]() -> int {
+    GLX_ENFORCE(alg != nullptr, "null algorithm");
+    alg->a->run();
+    return GLX_OK;
+  });
+}
+
+int64_t glx_algorithm_bytes_sent(glx_algorithm* alg) {
+  return alg ? alg->a->bytesSentPerRun() : -1;
+}
+
+void glx_algorithm_destroy(glx_algorithm* alg) {
+  guarded([&]() -> int {
+    delete alg;
+    return GLX_OK;
+  });
+}
+
+// ---- plan introspection --------------------------------------------------------
+
+int64_t glx_plan(int algo, int rank, int size, int64_t count, int64_t* steps, int64_t cap,
+                 int64_t* scratch_elems) {
+  int64_t n = -1;
+  guarded([&]() -> int {
+    glx::Plan p = glx::makePlan(algo, rank, size, count);
+    n = (int64_t)p.steps.size();
+    if (scratch_elems) *scratch_elems = p.scratch_elems;
+    for (int64_t i = 0; i < n && i < cap && steps != nullptr; i++) {
+      const glx::Step& s = p.steps[(size_t)i];
+      int64_t* o = steps + 8 * i;
+      o[0] = s.kind;
+      o[1] = s.peer;
+      o[2] = s.channel;
+      o[3] = s.off;
+      o[4] = s.len;
+      o[5] = s.boff;
+      o[6] = s.dst_off;
+      o[7] = s.flags;
+    }
+    return GLX_OK;
+  });
+  return n;
+}
+
+}  // extern "C"

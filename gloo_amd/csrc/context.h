@@ -1,0 +1,115 @@
+// context.h -- gloo::Context for the in-node xGMI device transport.
+//
+// Replaces gloo::Context (gloo/context.h:26-58) + rendezvous::Context
+// (gloo/rendezvous/context.h:25-35) + the transport Device/Pair factory
+// (gloo/transport/device.h:49, gloo/transport/pair.h:33-37).
+//
+// Data never touches the host: payload moves GPU->GPU with
+// hipMemcpyPeerAsync into the peer's device receive regions.  What the TCP
+// transport does with sockets and an epoll thread (completion of a message,
+// "inbox free" notifications) is done here with 64-bit monotonic counters in
+// a per-rank POSIX shared-memory control block that every rank of the node
+// maps: a sender bumps the receiver's delivery counter once its copy has
+// completed (observed with hipEventQuery), a receiver bumps the sender's
+// credit counter once the kernel that consumed the message has completed.
+// Ranks may be threads of one process (the reference's test topology,
+// gloo/test/base_test.h:91-166) or one process per GPU (torchrun).
+#pragma once
+
+#include <sys/types.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "store.h"
+
+namespace gloo {
+
+// One rank's control block: kWords counters, one per 64-byte line.
+class ControlBlock {
+ public:
+  static constexpr size_t kWords = 16384;
+  static constexpr size_t kLine = 64;
+  static constexpr size_t kBytes = kWords * kLine;
+
+  ControlBlock() = default;
+  ~ControlBlock();
+  ControlBlock(const ControlBlock&) = delete;
+  ControlBlock& operator=(const ControlBlock&) = delete;
+
+  void create(const std::string& name);  // shm_open(O_CREAT) + mmap
+  void open(const std::string& name);    // map a peer's block
+  void unlink();                         // drop the name (mappings stay)
+
+  std::atomic<uint64_t>* word(uint32_t i) const {
+    return reinterpret_cast<std::atomic<uint64_t>*>(base_ + (size_t)i * kLine);
+  }
+  const std::string& name() const { return name_; }
+
+  // Local word allocator (only on the owner's block).
+  uint32_t allocWord();
+  void freeWord(uint32_t i);
+
+ private:
+  std::string name_;
+  char* base_ = nullptr;
+  bool owner_ = false;
+  bool unlinked_ = false;
+  std::mutex m_;
+  std::vector<uint32_t> free_;
+  uint32_t next_ = 1;  // word 0 reserved
+};
+
+struct PeerEndpoint {
+  int rank = -1;
+  pid_t pid = 0;
+  int device = -1;       // device ordinal in the peer's process
+  int localDevice = -1;  // the same GPU's ordinal in this process (-1: unknown)
+  bool sameProcess = false;
+  std::string shmName;
+  std::unique_ptr<ControlBlock> ctl;  // mapped peer control block
+};
+
+class Context {
+ public:
+  Context(int rank, int size, int device);
+  ~Context();
+
+  const int rank;
+  const int size;
+
+  int device() const { return device_; }
+
+  // gloo/rendezvous/context.cc:43-113
+  void connectFullMesh(std::shared_ptr<rendezvous::Store> store);
+  bool connected() const { return connected_; }
+
+  int nextSlot(int numToSkip = 1);  // gloo/context.cc:49-54
+
+  void setTimeout(std::chrono::milliseconds t) { timeout_ = t; }  // gloo/context.cc:61
+  std::chrono::milliseconds getTimeout() const { return timeout_; }
+
+  rendezvous::Store& store() { return *store_; }
+  ControlBlock& localControl() { return local_; }
+  PeerEndpoint& peer(int r) { return peers_.at(r); }
+
+  // Throws IoException if a peer process has exited.
+  void checkPeersAlive();
+
+ private:
+  int device_;
+  int slot_ = 0;
+  bool connected_ = false;
+  std::chrono::milliseconds timeout_{30000};  // gloo/context.cc:18
+  std::shared_ptr<rendezvous::Store> store_;
+  ControlBlock local_;
+  std::vector<PeerEndpoint> peers_;
+  std::string busId_;
+};
+
+}  // namespace gloo

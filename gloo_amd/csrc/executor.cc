@@ -1,0 +1,420 @@
+// executor.cc -- see executor.h.
+#include "executor.h"
+
+#include <immintrin.h>
+#include <sched.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <map>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace gloo {
+
+namespace {
+
+constexpr uint32_t kAlgMagic = 0x474c5841u;  // "GLXA"
+
+template <typename T>
+void putPod(std::vector<char>& b, const T& v) {
+  b.insert(b.end(), (const char*)&v, (const char*)&v + sizeof(T));
+}
+
+template <typename T>
+T getPod(const std::vector<char>& b, size_t& at) {
+  GLX_ENFORCE(at + sizeof(T) <= b.size(), "truncated algorithm record");
+  T v;
+  memcpy(&v, b.data() + at, sizeof(T));
+  at += sizeof(T);
+  return v;
+}
+
+enum { DIR_IN = 0, DIR_OUT = 1 };
+
+}  // namespace
+
+HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
+                                 const std::vector<void*>& ptrs, int64_t count,
+                                 int dtype, int op,
+                                 const std::vector<hipStream_t>& streams)
+    : Algorithm(ctx), algo_(algo), ptrs_(ptrs), count_(count), dtype_(dtype), op_(op) {
+  GLX_ENFORCE(!ptrs.empty(), "at least one buffer pointer is required");
+  GLX_ENFORCE(count >= 0 && count <= INT32_MAX, "count out of range: ", count);
+  esize_ = glx_dtype_size(dtype);
+  GLX_ENFORCE(esize_ > 0, "unknown dtype ", dtype);
+  GLX_ENFORCE(op >= GLX_SUM && op <= GLX_MIN, "unknown reduction op ", op);
+  GLX_ENFORCE(streams.empty() || streams.size() == ptrs.size(),
+              "streams must be empty or one per pointer (got ", streams.size(),
+              " for ", ptrs.size(), " pointers)");
+  GLX_ENFORCE(ptrs.size() <= 8, "at most 8 local pointers are supported");
+  for (void* p : ptrs) GLX_ENFORCE(p != nullptr || count == 0, "null buffer pointer");
+  GLX_ENFORCE(contextSize_ == 1 || ctx->connected(),
+              "context must be connected (connectFullMesh) before creating algorithms");
+  device_ = ctx->device();
+  GLX_HIP_CHECK(hipSetDevice(device_));
+  slot_ = ctx->nextSlot();
+  plan_ = glx::makePlan(algo, contextRank_, contextSize_, count);
+
+  userStream_ = !streams.empty();
+  if (userStream_) {
+    compute_ = streams[0];
+  } else {
+    GLX_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
+    ownCompute_ = true;
+  }
+  GLX_HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
+  myPhase_ = (int)((uintptr_t)ptrs[0] % 16);
+
+  if (plan_.scratch_elems > 0) {
+    scratchBytes_ = (size_t)plan_.scratch_elems * esize_ + 64;
+    GLX_HIP_CHECK(hipMalloc((void**)&scratch_, scratchBytes_));
+    GLX_HIP_CHECK(hipMemset(scratch_, 0, scratchBytes_));
+    GLX_HIP_CHECK(hipDeviceSynchronize());
+  }
+
+  // Channels named by the plan; allocate our counter words.
+  auto& ctl = ctx->localControl();
+  stepChan_.assign(plan_.steps.size(), -1);
+  for (size_t i = 0; i < plan_.steps.size(); i++) {
+    const auto& s = plan_.steps[i];
+    if (s.kind == glx::SEND) {
+      int idx = outIndex((int)s.peer, (int)s.channel);
+      if (idx < 0) {
+        OutChan oc;
+        oc.peer = (int)s.peer;
+        oc.tag = (int)s.channel;
+        oc.creditWord = ctl.allocWord();
+        oc.credit = ctl.word(oc.creditWord);
+        out_.push_back(oc);
+        idx = (int)out_.size() - 1;
+      }
+      stepChan_[i] = idx;
+    } else if (s.kind == glx::RECV || s.kind == glx::RELEASE) {
+      int idx = inIndex((int)s.peer, (int)s.channel);
+      if (idx < 0) {
+        InChan ic;
+        ic.peer = (int)s.peer;
+        ic.tag = (int)s.channel;
+        ic.deliveryWord = ctl.allocWord();
+        ic.delivery = ctl.word(ic.deliveryWord);
+        in_.push_back(ic);
+        idx = (int)in_.size() - 1;
+      }
+      stepChan_[i] = idx;
+    }
+  }
+  events_.resize(plan_.steps.size(), nullptr);
+  for (auto& e : events_) GLX_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  GLX_HIP_CHECK(hipEventCreateWithFlags(&computeMark_, hipEventDisableTiming));
+  if (contextSize_ > 1 && count_ > 0) publish();
+}
+
+HipPlanExecutor::~HipPlanExecutor() noexcept(false) {
+  hipSetDevice(device_);
+  if (compute_ != nullptr) hipStreamSynchronize(compute_);
+  if (copy_ != nullptr) hipStreamSynchronize(copy_);
+  for (void* p : ipcOpened_) hipIpcCloseMemHandle(p);
+  for (auto& e : events_) hipEventDestroy(e);
+  if (computeMark_) hipEventDestroy(computeMark_);
+  if (scratch_) hipFree(scratch_);
+  if (copy_) hipStreamDestroy(copy_);
+  if (ownCompute_ && compute_) hipStreamDestroy(compute_);
+  auto& ctl = context_->localControl();
+  for (auto& oc : out_) ctl.freeWord(oc.creditWord);
+  for (auto& ic : in_) ctl.freeWord(ic.deliveryWord);
+}
+
+int HipPlanExecutor::outIndex(int peer, int tag) {
+  for (size_t i = 0; i < out_.size(); i++)
+    if (out_[i].peer == peer && out_[i].tag == tag) return (int)i;
+  return -1;
+}
+
+int HipPlanExecutor::inIndex(int peer, int tag) {
+  for (size_t i = 0; i < in_.size(); i++)
+    if (in_[i].peer == peer && in_[i].tag == tag) return (int)i;
+  return -1;
+}
+
+// Our record for this algorithm instance: where peers land their messages
+// (scratch pointer / IPC handle, ptr0 phase) and which counter words they
+// bump (our delivery words) or watch (our credit words).
+void HipPlanExecutor::publish() {
+  std::vector<char> b;
+  putPod<uint32_t>(b, kAlgMagic);
+  putPod<int64_t>(b, (int64_t)::getpid());
+  putPod<uint64_t>(b, (uint64_t)(uintptr_t)scratch_);
+  hipIpcMemHandle_t h;
+  memset(&h, 0, sizeof(h));
+  int32_t haveIpc = 0;
+  if (scratch_ != nullptr && hipIpcGetMemHandle(&h, scratch_) == hipSuccess) haveIpc = 1;
+  (void)hipGetLastError();
+  putPod<int32_t>(b, haveIpc);
+  putPod(b, h);
+  putPod<int32_t>(b, myPhase_);
+  putPod<int32_t>(b, (int32_t)(in_.size() + out_.size()));
+  for (auto& ic : in_) {
+    putPod<int32_t>(b, ic.peer);
+    putPod<int32_t>(b, ic.tag);
+    putPod<int32_t>(b, DIR_IN);
+    putPod<int32_t>(b, (int32_t)ic.deliveryWord);
+  }
+  for (auto& oc : out_) {
+    putPod<int32_t>(b, oc.peer);
+    putPod<int32_t>(b, oc.tag);
+    putPod<int32_t>(b, DIR_OUT);
+    putPod<int32_t>(b, (int32_t)oc.creditWord);
+  }
+  context_->store().set(
+      "glx/alg/" + std::to_string(slot_) + "/" + std::to_string(contextRank_), b);
+}
+
+void HipPlanExecutor::resolvePeers() {
+  std::map<int, bool> peers;
+  for (auto& oc : out_) peers[oc.peer] = true;
+  for (auto& ic : in_) peers[ic.peer] = true;
+  for (auto& kv : peers) {
+    const int r = kv.first;
+    PeerEndpoint& pe = context_->peer(r);
+    auto b = context_->store().get(
+        "glx/alg/" + std::to_string(slot_) + "/" + std::to_string(r),
+        context_->getTimeout());
+    size_t at = 0;
+    GLX_ENFORCE(getPod<uint32_t>(b, at) == kAlgMagic, "bad algorithm record from rank ", r);
+    getPod<int64_t>(b, at);  // pid (already known from the endpoint)
+    uint64_t scratch = getPod<uint64_t>(b, at);
+    int32_t haveIpc = getPod<int32_t>(b, at);
+    hipIpcMemHandle_t h = getPod<hipIpcMemHandle_t>(b, at);
+    int32_t phase = getPod<int32_t>(b, at);
+    int32_t n = getPod<int32_t>(b, at);
+    char* peerScratch = nullptr;
+    bool needScratch = false;
+    for (auto& oc : out_) needScratch = needScratch || oc.peer == r;
+    if (needScratch && scratch != 0) {
+      if (pe.sameProcess) {
+        peerScratch = reinterpret_cast<char*>((uintptr_t)scratch);
+      } else {
+        GLX_ENFORCE(haveIpc, "rank ", r, " could not export its receive buffer (hipIpcGetMemHandle)");
+        void* p = nullptr;
+        GLX_HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+        ipcOpened_.push_back(p);
+        peerScratch = static_cast<char*>(p);
+      }
+    }
+    for (int32_t i = 0; i < n; i++) {
+      int32_t peer = getPod<int32_t>(b, at);
+      int32_t tag = getPod<int32_t>(b, at);
+      int32_t dir = getPod<int32_t>(b, at);
+      int32_t word = getPod<int32_t>(b, at);
+      if (peer != contextRank_) continue;
+      if (dir == DIR_IN) {  // peer receives from us on `tag`
+        int idx = outIndex(r, tag);
+        if (idx >= 0) {
+          out_[idx].delivery = pe.ctl->word((uint32_t)word);
+          out_[idx].peerScratch = peerScratch;
+          out_[idx].peerPhase = phase;
+          out_[idx].peerDevice = pe.localDevice;
+        }
+      } else {  // peer sends to us on `tag`: its credit word
+        int idx = inIndex(r, tag);
+        if (idx >= 0) in_[idx].credit = pe.ctl->word((uint32_t)word);
+      }
+    }
+  }
+  for (auto& oc : out_) {
+    GLX_ENFORCE(oc.delivery != nullptr, "rank ", oc.peer, " has no receive channel ",
+                oc.tag, " from rank ", contextRank_, " (schedules disagree)");
+  }
+  for (auto& ic : in_) {
+    GLX_ENFORCE(ic.credit != nullptr, "rank ", ic.peer, " has no send channel ", ic.tag,
+                " to rank ", contextRank_, " (schedules disagree)");
+  }
+  resolved_ = true;
+}
+
+char* HipPlanExecutor::landing(char* base, int64_t boff, int64_t off, int phase) const {
+  uintptr_t at = ((uintptr_t)boff * esize_ + 15) & ~(uintptr_t)15;
+  at += ((uintptr_t)phase + (uintptr_t)off * esize_) % 16;
+  return base + at;
+}
+
+void HipPlanExecutor::pollPending() {
+  for (size_t i = 0; i < pending_.size();) {
+    Pending& p = pending_[i];
+    bool blocked = false;  // never overtake an earlier signal to the same word
+    for (size_t j = 0; j < i && !blocked; j++) blocked = pending_[j].word == p.word;
+    bool done = false;
+    if (!blocked) {
+      if (p.event == nullptr) {
+        done = true;
+      } else {
+        hipError_t e = hipEventQuery(p.event);
+        if (e == hipSuccess) {
+          done = true;
+        } else if (e != hipErrorNotReady) {
+          GLX_HIP_CHECK(e);
+        }
+      }
+    }
+    if (done) {
+      p.word->store(p.value, std::memory_order_release);
+      pending_.erase(pending_.begin() + (long)i);
+    } else {
+      i++;
+    }
+  }
+}
+
+template <typename Pred>
+void HipPlanExecutor::waitFor(Pred done, const char* what, int peer) {
+  if (done()) return;
+  const auto timeout = context_->getTimeout();
+  const auto start = std::chrono::steady_clock::now();
+  auto lastAlive = start;
+  for (uint64_t spin = 1;; spin++) {
+    pollPending();
+    if (done()) return;
+    if ((spin & 255) == 0) {
+      auto now = std::chrono::steady_clock::now();
+      if (now - start > timeout) {
+        GLX_THROW_TIMEOUT(
+            "Timed out waiting for ", what, " from rank ", peer, " (rank ",
+            contextRank_, ", after ",
+            std::chrono::duration_cast<std::chrono::milliseconds>(now - start).count(),
+            " ms, timeout ", timeout.count(), " ms)");
+      }
+      if (now - lastAlive > std::chrono::milliseconds(200)) {
+        context_->checkPeersAlive();
+        lastAlive = now;
+      }
+    }
+    if (spin > 4096) {
+      sched_yield();
+    } else {
+      _mm_pause();
+    }
+  }
+}
+
+void HipPlanExecutor::waitWar(int64_t off, int64_t len) {
+  for (size_t i = 0; i < inflight_.size();) {
+    const InflightSend& s = inflight_[i];
+    const bool overlap = s.off < off + len && off < s.off + s.len;
+    if (overlap) {
+      if (hipEventQuery(s.event) != hipSuccess) {
+        GLX_HIP_CHECK(hipStreamWaitEvent(compute_, s.event, 0));
+      }
+      inflight_.erase(inflight_.begin() + (long)i);
+    } else {
+      i++;
+    }
+  }
+}
+
+void HipPlanExecutor::drain() {
+  waitFor([&] { return pending_.empty(); }, "local completions", contextRank_);
+}
+
+void HipPlanExecutor::run() {
+  if (count_ == 0) return;  // gloo/allreduce_ring_chunked.h:84-86
+  GLX_HIP_CHECK(hipSetDevice(device_));
+  char* ptr0 = static_cast<char*>(ptrs_[0]);
+  const size_t bytes = (size_t)count_ * esize_;
+
+  // Local multi-pointer reduce into ptrs_[0] (left fold, :89-91).
+  if (ptrs_.size() > 1) {
+    std::vector<const void*> srcs(ptrs_.begin(), ptrs_.end());
+    GLX_HIP_CHECK(glx::launch_reduce_n(op_, dtype_, ptr0, srcs.data(), (int)srcs.size(),
+                                       (size_t)count_, compute_));
+  }
+  if (contextSize_ > 1) {
+    if (!resolved_) resolvePeers();
+    bool computeSinceMark = true;  // the caller's writes to ptr0 count as compute
+    lastCopy_ = nullptr;
+    const auto& steps = plan_.steps;
+    for (size_t i = 0; i < steps.size(); i++) {
+      const glx::Step& s = steps[i];
+      switch (s.kind) {
+        case glx::SEND: {
+          OutChan& oc = out_[stepChan_[i]];
+          const uint64_t n = ++oc.sent;
+          // one receive region per channel: message n may only land once the
+          // receiver has consumed message n-1
+          waitFor([&] { return oc.credit->load(std::memory_order_acquire) + 1 >= n; },
+                  "receive-region credit", oc.peer);
+          const size_t nbytes = (size_t)s.len * esize_;
+          if (nbytes > 0) {
+            if (computeSinceMark) {
+              GLX_HIP_CHECK(hipEventRecord(computeMark_, compute_));
+              GLX_HIP_CHECK(hipStreamWaitEvent(copy_, computeMark_, 0));
+              computeSinceMark = false;
+            }
+            char* dst = landing(oc.peerScratch, s.dst_off, s.off, oc.peerPhase);
+            const char* src = ptr0 + (size_t)s.off * esize_;
+            if (oc.peerDevice >= 0 && oc.peerDevice != device_) {
+              GLX_HIP_CHECK(hipMemcpyPeerAsync(dst, oc.peerDevice, src, device_, nbytes, copy_));
+            } else {
+              GLX_HIP_CHECK(hipMemcpyAsync(dst, src, nbytes, hipMemcpyDeviceToDevice, copy_));
+            }
+            GLX_HIP_CHECK(hipEventRecord(events_[i], copy_));
+            lastCopy_ = events_[i];
+            inflight_.push_back({s.off, s.len, events_[i]});
+            pending_.push_back({events_[i], oc.delivery, n});
+          } else {
+            pending_.push_back({nullptr, oc.delivery, n});
+          }
+          break;
+        }
+        case glx::RECV: {
+          InChan& ic = in_[stepChan_[i]];
+          const uint64_t n = ++ic.received;
+          waitFor([&] { return ic.delivery->load(std::memory_order_acquire) >= n; },
+                  "data", ic.peer);
+          break;
+        }
+        case glx::REDUCE: {
+          waitWar(s.off, s.len);
+          char* dst = ptr0 + (size_t)s.off * esize_;
+          const char* src = landing(scratch_, s.boff, s.off, myPhase_);
+          GLX_HIP_CHECK(glx::launch_reduce(op_, dtype_, dst, dst, src, (size_t)s.len, compute_));
+          computeSinceMark = true;
+          break;
+        }
+        case glx::COPY: {
+          waitWar(s.off, s.len);
+          char* dst = ptr0 + (size_t)s.off * esize_;
+          const char* src = landing(scratch_, s.boff, s.off, myPhase_);
+          GLX_HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)s.len * esize_,
+                                       hipMemcpyDeviceToDevice, compute_));
+          computeSinceMark = true;
+          break;
+        }
+        case glx::RELEASE: {
+          InChan& ic = in_[stepChan_[i]];
+          const uint64_t v = ++ic.consumed;
+          GLX_HIP_CHECK(hipEventRecord(events_[i], compute_));
+          pending_.push_back({events_[i], ic.credit, v});
+          break;
+        }
+        default:
+          GLX_ENFORCE(false, "bad plan step kind ", s.kind);
+      }
+      pollPending();
+    }
+    drain();
+    // the caller's stream must not run ahead of copies still reading ptr0
+    if (lastCopy_ != nullptr) GLX_HIP_CHECK(hipStreamWaitEvent(compute_, lastCopy_, 0));
+    inflight_.clear();
+  }
+  // Local broadcast of ptrs_[0] (:209-211).
+  for (size_t i = 1; i < ptrs_.size(); i++) {
+    GLX_HIP_CHECK(hipMemcpyAsync(ptrs_[i], ptr0, bytes, hipMemcpyDeviceToDevice, compute_));
+  }
+  if (!userStream_) GLX_HIP_CHECK(hipStreamSynchronize(compute_));
+}
+
+}  // namespace gloo

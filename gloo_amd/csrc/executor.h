@@ -1,0 +1,119 @@
+// executor.h -- runs a compiled schedule (plan.h) on this rank's GPU.
+//
+// This is the device-side Algorithm: HipAllreduceRingChunked and
+// HipAllreduceHalvingDoubling are an Executor over the corresponding plan.
+//   * payload: hipMemcpyPeerAsync ptr0 -> peer receive region, on a
+//     dedicated copy stream (side stream, as gloo's CUDA path keeps copies
+//     off the compute stream, gloo/cuda_allreduce_ring_chunked.cc:322-356);
+//   * reduction: glx reduce kernel on the compute stream (the user's
+//     stream when one is given);
+//   * copy/compute overlap: a SEND waits (GPU side, hipStreamWaitEvent) only
+//     for the compute work that produced its source; a REDUCE/COPY waits only
+//     for in-flight SENDs whose source range it overwrites;
+//   * completion signalling: host progress loop polls hipEventQuery and
+//     bumps peers' counters (see context.h), never blocking on one stream.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+#include <memory>
+#include <vector>
+
+#include "context.h"
+#include "plan.h"
+
+namespace gloo {
+
+class Algorithm {  // gloo/algorithm.h:20-38
+ public:
+  explicit Algorithm(const std::shared_ptr<Context>& ctx)
+      : context_(ctx), contextRank_(ctx->rank), contextSize_(ctx->size) {}
+  virtual ~Algorithm() noexcept(false) {}
+  virtual void run() = 0;
+
+ protected:
+  std::shared_ptr<Context> context_;
+  const int contextRank_;
+  const int contextSize_;
+};
+
+class HipPlanExecutor : public Algorithm {
+ public:
+  HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
+                  const std::vector<void*>& ptrs, int64_t count, int dtype,
+                  int op, const std::vector<hipStream_t>& streams);
+  ~HipPlanExecutor() noexcept(false) override;
+
+  void run() override;
+
+  int64_t bytesSentPerRun() const { return plan_.bytes_sent * (int64_t)esize_; }
+  const glx::Plan& plan() const { return plan_; }
+
+ private:
+  struct OutChan {  // this rank -> peer
+    int peer, tag;
+    uint32_t creditWord;            // in our control block, written by peer
+    std::atomic<uint64_t>* credit;  // = our word
+    std::atomic<uint64_t>* delivery = nullptr;  // in peer's block
+    uint64_t sent = 0;
+    char* peerScratch = nullptr;
+    int peerPhase = 0;  // peer ptr0 address mod 16
+    int peerDevice = -1;
+  };
+  struct InChan {  // peer -> this rank
+    int peer, tag;
+    uint32_t deliveryWord;
+    std::atomic<uint64_t>* delivery;  // our word, written by peer
+    std::atomic<uint64_t>* credit = nullptr;  // in peer's block
+    uint64_t received = 0, consumed = 0;
+  };
+  struct Pending {  // fire `value` into `word` once `event` (may be null) completes
+    hipEvent_t event;
+    std::atomic<uint64_t>* word;
+    uint64_t value;
+  };
+  struct InflightSend {
+    int64_t off, len;
+    hipEvent_t event;
+  };
+
+  void publish();
+  void resolvePeers();
+  int outIndex(int peer, int tag);
+  int inIndex(int peer, int tag);
+  void pollPending();
+  template <typename Pred>
+  void waitFor(Pred done, const char* what, int peer);
+  void drain();
+  char* landing(char* scratchBase, int64_t boff, int64_t off, int phase) const;
+  void waitWar(int64_t off, int64_t len);
+
+  glx::Plan plan_;
+  int algo_;
+  std::vector<void*> ptrs_;
+  int64_t count_;
+  int dtype_, op_;
+  size_t esize_;
+  int device_;
+  int slot_;
+  bool userStream_;
+  hipStream_t compute_ = nullptr;
+  hipStream_t copy_ = nullptr;
+  bool ownCompute_ = false;
+  char* scratch_ = nullptr;
+  size_t scratchBytes_ = 0;
+  int myPhase_ = 0;
+  std::vector<OutChan> out_;
+  std::vector<InChan> in_;
+  std::vector<int> stepChan_;        // channel index per step
+  std::vector<hipEvent_t> events_;   // one per step
+  hipEvent_t computeMark_ = nullptr;
+  hipEvent_t lastCopy_ = nullptr;
+  bool resolved_ = false;
+  std::vector<Pending> pending_;
+  std::vector<InflightSend> inflight_;
+  std::vector<void*> ipcOpened_;
+};
+
+}  // namespace gloo

@@ -1,0 +1,20 @@
+// kernels.h -- host-side launchers of the HIP kernels (reduce_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <stddef.h>
+
+namespace glx {
+
+// dst = op(a, b), n elements of dtype, on stream s.  Never synchronises.
+hipError_t launch_reduce(int op, int dtype, void* dst, const void* a,
+                         const void* b, size_t n, hipStream_t s);
+
+// dst = left fold of op over srcs[0..k-1] (2 <= k <= 8).
+hipError_t launch_reduce_n(int op, int dtype, void* dst, const void* const* srcs,
+                           int k, size_t n, hipStream_t s);
+
+// Tuning knobs of the vector kernel (lanes' unroll depth, grid cap per CU).
+void set_reduce_tuning(int unroll, int blocks_per_cu);
+
+}  // namespace glx

@@ -1,0 +1,59 @@
+// plan.h -- per-rank step programs of the allreduce schedules (host logic).
+//
+// A schedule is compiled, once per algorithm instance, into a straight-line
+// program of steps that the xGMI executor (executor.cc) runs on every
+// run().  The same programs are exported through glx_plan() so the CPU test
+// suite can replay them against the oracle without a GPU.
+//
+//   SEND    copy ptr0[off, off+len) into peer's receive region `dst_off`
+//           of channel `channel` (one hipMemcpyPeerAsync), then bump the
+//           channel's delivery counter in the peer's control block.
+//   RECV    wait until the next message on (peer, channel) has landed.
+//   REDUCE  ptr0[off, off+len) = op(ptr0[off, off+len), region(boff))
+//   COPY    ptr0[off, off+len) = region(boff)
+//   RELEASE the last message of (peer, channel) is consumed: once the GPU
+//           work reading it completes, credit the sender.
+//
+// Region offsets are in elements; each region is padded by kPadElems so a
+// message can land at the 16-byte phase of the receiver's ptr0 (keeps the
+// reduce kernel on its dwordx4 path for any chunk offset).
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+namespace glx {
+
+enum StepKind : int64_t { SEND = 0, RECV = 1, REDUCE = 2, COPY = 3, RELEASE = 4 };
+
+struct Step {
+  int64_t kind;
+  int64_t peer;     // SEND: destination rank; RECV/RELEASE: source rank
+  int64_t channel;  // channel tag (per ordered rank pair)
+  int64_t off;      // SEND: source offset; REDUCE/COPY: destination offset (elements of ptr0)
+  int64_t len;      // elements (0 allowed for SEND/RECV: a signal only)
+  int64_t boff;     // RECV/REDUCE/COPY: region base in this rank's scratch
+  int64_t dst_off;  // SEND: region base in the peer's scratch
+  int64_t flags;
+};
+
+struct Plan {
+  std::vector<Step> steps;
+  int64_t scratch_elems = 0;  // receive-region space (incl. padding), elements
+  int64_t bytes_sent = 0;     // payload bytes this rank sends per run (for metrics)
+};
+
+enum Algo { ALGO_RING_CHUNKED = 0, ALGO_HALVING_DOUBLING = 1 };
+
+// Region padding: room to land a message at any 16-byte phase after
+// rounding its region base up to 16 bytes (<= 30 bytes for 1-byte elements).
+constexpr int64_t kPadElems = 32;
+
+// gloo/allreduce_ring_chunked.h:22-236
+Plan planRingChunked(int rank, int size, int64_t count);
+// gloo/allreduce_halving_doubling.h:37-361
+Plan planHalvingDoubling(int rank, int size, int64_t count);
+
+Plan makePlan(int algo, int rank, int size, int64_t count);
+
+}  // namespace glx

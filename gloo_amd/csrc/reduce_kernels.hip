@@ -1,0 +1,476 @@
+// reduce_kernels.hip -- the per-chunk elementwise reduction of the gloo
+// allreduce hot path, hand-written for CDNA4 (gfx950).
+//
+// Replaces gloo::sum/product/max/min<T> (gloo/math.h:15-73) and the CUDA
+// analog cudaSum/... (gloo/cuda.cu:307-434).  Memory-bound: 3 streams of
+// n*sizeof(T) bytes (two reads, one write) per call, no reuse -> the roofline
+// is HBM (8 TB/s spec, ~6.3 TB/s achievable float4 copy on MI355X).  No MFMA,
+// no LDS: each lane moves 16-byte vectors (global_load/store_dwordx4), UNROLL
+// independent vectors in flight per lane, 256-thread (4-wave) workgroups,
+// grid-stride over a grid capped at a few workgroups per CU.
+//
+// Semantics are the reference CPU path's, bit for bit:
+//   sum / product : a + b, a * b (integers wrap, IEEE fp32/fp64 RNE)
+//   max           : (a < b) ? b : a     == std::max(a, b)  (gloo/math.h:51)
+//   min           : (b < a) ? b : a     == std::min(a, b)  (gloo/math.h:66)
+//   float16       : widen (exact), op in fp32, round-to-nearest-even once,
+//                   NaN -> 0x7fff          (gloo/types.h:181-204, 248-305)
+//                   max/min compare in fp32, return the raw 16-bit operand
+//                   (gloo/types.h:318-336 + std::max on float16 objects)
+//   bfloat16      : as float16 with bf16 rounding (no reference: unpinned)
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <type_traits>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace glx {
+namespace {
+
+constexpr int kBlock = 256;
+
+// ---- scalar element ops on storage types ---------------------------------
+
+__device__ __forceinline__ float h2f(uint16_t h) {
+  return __half2float(__ushort_as_half(h));  // v_cvt_f32_f16: exact
+}
+
+__device__ __forceinline__ uint16_t f2h(float f) {
+  // v_cvt_f16_f32 rounds to nearest even (default mode) with IEEE
+  // subnormals and overflow to inf; only the NaN encoding needs fixing.
+  return (f != f) ? (uint16_t)0x7fff : __half_as_ushort(__float2half_rn(f));
+}
+
+__device__ __forceinline__ float b2f(uint16_t h) {
+  return __uint_as_float((uint32_t)h << 16);
+}
+
+__device__ __forceinline__ uint16_t f2b(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fff;
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+template <typename T, int OP>
+struct Op;
+
+// Integers: sum/product computed in the unsigned type of the same width so
+// wrap-around is defined (the reference's signed overflow is UB; gcc wraps).
+template <typename T> struct UnsignedOf { using type = T; };
+template <> struct UnsignedOf<int8_t> { using type = uint8_t; };
+template <> struct UnsignedOf<int32_t> { using type = uint32_t; };
+template <> struct UnsignedOf<int64_t> { using type = uint64_t; };
+
+template <typename T>
+struct Op<T, GLX_SUM> {
+  static __device__ __forceinline__ T apply(T a, T b) {
+    using U = typename UnsignedOf<T>::type;
+    return (T)((U)a + (U)b);
+  }
+};
+template <typename T>
+struct Op<T, GLX_PRODUCT> {
+  static __device__ __forceinline__ T apply(T a, T b) {
+    using U = typename UnsignedOf<T>::type;
+    return (T)((U)a * (U)b);
+  }
+};
+template <typename T>
+struct Op<T, GLX_MAX> {
+  static __device__ __forceinline__ T apply(T a, T b) { return (a < b) ? b : a; }
+};
+template <typename T>
+struct Op<T, GLX_MIN> {
+  static __device__ __forceinline__ T apply(T a, T b) { return (b < a) ? b : a; }
+};
+
+template <>
+struct Op<float, GLX_SUM> {
+  static __device__ __forceinline__ float apply(float a, float b) {
+    return __fadd_rn(a, b);  // never contracted into an fma
+  }
+};
+template <>
+struct Op<float, GLX_PRODUCT> {
+  static __device__ __forceinline__ float apply(float a, float b) {
+    return __fmul_rn(a, b);
+  }
+};
+template <>
+struct Op<double, GLX_SUM> {
+  static __device__ __forceinline__ double apply(double a, double b) {
+    return __dadd_rn(a, b);
+  }
+};
+template <>
+struct Op<double, GLX_PRODUCT> {
+  static __device__ __forceinline__ double apply(double a, double b) {
+    return __dmul_rn(a, b);
+  }
+};
+
+// 16-bit floats are carried as their raw bits in these tag types.
+struct f16_t { uint16_t x; };
+struct bf16_t { uint16_t x; };
+
+template <typename H> struct HalfTraits;
+template <> struct HalfTraits<f16_t> {
+  static __device__ __forceinline__ float widen(uint16_t h) { return h2f(h); }
+  static __device__ __forceinline__ uint16_t narrow(float f) { return f2h(f); }
+};
+template <> struct HalfTraits<bf16_t> {
+  static __device__ __forceinline__ float widen(uint16_t h) { return b2f(h); }
+  static __device__ __forceinline__ uint16_t narrow(float f) { return f2b(f); }
+};
+
+template <typename H, int OP>
+struct HalfOp {
+  static __device__ __forceinline__ uint16_t apply(uint16_t a, uint16_t b) {
+    using Tr = HalfTraits<H>;
+    float x = Tr::widen(a), y = Tr::widen(b);
+    if (OP == GLX_SUM) return Tr::narrow(__fadd_rn(x, y));
+    if (OP == GLX_PRODUCT) return Tr::narrow(__fmul_rn(x, y));
+    if (OP == GLX_MAX) return (x < y) ? b : a;
+    return (y < x) ? b : a;  // GLX_MIN
+  }
+};
+
+// The reference's float16 assignment (gloo/types.h:129-147): `old = v` is
+// skipped when v.x == half((float)old.x) -- operator!= compares against the
+// old bits read as an integer.  Restated so fp16 results stay bit-exact.
+__device__ __forceinline__ uint16_t f16_assign(uint16_t old, uint16_t v) {
+  return (v == f2h((float)(uint32_t)old)) ? old : v;
+}
+
+// Storage type and element op for a tag type.  apply3(old, a, b) is the value
+// c[i] ends up with when c[i] held `old` (c == a in place: old == a).
+template <typename T, int OP> struct Elem {
+  using S = T;
+  static __device__ __forceinline__ S apply(S a, S b) { return Op<T, OP>::apply(a, b); }
+  static __device__ __forceinline__ S apply3(S, S a, S b) { return apply(a, b); }
+};
+template <int OP> struct Elem<f16_t, OP> {
+  using S = uint16_t;
+  static __device__ __forceinline__ S apply3(S old, S a, S b) {
+    S v = HalfOp<f16_t, OP>::apply(a, b);
+    if (OP == GLX_SUM || OP == GLX_PRODUCT) v = f16_assign(a, v);  // inside operator+=
+    return f16_assign(old, v);                                        // c[i] = ...
+  }
+  static __device__ __forceinline__ S apply(S a, S b) { return apply3(a, a, b); }
+};
+template <int OP> struct Elem<bf16_t, OP> {
+  using S = uint16_t;
+  static __device__ __forceinline__ S apply(S a, S b) { return HalfOp<bf16_t, OP>::apply(a, b); }
+  static __device__ __forceinline__ S apply3(S, S a, S b) { return apply(a, b); }
+};
+
+// ---- 16-byte vector op ----------------------------------------------------
+
+template <typename T, int OP>
+__device__ __forceinline__ uint4 vec_apply3(uint4 vo, uint4 va, uint4 vb) {
+  using E = Elem<T, OP>;
+  using S = typename E::S;
+  constexpr int V = 16 / sizeof(S);
+  union U { uint4 v; S s[V]; };
+  U o, a, b, c;
+  o.v = vo;
+  a.v = va;
+  b.v = vb;
+#pragma unroll
+  for (int i = 0; i < V; i++) c.s[i] = E::apply3(o.s[i], a.s[i], b.s[i]);
+  return c.v;
+}
+
+template <typename T, int OP>
+__device__ __forceinline__ uint4 vec_apply(uint4 va, uint4 vb) {
+  return vec_apply3<T, OP>(va, va, vb);
+}
+
+// ---- kernels --------------------------------------------------------------
+
+// Elements [0, head) and [head + nvec*V, head + nvec*V + tail) are done one
+// per thread by the first threads of the grid; [head, head + nvec*V) is the
+// 16-byte-aligned body, UNROLL vectors per lane per grid-stride step.
+// dst may alias a or b: every lane reads its vectors before writing them.
+// LOADC: dst is not a, and its prior value matters (float16 assignment
+// semantics) -- read it as a third stream.
+template <typename T, int OP, int UNROLL, bool LOADC>
+__global__ __launch_bounds__(kBlock) void reduce_kernel(
+    typename Elem<T, OP>::S* dst, const typename Elem<T, OP>::S* a,
+    const typename Elem<T, OP>::S* b, size_t head, size_t nvec, size_t tail) {
+  using E = Elem<T, OP>;
+  using S = typename E::S;
+  constexpr int V = 16 / sizeof(S);
+  const size_t gtid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+
+  if (gtid < head) dst[gtid] = E::apply3(LOADC ? dst[gtid] : a[gtid], a[gtid], b[gtid]);
+  if (gtid < tail) {
+    size_t i = head + nvec * V + gtid;
+    dst[i] = E::apply3(LOADC ? dst[i] : a[i], a[i], b[i]);
+  }
+
+  uint4* vd = reinterpret_cast<uint4*>(dst + head);
+  const uint4* va = reinterpret_cast<const uint4*>(a + head);
+  const uint4* vb = reinterpret_cast<const uint4*>(b + head);
+  const size_t step = (size_t)gridDim.x * kBlock * UNROLL;
+  for (size_t base = (size_t)blockIdx.x * kBlock * UNROLL + threadIdx.x;
+       base < nvec; base += step) {
+    uint4 x[UNROLL], y[UNROLL], z[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) {
+      size_t i = base + (size_t)u * kBlock;
+      if (i < nvec) {
+        x[u] = va[i];
+        y[u] = vb[i];
+        if (LOADC) z[u] = vd[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) {
+      size_t i = base + (size_t)u * kBlock;
+      if (i < nvec) vd[i] = vec_apply3<T, OP>(LOADC ? z[u] : x[u], x[u], y[u]);
+    }
+  }
+}
+
+// Fallback when a, b and dst do not share one 16-byte phase: element-wise,
+// still coalesced across lanes.
+template <typename T, int OP>
+__global__ __launch_bounds__(kBlock) void reduce_scalar_kernel(
+    typename Elem<T, OP>::S* dst, const typename Elem<T, OP>::S* a,
+    const typename Elem<T, OP>::S* b, size_t n) {
+  using E = Elem<T, OP>;
+  const size_t step = (size_t)gridDim.x * kBlock;
+  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += step)
+    dst[i] = E::apply3(dst[i], a[i], b[i]);
+}
+
+// Left fold over k <= 8 sources (local multi-pointer reduce).  Same phase
+// requirement as reduce_kernel; the host falls back to pairwise calls.
+struct SrcPtrs { const void* p[8]; };
+
+template <typename T, int OP, int UNROLL>
+__global__ __launch_bounds__(kBlock) void reduce_n_kernel(
+    typename Elem<T, OP>::S* dst, SrcPtrs srcs, int k, size_t head, size_t nvec,
+    size_t tail) {
+  using E = Elem<T, OP>;
+  using S = typename E::S;
+  constexpr int V = 16 / sizeof(S);
+  const size_t gtid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  auto src = [&](int j) { return reinterpret_cast<const S*>(srcs.p[j]); };
+  if (gtid < head || gtid < tail) {
+    for (int side = 0; side < 2; side++) {
+      size_t lim = side == 0 ? head : tail;
+      if (gtid >= lim) continue;
+      size_t i = side == 0 ? gtid : head + nvec * V + gtid;
+      S acc = E::apply(src(0)[i], src(1)[i]);
+      for (int j = 2; j < k; j++) acc = E::apply(acc, src(j)[i]);
+      dst[i] = acc;
+    }
+  }
+  uint4* vd = reinterpret_cast<uint4*>(dst + head);
+  const size_t step = (size_t)gridDim.x * kBlock * UNROLL;
+  for (size_t base = (size_t)blockIdx.x * kBlock * UNROLL + threadIdx.x;
+       base < nvec; base += step) {
+    uint4 acc[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) {
+      size_t i = base + (size_t)u * kBlock;
+      if (i < nvec) {
+        uint4 x = reinterpret_cast<const uint4*>(src(0) + head)[i];
+        uint4 y = reinterpret_cast<const uint4*>(src(1) + head)[i];
+        acc[u] = vec_apply<T, OP>(x, y);
+      }
+    }
+    for (int j = 2; j < k; j++) {
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++) {
+        size_t i = base + (size_t)u * kBlock;
+        if (i < nvec) {
+          uint4 y = reinterpret_cast<const uint4*>(src(j) + head)[i];
+          acc[u] = vec_apply<T, OP>(acc[u], y);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) {
+      size_t i = base + (size_t)u * kBlock;
+      if (i < nvec) vd[i] = acc[u];
+    }
+  }
+}
+
+// ---- launch ---------------------------------------------------------------
+
+int g_unroll = 4;         // tuned on MI355X
+int g_blocks_per_cu = 8;  // grid cap = CUs * this
+int g_num_cus = 0;
+
+int num_cus() {
+  if (g_num_cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
+            hipSuccess &&
+        n > 0) {
+      g_num_cus = n;
+    } else {
+      g_num_cus = 256;
+    }
+  }
+  return g_num_cus;
+}
+
+size_t grid_for(size_t work_items, int unroll) {
+  size_t per_block = (size_t)kBlock * unroll;
+  size_t blocks = (work_items + per_block - 1) / per_block;
+  size_t cap = (size_t)num_cus() * g_blocks_per_cu;
+  if (blocks > cap) blocks = cap;
+  if (blocks == 0) blocks = 1;
+  return blocks;
+}
+
+template <typename T, int OP, int UNROLL>
+hipError_t launch_vec(void* dst, const void* a, const void* b, size_t head,
+                      size_t nvec, size_t tail, hipStream_t s) {
+  using S = typename Elem<T, OP>::S;
+  size_t blocks = grid_for(nvec, UNROLL);
+  size_t edge_blocks = (std::max(head, tail) + kBlock - 1) / kBlock;
+  if (blocks < edge_blocks) blocks = edge_blocks;
+  if (std::is_same<T, f16_t>::value && dst != a) {
+    hipLaunchKernelGGL((reduce_kernel<T, OP, UNROLL, true>), dim3((unsigned)blocks),
+                       dim3(kBlock), 0, s, (S*)dst, (const S*)a, (const S*)b, head,
+                       nvec, tail);
+  } else {
+    hipLaunchKernelGGL((reduce_kernel<T, OP, UNROLL, false>), dim3((unsigned)blocks),
+                       dim3(kBlock), 0, s, (S*)dst, (const S*)a, (const S*)b, head,
+                       nvec, tail);
+  }
+  return hipGetLastError();
+}
+
+template <typename T, int OP>
+hipError_t launch_typed(void* dst, const void* a, const void* b, size_t n,
+                        hipStream_t s) {
+  using S = typename Elem<T, OP>::S;
+  constexpr size_t es = sizeof(S);
+  constexpr size_t V = 16 / es;
+  uintptr_t pd = (uintptr_t)dst, pa = (uintptr_t)a, pb = (uintptr_t)b;
+  if ((pd % 16) == (pa % 16) && (pd % 16) == (pb % 16) && (pd % es) == 0) {
+    size_t head = ((16 - (pd % 16)) % 16) / es;
+    if (head > n) head = n;
+    size_t nvec = (n - head) / V;
+    size_t tail = n - head - nvec * V;
+    switch (g_unroll) {
+      case 1: return launch_vec<T, OP, 1>(dst, a, b, head, nvec, tail, s);
+      case 2: return launch_vec<T, OP, 2>(dst, a, b, head, nvec, tail, s);
+      case 8: return launch_vec<T, OP, 8>(dst, a, b, head, nvec, tail, s);
+      default: return launch_vec<T, OP, 4>(dst, a, b, head, nvec, tail, s);
+    }
+  }
+  size_t blocks = grid_for(n, 4);
+  hipLaunchKernelGGL((reduce_scalar_kernel<T, OP>), dim3((unsigned)blocks),
+                     dim3(kBlock), 0, s, (S*)dst, (const S*)a, (const S*)b, n);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_op(int op, void* dst, const void* a, const void* b, size_t n,
+                     hipStream_t s) {
+  switch (op) {
+    case GLX_SUM: return launch_typed<T, GLX_SUM>(dst, a, b, n, s);
+    case GLX_PRODUCT: return launch_typed<T, GLX_PRODUCT>(dst, a, b, n, s);
+    case GLX_MAX: return launch_typed<T, GLX_MAX>(dst, a, b, n, s);
+    case GLX_MIN: return launch_typed<T, GLX_MIN>(dst, a, b, n, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+template <typename T, int OP>
+hipError_t launch_n_typed(void* dst, const void* const* srcs, int k, size_t n,
+                          hipStream_t s) {
+  using S = typename Elem<T, OP>::S;
+  constexpr size_t es = sizeof(S);
+  constexpr size_t V = 16 / es;
+  uintptr_t phase = (uintptr_t)dst % 16;
+  bool same = ((uintptr_t)dst % es) == 0;
+  for (int j = 0; j < k; j++) same = same && ((uintptr_t)srcs[j] % 16) == phase;
+  if (!same) {
+    // pairwise left fold keeps the exact same order of operations
+    hipError_t e = launch_typed<T, OP>(dst, srcs[0], srcs[1], n, s);
+    for (int j = 2; j < k && e == hipSuccess; j++)
+      e = launch_typed<T, OP>(dst, dst, srcs[j], n, s);
+    return e;
+  }
+  SrcPtrs sp{};
+  for (int j = 0; j < k; j++) sp.p[j] = srcs[j];
+  size_t head = ((16 - phase) % 16) / es;
+  if (head > n) head = n;
+  size_t nvec = (n - head) / V;
+  size_t tail = n - head - nvec * V;
+  size_t blocks = grid_for(nvec, 4);
+  size_t edge_blocks = (std::max(head, tail) + kBlock - 1) / kBlock;
+  if (blocks < edge_blocks) blocks = edge_blocks;
+  hipLaunchKernelGGL((reduce_n_kernel<T, OP, 4>), dim3((unsigned)blocks),
+                     dim3(kBlock), 0, s, (S*)dst, sp, k, head, nvec, tail);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_n_op(int op, void* dst, const void* const* srcs, int k,
+                       size_t n, hipStream_t s) {
+  switch (op) {
+    case GLX_SUM: return launch_n_typed<T, GLX_SUM>(dst, srcs, k, n, s);
+    case GLX_PRODUCT: return launch_n_typed<T, GLX_PRODUCT>(dst, srcs, k, n, s);
+    case GLX_MAX: return launch_n_typed<T, GLX_MAX>(dst, srcs, k, n, s);
+    case GLX_MIN: return launch_n_typed<T, GLX_MIN>(dst, srcs, k, n, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+hipError_t launch_reduce(int op, int dtype, void* dst, const void* a,
+                         const void* b, size_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  switch (dtype) {
+    case GLX_INT8: return launch_op<int8_t>(op, dst, a, b, n, s);
+    case GLX_UINT8: return launch_op<uint8_t>(op, dst, a, b, n, s);
+    case GLX_INT32: return launch_op<int32_t>(op, dst, a, b, n, s);
+    case GLX_INT64: return launch_op<int64_t>(op, dst, a, b, n, s);
+    case GLX_UINT64: return launch_op<uint64_t>(op, dst, a, b, n, s);
+    case GLX_FLOAT32: return launch_op<float>(op, dst, a, b, n, s);
+    case GLX_FLOAT64: return launch_op<double>(op, dst, a, b, n, s);
+    case GLX_FLOAT16: return launch_op<f16_t>(op, dst, a, b, n, s);
+    case GLX_BFLOAT16: return launch_op<bf16_t>(op, dst, a, b, n, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_reduce_n(int op, int dtype, void* dst, const void* const* srcs,
+                           int k, size_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  switch (dtype) {
+    case GLX_INT8: return launch_n_op<int8_t>(op, dst, srcs, k, n, s);
+    case GLX_UINT8: return launch_n_op<uint8_t>(op, dst, srcs, k, n, s);
+    case GLX_INT32: return launch_n_op<int32_t>(op, dst, srcs, k, n, s);
+    case GLX_INT64: return launch_n_op<int64_t>(op, dst, srcs, k, n, s);
+    case GLX_UINT64: return launch_n_op<uint64_t>(op, dst, srcs, k, n, s);
+    case GLX_FLOAT32: return launch_n_op<float>(op, dst, srcs, k, n, s);
+    case GLX_FLOAT64: return launch_n_op<double>(op, dst, srcs, k, n, s);
+    case GLX_FLOAT16: return launch_n_op<f16_t>(op, dst, srcs, k, n, s);
+    case GLX_BFLOAT16: return launch_n_op<bf16_t>(op, dst, srcs, k, n, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+void set_reduce_tuning(int unroll, int blocks_per_cu) {
+  if (unroll == 1 || unroll == 2 || unroll == 4 || unroll == 8) g_unroll = unroll;
+  if (blocks_per_cu > 0) g_blocks_per_cu = blocks_per_cu;
+}
+
+}  // namespace glx

@@ -1,0 +1,194 @@
+/*
+ * glx.h -- the C-ABI drop-in boundary of gloo_amd (MI355X-native gloo
+ * allreduce hot path).  Plain pointers, sizes and ints only: no C++ and no
+ * torch types cross this line.  Implemented by gloo_amd/libgloo_amd.so
+ * (sources under gloo_amd/csrc).
+ *
+ * Every entry point names the reference interface it replaces
+ * (liuxiaotiao/gloo, paths relative to the reference root).
+ *
+ * Conventions
+ *   - Return value: GLX_OK (0) or a GLX_ERR_* code.  Functions never throw.
+ *     glx_last_error() returns the message of the calling thread's last
+ *     failure (mirrors GLOO_ENFORCE -> EnforceNotMet, gloo/common/logging.h:21-52,
+ *     and IoException, gloo/common/error.h:45).
+ *   - Streams are hipStream_t passed as void*; NULL = the internal stream of
+ *     the object (or the legacy default stream for glx_reduce).
+ *   - dtype / op codes below; op values equal gloo::ReductionType
+ *     (gloo/algorithm.h:49-57).
+ */
+#ifndef GLOO_AMD_GLX_H_
+#define GLOO_AMD_GLX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- codes ------------------------------------------------------------ */
+enum glx_dtype {
+  GLX_INT8 = 0,
+  GLX_UINT8 = 1,
+  GLX_INT32 = 2,
+  GLX_INT64 = 3,
+  GLX_UINT64 = 4,
+  GLX_FLOAT32 = 5,
+  GLX_FLOAT64 = 6,
+  GLX_FLOAT16 = 7,  /* gloo::float16, gloo/types.h:96 */
+  GLX_BFLOAT16 = 8  /* no reference counterpart (parity unpinned) */
+};
+
+enum glx_op { /* == gloo::ReductionType, gloo/algorithm.h:49-57 */
+  GLX_SUM = 1,
+  GLX_PRODUCT = 2,
+  GLX_MAX = 3,
+  GLX_MIN = 4
+};
+
+enum glx_status {
+  GLX_OK = 0,
+  GLX_ERR_INVALID = 1,  /* bad argument -> EnforceNotMet */
+  GLX_ERR_HIP = 2,      /* HIP runtime error (CUDA_CHECK analog, gloo/cuda_private.h:25-37) */
+  GLX_ERR_TIMEOUT = 3,  /* IoException("Timed out ..."), gloo/common/error.h:45 */
+  GLX_ERR_IO = 4,       /* IoException (peer gone / closed) */
+  GLX_ERR_ENFORCE = 5,  /* EnforceNotMet, gloo/common/logging.h:21 */
+  GLX_ERR_INTERNAL = 6
+};
+
+typedef void* glx_stream_t; /* a hipStream_t */
+
+/* Message of this thread's last failed call ("" if none). */
+const char* glx_last_error(void);
+/* Library version, e.g. "0.1.0". */
+const char* glx_version(void);
+/* Size in bytes of one element of dtype (0 if unknown). */
+size_t glx_dtype_size(int dtype);
+
+/* ---- device kernels ---------------------------------------------------- */
+
+/* dst[i] = op(a[i], b[i]) for i < n, enqueued on `stream` (device pointers;
+ * dst may alias a or b).  Replaces the per-chunk reduction
+ *   gloo::sum/product/max/min<T>(void* c, const void* a, const void* b, size_t n)
+ *     -- gloo/math.h:15-73
+ * and its device analog cudaSum/cudaProduct/cudaMax/cudaMin(T*, const T*,
+ * size_t, cudaStream_t) -- gloo/cuda.h:274-284, gloo/cuda.cu:307-434.
+ * Semantics are the CPU path's: max(a,b) = (a < b) ? b : a (operand order
+ * matters for NaN / signed zero); 16-bit floats widen to fp32, op, and round
+ * to nearest even once (float16 NaN -> 0x7fff, gloo/types.h:181-204,248-305).
+ * Integer sum/product wrap. */
+int glx_reduce(int op, int dtype, void* dst, const void* a, const void* b,
+               size_t n, glx_stream_t stream);
+
+/* dst[i] = op(...op(op(srcs[0][i], srcs[1][i]), srcs[2][i])..., srcs[k-1][i])
+ * -- the left fold the reference performs for ptrs.size() > 1
+ * (gloo/allreduce_ring_chunked.h:89-91, gloo/allreduce_halving_doubling.h:232-234),
+ * fused into one pass.  2 <= k <= 8. */
+int glx_reduce_n(int op, int dtype, void* dst, const void* const* srcs, int k,
+                 size_t n, glx_stream_t stream);
+
+/* Device->device copy of `bytes` from (src on srcDev) to (dst on dstDev) over
+ * xGMI with hipMemcpyPeerAsync.  Replaces the D2D copy of CudaStream::copyAsync
+ * (gloo/cuda.cu:91-149) and the transport's Buffer::send for device buffers
+ * (gloo/transport/buffer.h:26-34). */
+int glx_peer_copy(void* dst, int dst_dev, const void* src, int src_dev,
+                  size_t bytes, glx_stream_t stream);
+
+/* hipDeviceEnablePeerAccess both ways between devices a and b (idempotent).
+ * Analog of cudaDeviceEnablePeerAccess in gloo/cuda_collectives_native.h:216-276. */
+int glx_enable_peer(int dev_a, int dev_b);
+
+/* Number of visible HIP devices (0 when no GPU). */
+int glx_device_count(int* count);
+
+/* ---- rendezvous stores (gloo/rendezvous/store.h) ----------------------- */
+typedef struct glx_store glx_store;
+
+/* In-process store shared by thread-ranks: gloo/rendezvous/hash_store.h:20. */
+glx_store* glx_hash_store_create(void);
+/* Directory-backed store for ranks in separate processes on one node:
+ * gloo/rendezvous/file_store.h:19. */
+glx_store* glx_file_store_create(const char* path);
+/* Key prefixing wrapper: gloo/rendezvous/prefix_store.h. */
+glx_store* glx_prefix_store_create(const char* prefix, glx_store* base);
+/* Store implemented by the caller (e.g. a torch.distributed TCPStore from
+ * Python).  set: store value.  get: copy the value of an EXISTING key into
+ * buf (cap bytes), return its full length or -1 if the key is absent. */
+typedef int (*glx_store_set_fn)(void* user, const char* key, const void* data,
+                                size_t len);
+typedef int64_t (*glx_store_get_fn)(void* user, const char* key, void* buf,
+                                    size_t cap);
+glx_store* glx_callback_store_create(glx_store_set_fn set_fn,
+                                     glx_store_get_fn get_fn, void* user);
+void glx_store_destroy(glx_store* store);
+int glx_store_set(glx_store* store, const char* key, const void* data,
+                  size_t len);
+/* Blocks until key exists (or timeout_ms elapses -> GLX_ERR_TIMEOUT).
+ * Writes min(len, cap) bytes to buf and the full length to *len_out. */
+int glx_store_get(glx_store* store, const char* key, void* buf, size_t cap,
+                  size_t* len_out, int64_t timeout_ms);
+
+/* ---- context (gloo/context.h:26-58, gloo/rendezvous/context.h:25-35) --- */
+typedef struct glx_context glx_context;
+
+/* A rank of `size` ranks bound to HIP device `device` (-1 = current).
+ * Replaces gloo::rendezvous::Context(rank, size) + transport::Device. */
+glx_context* glx_context_create(int rank, int size, int device);
+void glx_context_destroy(glx_context* ctx);
+/* Publish this rank's xGMI endpoint, wait for every peer's, map the peers'
+ * control blocks.  Replaces rendezvous::Context::connectFullMesh(Store&,
+ * shared_ptr<Device>&) -- gloo/rendezvous/context.cc:43-113. */
+int glx_context_connect_full_mesh(glx_context* ctx, glx_store* store);
+int glx_context_rank(glx_context* ctx);
+int glx_context_size(glx_context* ctx);
+int glx_context_device(glx_context* ctx);
+/* gloo::Context::setTimeout/getTimeout (gloo/context.h:50-53); default 30 s
+ * (gloo/context.cc:18). */
+int glx_context_set_timeout(glx_context* ctx, int64_t timeout_ms);
+int64_t glx_context_get_timeout(glx_context* ctx);
+/* gloo::Context::nextSlot(numToSkip), gloo/context.cc:49-54. */
+int glx_context_next_slot(glx_context* ctx, int num_to_skip);
+
+/* ---- allreduce algorithms (gloo/algorithm.h:20-38) ---------------------- */
+typedef struct glx_algorithm glx_algorithm;
+
+/* HipAllreduceRingChunked: gloo::AllreduceRingChunked<T>
+ * (gloo/allreduce_ring_chunked.h:22-26) on device buffers, constructor shaped
+ * like CudaAllreduceRingChunked<T>(context, ptrs, count, streams)
+ * (gloo/cuda_allreduce_ring_chunked.h:22-26).  ptrs: nptrs device pointers of
+ * this rank (same device), count elements each.  streams: 0 or nptrs
+ * hipStream_t; with streams the op is asynchronous w.r.t. the host beyond
+ * the last exchange and the outputs are valid once streams[0] completes;
+ * without, outputs are valid when run() returns (docs/cuda.md:9-11). */
+glx_algorithm* glx_allreduce_ring_chunked_create(glx_context* ctx,
+                                                 void* const* ptrs, int nptrs,
+                                                 int count, int dtype, int op,
+                                                 const glx_stream_t* streams,
+                                                 int nstreams);
+/* HipAllreduceHalvingDoubling: gloo::AllreduceHalvingDoubling<T>
+ * (gloo/allreduce_halving_doubling.h:67-71); ctor shaped like
+ * CudaAllreduceHalvingDoubling (gloo/cuda_allreduce_halving_doubling.h:25-30). */
+glx_algorithm* glx_allreduce_halving_doubling_create(
+    glx_context* ctx, void* const* ptrs, int nptrs, int count, int dtype, int op,
+    const glx_stream_t* streams, int nstreams);
+/* Algorithm::run() (gloo/algorithm.h:26). */
+int glx_algorithm_run(glx_algorithm* alg);
+/* Number of bytes moved over the peer links by this rank in one run(). */
+int64_t glx_algorithm_bytes_sent(glx_algorithm* alg);
+void glx_algorithm_destroy(glx_algorithm* alg);
+
+/* ---- schedule introspection (host logic; no GPU needed) ----------------- */
+/* The per-rank step program an algorithm executes.  Each step is 8 int64:
+ * {kind, peer, channel, off, len, boff, dst_off, flags}; kinds: 0 SEND,
+ * 1 RECV, 2 REDUCE, 3 COPY, 4 RELEASE.  algo: 0 ring_chunked,
+ * 1 halving_doubling.  Returns the number of steps (writes at most cap) or
+ * -1.  *scratch_elems receives the per-rank receive-buffer size. */
+int64_t glx_plan(int algo, int rank, int size, int64_t count, int64_t* steps,
+                 int64_t cap, int64_t* scratch_elems);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif /* GLOO_AMD_GLX_H_ */

@@ -1,0 +1,161 @@
+// ref_harness.cc -- TEST INFRASTRUCTURE ONLY (built into oracle/_ref/).
+//
+// A thin extern "C" shim over the REFERENCE implementation itself: it
+// includes the reference headers from /root/reference and is linked against
+// the reference's own tcp/rendezvous/core sources (compiled verbatim from
+// /root/reference by oracle/Makefile -- nothing is copied into this repo).
+// It lets the Python test-suite (and bench.py's cpu_baseline leg) run
+//   * gloo::sum/product/max/min<T>            (gloo/math.h:15-73)
+//   * gloo::AllreduceRingChunked<T>           (gloo/allreduce_ring_chunked.h:19)
+//   * gloo::AllreduceHalvingDoubling<T>       (gloo/allreduce_halving_doubling.h:37)
+// exactly the way the reference's tests do: P threads in one process, one
+// HashStore, tcp devices on loopback (gloo/test/base_test.h:91-166).
+#include <chrono>
+#include <cstdint>
+#include <cstring>
+#include <exception>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "gloo/allreduce_halving_doubling.h"
+#include "gloo/allreduce_ring_chunked.h"
+#include "gloo/math.h"
+#include "gloo/rendezvous/context.h"
+#include "gloo/rendezvous/hash_store.h"
+#include "gloo/transport/tcp/device.h"
+#include "gloo/types.h"
+
+namespace {
+
+enum { R_INT8 = 0, R_UINT8, R_INT32, R_INT64, R_UINT64, R_FLOAT32, R_FLOAT64,
+       R_FLOAT16, R_BFLOAT16 };
+enum { R_SUM = 1, R_PRODUCT = 2, R_MAX = 3, R_MIN = 4 };
+
+thread_local std::string g_err;
+
+template <typename T>
+int reduceT(int op, void* c, const void* a, const void* b, size_t n) {
+  switch (op) {
+    case R_SUM: gloo::sum<T>(c, a, b, n); return 0;
+    case R_PRODUCT: gloo::product<T>(c, a, b, n); return 0;
+    case R_MAX: gloo::max<T>(c, a, b, n); return 0;
+    case R_MIN: gloo::min<T>(c, a, b, n); return 0;
+  }
+  return -1;
+}
+
+template <typename T>
+const gloo::ReductionFunction<T>* fnFor(int op) {
+  switch (op) {
+    case R_SUM: return gloo::ReductionFunction<T>::sum;
+    case R_PRODUCT: return gloo::ReductionFunction<T>::product;
+    case R_MAX: return gloo::ReductionFunction<T>::max;
+    case R_MIN: return gloo::ReductionFunction<T>::min;
+  }
+  return nullptr;
+}
+
+// Runs `iters` back-to-back run() calls of one algorithm instance on every
+// rank (after `warmup` untimed calls).  Rank 0 reports the wall time of the
+// timed calls.  bufs[r * nptrs + i] is rank r's i-th buffer.
+template <typename T>
+int allreduceT(int algo, int op, int P, int nptrs, int count, void** bufs,
+               int warmup, int iters, double* seconds) {
+  auto fn = fnFor<T>(op);
+  if (fn == nullptr) return -1;
+  auto store = std::make_shared<gloo::rendezvous::HashStore>();
+  std::vector<std::thread> threads;
+  std::vector<std::string> errors(P);
+  for (int r = 0; r < P; r++) {
+    threads.emplace_back([&, r]() {
+      try {
+        gloo::transport::tcp::attr attr("127.0.0.1");
+        auto dev = gloo::transport::tcp::CreateDevice(attr);
+        auto ctx = std::make_shared<gloo::rendezvous::Context>(r, P);
+        ctx->connectFullMesh(*store, dev);
+        std::vector<T*> ptrs;
+        for (int i = 0; i < nptrs; i++) {
+          ptrs.push_back(static_cast<T*>(bufs[r * nptrs + i]));
+        }
+        std::unique_ptr<gloo::Algorithm> alg;
+        if (algo == 0) {
+          alg.reset(new gloo::AllreduceRingChunked<T>(ctx, ptrs, count, fn));
+        } else {
+          alg.reset(new gloo::AllreduceHalvingDoubling<T>(ctx, ptrs, count, fn));
+        }
+        for (int i = 0; i < warmup; i++) alg->run();
+        auto t0 = std::chrono::steady_clock::now();
+        for (int i = 0; i < iters; i++) alg->run();
+        auto t1 = std::chrono::steady_clock::now();
+        if (r == 0 && seconds != nullptr) {
+          *seconds = std::chrono::duration<double>(t1 - t0).count();
+        }
+      } catch (const std::exception& e) {
+        errors[r] = e.what();
+      }
+    });
+  }
+  for (auto& t : threads) t.join();
+  for (int r = 0; r < P; r++) {
+    if (!errors[r].empty()) {
+      g_err = "rank " + std::to_string(r) + ": " + errors[r];
+      return -2;
+    }
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* ref_last_error() { return g_err.c_str(); }
+
+// c = op(a, b) through the reference's own gloo/math.h templates.
+int ref_reduce(int op, int dtype, void* c, const void* a, const void* b,
+               size_t n) {
+  switch (dtype) {
+    case R_INT8: return reduceT<int8_t>(op, c, a, b, n);
+    case R_UINT8: return reduceT<uint8_t>(op, c, a, b, n);
+    case R_INT32: return reduceT<int32_t>(op, c, a, b, n);
+    case R_INT64: return reduceT<int64_t>(op, c, a, b, n);
+    case R_UINT64: return reduceT<uint64_t>(op, c, a, b, n);
+    case R_FLOAT32: return reduceT<float>(op, c, a, b, n);
+    case R_FLOAT64: return reduceT<double>(op, c, a, b, n);
+    case R_FLOAT16: return reduceT<gloo::float16>(op, c, a, b, n);
+  }
+  return -1;  // bf16: the reference has no such type
+}
+
+// Reference fp16 conversions (gloo/types.h:248-339) for conversion sweeps.
+void ref_f32_to_f16(const float* in, uint16_t* out, size_t n) {
+  for (size_t i = 0; i < n; i++) out[i] = gloo::cpu_float2half_rn(in[i]).x;
+}
+
+void ref_f16_to_f32(const uint16_t* in, float* out, size_t n) {
+  for (size_t i = 0; i < n; i++) {
+    gloo::float16 h;
+    h.x = in[i];
+    out[i] = gloo::cpu_half2float(h);
+  }
+}
+
+// algo: 0 = AllreduceRingChunked, 1 = AllreduceHalvingDoubling.
+int ref_allreduce(int algo, int op, int dtype, int P, int nptrs, int count,
+                  void** bufs, int warmup, int iters, double* seconds) {
+  switch (dtype) {
+    case R_INT8: return allreduceT<int8_t>(algo, op, P, nptrs, count, bufs, warmup, iters, seconds);
+    case R_UINT8: return allreduceT<uint8_t>(algo, op, P, nptrs, count, bufs, warmup, iters, seconds);
+    case R_INT32: return allreduceT<int32_t>(algo, op, P, nptrs, count, bufs, warmup, iters, seconds);
+    case R_INT64: return allreduceT<int64_t>(algo, op, P, nptrs, count, bufs, warmup, iters, seconds);
+    case R_UINT64: return allreduceT<uint64_t>(algo, op, P, nptrs, count, bufs, warmup, iters, seconds);
+    case R_FLOAT32: return allreduceT<float>(algo, op, P, nptrs, count, bufs, warmup, iters, seconds);
+    case R_FLOAT64: return allreduceT<double>(algo, op, P, nptrs, count, bufs, warmup, iters, seconds);
+    case R_FLOAT16: return allreduceT<gloo::float16>(algo, op, P, nptrs, count, bufs, warmup, iters, seconds);
+  }
+  return -1;
+}
+
+}  // extern "C"

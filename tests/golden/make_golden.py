@@ -1,0 +1,194 @@
+"""Generate the golden fixtures in tests/golden/ from the REFERENCE itself.
+
+Runs liuxiaotiao/gloo's own code -- gloo/math.h, gloo/types.h and
+AllreduceRingChunked / AllreduceHalvingDoubling over its tcp transport on
+loopback, P thread-ranks sharing a HashStore exactly like
+gloo/test/base_test.h:91-166 -- through oracle/_ref/libgloo_ref.so, which
+oracle/Makefile compiles from the sources under /root/reference.  Only
+inputs and outputs are stored (data, not source).
+
+Inputs are regenerated in the tests from (dtype, kind, seed, rank, ptr) by
+oracle.fill(); each fixture stores a checksum of its inputs so generator
+drift is caught.
+
+    make -C oracle all ref && python tests/golden/make_golden.py
+"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from oracle import oracle as O  # noqa: E402
+
+SEED = 1234
+
+
+def sha(arrs):
+    h = hashlib.sha256()
+    for a in arrs:
+        h.update(np.ascontiguousarray(a).view(np.uint8).tobytes())
+    return h.hexdigest()
+
+
+def edge_values(dtype):
+    """Special values the reference's semantics must preserve."""
+    if dtype == O.FLOAT32:
+        v = np.array([0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, np.nan, 1e-45, -1e-45,
+                      1.17549435e-38, 3.4028235e38, -3.4028235e38, 0.1, 1e30, -2.5],
+                     dtype=np.float32)
+        return v
+    if dtype == O.FLOAT64:
+        return np.array([0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, np.nan, 5e-324,
+                         1.7976931348623157e308, 0.1, -2.5], dtype=np.float64)
+    if dtype == O.FLOAT16:
+        return np.array([0x0000, 0x8000, 0x3c00, 0xbc00, 0x7c00, 0xfc00, 0x7e00, 0x7fff,
+                         0xfe01, 0x0001, 0x8001, 0x03ff, 0x0400, 0x7bff, 0xfbff, 0x3555],
+                        dtype=np.uint16)
+    if dtype in (O.INT8, O.UINT8, O.INT32, O.INT64, O.UINT64):
+        info = np.iinfo(O.NP_DTYPE[dtype])
+        return np.array([0, 1, info.max, info.min, info.max - 1, 7, 3],
+                        dtype=O.NP_DTYPE[dtype])
+    raise ValueError(dtype)
+
+
+def make_reduce():
+    """gloo/math.h ops: seeded + edge-value cross products, both orders."""
+    out = {}
+    meta = []
+    for dtype in (O.INT8, O.UINT8, O.INT32, O.INT64, O.UINT64, O.FLOAT32, O.FLOAT64,
+                  O.FLOAT16):
+        n = 1000
+        a = O.fill(dtype, n, 0, seed=SEED, rank=0)
+        b = O.fill(dtype, n, 0, seed=SEED, rank=1)
+        e = edge_values(dtype)
+        ea = np.repeat(e, len(e))
+        eb = np.tile(e, len(e))
+        A = np.concatenate([a, ea])
+        B = np.concatenate([b, eb])
+        if dtype == O.FLOAT16:
+            # hit the float16 assignment quirk: b = f2h((float)a.x), a < b
+            qa = np.array([0x0001, 0x0100, 0x3c00, 0x1234, 0x2000], dtype=np.uint16)
+            qb = O.f32_to_f16(qa.astype(np.float32), use_ref=True)
+            A = np.concatenate([A, qa, qb])
+            B = np.concatenate([B, qb, qa])
+        for op in (O.SUM, O.PRODUCT, O.MAX, O.MIN):
+            key = "reduce_%s_%s" % (O.DTYPE_NAMES[dtype], O.OP_NAMES[op])
+            out[key + "_a"] = A
+            out[key + "_b"] = B
+            # in place (the allreduce form) and into a zeroed c, both orders
+            out[key + "_ab"] = O.reduce(op, dtype, A, B, use_ref=True)
+            out[key + "_ba"] = O.reduce(op, dtype, B, A, use_ref=True)
+            out[key + "_ab0"] = O.reduce(op, dtype, A, B, use_ref=True, inplace=False)
+            out[key + "_ba0"] = O.reduce(op, dtype, B, A, use_ref=True, inplace=False)
+            meta.append(key)
+    np.savez_compressed(os.path.join(HERE, "reduce_kats.npz"), **out)
+    return meta
+
+
+def make_f16_conversions():
+    """cpu_float2half_rn over a strided sweep of all float bit patterns plus
+    every float that is exactly a half or a half midpoint."""
+    rng = np.random.default_rng(SEED)
+    stride = np.arange(0, 2**32, 65537, dtype=np.uint64).astype(np.uint32)
+    halves = np.arange(0, 2**16, dtype=np.uint32)
+    # exact halves and midpoints (as float bits) -- the RNE tie cases
+    h16 = halves.astype(np.uint16)
+    hf = np.empty(halves.size, dtype=np.float32)
+    O._load_ref().ref_f16_to_f32(O._ptr(h16), O._ptr(hf), halves.size)
+    hb = hf.view(np.uint32)
+    mids = hb[np.isfinite(hf)] + np.uint32(1 << 12)  # not exact midpoints for all, plus
+    near = np.concatenate([hb, hb + 1, hb - 1, mids, mids + 1, mids - 1])
+    rnd = rng.integers(0, 2**32, size=50000, dtype=np.uint64).astype(np.uint32)
+    bits = np.unique(np.concatenate([stride, near.astype(np.uint32), rnd]))
+    f = bits.view(np.float32)
+    h = O.f32_to_f16(f, use_ref=True)
+    np.savez_compressed(os.path.join(HERE, "f16_conversions.npz"), f32_bits=bits, f16=h,
+                        half_bits=h16, half_to_f32_bits=hf.view(np.uint32))
+
+
+ALLREDUCE_CASES = []
+for algo in (O.RING_CHUNKED, O.HALVING_DOUBLING):
+    for P in (1, 2, 3, 4, 5, 7, 8):
+        for N in (1, 255, 256, 1024, 4099, 100003):
+            ALLREDUCE_CASES.append((algo, P, N, O.FLOAT32, O.SUM, 1, 0))
+    for P in (2, 4, 8):
+        ALLREDUCE_CASES.append((algo, P, 4099, O.INT32, O.SUM, 1, 0))
+        ALLREDUCE_CASES.append((algo, P, 4099, O.FLOAT16, O.SUM, 1, 0))
+        ALLREDUCE_CASES.append((algo, P, 1000, O.FLOAT32, O.MAX, 1, 0))
+        ALLREDUCE_CASES.append((algo, P, 1000, O.FLOAT32, O.MIN, 2, 0))
+        ALLREDUCE_CASES.append((algo, P, 1000, O.FLOAT32, O.PRODUCT, 1, 0))
+    # the reference tests' own integer-valued patterns
+    for P in (3, 6):
+        ALLREDUCE_CASES.append((algo, P, 10000, O.FLOAT32, O.SUM, 1, 2))  # value = rank
+        ALLREDUCE_CASES.append((algo, P, 1000, O.FLOAT32, O.SUM, 2, 1))   # stride pattern
+        ALLREDUCE_CASES.append((algo, P, 1024, O.FLOAT16, O.SUM, 1, 2))
+
+
+def case_inputs(P, N, dtype, nptrs, kind):
+    ins = []
+    for r in range(P):
+        row = []
+        for i in range(nptrs):
+            if kind == 0:
+                row.append(O.fill(dtype, N, 0, seed=SEED, rank=r, ptr_index=i))
+            elif kind == 1:  # base_test.h:184-191
+                stride = P * nptrs
+                row.append(O.fill(dtype, N, 1, stride=stride, val=r * nptrs + i))
+            else:  # allreduce_test.cc:156-158
+                row.append(O.fill(dtype, N, 2, val=r))
+        ins.append(row)
+    return ins
+
+
+def case_name(c):
+    algo, P, N, dtype, op, nptrs, kind = c
+    return "%s_P%d_N%d_%s_%s_p%d_k%d" % (
+        "ring" if algo == O.RING_CHUNKED else "hd", P, N, O.DTYPE_NAMES[dtype],
+        O.OP_NAMES[op], nptrs, kind)
+
+
+def make_allreduce():
+    out = {}
+    index = []
+    for c in ALLREDUCE_CASES:
+        algo, P, N, dtype, op, nptrs, kind = c
+        ins = case_inputs(P, N, dtype, nptrs, kind)
+        res = O.allreduce(algo, op, dtype, ins, use_ref=True)
+        first = res[0][0]
+        for r in range(P):
+            for i in range(nptrs):
+                assert np.array_equal(res[r][i].view(np.uint8), first.view(np.uint8)), \
+                    "reference ranks disagree in %s" % case_name(c)
+        name = case_name(c)
+        rec = {"name": name, "algo": algo, "P": P, "N": N, "dtype": dtype, "op": op,
+               "nptrs": nptrs, "kind": kind, "seed": SEED,
+               "input_sha256": sha([x for row in ins for x in row]),
+               "output_sha256": sha([first])}
+        if N <= 4099:
+            out[name] = first
+        else:  # large: store a sample + checksum
+            idx = np.linspace(0, N - 1, 257).astype(np.int64)
+            out[name + "_idx"] = idx
+            out[name + "_sample"] = first[idx]
+        index.append(rec)
+        print(name, flush=True)
+    np.savez_compressed(os.path.join(HERE, "allreduce_golden.npz"), **out)
+    with open(os.path.join(HERE, "allreduce_golden.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py",
+                   "source": "oracle/_ref/libgloo_ref.so (reference compiled from "
+                             "/root/reference by oracle/Makefile)",
+                   "cases": index}, f, indent=1)
+
+
+if __name__ == "__main__":
+    if not O.ref_available():
+        sys.exit("oracle/_ref/libgloo_ref.so missing: make -C oracle ref")
+    make_reduce()
+    make_f16_conversions()
+    make_allreduce()
+    print("done")

@@ -1,0 +1,141 @@
+"""Shared test helpers: golden fixtures, plan replay, thread-rank launcher."""
+import hashlib
+import json
+import os
+import threading
+
+import numpy as np
+
+from oracle import oracle as O
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+SEED = 1234
+
+
+def sha(arrs):
+    h = hashlib.sha256()
+    for a in arrs:
+        h.update(np.ascontiguousarray(a).view(np.uint8).tobytes())
+    return h.hexdigest()
+
+
+def load_allreduce_golden():
+    with open(os.path.join(GOLDEN, "allreduce_golden.json")) as f:
+        index = json.load(f)["cases"]
+    data = np.load(os.path.join(GOLDEN, "allreduce_golden.npz"))
+    return index, data
+
+
+def case_inputs(P, N, dtype, nptrs, kind, seed=SEED):
+    ins = []
+    for r in range(P):
+        row = []
+        for i in range(nptrs):
+            if kind == 0:
+                row.append(O.fill(dtype, N, 0, seed=seed, rank=r, ptr_index=i))
+            elif kind == 1:
+                row.append(O.fill(dtype, N, 1, stride=P * nptrs, val=r * nptrs + i))
+            else:
+                row.append(O.fill(dtype, N, 2, val=r))
+        ins.append(row)
+    return ins
+
+
+def check_against_golden(rec, data, out):
+    """out: rank-0 result array of the case `rec`."""
+    name = rec["name"]
+    assert sha([out]) == rec["output_sha256"], "output checksum differs for " + name
+    if name in data:
+        assert np.array_equal(out.view(np.uint8), data[name].view(np.uint8))
+    else:
+        idx = data[name + "_idx"]
+        assert np.array_equal(out[idx].view(np.uint8), data[name + "_sample"].view(np.uint8))
+
+
+def same_bits(a, b):
+    return np.array_equal(np.ascontiguousarray(a).view(np.uint8),
+                          np.ascontiguousarray(b).view(np.uint8))
+
+
+# ---------------------------------------------------------------------------
+# Replay of the product's step programs (glx_plan) on the host, with the
+# executor's landing/credit rules: a message lands in the receiver's region
+# when it is SENT (as a hipMemcpyPeerAsync does), and only after the credit
+# for the previous message on that channel.  Any schedule bug that lets a
+# message overwrite an unconsumed one, or reads a region before its message
+# arrived, shows up as a result that differs from the oracle.
+# ---------------------------------------------------------------------------
+def replay_plans(plans, op, dtype, inputs):
+    P = len(plans)
+    data = [np.array(inputs[r], copy=True) for r in range(P)]
+    scratch = [np.zeros(max(sc, 1), dtype=data[0].dtype) for (_, sc) in plans]
+    pc = [0] * P
+    sent = {}       # (src, dst, tag) -> messages sent
+    delivered = {}  # (src, dst, tag) -> messages landed
+    consumed = {}   # (src, dst, tag) -> messages released
+    received = {}
+    blocked_rounds = 0
+    while True:
+        progress = False
+        done = True
+        for r in range(P):
+            steps = plans[r][0]
+            while pc[r] < len(steps):
+                kind, peer, tag, off, ln, boff, dst_off, _ = steps[pc[r]]
+                if kind == 0:  # SEND
+                    key = (r, peer, tag)
+                    n = sent.get(key, 0) + 1
+                    if consumed.get(key, 0) < n - 1:
+                        break  # no credit yet
+                    scratch[peer][dst_off:dst_off + ln] = data[r][off:off + ln]
+                    sent[key] = n
+                    delivered[key] = n
+                elif kind == 1:  # RECV
+                    key = (peer, r, tag)
+                    n = received.get(key, 0) + 1
+                    if delivered.get(key, 0) < n:
+                        break
+                    received[key] = n
+                elif kind == 2:  # REDUCE
+                    data[r][off:off + ln] = O.reduce(op, dtype, data[r][off:off + ln],
+                                                     scratch[r][boff:boff + ln])
+                elif kind == 3:  # COPY
+                    data[r][off:off + ln] = scratch[r][boff:boff + ln]
+                elif kind == 4:  # RELEASE
+                    key = (peer, r, tag)
+                    consumed[key] = consumed.get(key, 0) + 1
+                pc[r] += 1
+                progress = True
+            if pc[r] < len(steps):
+                done = False
+        if done:
+            break
+        if not progress:
+            blocked_rounds += 1
+            raise AssertionError("plan replay deadlocked at pcs %s" % pc)
+    return data
+
+
+def run_ranks(P, fn, timeout=120):
+    """Run fn(rank) on P threads (the reference tests' topology,
+    gloo/test/base_test.h:91-166); re-raise the first failure."""
+    errors = [None] * P
+    results = [None] * P
+
+    def body(r):
+        try:
+            results[r] = fn(r)
+        except BaseException as e:  # noqa: BLE001
+            errors[r] = e
+
+    threads = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(P)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout)
+        if t.is_alive():
+            raise TimeoutError("rank thread did not finish within %ss" % timeout)
+    for e in errors:
+        if e is not None:
+            raise e
+    return results

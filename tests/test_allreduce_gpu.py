@@ -1,0 +1,211 @@
+"""GPU parity of the MI355X allreduce path (HipAllreduceRingChunked /
+HipAllreduceHalvingDoubling through the C ABI) against the oracle and the
+reference's own outputs.  Ranks are threads sharing one GPU and a HashStore,
+the reference's test topology (gloo/test/base_test.h:91-166); the copies are
+intra-device, everything else (schedule, credits, progress engine) is the
+multi-GPU code path.  Bit-exact for every dtype."""
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+import pytest
+
+from helpers import case_inputs, check_against_golden, load_allreduce_golden, run_ranks
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from test_reduce_gpu import TORCH_VIEW, assert_same, from_dev, to_dev  # noqa: E402
+
+ALGOS = {O.RING_CHUNKED: "AllreduceRingChunked", O.HALVING_DOUBLING: "AllreduceHalvingDoubling"}
+
+
+def gpu_allreduce(algo, op, dtype, inputs, runs=1, streams=False, timeout_s=60,
+                  refill_between_runs=True):
+    """Run one algorithm instance per rank thread; returns results per rank/ptr."""
+    import gloo_amd
+    P, nptrs = len(inputs), len(inputs[0])
+    N = inputs[0][0].size
+    store = gloo_amd.rendezvous.HashStore()
+    bufs = [[to_dev(x, dtype) for x in row] for row in inputs]
+    torch.cuda.synchronize()
+    fn = {O.SUM: gloo_amd.ReductionFunction.sum, O.PRODUCT: gloo_amd.ReductionFunction.product,
+          O.MAX: gloo_amd.ReductionFunction.max, O.MIN: gloo_amd.ReductionFunction.min}[op]
+    cls = getattr(gloo_amd, ALGOS[algo])
+
+    def rank_fn(r):
+        ctx = gloo_amd.rendezvous.Context(r, P, 0)
+        ctx.setTimeout(timeout_s)
+        ctx.connectFullMesh(store)
+        ptrs = [b.data_ptr() for b in bufs[r]]
+        ss = [torch.cuda.Stream() for _ in range(nptrs)] if streams else None
+        alg = cls(ctx, ptrs, N, fn, streams=ss, dtype=dtype)
+        for k in range(runs):
+            if k > 0 and refill_between_runs:
+                for i in range(nptrs):
+                    bufs[r][i].copy_(to_dev(inputs[r][i], dtype))
+                torch.cuda.synchronize()
+            alg.run()
+            if streams:
+                ss[0].synchronize()
+        alg.close()
+        return True
+
+    run_ranks(P, rank_fn, timeout=timeout_s + 30)
+    torch.cuda.synchronize()
+    return [[from_dev(b, dtype) for b in row] for row in bufs]
+
+
+def check_all(out, exp, dtype, op):
+    for r in range(len(exp)):
+        for i in range(len(exp[r])):
+            assert_same(out[r][i], exp[r][i], dtype, op)
+
+
+@pytest.mark.parametrize("algo", [O.RING_CHUNKED, O.HALVING_DOUBLING],
+                         ids=["ring_chunked", "halving_doubling"])
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 5, 8])
+@pytest.mark.parametrize("N", [0, 1, 255, 256, 1000, 4099, 100003])
+def test_allreduce_fp32_vs_oracle(algo, P, N):
+    ins = case_inputs(P, N, O.FLOAT32, 1, 0)
+    out = gpu_allreduce(algo, O.SUM, O.FLOAT32, ins)
+    check_all(out, O.allreduce(algo, O.SUM, O.FLOAT32, ins), O.FLOAT32, O.SUM)
+
+
+INDEX, DATA = load_allreduce_golden()
+
+
+@pytest.mark.parametrize("rec", INDEX, ids=[r["name"] for r in INDEX])
+def test_allreduce_vs_reference_golden(rec):
+    ins = case_inputs(rec["P"], rec["N"], rec["dtype"], rec["nptrs"], rec["kind"], rec["seed"])
+    out = gpu_allreduce(rec["algo"], rec["op"], rec["dtype"], ins)
+    for r in range(rec["P"]):
+        for i in range(rec["nptrs"]):
+            check_against_golden(rec, DATA, out[r][i])
+
+
+@pytest.mark.parametrize("algo", [O.RING_CHUNKED, O.HALVING_DOUBLING],
+                         ids=["ring_chunked", "halving_doubling"])
+@pytest.mark.parametrize("dtype", [O.INT8, O.INT32, O.INT64, O.UINT64, O.FLOAT64,
+                                   O.FLOAT16, O.BFLOAT16],
+                         ids=lambda d: O.DTYPE_NAMES[d])
+@pytest.mark.parametrize("op", [O.SUM, O.PRODUCT, O.MAX, O.MIN],
+                         ids=lambda o: O.OP_NAMES[o])
+def test_allreduce_dtypes_ops(algo, dtype, op):
+    P, N = 3, 3001
+    ins = case_inputs(P, N, dtype, 1, 0, seed=77)
+    out = gpu_allreduce(algo, op, dtype, ins)
+    check_all(out, O.allreduce(algo, op, dtype, ins), dtype, op)
+
+
+@pytest.mark.parametrize("algo", [O.RING_CHUNKED, O.HALVING_DOUBLING],
+                         ids=["ring_chunked", "halving_doubling"])
+def test_multi_pointer_and_repeated_runs(algo):
+    """ptrs.size() > 1 (local fold + broadcast) and run() repeated on one
+    instance (credits carry across runs, gloo/allreduce_ring_chunked.h:202-206)."""
+    P, N, nptrs = 4, 20000, 3
+    ins = case_inputs(P, N, O.FLOAT32, nptrs, 0, seed=9)
+    out = gpu_allreduce(algo, O.SUM, O.FLOAT32, ins, runs=3)
+    check_all(out, O.allreduce(algo, O.SUM, O.FLOAT32, ins), O.FLOAT32, O.SUM)
+
+
+@pytest.mark.parametrize("algo", [O.RING_CHUNKED, O.HALVING_DOUBLING],
+                         ids=["ring_chunked", "halving_doubling"])
+def test_user_streams(algo):
+    P, N = 4, 300000
+    ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=21)
+    out = gpu_allreduce(algo, O.SUM, O.FLOAT32, ins, runs=2, streams=True)
+    check_all(out, O.allreduce(algo, O.SUM, O.FLOAT32, ins), O.FLOAT32, O.SUM)
+
+
+def test_back_to_back_without_refill_is_iterated_allreduce():
+    """Two runs without refilling = allreduce applied twice (the benchmark
+    loop of gloo/benchmark/runner.cc:361-392)."""
+    P, N = 4, 50000
+    ins = case_inputs(P, N, O.INT32, 1, 0, seed=4)
+    out = gpu_allreduce(O.RING_CHUNKED, O.SUM, O.INT32, ins, runs=2, refill_between_runs=False)
+    once = O.allreduce(O.RING_CHUNKED, O.SUM, O.INT32, ins)
+    twice = O.allreduce(O.RING_CHUNKED, O.SUM, O.INT32, once)
+    check_all(out, twice, O.INT32, O.SUM)
+
+
+def test_multiple_algorithms_one_context():
+    """gloo/test/allreduce_test.cc:171-210: several algorithms on one context,
+    each run twice (slots must not collide)."""
+    import gloo_amd
+    P, N = 4, 1000
+    store = gloo_amd.rendezvous.HashStore()
+    bufs = [torch.full((N,), float(r), device="cuda") for r in range(P)]
+    torch.cuda.synchronize()
+
+    def rank_fn(r):
+        ctx = gloo_amd.rendezvous.Context(r, P, 0)
+        ctx.connectFullMesh(store)
+        algs = [gloo_amd.AllreduceRingChunked(ctx, [bufs[r]]),
+                gloo_amd.AllreduceHalvingDoubling(ctx, [bufs[r]])]
+        for alg in algs:
+            for _ in range(2):
+                bufs[r].fill_(float(r))
+                torch.cuda.synchronize()
+                alg.run()
+                assert torch.all(bufs[r] == P * (P - 1) / 2).item()
+        return True
+
+    run_ranks(P, rank_fn)
+
+
+def test_timeout_raises_io_exception():
+    """gloo/test/allreduce_test.cc:386-402: a short timeout with a peer that
+    never joins the collective raises IoException("Timed out ...")."""
+    import gloo_amd
+    P = 2
+    store = gloo_amd.rendezvous.HashStore()
+    buf = torch.ones(1024, device="cuda")
+    ctxs = [None, None]
+
+    def rank_fn(r):
+        ctx = gloo_amd.rendezvous.Context(r, P, 0)
+        ctx.connectFullMesh(store)
+        ctxs[r] = ctx
+        return ctx
+
+    run_ranks(P, rank_fn)
+    ctx = ctxs[0]
+    ctx.setTimeout(0.05)
+    alg = gloo_amd.AllreduceRingChunked(ctx, [buf])
+    t0 = time.time()
+    with pytest.raises(gloo_amd.IoException, match="Timed out"):
+        alg.run()
+    assert time.time() - t0 < 5
+
+
+WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "mp_worker.py")
+
+
+@pytest.mark.parametrize("algo", ["ring_chunked", "halving_doubling"])
+def test_multiprocess_ipc(algo):
+    """One process per rank (the torchrun topology): endpoints via a FileStore,
+    receive regions shared with hipIpcGetMemHandle/hipIpcOpenMemHandle."""
+    P = 3
+    with tempfile.TemporaryDirectory() as d:
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), algo],
+                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                 for r in range(P)]
+        outs = []
+        for p in procs:
+            try:
+                o, _ = p.communicate(timeout=180)
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+            outs.append(o.decode(errors="replace"))
+        for r, p in enumerate(procs):
+            assert p.returncode == 0, "rank %d failed:\n%s" % (r, outs[r])
+            assert "OK" in outs[r]

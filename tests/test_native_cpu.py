@@ -1,0 +1,109 @@
+"""CPU: the C-ABI library loads, exports every symbol include/gloo_amd/glx.h
+declares, and its host logic (stores, rendezvous, errors) works without a
+GPU.  No compute calls here."""
+import ctypes
+import os
+import re
+import threading
+
+import pytest
+
+import gloo_amd
+from gloo_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "gloo_amd", "glx.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(glx_[a-z0-9_]+)\s*\(", text)) -
+                  {"glx_store_set_fn", "glx_store_get_fn"})
+
+
+def test_every_declared_symbol_is_exported():
+    syms = declared_symbols()
+    assert len(syms) >= 25
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    bound = {name for name, _, _ in _lib.SIGNATURES}
+    assert set(syms) <= bound, set(syms) - bound
+
+
+def test_version_and_dtype_sizes():
+    assert gloo_amd.__version__ == "0.1.0"
+    sizes = [_lib.lib.glx_dtype_size(d) for d in range(9)]
+    assert sizes == [1, 1, 4, 8, 8, 4, 8, 2, 2]
+    assert _lib.lib.glx_dtype_size(42) == 0
+
+
+def test_reduce_rejects_bad_arguments_without_gpu():
+    with pytest.raises(gloo_amd.EnforceNotMet):
+        gloo_amd.errors.check(_lib.lib.glx_reduce(99, 5, None, None, None, 0, None))
+    with pytest.raises(gloo_amd.EnforceNotMet):
+        gloo_amd.errors.check(_lib.lib.glx_reduce(1, 99, None, None, None, 0, None))
+    with pytest.raises(gloo_amd.EnforceNotMet):
+        gloo_amd.errors.check(_lib.lib.glx_reduce(1, 5, None, None, None, 10, None))
+
+
+def test_hash_store_and_prefix_store():
+    s = gloo_amd.rendezvous.HashStore()
+    s.set("k", b"v" * 70000)
+    assert s.get("k") == b"v" * 70000
+    p = gloo_amd.rendezvous.PrefixStore("pre", s)
+    p.set("a", b"1")
+    assert s.get("pre/a") == b"1"
+    with pytest.raises(gloo_amd.IoException, match="Timed out"):
+        s.get("missing", timeout_ms=20)
+
+
+def test_file_store(tmp_path):
+    s = gloo_amd.rendezvous.FileStore(str(tmp_path / "store"))
+    s.set("rank/0", b"\x00\x01payload")
+    s2 = gloo_amd.rendezvous.FileStore(str(tmp_path / "store"))
+    assert s2.get("rank/0") == b"\x00\x01payload"
+    with pytest.raises(gloo_amd.IoException):
+        s2.get("nope", timeout_ms=20)
+
+
+def test_context_validation():
+    with pytest.raises(gloo_amd.EnforceNotMet):
+        gloo_amd.rendezvous.Context(2, 2)
+    c = gloo_amd.rendezvous.Context(0, 1)
+    assert (c.rank, c.size) == (0, 1)
+    c.setTimeout(1.5)
+    assert c.getTimeout() == 1.5
+    assert [c.nextSlot(), c.nextSlot(3), c.nextSlot()] == [0, 1, 4]
+
+
+@pytest.mark.parametrize("P", [2, 5])
+def test_connect_full_mesh_threads(P):
+    """Endpoint exchange + shared-memory control blocks, ranks as threads
+    (gloo/rendezvous/context.cc:43-113); no GPU calls are needed for it."""
+    store = gloo_amd.rendezvous.HashStore()
+    errs, ctxs = [], [None] * P
+
+    def body(r):
+        try:
+            c = gloo_amd.rendezvous.Context(r, P)
+            c.connectFullMesh(store)
+            ctxs[r] = c
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(P)]
+    [t.start() for t in ts]
+    [t.join(30) for t in ts]
+    assert not errs, errs
+    assert all(c is not None for c in ctxs)
+    # control-block names are unlinked once everyone has mapped them
+    leftovers = [f for f in os.listdir("/dev/shm") if f.startswith("glx.%d." % os.getpid())]
+    assert not leftovers
+
+
+def test_algorithm_needs_connected_context():
+    c = gloo_amd.rendezvous.Context(0, 2)
+    with pytest.raises(gloo_amd.EnforceNotMet, match="connect"):
+        gloo_amd.AllreduceRingChunked(c, [1 << 20], count=16, dtype=5)

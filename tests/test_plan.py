@@ -1,0 +1,47 @@
+"""CPU: the product's step programs (glx_plan -- exactly what the GPU executor
+runs) replayed on the host with the executor's landing/credit rules must
+reproduce the oracle bit for bit."""
+import numpy as np
+import pytest
+
+import gloo_amd
+from helpers import case_inputs, replay_plans, same_bits
+from oracle import oracle as O
+
+NAMES = {O.RING_CHUNKED: "ring_chunked", O.HALVING_DOUBLING: "halving_doubling"}
+
+
+@pytest.mark.parametrize("algo", [O.RING_CHUNKED, O.HALVING_DOUBLING],
+                         ids=["ring_chunked", "halving_doubling"])
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 5, 6, 7, 8, 9, 13, 16])
+@pytest.mark.parametrize("N", [0, 1, 64, 255, 256, 1000, 4099])
+@pytest.mark.parametrize("op", [O.SUM, O.MAX])
+def test_plan_replay_matches_oracle(algo, P, N, op):
+    ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=99)
+    plans = [gloo_amd.plan(NAMES[algo], r, P, N) for r in range(P)]
+    got = replay_plans(plans, op, O.FLOAT32, [ins[r][0] for r in range(P)])
+    exp = O.allreduce(algo, op, O.FLOAT32, ins)
+    for r in range(P):
+        assert same_bits(got[r], exp[r][0]), "rank %d" % r
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_ring_plan_traffic(P):
+    """4P-4 chunk sends per rank, 1.75*S link bytes at P=8."""
+    N = 16 * P * 1000
+    steps, _ = gloo_amd.plan("ring_chunked", 0, P, N)
+    sends = [s for s in steps if s[0] == 0]
+    assert len(sends) == 4 * P - 4
+    assert sum(s[4] for s in sends) == (4 * P - 4) * N // (2 * P)
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_hd_plan_traffic(P):
+    N = 1 << 16
+    steps, _ = gloo_amd.plan("halving_doubling", 0, P, N)
+    assert sum(s[4] for s in steps if s[0] == 0) == 2 * N * (P - 1) // P
+
+
+def test_plan_rejects_bad_geometry():
+    with pytest.raises(gloo_amd.EnforceNotMet):
+        gloo_amd.plan("ring_chunked", 3, 2, 10)
