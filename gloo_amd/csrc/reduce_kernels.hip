@@ -42,7 +42,12 @@ __device__ __forceinline__ float h2f(uint16_t h) {
 __device__ __forceinline__ uint16_t f2h(float f) {
   // v_cvt_f16_f32 rounds to nearest even (default mode) with IEEE
   // subnormals and overflow to inf; only the NaN encoding needs fixing.
-  return (f != f) ? (uint16_t)0x7fff : __half_as_ushort(__float2half_rn(f));
+  // Issued as inline asm so the compiler cannot fold widen->op->narrow into
+  // a mixed-precision FMA (it lowers fptrunc(a*b) to v_fma_mixlo_f16 a,b,+0,
+  // which turns a -0 product into +0).
+  uint32_t r;
+  asm("v_cvt_f16_f32_e32 %0, %1" : "=v"(r) : "v"(f));
+  return (f != f) ? (uint16_t)0x7fff : (uint16_t)(r & 0xffffu);
 }
 
 __device__ __forceinline__ float b2f(uint16_t h) {
@@ -306,8 +311,8 @@ __global__ __launch_bounds__(kBlock) void reduce_n_kernel(
 
 // ---- launch ---------------------------------------------------------------
 
-int g_unroll = 4;         // tuned on MI355X
-int g_blocks_per_cu = 8;  // grid cap = CUs * this
+int g_unroll = 1;         // tuned on MI355X: tools/tune_reduce.py, profiles/r1_tune_reduce.log
+int g_blocks_per_cu = 2;  // grid cap = CUs * this (512 workgroups on 256 CUs)
 int g_num_cus = 0;
 
 int num_cus() {

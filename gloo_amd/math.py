@@ -3,6 +3,7 @@
 gloo::sum/product/max/min<T>(c, a, b, n) (gloo/math.h:15-73) as HIP kernels
 through glx_reduce.  Reference CPU semantics, bit for bit.
 """
+import builtins
 import ctypes
 
 from . import _lib
@@ -20,8 +21,8 @@ def reduce(op, c, a, b, n=None, stream=None):
     if torch_dtype_code(a) != dt or torch_dtype_code(b) != dt:
         raise TypeError("dtype mismatch")
     if n is None:
-        n = min(c.numel(), a.numel(), b.numel())
-    if n > min(c.numel(), a.numel(), b.numel()):
+        n = builtins.min(c.numel(), a.numel(), b.numel())
+    if n > builtins.min(c.numel(), a.numel(), b.numel()):
         raise ValueError("n exceeds a buffer")
     if stream is None:
         import torch
@@ -35,7 +36,7 @@ def reduce_n(op, dst, srcs, n=None, stream=None):
     """dst = left fold of op over srcs (2..8 tensors), one pass."""
     dt = torch_dtype_code(dst)
     if n is None:
-        n = min([dst.numel()] + [s.numel() for s in srcs])
+        n = builtins.min([dst.numel()] + [s.numel() for s in srcs])
     if stream is None:
         import torch
         stream = torch.cuda.current_stream(dst.device)
