@@ -173,6 +173,9 @@ def bench_multi(args):
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank))
+    # one GPU per rank; on a box with fewer GPUs than ranks (rehearsal only)
+    # ranks share devices round-robin
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist.init_process_group("gloo")  # host-side coordination only

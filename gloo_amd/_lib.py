@@ -37,7 +37,7 @@ SIGNATURES = [
     ("glx_reduce_n", _i, [_i, _i, _vp, ctypes.POINTER(_vp), _i, _sz, _vp]),
     ("glx_peer_copy", _i, [_vp, _i, _vp, _i, _sz, _vp]),
     ("glx_enable_peer", _i, [_i, _i]),
-    ("glx_tune_reduce", _i, [_i, _i]),
+    ("glx_tune_reduce", _i, [_i, _i, _i]),
     ("glx_device_count", _i, [ctypes.POINTER(_i)]),
     ("glx_hash_store_create", _vp, []),
     ("glx_file_store_create", _vp, [ctypes.c_char_p]),

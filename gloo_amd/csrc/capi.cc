@@ -148,12 +148,12 @@ int glx_enable_peer(int a, int b) {
   return GLX_OK;
 }
 
-int glx_tune_reduce(int unroll, int blocks_per_cu) {
+int glx_tune_reduce(int unroll, int blocks_per_cu, int nontemporal) {
   if (unroll != 1 && unroll != 2 && unroll != 4 && unroll != 8) {
     return fail(GLX_ERR_INVALID, "glx_tune_reduce: unroll must be 1, 2, 4 or 8");
   }
   if (blocks_per_cu < 0) return fail(GLX_ERR_INVALID, "glx_tune_reduce: blocks_per_cu < 0");
-  glx::set_reduce_tuning(unroll, blocks_per_cu);
+  glx::set_reduce_tuning(unroll, blocks_per_cu, nontemporal);
   return GLX_OK;
 }
 

@@ -14,7 +14,8 @@ hipError_t launch_reduce(int op, int dtype, void* dst, const void* a,
 hipError_t launch_reduce_n(int op, int dtype, void* dst, const void* const* srcs,
                            int k, size_t n, hipStream_t s);
 
-// Tuning knobs of the vector kernel (lanes' unroll depth, grid cap per CU).
-void set_reduce_tuning(int unroll, int blocks_per_cu);
+// Tuning knobs of the vector kernel (lanes' unroll depth, grid cap per CU,
+// nontemporal loads/stores: 0/1, -1 = keep).
+void set_reduce_tuning(int unroll, int blocks_per_cu, int nontemporal);
 
 }  // namespace glx

@@ -33,6 +33,24 @@ namespace {
 
 constexpr int kBlock = 256;
 
+// 16-byte vector as a native clang vector (one global_load/store_dwordx4).
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+// Streaming loads/stores; NT = nontemporal hint (the data is touched once).
+template <bool NT>
+__device__ __forceinline__ v4u ld16(const v4u* p) {
+  if (NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st16(v4u* p, v4u v) {
+  if (NT) {
+    __builtin_nontemporal_store(v, p);
+  } else {
+    *p = v;
+  }
+}
+
 // ---- scalar element ops on storage types ---------------------------------
 
 __device__ __forceinline__ float h2f(uint16_t h) {
@@ -176,11 +194,11 @@ template <int OP> struct Elem<bf16_t, OP> {
 // ---- 16-byte vector op ----------------------------------------------------
 
 template <typename T, int OP>
-__device__ __forceinline__ uint4 vec_apply3(uint4 vo, uint4 va, uint4 vb) {
+__device__ __forceinline__ v4u vec_apply3(v4u vo, v4u va, v4u vb) {
   using E = Elem<T, OP>;
   using S = typename E::S;
   constexpr int V = 16 / sizeof(S);
-  union U { uint4 v; S s[V]; };
+  union U { v4u v; S s[V]; };
   U o, a, b, c;
   o.v = vo;
   a.v = va;
@@ -191,7 +209,7 @@ __device__ __forceinline__ uint4 vec_apply3(uint4 vo, uint4 va, uint4 vb) {
 }
 
 template <typename T, int OP>
-__device__ __forceinline__ uint4 vec_apply(uint4 va, uint4 vb) {
+__device__ __forceinline__ v4u vec_apply(v4u va, v4u vb) {
   return vec_apply3<T, OP>(va, va, vb);
 }
 
@@ -203,7 +221,7 @@ __device__ __forceinline__ uint4 vec_apply(uint4 va, uint4 vb) {
 // dst may alias a or b: every lane reads its vectors before writing them.
 // LOADC: dst is not a, and its prior value matters (float16 assignment
 // semantics) -- read it as a third stream.
-template <typename T, int OP, int UNROLL, bool LOADC>
+template <typename T, int OP, int UNROLL, bool LOADC, bool NT>
 __global__ __launch_bounds__(kBlock) void reduce_kernel(
     typename Elem<T, OP>::S* dst, const typename Elem<T, OP>::S* a,
     const typename Elem<T, OP>::S* b, size_t head, size_t nvec, size_t tail) {
@@ -218,26 +236,26 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(
     dst[i] = E::apply3(LOADC ? dst[i] : a[i], a[i], b[i]);
   }
 
-  uint4* vd = reinterpret_cast<uint4*>(dst + head);
-  const uint4* va = reinterpret_cast<const uint4*>(a + head);
-  const uint4* vb = reinterpret_cast<const uint4*>(b + head);
+  v4u* vd = reinterpret_cast<v4u*>(dst + head);
+  const v4u* va = reinterpret_cast<const v4u*>(a + head);
+  const v4u* vb = reinterpret_cast<const v4u*>(b + head);
   const size_t step = (size_t)gridDim.x * kBlock * UNROLL;
   for (size_t base = (size_t)blockIdx.x * kBlock * UNROLL + threadIdx.x;
        base < nvec; base += step) {
-    uint4 x[UNROLL], y[UNROLL], z[UNROLL];
+    v4u x[UNROLL], y[UNROLL], z[UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) {
       size_t i = base + (size_t)u * kBlock;
       if (i < nvec) {
-        x[u] = va[i];
-        y[u] = vb[i];
+        x[u] = ld16<NT>(va + i);
+        y[u] = ld16<NT>(vb + i);
         if (LOADC) z[u] = vd[i];
       }
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) {
       size_t i = base + (size_t)u * kBlock;
-      if (i < nvec) vd[i] = vec_apply3<T, OP>(LOADC ? z[u] : x[u], x[u], y[u]);
+      if (i < nvec) st16<NT>(vd + i, vec_apply3<T, OP>(LOADC ? z[u] : x[u], x[u], y[u]));
     }
   }
 }
@@ -277,17 +295,17 @@ __global__ __launch_bounds__(kBlock) void reduce_n_kernel(
       dst[i] = acc;
     }
   }
-  uint4* vd = reinterpret_cast<uint4*>(dst + head);
+  v4u* vd = reinterpret_cast<v4u*>(dst + head);
   const size_t step = (size_t)gridDim.x * kBlock * UNROLL;
   for (size_t base = (size_t)blockIdx.x * kBlock * UNROLL + threadIdx.x;
        base < nvec; base += step) {
-    uint4 acc[UNROLL];
+    v4u acc[UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) {
       size_t i = base + (size_t)u * kBlock;
       if (i < nvec) {
-        uint4 x = reinterpret_cast<const uint4*>(src(0) + head)[i];
-        uint4 y = reinterpret_cast<const uint4*>(src(1) + head)[i];
+        v4u x = reinterpret_cast<const v4u*>(src(0) + head)[i];
+        v4u y = reinterpret_cast<const v4u*>(src(1) + head)[i];
         acc[u] = vec_apply<T, OP>(x, y);
       }
     }
@@ -296,7 +314,7 @@ __global__ __launch_bounds__(kBlock) void reduce_n_kernel(
       for (int u = 0; u < UNROLL; u++) {
         size_t i = base + (size_t)u * kBlock;
         if (i < nvec) {
-          uint4 y = reinterpret_cast<const uint4*>(src(j) + head)[i];
+          v4u y = reinterpret_cast<const v4u*>(src(j) + head)[i];
           acc[u] = vec_apply<T, OP>(acc[u], y);
         }
       }
@@ -311,9 +329,10 @@ __global__ __launch_bounds__(kBlock) void reduce_n_kernel(
 
 // ---- launch ---------------------------------------------------------------
 
-int g_unroll = 1;         // tuned on MI355X: tools/tune_reduce.py, profiles/r1_tune_reduce.log
-int g_blocks_per_cu = 2;  // grid cap = CUs * this (512 workgroups on 256 CUs)
+int g_unroll = 4;         // tuned on MI355X: tools/tune_reduce.py, profiles/r1_tune_reduce_nt.log
+int g_blocks_per_cu = 64; // grid cap = CUs * this (256 MiB fp32: one vector pass per lane)
 int g_num_cus = 0;
+bool g_nontemporal = true;  // nt loads/stores: 123 us vs 137 us at 256 MiB
 
 int num_cus() {
   if (g_num_cus == 0) {
@@ -347,11 +366,15 @@ hipError_t launch_vec(void* dst, const void* a, const void* b, size_t head,
   size_t edge_blocks = (std::max(head, tail) + kBlock - 1) / kBlock;
   if (blocks < edge_blocks) blocks = edge_blocks;
   if (std::is_same<T, f16_t>::value && dst != a) {
-    hipLaunchKernelGGL((reduce_kernel<T, OP, UNROLL, true>), dim3((unsigned)blocks),
+    hipLaunchKernelGGL((reduce_kernel<T, OP, UNROLL, true, false>), dim3((unsigned)blocks),
+                       dim3(kBlock), 0, s, (S*)dst, (const S*)a, (const S*)b, head,
+                       nvec, tail);
+  } else if (g_nontemporal) {
+    hipLaunchKernelGGL((reduce_kernel<T, OP, UNROLL, false, true>), dim3((unsigned)blocks),
                        dim3(kBlock), 0, s, (S*)dst, (const S*)a, (const S*)b, head,
                        nvec, tail);
   } else {
-    hipLaunchKernelGGL((reduce_kernel<T, OP, UNROLL, false>), dim3((unsigned)blocks),
+    hipLaunchKernelGGL((reduce_kernel<T, OP, UNROLL, false, false>), dim3((unsigned)blocks),
                        dim3(kBlock), 0, s, (S*)dst, (const S*)a, (const S*)b, head,
                        nvec, tail);
   }
@@ -473,9 +496,10 @@ hipError_t launch_reduce_n(int op, int dtype, void* dst, const void* const* srcs
   return hipErrorInvalidValue;
 }
 
-void set_reduce_tuning(int unroll, int blocks_per_cu) {
+void set_reduce_tuning(int unroll, int blocks_per_cu, int nontemporal) {
   if (unroll == 1 || unroll == 2 || unroll == 4 || unroll == 8) g_unroll = unroll;
   if (blocks_per_cu > 0) g_blocks_per_cu = blocks_per_cu;
+  if (nontemporal >= 0) g_nontemporal = nontemporal != 0;
 }
 
 }  // namespace glx

@@ -100,8 +100,9 @@ int glx_peer_copy(void* dst, int dst_dev, const void* src, int src_dev,
 int glx_enable_peer(int dev_a, int dev_b);
 
 /* Tuning hook of the reduce kernel: lanes' unroll depth (1, 2, 4 or 8 16-byte
- * vectors in flight per lane) and grid cap in workgroups per CU (0 = keep). */
-int glx_tune_reduce(int unroll, int blocks_per_cu);
+ * vectors in flight per lane), grid cap in workgroups per CU (0 = keep) and
+ * nontemporal streaming loads/stores (0 off, 1 on, -1 keep). */
+int glx_tune_reduce(int unroll, int blocks_per_cu, int nontemporal);
 
 /* Number of visible HIP devices (0 when no GPU). */
 int glx_device_count(int* count);

@@ -12,9 +12,10 @@ res = []
 for mib in (256, 16):
     n = (mib << 20) // 4
     a = torch.rand(n, device="cuda"); b = torch.rand(n, device="cuda"); c = torch.empty_like(a)
-    for unroll in (1, 2, 4, 8):
-        for bpc in (2, 4, 8, 16, 32, 64):
-            _lib.lib.glx_tune_reduce(unroll, bpc)
+    for unroll, bpc, nt in [(u, b, t) for t in (0, 1) for u in (1, 2, 4)
+                            for b in (1, 2, 3, 4, 8, 64)]:
+        if True:
+            _lib.lib.glx_tune_reduce(unroll, bpc, nt)
             for inplace in (False, True):
                 dst = a if inplace else c
                 for _ in range(3):
@@ -28,7 +29,7 @@ for mib in (256, 16):
                 e1.record(); torch.cuda.synchronize()
                 t = e0.elapsed_time(e1) / reps / 1e3
                 gbs = 3 * (mib << 20) / t / 1e9
-                res.append({"mib": mib, "unroll": unroll, "bpc": bpc, "inplace": inplace,
+                res.append({"mib": mib, "unroll": unroll, "bpc": bpc, "nt": nt, "inplace": inplace,
                             "us": round(t * 1e6, 2), "GBps": round(gbs, 1)})
                 print(json.dumps(res[-1]), flush=True)
 best = {}
