@@ -1,0 +1,268 @@
+// gloo_amd.hpp -- header-only C++ surface of the MI355X allreduce path, over
+// the C ABI in glx.h.  It mirrors the reference's operator interface so C++
+// callers of gloo's allreduce switch by changing the namespace:
+//
+//   gloo::rendezvous::HashStore / FileStore / PrefixStore  (gloo/rendezvous/*.h)
+//   gloo::rendezvous::Context(rank, size) + connectFullMesh (gloo/rendezvous/context.h:25-35)
+//   gloo::ReductionFunction<T>::sum/product/min/max         (gloo/algorithm.h:59-96)
+//   gloo::Algorithm::run()                                  (gloo/algorithm.h:20-38)
+//   gloo::CudaAllreduceRingChunked<T>(ctx, ptrs, count, streams)
+//                                      (gloo/cuda_allreduce_ring_chunked.h:22-26)
+//   gloo::CudaAllreduceHalvingDoubling<T>(ctx, ptrs, count, streams)
+//                                      (gloo/cuda_allreduce_halving_doubling.h:25-30)
+//   gloo::EnforceNotMet, gloo::IoException                  (gloo/common/logging.h:21,
+//                                                            gloo/common/error.h:45)
+// become gloo_amd::<same name> (device algorithms: HipAllreduceRingChunked<T>,
+// HipAllreduceHalvingDoubling<T>).  Link with -lgloo_amd.
+#pragma once
+
+#include <chrono>
+#include <cstdint>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "glx.h"
+
+namespace gloo_amd {
+
+struct Exception : public std::runtime_error {
+  explicit Exception(const std::string& m) : std::runtime_error(m) {}
+};
+struct EnforceNotMet : public Exception {
+  explicit EnforceNotMet(const std::string& m) : Exception(m) {}
+};
+struct IoException : public Exception {
+  explicit IoException(const std::string& m) : Exception(m) {}
+};
+struct HipError : public Exception {
+  explicit HipError(const std::string& m) : Exception(m) {}
+};
+
+inline void check(int rc, const char* what) {
+  if (rc == GLX_OK) return;
+  std::string m = std::string(what) + ": " + glx_last_error();
+  switch (rc) {
+    case GLX_ERR_TIMEOUT:
+    case GLX_ERR_IO:
+      throw IoException(m);
+    case GLX_ERR_HIP:
+      throw HipError(m);
+    case GLX_ERR_INVALID:
+    case GLX_ERR_ENFORCE:
+      throw EnforceNotMet(m);
+    default:
+      throw Exception(m);
+  }
+}
+
+template <typename P>
+P* checkHandle(P* p, const char* what) {
+  if (p == nullptr) {
+    std::string m = std::string(what) + ": " + glx_last_error();
+    if (m.find("Timed out") != std::string::npos) throw IoException(m);
+    throw EnforceNotMet(m);
+  }
+  return p;
+}
+
+// 16-bit float element types (raw bits), layout-compatible with gloo::float16.
+struct float16 {
+  uint16_t x;
+};
+struct bfloat16 {
+  uint16_t x;
+};
+
+template <typename T>
+struct DType;
+template <> struct DType<int8_t> { static constexpr int value = GLX_INT8; };
+template <> struct DType<uint8_t> { static constexpr int value = GLX_UINT8; };
+template <> struct DType<int32_t> { static constexpr int value = GLX_INT32; };
+template <> struct DType<int64_t> { static constexpr int value = GLX_INT64; };
+template <> struct DType<uint64_t> { static constexpr int value = GLX_UINT64; };
+template <> struct DType<float> { static constexpr int value = GLX_FLOAT32; };
+template <> struct DType<double> { static constexpr int value = GLX_FLOAT64; };
+template <> struct DType<float16> { static constexpr int value = GLX_FLOAT16; };
+template <> struct DType<bfloat16> { static constexpr int value = GLX_BFLOAT16; };
+
+enum ReductionType { SUM = GLX_SUM, PRODUCT = GLX_PRODUCT, MAX = GLX_MAX, MIN = GLX_MIN };
+
+// gloo::ReductionFunction<T>: the device kernel is selected by type().
+template <typename T>
+class ReductionFunction {
+ public:
+  explicit ReductionFunction(ReductionType t) : type_(t) {}
+  ReductionType type() const { return type_; }
+  static const ReductionFunction<T>* sum;
+  static const ReductionFunction<T>* product;
+  static const ReductionFunction<T>* min;
+  static const ReductionFunction<T>* max;
+
+ private:
+  ReductionType type_;
+};
+template <typename T>
+const ReductionFunction<T>* ReductionFunction<T>::sum = new ReductionFunction<T>(SUM);
+template <typename T>
+const ReductionFunction<T>* ReductionFunction<T>::product = new ReductionFunction<T>(PRODUCT);
+template <typename T>
+const ReductionFunction<T>* ReductionFunction<T>::min = new ReductionFunction<T>(MIN);
+template <typename T>
+const ReductionFunction<T>* ReductionFunction<T>::max = new ReductionFunction<T>(MAX);
+
+namespace rendezvous {
+
+class Store {
+ public:
+  explicit Store(glx_store* s) : s_(checkHandle(s, "Store")) {}
+  virtual ~Store() { glx_store_destroy(s_); }
+  Store(const Store&) = delete;
+  Store& operator=(const Store&) = delete;
+  void set(const std::string& key, const std::vector<char>& data) {
+    check(glx_store_set(s_, key.c_str(), data.data(), data.size()), "Store::set");
+  }
+  std::vector<char> get(const std::string& key,
+                        std::chrono::milliseconds timeout = std::chrono::seconds(30)) {
+    size_t n = 0;
+    check(glx_store_get(s_, key.c_str(), nullptr, 0, &n, timeout.count()), "Store::get");
+    std::vector<char> v(n);
+    check(glx_store_get(s_, key.c_str(), v.data(), v.size(), &n, timeout.count()),
+          "Store::get");
+    return v;
+  }
+  glx_store* handle() const { return s_; }
+
+ private:
+  glx_store* s_;
+};
+
+class HashStore : public Store {
+ public:
+  HashStore() : Store(glx_hash_store_create()) {}
+};
+
+class FileStore : public Store {
+ public:
+  explicit FileStore(const std::string& path) : Store(glx_file_store_create(path.c_str())) {}
+};
+
+class PrefixStore : public Store {
+ public:
+  PrefixStore(const std::string& prefix, Store& base)
+      : Store(glx_prefix_store_create(prefix.c_str(), base.handle())) {}
+};
+
+// gloo::rendezvous::Context bound to one HIP device.
+class Context {
+ public:
+  Context(int rank, int size, int device = -1)
+      : c_(checkHandle(glx_context_create(rank, size, device), "Context")),
+        rank(rank),
+        size(size) {}
+  ~Context() { glx_context_destroy(c_); }
+  Context(const Context&) = delete;
+  Context& operator=(const Context&) = delete;
+
+  void connectFullMesh(Store& store) {
+    check(glx_context_connect_full_mesh(c_, store.handle()), "connectFullMesh");
+  }
+  void setTimeout(std::chrono::milliseconds t) {
+    check(glx_context_set_timeout(c_, t.count()), "setTimeout");
+  }
+  std::chrono::milliseconds getTimeout() const {
+    return std::chrono::milliseconds(glx_context_get_timeout(c_));
+  }
+  int nextSlot(int numToSkip = 1) { return glx_context_next_slot(c_, numToSkip); }
+  glx_context* handle() const { return c_; }
+
+ private:
+  glx_context* c_;
+
+ public:
+  const int rank;
+  const int size;
+};
+
+}  // namespace rendezvous
+
+using Context = rendezvous::Context;
+
+class Algorithm {  // gloo::Algorithm
+ public:
+  virtual ~Algorithm() = default;
+  virtual void run() = 0;
+};
+
+namespace detail {
+template <typename T>
+class DeviceAllreduce : public Algorithm {
+ protected:
+  using Create = glx_algorithm* (*)(glx_context*, void* const*, int, int, int, int,
+                                    const glx_stream_t*, int);
+  DeviceAllreduce(Create create, const std::shared_ptr<Context>& ctx,
+                  const std::vector<T*>& ptrs, int count,
+                  const std::vector<glx_stream_t>& streams, const ReductionFunction<T>* fn)
+      : ctx_(ctx) {
+    std::vector<void*> p(ptrs.begin(), ptrs.end());
+    a_ = checkHandle(create(ctx->handle(), p.data(), (int)p.size(), count, DType<T>::value,
+                            fn->type(), streams.empty() ? nullptr : streams.data(),
+                            (int)streams.size()),
+                     "allreduce");
+  }
+
+ public:
+  ~DeviceAllreduce() override { glx_algorithm_destroy(a_); }
+  void run() override { check(glx_algorithm_run(a_), "run"); }
+  int64_t bytesSentPerRun() const { return glx_algorithm_bytes_sent(a_); }
+
+ private:
+  std::shared_ptr<Context> ctx_;
+  glx_algorithm* a_ = nullptr;
+};
+}  // namespace detail
+
+// gloo::CudaAllreduceRingChunked<T> analog (gloo/cuda_allreduce_ring_chunked.h:22-26).
+template <typename T>
+class HipAllreduceRingChunked : public detail::DeviceAllreduce<T> {
+ public:
+  HipAllreduceRingChunked(const std::shared_ptr<Context>& ctx, const std::vector<T*>& ptrs,
+                          int count, const std::vector<glx_stream_t>& streams = {},
+                          const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
+      : detail::DeviceAllreduce<T>(&glx_allreduce_ring_chunked_create, ctx, ptrs, count,
+                                   streams, fn) {}
+};
+
+// gloo::CudaAllreduceHalvingDoubling<T> analog (gloo/cuda_allreduce_halving_doubling.h:25-30).
+template <typename T>
+class HipAllreduceHalvingDoubling : public detail::DeviceAllreduce<T> {
+ public:
+  HipAllreduceHalvingDoubling(const std::shared_ptr<Context>& ctx,
+                              const std::vector<T*>& ptrs, int count,
+                              const std::vector<glx_stream_t>& streams = {},
+                              const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
+      : detail::DeviceAllreduce<T>(&glx_allreduce_halving_doubling_create, ctx, ptrs, count,
+                                   streams, fn) {}
+};
+
+// gloo::sum<T>(c, a, b, n) on the device (gloo/math.h:15-28).
+template <typename T>
+void sum(T* c, const T* a, const T* b, size_t n, glx_stream_t stream = nullptr) {
+  check(glx_reduce(GLX_SUM, DType<T>::value, c, a, b, n, stream), "sum");
+}
+template <typename T>
+void product(T* c, const T* a, const T* b, size_t n, glx_stream_t stream = nullptr) {
+  check(glx_reduce(GLX_PRODUCT, DType<T>::value, c, a, b, n, stream), "product");
+}
+template <typename T>
+void max(T* c, const T* a, const T* b, size_t n, glx_stream_t stream = nullptr) {
+  check(glx_reduce(GLX_MAX, DType<T>::value, c, a, b, n, stream), "max");
+}
+template <typename T>
+void min(T* c, const T* a, const T* b, size_t n, glx_stream_t stream = nullptr) {
+  check(glx_reduce(GLX_MIN, DType<T>::value, c, a, b, n, stream), "min");
+}
+
+}  // namespace gloo_amd

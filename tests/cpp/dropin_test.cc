@@ -1,0 +1,195 @@
+// dropin_test.cc -- the reference's allreduce test cases, written against the
+// C++ drop-in surface (include/gloo_amd/gloo_amd.hpp) the way
+// gloo/test/allreduce_test.cc is written against gloo: P thread-ranks, one
+// HashStore, one algorithm instance per rank (gloo/test/base_test.h:91-166).
+//
+//   SinglePointer   value = rank -> every element == P(P-1)/2 exactly
+//                   (gloo/test/allreduce_test.cc:143-169, sizes :251-269)
+//   stride pattern  srcs[i][j] = j*stride + rank*ptrs + i ->
+//                   j*stride^2 + stride(stride-1)/2, rel 1e-4
+//                   (gloo/test/base_test.h:184-235)
+//   MultipleAlgorithms: ring + hd on one context, each run twice (:171-210)
+//
+// Exit status 0 = all passed.  Needs a GPU (all ranks share device 0).
+#include <hip/hip_runtime_api.h>
+
+#include <cmath>
+#include <cstdio>
+#include <functional>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "gloo_amd/gloo_amd.hpp"
+
+namespace {
+
+int g_failures = 0;
+
+#define EXPECT(cond, ...)                                 \
+  do {                                                    \
+    if (!(cond)) {                                        \
+      std::fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+      std::fprintf(stderr, __VA_ARGS__);                  \
+      std::fprintf(stderr, "\n");                         \
+      g_failures++;                                       \
+    }                                                     \
+  } while (0)
+
+void hipCheck(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+void spawn(int P, const std::function<void(std::shared_ptr<gloo_amd::Context>)>& fn) {
+  gloo_amd::rendezvous::HashStore store;
+  std::vector<std::thread> ts;
+  std::vector<std::string> errs(P);
+  for (int r = 0; r < P; r++) {
+    ts.emplace_back([&, r] {
+      try {
+        hipCheck(hipSetDevice(0), "hipSetDevice");
+        auto ctx = std::make_shared<gloo_amd::Context>(r, P, 0);
+        ctx->connectFullMesh(store);
+        fn(ctx);
+      } catch (const std::exception& e) {
+        errs[r] = e.what();
+      }
+    });
+  }
+  for (auto& t : ts) t.join();
+  for (int r = 0; r < P; r++) EXPECT(errs[r].empty(), "rank %d threw: %s", r, errs[r].c_str());
+}
+
+template <template <typename> class Alg>
+void singlePointer(const char* name, int P, int N) {
+  spawn(P, [&](std::shared_ptr<gloo_amd::Context> ctx) {
+    std::vector<float> host(N, (float)ctx->rank);
+    float* dev = nullptr;
+    hipCheck(hipMalloc(&dev, std::max(N, 1) * sizeof(float)), "hipMalloc");
+    hipCheck(hipMemcpy(dev, host.data(), N * sizeof(float), hipMemcpyHostToDevice), "h2d");
+    {
+      Alg<float> alg(ctx, {dev}, N);
+      alg.run();
+    }
+    hipCheck(hipMemcpy(host.data(), dev, N * sizeof(float), hipMemcpyDeviceToHost), "d2h");
+    hipFree(dev);
+    const float expected = (float)(P * (P - 1) / 2);
+    for (int i = 0; i < N; i++) {
+      if (host[i] != expected) {
+        EXPECT(false, "%s P=%d N=%d: element %d = %f, expected %f", name, P, N, i, host[i],
+               expected);
+        break;
+      }
+    }
+  });
+}
+
+template <template <typename> class Alg>
+void stridePattern(const char* name, int P, int nptrs, int N) {
+  spawn(P, [&](std::shared_ptr<gloo_amd::Context> ctx) {
+    const int stride = P * nptrs;
+    std::vector<float*> devs(nptrs);
+    for (int i = 0; i < nptrs; i++) {
+      std::vector<float> host(N);
+      for (int j = 0; j < N; j++) host[j] = (float)(j * stride + ctx->rank * nptrs + i);
+      hipCheck(hipMalloc(&devs[i], N * sizeof(float)), "hipMalloc");
+      hipCheck(hipMemcpy(devs[i], host.data(), N * sizeof(float), hipMemcpyHostToDevice), "h2d");
+    }
+    {
+      Alg<float> alg(ctx, devs, N);
+      alg.run();
+    }
+    for (int i = 0; i < nptrs; i++) {
+      std::vector<float> host(N);
+      hipCheck(hipMemcpy(host.data(), devs[i], N * sizeof(float), hipMemcpyDeviceToHost), "d2h");
+      hipFree(devs[i]);
+      for (int j = 0; j < N; j++) {
+        double exp = (double)j * stride * stride + stride * (stride - 1) / 2.0;
+        if (std::fabs(host[j] - exp) > 1e-4 * std::fabs(exp) + 1e-6) {
+          EXPECT(false, "%s stride P=%d ptrs=%d: [%d][%d] = %f expected %f", name, P, nptrs, i,
+                 j, host[j], exp);
+          break;
+        }
+      }
+    }
+  });
+}
+
+void multipleAlgorithms() {
+  const int P = 4, N = 1000;
+  spawn(P, [&](std::shared_ptr<gloo_amd::Context> ctx) {
+    float* dev = nullptr;
+    hipCheck(hipMalloc(&dev, N * sizeof(float)), "hipMalloc");
+    std::vector<std::unique_ptr<gloo_amd::Algorithm>> algs;
+    algs.emplace_back(new gloo_amd::HipAllreduceRingChunked<float>(ctx, {dev}, N));
+    algs.emplace_back(new gloo_amd::HipAllreduceHalvingDoubling<float>(ctx, {dev}, N));
+    for (auto& alg : algs) {
+      for (int rep = 0; rep < 2; rep++) {
+        std::vector<float> host(N, (float)ctx->rank);
+        hipCheck(hipMemcpy(dev, host.data(), N * sizeof(float), hipMemcpyHostToDevice), "h2d");
+        alg->run();
+        hipCheck(hipMemcpy(host.data(), dev, N * sizeof(float), hipMemcpyDeviceToHost), "d2h");
+        for (int i = 0; i < N; i++) {
+          if (host[i] != (float)(P * (P - 1) / 2)) {
+            EXPECT(false, "MultipleAlgorithms rank %d element %d = %f", ctx->rank, i, host[i]);
+            break;
+          }
+        }
+      }
+    }
+    algs.clear();
+    hipFree(dev);
+  });
+}
+
+void timeoutThrowsIoException() {
+  // a lone rank of a 2-rank context: its peer never runs the collective
+  gloo_amd::rendezvous::HashStore store;
+  std::shared_ptr<gloo_amd::Context> ctxs[2];
+  std::thread t1([&] {
+    ctxs[1] = std::make_shared<gloo_amd::Context>(1, 2, 0);
+    ctxs[1]->connectFullMesh(store);
+  });
+  ctxs[0] = std::make_shared<gloo_amd::Context>(0, 2, 0);
+  ctxs[0]->connectFullMesh(store);
+  t1.join();
+  ctxs[0]->setTimeout(std::chrono::milliseconds(50));
+  float* dev = nullptr;
+  hipCheck(hipMalloc(&dev, 4096 * sizeof(float)), "hipMalloc");
+  bool threw = false;
+  try {
+    gloo_amd::HipAllreduceRingChunked<float> alg(ctxs[0], {dev}, 4096);
+    alg.run();
+  } catch (const gloo_amd::IoException& e) {
+    threw = std::string(e.what()).find("Timed out") != std::string::npos;
+  }
+  EXPECT(threw, "expected IoException(\"Timed out ...\")");
+  hipFree(dev);
+}
+
+}  // namespace
+
+int main() {
+  for (int P = 1; P <= 8; P++) {
+    for (int N : {0, 4, 100, 1000, 10000}) {
+      singlePointer<gloo_amd::HipAllreduceRingChunked>("ring_chunked", P, N);
+    }
+  }
+  for (int P : {1, 2, 3, 4, 5, 6, 7, 8, 9, 13}) {
+    for (int N : {0, 1, 64, 1000}) {
+      singlePointer<gloo_amd::HipAllreduceHalvingDoubling>("halving_doubling", P, N);
+    }
+  }
+  for (int P : {2, 3, 4}) {
+    for (int nptrs : {1, 2}) {
+      stridePattern<gloo_amd::HipAllreduceRingChunked>("ring_chunked", P, nptrs, 1000);
+      stridePattern<gloo_amd::HipAllreduceHalvingDoubling>("halving_doubling", P, nptrs, 1000);
+    }
+  }
+  multipleAlgorithms();
+  timeoutThrowsIoException();
+  if (g_failures == 0) std::printf("dropin_test: all passed\n");
+  return g_failures == 0 ? 0 : 1;
+}
