@@ -36,7 +36,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--size-mib", type=int, default=256)
     p.add_argument("--algo", default="ring_chunked",
-                   choices=["ring_chunked", "halving_doubling"])
+                   choices=["ring_chunked", "halving_doubling", "ring_chunked_mesh"])
+    p.add_argument("--no-alt", action="store_true",
+                   help="N>1: do not also time the other schedules")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bounded CPU baseline sample (seconds of CPU work)")
@@ -166,6 +168,35 @@ def reduce_kernel_roofline(torch, gloo_amd, dev, chunk_bytes, reps=50):
             "algorithmic_bytes_per_launch": 3 * chunk_bytes}
 
 
+def make_alg(gloo_amd, ctx, buf, algo):
+    if algo == "halving_doubling":
+        return gloo_amd.AllreduceHalvingDoubling(ctx, [buf])
+    return gloo_amd.AllreduceRingChunked(ctx, [buf],
+                                        schedule="mesh" if algo == "ring_chunked_mesh" else "ring")
+
+
+def time_schedule(torch, dist, gloo_amd, ctx, buf, algo, steps, warmup):
+    """warmup untimed runs, then `steps` timed runs between barriers +
+    device syncs; returns (max-over-ranks seconds per step, link bytes/run)."""
+    alg = make_alg(gloo_amd, ctx, buf, algo)
+    for _ in range(warmup):
+        alg.run()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        alg.run()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    dist.barrier()
+    el = torch.tensor([t1 - t0], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    sent = alg.bytes_sent()
+    alg.close()
+    return el.item() / steps, sent
+
+
 def bench_multi(args):
     import torch
     import torch.distributed as dist
@@ -183,37 +214,42 @@ def bench_multi(args):
     n = S // 4
     steps = args.steps or 20
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    buf = torch.rand(n, device=dev, generator=g) * 2 - 1
+    src = torch.rand(n, device=dev, generator=g) * 2 - 1
+    buf = src.clone()
     torch.cuda.synchronize()
     store = gloo_amd.rendezvous.PrefixStore(
         "gloo_amd_bench", gloo_amd.rendezvous.TorchStore(dist.distributed_c10d._get_default_store()))
     ctx = gloo_amd.rendezvous.Context(rank, world, local)
     ctx.setTimeout(120)
     ctx.connectFullMesh(store)
-    cls = gloo_amd.AllreduceRingChunked if args.algo == "ring_chunked" else \
-        gloo_amd.AllreduceHalvingDoubling
-    alg = cls(ctx, [buf])
-    for _ in range(args.warmup):
-        alg.run()
+    t, link_bytes = time_schedule(torch, dist, gloo_amd, ctx, buf, args.algo, steps,
+                                  args.warmup)
+    # correctness after the timing: one more run on fresh inputs; every rank
+    # must hold the same bits (the reduction order is rank-independent)
+    buf.copy_(src)
     torch.cuda.synchronize()
-    dist.barrier()
+    alg = make_alg(gloo_amd, ctx, buf, args.algo)
+    alg.run()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        alg.run()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    dist.barrier()
-    el = torch.tensor([t1 - t0], dtype=torch.float64)
-    dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    t = el.item() / steps
-    # every rank must hold the same bits (the reduction order is rank-independent)
+    alg.close()
     cs = torch.tensor([int(buf.view(torch.int32).to(torch.int64).sum().item())],
                       dtype=torch.int64)
     allcs = [torch.zeros_like(cs) for _ in range(world)]
     dist.all_gather(allcs, cs)
     verified = all(int(x.item()) == int(cs.item()) for x in allcs)
-    link_bytes = alg.bytes_sent()
+    alts = {}
+    if not args.no_alt:
+        for other in ("ring_chunked", "ring_chunked_mesh", "halving_doubling"):
+            if other == args.algo:
+                continue
+            buf.copy_(src)
+            torch.cuda.synchronize()
+            ta, sent_a = time_schedule(torch, dist, gloo_amd, ctx, buf, other, steps,
+                                       args.warmup)
+            alts[other] = {"value": round(world * S / ta / 1e9, 3),
+                           "ms_per_step": round(ta * 1e3, 4),
+                           "algbw_GBps": round(S / ta / 1e9, 3),
+                           "link_bytes_per_step": sent_a}
     res = None
     if rank == 0:
         chunk = max(256 * 4, -(-S // (2 * world)))
@@ -229,17 +265,19 @@ def bench_multi(args):
             "config": {"workload": "allreduce_%s_fp32_256MiB_per_rank" % args.algo,
                        "algorithm": args.algo, "bytes_per_rank": S, "elements": n,
                        "parallelism": "dp%d" % world, "transport": "hipMemcpyPeerAsync/xGMI",
-                       "baseline_config": "configs[2]" if args.algo == "ring_chunked"
-                       else "configs[3]"},
+                       "baseline_config": "configs[3]" if args.algo == "halving_doubling"
+                       else "configs[2]"},
             "algbw_GBps": round(algbw, 3), "busbw_GBps": round(busbw, 3),
             "roofline": reduce_kernel_roofline(torch, gloo_amd, dev, chunk),
             "link_roofline": {"bound": "xgmi_link", "achieved": round(link_ach, 2),
                               "peak": XGMI_LINK_GBPS, "unit": "GB/s",
                               "frac": round(link_ach / XGMI_LINK_GBPS, 4),
-                              "link_bytes_per_step": link_bytes},
+                              "link_bytes_per_step": link_bytes,
+                              "note": "bytes this rank sent per step / step time; the "
+                                      "ring uses one link per direction"},
+            "alt_schedules": alts,
             "verified": verified,
         }
-    alg.close()
     dist.barrier()
     dist.destroy_process_group()
     return res

@@ -59,11 +59,14 @@ SIGNATURES = [
      [_vp, ctypes.POINTER(_vp), _i, _i, _i, _i, ctypes.POINTER(_vp), _i]),
     ("glx_allreduce_halving_doubling_create", _vp,
      [_vp, ctypes.POINTER(_vp), _i, _i, _i, _i, ctypes.POINTER(_vp), _i]),
+    ("glx_allreduce_create", _vp,
+     [_vp, _i, ctypes.POINTER(_vp), _i, _i, _i, _i, ctypes.POINTER(_vp), _i]),
     ("glx_algorithm_run", _i, [_vp]),
     ("glx_algorithm_bytes_sent", _i64, [_vp]),
     ("glx_algorithm_destroy", None, [_vp]),
     ("glx_plan", _i64, [_i, _i, _i, _i64, ctypes.POINTER(_i64), _i64,
                         ctypes.POINTER(_i64)]),
+    ("glx_plan_fold", _i64, [_i, _i, _i, _i64, _i64, ctypes.POINTER(_i64), _i64]),
 ]
 
 for _name, _res, _args in SIGNATURES:

@@ -93,10 +93,16 @@ def _stream_ptr(s):
     return s.cuda_stream  # torch.cuda.Stream
 
 
+ALGO_CODES = {"ring_chunked": 0, "halving_doubling": 1, "ring_chunked_mesh": 2}
+
+
 class Algorithm:
     """gloo::Algorithm (gloo/algorithm.h:20-38)."""
 
-    _create = None
+    _algo = None
+
+    def _create(self, *args):
+        return lib.glx_allreduce_create(args[0], self._algo, *args[1:])
 
     def __init__(self, context, ptrs, count=None, fn=None, streams=None, dtype=None):
         if fn is None:
@@ -124,8 +130,7 @@ class Algorithm:
             sarr, ns = None, 0
         self._streams = streams
         self._h = check_handle(
-            type(self)._create(context.handle, arr, len(pp), self.count, dt, fn.type(),
-                               sarr, ns),
+            self._create(context.handle, arr, len(pp), self.count, dt, fn.type(), sarr, ns),
             type(self).__name__)
 
     def run(self):
@@ -147,13 +152,25 @@ class Algorithm:
 
 class AllreduceRingChunked(Algorithm):
     """gloo::AllreduceRingChunked<T> (gloo/allreduce_ring_chunked.h:19) on
-    MI355X: xGMI peer copies + HIP reduce kernel, same chunking and order."""
-    _create = lib.glx_allreduce_ring_chunked_create
+    MI355X: xGMI peer copies + HIP reduce kernel, same chunking and order.
+
+    schedule="ring" (default) moves chunks around the ring exactly as the
+    reference does (one link per direction); schedule="mesh" computes the
+    identical result (same chunks, same reduction chain and operand order)
+    with every rank exchanging directly with every peer over all links."""
+
+    def __init__(self, context, ptrs, count=None, fn=None, streams=None, dtype=None,
+                 schedule="ring"):
+        if schedule not in ("ring", "mesh"):
+            raise ValueError("schedule must be 'ring' or 'mesh'")
+        self._algo = ALGO_CODES["ring_chunked_mesh" if schedule == "mesh" else "ring_chunked"]
+        self.schedule = schedule
+        super().__init__(context, ptrs, count, fn, streams, dtype)
 
 
 class AllreduceHalvingDoubling(Algorithm):
     """gloo::AllreduceHalvingDoubling<T> (gloo/allreduce_halving_doubling.h:37)."""
-    _create = lib.glx_allreduce_halving_doubling_create
+    _algo = ALGO_CODES["halving_doubling"]
 
 
 # The device classes under the names the reference's GPU path uses.
@@ -161,10 +178,10 @@ HipAllreduceRingChunked = AllreduceRingChunked
 HipAllreduceHalvingDoubling = AllreduceHalvingDoubling
 
 
-def plan(algo, rank, size, count):
-    """The step program of one rank (host logic, no GPU).  algo: 'ring_chunked'
-    or 'halving_doubling'.  Returns (steps as list of 8-tuples, scratch_elems)."""
-    code = {"ring_chunked": 0, "halving_doubling": 1}[algo]
+def plan(algo, rank, size, count, with_folds=False):
+    """The step program of one rank (host logic, no GPU).  algo: a key of
+    ALGO_CODES.  Returns (steps as 8-tuples, scratch_elems[, fold sources])."""
+    code = ALGO_CODES[algo]
     scratch = ctypes.c_int64(0)
     n = lib.glx_plan(code, rank, size, count, None, 0, ctypes.byref(scratch))
     if n < 0:
@@ -172,4 +189,13 @@ def plan(algo, rank, size, count):
     buf = (ctypes.c_int64 * (8 * max(n, 1)))()
     lib.glx_plan(code, rank, size, count, buf, n, ctypes.byref(scratch))
     steps = [tuple(buf[8 * i: 8 * i + 8]) for i in range(n)]
-    return steps, scratch.value
+    if not with_folds:
+        return steps, scratch.value
+    folds = {}
+    for st in steps:
+        if st[0] == 5:
+            k = lib.glx_plan_fold(code, rank, size, count, st[5], None, 0)
+            fb = (ctypes.c_int64 * max(k, 1))()
+            lib.glx_plan_fold(code, rank, size, count, st[5], fb, k)
+            folds[st[5]] = list(fb[:k])
+    return steps, scratch.value, folds

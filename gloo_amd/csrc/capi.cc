@@ -283,6 +283,16 @@ glx_algorithm* glx_allreduce_halving_doubling_create(glx_context* ctx, void* con
                        streams, nstreams);
 }
 
+glx_algorithm* glx_allreduce_create(glx_context* ctx, int algo, void* const* ptrs, int nptrs,
+                                    int count, int dtype, int op, const glx_stream_t* streams,
+                                    int nstreams) {
+  if (algo < GLX_ALGO_RING_CHUNKED || algo > GLX_ALGO_RING_CHUNKED_MESH) {
+    fail(GLX_ERR_INVALID, "glx_allreduce_create: unknown algorithm");
+    return nullptr;
+  }
+  return makeAlgorithm(algo, ctx, ptrs, nptrs, count, dtype, op, streams, nstreams);
+}
+
 int glx_algorithm_run(glx_algorithm* alg) {
   return guarded([&]() -> int {
     GLX_ENFORCE(alg != nullptr, "null algorithm");
@@ -323,6 +333,20 @@ int64_t glx_plan(int algo, int rank, int size, int64_t count, int64_t* steps, in
       o[6] = s.dst_off;
       o[7] = s.flags;
     }
+    return GLX_OK;
+  });
+  return n;
+}
+
+int64_t glx_plan_fold(int algo, int rank, int size, int64_t count, int64_t fold,
+                      int64_t* srcs, int64_t cap) {
+  int64_t n = -1;
+  guarded([&]() -> int {
+    glx::Plan p = glx::makePlan(algo, rank, size, count);
+    GLX_ENFORCE(fold >= 0 && fold < (int64_t)p.folds.size(), "fold index out of range");
+    const auto& f = p.folds[(size_t)fold];
+    n = (int64_t)f.size();
+    for (int64_t i = 0; i < n && i < cap && srcs != nullptr; i++) srcs[i] = f[(size_t)i];
     return GLX_OK;
   });
   return n;

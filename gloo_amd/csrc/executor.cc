@@ -66,7 +66,6 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
     GLX_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
     ownCompute_ = true;
   }
-  GLX_HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
   myPhase_ = (int)((uintptr_t)ptrs[0] % 16);
 
   if (plan_.scratch_elems > 0) {
@@ -89,6 +88,18 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
         oc.tag = (int)s.channel;
         oc.creditWord = ctl.allocWord();
         oc.credit = ctl.word(oc.creditWord);
+        // one copy stream per destination peer: copies to different peers
+        // run concurrently on different xGMI links
+        oc.stream = -1;
+        for (const auto& o : out_) {
+          if (o.peer == oc.peer) oc.stream = o.stream;
+        }
+        if (oc.stream < 0) {
+          CopyStream cs;
+          GLX_HIP_CHECK(hipStreamCreateWithFlags(&cs.s, hipStreamNonBlocking));
+          copies_.push_back(cs);
+          oc.stream = (int)copies_.size() - 1;
+        }
         out_.push_back(oc);
         idx = (int)out_.size() - 1;
       }
@@ -116,12 +127,12 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
 HipPlanExecutor::~HipPlanExecutor() noexcept(false) {
   hipSetDevice(device_);
   if (compute_ != nullptr) hipStreamSynchronize(compute_);
-  if (copy_ != nullptr) hipStreamSynchronize(copy_);
+  for (auto& c : copies_) hipStreamSynchronize(c.s);
   for (void* p : ipcOpened_) hipIpcCloseMemHandle(p);
   for (auto& e : events_) hipEventDestroy(e);
   if (computeMark_) hipEventDestroy(computeMark_);
   if (scratch_) hipFree(scratch_);
-  if (copy_) hipStreamDestroy(copy_);
+  for (auto& c : copies_) hipStreamDestroy(c.s);
   if (ownCompute_ && compute_) hipStreamDestroy(compute_);
   auto& ctl = context_->localControl();
   for (auto& oc : out_) ctl.freeWord(oc.creditWord);
@@ -334,7 +345,7 @@ void HipPlanExecutor::run() {
   if (contextSize_ > 1) {
     if (!resolved_) resolvePeers();
     bool computeSinceMark = true;  // the caller's writes to ptr0 count as compute
-    lastCopy_ = nullptr;
+    for (auto& c : copies_) c.last = nullptr;
     const auto& steps = plan_.steps;
     for (size_t i = 0; i < steps.size(); i++) {
       const glx::Step& s = steps[i];
@@ -348,20 +359,26 @@ void HipPlanExecutor::run() {
                   "receive-region credit", oc.peer);
           const size_t nbytes = (size_t)s.len * esize_;
           if (nbytes > 0) {
+            CopyStream& cs = copies_[oc.stream];
             if (computeSinceMark) {
               GLX_HIP_CHECK(hipEventRecord(computeMark_, compute_));
-              GLX_HIP_CHECK(hipStreamWaitEvent(copy_, computeMark_, 0));
+              markEpoch_++;
               computeSinceMark = false;
+            }
+            if (cs.waitedMark != markEpoch_) {
+              // the chunk may have been produced by compute work: order after it
+              GLX_HIP_CHECK(hipStreamWaitEvent(cs.s, computeMark_, 0));
+              cs.waitedMark = markEpoch_;
             }
             char* dst = landing(oc.peerScratch, s.dst_off, s.off, oc.peerPhase);
             const char* src = ptr0 + (size_t)s.off * esize_;
             if (oc.peerDevice >= 0 && oc.peerDevice != device_) {
-              GLX_HIP_CHECK(hipMemcpyPeerAsync(dst, oc.peerDevice, src, device_, nbytes, copy_));
+              GLX_HIP_CHECK(hipMemcpyPeerAsync(dst, oc.peerDevice, src, device_, nbytes, cs.s));
             } else {
-              GLX_HIP_CHECK(hipMemcpyAsync(dst, src, nbytes, hipMemcpyDeviceToDevice, copy_));
+              GLX_HIP_CHECK(hipMemcpyAsync(dst, src, nbytes, hipMemcpyDeviceToDevice, cs.s));
             }
-            GLX_HIP_CHECK(hipEventRecord(events_[i], copy_));
-            lastCopy_ = events_[i];
+            GLX_HIP_CHECK(hipEventRecord(events_[i], cs.s));
+            cs.last = events_[i];
             inflight_.push_back({s.off, s.len, events_[i]});
             pending_.push_back({events_[i], oc.delivery, n});
           } else {
@@ -381,6 +398,20 @@ void HipPlanExecutor::run() {
           char* dst = ptr0 + (size_t)s.off * esize_;
           const char* src = landing(scratch_, s.boff, s.off, myPhase_);
           GLX_HIP_CHECK(glx::launch_reduce(op_, dtype_, dst, dst, src, (size_t)s.len, compute_));
+          computeSinceMark = true;
+          break;
+        }
+        case glx::FOLD: {
+          waitWar(s.off, s.len);
+          char* dst = ptr0 + (size_t)s.off * esize_;
+          const auto& regions = plan_.folds[(size_t)s.boff];
+          std::vector<const void*> srcs;
+          for (int64_t r : regions) {
+            srcs.push_back(r < 0 ? (const void*)dst
+                                 : (const void*)landing(scratch_, r, s.off, myPhase_));
+          }
+          GLX_HIP_CHECK(glx::launch_reduce_n(op_, dtype_, dst, srcs.data(), (int)srcs.size(),
+                                             (size_t)s.len, compute_, /*rev=*/true));
           computeSinceMark = true;
           break;
         }
@@ -407,7 +438,9 @@ void HipPlanExecutor::run() {
     }
     drain();
     // the caller's stream must not run ahead of copies still reading ptr0
-    if (lastCopy_ != nullptr) GLX_HIP_CHECK(hipStreamWaitEvent(compute_, lastCopy_, 0));
+    for (auto& c : copies_) {
+      if (c.last != nullptr) GLX_HIP_CHECK(hipStreamWaitEvent(compute_, c.last, 0));
+    }
     inflight_.clear();
   }
   // Local broadcast of ptrs_[0] (:209-211).

@@ -60,6 +60,12 @@ class HipPlanExecutor : public Algorithm {
     char* peerScratch = nullptr;
     int peerPhase = 0;  // peer ptr0 address mod 16
     int peerDevice = -1;
+    int stream = 0;     // index into copies_ (one copy stream per destination peer)
+  };
+  struct CopyStream {
+    hipStream_t s = nullptr;
+    uint64_t waitedMark = 0;      // last compute mark this stream waited on
+    hipEvent_t last = nullptr;    // last copy recorded in the current run
   };
   struct InChan {  // peer -> this rank
     int peer, tag;
@@ -99,7 +105,8 @@ class HipPlanExecutor : public Algorithm {
   int slot_;
   bool userStream_;
   hipStream_t compute_ = nullptr;
-  hipStream_t copy_ = nullptr;
+  std::vector<CopyStream> copies_;
+  uint64_t markEpoch_ = 0;
   bool ownCompute_ = false;
   char* scratch_ = nullptr;
   size_t scratchBytes_ = 0;
@@ -109,7 +116,6 @@ class HipPlanExecutor : public Algorithm {
   std::vector<int> stepChan_;        // channel index per step
   std::vector<hipEvent_t> events_;   // one per step
   hipEvent_t computeMark_ = nullptr;
-  hipEvent_t lastCopy_ = nullptr;
   bool resolved_ = false;
   std::vector<Pending> pending_;
   std::vector<InflightSend> inflight_;

@@ -10,9 +10,11 @@ namespace glx {
 hipError_t launch_reduce(int op, int dtype, void* dst, const void* a,
                          const void* b, size_t n, hipStream_t s);
 
-// dst = left fold of op over srcs[0..k-1] (2 <= k <= 8).
+// Fold of op over srcs[0..k-1] (k >= 1): acc = srcs[0], then
+// acc = op(acc, srcs[j]) (rev = false, left fold) or acc = op(srcs[j], acc)
+// (rev = true, the ring's chain order).  dst may alias srcs[0].
 hipError_t launch_reduce_n(int op, int dtype, void* dst, const void* const* srcs,
-                           int k, size_t n, hipStream_t s);
+                           int k, size_t n, hipStream_t s, bool rev = false);
 
 // Tuning knobs of the vector kernel (lanes' unroll depth, grid cap per CU,
 // nontemporal loads/stores: 0/1, -1 = keep).

@@ -280,10 +280,76 @@ Plan planHalvingDoubling(int rank, int size, int64_t count) {
   return p;
 }
 
+// ---------------------------------------------------------------------------
+// ring_chunked semantics over the full xGMI mesh
+// ---------------------------------------------------------------------------
+// The ring (gloo/allreduce_ring_chunked.h:106-158) reduces chunk pair j
+// (chunks 2j, 2j+1) along ranks j, j+1, ..., j+P-1: rank j+k computes
+// op(x[j+k], partial) in place.  Here rank j receives x[j+1..j+P-1] of pair j
+// directly from each owner (P-1 copies, P-1 different links) and evaluates the
+// same chain in one FOLD; then it sends the finished pair to every rank
+// (the broadcast pass, :163-200, as one all-to-all round).
+Plan planRingChunkedMesh(int rank, int size, int64_t count) {
+  Plan p;
+  if (count == 0 || size == 1) return p;
+  const int64_t chunks = 2 * (int64_t)size;
+  const int64_t chunkSize = std::max<int64_t>(256, (count + chunks - 1) / chunks);
+  const int64_t region = 2 * chunkSize + kPadElems;
+  auto pair = [&](int j, int64_t* off, int64_t* len) {
+    int64_t o = 2 * (int64_t)j * chunkSize;
+    int64_t l = 0;
+    if (o < count) l = std::min(2 * chunkSize, count - o);
+    *off = o;
+    *len = l;
+  };
+  // scratch: [0, P) reduce-scatter regions by source rank, [P, 2P) results
+  p.scratch_elems = 2 * (int64_t)size * region;
+  int64_t myOff, myLen;
+  pair(rank, &myOff, &myLen);
+  for (int d = 1; d < size; d++) {  // my copy of pair j to its owner j
+    const int j = (rank + d) % size;
+    int64_t off, len;
+    pair(j, &off, &len);
+    if (len == 0) continue;
+    p.steps.push_back({SEND, j, 0, off, len, 0, (int64_t)rank * region, 0});
+    p.bytes_sent += len;
+  }
+  if (myLen > 0) {
+    std::vector<int64_t> srcs{-1};  // x[rank] is ptr0 itself
+    for (int k = 1; k < size; k++) {
+      const int from = (rank + k) % size;
+      p.steps.push_back({RECV, from, 0, 0, myLen, (int64_t)from * region, 0, 0});
+      srcs.push_back((int64_t)from * region);
+    }
+    p.folds.push_back(srcs);
+    p.steps.push_back({FOLD, -1, (int64_t)srcs.size(), myOff, myLen,
+                       (int64_t)p.folds.size() - 1, 0, 0});
+    for (int k = 1; k < size; k++) {
+      p.steps.push_back({RELEASE, (rank + k) % size, 0, 0, 0, 0, 0, 0});
+    }
+    for (int d = 1; d < size; d++) {  // the finished pair to everyone
+      const int j = (rank + d) % size;
+      p.steps.push_back({SEND, j, 1, myOff, myLen, 0, (int64_t)(size + rank) * region, 0});
+      p.bytes_sent += myLen;
+    }
+  }
+  for (int d = 1; d < size; d++) {
+    const int k = (rank - d + size) % size;
+    int64_t off, len;
+    pair(k, &off, &len);
+    if (len == 0) continue;
+    p.steps.push_back({RECV, k, 1, 0, len, (int64_t)(size + k) * region, 0, 0});
+    p.steps.push_back({COPY, 0, 0, off, len, (int64_t)(size + k) * region, 0, 0});
+    p.steps.push_back({RELEASE, k, 1, 0, 0, 0, 0, 0});
+  }
+  return p;
+}
+
 Plan makePlan(int algo, int rank, int size, int64_t count) {
   if (size < 1 || rank < 0 || rank >= size || count < 0) fail("bad geometry");
   if (algo == ALGO_RING_CHUNKED) return planRingChunked(rank, size, count);
   if (algo == ALGO_HALVING_DOUBLING) return planHalvingDoubling(rank, size, count);
+  if (algo == ALGO_RING_CHUNKED_MESH) return planRingChunkedMesh(rank, size, count);
   fail("unknown algorithm");
   return Plan();
 }

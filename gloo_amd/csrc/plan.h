@@ -13,6 +13,11 @@
 //   COPY    ptr0[off, off+len) = region(boff)
 //   RELEASE the last message of (peer, channel) is consumed: once the GPU
 //           work reading it completes, credit the sender.
+//   FOLD    ptr0[off, off+len) = op(s[k-1], ... op(s[2], op(s[1], s[0]))),
+//           s[0] = ptr0[off, off+len) and s[i] = region(folds[boff][i]) --
+//           the ring's per-chunk reduction chain evaluated in one pass (the
+//           operand order of every op is the ring's: the newer rank's value
+//           first, the running partial second).
 //
 // Region offsets are in elements; each region is padded by kPadElems so a
 // message can land at the 16-byte phase of the receiver's ptr0 (keeps the
@@ -24,7 +29,7 @@
 
 namespace glx {
 
-enum StepKind : int64_t { SEND = 0, RECV = 1, REDUCE = 2, COPY = 3, RELEASE = 4 };
+enum StepKind : int64_t { SEND = 0, RECV = 1, REDUCE = 2, COPY = 3, RELEASE = 4, FOLD = 5 };
 
 struct Step {
   int64_t kind;
@@ -39,11 +44,12 @@ struct Step {
 
 struct Plan {
   std::vector<Step> steps;
+  std::vector<std::vector<int64_t>> folds;  // FOLD sources (region offsets; -1 = ptr0)
   int64_t scratch_elems = 0;  // receive-region space (incl. padding), elements
   int64_t bytes_sent = 0;     // payload bytes this rank sends per run (for metrics)
 };
 
-enum Algo { ALGO_RING_CHUNKED = 0, ALGO_HALVING_DOUBLING = 1 };
+enum Algo { ALGO_RING_CHUNKED = 0, ALGO_HALVING_DOUBLING = 1, ALGO_RING_CHUNKED_MESH = 2 };
 
 // Region padding: room to land a message at any 16-byte phase after
 // rounding its region base up to 16 bytes (<= 30 bytes for 1-byte elements).
@@ -53,6 +59,11 @@ constexpr int64_t kPadElems = 32;
 Plan planRingChunked(int rank, int size, int64_t count);
 // gloo/allreduce_halving_doubling.h:37-361
 Plan planHalvingDoubling(int rank, int size, int64_t count);
+
+// ring_chunked's chunking and exact reduction order, moved over all links:
+// every rank folds its own chunk pair from the other ranks' copies (one
+// xGMI link per peer), then sends the result to everyone.
+Plan planRingChunkedMesh(int rank, int size, int64_t count);
 
 Plan makePlan(int algo, int rank, int size, int64_t count);
 

@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <type_traits>
+#include <vector>
 
 #include "common.h"
 #include "kernels.h"
@@ -272,11 +273,23 @@ __global__ __launch_bounds__(kBlock) void reduce_scalar_kernel(
     dst[i] = E::apply3(dst[i], a[i], b[i]);
 }
 
-// Left fold over k <= 8 sources (local multi-pointer reduce).  Same phase
-// requirement as reduce_kernel; the host falls back to pairwise calls.
-struct SrcPtrs { const void* p[8]; };
+// Fold over k <= kMaxSrc sources, one pass:
+//   REV = false: acc = s0; acc = op(acc, s_j)   -- left fold, the reference's
+//                local multi-pointer reduce (gloo/allreduce_ring_chunked.h:89-91)
+//   REV = true : acc = s0; acc = op(s_j, acc)   -- the ring's per-chunk chain,
+//                where each rank applies op(own value, incoming partial)
+//                (gloo/allreduce_ring_chunked.h:145)
+// Same 16-byte phase requirement as reduce_kernel (else the scalar kernel).
+constexpr int kMaxSrc = 16;
+struct SrcPtrs { const void* p[kMaxSrc]; };
 
-template <typename T, int OP, int UNROLL>
+template <typename T, int OP, bool REV>
+__device__ __forceinline__ typename Elem<T, OP>::S fold_step(typename Elem<T, OP>::S acc,
+                                                             typename Elem<T, OP>::S y) {
+  return REV ? Elem<T, OP>::apply(y, acc) : Elem<T, OP>::apply(acc, y);
+}
+
+template <typename T, int OP, int UNROLL, bool REV>
 __global__ __launch_bounds__(kBlock) void reduce_n_kernel(
     typename Elem<T, OP>::S* dst, SrcPtrs srcs, int k, size_t head, size_t nvec,
     size_t tail) {
@@ -285,15 +298,13 @@ __global__ __launch_bounds__(kBlock) void reduce_n_kernel(
   constexpr int V = 16 / sizeof(S);
   const size_t gtid = (size_t)blockIdx.x * kBlock + threadIdx.x;
   auto src = [&](int j) { return reinterpret_cast<const S*>(srcs.p[j]); };
-  if (gtid < head || gtid < tail) {
-    for (int side = 0; side < 2; side++) {
-      size_t lim = side == 0 ? head : tail;
-      if (gtid >= lim) continue;
-      size_t i = side == 0 ? gtid : head + nvec * V + gtid;
-      S acc = E::apply(src(0)[i], src(1)[i]);
-      for (int j = 2; j < k; j++) acc = E::apply(acc, src(j)[i]);
-      dst[i] = acc;
-    }
+  for (int side = 0; side < 2; side++) {
+    size_t lim = side == 0 ? head : tail;
+    if (gtid >= lim) continue;
+    size_t i = side == 0 ? gtid : head + nvec * V + gtid;
+    S acc = src(0)[i];
+    for (int j = 1; j < k; j++) acc = fold_step<T, OP, REV>(acc, src(j)[i]);
+    dst[i] = acc;
   }
   v4u* vd = reinterpret_cast<v4u*>(dst + head);
   const size_t step = (size_t)gridDim.x * kBlock * UNROLL;
@@ -303,27 +314,39 @@ __global__ __launch_bounds__(kBlock) void reduce_n_kernel(
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) {
       size_t i = base + (size_t)u * kBlock;
-      if (i < nvec) {
-        v4u x = reinterpret_cast<const v4u*>(src(0) + head)[i];
-        v4u y = reinterpret_cast<const v4u*>(src(1) + head)[i];
-        acc[u] = vec_apply<T, OP>(x, y);
-      }
+      if (i < nvec) acc[u] = ld16<true>(reinterpret_cast<const v4u*>(src(0) + head) + i);
     }
-    for (int j = 2; j < k; j++) {
+    for (int j = 1; j < k; j++) {
+      v4u y[UNROLL];
 #pragma unroll
       for (int u = 0; u < UNROLL; u++) {
         size_t i = base + (size_t)u * kBlock;
-        if (i < nvec) {
-          v4u y = reinterpret_cast<const v4u*>(src(j) + head)[i];
-          acc[u] = vec_apply<T, OP>(acc[u], y);
-        }
+        if (i < nvec) y[u] = ld16<true>(reinterpret_cast<const v4u*>(src(j) + head) + i);
+      }
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++) {
+        size_t i = base + (size_t)u * kBlock;
+        if (i < nvec) acc[u] = REV ? vec_apply<T, OP>(y[u], acc[u]) : vec_apply<T, OP>(acc[u], y[u]);
       }
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) {
       size_t i = base + (size_t)u * kBlock;
-      if (i < nvec) vd[i] = acc[u];
+      if (i < nvec) st16<true>(vd + i, acc[u]);
     }
+  }
+}
+
+template <typename T, int OP, bool REV>
+__global__ __launch_bounds__(kBlock) void reduce_n_scalar_kernel(
+    typename Elem<T, OP>::S* dst, SrcPtrs srcs, int k, size_t n) {
+  using S = typename Elem<T, OP>::S;
+  const size_t step = (size_t)gridDim.x * kBlock;
+  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += step) {
+    S acc = reinterpret_cast<const S*>(srcs.p[0])[i];
+    for (int j = 1; j < k; j++)
+      acc = fold_step<T, OP, REV>(acc, reinterpret_cast<const S*>(srcs.p[j])[i]);
+    dst[i] = acc;
   }
 }
 
@@ -418,24 +441,23 @@ hipError_t launch_op(int op, void* dst, const void* a, const void* b, size_t n,
   return hipErrorInvalidValue;
 }
 
-template <typename T, int OP>
-hipError_t launch_n_typed(void* dst, const void* const* srcs, int k, size_t n,
-                          hipStream_t s) {
+template <typename T, int OP, bool REV>
+hipError_t launch_n_pass(void* dst, const void* const* srcs, int k, size_t n,
+                         hipStream_t s) {
   using S = typename Elem<T, OP>::S;
   constexpr size_t es = sizeof(S);
   constexpr size_t V = 16 / es;
+  SrcPtrs sp{};
+  for (int j = 0; j < k; j++) sp.p[j] = srcs[j];
   uintptr_t phase = (uintptr_t)dst % 16;
   bool same = ((uintptr_t)dst % es) == 0;
   for (int j = 0; j < k; j++) same = same && ((uintptr_t)srcs[j] % 16) == phase;
   if (!same) {
-    // pairwise left fold keeps the exact same order of operations
-    hipError_t e = launch_typed<T, OP>(dst, srcs[0], srcs[1], n, s);
-    for (int j = 2; j < k && e == hipSuccess; j++)
-      e = launch_typed<T, OP>(dst, dst, srcs[j], n, s);
-    return e;
+    size_t blocks = grid_for(n, 4);
+    hipLaunchKernelGGL((reduce_n_scalar_kernel<T, OP, REV>), dim3((unsigned)blocks),
+                       dim3(kBlock), 0, s, (S*)dst, sp, k, n);
+    return hipGetLastError();
   }
-  SrcPtrs sp{};
-  for (int j = 0; j < k; j++) sp.p[j] = srcs[j];
   size_t head = ((16 - phase) % 16) / es;
   if (head > n) head = n;
   size_t nvec = (n - head) / V;
@@ -443,19 +465,40 @@ hipError_t launch_n_typed(void* dst, const void* const* srcs, int k, size_t n,
   size_t blocks = grid_for(nvec, 4);
   size_t edge_blocks = (std::max(head, tail) + kBlock - 1) / kBlock;
   if (blocks < edge_blocks) blocks = edge_blocks;
-  hipLaunchKernelGGL((reduce_n_kernel<T, OP, 4>), dim3((unsigned)blocks),
+  hipLaunchKernelGGL((reduce_n_kernel<T, OP, 4, REV>), dim3((unsigned)blocks),
                      dim3(kBlock), 0, s, (S*)dst, sp, k, head, nvec, tail);
   return hipGetLastError();
 }
 
+// Folds of more than kMaxSrc sources continue from dst in further passes.
+template <typename T, int OP>
+hipError_t launch_n_typed(void* dst, const void* const* srcs, int k, size_t n,
+                          hipStream_t s, bool rev) {
+  std::vector<const void*> v(srcs, srcs + k);
+  int at = 0;
+  hipError_t e = hipSuccess;
+  bool first = true;
+  while (e == hipSuccess && (first || at < k)) {
+    std::vector<const void*> pass;
+    if (!first) pass.push_back(dst);
+    while (at < k && (int)pass.size() < kMaxSrc) pass.push_back(v[at++]);
+    if (pass.size() >= 2 || first) {
+      e = rev ? launch_n_pass<T, OP, true>(dst, pass.data(), (int)pass.size(), n, s)
+              : launch_n_pass<T, OP, false>(dst, pass.data(), (int)pass.size(), n, s);
+    }
+    first = false;
+  }
+  return e;
+}
+
 template <typename T>
 hipError_t launch_n_op(int op, void* dst, const void* const* srcs, int k,
-                       size_t n, hipStream_t s) {
+                       size_t n, hipStream_t s, bool rev) {
   switch (op) {
-    case GLX_SUM: return launch_n_typed<T, GLX_SUM>(dst, srcs, k, n, s);
-    case GLX_PRODUCT: return launch_n_typed<T, GLX_PRODUCT>(dst, srcs, k, n, s);
-    case GLX_MAX: return launch_n_typed<T, GLX_MAX>(dst, srcs, k, n, s);
-    case GLX_MIN: return launch_n_typed<T, GLX_MIN>(dst, srcs, k, n, s);
+    case GLX_SUM: return launch_n_typed<T, GLX_SUM>(dst, srcs, k, n, s, rev);
+    case GLX_PRODUCT: return launch_n_typed<T, GLX_PRODUCT>(dst, srcs, k, n, s, rev);
+    case GLX_MAX: return launch_n_typed<T, GLX_MAX>(dst, srcs, k, n, s, rev);
+    case GLX_MIN: return launch_n_typed<T, GLX_MIN>(dst, srcs, k, n, s, rev);
   }
   return hipErrorInvalidValue;
 }
@@ -480,18 +523,18 @@ hipError_t launch_reduce(int op, int dtype, void* dst, const void* a,
 }
 
 hipError_t launch_reduce_n(int op, int dtype, void* dst, const void* const* srcs,
-                           int k, size_t n, hipStream_t s) {
+                           int k, size_t n, hipStream_t s, bool rev) {
   if (n == 0) return hipSuccess;
   switch (dtype) {
-    case GLX_INT8: return launch_n_op<int8_t>(op, dst, srcs, k, n, s);
-    case GLX_UINT8: return launch_n_op<uint8_t>(op, dst, srcs, k, n, s);
-    case GLX_INT32: return launch_n_op<int32_t>(op, dst, srcs, k, n, s);
-    case GLX_INT64: return launch_n_op<int64_t>(op, dst, srcs, k, n, s);
-    case GLX_UINT64: return launch_n_op<uint64_t>(op, dst, srcs, k, n, s);
-    case GLX_FLOAT32: return launch_n_op<float>(op, dst, srcs, k, n, s);
-    case GLX_FLOAT64: return launch_n_op<double>(op, dst, srcs, k, n, s);
-    case GLX_FLOAT16: return launch_n_op<f16_t>(op, dst, srcs, k, n, s);
-    case GLX_BFLOAT16: return launch_n_op<bf16_t>(op, dst, srcs, k, n, s);
+    case GLX_INT8: return launch_n_op<int8_t>(op, dst, srcs, k, n, s, rev);
+    case GLX_UINT8: return launch_n_op<uint8_t>(op, dst, srcs, k, n, s, rev);
+    case GLX_INT32: return launch_n_op<int32_t>(op, dst, srcs, k, n, s, rev);
+    case GLX_INT64: return launch_n_op<int64_t>(op, dst, srcs, k, n, s, rev);
+    case GLX_UINT64: return launch_n_op<uint64_t>(op, dst, srcs, k, n, s, rev);
+    case GLX_FLOAT32: return launch_n_op<float>(op, dst, srcs, k, n, s, rev);
+    case GLX_FLOAT64: return launch_n_op<double>(op, dst, srcs, k, n, s, rev);
+    case GLX_FLOAT16: return launch_n_op<f16_t>(op, dst, srcs, k, n, s, rev);
+    case GLX_BFLOAT16: return launch_n_op<bf16_t>(op, dst, srcs, k, n, s, rev);
   }
   return hipErrorInvalidValue;
 }

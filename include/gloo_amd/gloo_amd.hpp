@@ -224,15 +224,33 @@ class DeviceAllreduce : public Algorithm {
 };
 }  // namespace detail
 
+// Data movement of HipAllreduceRingChunked (results are bit-identical):
+// RING = the reference's ring (one link per direction); MESH = each rank
+// folds its chunk pair from every peer directly (all links at once).
+enum class Schedule { RING, MESH };
+
+namespace detail {
+inline glx_algorithm* createRing(glx_context* c, void* const* p, int n, int count, int dt,
+                                 int op, const glx_stream_t* s, int ns) {
+  return glx_allreduce_create(c, GLX_ALGO_RING_CHUNKED, p, n, count, dt, op, s, ns);
+}
+inline glx_algorithm* createMesh(glx_context* c, void* const* p, int n, int count, int dt,
+                                 int op, const glx_stream_t* s, int ns) {
+  return glx_allreduce_create(c, GLX_ALGO_RING_CHUNKED_MESH, p, n, count, dt, op, s, ns);
+}
+}  // namespace detail
+
 // gloo::CudaAllreduceRingChunked<T> analog (gloo/cuda_allreduce_ring_chunked.h:22-26).
 template <typename T>
 class HipAllreduceRingChunked : public detail::DeviceAllreduce<T> {
  public:
   HipAllreduceRingChunked(const std::shared_ptr<Context>& ctx, const std::vector<T*>& ptrs,
                           int count, const std::vector<glx_stream_t>& streams = {},
-                          const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
-      : detail::DeviceAllreduce<T>(&glx_allreduce_ring_chunked_create, ctx, ptrs, count,
-                                   streams, fn) {}
+                          const ReductionFunction<T>* fn = ReductionFunction<T>::sum,
+                          Schedule schedule = Schedule::RING)
+      : detail::DeviceAllreduce<T>(
+            schedule == Schedule::MESH ? &detail::createMesh : &detail::createRing, ctx, ptrs,
+            count, streams, fn) {}
 };
 
 // gloo::CudaAllreduceHalvingDoubling<T> analog (gloo/cuda_allreduce_halving_doubling.h:25-30).

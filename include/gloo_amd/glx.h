@@ -177,6 +177,21 @@ glx_algorithm* glx_allreduce_ring_chunked_create(glx_context* ctx,
 glx_algorithm* glx_allreduce_halving_doubling_create(
     glx_context* ctx, void* const* ptrs, int nptrs, int count, int dtype, int op,
     const glx_stream_t* streams, int nstreams);
+/* Schedules.  GLX_ALGO_RING_CHUNKED_MESH computes exactly what
+ * AllreduceRingChunked computes -- same chunking, same per-chunk reduction
+ * chain and operand order, bit-identical results -- but moves the data over
+ * every peer link at once: each rank receives its chunk pair's operands from
+ * all peers (one xGMI link each), evaluates the ring's chain in one fold
+ * kernel, and sends the result to every peer. */
+enum glx_algo {
+  GLX_ALGO_RING_CHUNKED = 0,
+  GLX_ALGO_HALVING_DOUBLING = 1,
+  GLX_ALGO_RING_CHUNKED_MESH = 2
+};
+glx_algorithm* glx_allreduce_create(glx_context* ctx, int algo, void* const* ptrs,
+                                    int nptrs, int count, int dtype, int op,
+                                    const glx_stream_t* streams, int nstreams);
+
 /* Algorithm::run() (gloo/algorithm.h:26). */
 int glx_algorithm_run(glx_algorithm* alg);
 /* Number of bytes moved over the peer links by this rank in one run(). */
@@ -186,11 +201,15 @@ void glx_algorithm_destroy(glx_algorithm* alg);
 /* ---- schedule introspection (host logic; no GPU needed) ----------------- */
 /* The per-rank step program an algorithm executes.  Each step is 8 int64:
  * {kind, peer, channel, off, len, boff, dst_off, flags}; kinds: 0 SEND,
- * 1 RECV, 2 REDUCE, 3 COPY, 4 RELEASE.  algo: 0 ring_chunked,
- * 1 halving_doubling.  Returns the number of steps (writes at most cap) or
- * -1.  *scratch_elems receives the per-rank receive-buffer size. */
+ * 1 RECV, 2 REDUCE, 3 COPY, 4 RELEASE, 5 FOLD.  algo: glx_algo.  Returns the
+ * number of steps (writes at most cap) or -1.  *scratch_elems receives the
+ * per-rank receive-buffer size. */
 int64_t glx_plan(int algo, int rank, int size, int64_t count, int64_t* steps,
                  int64_t cap, int64_t* scratch_elems);
+/* Sources of FOLD step number `fold` (its boff field): region offsets, -1 =
+ * the rank's own buffer.  Returns the count (writes at most cap) or -1. */
+int64_t glx_plan_fold(int algo, int rank, int size, int64_t count, int64_t fold,
+                      int64_t* srcs, int64_t cap);
 
 #ifdef __cplusplus
 }  /* extern "C" */

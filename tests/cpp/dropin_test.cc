@@ -62,6 +62,16 @@ void spawn(int P, const std::function<void(std::shared_ptr<gloo_amd::Context>)>&
   for (int r = 0; r < P; r++) EXPECT(errs[r].empty(), "rank %d threw: %s", r, errs[r].c_str());
 }
 
+template <typename T>
+class MeshRingChunked : public gloo_amd::HipAllreduceRingChunked<T> {
+ public:
+  MeshRingChunked(const std::shared_ptr<gloo_amd::Context>& ctx, const std::vector<T*>& ptrs,
+                  int count)
+      : gloo_amd::HipAllreduceRingChunked<T>(ctx, ptrs, count, {},
+                                             gloo_amd::ReductionFunction<T>::sum,
+                                             gloo_amd::Schedule::MESH) {}
+};
+
 template <template <typename> class Alg>
 void singlePointer(const char* name, int P, int N) {
   spawn(P, [&](std::shared_ptr<gloo_amd::Context> ctx) {
@@ -182,8 +192,14 @@ int main() {
       singlePointer<gloo_amd::HipAllreduceHalvingDoubling>("halving_doubling", P, N);
     }
   }
+  for (int P = 1; P <= 8; P++) {
+    for (int N : {0, 4, 100, 1000, 10000}) {
+      singlePointer<MeshRingChunked>("ring_chunked/mesh", P, N);
+    }
+  }
   for (int P : {2, 3, 4}) {
     for (int nptrs : {1, 2}) {
+      stridePattern<MeshRingChunked>("ring_chunked/mesh", P, nptrs, 1000);
       stridePattern<gloo_amd::HipAllreduceRingChunked>("ring_chunked", P, nptrs, 1000);
       stridePattern<gloo_amd::HipAllreduceHalvingDoubling>("halving_doubling", P, nptrs, 1000);
     }

@@ -68,7 +68,7 @@ def same_bits(a, b):
 def replay_plans(plans, op, dtype, inputs):
     P = len(plans)
     data = [np.array(inputs[r], copy=True) for r in range(P)]
-    scratch = [np.zeros(max(sc, 1), dtype=data[0].dtype) for (_, sc) in plans]
+    scratch = [np.zeros(max(pl[1], 1), dtype=data[0].dtype) for pl in plans]
     pc = [0] * P
     sent = {}       # (src, dst, tag) -> messages sent
     delivered = {}  # (src, dst, tag) -> messages landed
@@ -101,6 +101,13 @@ def replay_plans(plans, op, dtype, inputs):
                                                      scratch[r][boff:boff + ln])
                 elif kind == 3:  # COPY
                     data[r][off:off + ln] = scratch[r][boff:boff + ln]
+                elif kind == 5:  # FOLD: acc = s0; acc = op(s_k, acc)
+                    srcs = plans[r][2][boff]
+                    assert srcs[0] == -1
+                    acc = np.array(data[r][off:off + ln], copy=True)
+                    for reg in srcs[1:]:
+                        acc = O.reduce(op, dtype, scratch[r][reg:reg + ln], acc)
+                    data[r][off:off + ln] = acc
                 elif kind == 4:  # RELEASE
                     key = (peer, r, tag)
                     consumed[key] = consumed.get(key, 0) + 1

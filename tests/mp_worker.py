@@ -21,7 +21,7 @@ def main():
     from oracle import oracle as O
 
     N = 100003
-    code = O.RING_CHUNKED if algo == "ring_chunked" else O.HALVING_DOUBLING
+    code = O.HALVING_DOUBLING if algo == "halving_doubling" else O.RING_CHUNKED
     ins = case_inputs(size, N, O.FLOAT32, 1, 0, seed=31)
     buf = torch.from_numpy(ins[rank][0].copy()).cuda()
     torch.cuda.synchronize()
@@ -29,9 +29,11 @@ def main():
     ctx = gloo_amd.rendezvous.Context(rank, size, 0)
     ctx.setTimeout(60)
     ctx.connectFullMesh(store)
-    cls = gloo_amd.AllreduceRingChunked if code == O.RING_CHUNKED else \
-        gloo_amd.AllreduceHalvingDoubling
-    alg = cls(ctx, [buf])
+    if algo == "halving_doubling":
+        alg = gloo_amd.AllreduceHalvingDoubling(ctx, [buf])
+    else:
+        alg = gloo_amd.AllreduceRingChunked(
+            ctx, [buf], schedule="mesh" if algo == "ring_chunked_mesh" else "ring")
     for _ in range(2):
         buf.copy_(torch.from_numpy(ins[rank][0].copy()).cuda())
         torch.cuda.synchronize()

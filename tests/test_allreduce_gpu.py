@@ -25,6 +25,9 @@ from test_reduce_gpu import TORCH_VIEW, assert_same, from_dev, to_dev  # noqa: E
 ALGOS = {O.RING_CHUNKED: "AllreduceRingChunked", O.HALVING_DOUBLING: "AllreduceHalvingDoubling"}
 
 
+MESH = 2  # ring_chunked semantics, mesh schedule
+
+
 def gpu_allreduce(algo, op, dtype, inputs, runs=1, streams=False, timeout_s=60,
                   refill_between_runs=True):
     """Run one algorithm instance per rank thread; returns results per rank/ptr."""
@@ -36,7 +39,11 @@ def gpu_allreduce(algo, op, dtype, inputs, runs=1, streams=False, timeout_s=60,
     torch.cuda.synchronize()
     fn = {O.SUM: gloo_amd.ReductionFunction.sum, O.PRODUCT: gloo_amd.ReductionFunction.product,
           O.MAX: gloo_amd.ReductionFunction.max, O.MIN: gloo_amd.ReductionFunction.min}[op]
-    cls = getattr(gloo_amd, ALGOS[algo])
+    if algo == MESH:
+        def cls(*a, **kw):
+            return gloo_amd.AllreduceRingChunked(*a, schedule="mesh", **kw)
+    else:
+        cls = getattr(gloo_amd, ALGOS[algo])
 
     def rank_fn(r):
         ctx = gloo_amd.rendezvous.Context(r, P, 0)
@@ -184,10 +191,41 @@ def test_timeout_raises_io_exception():
     assert time.time() - t0 < 5
 
 
+@pytest.mark.parametrize("P", [2, 3, 4, 8])
+@pytest.mark.parametrize("N", [1, 255, 1000, 4099, 100003])
+def test_mesh_schedule_matches_ring_chunked_oracle(P, N):
+    ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=8)
+    out = gpu_allreduce(MESH, O.SUM, O.FLOAT32, ins, runs=2)
+    check_all(out, O.allreduce(O.RING_CHUNKED, O.SUM, O.FLOAT32, ins), O.FLOAT32, O.SUM)
+
+
+@pytest.mark.parametrize("dtype,op", [(O.FLOAT32, O.MAX), (O.FLOAT16, O.SUM),
+                                      (O.BFLOAT16, O.SUM), (O.INT32, O.PRODUCT),
+                                      (O.FLOAT64, O.MIN)],
+                         ids=lambda x: str(x))
+def test_mesh_schedule_dtypes(dtype, op):
+    P, N = 5, 30011
+    ins = case_inputs(P, N, dtype, 2, 0, seed=12)
+    out = gpu_allreduce(MESH, op, dtype, ins, streams=True)
+    check_all(out, O.allreduce(O.RING_CHUNKED, op, dtype, ins), dtype, op)
+
+
+RING_GOLDEN = [r for r in INDEX if r["algo"] == O.RING_CHUNKED]
+
+
+@pytest.mark.parametrize("rec", RING_GOLDEN, ids=[r["name"] for r in RING_GOLDEN])
+def test_mesh_schedule_vs_reference_ring_golden(rec):
+    ins = case_inputs(rec["P"], rec["N"], rec["dtype"], rec["nptrs"], rec["kind"], rec["seed"])
+    out = gpu_allreduce(MESH, rec["op"], rec["dtype"], ins)
+    for r in range(rec["P"]):
+        for i in range(rec["nptrs"]):
+            check_against_golden(rec, DATA, out[r][i])
+
+
 WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "mp_worker.py")
 
 
-@pytest.mark.parametrize("algo", ["ring_chunked", "halving_doubling"])
+@pytest.mark.parametrize("algo", ["ring_chunked", "halving_doubling", "ring_chunked_mesh"])
 def test_multiprocess_ipc(algo):
     """One process per rank (the torchrun topology): endpoints via a FileStore,
     receive regions shared with hipIpcGetMemHandle/hipIpcOpenMemHandle."""

@@ -25,6 +25,40 @@ def test_plan_replay_matches_oracle(algo, P, N, op):
         assert same_bits(got[r], exp[r][0]), "rank %d" % r
 
 
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 5, 7, 8, 9, 16, 17])
+@pytest.mark.parametrize("N", [0, 1, 255, 256, 1000, 4099, 65537])
+@pytest.mark.parametrize("dtype,op", [(O.FLOAT32, O.SUM), (O.FLOAT32, O.MAX),
+                                      (O.FLOAT32, O.MIN), (O.FLOAT16, O.SUM),
+                                      (O.FLOAT16, O.PRODUCT), (O.INT32, O.PRODUCT)])
+def test_mesh_schedule_is_bit_identical_to_ring_chunked(P, N, dtype, op):
+    """The mesh schedule folds each chunk pair's chain in one pass with the
+    ring's operand order, so it must reproduce AllreduceRingChunked exactly
+    (fp32 sum rounding, max/min NaN/signed-zero choices, the fp16 quirk)."""
+    ins = case_inputs(P, N, dtype, 1, 0, seed=123)
+    if dtype == O.FLOAT32 and N > 10:
+        for r in range(P):  # signed zeros and NaNs exercise max/min operand order
+            ins[r][0][3] = -0.0 if r % 2 else 0.0
+            ins[r][0][7] = np.nan if r == 1 else ins[r][0][7]
+    plans = [gloo_amd.plan("ring_chunked_mesh", r, P, N, with_folds=True) for r in range(P)]
+    got = replay_plans(plans, op, dtype, [ins[r][0] for r in range(P)])
+    exp = O.allreduce(O.RING_CHUNKED, op, dtype, ins)
+    for r in range(P):
+        assert same_bits(got[r], exp[r][0]), "rank %d" % r
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_mesh_plan_traffic(P):
+    """Per peer link: 2*S/P bytes (vs the ring's 2(P-1)/P * S over one link)."""
+    N = 2 * P * 1024
+    steps, _ = gloo_amd.plan("ring_chunked_mesh", 0, P, N)
+    sends = [s for s in steps if s[0] == 0]
+    per_peer = {}
+    for s in sends:
+        per_peer[s[1]] = per_peer.get(s[1], 0) + s[4]
+    assert len(per_peer) == P - 1
+    assert all(v == 2 * N // P for v in per_peer.values())
+
+
 @pytest.mark.parametrize("P", [2, 4, 8])
 def test_ring_plan_traffic(P):
     """4P-4 chunk sends per rank, 1.75*S link bytes at P=8."""
