@@ -37,11 +37,18 @@ def parse():
     p.add_argument("--size-mib", type=int, default=256)
     p.add_argument("--algo", default="ring_chunked",
                    choices=["ring_chunked", "halving_doubling", "ring_chunked_mesh"])
+    p.add_argument("--copy-split", default="auto",
+                   help="N>1: streams per peer copy (1, 2, 4) or 'auto' (short calibration)")
     p.add_argument("--no-alt", action="store_true",
                    help="N>1: do not also time the other schedules")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bounded CPU baseline sample (seconds of CPU work)")
+    p.add_argument("--dtype", default="f32", choices=["f32", "f16", "bf16"],
+                   help="element type (configs[4]: f16/bf16 at --size-mib 1024)")
+    p.add_argument("--staged", action="store_true", default=True,
+                   help="also time the host-staged (H2D + op + D2H) rate")
+    p.add_argument("--no-staged", dest="staged", action="store_false")
     p.add_argument("--kernel-only", action="store_true",
                    help="N=1: run only the timed kernel loop (for rocprofv3 --pmc)")
     return p.parse_args()
@@ -60,25 +67,33 @@ def load_traffic(workload):
         return None
 
 
-def cpu_baseline(nbytes, seconds):
-    """gloo::sum<float> on the host cores (single thread, like the reference):
+def cpu_baseline(nbytes, seconds, dtype="f32"):
+    """gloo::sum<T> on the host cores (single thread, like the reference):
     the reference itself (oracle/_ref, compiled from the reference sources in
     the build container) when present, else the oracle's restatement."""
     import numpy as np
     from oracle import oracle as O
-    n = nbytes // 4
-    a = O.fill(O.FLOAT32, n, 0, seed=1234, rank=0)
-    b = O.fill(O.FLOAT32, n, 0, seed=1234, rank=1)
+    code = {"f32": O.FLOAT32, "f16": O.FLOAT16, "bf16": O.BFLOAT16}[dtype]
+    es = 4 if dtype == "f32" else 2
+    n = nbytes // es
+    a = O.fill(code, n, 0, seed=1234, rank=0)
+    b = O.fill(code, n, 0, seed=1234, rank=1)
     c = np.empty_like(a)
-    kind = "reference" if O.ref_available() else "port"
+    # bf16 has no reference type: the oracle restatement is the only CPU path
+    kind = "reference" if (O.ref_available() and dtype != "bf16") else "port"
     if kind == "reference":
         lib = O._load_ref()
 
         def step():
-            lib.ref_reduce(O.SUM, O.FLOAT32, O._ptr(c), O._ptr(a), O._ptr(b), n)
-    else:
+            lib.ref_reduce(O.SUM, code, O._ptr(c), O._ptr(a), O._ptr(b), n)
+    elif dtype == "f32":
         def step():
             O.sum_f32(c, a, b)
+    else:
+        lib = O._load_oracle()
+
+        def step():
+            lib.oracle_reduce(O.SUM, code, O._ptr(c), O._ptr(a), O._ptr(b), n)
     step()  # page in
     reps, t0 = 0, time.perf_counter()
     while True:
@@ -88,24 +103,72 @@ def cpu_baseline(nbytes, seconds):
         if el >= seconds or reps >= 2000:
             break
     t = el / reps
+    src = ("oracle/_ref: the reference's gloo/math.h" if kind == "reference"
+           else "oracle port of gloo/math.h")
     return {"value": round(nbytes / t / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": kind,
-            "sample": "gloo::sum<float> c=a+b over %d MiB, %d reps in %.1f s, 1 thread "
-                      "(%s)" % (nbytes >> 20, reps, el,
-                                "oracle/_ref: reference gloo/math.h" if kind == "reference"
-                                else "oracle port of gloo/math.h"),
+            "sample": "gloo::sum<%s> c=a+b over %d MiB, %d reps in %.1f s, 1 thread (%s)"
+                      % (DTYPES[dtype][0], nbytes >> 20, reps, el, src),
             "ms_per_step": round(t * 1e3, 3), "nproc": os.cpu_count()}
+
+
+DTYPES = {"f32": ("float32", 4), "f16": ("float16", 2), "bf16": ("bfloat16", 2)}
+
+
+def synthetic(torch, n, dtype, dev, seed):
+    """Uniform [-1, 1) fp32 values (rounded to the element type), on device."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    x = torch.rand(n, device=dev, generator=g) * 2 - 1
+    return x.to(getattr(torch, DTYPES[dtype][0]))
+
+
+def expected_sum(torch, a, b):
+    """Independent torch restatement of c = a + b with the reference's
+    semantics: IEEE add in fp32 rounded once to the element type; for float16
+    also the reference's assignment quirk (gloo/types.h:129-147: the store is
+    skipped when the new bits equal half((float)old_bits)) with old = a."""
+    if a.dtype == torch.float32:
+        return a + b
+    c = (a.float() + b.float()).to(a.dtype)
+    if a.dtype == torch.float16:
+        old = a.view(torch.int16).to(torch.int32) & 0xFFFF
+        q = old.float().to(torch.float16).view(torch.int16)
+        c = torch.where(c.view(torch.int16) == q, a, c)
+    return c
+
+
+def staged_rate(torch, fn, nbytes, host_bufs, dev_bufs, out_dev, out_host, reps):
+    """Host-resident inputs -> pinned H2D -> fn() on the device -> D2H, end to
+    end (the path starts and ends in host memory, SURVEY 8f #1)."""
+    s = torch.cuda.current_stream()
+    for _ in range(2):
+        for h, d in zip(host_bufs, dev_bufs):
+            d.copy_(h, non_blocking=True)
+        fn()
+        out_host.copy_(out_dev, non_blocking=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        for h, d in zip(host_bufs, dev_bufs):
+            d.copy_(h, non_blocking=True)
+        fn()
+        out_host.copy_(out_dev, non_blocking=True)
+    s.synchronize()
+    t = (time.perf_counter() - t0) / reps
+    return {"GBps": round(nbytes / t / 1e9, 3), "ms_per_step": round(t * 1e3, 4),
+            "h2d_bytes": nbytes * len(host_bufs), "d2h_bytes": nbytes,
+            "note": "pinned host buffers; H2D + compute + D2H per step"}
 
 
 def bench_single(args):
     import torch
     import gloo_amd
     S = args.size_mib << 20
-    n = S // 4
+    es = DTYPES[args.dtype][1]
+    n = S // es
     steps = args.steps or 100
     dev = torch.device("cuda:0")
-    g = torch.Generator(device=dev).manual_seed(1234)
-    a = torch.rand(n, device=dev, generator=g) * 2 - 1
-    b = torch.rand(n, device=dev, generator=g) * 2 - 1
+    a = synthetic(torch, n, args.dtype, dev, 1234)
+    b = synthetic(torch, n, args.dtype, dev, 4321)
     c = torch.empty_like(a)
     stream = torch.cuda.current_stream(dev)
     for _ in range(args.warmup):
@@ -120,28 +183,37 @@ def bench_single(args):
     ms = ev0.elapsed_time(ev1) / steps
     if args.kernel_only:
         return None
-    ok = bool(torch.equal(c, a + b))
+    ok = bool(torch.equal(c.view(torch.int16) if es == 2 else c,
+                          expected_sum(torch, a, b).view(torch.int16) if es == 2
+                          else expected_sum(torch, a, b)))
     t = ms / 1e3
     alg_bytes = 3 * S  # two reads + one write per launch
     achieved = alg_bytes / t / 1e9
-    workload = "local_reduce_sum_fp32_256MiB"
+    workload = "local_reduce_sum_%s_%dMiB" % ({"f32": "fp32"}.get(args.dtype, args.dtype),
+                                               args.size_mib)
     traffic = load_traffic(workload)
     res = {
         "metric": "allreduce GB/s (device-resident, fp32) at 1/2/4/8 MI355X; % HBM|xGMI roofline",
         "value": round(S / t / 1e9, 3), "unit": "GB/s", "n_gpus": 1, "steps": steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
         "config": {"workload": workload, "bytes_per_rank": S, "elements": n,
-                   "op": "sum", "kernel": "glx reduce_kernel<float,SUM> (HIP, gfx950)",
-                   "baseline_config": "configs[1]"},
+                   "op": "sum", "kernel": "glx reduce_kernel<%s,SUM> (HIP, gfx950)"
+                   % DTYPES[args.dtype][0], "baseline_config": "configs[1]"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": traffic,
                      "algorithmic_bytes_per_launch": alg_bytes},
         "verified": ok,
     }
+    if args.staged:
+        ah, bh = a.cpu().pin_memory(), b.cpu().pin_memory()
+        ch = torch.empty_like(ah).pin_memory()
+        res["host_staged"] = staged_rate(
+            torch, lambda: gloo_amd.math.sum(c, a, b), S, [ah, bh], [a, b], c, ch,
+            reps=min(steps, 10))
     if not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(S, args.cpu_seconds)
+        res["cpu_baseline"] = cpu_baseline(S, args.cpu_seconds, args.dtype)
     return res
 
 
@@ -211,10 +283,10 @@ def bench_multi(args):
     dev = torch.device("cuda", local)
     dist.init_process_group("gloo")  # host-side coordination only
     S = args.size_mib << 20
-    n = S // 4
+    es = DTYPES[args.dtype][1]
+    n = S // es
     steps = args.steps or 20
-    g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    src = torch.rand(n, device=dev, generator=g) * 2 - 1
+    src = synthetic(torch, n, args.dtype, dev, 1234 + rank)
     buf = src.clone()
     torch.cuda.synchronize()
     store = gloo_amd.rendezvous.PrefixStore(
@@ -222,6 +294,19 @@ def bench_multi(args):
     ctx = gloo_amd.rendezvous.Context(rank, world, local)
     ctx.setTimeout(120)
     ctx.connectFullMesh(store)
+    # copy split: a short calibration of 1/2/4 streams per peer copy (every
+    # rank sees the same max-over-ranks times, so all pick the same value)
+    calib = {}
+    if args.copy_split == "auto":
+        for k in (1, 2, 4):
+            gloo_amd.set_copy_split(k)
+            calib[k], _ = time_schedule(torch, dist, gloo_amd, ctx, buf, args.algo, 3, 1)
+        split = min(calib, key=lambda k: calib[k])
+    else:
+        split = int(args.copy_split)
+    gloo_amd.set_copy_split(split)
+    buf.copy_(src)
+    torch.cuda.synchronize()
     t, link_bytes = time_schedule(torch, dist, gloo_amd, ctx, buf, args.algo, steps,
                                   args.warmup)
     # correctness after the timing: one more run on fresh inputs; every rank
@@ -232,8 +317,8 @@ def bench_multi(args):
     alg.run()
     torch.cuda.synchronize()
     alg.close()
-    cs = torch.tensor([int(buf.view(torch.int32).to(torch.int64).sum().item())],
-                      dtype=torch.int64)
+    cs = torch.tensor([int(buf.view(torch.int16 if es == 2 else torch.int32)
+                           .to(torch.int64).sum().item())], dtype=torch.int64)
     allcs = [torch.zeros_like(cs) for _ in range(world)]
     dist.all_gather(allcs, cs)
     verified = all(int(x.item()) == int(cs.item()) for x in allcs)
@@ -250,9 +335,19 @@ def bench_multi(args):
                            "ms_per_step": round(ta * 1e3, 4),
                            "algbw_GBps": round(S / ta / 1e9, 3),
                            "link_bytes_per_step": sent_a}
+    staged = None
+    if args.staged:
+        host_src = src.cpu().pin_memory()
+        host_out = torch.empty_like(host_src).pin_memory()
+        alg = make_alg(gloo_amd, ctx, buf, args.algo)
+        dist.barrier()
+        staged = staged_rate(torch, alg.run, S, [host_src], [buf], buf, host_out,
+                             reps=min(steps, 5))
+        alg.close()
+        dist.barrier()
     res = None
     if rank == 0:
-        chunk = max(256 * 4, -(-S // (2 * world)))
+        chunk = max(256 * es, -(-S // (2 * world)))
         algbw = S / t / 1e9
         busbw = algbw * 2 * (world - 1) / world
         link_ach = link_bytes / t / 1e9
@@ -261,10 +356,14 @@ def bench_multi(args):
             "value": round(world * S / t / 1e9, 3), "unit": "GB/s", "n_gpus": world,
             "steps": steps, "warmup": args.warmup, "ms_per_step": round(t * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f32", "data": "synthetic",
-            "config": {"workload": "allreduce_%s_fp32_256MiB_per_rank" % args.algo,
+            "dtype": args.dtype, "data": "synthetic",
+            "config": {"workload": "allreduce_%s_%s_%dMiB_per_rank" % (
+                           args.algo, {"f32": "fp32"}.get(args.dtype, args.dtype), args.size_mib),
                        "algorithm": args.algo, "bytes_per_rank": S, "elements": n,
                        "parallelism": "dp%d" % world, "transport": "hipMemcpyPeerAsync/xGMI",
+                       "copy_split": split,
+                       "copy_split_calibration_ms": {str(k): round(v * 1e3, 3)
+                                                     for k, v in calib.items()},
                        "baseline_config": "configs[3]" if args.algo == "halving_doubling"
                        else "configs[2]"},
             "algbw_GBps": round(algbw, 3), "busbw_GBps": round(busbw, 3),
@@ -278,6 +377,8 @@ def bench_multi(args):
             "alt_schedules": alts,
             "verified": verified,
         }
+        if staged is not None:
+            res["host_staged"] = staged
     dist.barrier()
     dist.destroy_process_group()
     return res

@@ -19,10 +19,17 @@ from .algorithms import (  # noqa: F401
     ReductionType,
     plan,
 )
+from . import errors  # noqa: F401
 from .errors import EnforceNotMet, Exception, HipError, IoException  # noqa: F401,A004
 
 __version__ = _lib.lib.glx_version().decode()
 LIB_PATH = _lib.LIB_PATH
+
+
+def set_copy_split(k):
+    """Split each peer copy of algorithms created afterwards over k streams
+    (k DMA engines per destination link)."""
+    errors.check(_lib.lib.glx_set_copy_split(int(k)), "set_copy_split")
 
 
 def device_count():

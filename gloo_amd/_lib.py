@@ -38,6 +38,7 @@ SIGNATURES = [
     ("glx_peer_copy", _i, [_vp, _i, _vp, _i, _sz, _vp]),
     ("glx_enable_peer", _i, [_i, _i]),
     ("glx_tune_reduce", _i, [_i, _i, _i]),
+    ("glx_set_copy_split", _i, [_i]),
     ("glx_device_count", _i, [ctypes.POINTER(_i)]),
     ("glx_hash_store_create", _vp, []),
     ("glx_file_store_create", _vp, [ctypes.c_char_p]),

@@ -157,6 +157,12 @@ int glx_tune_reduce(int unroll, int blocks_per_cu, int nontemporal) {
   return GLX_OK;
 }
 
+int glx_set_copy_split(int k) {
+  if (k < 1 || k > 8) return fail(GLX_ERR_INVALID, "glx_set_copy_split: k must be in [1, 8]");
+  gloo::HipPlanExecutor::setCopySplit(k);
+  return GLX_OK;
+}
+
 int glx_device_count(int* count) {
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);

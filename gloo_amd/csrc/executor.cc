@@ -6,7 +6,9 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 
@@ -35,7 +37,24 @@ T getPod(const std::vector<char>& b, size_t& at) {
 
 enum { DIR_IN = 0, DIR_OUT = 1 };
 
+// A SEND is split only when every part is at least this big.
+constexpr size_t kMinSplitBytes = 1 << 20;
+
+int initialSplit() {
+  const char* e = std::getenv("GLOO_AMD_COPY_SPLIT");
+  int k = e ? std::atoi(e) : 1;
+  return k < 1 ? 1 : k;
+}
+
+std::atomic<int> g_copy_split{initialSplit()};
+
 }  // namespace
+
+void HipPlanExecutor::setCopySplit(int k) {
+  g_copy_split.store(std::max(1, std::min(k, (int)kMaxSplit)));
+}
+
+int HipPlanExecutor::copySplit() { return g_copy_split.load(); }
 
 HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
                                  const std::vector<void*>& ptrs, int64_t count,
@@ -67,6 +86,7 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
     ownCompute_ = true;
   }
   myPhase_ = (int)((uintptr_t)ptrs[0] % 16);
+  split_ = std::max(1, std::min(copySplit(), (int)kMaxSplit));
 
   if (plan_.scratch_elems > 0) {
     scratchBytes_ = (size_t)plan_.scratch_elems * esize_ + 64;
@@ -95,10 +115,12 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
           if (o.peer == oc.peer) oc.stream = o.stream;
         }
         if (oc.stream < 0) {
-          CopyStream cs;
-          GLX_HIP_CHECK(hipStreamCreateWithFlags(&cs.s, hipStreamNonBlocking));
-          copies_.push_back(cs);
-          oc.stream = (int)copies_.size() - 1;
+          oc.stream = (int)copies_.size();
+          for (int j = 0; j < split_; j++) {
+            CopyStream cs;
+            GLX_HIP_CHECK(hipStreamCreateWithFlags(&cs.s, hipStreamNonBlocking));
+            copies_.push_back(cs);
+          }
         }
         out_.push_back(oc);
         idx = (int)out_.size() - 1;
@@ -118,7 +140,7 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
       stepChan_[i] = idx;
     }
   }
-  events_.resize(plan_.steps.size(), nullptr);
+  events_.resize(plan_.steps.size() * (size_t)split_, nullptr);
   for (auto& e : events_) GLX_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   GLX_HIP_CHECK(hipEventCreateWithFlags(&computeMark_, hipEventDisableTiming));
   if (contextSize_ > 1 && count_ > 0) publish();
@@ -260,13 +282,12 @@ void HipPlanExecutor::pollPending() {
     for (size_t j = 0; j < i && !blocked; j++) blocked = pending_[j].word == p.word;
     bool done = false;
     if (!blocked) {
-      if (p.event == nullptr) {
-        done = true;
-      } else {
-        hipError_t e = hipEventQuery(p.event);
-        if (e == hipSuccess) {
-          done = true;
-        } else if (e != hipErrorNotReady) {
+      done = true;
+      for (int k = 0; k < p.nev && done; k++) {
+        hipError_t e = hipEventQuery(p.ev[k]);
+        if (e == hipErrorNotReady) {
+          done = false;
+        } else if (e != hipSuccess) {
           GLX_HIP_CHECK(e);
         }
       }
@@ -358,32 +379,50 @@ void HipPlanExecutor::run() {
           waitFor([&] { return oc.credit->load(std::memory_order_acquire) + 1 >= n; },
                   "receive-region credit", oc.peer);
           const size_t nbytes = (size_t)s.len * esize_;
+          Pending pd{};
+          pd.word = oc.delivery;
+          pd.value = n;
           if (nbytes > 0) {
-            CopyStream& cs = copies_[oc.stream];
             if (computeSinceMark) {
               GLX_HIP_CHECK(hipEventRecord(computeMark_, compute_));
               markEpoch_++;
               computeSinceMark = false;
             }
-            if (cs.waitedMark != markEpoch_) {
-              // the chunk may have been produced by compute work: order after it
-              GLX_HIP_CHECK(hipStreamWaitEvent(cs.s, computeMark_, 0));
-              cs.waitedMark = markEpoch_;
-            }
             char* dst = landing(oc.peerScratch, s.dst_off, s.off, oc.peerPhase);
             const char* src = ptr0 + (size_t)s.off * esize_;
-            if (oc.peerDevice >= 0 && oc.peerDevice != device_) {
-              GLX_HIP_CHECK(hipMemcpyPeerAsync(dst, oc.peerDevice, src, device_, nbytes, cs.s));
-            } else {
-              GLX_HIP_CHECK(hipMemcpyAsync(dst, src, nbytes, hipMemcpyDeviceToDevice, cs.s));
+            int parts = split_;
+            while (parts > 1 && nbytes / (size_t)parts < kMinSplitBytes) parts--;
+            const size_t per = ((nbytes / (size_t)parts) + 255) & ~(size_t)255;
+            for (int j = 0; j < parts; j++) {
+              const size_t at = (size_t)j * per;
+              if (at >= nbytes) break;
+              const size_t len = std::min(per, nbytes - at);
+              CopyStream& cs = copies_[oc.stream + j];
+              if (cs.waitedMark != markEpoch_) {
+                // the chunk may have been produced by compute work: order after it
+                GLX_HIP_CHECK(hipStreamWaitEvent(cs.s, computeMark_, 0));
+                cs.waitedMark = markEpoch_;
+              }
+              hipError_t ce = hipErrorUnknown;
+              if (peerCopyOk_ && oc.peerDevice >= 0 && oc.peerDevice != device_) {
+                ce = hipMemcpyPeerAsync(dst + at, oc.peerDevice, src + at, device_, len, cs.s);
+                if (ce != hipSuccess) {
+                  (void)hipGetLastError();
+                  peerCopyOk_ = false;  // e.g. an IPC mapping the peer API rejects
+                }
+              }
+              if (ce != hipSuccess) {
+                GLX_HIP_CHECK(hipMemcpyAsync(dst + at, src + at, len, hipMemcpyDeviceToDevice,
+                                             cs.s));
+              }
+              hipEvent_t ev = events_[i * (size_t)split_ + (size_t)j];
+              GLX_HIP_CHECK(hipEventRecord(ev, cs.s));
+              cs.last = ev;
+              inflight_.push_back({s.off, s.len, ev});
+              pd.ev[pd.nev++] = ev;
             }
-            GLX_HIP_CHECK(hipEventRecord(events_[i], cs.s));
-            cs.last = events_[i];
-            inflight_.push_back({s.off, s.len, events_[i]});
-            pending_.push_back({events_[i], oc.delivery, n});
-          } else {
-            pending_.push_back({nullptr, oc.delivery, n});
           }
+          pending_.push_back(pd);
           break;
         }
         case glx::RECV: {
@@ -427,8 +466,14 @@ void HipPlanExecutor::run() {
         case glx::RELEASE: {
           InChan& ic = in_[stepChan_[i]];
           const uint64_t v = ++ic.consumed;
-          GLX_HIP_CHECK(hipEventRecord(events_[i], compute_));
-          pending_.push_back({events_[i], ic.credit, v});
+          hipEvent_t ev = events_[i * (size_t)split_];
+          GLX_HIP_CHECK(hipEventRecord(ev, compute_));
+          Pending pd{};
+          pd.ev[0] = ev;
+          pd.nev = 1;
+          pd.word = ic.credit;
+          pd.value = v;
+          pending_.push_back(pd);
           break;
         }
         default:

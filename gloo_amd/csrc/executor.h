@@ -48,6 +48,11 @@ class HipPlanExecutor : public Algorithm {
   void run() override;
 
   int64_t bytesSentPerRun() const { return plan_.bytes_sent * (int64_t)esize_; }
+
+  // Copies of one SEND are split over this many streams per destination
+  // (several DMA engines feeding one link).  Read at construction.
+  static void setCopySplit(int k);
+  static int copySplit();
   const glx::Plan& plan() const { return plan_; }
 
  private:
@@ -74,8 +79,10 @@ class HipPlanExecutor : public Algorithm {
     std::atomic<uint64_t>* credit = nullptr;  // in peer's block
     uint64_t received = 0, consumed = 0;
   };
-  struct Pending {  // fire `value` into `word` once `event` (may be null) completes
-    hipEvent_t event;
+  static constexpr int kMaxSplit = 8;
+  struct Pending {  // fire `value` into `word` once all `ev` (maybe none) complete
+    hipEvent_t ev[kMaxSplit];
+    int nev;
     std::atomic<uint64_t>* word;
     uint64_t value;
   };
@@ -107,6 +114,8 @@ class HipPlanExecutor : public Algorithm {
   hipStream_t compute_ = nullptr;
   std::vector<CopyStream> copies_;
   uint64_t markEpoch_ = 0;
+  int split_ = 1;
+  bool peerCopyOk_ = true;  // hipMemcpyPeerAsync accepted for IPC-mapped peers
   bool ownCompute_ = false;
   char* scratch_ = nullptr;
   size_t scratchBytes_ = 0;
@@ -114,7 +123,7 @@ class HipPlanExecutor : public Algorithm {
   std::vector<OutChan> out_;
   std::vector<InChan> in_;
   std::vector<int> stepChan_;        // channel index per step
-  std::vector<hipEvent_t> events_;   // one per step
+  std::vector<hipEvent_t> events_;   // split_ per step
   hipEvent_t computeMark_ = nullptr;
   bool resolved_ = false;
   std::vector<Pending> pending_;

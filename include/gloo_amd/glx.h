@@ -104,6 +104,11 @@ int glx_enable_peer(int dev_a, int dev_b);
  * nontemporal streaming loads/stores (0 off, 1 on, -1 keep). */
 int glx_tune_reduce(int unroll, int blocks_per_cu, int nontemporal);
 
+/* Split every peer copy of algorithms created afterwards over k streams per
+ * destination (k DMA engines feeding one link; parts >= 1 MiB).  Default 1,
+ * or $GLOO_AMD_COPY_SPLIT. */
+int glx_set_copy_split(int k);
+
 /* Number of visible HIP devices (0 when no GPU). */
 int glx_device_count(int* count);
 

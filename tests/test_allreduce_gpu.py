@@ -247,3 +247,21 @@ def test_multiprocess_ipc(algo):
         for r, p in enumerate(procs):
             assert p.returncode == 0, "rank %d failed:\n%s" % (r, outs[r])
             assert "OK" in outs[r]
+
+
+@pytest.mark.parametrize("split", [2, 4])
+@pytest.mark.parametrize("algo", [O.RING_CHUNKED, O.HALVING_DOUBLING, MESH],
+                         ids=["ring_chunked", "halving_doubling", "mesh"])
+def test_split_peer_copies(algo, split):
+    """Each SEND split over several copy streams (parts >= 1 MiB) must give the
+    same bits; the split is read when the algorithm is created."""
+    import gloo_amd
+    P, N = 3, (6 << 20) // 4 + 77
+    ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=5)
+    gloo_amd.set_copy_split(split)
+    try:
+        out = gpu_allreduce(algo, O.SUM, O.FLOAT32, ins, runs=2)
+    finally:
+        gloo_amd.set_copy_split(1)
+    ref_algo = O.HALVING_DOUBLING if algo == O.HALVING_DOUBLING else O.RING_CHUNKED
+    check_all(out, O.allreduce(ref_algo, O.SUM, O.FLOAT32, ins), O.FLOAT32, O.SUM)
