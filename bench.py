@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--staged", action="store_true", default=True,
                    help="also time the host-staged (H2D + op + D2H) rate")
     p.add_argument("--no-staged", dest="staged", action="store_false")
+    p.add_argument("--watchdog", type=float, default=900.0,
+                   help="seconds before dumping stacks and exiting")
     p.add_argument("--kernel-only", action="store_true",
                    help="N=1: run only the timed kernel loop (for rocprofv3 --pmc)")
     return p.parse_args()
@@ -169,23 +171,32 @@ def bench_single(args):
     dev = torch.device("cuda:0")
     a = synthetic(torch, n, args.dtype, dev, 1234)
     b = synthetic(torch, n, args.dtype, dev, 4321)
-    c = torch.empty_like(a)
+    a0 = a.clone()
     stream = torch.cuda.current_stream(dev)
+    # in place, a = op(a, b): the form the allreduce runs (gloo::sum(T* a,
+    # const T* b, n), gloo/math.h:25-28); 2 reads + 1 write per element
     for _ in range(args.warmup):
-        gloo_amd.math.sum(c, a, b, stream=stream)
+        gloo_amd.math.sum(a, a, b, stream=stream)
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record(stream)  # the kernels are launched on this stream
     for _ in range(steps):
-        gloo_amd.math.sum(c, a, b, stream=stream)
+        gloo_amd.math.sum(a, a, b, stream=stream)
     ev1.record(stream)
     torch.cuda.synchronize()
     ms = ev0.elapsed_time(ev1) / steps
     if args.kernel_only:
         return None
-    ok = bool(torch.equal(c.view(torch.int16) if es == 2 else c,
-                          expected_sum(torch, a, b).view(torch.int16) if es == 2
-                          else expected_sum(torch, a, b)))
+    # correctness of one launch on the original inputs
+    a.copy_(a0)
+    gloo_amd.math.sum(a, a, b, stream=stream)
+    exp = expected_sum(torch, a0, b)
+    torch.cuda.synchronize()
+    if es == 2:
+        ok = bool(torch.equal(a.view(torch.int16), exp.view(torch.int16)))
+    else:
+        ok = bool(torch.equal(a, exp))
+    c = a
     t = ms / 1e3
     alg_bytes = 3 * S  # two reads + one write per launch
     achieved = alg_bytes / t / 1e9
@@ -207,10 +218,10 @@ def bench_single(args):
         "verified": ok,
     }
     if args.staged:
-        ah, bh = a.cpu().pin_memory(), b.cpu().pin_memory()
+        ah, bh = a0.cpu().pin_memory(), b.cpu().pin_memory()
         ch = torch.empty_like(ah).pin_memory()
         res["host_staged"] = staged_rate(
-            torch, lambda: gloo_amd.math.sum(c, a, b), S, [ah, bh], [a, b], c, ch,
+            torch, lambda: gloo_amd.math.sum(a, a, b), S, [ah, bh], [a, b], a, ch,
             reps=min(steps, 10))
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(S, args.cpu_seconds, args.dtype)
@@ -251,8 +262,10 @@ def time_schedule(torch, dist, gloo_amd, ctx, buf, algo, steps, warmup):
     """warmup untimed runs, then `steps` timed runs between barriers +
     device syncs; returns (max-over-ranks seconds per step, link bytes/run)."""
     alg = make_alg(gloo_amd, ctx, buf, algo)
+    log("%s: created, warmup %d" % (algo, warmup))
     for _ in range(warmup):
         alg.run()
+    log("%s: warm, timing %d steps" % (algo, steps))
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
@@ -266,6 +279,7 @@ def time_schedule(torch, dist, gloo_amd, ctx, buf, algo, steps, warmup):
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     sent = alg.bytes_sent()
     alg.close()
+    log("%s: %.3f ms/step" % (algo, el.item() / steps * 1e3))
     return el.item() / steps, sent
 
 
@@ -294,6 +308,7 @@ def bench_multi(args):
     ctx = gloo_amd.rendezvous.Context(rank, world, local)
     ctx.setTimeout(120)
     ctx.connectFullMesh(store)
+    log("connected (world %d, device %d)" % (world, local))
     # copy split: a short calibration of 1/2/4 streams per peer copy (every
     # rank sees the same max-over-ranks times, so all pick the same value)
     calib = {}
@@ -384,8 +399,18 @@ def bench_multi(args):
     return res
 
 
+def log(msg):
+    r = os.environ.get("RANK", "0")
+    sys.stderr.write("[bench r%s %.3f] %s\n" % (r, time.time(), msg))
+    sys.stderr.flush()
+
+
 def main():
     args = parse()
+    import faulthandler
+    # never hang the driver: dump every thread's stack and exit if a run
+    # exceeds the watchdog (the transport's own timeouts are 120 s)
+    faulthandler.dump_traceback_later(args.watchdog, exit=True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
         res = bench_multi(args)

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -307,11 +308,20 @@ void HipPlanExecutor::waitFor(Pred done, const char* what, int peer) {
   const auto timeout = context_->getTimeout();
   const auto start = std::chrono::steady_clock::now();
   auto lastAlive = start;
+  bool warned = false;
   for (uint64_t spin = 1;; spin++) {
     pollPending();
     if (done()) return;
     if ((spin & 255) == 0) {
       auto now = std::chrono::steady_clock::now();
+      if (!warned && now - start > std::chrono::seconds(10)) {
+        // a stuck collective should say where it is stuck long before the timeout
+        std::fprintf(stderr,
+                     "[gloo_amd] rank %d still waiting for %s from rank %d after 10 s "
+                     "(%zu completions pending)\n",
+                     contextRank_, what, peer, pending_.size());
+        warned = true;
+      }
       if (now - start > timeout) {
         GLX_THROW_TIMEOUT(
             "Timed out waiting for ", what, " from rank ", peer, " (rank ",
