@@ -258,6 +258,18 @@ def make_alg(gloo_amd, ctx, buf, algo):
                                         schedule="mesh" if algo == "ring_chunked_mesh" else "ring")
 
 
+def busiest_link_bytes(gloo_amd, algo, rank, world, count, es):
+    """Bytes this rank sends to its most-loaded destination per run (from the
+    compiled step program): the per-link load that bounds the step on a
+    point-to-point xGMI fabric."""
+    steps, _ = gloo_amd.plan(algo, rank, world, count)
+    per_peer = {}
+    for st in steps:
+        if st[0] == 0:
+            per_peer[st[1]] = per_peer.get(st[1], 0) + st[4] * es
+    return max(per_peer.values()) if per_peer else 0
+
+
 def time_schedule(torch, dist, gloo_amd, ctx, buf, algo, steps, warmup):
     """warmup untimed runs, then `steps` timed runs between barriers +
     device syncs; returns (max-over-ranks seconds per step, link bytes/run)."""
@@ -346,10 +358,12 @@ def bench_multi(args):
             torch.cuda.synchronize()
             ta, sent_a = time_schedule(torch, dist, gloo_amd, ctx, buf, other, steps,
                                        args.warmup)
+            lm = busiest_link_bytes(gloo_amd, other, rank, world, n, es)
             alts[other] = {"value": round(world * S / ta / 1e9, 3),
                            "ms_per_step": round(ta * 1e3, 4),
                            "algbw_GBps": round(S / ta / 1e9, 3),
-                           "link_bytes_per_step": sent_a}
+                           "bytes_sent_per_step": sent_a,
+                           "busiest_link_GBps": round(lm / ta / 1e9, 2)}
     staged = None
     if args.staged:
         host_src = src.cpu().pin_memory()
@@ -365,7 +379,8 @@ def bench_multi(args):
         chunk = max(256 * es, -(-S // (2 * world)))
         algbw = S / t / 1e9
         busbw = algbw * 2 * (world - 1) / world
-        link_ach = link_bytes / t / 1e9
+        link_max = busiest_link_bytes(gloo_amd, args.algo, rank, world, n, es)
+        link_ach = link_max / t / 1e9
         res = {
             "metric": "allreduce GB/s (device-resident, fp32) at 1/2/4/8 MI355X; % HBM|xGMI roofline",
             "value": round(world * S / t / 1e9, 3), "unit": "GB/s", "n_gpus": world,
@@ -386,9 +401,11 @@ def bench_multi(args):
             "link_roofline": {"bound": "xgmi_link", "achieved": round(link_ach, 2),
                               "peak": XGMI_LINK_GBPS, "unit": "GB/s",
                               "frac": round(link_ach / XGMI_LINK_GBPS, 4),
-                              "link_bytes_per_step": link_bytes,
-                              "note": "bytes this rank sent per step / step time; the "
-                                      "ring uses one link per direction"},
+                              "busiest_link_bytes_per_step": link_max,
+                              "bytes_sent_per_step": link_bytes,
+                              "note": "busiest outgoing link's bytes per step / step time "
+                                      "(ring: everything on rank->rank+1; mesh: 1/(P-1) "
+                                      "per peer link)"},
             "alt_schedules": alts,
             "verified": verified,
         }

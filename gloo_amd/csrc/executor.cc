@@ -49,6 +49,20 @@ int initialSplit() {
 
 std::atomic<int> g_copy_split{initialSplit()};
 
+// GLOO_AMD_TRACE=1: one stderr line per executor step / runtime call.
+const bool g_trace = [] {
+  const char* e = std::getenv("GLOO_AMD_TRACE");
+  return e != nullptr && e[0] == '1';
+}();
+
+#define GLX_TRACE(...)                        \
+  do {                                        \
+    if (g_trace) {                            \
+      std::fprintf(stderr, "[glx-trace] " __VA_ARGS__); \
+      std::fputc('\n', stderr);              \
+    }                                         \
+  } while (0)
+
 }  // namespace
 
 void HipPlanExecutor::setCopySplit(int k) {
@@ -89,12 +103,7 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
   myPhase_ = (int)((uintptr_t)ptrs[0] % 16);
   split_ = std::max(1, std::min(copySplit(), (int)kMaxSplit));
 
-  if (plan_.scratch_elems > 0) {
-    scratchBytes_ = (size_t)plan_.scratch_elems * esize_ + 64;
-    GLX_HIP_CHECK(hipMalloc((void**)&scratch_, scratchBytes_));
-    GLX_HIP_CHECK(hipMemset(scratch_, 0, scratchBytes_));
-    GLX_HIP_CHECK(hipDeviceSynchronize());
-  }
+  allocScratch();
 
   // Channels named by the plan; allocate our counter words.
   auto& ctl = ctx->localControl();
@@ -154,7 +163,7 @@ HipPlanExecutor::~HipPlanExecutor() noexcept(false) {
   for (void* p : ipcOpened_) hipIpcCloseMemHandle(p);
   for (auto& e : events_) hipEventDestroy(e);
   if (computeMark_) hipEventDestroy(computeMark_);
-  if (scratch_) hipFree(scratch_);
+  for (auto& b : blocks_) hipFree(b.ptr);
   for (auto& c : copies_) hipStreamDestroy(c.s);
   if (ownCompute_ && compute_) hipStreamDestroy(compute_);
   auto& ctl = context_->localControl();
@@ -181,14 +190,18 @@ void HipPlanExecutor::publish() {
   std::vector<char> b;
   putPod<uint32_t>(b, kAlgMagic);
   putPod<int64_t>(b, (int64_t)::getpid());
-  putPod<uint64_t>(b, (uint64_t)(uintptr_t)scratch_);
-  hipIpcMemHandle_t h;
-  memset(&h, 0, sizeof(h));
-  int32_t haveIpc = 0;
-  if (scratch_ != nullptr && hipIpcGetMemHandle(&h, scratch_) == hipSuccess) haveIpc = 1;
-  (void)hipGetLastError();
-  putPod<int32_t>(b, haveIpc);
-  putPod(b, h);
+  putPod<int32_t>(b, (int32_t)blocks_.size());
+  for (const auto& blk : blocks_) {
+    putPod<int64_t>(b, blk.start);
+    putPod<int64_t>(b, blk.elems);
+    putPod<uint64_t>(b, (uint64_t)(uintptr_t)blk.ptr);
+    hipIpcMemHandle_t h;
+    memset(&h, 0, sizeof(h));
+    int32_t haveIpc = hipIpcGetMemHandle(&h, blk.ptr) == hipSuccess ? 1 : 0;
+    (void)hipGetLastError();
+    putPod<int32_t>(b, haveIpc);
+    putPod(b, h);
+  }
   putPod<int32_t>(b, myPhase_);
   putPod<int32_t>(b, (int32_t)(in_.size() + out_.size()));
   for (auto& ic : in_) {
@@ -214,31 +227,43 @@ void HipPlanExecutor::resolvePeers() {
   for (auto& kv : peers) {
     const int r = kv.first;
     PeerEndpoint& pe = context_->peer(r);
+    GLX_TRACE("r%d resolve: get record of rank %d", contextRank_, r);
     auto b = context_->store().get(
         "glx/alg/" + std::to_string(slot_) + "/" + std::to_string(r),
         context_->getTimeout());
     size_t at = 0;
     GLX_ENFORCE(getPod<uint32_t>(b, at) == kAlgMagic, "bad algorithm record from rank ", r);
     getPod<int64_t>(b, at);  // pid (already known from the endpoint)
-    uint64_t scratch = getPod<uint64_t>(b, at);
-    int32_t haveIpc = getPod<int32_t>(b, at);
-    hipIpcMemHandle_t h = getPod<hipIpcMemHandle_t>(b, at);
-    int32_t phase = getPod<int32_t>(b, at);
-    int32_t n = getPod<int32_t>(b, at);
-    char* peerScratch = nullptr;
+    const int32_t nblocks = getPod<int32_t>(b, at);
     bool needScratch = false;
     for (auto& oc : out_) needScratch = needScratch || oc.peer == r;
-    if (needScratch && scratch != 0) {
+    std::vector<ScratchBlock> pb;
+    for (int32_t k = 0; k < nblocks; k++) {
+      ScratchBlock blk;
+      blk.start = getPod<int64_t>(b, at);
+      blk.elems = getPod<int64_t>(b, at);
+      const uint64_t ptr = getPod<uint64_t>(b, at);
+      const int32_t haveIpc = getPod<int32_t>(b, at);
+      const hipIpcMemHandle_t h = getPod<hipIpcMemHandle_t>(b, at);
+      if (!needScratch) continue;
       if (pe.sameProcess) {
-        peerScratch = reinterpret_cast<char*>((uintptr_t)scratch);
+        blk.ptr = reinterpret_cast<char*>((uintptr_t)ptr);
       } else {
-        GLX_ENFORCE(haveIpc, "rank ", r, " could not export its receive buffer (hipIpcGetMemHandle)");
+        GLX_ENFORCE(haveIpc, "rank ", r,
+                    " could not export its receive buffer (hipIpcGetMemHandle)");
         void* p = nullptr;
+        GLX_TRACE("r%d resolve: hipIpcOpenMemHandle(rank %d, block %d, %ld elems)",
+                  contextRank_, r, k, (long)blk.elems);
         GLX_HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+        GLX_TRACE("r%d resolve: opened %p", contextRank_, p);
         ipcOpened_.push_back(p);
-        peerScratch = static_cast<char*>(p);
+        blk.ptr = static_cast<char*>(p);
       }
+      pb.push_back(blk);
     }
+    if (needScratch) peerBlocks_[r] = pb;
+    int32_t phase = getPod<int32_t>(b, at);
+    int32_t n = getPod<int32_t>(b, at);
     for (int32_t i = 0; i < n; i++) {
       int32_t peer = getPod<int32_t>(b, at);
       int32_t tag = getPod<int32_t>(b, at);
@@ -249,7 +274,6 @@ void HipPlanExecutor::resolvePeers() {
         int idx = outIndex(r, tag);
         if (idx >= 0) {
           out_[idx].delivery = pe.ctl->word((uint32_t)word);
-          out_[idx].peerScratch = peerScratch;
           out_[idx].peerPhase = phase;
           out_[idx].peerDevice = pe.localDevice;
         }
@@ -270,10 +294,51 @@ void HipPlanExecutor::resolvePeers() {
   resolved_ = true;
 }
 
-char* HipPlanExecutor::landing(char* base, int64_t boff, int64_t off, int phase) const {
-  uintptr_t at = ((uintptr_t)boff * esize_ + 15) & ~(uintptr_t)15;
+char* HipPlanExecutor::landing(const std::vector<ScratchBlock>& blocks, int64_t boff,
+                               int64_t off, int phase) const {
+  const ScratchBlock* blk = nullptr;
+  for (const auto& b : blocks) {
+    if (b.start <= boff && boff < b.start + b.elems) {
+      blk = &b;
+      break;
+    }
+  }
+  GLX_ENFORCE(blk != nullptr && blk->ptr != nullptr, "no receive block holds region ", boff);
+  uintptr_t at = ((uintptr_t)(boff - blk->start) * esize_ + 15) & ~(uintptr_t)15;
   at += ((uintptr_t)phase + (uintptr_t)off * esize_) % 16;
-  return base + at;
+  return blk->ptr + at;
+}
+
+void HipPlanExecutor::allocScratch() {
+  if (plan_.scratch_elems <= 0) return;
+  // region starts = where messages land
+  std::vector<int64_t> starts;
+  for (const auto& s : plan_.steps) {
+    if (s.kind == glx::RECV) starts.push_back(s.boff);
+  }
+  starts.push_back(0);
+  std::sort(starts.begin(), starts.end());
+  starts.erase(std::unique(starts.begin(), starts.end()), starts.end());
+  starts.push_back(plan_.scratch_elems);  // sentinel
+  ScratchBlock cur;
+  cur.start = 0;
+  for (size_t i = 0; i + 1 < starts.size(); i++) {
+    const int64_t regionElems = starts[i + 1] - starts[i];
+    const size_t curBytes = (size_t)cur.elems * esize_;
+    if (cur.elems > 0 && curBytes + (size_t)regionElems * esize_ > kMaxBlockBytes) {
+      blocks_.push_back(cur);
+      cur = ScratchBlock();
+      cur.start = starts[i];
+    }
+    cur.elems += regionElems;
+  }
+  if (cur.elems > 0) blocks_.push_back(cur);
+  for (auto& b : blocks_) {
+    const size_t bytes = (size_t)b.elems * esize_ + 64;
+    GLX_HIP_CHECK(hipMalloc((void**)&b.ptr, bytes));
+    GLX_HIP_CHECK(hipMemset(b.ptr, 0, bytes));
+  }
+  GLX_HIP_CHECK(hipDeviceSynchronize());
 }
 
 void HipPlanExecutor::pollPending() {
@@ -380,6 +445,8 @@ void HipPlanExecutor::run() {
     const auto& steps = plan_.steps;
     for (size_t i = 0; i < steps.size(); i++) {
       const glx::Step& s = steps[i];
+      GLX_TRACE("r%d step %zu kind %d peer %d chan %d off %ld len %ld", contextRank_, i,
+                (int)s.kind, (int)s.peer, (int)s.channel, (long)s.off, (long)s.len);
       switch (s.kind) {
         case glx::SEND: {
           OutChan& oc = out_[stepChan_[i]];
@@ -398,7 +465,7 @@ void HipPlanExecutor::run() {
               markEpoch_++;
               computeSinceMark = false;
             }
-            char* dst = landing(oc.peerScratch, s.dst_off, s.off, oc.peerPhase);
+            char* dst = landing(peerBlocks_[oc.peer], s.dst_off, s.off, oc.peerPhase);
             const char* src = ptr0 + (size_t)s.off * esize_;
             int parts = split_;
             while (parts > 1 && nbytes / (size_t)parts < kMinSplitBytes) parts--;
@@ -425,6 +492,7 @@ void HipPlanExecutor::run() {
                 GLX_HIP_CHECK(hipMemcpyAsync(dst + at, src + at, len, hipMemcpyDeviceToDevice,
                                              cs.s));
               }
+              GLX_TRACE("r%d   copy part %d issued (%zu bytes)", contextRank_, j, len);
               hipEvent_t ev = events_[i * (size_t)split_ + (size_t)j];
               GLX_HIP_CHECK(hipEventRecord(ev, cs.s));
               cs.last = ev;
@@ -445,7 +513,7 @@ void HipPlanExecutor::run() {
         case glx::REDUCE: {
           waitWar(s.off, s.len);
           char* dst = ptr0 + (size_t)s.off * esize_;
-          const char* src = landing(scratch_, s.boff, s.off, myPhase_);
+          const char* src = landing(blocks_, s.boff, s.off, myPhase_);
           GLX_HIP_CHECK(glx::launch_reduce(op_, dtype_, dst, dst, src, (size_t)s.len, compute_));
           computeSinceMark = true;
           break;
@@ -457,7 +525,7 @@ void HipPlanExecutor::run() {
           std::vector<const void*> srcs;
           for (int64_t r : regions) {
             srcs.push_back(r < 0 ? (const void*)dst
-                                 : (const void*)landing(scratch_, r, s.off, myPhase_));
+                                 : (const void*)landing(blocks_, r, s.off, myPhase_));
           }
           GLX_HIP_CHECK(glx::launch_reduce_n(op_, dtype_, dst, srcs.data(), (int)srcs.size(),
                                              (size_t)s.len, compute_, /*rev=*/true));
@@ -467,7 +535,7 @@ void HipPlanExecutor::run() {
         case glx::COPY: {
           waitWar(s.off, s.len);
           char* dst = ptr0 + (size_t)s.off * esize_;
-          const char* src = landing(scratch_, s.boff, s.off, myPhase_);
+          const char* src = landing(blocks_, s.boff, s.off, myPhase_);
           GLX_HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)s.len * esize_,
                                        hipMemcpyDeviceToDevice, compute_));
           computeSinceMark = true;
@@ -491,7 +559,9 @@ void HipPlanExecutor::run() {
       }
       pollPending();
     }
+    GLX_TRACE("r%d drain (%zu pending)", contextRank_, pending_.size());
     drain();
+    GLX_TRACE("r%d drained", contextRank_);
     // the caller's stream must not run ahead of copies still reading ptr0
     for (auto& c : copies_) {
       if (c.last != nullptr) GLX_HIP_CHECK(hipStreamWaitEvent(compute_, c.last, 0));
@@ -502,7 +572,9 @@ void HipPlanExecutor::run() {
   for (size_t i = 1; i < ptrs_.size(); i++) {
     GLX_HIP_CHECK(hipMemcpyAsync(ptrs_[i], ptr0, bytes, hipMemcpyDeviceToDevice, compute_));
   }
+  GLX_TRACE("r%d sync", contextRank_);
   if (!userStream_) GLX_HIP_CHECK(hipStreamSynchronize(compute_));
+  GLX_TRACE("r%d done", contextRank_);
 }
 
 }  // namespace gloo

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstdint>
+#include <map>
 #include <memory>
 #include <vector>
 
@@ -62,7 +63,6 @@ class HipPlanExecutor : public Algorithm {
     std::atomic<uint64_t>* credit;  // = our word
     std::atomic<uint64_t>* delivery = nullptr;  // in peer's block
     uint64_t sent = 0;
-    char* peerScratch = nullptr;
     int peerPhase = 0;  // peer ptr0 address mod 16
     int peerDevice = -1;
     int stream = 0;     // index into copies_ (one copy stream per destination peer)
@@ -86,6 +86,15 @@ class HipPlanExecutor : public Algorithm {
     std::atomic<uint64_t>* word;
     uint64_t value;
   };
+  // Receive scratch is allocated in blocks (each region whole in one block,
+  // blocks <= kMaxBlockBytes unless one region is larger), each exported with
+  // its own IPC handle.
+  struct ScratchBlock {
+    int64_t start = 0;  // first element (in plan region coordinates)
+    int64_t elems = 0;
+    char* ptr = nullptr;
+  };
+  static constexpr size_t kMaxBlockBytes = size_t(256) << 20;
   struct InflightSend {
     int64_t off, len;
     hipEvent_t event;
@@ -99,7 +108,9 @@ class HipPlanExecutor : public Algorithm {
   template <typename Pred>
   void waitFor(Pred done, const char* what, int peer);
   void drain();
-  char* landing(char* scratchBase, int64_t boff, int64_t off, int phase) const;
+  char* landing(const std::vector<ScratchBlock>& blocks, int64_t boff, int64_t off,
+                int phase) const;
+  void allocScratch();
   void waitWar(int64_t off, int64_t len);
 
   glx::Plan plan_;
@@ -117,8 +128,8 @@ class HipPlanExecutor : public Algorithm {
   int split_ = 1;
   bool peerCopyOk_ = true;  // hipMemcpyPeerAsync accepted for IPC-mapped peers
   bool ownCompute_ = false;
-  char* scratch_ = nullptr;
-  size_t scratchBytes_ = 0;
+  std::vector<ScratchBlock> blocks_;                  // ours
+  std::map<int, std::vector<ScratchBlock>> peerBlocks_;  // by destination rank
   int myPhase_ = 0;
   std::vector<OutChan> out_;
   std::vector<InChan> in_;
