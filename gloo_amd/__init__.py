@@ -2,8 +2,9 @@
 
 The drop-in surface of liuxiaotiao/gloo for its data-parallel allreduce:
 gloo::Context / rendezvous, gloo::Algorithm with AllreduceRingChunked and
-AllreduceHalvingDoubling, ReductionFunction, and the elementwise reductions
-of gloo/math.h -- executed on MI355X GPUs (HIP kernels for gfx950, chunks
+AllreduceHalvingDoubling, the function-style gloo::allreduce(AllreduceOptions)
+(ring and bcube), ReductionFunction, and the elementwise reductions of
+gloo/math.h -- executed on MI355X GPUs (HIP kernels for gfx950, chunks
 moved between the GPUs of a node with hipMemcpyPeerAsync over xGMI).
 The native library (libgloo_amd.so, C ABI in include/gloo_amd/glx.h) is
 required; there is no CPU fallback.
@@ -19,6 +20,7 @@ from .algorithms import (  # noqa: F401
     ReductionType,
     plan,
 )
+from .collectives import AllreduceOptions, allreduce  # noqa: F401
 from . import errors  # noqa: F401
 from .errors import EnforceNotMet, Exception, HipError, IoException  # noqa: F401,A004
 

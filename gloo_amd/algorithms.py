@@ -93,7 +93,9 @@ def _stream_ptr(s):
     return s.cuda_stream  # torch.cuda.Stream
 
 
-ALGO_CODES = {"ring_chunked": 0, "halving_doubling": 1, "ring_chunked_mesh": 2}
+ALGO_CODES = {"ring_chunked": 0, "halving_doubling": 1, "ring_chunked_mesh": 2,
+              # schedules of gloo_amd.allreduce (plan introspection)
+              "fn_ring": 3, "fn_ring_mesh": 4, "fn_bcube": 5}
 
 
 class Algorithm:
@@ -178,24 +180,32 @@ HipAllreduceRingChunked = AllreduceRingChunked
 HipAllreduceHalvingDoubling = AllreduceHalvingDoubling
 
 
-def plan(algo, rank, size, count, with_folds=False):
+DEFAULT_MIN_PIECE_BYTES = 4 << 20
+
+
+def plan(algo, rank, size, count, with_folds=False, esize=4, max_segment_size=0,
+         min_piece_bytes=DEFAULT_MIN_PIECE_BYTES):
     """The step program of one rank (host logic, no GPU).  algo: a key of
-    ALGO_CODES.  Returns (steps as 8-tuples, scratch_elems[, fold sources])."""
+    ALGO_CODES.  The fn_* schedules also depend on the element size, the
+    options' maxSegmentSize (0: default) and the ring's device piece size
+    (0: the reference's own segments).  Returns (steps as 8-tuples,
+    scratch_elems[, fold sources])."""
     code = ALGO_CODES[algo]
+    args = (code, rank, size, count, esize, max_segment_size, min_piece_bytes)
     scratch = ctypes.c_int64(0)
-    n = lib.glx_plan(code, rank, size, count, None, 0, ctypes.byref(scratch))
+    n = lib.glx_plan_ex(*args, None, 0, ctypes.byref(scratch))
     if n < 0:
         check(_lib.ERR_INVALID, "plan")
     buf = (ctypes.c_int64 * (8 * max(n, 1)))()
-    lib.glx_plan(code, rank, size, count, buf, n, ctypes.byref(scratch))
+    lib.glx_plan_ex(*args, buf, n, ctypes.byref(scratch))
     steps = [tuple(buf[8 * i: 8 * i + 8]) for i in range(n)]
     if not with_folds:
         return steps, scratch.value
     folds = {}
     for st in steps:
         if st[0] == 5:
-            k = lib.glx_plan_fold(code, rank, size, count, st[5], None, 0)
+            k = lib.glx_plan_fold_ex(*args, st[5], None, 0)
             fb = (ctypes.c_int64 * max(k, 1))()
-            lib.glx_plan_fold(code, rank, size, count, st[5], fb, k)
+            lib.glx_plan_fold_ex(*args, st[5], fb, k)
             folds[st[5]] = list(fb[:k])
     return steps, scratch.value, folds

@@ -1,0 +1,137 @@
+"""Function-style collective: gloo::allreduce(AllreduceOptions) on device
+buffers (gloo/allreduce.h:89-193, gloo/allreduce.cc:97-146).
+
+    opts = AllreduceOptions(context)
+    opts.setOutput(t)                  # in place; or setInputs([...]) + setOutputs([...])
+    opts.setReduceFunction(ReductionFunction.sum)
+    opts.setAlgorithm(AllreduceOptions.Algorithm.RING)
+    allreduce(opts)
+
+Differences forced by the device: the reduce function is one of the
+gloo/math.h ops (ReductionFunction / ReductionType / gloo_amd.math.sum ...),
+not an arbitrary host callable; buffers are device tensors (or raw device
+pointers with an explicit dtype).  Results are bit-identical to the
+reference's for the same inputs, ring and bcube.
+"""
+import ctypes
+import datetime
+
+from . import _lib
+from . import math as _math
+from .algorithms import ReductionFunction, _as_ptrs, _stream_ptr
+from .errors import EnforceNotMet, check
+
+lib = _lib.lib
+
+_MATH_FUNCS = {_math.sum: 1, _math.product: 2, _math.max: 3, _math.min: 4}
+
+
+class AllreduceOptions:
+    """gloo::AllreduceOptions (gloo/allreduce.h:89-193)."""
+
+    class Algorithm:  # gloo/allreduce.h:38-42 (+ RING_MESH: RING's result over all links)
+        UNSPECIFIED = 0
+        RING = 1
+        BCUBE = 2
+        RING_MESH = 3
+
+    def __init__(self, context):
+        self.context = context
+        self.algorithm = self.Algorithm.UNSPECIFIED
+        self.inputs = []
+        self.outputs = []
+        self.elements = None
+        self.dtype = None
+        self.op = None
+        self.tag = 0
+        self.max_segment_size = 0  # 0: the reference's 1 MiB default (allreduce.h:80)
+        self.timeout_ms = 0        # 0: the context's timeout
+        self.stream = None
+
+    def setAlgorithm(self, algorithm):
+        self.algorithm = int(algorithm)
+
+    def setInput(self, buf, elements=None):
+        self.setInputs([buf], elements)
+
+    def setInputs(self, bufs, elements=None, dtype=None):
+        self.inputs = list(bufs)
+        self._sizes(self.inputs, elements, dtype)
+
+    def setOutput(self, buf, elements=None):
+        self.setOutputs([buf], elements)
+
+    def setOutputs(self, bufs, elements=None, dtype=None):
+        self.outputs = list(bufs)
+        self._sizes(self.outputs, elements, dtype)
+
+    def _sizes(self, bufs, elements, dtype):
+        _, dt, numel = _as_ptrs(bufs, dtype if dtype is not None else self.dtype)
+        if self.dtype is not None and dt != self.dtype:
+            raise TypeError("inputs and outputs must share one dtype")
+        self.dtype = dt
+        if elements is None:
+            if numel is None:
+                raise ValueError("elements is required with raw pointers")
+            elements = numel
+        if numel is not None and elements > numel:
+            raise ValueError("elements %d exceeds buffer size %d" % (elements, numel))
+        self.elements = int(elements)
+
+    def setReduceFunction(self, fn):
+        """ReductionFunction.sum/..., a ReductionType value, or
+        gloo_amd.math.sum/product/max/min."""
+        if isinstance(fn, ReductionFunction):
+            self.op = fn.type()
+        elif isinstance(fn, int) and 1 <= fn <= 4:
+            self.op = fn
+        elif fn in _MATH_FUNCS:
+            self.op = _MATH_FUNCS[fn]
+        else:
+            raise EnforceNotMet("only the gloo/math.h reductions run on the device "
+                                "(sum, product, max, min); got %r" % (fn,))
+
+    def setTag(self, tag):
+        self.tag = int(tag) & 0xFFFFFFFF
+
+    def setMaxSegmentSize(self, nbytes):
+        self.max_segment_size = int(nbytes)
+
+    def setTimeout(self, timeout):
+        """seconds (float) or datetime.timedelta."""
+        if isinstance(timeout, datetime.timedelta):
+            timeout = timeout.total_seconds()
+        self.timeout_ms = max(1, int(round(float(timeout) * 1000)))
+
+    def setStream(self, stream):
+        """Order the work on `stream` (torch.cuda.Stream or a hipStream_t)
+        instead of returning with the outputs complete."""
+        self.stream = stream
+
+
+def allreduce(opts):
+    """gloo::allreduce(opts) (gloo/allreduce.cc:97-146).  Without a stream
+    the call is ordered after the work queued on torch's current stream and
+    returns with the outputs complete, like the reference's blocking call."""
+    if not opts.outputs:
+        raise EnforceNotMet("allreduce: at least one output is required")
+    op = opts.op if opts.op is not None else 1
+    inp, _, _ = _as_ptrs(opts.inputs, opts.dtype) if opts.inputs else ([], None, None)
+    outp, _, _ = _as_ptrs(opts.outputs, opts.dtype)
+    iarr = (ctypes.c_void_p * max(len(inp), 1))(*inp)
+    oarr = (ctypes.c_void_p * len(outp))(*outp)
+    sync = None
+    stream = _stream_ptr(opts.stream)
+    if stream is None and any(not isinstance(b, int) for b in opts.outputs + opts.inputs):
+        import torch
+        cur = torch.cuda.current_stream()
+        if cur.cuda_stream:
+            sync, stream = cur, cur.cuda_stream  # ordered on it, then waited for
+        else:
+            cur.synchronize()  # the null stream: let its queued writes land first
+    check(lib.glx_allreduce(opts.context.handle, opts.algorithm, opts.dtype, op,
+                            iarr, len(inp), oarr, len(outp), opts.elements or 0,
+                            opts.tag, opts.max_segment_size, opts.timeout_ms, stream),
+          "allreduce")
+    if sync is not None:
+        sync.synchronize()

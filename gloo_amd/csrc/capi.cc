@@ -8,6 +8,7 @@
 #include <string>
 
 #include "../../include/gloo_amd/glx.h"
+#include "collectives.h"
 #include "common.h"
 #include "context.h"
 #include "executor.h"
@@ -82,6 +83,14 @@ glx_algorithm* makeAlgorithm(int algo, glx_context* ctx, void* const* ptrs, int 
     return GLX_OK;
   });
   return out;
+}
+
+glx::PlanParams planParams(int esize, int64_t maxSegmentBytes, int64_t minPieceBytes) {
+  glx::PlanParams p;
+  p.esize = esize;
+  if (maxSegmentBytes > 0) p.maxSegmentBytes = maxSegmentBytes;
+  p.minPieceBytes = minPieceBytes < 0 ? 0 : minPieceBytes;
+  return p;
 }
 
 }  // namespace
@@ -234,7 +243,14 @@ glx_context* glx_context_create(int rank, int size, int device) {
   return out;
 }
 
-void glx_context_destroy(glx_context* ctx) { delete ctx; }
+void glx_context_destroy(glx_context* ctx) {
+  if (ctx == nullptr) return;
+  guarded([&]() -> int {
+    ctx->c->clearOps();
+    return GLX_OK;
+  });
+  delete ctx;
+}
 
 int glx_context_connect_full_mesh(glx_context* ctx, glx_store* store) {
   return guarded([&]() -> int {
@@ -299,6 +315,30 @@ glx_algorithm* glx_allreduce_create(glx_context* ctx, int algo, void* const* ptr
   return makeAlgorithm(algo, ctx, ptrs, nptrs, count, dtype, op, streams, nstreams);
 }
 
+int glx_allreduce(glx_context* ctx, int algorithm, int dtype, int op, void* const* inputs,
+                  int num_inputs, void* const* outputs, int num_outputs, size_t elements,
+                  uint32_t tag, size_t max_segment_size, int64_t timeout_ms,
+                  glx_stream_t stream) {
+  return guarded([&]() -> int {
+    GLX_ENFORCE(ctx != nullptr, "null context");
+    GLX_ENFORCE(num_inputs >= 0 && (num_inputs == 0 || inputs != nullptr), "bad inputs");
+    GLX_ENFORCE(num_outputs >= 0 && (num_outputs == 0 || outputs != nullptr), "bad outputs");
+    gloo::AllreduceOptions o(ctx->c);
+    o.algorithm = algorithm;
+    o.dtype = dtype;
+    o.op = op;
+    o.in.assign(inputs, inputs + num_inputs);
+    o.out.assign(outputs, outputs + num_outputs);
+    o.elements = elements;
+    o.tag = tag;
+    o.maxSegmentSize = max_segment_size;
+    o.timeout = std::chrono::milliseconds(timeout_ms > 0 ? timeout_ms : 0);
+    o.stream = (hipStream_t)stream;
+    gloo::allreduce(o);
+    return GLX_OK;
+  });
+}
+
 int glx_algorithm_run(glx_algorithm* alg) {
   return guarded([&]() -> int {
     GLX_ENFORCE(alg != nullptr, "null algorithm");
@@ -322,9 +362,17 @@ void glx_algorithm_destroy(glx_algorithm* alg) {
 
 int64_t glx_plan(int algo, int rank, int size, int64_t count, int64_t* steps, int64_t cap,
                  int64_t* scratch_elems) {
+  return glx_plan_ex(algo, rank, size, count, 4, 0, glx::PlanParams().minPieceBytes, steps,
+                     cap, scratch_elems);
+}
+
+int64_t glx_plan_ex(int algo, int rank, int size, int64_t count, int esize,
+                    int64_t max_segment_bytes, int64_t min_piece_bytes, int64_t* steps,
+                    int64_t cap, int64_t* scratch_elems) {
   int64_t n = -1;
   guarded([&]() -> int {
-    glx::Plan p = glx::makePlan(algo, rank, size, count);
+    glx::Plan p = glx::makePlan(algo, rank, size, count,
+                                planParams(esize, max_segment_bytes, min_piece_bytes));
     n = (int64_t)p.steps.size();
     if (scratch_elems) *scratch_elems = p.scratch_elems;
     for (int64_t i = 0; i < n && i < cap && steps != nullptr; i++) {
@@ -346,9 +394,17 @@ int64_t glx_plan(int algo, int rank, int size, int64_t count, int64_t* steps, in
 
 int64_t glx_plan_fold(int algo, int rank, int size, int64_t count, int64_t fold,
                       int64_t* srcs, int64_t cap) {
+  return glx_plan_fold_ex(algo, rank, size, count, 4, 0, glx::PlanParams().minPieceBytes,
+                          fold, srcs, cap);
+}
+
+int64_t glx_plan_fold_ex(int algo, int rank, int size, int64_t count, int esize,
+                         int64_t max_segment_bytes, int64_t min_piece_bytes, int64_t fold,
+                         int64_t* srcs, int64_t cap) {
   int64_t n = -1;
   guarded([&]() -> int {
-    glx::Plan p = glx::makePlan(algo, rank, size, count);
+    glx::Plan p = glx::makePlan(algo, rank, size, count,
+                                planParams(esize, max_segment_bytes, min_piece_bytes));
     GLX_ENFORCE(fold >= 0 && fold < (int64_t)p.folds.size(), "fold index out of range");
     const auto& f = p.folds[(size_t)fold];
     n = (int64_t)f.size();

@@ -140,6 +140,15 @@ Context::Context(int rank_, int size_, int device) : rank(rank_), size(size_), d
 
 Context::~Context() = default;
 
+void Context::clearOps() {
+  std::map<std::string, std::shared_ptr<Algorithm>> drop;
+  {
+    std::lock_guard<std::mutex> g(opsMutex);
+    drop.swap(ops);
+  }
+  drop.clear();  // executors release their reference to this context here
+}
+
 int Context::nextSlot(int numToSkip) {
   GLX_ENFORCE(numToSkip > 0, "numToSkip must be > 0");
   int s = slot_;

@@ -20,6 +20,7 @@
 
 #include <atomic>
 #include <chrono>
+#include <map>
 #include <cstdint>
 #include <memory>
 #include <mutex>
@@ -29,6 +30,8 @@
 #include "store.h"
 
 namespace gloo {
+
+class Algorithm;
 
 // One rank's control block: kWords counters, one per 64-byte line.
 class ControlBlock {
@@ -100,6 +103,13 @@ class Context {
 
   // Throws IoException if a peer process has exited.
   void checkPeersAlive();
+
+  // Executors of function-style collectives by options key (see
+  // collectives.cc).  They hold a reference to this context: clearOps()
+  // breaks that cycle when the context's owner lets go of it.
+  std::mutex opsMutex;
+  std::map<std::string, std::shared_ptr<Algorithm>> ops;
+  void clearOps();
 
  private:
   int device_;

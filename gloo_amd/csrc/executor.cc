@@ -74,10 +74,11 @@ int HipPlanExecutor::copySplit() { return g_copy_split.load(); }
 HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
                                  const std::vector<void*>& ptrs, int64_t count,
                                  int dtype, int op,
-                                 const std::vector<hipStream_t>& streams)
+                                 const std::vector<hipStream_t>& streams,
+                                 const glx::PlanParams& prm)
     : Algorithm(ctx), algo_(algo), ptrs_(ptrs), count_(count), dtype_(dtype), op_(op) {
   GLX_ENFORCE(!ptrs.empty(), "at least one buffer pointer is required");
-  GLX_ENFORCE(count >= 0 && count <= INT32_MAX, "count out of range: ", count);
+  GLX_ENFORCE(count >= 0 && count <= (int64_t(1) << 40), "count out of range: ", count);
   esize_ = glx_dtype_size(dtype);
   GLX_ENFORCE(esize_ > 0, "unknown dtype ", dtype);
   GLX_ENFORCE(op >= GLX_SUM && op <= GLX_MIN, "unknown reduction op ", op);
@@ -91,7 +92,9 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
   device_ = ctx->device();
   GLX_HIP_CHECK(hipSetDevice(device_));
   slot_ = ctx->nextSlot();
-  plan_ = glx::makePlan(algo, contextRank_, contextSize_, count);
+  glx::PlanParams pp = prm;
+  pp.esize = (int)esize_;
+  plan_ = glx::makePlan(algo, contextRank_, contextSize_, count, pp);
 
   userStream_ = !streams.empty();
   if (userStream_) {
@@ -100,7 +103,6 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
     GLX_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
     ownCompute_ = true;
   }
-  myPhase_ = (int)((uintptr_t)ptrs[0] % 16);
   split_ = std::max(1, std::min(copySplit(), (int)kMaxSplit));
 
   allocScratch();
@@ -184,8 +186,8 @@ int HipPlanExecutor::inIndex(int peer, int tag) {
 }
 
 // Our record for this algorithm instance: where peers land their messages
-// (scratch pointer / IPC handle, ptr0 phase) and which counter words they
-// bump (our delivery words) or watch (our credit words).
+// (scratch pointer / IPC handle) and which counter words they bump (our
+// delivery words) or watch (our credit words).
 void HipPlanExecutor::publish() {
   std::vector<char> b;
   putPod<uint32_t>(b, kAlgMagic);
@@ -202,7 +204,6 @@ void HipPlanExecutor::publish() {
     putPod<int32_t>(b, haveIpc);
     putPod(b, h);
   }
-  putPod<int32_t>(b, myPhase_);
   putPod<int32_t>(b, (int32_t)(in_.size() + out_.size()));
   for (auto& ic : in_) {
     putPod<int32_t>(b, ic.peer);
@@ -230,7 +231,7 @@ void HipPlanExecutor::resolvePeers() {
     GLX_TRACE("r%d resolve: get record of rank %d", contextRank_, r);
     auto b = context_->store().get(
         "glx/alg/" + std::to_string(slot_) + "/" + std::to_string(r),
-        context_->getTimeout());
+        effectiveTimeout());
     size_t at = 0;
     GLX_ENFORCE(getPod<uint32_t>(b, at) == kAlgMagic, "bad algorithm record from rank ", r);
     getPod<int64_t>(b, at);  // pid (already known from the endpoint)
@@ -262,7 +263,6 @@ void HipPlanExecutor::resolvePeers() {
       pb.push_back(blk);
     }
     if (needScratch) peerBlocks_[r] = pb;
-    int32_t phase = getPod<int32_t>(b, at);
     int32_t n = getPod<int32_t>(b, at);
     for (int32_t i = 0; i < n; i++) {
       int32_t peer = getPod<int32_t>(b, at);
@@ -274,7 +274,6 @@ void HipPlanExecutor::resolvePeers() {
         int idx = outIndex(r, tag);
         if (idx >= 0) {
           out_[idx].delivery = pe.ctl->word((uint32_t)word);
-          out_[idx].peerPhase = phase;
           out_[idx].peerDevice = pe.localDevice;
         }
       } else {  // peer sends to us on `tag`: its credit word
@@ -294,8 +293,12 @@ void HipPlanExecutor::resolvePeers() {
   resolved_ = true;
 }
 
+// A message for ptr0[off, ...) lands at the 16-byte phase that offset has in
+// a 16-byte aligned buffer, so the reduce kernel reading it next to ptr0 stays
+// on its 16-byte vector path (an unaligned ptr0 still works: the kernel then
+// takes its scalar path).  Both sides compute it from `off` alone.
 char* HipPlanExecutor::landing(const std::vector<ScratchBlock>& blocks, int64_t boff,
-                               int64_t off, int phase) const {
+                               int64_t off) const {
   const ScratchBlock* blk = nullptr;
   for (const auto& b : blocks) {
     if (b.start <= boff && boff < b.start + b.elems) {
@@ -305,7 +308,7 @@ char* HipPlanExecutor::landing(const std::vector<ScratchBlock>& blocks, int64_t 
   }
   GLX_ENFORCE(blk != nullptr && blk->ptr != nullptr, "no receive block holds region ", boff);
   uintptr_t at = ((uintptr_t)(boff - blk->start) * esize_ + 15) & ~(uintptr_t)15;
-  at += ((uintptr_t)phase + (uintptr_t)off * esize_) % 16;
+  at += ((uintptr_t)off * esize_) % 16;
   return blk->ptr + at;
 }
 
@@ -370,7 +373,7 @@ void HipPlanExecutor::pollPending() {
 template <typename Pred>
 void HipPlanExecutor::waitFor(Pred done, const char* what, int peer) {
   if (done()) return;
-  const auto timeout = context_->getTimeout();
+  const auto timeout = effectiveTimeout();
   const auto start = std::chrono::steady_clock::now();
   auto lastAlive = start;
   bool warned = false;
@@ -438,136 +441,7 @@ void HipPlanExecutor::run() {
     GLX_HIP_CHECK(glx::launch_reduce_n(op_, dtype_, ptr0, srcs.data(), (int)srcs.size(),
                                        (size_t)count_, compute_));
   }
-  if (contextSize_ > 1) {
-    if (!resolved_) resolvePeers();
-    bool computeSinceMark = true;  // the caller's writes to ptr0 count as compute
-    for (auto& c : copies_) c.last = nullptr;
-    const auto& steps = plan_.steps;
-    for (size_t i = 0; i < steps.size(); i++) {
-      const glx::Step& s = steps[i];
-      GLX_TRACE("r%d step %zu kind %d peer %d chan %d off %ld len %ld", contextRank_, i,
-                (int)s.kind, (int)s.peer, (int)s.channel, (long)s.off, (long)s.len);
-      switch (s.kind) {
-        case glx::SEND: {
-          OutChan& oc = out_[stepChan_[i]];
-          const uint64_t n = ++oc.sent;
-          // one receive region per channel: message n may only land once the
-          // receiver has consumed message n-1
-          waitFor([&] { return oc.credit->load(std::memory_order_acquire) + 1 >= n; },
-                  "receive-region credit", oc.peer);
-          const size_t nbytes = (size_t)s.len * esize_;
-          Pending pd{};
-          pd.word = oc.delivery;
-          pd.value = n;
-          if (nbytes > 0) {
-            if (computeSinceMark) {
-              GLX_HIP_CHECK(hipEventRecord(computeMark_, compute_));
-              markEpoch_++;
-              computeSinceMark = false;
-            }
-            char* dst = landing(peerBlocks_[oc.peer], s.dst_off, s.off, oc.peerPhase);
-            const char* src = ptr0 + (size_t)s.off * esize_;
-            int parts = split_;
-            while (parts > 1 && nbytes / (size_t)parts < kMinSplitBytes) parts--;
-            const size_t per = ((nbytes / (size_t)parts) + 255) & ~(size_t)255;
-            for (int j = 0; j < parts; j++) {
-              const size_t at = (size_t)j * per;
-              if (at >= nbytes) break;
-              const size_t len = std::min(per, nbytes - at);
-              CopyStream& cs = copies_[oc.stream + j];
-              if (cs.waitedMark != markEpoch_) {
-                // the chunk may have been produced by compute work: order after it
-                GLX_HIP_CHECK(hipStreamWaitEvent(cs.s, computeMark_, 0));
-                cs.waitedMark = markEpoch_;
-              }
-              hipError_t ce = hipErrorUnknown;
-              if (peerCopyOk_ && oc.peerDevice >= 0 && oc.peerDevice != device_) {
-                ce = hipMemcpyPeerAsync(dst + at, oc.peerDevice, src + at, device_, len, cs.s);
-                if (ce != hipSuccess) {
-                  (void)hipGetLastError();
-                  peerCopyOk_ = false;  // e.g. an IPC mapping the peer API rejects
-                }
-              }
-              if (ce != hipSuccess) {
-                GLX_HIP_CHECK(hipMemcpyAsync(dst + at, src + at, len, hipMemcpyDeviceToDevice,
-                                             cs.s));
-              }
-              GLX_TRACE("r%d   copy part %d issued (%zu bytes)", contextRank_, j, len);
-              hipEvent_t ev = events_[i * (size_t)split_ + (size_t)j];
-              GLX_HIP_CHECK(hipEventRecord(ev, cs.s));
-              cs.last = ev;
-              inflight_.push_back({s.off, s.len, ev});
-              pd.ev[pd.nev++] = ev;
-            }
-          }
-          pending_.push_back(pd);
-          break;
-        }
-        case glx::RECV: {
-          InChan& ic = in_[stepChan_[i]];
-          const uint64_t n = ++ic.received;
-          waitFor([&] { return ic.delivery->load(std::memory_order_acquire) >= n; },
-                  "data", ic.peer);
-          break;
-        }
-        case glx::REDUCE: {
-          waitWar(s.off, s.len);
-          char* dst = ptr0 + (size_t)s.off * esize_;
-          const char* src = landing(blocks_, s.boff, s.off, myPhase_);
-          GLX_HIP_CHECK(glx::launch_reduce(op_, dtype_, dst, dst, src, (size_t)s.len, compute_));
-          computeSinceMark = true;
-          break;
-        }
-        case glx::FOLD: {
-          waitWar(s.off, s.len);
-          char* dst = ptr0 + (size_t)s.off * esize_;
-          const auto& regions = plan_.folds[(size_t)s.boff];
-          std::vector<const void*> srcs;
-          for (int64_t r : regions) {
-            srcs.push_back(r < 0 ? (const void*)dst
-                                 : (const void*)landing(blocks_, r, s.off, myPhase_));
-          }
-          GLX_HIP_CHECK(glx::launch_reduce_n(op_, dtype_, dst, srcs.data(), (int)srcs.size(),
-                                             (size_t)s.len, compute_, /*rev=*/true));
-          computeSinceMark = true;
-          break;
-        }
-        case glx::COPY: {
-          waitWar(s.off, s.len);
-          char* dst = ptr0 + (size_t)s.off * esize_;
-          const char* src = landing(blocks_, s.boff, s.off, myPhase_);
-          GLX_HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)s.len * esize_,
-                                       hipMemcpyDeviceToDevice, compute_));
-          computeSinceMark = true;
-          break;
-        }
-        case glx::RELEASE: {
-          InChan& ic = in_[stepChan_[i]];
-          const uint64_t v = ++ic.consumed;
-          hipEvent_t ev = events_[i * (size_t)split_];
-          GLX_HIP_CHECK(hipEventRecord(ev, compute_));
-          Pending pd{};
-          pd.ev[0] = ev;
-          pd.nev = 1;
-          pd.word = ic.credit;
-          pd.value = v;
-          pending_.push_back(pd);
-          break;
-        }
-        default:
-          GLX_ENFORCE(false, "bad plan step kind ", s.kind);
-      }
-      pollPending();
-    }
-    GLX_TRACE("r%d drain (%zu pending)", contextRank_, pending_.size());
-    drain();
-    GLX_TRACE("r%d drained", contextRank_);
-    // the caller's stream must not run ahead of copies still reading ptr0
-    for (auto& c : copies_) {
-      if (c.last != nullptr) GLX_HIP_CHECK(hipStreamWaitEvent(compute_, c.last, 0));
-    }
-    inflight_.clear();
-  }
+  if (contextSize_ > 1) exchange(ptr0);
   // Local broadcast of ptrs_[0] (:209-211).
   for (size_t i = 1; i < ptrs_.size(); i++) {
     GLX_HIP_CHECK(hipMemcpyAsync(ptrs_[i], ptr0, bytes, hipMemcpyDeviceToDevice, compute_));
@@ -575,6 +449,200 @@ void HipPlanExecutor::run() {
   GLX_TRACE("r%d sync", contextRank_);
   if (!userStream_) GLX_HIP_CHECK(hipStreamSynchronize(compute_));
   GLX_TRACE("r%d done", contextRank_);
+}
+
+// genLocalReduceFunction (gloo/allreduce.cc:44-82) over the whole buffer at
+// once: each segment's local reduction happens exactly once in the
+// reference, before the segment is first sent or reduced into, and it is
+// elementwise, so doing it up front gives the same bits.
+void HipPlanExecutor::localReduce(const std::vector<void*>& in,
+                                  const std::vector<void*>& out) {
+  const size_t n = (size_t)count_;
+  void* out0 = out[0];
+  if (in.size() == 1) {  // :50-56
+    if (in[0] != out0) {
+      GLX_HIP_CHECK(hipMemcpyAsync(out0, in[0], n * esize_, hipMemcpyDeviceToDevice, compute_));
+    }
+  } else if (in.size() >= 2) {  // :58-71
+    std::vector<const void*> rest;
+    if (dtype_ == GLX_FLOAT16) {
+      // out0 = fn(in0, in1) writes a buffer other than its first operand,
+      // and float16's assignment reads the destination's old value
+      // (gloo/types.h operator=): the two-operand kernel reproduces that
+      GLX_HIP_CHECK(glx::launch_reduce(op_, dtype_, out0, in[0], in[1], n, compute_));
+      rest.push_back(out0);
+      for (size_t i = 2; i < in.size(); i++) rest.push_back(in[i]);
+    } else {
+      rest.assign(in.begin(), in.end());
+    }
+    if (rest.size() >= 2) {
+      GLX_HIP_CHECK(glx::launch_reduce_n(op_, dtype_, out0, rest.data(), (int)rest.size(), n,
+                                         compute_));
+    }
+  } else if (out.size() >= 2) {  // :72-81, no inputs: fold the outputs
+    std::vector<const void*> srcs(out.begin(), out.end());
+    GLX_HIP_CHECK(glx::launch_reduce_n(op_, dtype_, out0, srcs.data(), (int)srcs.size(), n,
+                                       compute_));
+  }
+}
+
+void HipPlanExecutor::runFn(const FnCall& call) {
+  GLX_ENFORCE(!call.out.empty(), "allreduce needs at least one output");
+  for (void* p : call.out) GLX_ENFORCE(p != nullptr || count_ == 0, "null output pointer");
+  for (void* p : call.in) GLX_ENFORCE(p != nullptr || count_ == 0, "null input pointer");
+  if (count_ == 0) return;  // gloo/allreduce.cc:98-100
+  GLX_HIP_CHECK(hipSetDevice(device_));
+  // per-call stream and timeout (opts.timeout, gloo/allreduce.h:50)
+  struct Restore {
+    HipPlanExecutor* e;
+    hipStream_t s;
+    ~Restore() {
+      e->compute_ = s;
+      e->timeout_ = std::chrono::milliseconds(0);
+    }
+  } restore{this, compute_};
+  if (call.stream != nullptr) compute_ = call.stream;
+  timeout_ = call.timeout;
+  localReduce(call.in, call.out);
+  char* out0 = static_cast<char*>(call.out[0]);
+  if (contextSize_ > 1) exchange(out0);  // :129-146
+  for (size_t i = 1; i < call.out.size(); i++) {  // broadcastOutputs
+    GLX_HIP_CHECK(hipMemcpyAsync(call.out[i], out0, (size_t)count_ * esize_,
+                                 hipMemcpyDeviceToDevice, compute_));
+  }
+  if (call.stream == nullptr) GLX_HIP_CHECK(hipStreamSynchronize(compute_));
+}
+
+void HipPlanExecutor::exchange(char* ptr0) {
+  if (!resolved_) resolvePeers();
+  bool computeSinceMark = true;  // the caller's writes to ptr0 count as compute
+  for (auto& c : copies_) c.last = nullptr;
+  const auto& steps = plan_.steps;
+  for (size_t i = 0; i < steps.size(); i++) {
+    const glx::Step& s = steps[i];
+    GLX_TRACE("r%d step %zu kind %d peer %d chan %d off %ld len %ld", contextRank_, i,
+              (int)s.kind, (int)s.peer, (int)s.channel, (long)s.off, (long)s.len);
+    switch (s.kind) {
+      case glx::SEND: {
+        OutChan& oc = out_[stepChan_[i]];
+        const uint64_t n = ++oc.sent;
+        // one receive region per channel: message n may only land once the
+        // receiver has consumed message n-1
+        waitFor([&] { return oc.credit->load(std::memory_order_acquire) + 1 >= n; },
+                "receive-region credit", oc.peer);
+        const size_t nbytes = (size_t)s.len * esize_;
+        Pending pd{};
+        pd.word = oc.delivery;
+        pd.value = n;
+        if (nbytes > 0) {
+          if (computeSinceMark) {
+            GLX_HIP_CHECK(hipEventRecord(computeMark_, compute_));
+            markEpoch_++;
+            computeSinceMark = false;
+          }
+          char* dst = landing(peerBlocks_[oc.peer], s.dst_off, s.off);
+          const char* src = ptr0 + (size_t)s.off * esize_;
+          int parts = split_;
+          while (parts > 1 && nbytes / (size_t)parts < kMinSplitBytes) parts--;
+          const size_t per = ((nbytes / (size_t)parts) + 255) & ~(size_t)255;
+          for (int j = 0; j < parts; j++) {
+            const size_t at = (size_t)j * per;
+            if (at >= nbytes) break;
+            const size_t len = std::min(per, nbytes - at);
+            CopyStream& cs = copies_[oc.stream + j];
+            if (cs.waitedMark != markEpoch_) {
+              // the chunk may have been produced by compute work: order after it
+              GLX_HIP_CHECK(hipStreamWaitEvent(cs.s, computeMark_, 0));
+              cs.waitedMark = markEpoch_;
+            }
+            hipError_t ce = hipErrorUnknown;
+            if (peerCopyOk_ && oc.peerDevice >= 0 && oc.peerDevice != device_) {
+              ce = hipMemcpyPeerAsync(dst + at, oc.peerDevice, src + at, device_, len, cs.s);
+              if (ce != hipSuccess) {
+                (void)hipGetLastError();
+                peerCopyOk_ = false;  // e.g. an IPC mapping the peer API rejects
+              }
+            }
+            if (ce != hipSuccess) {
+              GLX_HIP_CHECK(hipMemcpyAsync(dst + at, src + at, len, hipMemcpyDeviceToDevice,
+                                           cs.s));
+            }
+            GLX_TRACE("r%d   copy part %d issued (%zu bytes)", contextRank_, j, len);
+            hipEvent_t ev = events_[i * (size_t)split_ + (size_t)j];
+            GLX_HIP_CHECK(hipEventRecord(ev, cs.s));
+            cs.last = ev;
+            inflight_.push_back({s.off, s.len, ev});
+            pd.ev[pd.nev++] = ev;
+          }
+        }
+        pending_.push_back(pd);
+        break;
+      }
+      case glx::RECV: {
+        InChan& ic = in_[stepChan_[i]];
+        const uint64_t n = ++ic.received;
+        waitFor([&] { return ic.delivery->load(std::memory_order_acquire) >= n; },
+                "data", ic.peer);
+        break;
+      }
+      case glx::REDUCE: {
+        waitWar(s.off, s.len);
+        char* dst = ptr0 + (size_t)s.off * esize_;
+        const char* src = landing(blocks_, s.boff, s.off);
+        GLX_HIP_CHECK(glx::launch_reduce(op_, dtype_, dst, dst, src, (size_t)s.len, compute_));
+        computeSinceMark = true;
+        break;
+      }
+      case glx::FOLD: {
+        waitWar(s.off, s.len);
+        char* dst = ptr0 + (size_t)s.off * esize_;
+        const auto& regions = plan_.folds[(size_t)s.boff];
+        std::vector<const void*> srcs;
+        for (int64_t r : regions) {
+          srcs.push_back(r < 0 ? (const void*)dst
+                               : (const void*)landing(blocks_, r, s.off));
+        }
+        const bool rev = (s.flags & glx::kFoldLeft) == 0;  // ring chain vs left fold
+        GLX_HIP_CHECK(glx::launch_reduce_n(op_, dtype_, dst, srcs.data(), (int)srcs.size(),
+                                           (size_t)s.len, compute_, rev));
+        computeSinceMark = true;
+        break;
+      }
+      case glx::COPY: {
+        waitWar(s.off, s.len);
+        char* dst = ptr0 + (size_t)s.off * esize_;
+        const char* src = landing(blocks_, s.boff, s.off);
+        GLX_HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)s.len * esize_,
+                                     hipMemcpyDeviceToDevice, compute_));
+        computeSinceMark = true;
+        break;
+      }
+      case glx::RELEASE: {
+        InChan& ic = in_[stepChan_[i]];
+        const uint64_t v = ++ic.consumed;
+        hipEvent_t ev = events_[i * (size_t)split_];
+        GLX_HIP_CHECK(hipEventRecord(ev, compute_));
+        Pending pd{};
+        pd.ev[0] = ev;
+        pd.nev = 1;
+        pd.word = ic.credit;
+        pd.value = v;
+        pending_.push_back(pd);
+        break;
+      }
+      default:
+        GLX_ENFORCE(false, "bad plan step kind ", s.kind);
+    }
+    pollPending();
+  }
+  GLX_TRACE("r%d drain (%zu pending)", contextRank_, pending_.size());
+  drain();
+  GLX_TRACE("r%d drained", contextRank_);
+  // the caller's stream must not run ahead of copies still reading ptr0
+  for (auto& c : copies_) {
+    if (c.last != nullptr) GLX_HIP_CHECK(hipStreamWaitEvent(compute_, c.last, 0));
+  }
+  inflight_.clear();
 }
 
 }  // namespace gloo

@@ -16,6 +16,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <chrono>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -43,10 +44,25 @@ class HipPlanExecutor : public Algorithm {
  public:
   HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
                   const std::vector<void*>& ptrs, int64_t count, int dtype,
-                  int op, const std::vector<hipStream_t>& streams);
+                  int op, const std::vector<hipStream_t>& streams,
+                  const glx::PlanParams& prm = glx::PlanParams());
   ~HipPlanExecutor() noexcept(false) override;
 
+  // Class-style run (gloo/allreduce_ring_chunked.h:83-212): fold ptrs into
+  // ptrs[0], run the schedule on it, copy it to the other pointers.
   void run() override;
+
+  // Function-style run (gloo/allreduce.cc:97-146) on buffers given per call:
+  // inputs reduced into out[0] (genLocalReduceFunction, :44-82), the schedule
+  // on out[0], out[0] copied to out[1..] (genLocalBroadcastFunction, :87-95).
+  // The buffers may differ from call to call; nothing about them is
+  // published to peers.
+  struct FnCall {
+    std::vector<void*> in, out;
+    hipStream_t stream = nullptr;  // null: own stream, complete on return
+    std::chrono::milliseconds timeout{0};  // 0: the context's
+  };
+  void runFn(const FnCall& call);
 
   int64_t bytesSentPerRun() const { return plan_.bytes_sent * (int64_t)esize_; }
 
@@ -63,7 +79,6 @@ class HipPlanExecutor : public Algorithm {
     std::atomic<uint64_t>* credit;  // = our word
     std::atomic<uint64_t>* delivery = nullptr;  // in peer's block
     uint64_t sent = 0;
-    int peerPhase = 0;  // peer ptr0 address mod 16
     int peerDevice = -1;
     int stream = 0;     // index into copies_ (one copy stream per destination peer)
   };
@@ -108,8 +123,12 @@ class HipPlanExecutor : public Algorithm {
   template <typename Pred>
   void waitFor(Pred done, const char* what, int peer);
   void drain();
-  char* landing(const std::vector<ScratchBlock>& blocks, int64_t boff, int64_t off,
-                int phase) const;
+  char* landing(const std::vector<ScratchBlock>& blocks, int64_t boff, int64_t off) const;
+  void exchange(char* ptr0);
+  std::chrono::milliseconds effectiveTimeout() const {
+    return timeout_.count() > 0 ? timeout_ : context_->getTimeout();
+  }  // the plan's steps on ptr0 (contextSize_ > 1)
+  void localReduce(const std::vector<void*>& in, const std::vector<void*>& out);
   void allocScratch();
   void waitWar(int64_t off, int64_t len);
 
@@ -130,7 +149,7 @@ class HipPlanExecutor : public Algorithm {
   bool ownCompute_ = false;
   std::vector<ScratchBlock> blocks_;                  // ours
   std::map<int, std::vector<ScratchBlock>> peerBlocks_;  // by destination rank
-  int myPhase_ = 0;
+  std::chrono::milliseconds timeout_{0};  // per-call override (0: context's)
   std::vector<OutChan> out_;
   std::vector<InChan> in_;
   std::vector<int> stepChan_;        // channel index per step

@@ -281,53 +281,56 @@ Plan planHalvingDoubling(int rank, int size, int64_t count) {
 }
 
 // ---------------------------------------------------------------------------
-// ring_chunked semantics over the full xGMI mesh
+// Owner-computes over the full xGMI mesh
 // ---------------------------------------------------------------------------
-// The ring (gloo/allreduce_ring_chunked.h:106-158) reduces chunk pair j
-// (chunks 2j, 2j+1) along ranks j, j+1, ..., j+P-1: rank j+k computes
-// op(x[j+k], partial) in place.  Here rank j receives x[j+1..j+P-1] of pair j
-// directly from each owner (P-1 copies, P-1 different links) and evaluates the
-// same chain in one FOLD; then it sends the finished pair to every rank
-// (the broadcast pass, :163-200, as one all-to-all round).
-Plan planRingChunkedMesh(int rank, int size, int64_t count) {
+// A ring reduces each owner's range along a chain of ranks, every rank
+// computing op(its value, partial) in place.  Here the owner receives the
+// other ranks' copies of its range directly (P-1 copies on P-1 different
+// links) and evaluates the same chain in one FOLD; then it sends the
+// finished range to every rank (the allgather as one all-to-all round).
+// chain(c) lists the ranks of owner c's chain in FOLD order (s[0] first).
+namespace {
+
+template <typename Range, typename Chain>
+Plan meshPlan(int rank, int size, Range range, Chain chain) {
   Plan p;
-  if (count == 0 || size == 1) return p;
-  const int64_t chunks = 2 * (int64_t)size;
-  const int64_t chunkSize = std::max<int64_t>(256, (count + chunks - 1) / chunks);
-  const int64_t region = 2 * chunkSize + kPadElems;
-  auto pair = [&](int j, int64_t* off, int64_t* len) {
-    int64_t o = 2 * (int64_t)j * chunkSize;
-    int64_t l = 0;
-    if (o < count) l = std::min(2 * chunkSize, count - o);
-    *off = o;
-    *len = l;
-  };
+  int64_t maxLen = 0;
+  for (int c = 0; c < size; c++) {
+    int64_t off, len;
+    range(c, &off, &len);
+    maxLen = std::max(maxLen, len);
+  }
+  const int64_t region = maxLen + kPadElems;
   // scratch: [0, P) reduce-scatter regions by source rank, [P, 2P) results
   p.scratch_elems = 2 * (int64_t)size * region;
   int64_t myOff, myLen;
-  pair(rank, &myOff, &myLen);
-  for (int d = 1; d < size; d++) {  // my copy of pair j to its owner j
+  range(rank, &myOff, &myLen);
+  for (int d = 1; d < size; d++) {  // my copy of range j to its owner j
     const int j = (rank + d) % size;
     int64_t off, len;
-    pair(j, &off, &len);
+    range(j, &off, &len);
     if (len == 0) continue;
     p.steps.push_back({SEND, j, 0, off, len, 0, (int64_t)rank * region, 0});
     p.bytes_sent += len;
   }
   if (myLen > 0) {
-    std::vector<int64_t> srcs{-1};  // x[rank] is ptr0 itself
-    for (int k = 1; k < size; k++) {
-      const int from = (rank + k) % size;
+    const std::vector<int> order = chain(rank);
+    std::vector<int64_t> srcs;
+    for (int from : order) {
+      if (from == rank) {
+        srcs.push_back(-1);  // our own copy is ptr0 itself
+        continue;
+      }
       p.steps.push_back({RECV, from, 0, 0, myLen, (int64_t)from * region, 0, 0});
       srcs.push_back((int64_t)from * region);
     }
     p.folds.push_back(srcs);
     p.steps.push_back({FOLD, -1, (int64_t)srcs.size(), myOff, myLen,
                        (int64_t)p.folds.size() - 1, 0, 0});
-    for (int k = 1; k < size; k++) {
-      p.steps.push_back({RELEASE, (rank + k) % size, 0, 0, 0, 0, 0, 0});
+    for (int from : order) {
+      if (from != rank) p.steps.push_back({RELEASE, from, 0, 0, 0, 0, 0, 0});
     }
-    for (int d = 1; d < size; d++) {  // the finished pair to everyone
+    for (int d = 1; d < size; d++) {  // the finished range to everyone
       const int j = (rank + d) % size;
       p.steps.push_back({SEND, j, 1, myOff, myLen, 0, (int64_t)(size + rank) * region, 0});
       p.bytes_sent += myLen;
@@ -336,7 +339,7 @@ Plan planRingChunkedMesh(int rank, int size, int64_t count) {
   for (int d = 1; d < size; d++) {
     const int k = (rank - d + size) % size;
     int64_t off, len;
-    pair(k, &off, &len);
+    range(k, &off, &len);
     if (len == 0) continue;
     p.steps.push_back({RECV, k, 1, 0, len, (int64_t)(size + k) * region, 0, 0});
     p.steps.push_back({COPY, 0, 0, off, len, (int64_t)(size + k) * region, 0, 0});
@@ -345,11 +348,305 @@ Plan planRingChunkedMesh(int rank, int size, int64_t count) {
   return p;
 }
 
-Plan makePlan(int algo, int rank, int size, int64_t count) {
+}  // namespace
+
+// ring_chunked (gloo/allreduce_ring_chunked.h:106-158) reduces chunk pair j
+// (chunks 2j, 2j+1) along ranks j, j+1, ..., j+P-1: rank j+k computes
+// op(x[j+k], partial) in place.  The broadcast pass (:163-200) becomes the
+// all-to-all round.
+Plan planRingChunkedMesh(int rank, int size, int64_t count) {
+  if (count == 0 || size == 1) return Plan();
+  const int64_t chunks = 2 * (int64_t)size;
+  const int64_t chunkSize = std::max<int64_t>(256, (count + chunks - 1) / chunks);
+  auto pair = [&](int j, int64_t* off, int64_t* len) {
+    int64_t o = 2 * (int64_t)j * chunkSize;
+    *off = o;
+    *len = o < count ? std::min(2 * chunkSize, count - o) : 0;
+  };
+  auto chain = [&](int j) {
+    std::vector<int> v;
+    for (int k = 0; k < size; k++) v.push_back((j + k) % size);
+    return v;
+  };
+  return meshPlan(rank, size, pair, chain);
+}
+
+// ---------------------------------------------------------------------------
+// gloo::allreduce(opts), Algorithm::RING (gloo/allreduce.cc:148-393)
+// ---------------------------------------------------------------------------
+namespace {
+
+struct FnRingGeom {
+  int64_t count = 0, chunkE = 0, npc = 0, pieceE = 0, S = 0;
+
+  // piece g (mod S): owner chunk g / npc, piece g % npc within it; the
+  // length is clipped to the buffer and may be 0 (the reference's
+  // out-of-range segments, :256-262).
+  void piece(int64_t g, int64_t* off, int64_t* len) const {
+    g %= S;
+    const int64_t c = g / npc, j = g % npc;
+    const int64_t o = c * chunkE + j * pieceE;
+    int64_t l = std::max<int64_t>(0, std::min(pieceE, chunkE - j * pieceE));
+    l = o < count ? std::min(l, count - o) : 0;
+    *off = o;
+    *len = l;
+  }
+};
+
+int64_t roundUp(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+FnRingGeom fnRingGeom(int size, int64_t count, const PlanParams& prm) {
+  const int64_t es = prm.esize;
+  if (es <= 0) fail("element size must be positive");
+  const int64_t P = size;
+  const int64_t totalBytes = count * es;
+  // :193-219 (maxSegmentBytes, numSegments, segmentBytes)
+  const int64_t maxSegmentBytes = es * std::max<int64_t>(1, prm.maxSegmentBytes / es);
+  const int64_t numSegments = roundUp(
+      std::max((totalBytes + maxSegmentBytes - 1) / maxSegmentBytes, 2 * P), P);
+  const int64_t spr = numSegments / P;
+  const int64_t segmentBytes = roundUp((totalBytes + numSegments - 1) / numSegments, es);
+  const int64_t segE = segmentBytes / es;
+  FnRingGeom g;
+  g.count = count;
+  // Rank c ends the reduce-scatter owning segments [c*spr, (c+1)*spr): the
+  // element range [c*chunkE, (c+1)*chunkE).  That ownership (and the chain
+  // c-1, c-2, ..., c along which it is reduced) fixes every result bit; the
+  // pieces it is moved in do not.
+  g.chunkE = spr * segE;
+  const int64_t target = std::max(segE, prm.minPieceBytes / es);
+  // >= 2 pieces per chunk keeps the reference's invariant that a piece is
+  // reduced before it is forwarded (spr >= 2, :214-216)
+  g.npc = std::max<int64_t>(2, (g.chunkE + target - 1) / target);
+  g.npc = std::min(g.npc, spr);
+  g.pieceE = (g.chunkE + g.npc - 1) / g.npc;
+  g.S = P * g.npc;
+  return g;
+}
+
+}  // namespace
+
+Plan planFnRing(int rank, int size, int64_t count, const PlanParams& prm) {
+  Plan p;
+  if (count == 0 || size == 1) return p;  // :98-100, :129-133
+  const FnRingGeom g = fnRingGeom(size, count, prm);
+  const int64_t region = g.pieceE + kPadElems;
+  // tmp (two segments, :221-232) for the reduce-scatter; the allgather
+  // receives into out directly in the reference (:382), here via two more
+  // regions and a COPY
+  p.scratch_elems = 4 * region;
+  const int recvRank = (rank + 1) % size;         // :158
+  const int sendRank = (rank + size - 1) % size;  // :159
+  const int64_t iters = g.S - g.npc + 2;          // :264-279
+  // reduce/scatter (:279-322)
+  for (int64_t i = 0; i < iters; i++) {
+    if (i >= 2) {
+      const int64_t k = i - 2;
+      int64_t off, len;
+      g.piece((rank + 2) * (int64_t)g.npc + k, &off, &len);  // recvOffset, :252-254
+      if (len > 0) {
+        const int64_t ch = k & 1;
+        p.steps.push_back({RECV, recvRank, ch, 0, len, ch * region, 0, 0});
+        p.steps.push_back({REDUCE, 0, 0, off, len, ch * region, 0, 0});
+        p.steps.push_back({RELEASE, recvRank, ch, 0, 0, 0, 0, 0});
+      }
+    }
+    if (i < g.S - g.npc) {
+      int64_t off, len;
+      g.piece((rank + 1) * (int64_t)g.npc + i, &off, &len);  // sendOffset, :249-251
+      if (len > 0) {
+        const int64_t ch = i & 1;
+        p.steps.push_back({SEND, sendRank, ch, off, len, 0, ch * region, 0});
+        p.bytes_sent += len;
+      }
+    }
+  }
+  // allgather (:362-392)
+  for (int64_t i = 0; i < iters; i++) {
+    if (i >= 2) {
+      const int64_t k = i - 2;
+      int64_t off, len;
+      g.piece((rank + 1) * (int64_t)g.npc + k, &off, &len);  // recvOffset, :336-338
+      if (len > 0) {
+        const int64_t ch = 2 + (k & 1);
+        p.steps.push_back({RECV, recvRank, ch, 0, len, ch * region, 0, 0});
+        p.steps.push_back({COPY, 0, 0, off, len, ch * region, 0, 0});
+        p.steps.push_back({RELEASE, recvRank, ch, 0, 0, 0, 0, 0});
+      }
+    }
+    if (i < g.S - g.npc) {
+      int64_t off, len;
+      g.piece((int64_t)rank * g.npc + i, &off, &len);  // sendOffset, :333-335
+      if (len > 0) {
+        const int64_t ch = 2 + (i & 1);
+        p.steps.push_back({SEND, sendRank, ch, off, len, 0, ch * region, 0});
+        p.bytes_sent += len;
+      }
+    }
+  }
+  return p;
+}
+
+Plan planFnRingMesh(int rank, int size, int64_t count, const PlanParams& prm) {
+  if (count == 0 || size == 1) return Plan();
+  const FnRingGeom g = fnRingGeom(size, count, prm);
+  auto range = [&](int c, int64_t* off, int64_t* len) {
+    const int64_t o = (int64_t)c * g.chunkE;
+    *off = o;
+    *len = o < count ? std::min(g.chunkE, count - o) : 0;
+  };
+  // chunk c starts at rank c-1 (:313-318) and moves leftward, each rank
+  // computing op(its value, partial) (:286-297), ending at rank c
+  auto chain = [&](int c) {
+    std::vector<int> v;
+    for (int k = 1; k <= size; k++) v.push_back((c - k + 2 * size) % size);
+    return v;
+  };
+  return meshPlan(rank, size, range, chain);
+}
+
+// ---------------------------------------------------------------------------
+// gloo::allreduce(opts), Algorithm::BCUBE (gloo/allreduce.cc:395-669)
+// ---------------------------------------------------------------------------
+namespace {
+
+struct BcubeGroup {
+  int64_t bufferOffset = 0, bufferLength = 0, chunkLength = 0;
+  int64_t myChunkOffset = 0, myChunkLength = 0;
+  int groupRank = 0;
+  std::vector<int> ranks;
+  int64_t slot = 0;    // receive slot size (elements) for one member
+  int64_t rsBase = 0;  // receive regions of this step: member i at base + i * slot
+  int64_t agBase = 0;
+
+  int64_t len(int i) const {  // :545-550
+    return std::min(chunkLength, std::max<int64_t>(0, bufferLength - i * chunkLength));
+  }
+};
+
+struct BcubeGeom {
+  std::vector<BcubeGroup> groups;
+  int64_t scratch = 0;
+
+  BcubeGeom(int rank, int size, int64_t count) {
+    // computeGroupSizePerStep(size, 2), :398-409
+    std::vector<int64_t> sizes;
+    int64_t rest = size;
+    while (rest % 2 == 0) {
+      sizes.push_back(2);
+      rest /= 2;
+    }
+    if (rest > 1) sizes.push_back(rest);
+    int64_t peerDistance = 1, bufferOffset = 0, bufferLength = count;
+    for (int64_t gs : sizes) {  // :466-511
+      BcubeGroup g;
+      g.groupRank = (int)((rank / peerDistance) % gs);
+      const int64_t base = rank - g.groupRank * peerDistance;
+      for (int64_t i = 0; i < gs; i++) g.ranks.push_back((int)(base + i * peerDistance));
+      g.bufferOffset = bufferOffset;
+      g.bufferLength = bufferLength;
+      g.chunkLength = (bufferLength + gs - 1) / gs;
+      g.myChunkOffset = bufferOffset + g.groupRank * g.chunkLength;
+      g.myChunkLength = g.len(g.groupRank);
+      groups.push_back(g);
+      peerDistance *= gs;
+      bufferOffset = g.myChunkOffset;
+      bufferLength = g.myChunkLength;
+    }
+    int64_t at = 0;
+    for (auto& g : groups) {
+      g.slot = g.chunkLength + kPadElems;
+      g.rsBase = at;
+      at += (int64_t)g.ranks.size() * g.slot;
+      g.agBase = at;
+      at += (int64_t)g.ranks.size() * g.slot;
+    }
+    scratch = at;
+  }
+};
+
+}  // namespace
+
+Plan planFnBcube(int rank, int size, int64_t count) {
+  Plan p;
+  if (count == 0 || size == 1) return p;
+  const BcubeGeom geo(rank, size, count);
+  p.scratch_elems = geo.scratch;
+  std::vector<BcubeGeom> peerGeo;  // receivers' region layouts
+  peerGeo.reserve((size_t)size);
+  for (int r = 0; r < size; r++) peerGeo.emplace_back(r, size, count);
+  const size_t nsteps = geo.groups.size();
+  // reduce/scatter (:520-597)
+  for (size_t s = 0; s < nsteps; s++) {
+    const BcubeGroup& g = geo.groups[s];
+    for (size_t i = 0; i < g.ranks.size(); i++) {  // :534-556
+      const int dst = g.ranks[i];
+      if (dst == rank) continue;
+      const int64_t len = g.len((int)i);
+      if (len == 0) continue;  // the peer's receive is empty too
+      const BcubeGroup& pg = peerGeo[(size_t)dst].groups[s];
+      p.steps.push_back({SEND, dst, 0, g.bufferOffset + (int64_t)i * g.chunkLength, len, 0,
+                         pg.rsBase + (int64_t)g.groupRank * pg.slot, 0});
+      p.bytes_sent += len;
+    }
+    if (g.myChunkLength == 0) continue;
+    std::vector<int64_t> srcs{-1};
+    for (size_t i = 0; i < g.ranks.size(); i++) {  // :521-532
+      const int src = g.ranks[i];
+      if (src == rank) continue;
+      const int64_t region = g.rsBase + (int64_t)i * g.slot;
+      p.steps.push_back({RECV, src, 0, 0, g.myChunkLength, region, 0, 0});
+      srcs.push_back(region);
+    }
+    // out = op(out, tmp[i]) for the peers in group order (:580-596)
+    if (srcs.size() == 2) {
+      p.steps.push_back({REDUCE, 0, 0, g.myChunkOffset, g.myChunkLength, srcs[1], 0, 0});
+    } else {
+      p.folds.push_back(srcs);
+      p.steps.push_back({FOLD, -1, (int64_t)srcs.size(), g.myChunkOffset, g.myChunkLength,
+                         (int64_t)p.folds.size() - 1, 0, kFoldLeft});
+    }
+    for (size_t i = 0; i < g.ranks.size(); i++) {
+      if (g.ranks[i] != rank) p.steps.push_back({RELEASE, g.ranks[i], 0, 0, 0, 0, 0, 0});
+    }
+  }
+  // allgather, groups in reverse (:606-669)
+  for (size_t s = nsteps; s-- > 0;) {
+    const BcubeGroup& g = geo.groups[s];
+    if (g.myChunkLength > 0) {
+      for (size_t i = 0; i < g.ranks.size(); i++) {
+        const int dst = g.ranks[i];
+        if (dst == rank) continue;
+        const BcubeGroup& pg = peerGeo[(size_t)dst].groups[s];
+        p.steps.push_back({SEND, dst, 1, g.myChunkOffset, g.myChunkLength, 0,
+                           pg.agBase + (int64_t)g.groupRank * pg.slot, 0});
+        p.bytes_sent += g.myChunkLength;
+      }
+    }
+    for (size_t i = 0; i < g.ranks.size(); i++) {
+      const int src = g.ranks[i];
+      if (src == rank) continue;
+      const int64_t len = g.len((int)i);
+      if (len == 0) continue;
+      const int64_t region = g.agBase + (int64_t)i * g.slot;
+      p.steps.push_back({RECV, src, 1, 0, len, region, 0, 0});
+      p.steps.push_back({COPY, 0, 0, g.bufferOffset + (int64_t)i * g.chunkLength, len, region, 0});
+      p.steps.push_back({RELEASE, src, 1, 0, 0, 0, 0, 0});
+    }
+  }
+  return p;
+}
+
+Plan makePlan(int algo, int rank, int size, int64_t count, const PlanParams& prm) {
   if (size < 1 || rank < 0 || rank >= size || count < 0) fail("bad geometry");
-  if (algo == ALGO_RING_CHUNKED) return planRingChunked(rank, size, count);
-  if (algo == ALGO_HALVING_DOUBLING) return planHalvingDoubling(rank, size, count);
-  if (algo == ALGO_RING_CHUNKED_MESH) return planRingChunkedMesh(rank, size, count);
+  switch (algo) {
+    case ALGO_RING_CHUNKED: return planRingChunked(rank, size, count);
+    case ALGO_HALVING_DOUBLING: return planHalvingDoubling(rank, size, count);
+    case ALGO_RING_CHUNKED_MESH: return planRingChunkedMesh(rank, size, count);
+    case ALGO_FN_RING: return planFnRing(rank, size, count, prm);
+    case ALGO_FN_RING_MESH: return planFnRingMesh(rank, size, count, prm);
+    case ALGO_FN_BCUBE: return planFnBcube(rank, size, count);
+  }
   fail("unknown algorithm");
   return Plan();
 }

@@ -14,10 +14,12 @@
 //   RELEASE the last message of (peer, channel) is consumed: once the GPU
 //           work reading it completes, credit the sender.
 //   FOLD    ptr0[off, off+len) = op(s[k-1], ... op(s[2], op(s[1], s[0]))),
-//           s[0] = ptr0[off, off+len) and s[i] = region(folds[boff][i]) --
-//           the ring's per-chunk reduction chain evaluated in one pass (the
-//           operand order of every op is the ring's: the newer rank's value
-//           first, the running partial second).
+//           s[i] = region(folds[boff][i]), or ptr0[off, off+len) itself for
+//           an entry of -1 -- a ring's per-chunk reduction chain evaluated in
+//           one pass (the operand order of every op is the ring's: the newer
+//           rank's value first, the running partial second).  With flags &
+//           kFoldLeft the order is the left fold op(...op(op(s0, s1), s2)...),
+//           i.e. bcube's "out = op(out, peer)" for peers in group order.
 //
 // Region offsets are in elements; each region is padded by kPadElems so a
 // message can land at the 16-byte phase of the receiver's ptr0 (keeps the
@@ -49,7 +51,30 @@ struct Plan {
   int64_t bytes_sent = 0;     // payload bytes this rank sends per run (for metrics)
 };
 
-enum Algo { ALGO_RING_CHUNKED = 0, ALGO_HALVING_DOUBLING = 1, ALGO_RING_CHUNKED_MESH = 2 };
+enum Algo {
+  ALGO_RING_CHUNKED = 0,       // class AllreduceRingChunked
+  ALGO_HALVING_DOUBLING = 1,   // class AllreduceHalvingDoubling
+  ALGO_RING_CHUNKED_MESH = 2,  // ring_chunked's result over all links
+  ALGO_FN_RING = 3,            // gloo::allreduce(opts), Algorithm::RING
+  ALGO_FN_RING_MESH = 4,       // its result over all links
+  ALGO_FN_BCUBE = 5,           // gloo::allreduce(opts), Algorithm::BCUBE
+};
+
+constexpr int64_t kFoldLeft = 1;  // FOLD flag, see above
+
+// gloo/allreduce.h:80 (AllreduceOptionsImpl::kMaxSegmentSize)
+constexpr int64_t kMaxSegmentBytes = 1 << 20;
+
+// Inputs of the function-style schedules besides (rank, size, count).
+struct PlanParams {
+  int esize = 4;                                // bytes per element
+  int64_t maxSegmentBytes = kMaxSegmentBytes;   // opts.maxSegmentSize
+  // Device pipelining granularity of the function-style ring: a chunk's
+  // segments are moved in pieces of at least this many bytes (results are
+  // unchanged: they depend only on which rank owns which element, which
+  // maxSegmentBytes fixes exactly as the reference does).
+  int64_t minPieceBytes = 4 << 20;
+};
 
 // Region padding: room to land a message at any 16-byte phase after
 // rounding its region base up to 16 bytes (<= 30 bytes for 1-byte elements).
@@ -65,6 +90,16 @@ Plan planHalvingDoubling(int rank, int size, int64_t count);
 // xGMI link per peer), then sends the result to everyone.
 Plan planRingChunkedMesh(int rank, int size, int64_t count);
 
-Plan makePlan(int algo, int rank, int size, int64_t count);
+// gloo/allreduce.cc:148-393 (ring) with the reference's segment ownership;
+// pieces of >= minPieceBytes move two at a time per direction.
+Plan planFnRing(int rank, int size, int64_t count, const PlanParams& prm);
+// The same chunks and reduction chains, each owner folding its chunk from
+// all peers at once.
+Plan planFnRingMesh(int rank, int size, int64_t count, const PlanParams& prm);
+// gloo/allreduce.cc:395-669 (bcube, n = 2)
+Plan planFnBcube(int rank, int size, int64_t count);
+
+Plan makePlan(int algo, int rank, int size, int64_t count,
+              const PlanParams& prm = PlanParams());
 
 }  // namespace glx

@@ -10,6 +10,7 @@
 //                                      (gloo/cuda_allreduce_ring_chunked.h:22-26)
 //   gloo::CudaAllreduceHalvingDoubling<T>(ctx, ptrs, count, streams)
 //                                      (gloo/cuda_allreduce_halving_doubling.h:25-30)
+//   gloo::AllreduceOptions + gloo::allreduce(opts)          (gloo/allreduce.h:89-195)
 //   gloo::EnforceNotMet, gloo::IoException                  (gloo/common/logging.h:21,
 //                                                            gloo/common/error.h:45)
 // become gloo_amd::<same name> (device algorithms: HipAllreduceRingChunked<T>,
@@ -281,6 +282,149 @@ void max(T* c, const T* a, const T* b, size_t n, glx_stream_t stream = nullptr) 
 template <typename T>
 void min(T* c, const T* a, const T* b, size_t n, glx_stream_t stream = nullptr) {
   check(glx_reduce(GLX_MIN, DType<T>::value, c, a, b, n, stream), "min");
+}
+
+// gloo::sum<T>(void*, const void*, const void*, size_t) and friends with the
+// reference's untyped signature (gloo/math.h:15-73), on device pointers:
+// these are what AllreduceOptions::setReduceFunction recognises.
+template <typename T>
+void sum(void* c, const void* a, const void* b, size_t n) {
+  check(glx_reduce(GLX_SUM, DType<T>::value, c, a, b, n, nullptr), "sum");
+}
+template <typename T>
+void product(void* c, const void* a, const void* b, size_t n) {
+  check(glx_reduce(GLX_PRODUCT, DType<T>::value, c, a, b, n, nullptr), "product");
+}
+template <typename T>
+void max(void* c, const void* a, const void* b, size_t n) {
+  check(glx_reduce(GLX_MAX, DType<T>::value, c, a, b, n, nullptr), "max");
+}
+template <typename T>
+void min(void* c, const void* a, const void* b, size_t n) {
+  check(glx_reduce(GLX_MIN, DType<T>::value, c, a, b, n, nullptr), "min");
+}
+
+// gloo::AllreduceOptions (gloo/allreduce.h:89-193) for device buffers.  The
+// reduction is one of the gloo/math.h ops: pass &gloo_amd::sum<T> (the
+// reference's idiom, allreduce_test.cc:380-383), a ReductionFunction<T>, or a
+// ReductionType.  setStream() is an addition: without it allreduce() returns
+// with the outputs complete, like the reference.
+class AllreduceOptions {
+ public:
+  using Func = void (*)(void*, const void*, const void*, size_t);
+  enum Algorithm {
+    UNSPECIFIED = GLX_ALLREDUCE_UNSPECIFIED,
+    RING = GLX_ALLREDUCE_RING,
+    BCUBE = GLX_ALLREDUCE_BCUBE,
+    RING_MESH = GLX_ALLREDUCE_RING_MESH,  // RING's result over all links
+  };
+
+  explicit AllreduceOptions(const std::shared_ptr<Context>& context) : context_(context) {}
+
+  void setAlgorithm(Algorithm algorithm) { algorithm_ = algorithm; }
+
+  template <typename T>
+  void setInput(T* ptr, size_t elements) {
+    setInputs(&ptr, 1, elements);
+  }
+  template <typename T>
+  void setInputs(std::vector<T*> ptrs, size_t elements) {
+    setInputs(ptrs.data(), ptrs.size(), elements);
+  }
+  template <typename T>
+  void setInputs(T** ptrs, size_t len, size_t elements) {
+    setType<T>(elements);
+    in_.assign(ptrs, ptrs + len);
+  }
+  template <typename T>
+  void setOutput(T* ptr, size_t elements) {
+    setOutputs(&ptr, 1, elements);
+  }
+  template <typename T>
+  void setOutputs(std::vector<T*> ptrs, size_t elements) {
+    setOutputs(ptrs.data(), ptrs.size(), elements);
+  }
+  template <typename T>
+  void setOutputs(T** ptrs, size_t len, size_t elements) {
+    setType<T>(elements);
+    out_.assign(ptrs, ptrs + len);
+  }
+
+  void setReduceFunction(Func fn) {
+    fn_ = fn;
+    op_ = -1;
+  }
+  void setReduceFunction(ReductionType t) {
+    op_ = t;
+    fn_ = nullptr;
+  }
+  template <typename T>
+  void setReduceFunction(const ReductionFunction<T>* fn) {
+    setReduceFunction(fn->type());
+  }
+  void setTag(uint32_t tag) { tag_ = tag; }
+  void setMaxSegmentSize(size_t maxSegmentSize) { maxSegmentSize_ = maxSegmentSize; }
+  void setTimeout(std::chrono::milliseconds timeout) { timeout_ = timeout; }
+  void setStream(glx_stream_t stream) { stream_ = stream; }
+
+ private:
+  template <typename T>
+  void setType(size_t elements) {
+    dtype_ = DType<T>::value;
+    elements_ = elements;
+  }
+  template <typename T>
+  static int opOf(Func f) {
+    if (f == static_cast<Func>(&sum<T>)) return GLX_SUM;
+    if (f == static_cast<Func>(&product<T>)) return GLX_PRODUCT;
+    if (f == static_cast<Func>(&max<T>)) return GLX_MAX;
+    if (f == static_cast<Func>(&min<T>)) return GLX_MIN;
+    return -1;
+  }
+  int resolveOp() const {
+    if (fn_ == nullptr) return op_ < 0 ? GLX_SUM : op_;
+    switch (dtype_) {
+      case GLX_INT8: return opOf<int8_t>(fn_);
+      case GLX_UINT8: return opOf<uint8_t>(fn_);
+      case GLX_INT32: return opOf<int32_t>(fn_);
+      case GLX_INT64: return opOf<int64_t>(fn_);
+      case GLX_UINT64: return opOf<uint64_t>(fn_);
+      case GLX_FLOAT32: return opOf<float>(fn_);
+      case GLX_FLOAT64: return opOf<double>(fn_);
+      case GLX_FLOAT16: return opOf<float16>(fn_);
+      case GLX_BFLOAT16: return opOf<bfloat16>(fn_);
+    }
+    return -1;
+  }
+
+  std::shared_ptr<Context> context_;
+  int algorithm_ = UNSPECIFIED;
+  std::vector<void*> in_, out_;
+  size_t elements_ = 0;
+  int dtype_ = -1;
+  Func fn_ = nullptr;
+  int op_ = -1;
+  uint32_t tag_ = 0;
+  size_t maxSegmentSize_ = 0;
+  std::chrono::milliseconds timeout_{0};
+  glx_stream_t stream_ = nullptr;
+
+  friend void allreduce(const AllreduceOptions& opts);
+};
+
+// gloo::allreduce (gloo/allreduce.h:195, gloo/allreduce.cc:97-146)
+inline void allreduce(const AllreduceOptions& opts) {
+  const int op = opts.resolveOp();
+  if (op < 0) {
+    throw EnforceNotMet(
+        "allreduce: only the gloo/math.h reductions (sum, product, max, min of the "
+        "buffers' type) run on the device");
+  }
+  check(glx_allreduce(opts.context_->handle(), opts.algorithm_, opts.dtype_, op,
+                      opts.in_.data(), (int)opts.in_.size(), opts.out_.data(),
+                      (int)opts.out_.size(), opts.elements_, opts.tag_, opts.maxSegmentSize_,
+                      (int64_t)opts.timeout_.count(), opts.stream_),
+        "allreduce");
 }
 
 }  // namespace gloo_amd

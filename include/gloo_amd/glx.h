@@ -191,11 +191,50 @@ glx_algorithm* glx_allreduce_halving_doubling_create(
 enum glx_algo {
   GLX_ALGO_RING_CHUNKED = 0,
   GLX_ALGO_HALVING_DOUBLING = 1,
-  GLX_ALGO_RING_CHUNKED_MESH = 2
+  GLX_ALGO_RING_CHUNKED_MESH = 2,
+  /* schedules of glx_allreduce (plan introspection only) */
+  GLX_ALGO_FN_RING = 3,
+  GLX_ALGO_FN_RING_MESH = 4,
+  GLX_ALGO_FN_BCUBE = 5
 };
 glx_algorithm* glx_allreduce_create(glx_context* ctx, int algo, void* const* ptrs,
                                     int nptrs, int count, int dtype, int op,
                                     const glx_stream_t* streams, int nstreams);
+
+/* ---- function-style collective ---------------------------------------- */
+/* gloo::AllreduceOptions::Algorithm (gloo/allreduce.h:38-42), plus
+ * GLX_ALLREDUCE_RING_MESH: RING's exact result (same chunk ownership, same
+ * reduction chain and operand order) with every owner folding its chunk from
+ * all peers at once over all xGMI links. */
+enum glx_allreduce_algorithm {
+  GLX_ALLREDUCE_UNSPECIFIED = 0,
+  GLX_ALLREDUCE_RING = 1,
+  GLX_ALLREDUCE_BCUBE = 2,
+  GLX_ALLREDUCE_RING_MESH = 3
+};
+/* gloo::allreduce(const AllreduceOptions&) (gloo/allreduce.cc:97-146,
+ * gloo/allreduce.h:89-193) on device buffers.  The reduce function is one of
+ * the gloo/math.h templates for `dtype`, selected by `op` (the device cannot
+ * run a host std::function).
+ *   inputs/num_inputs   opts.setInputs (may be 0: out[0] is the input and
+ *                       out[1..] are folded into it)
+ *   outputs/num_outputs opts.setOutputs (>= 1; all get the result)
+ *   elements            element count of every buffer
+ *   tag                 opts.setTag: concurrent operations need distinct tags
+ *   max_segment_size    opts.setMaxSegmentSize in bytes (0: 1 MiB default);
+ *                       it fixes which rank reduces which elements, hence
+ *                       the result bits, exactly as in the reference
+ *   timeout_ms          opts.setTimeout (<= 0: the context's timeout)
+ *   stream              NULL: the call returns with the outputs complete;
+ *                       else the work is ordered on `stream`.
+ * Every rank calls with the same algorithm/dtype/op/elements/tag/
+ * max_segment_size.  The first call with a given combination sets up and
+ * exchanges receive buffers with the peers (once; later calls reuse them).
+ * UNSPECIFIED means RING, or RING_MESH with GLOO_AMD_ALLREDUCE_SCHEDULE=mesh. */
+int glx_allreduce(glx_context* ctx, int algorithm, int dtype, int op,
+                  void* const* inputs, int num_inputs, void* const* outputs,
+                  int num_outputs, size_t elements, uint32_t tag,
+                  size_t max_segment_size, int64_t timeout_ms, glx_stream_t stream);
 
 /* Algorithm::run() (gloo/algorithm.h:26). */
 int glx_algorithm_run(glx_algorithm* alg);
@@ -215,6 +254,15 @@ int64_t glx_plan(int algo, int rank, int size, int64_t count, int64_t* steps,
  * the rank's own buffer.  Returns the count (writes at most cap) or -1. */
 int64_t glx_plan_fold(int algo, int rank, int size, int64_t count, int64_t fold,
                       int64_t* srcs, int64_t cap);
+/* The same for the function-style schedules, whose geometry also depends on
+ * the element size, opts.maxSegmentSize (0: default) and the device piece
+ * size of the ring (min_piece_bytes; 0: the reference's own segments). */
+int64_t glx_plan_ex(int algo, int rank, int size, int64_t count, int esize,
+                    int64_t max_segment_bytes, int64_t min_piece_bytes, int64_t* steps,
+                    int64_t cap, int64_t* scratch_elems);
+int64_t glx_plan_fold_ex(int algo, int rank, int size, int64_t count, int esize,
+                         int64_t max_segment_bytes, int64_t min_piece_bytes, int64_t fold,
+                         int64_t* srcs, int64_t cap);
 
 #ifdef __cplusplus
 }  /* extern "C" */

@@ -309,7 +309,9 @@ void oracle_fill(int dtype, int kind, uint64_t seed, int rank, int ptr_index,
 /* Message-passing simulator for the collectives.                     */
 /* ------------------------------------------------------------------ */
 
-enum { ST_SEND = 0, ST_RECV, ST_REDUCE, ST_COPY };
+enum { ST_SEND = 0, ST_RECV, ST_REDUCE, ST_COPY, ST_LOCAL, ST_BCAST };
+/* ST_LOCAL / ST_BCAST (function-style allreduce only): the reference's
+ * reduceInputs / broadcastOutputs for [off, off+len) of this rank. */
 
 typedef struct {
   int kind;
@@ -373,10 +375,23 @@ static chan_t* chan_get(chans_t* cs, int src, int dst, int tag) {
   return &cs->v[cs->n++];
 }
 
+/* Per-rank input/output buffers of the function-style allreduce. */
+typedef struct {
+  int nin, nout;
+  void** ins;  /* ins[r * nin + i] */
+  void** outs; /* outs[r * nout + i] */
+} fnbufs_t;
+
+static void fn_local_reduce(const fnbufs_t* fb, int r, int op, int dtype,
+                            size_t off, size_t len);
+static void fn_local_broadcast(const fnbufs_t* fb, int r, int dtype, size_t off,
+                               size_t len);
+
 /* Run P programs to completion.  data[r] = rank r's ptr0; scratch[r] = its
  * receive buffers.  Returns 0, or -2 on deadlock, -3 on length overflow. */
-static int simulate(int P, prog_t* progs, int op, int dtype, unsigned char** data,
-                    unsigned char** scratch, size_t* scratch_elems) {
+static int simulate_fn(int P, prog_t* progs, int op, int dtype, unsigned char** data,
+                       unsigned char** scratch, size_t* scratch_elems,
+                       const fnbufs_t* fb) {
   size_t es = kSize[dtype];
   size_t* pc = (size_t*)calloc((size_t)P, sizeof(size_t));
   chans_t cs = {0};
@@ -411,6 +426,10 @@ static int simulate(int P, prog_t* progs, int op, int dtype, unsigned char** dat
         } else if (s->kind == ST_REDUCE) {
           unsigned char* d = data[r] + s->off * es;
           oracle_reduce(op, dtype, d, d, scratch[r] + s->boff * es, s->len);
+        } else if (s->kind == ST_LOCAL) {
+          fn_local_reduce(fb, r, op, dtype, s->off, s->len);
+        } else if (s->kind == ST_BCAST) {
+          fn_local_broadcast(fb, r, dtype, s->off, s->len);
         } else { /* ST_COPY */
           memcpy(data[r] + s->off * es, scratch[r] + s->boff * es, s->len * es);
         }
@@ -438,6 +457,11 @@ out:
   }
   free(pc);
   return rc;
+}
+
+static int simulate(int P, prog_t* progs, int op, int dtype, unsigned char** data,
+                    unsigned char** scratch, size_t* scratch_elems) {
+  return simulate_fn(P, progs, op, dtype, data, scratch, scratch_elems, NULL);
 }
 
 static void local_reduce_and(int P, int nptrs, int op, int dtype, size_t count,
@@ -780,6 +804,251 @@ int oracle_allreduce_halving_doubling(int op, int dtype, int P, int nptrs,
   }
   rc = simulate(P, progs, op, dtype, data, scratch, scratch_elems);
   if (rc == 0) local_broadcast(P, nptrs, dtype, (size_t)count, bufs); /* :344-346 */
+done:
+  if (progs) for (r = 0; r < P; r++) free(progs[r].v);
+  if (scratch) for (r = 0; r < P; r++) free(scratch[r]);
+  free(progs);
+  free(data);
+  free(scratch);
+  free(scratch_elems);
+  return rc;
+}
+
+/* ---- gloo::allreduce(opts) (gloo/allreduce.cc) --------------------- */
+
+/* genLocalReduceFunction (:44-82): the local reduction of [off, off+len)
+ * into out[0]. */
+static void fn_local_reduce(const fnbufs_t* fb, int r, int op, int dtype,
+                            size_t off, size_t len) {
+  size_t es = kSize[dtype], b = off * es;
+  unsigned char* out0 = (unsigned char*)fb->outs[(size_t)r * fb->nout] + b;
+  int i;
+  if (fb->nin == 1) {
+    memmove(out0, (unsigned char*)fb->ins[(size_t)r * fb->nin] + b, len * es);
+  } else if (fb->nin >= 2) {
+    oracle_reduce(op, dtype, out0, (unsigned char*)fb->ins[(size_t)r * fb->nin] + b,
+                  (unsigned char*)fb->ins[(size_t)r * fb->nin + 1] + b, len);
+    for (i = 2; i < fb->nin; i++)
+      oracle_reduce(op, dtype, out0, out0,
+                    (unsigned char*)fb->ins[(size_t)r * fb->nin + i] + b, len);
+  } else {
+    for (i = 1; i < fb->nout; i++)
+      oracle_reduce(op, dtype, out0, out0,
+                    (unsigned char*)fb->outs[(size_t)r * fb->nout + i] + b, len);
+  }
+}
+
+/* genLocalBroadcastFunction (:87-95) */
+static void fn_local_broadcast(const fnbufs_t* fb, int r, int dtype, size_t off,
+                               size_t len) {
+  size_t es = kSize[dtype], b = off * es;
+  unsigned char* out0 = (unsigned char*)fb->outs[(size_t)r * fb->nout] + b;
+  int i;
+  for (i = 1; i < fb->nout; i++)
+    memcpy((unsigned char*)fb->outs[(size_t)r * fb->nout + i] + b, out0, len * es);
+}
+
+static void push(prog_t* p, int kind, int peer, size_t off, size_t len, size_t boff) {
+  step_t s;
+  s.kind = kind;
+  s.peer = peer;
+  s.tag = 0; /* one slot per operation: messages of a pair match in order */
+  s.off = off;
+  s.len = len;
+  s.boff = boff;
+  prog_push(p, s);
+}
+
+/* ring (:148-393).  Byte offsets of the reference become element offsets:
+ * segmentBytes is a multiple of the element size (:218-219). */
+static void fn_ring_prog(int r, int P, size_t count, size_t es, size_t max_seg,
+                         prog_t* p, size_t* scratch_elems) {
+  size_t total = count * es;
+  size_t max_seg_bytes = es * (max_seg / es > 0 ? max_seg / es : 1);    /* :193-194 */
+  size_t nseg = (total + max_seg_bytes - 1) / max_seg_bytes;             /* :210-214 */
+  size_t spr, seg_bytes, seg, iters, i;
+  int recv_rank = (P + r + 1) % P, send_rank = (P + r - 1) % P;          /* :158-159 */
+  if (nseg < (size_t)P * 2) nseg = (size_t)P * 2;
+  nseg = (nseg + (size_t)P - 1) / (size_t)P * (size_t)P;
+  spr = nseg / (size_t)P;
+  seg_bytes = (total + nseg - 1) / nseg;                                 /* :217-218 */
+  seg_bytes = (seg_bytes + es - 1) / es * es;
+  seg = seg_bytes / es;
+  *scratch_elems = 2 * seg;                                              /* :221-225 */
+  iters = nseg - spr + 2;
+#define SEG_OFF(k) ((((k) % nseg) * seg))
+#define SEG_LEN(o) ((o) >= count ? 0 : ((count - (o)) < seg ? (count - (o)) : seg))
+  for (i = 0; i < iters; i++) {                                          /* :279-322 */
+    if (i >= 2) {
+      size_t k = i - 2;
+      size_t ro = SEG_OFF(((size_t)r + 2) * spr + k), rl = SEG_LEN(ro);  /* :252-254 */
+      if (rl > 0) {
+        push(p, ST_LOCAL, 0, ro, rl, 0);                                 /* :288 */
+        push(p, ST_RECV, recv_rank, 0, rl, (i & 1) * seg);               /* :290 */
+        push(p, ST_REDUCE, 0, ro, rl, (i & 1) * seg);                    /* :292-296 */
+      }
+    }
+    if (i < nseg - spr) {
+      size_t so = SEG_OFF(((size_t)r + 1) * spr + i), sl = SEG_LEN(so);  /* :249-251 */
+      if (sl > 0) {
+        if (i < spr) push(p, ST_LOCAL, 0, so, sl, 0);                    /* :314-316 */
+        push(p, ST_SEND, send_rank, so, sl, 0);                          /* :318 */
+      }
+    }
+  }
+  for (i = 0; i < iters; i++) {                                          /* :362-392 */
+    if (i >= 2) {
+      size_t k = i - 2;
+      size_t ro = SEG_OFF(((size_t)r + 1) * spr + k), rl = SEG_LEN(ro);  /* :336-338 */
+      if (rl > 0) {
+        push(p, ST_RECV, recv_rank, 0, rl, 0);                           /* :366 */
+        push(p, ST_COPY, 0, ro, rl, 0);       /* the reference receives in place */
+        push(p, ST_BCAST, 0, ro, rl, 0);                                 /* :368 */
+      }
+    }
+    if (i < nseg - spr) {
+      size_t so = SEG_OFF((size_t)r * spr + i), sl = SEG_LEN(so);        /* :333-335 */
+      if (sl > 0) {
+        push(p, ST_SEND, send_rank, so, sl, 0);                          /* :385 */
+        if (i < spr) push(p, ST_BCAST, 0, so, sl, 0);                    /* :387-389 */
+      }
+    }
+  }
+#undef SEG_OFF
+#undef SEG_LEN
+}
+
+/* bcube with n = 2 (:395-669) */
+typedef struct {
+  size_t buffer_offset, buffer_length, chunk_length, my_off, my_len;
+  int group_rank, nranks;
+  int ranks[64];
+} bgroup_t;
+
+static size_t bgroup_len(const bgroup_t* g, int i) { /* :545-550 */
+  long rest = (long)g->buffer_length - (long)((size_t)i * g->chunk_length);
+  if (rest < 0) rest = 0;
+  return (size_t)rest < g->chunk_length ? (size_t)rest : g->chunk_length;
+}
+
+static int bcube_groups(int r, int P, size_t count, bgroup_t* gs) {
+  int sizes[64], ns = 0, s, i;
+  size_t rest = (size_t)P, dist = 1, boff = 0, blen = count;
+  while (rest % 2 == 0) { sizes[ns++] = 2; rest /= 2; }                  /* :398-409 */
+  if (rest > 1) sizes[ns++] = (int)rest;
+  for (s = 0; s < ns; s++) {                                             /* :466-511 */
+    bgroup_t* g = &gs[s];
+    size_t gsz = (size_t)sizes[s];
+    size_t group_rank = ((size_t)r / dist) % gsz;
+    size_t base = (size_t)r - group_rank * dist;
+    if (gsz > 64) return -1;
+    g->group_rank = (int)group_rank;
+    g->nranks = (int)gsz;
+    for (i = 0; i < (int)gsz; i++) g->ranks[i] = (int)(base + (size_t)i * dist);
+    g->buffer_offset = boff;
+    g->buffer_length = blen;
+    g->chunk_length = (blen + gsz - 1) / gsz;
+    g->my_off = boff + group_rank * g->chunk_length;
+    g->my_len = bgroup_len(g, (int)group_rank);
+    dist *= gsz;
+    boff = g->my_off;
+    blen = g->my_len;
+  }
+  return ns;
+}
+
+static int fn_bcube_prog(int r, int P, size_t count, prog_t* p, size_t* scratch_elems) {
+  bgroup_t gs[64];
+  int ns = bcube_groups(r, P, count, gs), s, i;
+  size_t need = count;
+  if (ns < 0) return -1;
+  for (s = 0; s < ns; s++) {                                             /* :503-509 */
+    size_t v = (size_t)gs[s].nranks * gs[s].chunk_length;
+    if (v > need) need = v;
+  }
+  *scratch_elems = need;
+  for (s = 0; s < ns; s++) {                                             /* :520-597 */
+    const bgroup_t* g = &gs[s];
+    for (i = 0; i < g->nranks; i++) {                                    /* :534-556 */
+      size_t off = g->buffer_offset + (size_t)i * g->chunk_length, len = bgroup_len(g, i);
+      if (g->ranks[i] == r) continue;
+      if (s == 0) push(p, ST_LOCAL, 0, off, len, 0);
+      push(p, ST_SEND, g->ranks[i], off, len, 0);
+    }
+    for (i = 0; i < g->nranks; i++) {                                    /* :521-532 */
+      if (g->ranks[i] == r) continue;
+      push(p, ST_RECV, g->ranks[i], 0, g->my_len, (size_t)i * g->chunk_length);
+    }
+    if (s == 0) push(p, ST_LOCAL, 0, g->my_off, g->my_len, 0);            /* :575-578 */
+    for (i = 0; i < g->nranks; i++) {                                    /* :580-596 */
+      if (g->ranks[i] == r) continue;
+      push(p, ST_REDUCE, 0, g->my_off, g->my_len, (size_t)i * g->chunk_length);
+    }
+  }
+  push(p, ST_BCAST, 0, gs[ns - 1].my_off, gs[ns - 1].my_len, 0);          /* :599-605 */
+  for (s = ns - 1; s >= 0; s--) {                                        /* :606-669 */
+    const bgroup_t* g = &gs[s];
+    for (i = 0; i < g->nranks; i++) {
+      if (g->ranks[i] == r) continue;
+      push(p, ST_SEND, g->ranks[i], g->my_off, g->my_len, 0);
+    }
+    for (i = 0; i < g->nranks; i++) {
+      size_t off = g->buffer_offset + (size_t)i * g->chunk_length, len = bgroup_len(g, i);
+      if (g->ranks[i] == r) continue;
+      push(p, ST_RECV, g->ranks[i], 0, len, 0);
+      push(p, ST_COPY, 0, off, len, 0);
+    }
+    for (i = 0; i < g->nranks; i++) {                                    /* :653-667 */
+      size_t off = g->buffer_offset + (size_t)i * g->chunk_length, len = bgroup_len(g, i);
+      if (g->ranks[i] == r) continue;
+      push(p, ST_BCAST, 0, off, len, 0);
+    }
+  }
+  return 0;
+}
+
+/* gloo::allreduce(opts) for P ranks.  algo: 1 = RING (and UNSPECIFIED),
+ * 2 = BCUBE.  ins[r * nin + i], outs[r * nout + i] (nout >= 1); the result
+ * is left in every rank's outputs.  max_seg: opts.maxSegmentSize in bytes
+ * (0: 1 MiB, gloo/allreduce.h:80). */
+int oracle_allreduce_fn(int algo, int op, int dtype, int P, int nin, int nout,
+                        size_t count, size_t max_seg, void** ins, void** outs) {
+  fnbufs_t fb;
+  prog_t* progs = NULL;
+  unsigned char** data = NULL;
+  unsigned char** scratch = NULL;
+  size_t* scratch_elems = NULL;
+  int r, rc = 0;
+  if (P < 1 || nin < 0 || nout < 1 || dtype < 0 || dtype >= OR_NDTYPES) return -1;
+  if (algo != 1 && algo != 2) return -1;
+  if (max_seg == 0) max_seg = 1024 * 1024;
+  fb.nin = nin;
+  fb.nout = nout;
+  fb.ins = ins;
+  fb.outs = outs;
+  if (count == 0) return 0;                                              /* :98-100 */
+  if (P == 1) {                                                          /* :129-133 */
+    fn_local_reduce(&fb, 0, op, dtype, 0, count);
+    fn_local_broadcast(&fb, 0, dtype, 0, count);
+    return 0;
+  }
+  progs = (prog_t*)calloc((size_t)P, sizeof(prog_t));
+  data = (unsigned char**)calloc((size_t)P, sizeof(void*));
+  scratch = (unsigned char**)calloc((size_t)P, sizeof(void*));
+  scratch_elems = (size_t*)calloc((size_t)P, sizeof(size_t));
+  if (!progs || !data || !scratch || !scratch_elems) { rc = -1; goto done; }
+  for (r = 0; r < P; r++) {
+    data[r] = (unsigned char*)outs[(size_t)r * nout];
+    if (algo == 1) {
+      fn_ring_prog(r, P, count, kSize[dtype], max_seg, &progs[r], &scratch_elems[r]);
+    } else if (fn_bcube_prog(r, P, count, &progs[r], &scratch_elems[r]) != 0) {
+      rc = -1;
+      goto done;
+    }
+    scratch[r] = (unsigned char*)calloc(scratch_elems[r] + 1, kSize[dtype]);
+    if (!scratch[r]) { rc = -1; goto done; }
+  }
+  rc = simulate_fn(P, progs, op, dtype, data, scratch, scratch_elems, &fb);
 done:
   if (progs) for (r = 0; r < P; r++) free(progs[r].v);
   if (scratch) for (r = 0; r < P; r++) free(scratch[r]);

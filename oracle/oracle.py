@@ -50,6 +50,9 @@ def _load_oracle():
             f = getattr(lib, name)
             f.argtypes = [i, i, i, i, i, ctypes.POINTER(vp)]
             f.restype = i
+        lib.oracle_allreduce_fn.argtypes = [i, i, i, i, i, i, sz, sz, ctypes.POINTER(vp),
+                                            ctypes.POINTER(vp)]
+        lib.oracle_allreduce_fn.restype = i
         lib.oracle_f32_to_f16.argtypes = [ctypes.c_float]
         lib.oracle_f32_to_f16.restype = ctypes.c_uint16
         lib.oracle_f16_to_f32.argtypes = [ctypes.c_uint16]
@@ -78,6 +81,9 @@ def _load_ref():
         lib.ref_allreduce.argtypes = [i, i, i, i, i, i, ctypes.POINTER(vp), i, i,
                                       ctypes.POINTER(ctypes.c_double)]
         lib.ref_allreduce.restype = i
+        lib.ref_allreduce_fn.argtypes = [i, i, i, i, i, i, sz, sz, ctypes.POINTER(vp),
+                                         ctypes.POINTER(vp)]
+        lib.ref_allreduce_fn.restype = i
         lib.ref_last_error.restype = ctypes.c_char_p
         lib.ref_f32_to_f16.argtypes = [vp, vp, sz]
         lib.ref_f16_to_f32.argtypes = [vp, vp, sz]
@@ -153,6 +159,43 @@ def allreduce(algo, op, dtype, inputs, use_ref=False, warmup=0, iters=1):
         if rc != 0:
             raise RuntimeError("oracle allreduce failed rc=%d" % rc)
     return bufs
+
+
+FN_RING = 1   # AllreduceOptions::Algorithm::RING (gloo/allreduce.h:40)
+FN_BCUBE = 2  # AllreduceOptions::Algorithm::BCUBE
+
+
+def allreduce_fn(algo, op, dtype, inputs, outputs, max_segment_size=0, use_ref=False):
+    """gloo::allreduce(opts) over P ranks (gloo/allreduce.cc:97-146).
+    inputs: per rank a list (maybe empty) of 1-D arrays; outputs: per rank a
+    non-empty list of 1-D arrays holding the outputs' initial contents (they
+    are the input when `inputs` is empty).  Returns new output arrays."""
+    P = len(outputs)
+    nin = len(inputs[0]) if inputs else 0
+    nout = len(outputs[0])
+    count = outputs[0][0].size
+    ins = [[np.array(x, copy=True) for x in (inputs[r] if nin else [])] for r in range(P)]
+    outs = [[np.array(x, copy=True) for x in outputs[r]] for r in range(P)]
+    fin = (ctypes.c_void_p * max(P * nin, 1))()
+    fout = (ctypes.c_void_p * (P * nout))()
+    for r in range(P):
+        for i in range(nin):
+            fin[r * nin + i] = ins[r][i].ctypes.data
+        for i in range(nout):
+            fout[r * nout + i] = outs[r][i].ctypes.data
+    if use_ref:
+        lib = _load_ref()
+        rc = lib.ref_allreduce_fn(algo, op, dtype, P, nin, nout, count, max_segment_size,
+                                  fin, fout)
+        if rc != 0:
+            raise RuntimeError("reference allreduce failed rc=%d: %s"
+                               % (rc, lib.ref_last_error().decode()))
+    else:
+        rc = _load_oracle().oracle_allreduce_fn(algo, op, dtype, P, nin, nout, count,
+                                                max_segment_size, fin, fout)
+        if rc != 0:
+            raise RuntimeError("oracle allreduce failed rc=%d" % rc)
+    return outs
 
 
 def f32_to_f16(x, use_ref=False):

@@ -8,6 +8,7 @@
 //   * gloo::sum/product/max/min<T>            (gloo/math.h:15-73)
 //   * gloo::AllreduceRingChunked<T>           (gloo/allreduce_ring_chunked.h:19)
 //   * gloo::AllreduceHalvingDoubling<T>       (gloo/allreduce_halving_doubling.h:37)
+//   * gloo::allreduce(AllreduceOptions)       (gloo/allreduce.cc:97-146, RING/BCUBE)
 // exactly the way the reference's tests do: P threads in one process, one
 // HashStore, tcp devices on loopback (gloo/test/base_test.h:91-166).
 #include <chrono>
@@ -19,6 +20,7 @@
 #include <thread>
 #include <vector>
 
+#include "gloo/allreduce.h"
 #include "gloo/allreduce_halving_doubling.h"
 #include "gloo/allreduce_ring_chunked.h"
 #include "gloo/math.h"
@@ -107,6 +109,60 @@ int allreduceT(int algo, int op, int P, int nptrs, int count, void** bufs,
   return 0;
 }
 
+template <typename T>
+gloo::AllreduceOptions::Func mathFn(int op) {
+  void (*f)(void*, const void*, const void*, size_t) = nullptr;
+  switch (op) {
+    case R_SUM: f = &gloo::sum<T>; break;
+    case R_PRODUCT: f = &gloo::product<T>; break;
+    case R_MAX: f = &gloo::max<T>; break;
+    case R_MIN: f = &gloo::min<T>; break;
+  }
+  return gloo::AllreduceOptions::Func(f);
+}
+
+// One gloo::allreduce(opts) call on every rank (gloo/test/allreduce_test.cc:
+// 306-356 shows the options the reference's own tests use).
+template <typename T>
+int allreduceFnT(int algo, int op, int P, int nin, int nout, size_t count, size_t maxSeg,
+                 void** ins, void** outs) {
+  if (op < R_SUM || op > R_MIN) return -1;
+  auto store = std::make_shared<gloo::rendezvous::HashStore>();
+  std::vector<std::thread> threads;
+  std::vector<std::string> errors(P);
+  for (int r = 0; r < P; r++) {
+    threads.emplace_back([&, r]() {
+      try {
+        gloo::transport::tcp::attr attr("127.0.0.1");
+        auto dev = gloo::transport::tcp::CreateDevice(attr);
+        auto ctx = std::make_shared<gloo::rendezvous::Context>(r, P);
+        ctx->connectFullMesh(*store, dev);
+        gloo::AllreduceOptions opts(ctx);
+        opts.setAlgorithm(algo == 2 ? gloo::AllreduceOptions::Algorithm::BCUBE
+                                    : gloo::AllreduceOptions::Algorithm::RING);
+        std::vector<T*> in, out;
+        for (int i = 0; i < nin; i++) in.push_back(static_cast<T*>(ins[r * nin + i]));
+        for (int i = 0; i < nout; i++) out.push_back(static_cast<T*>(outs[r * nout + i]));
+        if (nin > 0) opts.setInputs(in, count);
+        opts.setOutputs(out, count);
+        opts.setReduceFunction(mathFn<T>(op));
+        if (maxSeg > 0) opts.setMaxSegmentSize(maxSeg);
+        gloo::allreduce(opts);
+      } catch (const std::exception& e) {
+        errors[r] = e.what();
+      }
+    });
+  }
+  for (auto& t : threads) t.join();
+  for (int r = 0; r < P; r++) {
+    if (!errors[r].empty()) {
+      g_err = "rank " + std::to_string(r) + ": " + errors[r];
+      return -2;
+    }
+  }
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -154,6 +210,23 @@ int ref_allreduce(int algo, int op, int dtype, int P, int nptrs, int count,
     case R_FLOAT32: return allreduceT<float>(algo, op, P, nptrs, count, bufs, warmup, iters, seconds);
     case R_FLOAT64: return allreduceT<double>(algo, op, P, nptrs, count, bufs, warmup, iters, seconds);
     case R_FLOAT16: return allreduceT<gloo::float16>(algo, op, P, nptrs, count, bufs, warmup, iters, seconds);
+  }
+  return -1;
+}
+
+// algo: 1 = Algorithm::RING, 2 = Algorithm::BCUBE.  ins[r * nin + i],
+// outs[r * nout + i]; max_seg 0 = the default segment size.
+int ref_allreduce_fn(int algo, int op, int dtype, int P, int nin, int nout, size_t count,
+                     size_t max_seg, void** ins, void** outs) {
+  switch (dtype) {
+    case R_INT8: return allreduceFnT<int8_t>(algo, op, P, nin, nout, count, max_seg, ins, outs);
+    case R_UINT8: return allreduceFnT<uint8_t>(algo, op, P, nin, nout, count, max_seg, ins, outs);
+    case R_INT32: return allreduceFnT<int32_t>(algo, op, P, nin, nout, count, max_seg, ins, outs);
+    case R_INT64: return allreduceFnT<int64_t>(algo, op, P, nin, nout, count, max_seg, ins, outs);
+    case R_UINT64: return allreduceFnT<uint64_t>(algo, op, P, nin, nout, count, max_seg, ins, outs);
+    case R_FLOAT32: return allreduceFnT<float>(algo, op, P, nin, nout, count, max_seg, ins, outs);
+    case R_FLOAT64: return allreduceFnT<double>(algo, op, P, nin, nout, count, max_seg, ins, outs);
+    case R_FLOAT16: return allreduceFnT<gloo::float16>(algo, op, P, nin, nout, count, max_seg, ins, outs);
   }
   return -1;
 }

@@ -9,6 +9,9 @@
 //                   j*stride^2 + stride(stride-1)/2, rel 1e-4
 //                   (gloo/test/base_test.h:184-235)
 //   MultipleAlgorithms: ring + hd on one context, each run twice (:171-210)
+//   AllreduceNewTest: gloo::allreduce(opts), RING/BCUBE, uint64 sum through
+//                   &sum<uint64_t>, in place or not, maxSegmentSize 128
+//                   (gloo/test/allreduce_test.cc:306-378); TestTimeout (:386-402)
 //
 // Exit status 0 = all passed.  Needs a GPU (all ranks share device 0).
 #include <hip/hip_runtime_api.h>
@@ -179,6 +182,79 @@ void timeoutThrowsIoException() {
   hipFree(dev);
 }
 
+// gloo/test/allreduce_test.cc:306-356 on device buffers
+void allreduceNew(gloo_amd::AllreduceOptions::Algorithm algorithm, const char* name, int P,
+                  int nptrs, int N, bool inPlace) {
+  spawn(P, [&](std::shared_ptr<gloo_amd::Context> ctx) {
+    const uint64_t stride = (uint64_t)P * nptrs;
+    auto make = [&](bool values) {
+      std::vector<uint64_t*> v(nptrs);
+      for (int i = 0; i < nptrs; i++) {
+        std::vector<uint64_t> host(std::max(N, 1), 0);
+        if (values) {
+          for (int j = 0; j < N; j++) host[j] = j * stride + (uint64_t)ctx->rank * nptrs + i;
+        }
+        hipCheck(hipMalloc(&v[i], host.size() * sizeof(uint64_t)), "hipMalloc");
+        hipCheck(hipMemcpy(v[i], host.data(), host.size() * sizeof(uint64_t),
+                           hipMemcpyHostToDevice), "h2d");
+      }
+      return v;
+    };
+    std::vector<uint64_t*> inputs = make(!inPlace), outputs = make(inPlace);
+    gloo_amd::AllreduceOptions opts(ctx);
+    opts.setAlgorithm(algorithm);
+    opts.setOutputs(outputs, N);
+    if (!inPlace) opts.setInputs(inputs, N);
+    void (*fn)(void*, const void*, const void*, size_t) = &gloo_amd::sum<uint64_t>;
+    opts.setReduceFunction(fn);
+    opts.setMaxSegmentSize(128);
+    gloo_amd::allreduce(opts);
+    const uint64_t base = stride * (stride - 1) / 2;
+    for (int i = 0; i < nptrs; i++) {
+      std::vector<uint64_t> host(std::max(N, 1));
+      hipCheck(hipMemcpy(host.data(), outputs[i], host.size() * sizeof(uint64_t),
+                         hipMemcpyDeviceToHost), "d2h");
+      for (int k = 0; k < N; k++) {
+        if (host[k] != k * stride * stride + base) {
+          EXPECT(false, "%s P=%d ptrs=%d N=%d inPlace=%d: out[%d][%d] = %llu", name, P, nptrs,
+                 N, (int)inPlace, i, k, (unsigned long long)host[k]);
+          break;
+        }
+      }
+      hipFree(outputs[i]);
+      hipFree(inputs[i]);
+    }
+  });
+}
+
+// gloo/test/allreduce_test.cc:386-402
+void allreduceNewTimeout() {
+  gloo_amd::rendezvous::HashStore store;
+  std::shared_ptr<gloo_amd::Context> ctxs[2];
+  std::thread t1([&] {
+    ctxs[1] = std::make_shared<gloo_amd::Context>(1, 2, 0);
+    ctxs[1]->connectFullMesh(store);
+  });
+  ctxs[0] = std::make_shared<gloo_amd::Context>(0, 2, 0);
+  ctxs[0]->connectFullMesh(store);
+  t1.join();
+  uint64_t* dev = nullptr;
+  hipCheck(hipMalloc(&dev, sizeof(uint64_t)), "hipMalloc");
+  gloo_amd::AllreduceOptions opts(ctxs[0]);
+  opts.setOutput(dev, 1);
+  opts.setReduceFunction(static_cast<void (*)(void*, const void*, const void*, size_t)>(
+      &gloo_amd::sum<uint64_t>));
+  opts.setTimeout(std::chrono::milliseconds(10));
+  bool threw = false;
+  try {
+    gloo_amd::allreduce(opts);
+  } catch (const gloo_amd::IoException& e) {
+    threw = std::string(e.what()).find("Timed out") != std::string::npos;
+  }
+  EXPECT(threw, "allreduce(opts) with a 10 ms timeout: expected IoException(\"Timed out ...\")");
+  hipFree(dev);
+}
+
 }  // namespace
 
 int main() {
@@ -206,6 +282,19 @@ int main() {
   }
   multipleAlgorithms();
   timeoutThrowsIoException();
+  using Opts = gloo_amd::AllreduceOptions;
+  for (auto algo : {Opts::RING, Opts::BCUBE, Opts::RING_MESH}) {
+    const char* name = algo == Opts::RING ? "allreduce/ring"
+                       : algo == Opts::BCUBE ? "allreduce/bcube" : "allreduce/ring_mesh";
+    for (int P : {1, 2, 4, 7}) {
+      for (int nptrs : {1, 2, 3}) {
+        for (int N : {0, 1, 10, 100, 1000, 10000}) {
+          for (bool inPlace : {true, false}) allreduceNew(algo, name, P, nptrs, N, inPlace);
+        }
+      }
+    }
+  }
+  allreduceNewTimeout();
   if (g_failures == 0) std::printf("dropin_test: all passed\n");
   return g_failures == 0 ? 0 : 1;
 }

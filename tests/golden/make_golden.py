@@ -185,10 +185,100 @@ def make_allreduce():
                    "cases": index}, f, indent=1)
 
 
+# ---- gloo::allreduce(AllreduceOptions) (gloo/allreduce.cc) ----------------
+# (algo, P, N, dtype, op, nin, nout, max_seg, kind, out_init)
+#   kind      0 seeded, 1 stride pattern (base_test.h:184-191)
+#   out_init  "pattern": the outputs hold the data (in place, no inputs);
+#             "zero": outputs cleared (allreduce_test.cc:325-327);
+#             "seeded": outputs hold other seeded data (exposes float16's
+#             assignment reading the destination, gloo/types.h)
+FN_CASES = []
+for _algo in (O.FN_RING, O.FN_BCUBE):
+    # the reference's AllreduceNewTest grid (allreduce_test.cc:306-378), uint64 sum,
+    # maxSegmentSize 128
+    for _P in (1, 2, 4, 7):
+        for _np in (1, 2, 3):
+            for _N in (0, 1, 10, 100, 1000, 10000):
+                FN_CASES.append((_algo, _P, _N, O.UINT64, O.SUM, 0, _np, 128, 1, "pattern"))
+                FN_CASES.append((_algo, _P, _N, O.UINT64, O.SUM, _np, _np, 128, 1, "zero"))
+    # seeded data, rounding-sensitive types and every op
+    for _P in (2, 3, 5, 8):
+        for _N, _ms in ((1000, 0), (4099, 128), (100003, 0), (100003, 4096)):
+            FN_CASES.append((_algo, _P, _N, O.FLOAT32, O.SUM, 0, 1, _ms, 0, "pattern"))
+        FN_CASES.append((_algo, _P, 4099, O.INT32, O.SUM, 2, 1, 256, 0, "seeded"))
+        FN_CASES.append((_algo, _P, 4099, O.FLOAT16, O.SUM, 2, 2, 256, 0, "seeded"))
+        FN_CASES.append((_algo, _P, 4099, O.FLOAT16, O.MAX, 3, 1, 0, 0, "seeded"))
+        FN_CASES.append((_algo, _P, 2048, O.FLOAT16, O.MIN, 0, 2, 0, 0, "pattern"))
+        FN_CASES.append((_algo, _P, 1000, O.FLOAT32, O.MAX, 1, 1, 0, 0, "seeded"))
+        FN_CASES.append((_algo, _P, 1000, O.FLOAT64, O.PRODUCT, 0, 1, 0, 0, "pattern"))
+
+
+def fn_case_buffers(c):
+    """(inputs, outputs) per rank of a FN_CASES entry, as the tests rebuild them."""
+    algo, P, N, dtype, op, nin, nout, ms, kind, out_init = c
+    if out_init == "pattern":
+        data = case_inputs(P, N, dtype, nout, kind)
+        return [[] for _ in range(P)], data
+    ins = case_inputs(P, N, dtype, nin, kind)
+    if out_init == "zero":
+        outs = [[np.zeros(N, dtype=O.NP_DTYPE[dtype]) for _ in range(nout)] for _ in range(P)]
+    else:
+        outs = [[O.fill(dtype, N, 0, seed=SEED + 1, rank=r, ptr_index=i) for i in range(nout)]
+                for r in range(P)]
+    return ins, outs
+
+
+def fn_case_name(c):
+    algo, P, N, dtype, op, nin, nout, ms, kind, out_init = c
+    return "%s_P%d_N%d_%s_%s_in%d_out%d_seg%d_k%d_%s" % (
+        "ring" if algo == O.FN_RING else "bcube", P, N, O.DTYPE_NAMES[dtype],
+        O.OP_NAMES[op], nin, nout, ms, kind, out_init)
+
+
+def make_allreduce_fn():
+    out = {}
+    index = []
+    for c in FN_CASES:
+        algo, P, N, dtype, op, nin, nout, ms, kind, out_init = c
+        ins, outs = fn_case_buffers(c)
+        res = O.allreduce_fn(algo, op, dtype, ins, outs, ms, use_ref=True)
+        first = res[0][0]
+        for r in range(P):
+            for i in range(nout):
+                assert np.array_equal(res[r][i].view(np.uint8), first.view(np.uint8)), \
+                    "reference ranks disagree in %s" % fn_case_name(c)
+        name = fn_case_name(c)
+        rec = {"name": name, "algo": algo, "P": P, "N": N, "dtype": dtype, "op": op,
+               "nin": nin, "nout": nout, "max_segment_size": ms, "kind": kind,
+               "out_init": out_init, "seed": SEED,
+               "input_sha256": sha([x for row in ins + outs for x in row]),
+               "output_sha256": sha([first])}
+        if N <= 4099:
+            out[name] = first
+        else:
+            idx = np.linspace(0, N - 1, 257).astype(np.int64)
+            out[name + "_idx"] = idx
+            out[name + "_sample"] = first[idx]
+        index.append(rec)
+    np.savez_compressed(os.path.join(HERE, "allreduce_fn_golden.npz"), **out)
+    with open(os.path.join(HERE, "allreduce_fn_golden.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py (make_allreduce_fn)",
+                   "source": "gloo::allreduce(AllreduceOptions) of oracle/_ref/libgloo_ref.so "
+                             "(reference compiled from /root/reference by oracle/Makefile)",
+                   "cases": index}, f, indent=1)
+    print("allreduce_fn: %d cases" % len(index))
+
+
 if __name__ == "__main__":
     if not O.ref_available():
         sys.exit("oracle/_ref/libgloo_ref.so missing: make -C oracle ref")
-    make_reduce()
-    make_f16_conversions()
-    make_allreduce()
+    which = sys.argv[1:] or ["reduce", "f16", "allreduce", "allreduce_fn"]
+    if "reduce" in which:
+        make_reduce()
+    if "f16" in which:
+        make_f16_conversions()
+    if "allreduce" in which:
+        make_allreduce()
+    if "allreduce_fn" in which:
+        make_allreduce_fn()
     print("done")

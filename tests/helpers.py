@@ -41,6 +41,29 @@ def case_inputs(P, N, dtype, nptrs, kind, seed=SEED):
     return ins
 
 
+def load_allreduce_fn_golden():
+    with open(os.path.join(GOLDEN, "allreduce_fn_golden.json")) as f:
+        index = json.load(f)["cases"]
+    data = np.load(os.path.join(GOLDEN, "allreduce_fn_golden.npz"))
+    return index, data
+
+
+def fn_case_buffers(rec):
+    """(inputs, outputs) per rank of a gloo::allreduce golden case, rebuilt
+    exactly as tests/golden/make_golden.py made them."""
+    P, N, dtype = rec["P"], rec["N"], rec["dtype"]
+    nin, nout, kind = rec["nin"], rec["nout"], rec["kind"]
+    if rec["out_init"] == "pattern":
+        return [[] for _ in range(P)], case_inputs(P, N, dtype, nout, kind)
+    ins = case_inputs(P, N, dtype, nin, kind)
+    if rec["out_init"] == "zero":
+        outs = [[np.zeros(N, dtype=O.NP_DTYPE[dtype]) for _ in range(nout)] for _ in range(P)]
+    else:
+        outs = [[O.fill(dtype, N, 0, seed=SEED + 1, rank=r, ptr_index=i) for i in range(nout)]
+                for r in range(P)]
+    return ins, outs
+
+
 def check_against_golden(rec, data, out):
     """out: rank-0 result array of the case `rec`."""
     name = rec["name"]
@@ -101,12 +124,18 @@ def replay_plans(plans, op, dtype, inputs):
                                                      scratch[r][boff:boff + ln])
                 elif kind == 3:  # COPY
                     data[r][off:off + ln] = scratch[r][boff:boff + ln]
-                elif kind == 5:  # FOLD: acc = s0; acc = op(s_k, acc)
+                elif kind == 5:  # FOLD: acc = s0; acc = op(s_k, acc) (or op(acc, s_k))
                     srcs = plans[r][2][boff]
-                    assert srcs[0] == -1
-                    acc = np.array(data[r][off:off + ln], copy=True)
+                    left = bool(steps[pc[r]][7] & 1)
+
+                    def val(reg, r=r, off=off, ln=ln):
+                        if reg == -1:
+                            return np.array(data[r][off:off + ln], copy=True)
+                        return scratch[r][reg:reg + ln]
+                    acc = np.array(val(srcs[0]), copy=True)
                     for reg in srcs[1:]:
-                        acc = O.reduce(op, dtype, scratch[r][reg:reg + ln], acc)
+                        acc = (O.reduce(op, dtype, acc, val(reg)) if left
+                               else O.reduce(op, dtype, val(reg), acc))
                     data[r][off:off + ln] = acc
                 elif kind == 4:  # RELEASE
                     key = (peer, r, tag)
