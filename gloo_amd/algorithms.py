@@ -62,8 +62,14 @@ def torch_dtype_code(t):
     return table[t.dtype]
 
 
-def _as_ptrs(bufs, dtype):
-    """tensors or ints -> (list of device pointers, dtype code, min numel)."""
+NUMPY_CODES = {"int8": INT8, "uint8": UINT8, "int32": INT32, "int64": INT64,
+               "uint64": UINT64, "float32": FLOAT32, "float64": FLOAT64, "float16": FLOAT16}
+
+
+def _as_ptrs(bufs, dtype, allow_host=True):
+    """Buffers -> (list of pointers, dtype code, min numel).  A buffer is a
+    device tensor, a host tensor or numpy array (host-memory endpoints:
+    staged by the algorithm), or a raw pointer int with an explicit dtype."""
     ptrs, numel = [], None
     for b in bufs:
         if isinstance(b, int):
@@ -71,7 +77,22 @@ def _as_ptrs(bufs, dtype):
                 raise TypeError("raw pointers need an explicit dtype")
             ptrs.append(b)
             continue
-        if not b.is_cuda:
+        if hasattr(b, "__array_interface__") and not hasattr(b, "is_cuda"):  # numpy
+            if not allow_host:
+                raise ValueError("device buffers required")
+            if not b.flags["C_CONTIGUOUS"] or not b.flags["WRITEABLE"]:
+                raise ValueError("host buffers must be contiguous and writeable")
+            code = NUMPY_CODES.get(b.dtype.name)
+            if code is None:
+                raise TypeError("unsupported dtype %s" % b.dtype)
+            if dtype is None:
+                dtype = code
+            elif dtype != code:
+                raise TypeError("all buffers must share one dtype")
+            ptrs.append(b.ctypes.data)
+            numel = b.size if numel is None else min(numel, b.size)
+            continue
+        if not b.is_cuda and not allow_host:
             raise ValueError("buffers must be device tensors (got %s)" % b.device)
         if not b.is_contiguous():
             raise ValueError("buffers must be contiguous")
@@ -209,3 +230,23 @@ def plan(algo, rank, size, count, with_folds=False, esize=4, max_segment_size=0,
             lib.glx_plan_fold_ex(*args, st[5], fb, k)
             folds[st[5]] = list(fb[:k])
     return steps, scratch.value, folds
+
+
+def stage_plan(algo, rank, size, count, esize=4, max_piece=None):
+    """Host-memory staging of a plan (glx_plan_stage): (h2d pieces [(off,
+    len)] in issue order, copy-backs [(step, off, len)], step -1 = after the
+    last step)."""
+    code = ALGO_CODES[algo]
+    if max_piece is None:
+        max_piece = max(1, (8 << 20) // esize)
+    nd = ctypes.c_int64(0)
+    n = lib.glx_plan_stage(code, rank, size, count, esize, max_piece, None, 0, None, 0,
+                           ctypes.byref(nd))
+    if n < 0:
+        check(_lib.ERR_INVALID, "stage_plan")
+    h = (ctypes.c_int64 * (2 * max(n, 1)))()
+    d = (ctypes.c_int64 * (3 * max(nd.value, 1)))()
+    lib.glx_plan_stage(code, rank, size, count, esize, max_piece, h, n, d, nd.value,
+                       ctypes.byref(nd))
+    return ([(h[2 * i], h[2 * i + 1]) for i in range(n)],
+            [(d[3 * i], d[3 * i + 1], d[3 * i + 2]) for i in range(nd.value)])

@@ -66,7 +66,8 @@ class AllreduceOptions:
         self._sizes(self.outputs, elements, dtype)
 
     def _sizes(self, bufs, elements, dtype):
-        _, dt, numel = _as_ptrs(bufs, dtype if dtype is not None else self.dtype)
+        _, dt, numel = _as_ptrs(bufs, dtype if dtype is not None else self.dtype,
+                                allow_host=False)
         if self.dtype is not None and dt != self.dtype:
             raise TypeError("inputs and outputs must share one dtype")
         self.dtype = dt
@@ -116,8 +117,9 @@ def allreduce(opts):
     if not opts.outputs:
         raise EnforceNotMet("allreduce: at least one output is required")
     op = opts.op if opts.op is not None else 1
-    inp, _, _ = _as_ptrs(opts.inputs, opts.dtype) if opts.inputs else ([], None, None)
-    outp, _, _ = _as_ptrs(opts.outputs, opts.dtype)
+    inp, _, _ = (_as_ptrs(opts.inputs, opts.dtype, allow_host=False) if opts.inputs
+                 else ([], None, None))
+    outp, _, _ = _as_ptrs(opts.outputs, opts.dtype, allow_host=False)
     iarr = (ctypes.c_void_p * max(len(inp), 1))(*inp)
     oarr = (ctypes.c_void_p * len(outp))(*outp)
     sync = None

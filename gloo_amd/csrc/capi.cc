@@ -392,6 +392,38 @@ int64_t glx_plan_ex(int algo, int rank, int size, int64_t count, int esize,
   return n;
 }
 
+int64_t glx_plan_stage(int algo, int rank, int size, int64_t count, int esize,
+                       int64_t max_piece, int64_t* h2d, int64_t h2d_cap, int64_t* d2h,
+                       int64_t d2h_cap, int64_t* n_d2h) {
+  int64_t n = -1;
+  guarded([&]() -> int {
+    glx::Plan p = glx::makePlan(algo, rank, size, count,
+                                planParams(esize, 0, glx::PlanParams().minPieceBytes));
+    glx::StagePlan sp = glx::stagePlan(p, count, max_piece);
+    n = (int64_t)sp.h2d.size();
+    for (int64_t i = 0; i < n && i < h2d_cap && h2d != nullptr; i++) {
+      h2d[2 * i] = sp.h2d[(size_t)i].off;
+      h2d[2 * i + 1] = sp.h2d[(size_t)i].len;
+    }
+    int64_t k = 0;
+    auto put = [&](int64_t step, const glx::Range& r) {
+      if (k < d2h_cap && d2h != nullptr) {
+        d2h[3 * k] = step;
+        d2h[3 * k + 1] = r.off;
+        d2h[3 * k + 2] = r.len;
+      }
+      k++;
+    };
+    for (size_t i = 0; i < sp.d2h.size(); i++) {
+      for (const auto& r : sp.d2h[i]) put((int64_t)i, r);
+    }
+    for (const auto& r : sp.d2hRest) put(-1, r);
+    if (n_d2h) *n_d2h = k;
+    return GLX_OK;
+  });
+  return n;
+}
+
 int64_t glx_plan_fold(int algo, int rank, int size, int64_t count, int64_t fold,
                       int64_t* srcs, int64_t cap) {
   return glx_plan_fold_ex(algo, rank, size, count, 4, 0, glx::PlanParams().minPieceBytes,

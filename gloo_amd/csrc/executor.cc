@@ -63,6 +63,29 @@ const bool g_trace = [] {
     }                                         \
   } while (0)
 
+// Host memory (pageable or pinned) as opposed to device/managed memory.
+bool isHostPointer(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return true;  // unknown to HIP: plain pageable host memory
+  }
+  return a.type == hipMemoryTypeHost || a.type == hipMemoryTypeUnregistered;
+}
+
+bool isPinnedHost(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+// H2D pieces of host-mode staging: small enough that the schedule starts
+// early, large enough to run the PCIe link at full rate.
+constexpr int64_t kStagePieceBytes = int64_t(8) << 20;
+
 }  // namespace
 
 void HipPlanExecutor::setCopySplit(int k) {
@@ -104,6 +127,14 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
     ownCompute_ = true;
   }
   split_ = std::max(1, std::min(copySplit(), (int)kMaxSplit));
+
+  hostMode_ = count_ > 0 && isHostPointer(ptrs[0]);
+  for (void* p : ptrs) {
+    GLX_ENFORCE(count_ == 0 || isHostPointer(p) == hostMode_,
+                "buffers must be all device memory or all host memory");
+  }
+  GLX_ENFORCE(!hostMode_ || !userStream_, "streams cannot be used with host-memory buffers");
+  if (hostMode_) setupHostMode();
 
   allocScratch();
 
@@ -162,6 +193,19 @@ HipPlanExecutor::~HipPlanExecutor() noexcept(false) {
   hipSetDevice(device_);
   if (compute_ != nullptr) hipStreamSynchronize(compute_);
   for (auto& c : copies_) hipStreamSynchronize(c.s);
+  for (hipStream_t st : {h2d_, d2h_}) {
+    if (st != nullptr) {
+      hipStreamSynchronize(st);
+      hipStreamDestroy(st);
+    }
+  }
+  for (auto& e : h2dEvents_) hipEventDestroy(e);
+  for (auto& e : d2hEvents_) {
+    if (e != nullptr) hipEventDestroy(e);
+  }
+  if (hostDone_) hipEventDestroy(hostDone_);
+  for (char* d : devBufs_) hipFree(d);
+  for (void* p : registered_) hipHostUnregister(p);
   for (void* p : ipcOpened_) hipIpcCloseMemHandle(p);
   for (auto& e : events_) hipEventDestroy(e);
   if (computeMark_) hipEventDestroy(computeMark_);
@@ -432,6 +476,10 @@ void HipPlanExecutor::drain() {
 void HipPlanExecutor::run() {
   if (count_ == 0) return;  // gloo/allreduce_ring_chunked.h:84-86
   GLX_HIP_CHECK(hipSetDevice(device_));
+  if (hostMode_) {
+    runHost();
+    return;
+  }
   char* ptr0 = static_cast<char*>(ptrs_[0]);
   const size_t bytes = (size_t)count_ * esize_;
 
@@ -491,6 +539,13 @@ void HipPlanExecutor::runFn(const FnCall& call) {
   for (void* p : call.out) GLX_ENFORCE(p != nullptr || count_ == 0, "null output pointer");
   for (void* p : call.in) GLX_ENFORCE(p != nullptr || count_ == 0, "null input pointer");
   if (count_ == 0) return;  // gloo/allreduce.cc:98-100
+  for (void* p : call.out) {
+    GLX_ENFORCE(!isHostPointer(p), "allreduce(opts) takes device buffers; host-memory "
+                "buffers are staged by the class algorithms (AllreduceRingChunked, ...)");
+  }
+  for (void* p : call.in) {
+    GLX_ENFORCE(!isHostPointer(p), "allreduce(opts) takes device buffers");
+  }
   GLX_HIP_CHECK(hipSetDevice(device_));
   // per-call stream and timeout (opts.timeout, gloo/allreduce.h:50)
   struct Restore {
@@ -511,6 +566,95 @@ void HipPlanExecutor::runFn(const FnCall& call) {
                                  hipMemcpyDeviceToDevice, compute_));
   }
   if (call.stream == nullptr) GLX_HIP_CHECK(hipStreamSynchronize(compute_));
+}
+
+void HipPlanExecutor::setupHostMode() {
+  const size_t bytes = (size_t)count_ * esize_;
+  for (void* p : ptrs_) {
+    if (!isPinnedHost(p)) {
+      // pin the caller's buffer for the algorithm's lifetime (the reference's
+      // algorithms also bind their buffers at construction); if the runtime
+      // refuses, pageable copies are still correct, only slower
+      if (hipHostRegister(p, bytes, hipHostRegisterPortable) == hipSuccess) {
+        registered_.push_back(p);
+      } else {
+        (void)hipGetLastError();
+      }
+    }
+    char* d = nullptr;
+    GLX_HIP_CHECK(hipMalloc((void**)&d, bytes));
+    devBufs_.push_back(d);
+  }
+  GLX_HIP_CHECK(hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking));
+  GLX_HIP_CHECK(hipStreamCreateWithFlags(&d2h_, hipStreamNonBlocking));
+  stage_ = glx::stagePlan(plan_, count_, std::max<int64_t>(1, kStagePieceBytes / (int64_t)esize_));
+  h2dEvents_.resize(stage_.h2d.size(), nullptr);
+  for (auto& e : h2dEvents_) GLX_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  d2hEvents_.assign(plan_.steps.size(), nullptr);
+  for (size_t i = 0; i < plan_.steps.size(); i++) {
+    if (!stage_.d2h[i].empty()) {
+      GLX_HIP_CHECK(hipEventCreateWithFlags(&d2hEvents_[i], hipEventDisableTiming));
+    }
+  }
+  GLX_HIP_CHECK(hipEventCreateWithFlags(&hostDone_, hipEventDisableTiming));
+}
+
+// Make `s` wait for the H2D pieces overlapping [off, off+len).  h2d_ is one
+// in-order stream, so waiting for the latest such piece covers the others.
+void HipPlanExecutor::waitH2D(hipStream_t s, int& waited, int64_t off, int64_t len) {
+  int last = -1;
+  for (size_t j = 0; j < stage_.h2d.size(); j++) {
+    const glx::Range& r = stage_.h2d[j];
+    if (r.off < off + len && off < r.off + r.len) last = (int)j;
+  }
+  if (last > waited) {
+    GLX_HIP_CHECK(hipStreamWaitEvent(s, h2dEvents_[(size_t)last], 0));
+    waited = last;
+  }
+}
+
+// Final values of `ranges` (in devBufs_[0]) to every user pointer, on d2h_
+// (the caller has made d2h_ wait for the writes).
+void HipPlanExecutor::copyBack(const std::vector<glx::Range>& ranges) {
+  for (const glx::Range& r : ranges) {
+    const size_t at = (size_t)r.off * esize_, n = (size_t)r.len * esize_;
+    for (void* p : ptrs_) {
+      GLX_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(p) + at, devBufs_[0] + at, n,
+                                   hipMemcpyDeviceToHost, d2h_));
+    }
+  }
+}
+
+void HipPlanExecutor::runHost() {
+  if (contextSize_ == 1 && ptrs_.size() == 1) return;  // the result is the input
+  computeH2dWaited_ = -1;
+  for (auto& c : copies_) c.h2dWaited = -1;
+  for (size_t j = 0; j < stage_.h2d.size(); j++) {
+    const glx::Range& r = stage_.h2d[j];
+    const size_t at = (size_t)r.off * esize_, n = (size_t)r.len * esize_;
+    for (size_t k = 0; k < ptrs_.size(); k++) {
+      GLX_HIP_CHECK(hipMemcpyAsync(devBufs_[k] + at, static_cast<const char*>(ptrs_[k]) + at, n,
+                                   hipMemcpyHostToDevice, h2d_));
+    }
+    GLX_HIP_CHECK(hipEventRecord(h2dEvents_[j], h2d_));
+  }
+  if (ptrs_.size() > 1) {  // local fold needs every buffer whole
+    waitH2D(compute_, computeH2dWaited_, 0, count_);
+    std::vector<const void*> srcs(devBufs_.begin(), devBufs_.end());
+    GLX_HIP_CHECK(glx::launch_reduce_n(op_, dtype_, devBufs_[0], srcs.data(), (int)srcs.size(),
+                                       (size_t)count_, compute_));
+  }
+  if (contextSize_ > 1) exchange(devBufs_[0]);
+  // ranges no step wrote: their value is the local fold (a no-op for one
+  // pointer, whose host copy already holds it)
+  if (ptrs_.size() > 1 && !stage_.d2hRest.empty()) {
+    GLX_HIP_CHECK(hipEventRecord(hostDone_, compute_));
+    GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, hostDone_, 0));
+    copyBack(stage_.d2hRest);
+  }
+  GLX_HIP_CHECK(hipStreamSynchronize(d2h_));
+  GLX_HIP_CHECK(hipStreamSynchronize(compute_));
+  GLX_HIP_CHECK(hipStreamSynchronize(h2d_));
 }
 
 void HipPlanExecutor::exchange(char* ptr0) {
@@ -555,6 +699,7 @@ void HipPlanExecutor::exchange(char* ptr0) {
               GLX_HIP_CHECK(hipStreamWaitEvent(cs.s, computeMark_, 0));
               cs.waitedMark = markEpoch_;
             }
+            if (hostMode_) waitH2D(cs.s, cs.h2dWaited, s.off, s.len);
             hipError_t ce = hipErrorUnknown;
             if (peerCopyOk_ && oc.peerDevice >= 0 && oc.peerDevice != device_) {
               ce = hipMemcpyPeerAsync(dst + at, oc.peerDevice, src + at, device_, len, cs.s);
@@ -587,14 +732,21 @@ void HipPlanExecutor::exchange(char* ptr0) {
       }
       case glx::REDUCE: {
         waitWar(s.off, s.len);
+        if (hostMode_) waitH2D(compute_, computeH2dWaited_, s.off, s.len);
         char* dst = ptr0 + (size_t)s.off * esize_;
         const char* src = landing(blocks_, s.boff, s.off);
         GLX_HIP_CHECK(glx::launch_reduce(op_, dtype_, dst, dst, src, (size_t)s.len, compute_));
         computeSinceMark = true;
+        if (hostMode_ && !stage_.d2h[i].empty()) {  // final values: copy back now
+          GLX_HIP_CHECK(hipEventRecord(d2hEvents_[i], compute_));
+          GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, d2hEvents_[i], 0));
+          copyBack(stage_.d2h[i]);
+        }
         break;
       }
       case glx::FOLD: {
         waitWar(s.off, s.len);
+        if (hostMode_) waitH2D(compute_, computeH2dWaited_, s.off, s.len);
         char* dst = ptr0 + (size_t)s.off * esize_;
         const auto& regions = plan_.folds[(size_t)s.boff];
         std::vector<const void*> srcs;
@@ -606,15 +758,26 @@ void HipPlanExecutor::exchange(char* ptr0) {
         GLX_HIP_CHECK(glx::launch_reduce_n(op_, dtype_, dst, srcs.data(), (int)srcs.size(),
                                            (size_t)s.len, compute_, rev));
         computeSinceMark = true;
+        if (hostMode_ && !stage_.d2h[i].empty()) {  // final values: copy back now
+          GLX_HIP_CHECK(hipEventRecord(d2hEvents_[i], compute_));
+          GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, d2hEvents_[i], 0));
+          copyBack(stage_.d2h[i]);
+        }
         break;
       }
       case glx::COPY: {
         waitWar(s.off, s.len);
+        if (hostMode_) waitH2D(compute_, computeH2dWaited_, s.off, s.len);
         char* dst = ptr0 + (size_t)s.off * esize_;
         const char* src = landing(blocks_, s.boff, s.off);
         GLX_HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)s.len * esize_,
                                      hipMemcpyDeviceToDevice, compute_));
         computeSinceMark = true;
+        if (hostMode_ && !stage_.d2h[i].empty()) {  // final values: copy back now
+          GLX_HIP_CHECK(hipEventRecord(d2hEvents_[i], compute_));
+          GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, d2hEvents_[i], 0));
+          copyBack(stage_.d2h[i]);
+        }
         break;
       }
       case glx::RELEASE: {

@@ -86,6 +86,7 @@ class HipPlanExecutor : public Algorithm {
     hipStream_t s = nullptr;
     uint64_t waitedMark = 0;      // last compute mark this stream waited on
     hipEvent_t last = nullptr;    // last copy recorded in the current run
+    int h2dWaited = -1;           // host mode: last H2D piece waited on this run
   };
   struct InChan {  // peer -> this rank
     int peer, tag;
@@ -150,6 +151,25 @@ class HipPlanExecutor : public Algorithm {
   std::vector<ScratchBlock> blocks_;                  // ours
   std::map<int, std::vector<ScratchBlock>> peerBlocks_;  // by destination rank
   std::chrono::milliseconds timeout_{0};  // per-call override (0: context's)
+
+  // Host-memory endpoints (host mode): the user's pointers are
+  // host memory (pinned here with hipHostRegister when possible); the
+  // schedule runs on device copies.  H2D pieces go out in first-use order on
+  // h2d_ and every step waits only for the pieces of its own range; each
+  // range is copied back on d2h_ right after its final write.
+  bool hostMode_ = false;
+  std::vector<char*> devBufs_;     // device copy of each user pointer
+  std::vector<void*> registered_;  // host ranges pinned by us
+  hipStream_t h2d_ = nullptr, d2h_ = nullptr;
+  glx::StagePlan stage_;
+  std::vector<hipEvent_t> h2dEvents_;  // one per stage_.h2d piece
+  std::vector<hipEvent_t> d2hEvents_;  // one per step (recorded where d2h is non-empty)
+  hipEvent_t hostDone_ = nullptr;
+  int computeH2dWaited_ = -1;
+  void setupHostMode();
+  void waitH2D(hipStream_t s, int& waited, int64_t off, int64_t len);
+  void copyBack(const std::vector<glx::Range>& ranges);
+  void runHost();
   std::vector<OutChan> out_;
   std::vector<InChan> in_;
   std::vector<int> stepChan_;        // channel index per step

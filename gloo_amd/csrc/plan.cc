@@ -651,4 +651,85 @@ Plan makePlan(int algo, int rank, int size, int64_t count, const PlanParams& prm
   return Plan();
 }
 
+// ---------------------------------------------------------------------------
+// Staging of host-memory buffers
+// ---------------------------------------------------------------------------
+namespace {
+
+// A set of disjoint element intervals.
+class IntervalSet {
+ public:
+  // the parts of [off, off+len) not in the set, ascending
+  std::vector<Range> missing(int64_t off, int64_t len) const {
+    std::vector<Range> out;
+    int64_t at = off;
+    const int64_t end = off + len;
+    for (const auto& r : v_) {
+      if (r.off + r.len <= at) continue;
+      if (r.off >= end) break;
+      if (r.off > at) out.push_back({at, r.off - at});
+      at = std::max(at, r.off + r.len);
+      if (at >= end) break;
+    }
+    if (at < end) out.push_back({at, end - at});
+    return out;
+  }
+  void add(int64_t off, int64_t len) {
+    if (len <= 0) return;
+    std::vector<Range> nv;
+    int64_t lo = off, hi = off + len;
+    bool placed = false;
+    for (const auto& r : v_) {
+      if (r.off + r.len < lo) {
+        nv.push_back(r);
+      } else if (r.off > hi) {
+        if (!placed) nv.push_back({lo, hi - lo});
+        placed = true;
+        nv.push_back(r);
+      } else {
+        lo = std::min(lo, r.off);
+        hi = std::max(hi, r.off + r.len);
+      }
+    }
+    if (!placed) nv.push_back({lo, hi - lo});
+    v_.swap(nv);
+  }
+
+ private:
+  std::vector<Range> v_;  // sorted, disjoint, non-adjacent
+};
+
+bool writes(const Step& s) { return s.kind == REDUCE || s.kind == COPY || s.kind == FOLD; }
+bool touches(const Step& s) { return (s.kind == SEND || writes(s)) && s.len > 0; }
+
+}  // namespace
+
+StagePlan stagePlan(const Plan& plan, int64_t count, int64_t maxPiece) {
+  StagePlan sp;
+  if (maxPiece <= 0) maxPiece = count > 0 ? count : 1;
+  IntervalSet issued;
+  auto issue = [&](int64_t off, int64_t len) {
+    for (const Range& r : issued.missing(off, len)) {
+      for (int64_t at = r.off; at < r.off + r.len; at += maxPiece) {
+        sp.h2d.push_back({at, std::min(maxPiece, r.off + r.len - at)});
+      }
+      issued.add(r.off, r.len);
+    }
+  };
+  for (const Step& s : plan.steps) {
+    if (touches(s)) issue(s.off, s.len);
+  }
+  issue(0, count);
+  sp.d2h.resize(plan.steps.size());
+  IntervalSet later;  // written by a later step
+  for (size_t i = plan.steps.size(); i-- > 0;) {
+    const Step& s = plan.steps[i];
+    if (!writes(s) || s.len <= 0) continue;
+    sp.d2h[i] = later.missing(s.off, s.len);
+    later.add(s.off, s.len);
+  }
+  sp.d2hRest = later.missing(0, count);
+  return sp;
+}
+
 }  // namespace glx

@@ -102,4 +102,21 @@ Plan planFnBcube(int rank, int size, int64_t count);
 Plan makePlan(int algo, int rank, int size, int64_t count,
               const PlanParams& prm = PlanParams());
 
+// Host-memory endpoints: when the user's buffer is in host
+// memory the executor stages it through a device buffer.  This derives from
+// a plan (1) the order to copy the buffer in: pieces in the order the steps
+// first touch them, so the schedule starts after the first piece instead of
+// the whole buffer; (2) for every step, the ranges whose final value it
+// writes (copied back right after it), and the ranges no step writes
+// (copied back at the end).  Pieces are at most maxPiece elements.
+struct Range {
+  int64_t off, len;
+};
+struct StagePlan {
+  std::vector<Range> h2d;                 // issue order
+  std::vector<std::vector<Range>> d2h;    // per step index
+  std::vector<Range> d2hRest;
+};
+StagePlan stagePlan(const Plan& plan, int64_t count, int64_t maxPiece);
+
 }  // namespace glx

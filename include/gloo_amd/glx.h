@@ -201,6 +201,13 @@ glx_algorithm* glx_allreduce_create(glx_context* ctx, int algo, void* const* ptr
                                     int nptrs, int count, int dtype, int op,
                                     const glx_stream_t* streams, int nstreams);
 
+/* Buffers may be device memory or host memory (pageable or pinned; all
+ * pointers of one algorithm alike).  Host buffers are pinned with
+ * hipHostRegister for the algorithm's lifetime when the runtime allows and
+ * staged through device copies: H2D in the order the schedule first touches
+ * each piece, every step waiting only for its own range, and each range
+ * copied back as soon as its final value is written. */
+
 /* ---- function-style collective ---------------------------------------- */
 /* gloo::AllreduceOptions::Algorithm (gloo/allreduce.h:38-42), plus
  * GLX_ALLREDUCE_RING_MESH: RING's exact result (same chunk ownership, same
@@ -263,6 +270,15 @@ int64_t glx_plan_ex(int algo, int rank, int size, int64_t count, int esize,
 int64_t glx_plan_fold_ex(int algo, int rank, int size, int64_t count, int esize,
                          int64_t max_segment_bytes, int64_t min_piece_bytes, int64_t fold,
                          int64_t* srcs, int64_t cap);
+/* Host-memory staging derived from a plan (the algorithm's buffers are in
+ * host memory): h2d receives {off, len} pairs in issue order (returns their
+ * number, writes at most h2d_cap); d2h receives {step, off, len} triples --
+ * a range copied back right after step `step` writes its final value, step
+ * -1 for ranges no step writes -- (*n_d2h = their number, writes at most
+ * d2h_cap).  Pieces are at most max_piece elements. */
+int64_t glx_plan_stage(int algo, int rank, int size, int64_t count, int esize,
+                       int64_t max_piece, int64_t* h2d, int64_t h2d_cap, int64_t* d2h,
+                       int64_t d2h_cap, int64_t* n_d2h);
 
 #ifdef __cplusplus
 }  /* extern "C" */

@@ -227,6 +227,28 @@ void allreduceNew(gloo_amd::AllreduceOptions::Algorithm algorithm, const char* n
   });
 }
 
+// The reference's CPU calling convention unchanged: host buffers
+// (std::vector), staged through the GPU by the algorithm.
+template <template <typename> class Alg>
+void hostBuffers(const char* name, int P, int N) {
+  spawn(P, [&](std::shared_ptr<gloo_amd::Context> ctx) {
+    std::vector<float> a(N, (float)ctx->rank), b(N, 2.0f * ctx->rank);
+    {
+      Alg<float> alg(ctx, {a.data(), b.data()}, N);
+      alg.run();
+      alg.run();  // iterated: a = b = sum of (previous sums)
+    }
+    const float once = 3.0f * P * (P - 1) / 2, expected = P * 2 * once;
+    for (int i = 0; i < N; i++) {
+      if (a[i] != expected || b[i] != expected) {
+        EXPECT(false, "%s host P=%d N=%d: [%d] = %f / %f, expected %f", name, P, N, i, a[i],
+               b[i], expected);
+        break;
+      }
+    }
+  });
+}
+
 // gloo/test/allreduce_test.cc:386-402
 void allreduceNewTimeout() {
   gloo_amd::rendezvous::HashStore store;
@@ -295,6 +317,10 @@ int main() {
     }
   }
   allreduceNewTimeout();
+  for (int P : {1, 2, 3, 4}) {
+    hostBuffers<gloo_amd::HipAllreduceRingChunked>("ring_chunked", P, 100003);
+    hostBuffers<gloo_amd::HipAllreduceHalvingDoubling>("halving_doubling", P, 100003);
+  }
   if (g_failures == 0) std::printf("dropin_test: all passed\n");
   return g_failures == 0 ? 0 : 1;
 }

@@ -1,0 +1,102 @@
+"""Host-memory endpoints: the class algorithms on buffers in
+host memory -- the reference's own calling convention, AllreduceRingChunked<T>
+(ctx, {host ptr}, count) -- staged through the GPU: H2D in first-use order,
+the schedule on device copies, each range copied back after its final write.
+Results must be the reference's bits (oracle), for pageable numpy buffers and
+pinned torch buffers."""
+import numpy as np
+import pytest
+
+from helpers import case_inputs, run_ranks, same_bits
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+ALGOS = {"ring_chunked": O.RING_CHUNKED, "halving_doubling": O.HALVING_DOUBLING,
+         "ring_chunked_mesh": O.RING_CHUNKED}
+
+
+def make(gloo_amd, algo, ctx, bufs, op):
+    fn = {O.SUM: gloo_amd.ReductionFunction.sum, O.MAX: gloo_amd.ReductionFunction.max,
+          O.MIN: gloo_amd.ReductionFunction.min,
+          O.PRODUCT: gloo_amd.ReductionFunction.product}[op]
+    if algo == "halving_doubling":
+        return gloo_amd.AllreduceHalvingDoubling(ctx, bufs, fn=fn)
+    return gloo_amd.AllreduceRingChunked(
+        ctx, bufs, fn=fn, schedule="mesh" if algo == "ring_chunked_mesh" else "ring")
+
+
+def host_allreduce(algo, op, dtype, inputs, runs=1, pinned=False):
+    import gloo_amd
+    P = len(inputs)
+    store = gloo_amd.rendezvous.HashStore()
+    if pinned:
+        tv = {O.FLOAT32: torch.float32, O.INT32: torch.int32, O.FLOAT16: torch.float16,
+              O.FLOAT64: torch.float64}[dtype]
+        bufs = [[torch.from_numpy(x.copy()).view(tv).pin_memory() for x in row]
+                for row in inputs]
+    else:
+        bufs = [[np.array(x, copy=True) for x in row] for row in inputs]
+
+    def rank_fn(r):
+        ctx = gloo_amd.rendezvous.Context(r, P, 0)
+        ctx.setTimeout(60)
+        ctx.connectFullMesh(store)
+        alg = make(gloo_amd, algo, ctx, bufs[r], op)
+        for k in range(runs):
+            if k > 0:  # the host buffers are the algorithm's: refill in place
+                for b, x in zip(bufs[r], inputs[r]):
+                    if pinned:
+                        b.copy_(torch.from_numpy(x.copy()).view(b.dtype))
+                    else:
+                        b[...] = x
+            alg.run()
+        alg.close()
+        return True
+
+    run_ranks(P, rank_fn, timeout=120)
+    if pinned:
+        return [[b.view(torch.uint8).numpy().view(O.NP_DTYPE[dtype]).copy() for b in row]
+                for row in bufs]
+    return bufs
+
+
+def check(out, exp):
+    for r in range(len(exp)):
+        for i in range(len(exp[r])):
+            assert same_bits(out[r][i], exp[r][i]), (r, i)
+
+
+@pytest.mark.parametrize("algo", list(ALGOS))
+@pytest.mark.parametrize("P,N", [(1, 1000), (2, 1), (2, 100003), (3, 4099), (4, 1 << 20),
+                                 (5, 3 << 20), (8, (2 << 20) + 5)])
+def test_pageable_host_buffers_vs_oracle(algo, P, N):
+    ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=3)
+    out = host_allreduce(algo, O.SUM, O.FLOAT32, ins, runs=2)
+    check(out, O.allreduce(ALGOS[algo], O.SUM, O.FLOAT32, ins))
+
+
+@pytest.mark.parametrize("algo", list(ALGOS))
+@pytest.mark.parametrize("dtype,op", [(O.FLOAT16, O.SUM), (O.INT32, O.MAX),
+                                      (O.FLOAT64, O.PRODUCT)], ids=str)
+def test_pinned_multi_pointer_host_buffers(algo, dtype, op):
+    P, N = 3, 300007
+    ins = case_inputs(P, N, dtype, 2, 0, seed=4)
+    out = host_allreduce(algo, op, dtype, ins, runs=2, pinned=True)
+    check(out, O.allreduce(ALGOS[algo], op, dtype, ins))
+
+
+def test_single_rank_multi_pointer_host():
+    ins = case_inputs(1, 5000, O.FLOAT32, 3, 0, seed=6)
+    out = host_allreduce("ring_chunked", O.SUM, O.FLOAT32, ins)
+    check(out, O.allreduce(O.RING_CHUNKED, O.SUM, O.FLOAT32, ins))
+
+
+def test_mixed_host_and_device_buffers_are_rejected():
+    import gloo_amd
+    ctx = gloo_amd.rendezvous.Context(0, 1, 0)
+    with pytest.raises(gloo_amd.EnforceNotMet):
+        gloo_amd.AllreduceRingChunked(ctx, [np.zeros(64, np.float32),
+                                            torch.zeros(64, device="cuda")])

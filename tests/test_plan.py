@@ -79,3 +79,38 @@ def test_hd_plan_traffic(P):
 def test_plan_rejects_bad_geometry():
     with pytest.raises(gloo_amd.EnforceNotMet):
         gloo_amd.plan("ring_chunked", 3, 2, 10)
+
+
+# ---------------------------------------------------------------------------
+# Host-memory staging (glx_plan_stage): every element copied in exactly once,
+# copied back exactly once after its final write, pieces in first-use order.
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("algo", ["ring_chunked", "halving_doubling", "ring_chunked_mesh",
+                                  "fn_ring", "fn_ring_mesh", "fn_bcube"])
+@pytest.mark.parametrize("P,N", [(1, 1000), (2, 1), (2, 1000), (3, 4099), (5, 100003),
+                                 (8, 1 << 16), (8, 4 << 20)])
+def test_stage_plan_covers_each_element_once(algo, P, N):
+    from gloo_amd import algorithms as A
+    for r in range(P):
+        steps, _ = A.plan(algo, r, P, N)
+        h2d, d2h = A.stage_plan(algo, r, P, N, max_piece=1 << 18)
+        cover = np.zeros(N, np.int32)
+        for off, ln in h2d:
+            assert 0 < ln <= 1 << 18
+            cover[off:off + ln] += 1
+        assert (cover == 1).all()
+        back = np.zeros(N, np.int32)
+        last_write = np.full(N, -1, np.int64)
+        for i, st in enumerate(steps):
+            if st[0] in (2, 3, 5) and st[4] > 0:
+                last_write[st[3]:st[3] + st[4]] = i
+        for step, off, ln in d2h:
+            back[off:off + ln] += 1
+            # copied back right after the step that writes the final value
+            assert (last_write[off:off + ln] == step).all()
+        assert (back == 1).all()
+        # first-use order: the first piece holds what the first touching step needs
+        touching = [st for st in steps if st[0] in (0, 2, 3, 5) and st[4] > 0]
+        if touching:
+            st = touching[0]
+            assert h2d[0][0] <= st[3] < h2d[0][0] + h2d[0][1]
