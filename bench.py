@@ -37,8 +37,12 @@ def parse():
     p.add_argument("--size-mib", type=int, default=256)
     p.add_argument("--algo", default="ring_chunked",
                    choices=["ring_chunked", "halving_doubling", "ring_chunked_mesh"])
+    p.add_argument("--schedule", default="auto", choices=["auto", "ring", "mesh"],
+                   help="N>1, ring_chunked: data movement (bit-identical results); 'auto' "
+                        "times both and reports the faster as value, the other beside it")
     p.add_argument("--copy-split", default="auto",
-                   help="N>1: streams per peer copy (1, 2, 4) or 'auto' (short calibration)")
+                   help="N>1: peer-copy transport: 'auto' (short calibration over DMA with "
+                        "1/2/4 streams per copy and the xGMI copy kernel) or a DMA split 1/2/4")
     p.add_argument("--no-alt", action="store_true",
                    help="N>1: do not also time the other schedules")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -354,39 +358,83 @@ def bench_multi(args):
     ctx.setTimeout(120)
     ctx.connectFullMesh(store)
     log("connected (world %d, device %d)" % (world, local))
-    # copy split: a short calibration of 1/2/4 streams per peer copy (every
-    # rank sees the same max-over-ranks times, so all pick the same value)
-    calib = {}
-    if args.copy_split == "auto":
-        for k in (1, 2, 4):
-            gloo_amd.set_copy_split(k)
-            calib[k], _ = time_schedule(torch, dist, gloo_amd, ctx, buf, args.algo, 3, 1)
-        split = min(calib, key=lambda k: calib[k])
+    # Transport calibration: peer copies by the DMA engines split over 1/2/4
+    # streams, or by the xGMI copy kernel (32/128 workgroups); a few runs
+    # each, max over ranks (every rank sees the same times and picks alike).
+    TRANSPORTS = [("dma", 1, 0), ("dma", 2, 0), ("dma", 4, 0), ("kernel", 1, 32),
+                  ("kernel", 1, 128)]
+
+    def set_transport(tr):
+        eng, k, blocks = tr
+        gloo_amd.set_copy_engine(eng, blocks or 64)
+        gloo_amd.set_copy_split(k)
+
+    def tname(tr):
+        return "dma/split%d" % tr[1] if tr[0] == "dma" else "kernel/%dwg" % tr[2]
+
+    def tuned(algo):
+        calib = {}
+        if args.copy_split == "auto":
+            for tr in TRANSPORTS:
+                set_transport(tr)
+                buf.copy_(src)
+                calib[tr], _ = time_schedule(torch, dist, gloo_amd, ctx, buf, algo, 3, 1)
+            best = min(calib, key=lambda k: calib[k])
+        else:
+            best = ("dma", int(args.copy_split), 0)
+        set_transport(best)
+        buf.copy_(src)
+        torch.cuda.synchronize()
+        t, sent = time_schedule(torch, dist, gloo_amd, ctx, buf, algo, steps, args.warmup)
+        # correctness after the timing: one run on fresh inputs; every rank
+        # must hold the same bits (the reduction order is rank-independent)
+        buf.copy_(src)
+        torch.cuda.synchronize()
+        alg = make_alg(gloo_amd, ctx, buf, algo)
+        alg.run()
+        torch.cuda.synchronize()
+        alg.close()
+        result = buf.clone()
+        return {"t": t, "sent": sent, "transport": tname(best), "tr": best,
+                "calib_ms": {tname(k): round(v * 1e3, 3) for k, v in calib.items()},
+                "result": result}
+
+    def checksum(t):
+        return int(t.view(torch.int16 if es == 2 else torch.int32).to(torch.int64).sum().item())
+
+    if args.algo == "ring_chunked" and args.schedule == "auto":
+        candidates = ["ring_chunked", "ring_chunked_mesh"]
+    elif args.algo == "ring_chunked" and args.schedule == "mesh":
+        candidates = ["ring_chunked_mesh"]
     else:
-        split = int(args.copy_split)
-    gloo_amd.set_copy_split(split)
-    buf.copy_(src)
-    torch.cuda.synchronize()
-    t, link_bytes = time_schedule(torch, dist, gloo_amd, ctx, buf, args.algo, steps,
-                                  args.warmup)
-    # correctness after the timing: one more run on fresh inputs; every rank
-    # must hold the same bits (the reduction order is rank-independent)
-    buf.copy_(src)
-    torch.cuda.synchronize()
-    alg = make_alg(gloo_amd, ctx, buf, args.algo)
-    alg.run()
-    torch.cuda.synchronize()
-    alg.close()
-    dev_result = buf.clone()
-    cs = torch.tensor([int(buf.view(torch.int16 if es == 2 else torch.int32)
-                           .to(torch.int64).sum().item())], dtype=torch.int64)
+        candidates = [args.algo]
+    runs = {a: tuned(a) for a in candidates}
+    chosen = min(runs, key=lambda a: runs[a]["t"])
+    t, link_bytes = runs[chosen]["t"], runs[chosen]["sent"]
+    dev_result = runs[chosen]["result"]
+    set_transport(runs[chosen]["tr"])
+    # every rank holds the same bits, and the schedules agree bit for bit
+    cs = torch.tensor([checksum(runs[a]["result"]) for a in candidates], dtype=torch.int64)
     allcs = [torch.zeros_like(cs) for _ in range(world)]
     dist.all_gather(allcs, cs)
-    verified = all(int(x.item()) == int(cs.item()) for x in allcs)
+    verified = all(torch.equal(x, cs) for x in allcs) and len(set(cs.tolist())) == 1
+    if len(candidates) > 1:
+        verified = verified and all(torch.equal(runs[a]["result"].view(torch.uint8),
+                                                dev_result.view(torch.uint8))
+                                    for a in candidates)
     alts = {}
+    for a in candidates:
+        if a == chosen:
+            continue
+        lm = busiest_link_bytes(gloo_amd, a, rank, world, n, es)
+        alts[a] = {"value": round(world * S / runs[a]["t"] / 1e9, 3),
+                   "ms_per_step": round(runs[a]["t"] * 1e3, 4),
+                   "algbw_GBps": round(S / runs[a]["t"] / 1e9, 3),
+                   "bytes_sent_per_step": runs[a]["sent"], "transport": runs[a]["transport"],
+                   "busiest_link_GBps": round(lm / runs[a]["t"] / 1e9, 2)}
     if not args.no_alt:
         for other in ("ring_chunked", "ring_chunked_mesh", "halving_doubling"):
-            if other == args.algo:
+            if other in runs:
                 continue
             buf.copy_(src)
             torch.cuda.synchronize()
@@ -397,17 +445,18 @@ def bench_multi(args):
                            "ms_per_step": round(ta * 1e3, 4),
                            "algbw_GBps": round(S / ta / 1e9, 3),
                            "bytes_sent_per_step": sent_a,
+                           "transport": runs[chosen]["transport"],
                            "busiest_link_GBps": round(lm / ta / 1e9, 2)}
     staged = None
     if args.staged:
-        staged = host_endpoint_rate(torch, dist, gloo_amd, ctx, src, dev_result, args.algo,
+        staged = host_endpoint_rate(torch, dist, gloo_amd, ctx, src, dev_result, chosen,
                                     reps=min(steps, 5))
     res = None
     if rank == 0:
         chunk = max(256 * es, -(-S // (2 * world)))
         algbw = S / t / 1e9
         busbw = algbw * 2 * (world - 1) / world
-        link_max = busiest_link_bytes(gloo_amd, args.algo, rank, world, n, es)
+        link_max = busiest_link_bytes(gloo_amd, chosen, rank, world, n, es)
         link_ach = link_max / t / 1e9
         res = {
             "metric": "allreduce GB/s (device-resident, fp32) at 1/2/4/8 MI355X; % HBM|xGMI roofline",
@@ -417,11 +466,16 @@ def bench_multi(args):
             "dtype": args.dtype, "data": "synthetic",
             "config": {"workload": "allreduce_%s_%s_%dMiB_per_rank" % (
                            args.algo, {"f32": "fp32"}.get(args.dtype, args.dtype), args.size_mib),
-                       "algorithm": args.algo, "bytes_per_rank": S, "elements": n,
-                       "parallelism": "dp%d" % world, "transport": "hipMemcpyPeerAsync/xGMI",
-                       "copy_split": split,
-                       "copy_split_calibration_ms": {str(k): round(v * 1e3, 3)
-                                                     for k, v in calib.items()},
+                       "algorithm": args.algo,
+                       "schedule": {"ring_chunked": "ring", "ring_chunked_mesh": "mesh",
+                                    "halving_doubling": "halving_doubling"}[chosen],
+                       "schedule_note": "ring_chunked's chunking and reduction order; ring = "
+                                        "the reference's data movement, mesh = all links "
+                                        "(bit-identical, checked)",
+                       "bytes_per_rank": S, "elements": n,
+                       "parallelism": "dp%d" % world,
+                       "transport": "xGMI peer copies: " + runs[chosen]["transport"],
+                       "transport_calibration_ms": runs[chosen]["calib_ms"],
                        "baseline_config": "configs[3]" if args.algo == "halving_doubling"
                        else "configs[2]"},
             "algbw_GBps": round(algbw, 3), "busbw_GBps": round(busbw, 3),

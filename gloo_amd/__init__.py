@@ -34,6 +34,13 @@ def set_copy_split(k):
     errors.check(_lib.lib.glx_set_copy_split(int(k)), "set_copy_split")
 
 
+def set_copy_engine(engine, blocks=0):
+    """Peer copies of algorithms created afterwards: "dma" (hipMemcpyPeerAsync,
+    default) or "kernel" (a copy kernel storing over xGMI, `blocks` workgroups)."""
+    code = {"dma": 0, "kernel": 1}[engine]
+    errors.check(_lib.lib.glx_set_copy_engine(code, int(blocks)), "set_copy_engine")
+
+
 def device_count():
     import ctypes
     n = ctypes.c_int(0)

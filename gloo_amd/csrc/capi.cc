@@ -166,6 +166,13 @@ int glx_tune_reduce(int unroll, int blocks_per_cu, int nontemporal) {
   return GLX_OK;
 }
 
+int glx_set_copy_engine(int engine, int blocks) {
+  if (engine != 0 && engine != 1) return fail(GLX_ERR_INVALID, "copy engine must be 0 or 1");
+  gloo::HipPlanExecutor::setCopyEngine(engine);
+  glx::set_copy_blocks(blocks);
+  return GLX_OK;
+}
+
 int glx_set_copy_split(int k) {
   if (k < 1 || k > 8) return fail(GLX_ERR_INVALID, "glx_set_copy_split: k must be in [1, 8]");
   gloo::HipPlanExecutor::setCopySplit(k);

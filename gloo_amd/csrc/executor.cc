@@ -49,6 +49,13 @@ int initialSplit() {
 
 std::atomic<int> g_copy_split{initialSplit()};
 
+int initialEngine() {
+  const char* e = std::getenv("GLOO_AMD_COPY_ENGINE");
+  return (e != nullptr && std::strcmp(e, "kernel") == 0) ? 1 : 0;
+}
+
+std::atomic<int> g_copy_engine{initialEngine()};
+
 // GLOO_AMD_TRACE=1: one stderr line per executor step / runtime call.
 const bool g_trace = [] {
   const char* e = std::getenv("GLOO_AMD_TRACE");
@@ -94,6 +101,10 @@ void HipPlanExecutor::setCopySplit(int k) {
 
 int HipPlanExecutor::copySplit() { return g_copy_split.load(); }
 
+void HipPlanExecutor::setCopyEngine(int engine) { g_copy_engine.store(engine == 1 ? 1 : 0); }
+
+int HipPlanExecutor::copyEngine() { return g_copy_engine.load(); }
+
 HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
                                  const std::vector<void*>& ptrs, int64_t count,
                                  int dtype, int op,
@@ -127,6 +138,7 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
     ownCompute_ = true;
   }
   split_ = std::max(1, std::min(copySplit(), (int)kMaxSplit));
+  copyEngine_ = copyEngine();
 
   hostMode_ = count_ > 0 && isHostPointer(ptrs[0]);
   for (void* p : ptrs) {
@@ -701,7 +713,10 @@ void HipPlanExecutor::exchange(char* ptr0) {
             }
             if (hostMode_) waitH2D(cs.s, cs.h2dWaited, s.off, s.len);
             hipError_t ce = hipErrorUnknown;
-            if (peerCopyOk_ && oc.peerDevice >= 0 && oc.peerDevice != device_) {
+            if (copyEngine_ == kCopyKernel) {
+              ce = glx::launch_copy(dst + at, src + at, len, cs.s);
+              GLX_HIP_CHECK(ce);
+            } else if (peerCopyOk_ && oc.peerDevice >= 0 && oc.peerDevice != device_) {
               ce = hipMemcpyPeerAsync(dst + at, oc.peerDevice, src + at, device_, len, cs.s);
               if (ce != hipSuccess) {
                 (void)hipGetLastError();

@@ -70,6 +70,12 @@ class HipPlanExecutor : public Algorithm {
   // (several DMA engines feeding one link).  Read at construction.
   static void setCopySplit(int k);
   static int copySplit();
+  // How a SEND moves its bytes: kCopyDma = hipMemcpyPeerAsync (copy
+  // engines), kCopyKernel = a copy kernel storing into the peer's memory
+  // over xGMI.  Read at construction.
+  static constexpr int kCopyDma = 0, kCopyKernel = 1;
+  static void setCopyEngine(int engine);
+  static int copyEngine();
   const glx::Plan& plan() const { return plan_; }
 
  private:
@@ -146,6 +152,7 @@ class HipPlanExecutor : public Algorithm {
   std::vector<CopyStream> copies_;
   uint64_t markEpoch_ = 0;
   int split_ = 1;
+  int copyEngine_ = kCopyDma;
   bool peerCopyOk_ = true;  // hipMemcpyPeerAsync accepted for IPC-mapped peers
   bool ownCompute_ = false;
   std::vector<ScratchBlock> blocks_;                  // ours

@@ -16,6 +16,13 @@ hipError_t launch_reduce(int op, int dtype, void* dst, const void* a,
 hipError_t launch_reduce_n(int op, int dtype, void* dst, const void* const* srcs,
                            int k, size_t n, hipStream_t s, bool rev = false);
 
+// Byte copy dst <- src as a kernel on stream s (dst may be a peer GPU's
+// IPC-mapped memory: the stores then travel over xGMI).  Never synchronises.
+hipError_t launch_copy(void* dst, const void* src, size_t bytes, hipStream_t s);
+// Grid (workgroups) of the copy kernel.
+void set_copy_blocks(int blocks);
+int copy_blocks();
+
 // Tuning knobs of the vector kernel (lanes' unroll depth, grid cap per CU,
 // nontemporal loads/stores: 0/1, -1 = keep).
 void set_reduce_tuning(int unroll, int blocks_per_cu, int nontemporal);

@@ -350,6 +350,49 @@ __global__ __launch_bounds__(kBlock) void reduce_n_scalar_kernel(
   }
 }
 
+// ---- peer copy ------------------------------------------------------------
+// The chunk exchange as a kernel instead of a DMA (SDMA) copy: the lanes of
+// the sending GPU store 16-byte vectors straight into the peer's receive
+// region through its IPC-mapped address, so the copy runs over xGMI at the
+// rate of the compute units' remote stores rather than one copy engine's.
+// Nontemporal loads (the source is read once); plain stores (they leave the
+// GPU).  The first lanes move the unaligned head and tail bytes.
+template <int UNROLL>
+__global__ __launch_bounds__(kBlock) void copy_kernel(char* __restrict__ dst,
+                                                      const char* __restrict__ src,
+                                                      size_t head, size_t nvec, size_t tail) {
+  const size_t gtid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  if (gtid < head) dst[gtid] = src[gtid];
+  const size_t tail_at = head + nvec * 16;
+  if (gtid < tail) dst[tail_at + gtid] = src[tail_at + gtid];
+  const v4u* vs = reinterpret_cast<const v4u*>(src + head);
+  v4u* vd = reinterpret_cast<v4u*>(dst + head);
+  const size_t stride = (size_t)gridDim.x * kBlock * UNROLL;
+  for (size_t base = (size_t)blockIdx.x * kBlock * UNROLL + threadIdx.x; base < nvec;
+       base += stride) {
+    v4u x[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) {
+      size_t i = base + (size_t)u * kBlock;
+      if (i < nvec) x[u] = ld16<true>(vs + i);
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) {
+      size_t i = base + (size_t)u * kBlock;
+      if (i < nvec) st16<false>(vd + i, x[u]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void copy_bytes_kernel(char* __restrict__ dst,
+                                                            const char* __restrict__ src,
+                                                            size_t n) {
+  const size_t step = (size_t)gridDim.x * kBlock;
+  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += step) dst[i] = src[i];
+}
+
+int g_copy_blocks = 64;  // grid of the copy kernel (workgroups)
+
 // ---- launch ---------------------------------------------------------------
 
 int g_unroll = 4;         // tuned on MI355X: tools/tune_reduce.py, profiles/r1_tune_reduce_nt.log
@@ -504,6 +547,30 @@ hipError_t launch_n_op(int op, void* dst, const void* const* srcs, int k,
 }
 
 }  // namespace
+
+hipError_t launch_copy(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return hipSuccess;
+  const uintptr_t pd = (uintptr_t)dst, ps = (uintptr_t)src;
+  const unsigned blocks = (unsigned)std::max(1, g_copy_blocks);
+  if (pd % 16 != ps % 16) {
+    hipLaunchKernelGGL(copy_bytes_kernel, dim3(blocks), dim3(kBlock), 0, s, (char*)dst,
+                       (const char*)src, bytes);
+    return hipGetLastError();
+  }
+  size_t head = (16 - pd % 16) % 16;
+  if (head > bytes) head = bytes;
+  const size_t nvec = (bytes - head) / 16;
+  const size_t tail = bytes - head - nvec * 16;
+  hipLaunchKernelGGL((copy_kernel<4>), dim3(blocks), dim3(kBlock), 0, s, (char*)dst,
+                     (const char*)src, head, nvec, tail);
+  return hipGetLastError();
+}
+
+void set_copy_blocks(int blocks) {
+  if (blocks > 0) g_copy_blocks = blocks;
+}
+
+int copy_blocks() { return g_copy_blocks; }
 
 hipError_t launch_reduce(int op, int dtype, void* dst, const void* a,
                          const void* b, size_t n, hipStream_t s) {

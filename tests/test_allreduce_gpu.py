@@ -265,3 +265,27 @@ def test_split_peer_copies(algo, split):
         gloo_amd.set_copy_split(1)
     ref_algo = O.HALVING_DOUBLING if algo == O.HALVING_DOUBLING else O.RING_CHUNKED
     check_all(out, O.allreduce(ref_algo, O.SUM, O.FLOAT32, ins), O.FLOAT32, O.SUM)
+
+
+@pytest.mark.parametrize("split", [1, 2])
+@pytest.mark.parametrize("algo", [O.RING_CHUNKED, O.HALVING_DOUBLING, MESH],
+                         ids=["ring_chunked", "halving_doubling", "mesh"])
+def test_kernel_copy_engine(algo, split):
+    """Peer copies made by the xGMI copy kernel instead of the DMA engines:
+    same bits, including unaligned chunk boundaries (odd N)."""
+    import gloo_amd
+    P, N = 4, (3 << 20) // 4 + 13
+    ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=9)
+    gloo_amd.set_copy_engine("kernel", blocks=16)
+    gloo_amd.set_copy_split(split)
+    try:
+        out = gpu_allreduce(algo, O.SUM, O.FLOAT32, ins, runs=2)
+        out16 = gpu_allreduce(algo, O.SUM, O.FLOAT16,
+                              case_inputs(3, 1001, O.FLOAT16, 1, 0, seed=2))
+    finally:
+        gloo_amd.set_copy_engine("dma", blocks=64)
+        gloo_amd.set_copy_split(1)
+    ref_algo = O.HALVING_DOUBLING if algo == O.HALVING_DOUBLING else O.RING_CHUNKED
+    check_all(out, O.allreduce(ref_algo, O.SUM, O.FLOAT32, ins), O.FLOAT32, O.SUM)
+    ins16 = case_inputs(3, 1001, O.FLOAT16, 1, 0, seed=2)
+    check_all(out16, O.allreduce(ref_algo, O.SUM, O.FLOAT16, ins16), O.FLOAT16, O.SUM)
