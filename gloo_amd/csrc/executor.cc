@@ -147,6 +147,30 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
   }
   GLX_ENFORCE(!hostMode_ || !userStream_, "streams cannot be used with host-memory buffers");
   if (hostMode_) setupHostMode();
+  if (!hostMode_ && count_ > 0) {
+    // pointers on other GPUs of this rank (the reference's multi-device
+    // ranks, gloo/cuda_allreduce_ring_chunked.cc): the fold kernel reads them
+    // and the broadcast writes them over xGMI from this rank's device
+    for (void* p : ptrs) {
+      hipPointerAttribute_t a;
+      if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        continue;
+      }
+      if (a.type == hipMemoryTypeDevice && a.device >= 0 && a.device != device_) {
+        int can = 0;
+        GLX_HIP_CHECK(hipDeviceCanAccessPeer(&can, device_, a.device));
+        GLX_ENFORCE(can, "buffer on device ", a.device, " is not reachable from device ",
+                    device_, " (no peer access)");
+        hipError_t e = hipDeviceEnablePeerAccess(a.device, 0);
+        if (e == hipErrorPeerAccessAlreadyEnabled) {
+          (void)hipGetLastError();
+        } else {
+          GLX_HIP_CHECK(e);
+        }
+      }
+    }
+  }
 
   allocScratch();
 

@@ -167,7 +167,10 @@ struct HalfOp {
 // skipped when v.x == half((float)old.x) -- operator!= compares against the
 // old bits read as an integer.  Restated so fp16 results stay bit-exact.
 __device__ __forceinline__ uint16_t f16_assign(uint16_t old, uint16_t v) {
-  return (v == f2h((float)(uint32_t)old)) ? old : v;
+  // (float)old is an integer 0..65535, never NaN: the bare conversion suffices
+  uint32_t g;
+  asm("v_cvt_f16_f32_e32 %0, %1" : "=v"(g) : "v"((float)(uint32_t)old));
+  return (v == (uint16_t)(g & 0xffffu)) ? old : v;
 }
 
 // Storage type and element op for a tag type.  apply3(old, a, b) is the value
@@ -184,7 +187,12 @@ template <int OP> struct Elem<f16_t, OP> {
     if (OP == GLX_SUM || OP == GLX_PRODUCT) v = f16_assign(a, v);  // inside operator+=
     return f16_assign(old, v);                                        // c[i] = ...
   }
-  static __device__ __forceinline__ S apply(S a, S b) { return apply3(a, a, b); }
+  // In place (c == a): the assignment at `c[i] = ...` repeats the one inside
+  // operator+=/*= with the same old value, which cannot change the result
+  // (if the first kept `a`, the second keeps it too), so one suffices.
+  static __device__ __forceinline__ S apply(S a, S b) {
+    return f16_assign(a, HalfOp<f16_t, OP>::apply(a, b));
+  }
 };
 template <int OP> struct Elem<bf16_t, OP> {
   using S = uint16_t;
@@ -211,7 +219,16 @@ __device__ __forceinline__ v4u vec_apply3(v4u vo, v4u va, v4u vb) {
 
 template <typename T, int OP>
 __device__ __forceinline__ v4u vec_apply(v4u va, v4u vb) {
-  return vec_apply3<T, OP>(va, va, vb);
+  using E = Elem<T, OP>;
+  using S = typename E::S;
+  constexpr int V = 16 / sizeof(S);
+  union U { v4u v; S s[V]; };
+  U a, b, c;
+  a.v = va;
+  b.v = vb;
+#pragma unroll
+  for (int i = 0; i < V; i++) c.s[i] = E::apply(a.s[i], b.s[i]);
+  return c.v;
 }
 
 // ---- kernels --------------------------------------------------------------
@@ -231,10 +248,10 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(
   constexpr int V = 16 / sizeof(S);
   const size_t gtid = (size_t)blockIdx.x * kBlock + threadIdx.x;
 
-  if (gtid < head) dst[gtid] = E::apply3(LOADC ? dst[gtid] : a[gtid], a[gtid], b[gtid]);
+  if (gtid < head) dst[gtid] = LOADC ? E::apply3(dst[gtid], a[gtid], b[gtid]) : E::apply(a[gtid], b[gtid]);
   if (gtid < tail) {
     size_t i = head + nvec * V + gtid;
-    dst[i] = E::apply3(LOADC ? dst[i] : a[i], a[i], b[i]);
+    dst[i] = LOADC ? E::apply3(dst[i], a[i], b[i]) : E::apply(a[i], b[i]);
   }
 
   v4u* vd = reinterpret_cast<v4u*>(dst + head);
@@ -256,7 +273,9 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) {
       size_t i = base + (size_t)u * kBlock;
-      if (i < nvec) st16<NT>(vd + i, vec_apply3<T, OP>(LOADC ? z[u] : x[u], x[u], y[u]));
+      if (i < nvec) {
+        st16<NT>(vd + i, LOADC ? vec_apply3<T, OP>(z[u], x[u], y[u]) : vec_apply<T, OP>(x[u], y[u]));
+      }
     }
   }
 }

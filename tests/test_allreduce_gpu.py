@@ -289,3 +289,35 @@ def test_kernel_copy_engine(algo, split):
     check_all(out, O.allreduce(ref_algo, O.SUM, O.FLOAT32, ins), O.FLOAT32, O.SUM)
     ins16 = case_inputs(3, 1001, O.FLOAT16, 1, 0, seed=2)
     check_all(out16, O.allreduce(ref_algo, O.SUM, O.FLOAT16, ins16), O.FLOAT16, O.SUM)
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs in one process")
+@pytest.mark.parametrize("algo", [O.RING_CHUNKED, O.HALVING_DOUBLING],
+                         ids=["ring_chunked", "halving_doubling"])
+def test_multi_device_pointers_in_one_rank(algo):
+    """one rank's pointers on different GPUs (the reference's
+    multi-device CUDA ranks): folded and broadcast over peer access."""
+    import gloo_amd
+    P, N, nptrs = 2, 100003, 2
+    ins = case_inputs(P, N, O.FLOAT32, nptrs, 0, seed=14)
+    store = gloo_amd.rendezvous.HashStore()
+    bufs = [[torch.from_numpy(ins[r][i].copy()).to("cuda:%d" % i) for i in range(nptrs)]
+            for r in range(P)]
+    for d in range(nptrs):
+        torch.cuda.synchronize(d)
+
+    def rank_fn(r):
+        ctx = gloo_amd.rendezvous.Context(r, P, 0)
+        ctx.connectFullMesh(store)
+        cls = (gloo_amd.AllreduceHalvingDoubling if algo == O.HALVING_DOUBLING
+               else gloo_amd.AllreduceRingChunked)
+        alg = cls(ctx, bufs[r])
+        alg.run()
+        alg.close()
+        return True
+
+    run_ranks(P, rank_fn)
+    exp = O.allreduce(algo, O.SUM, O.FLOAT32, ins)
+    for r in range(P):
+        for i in range(nptrs):
+            assert_same(bufs[r][i].cpu().numpy(), exp[r][i], O.FLOAT32, O.SUM)

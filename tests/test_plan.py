@@ -114,3 +114,19 @@ def test_stage_plan_covers_each_element_once(algo, P, N):
         if touching:
             st = touching[0]
             assert h2d[0][0] <= st[3] < h2d[0][0] + h2d[0][1]
+
+
+@pytest.mark.parametrize("algo,P", [(O.HALVING_DOUBLING, 24), (O.HALVING_DOUBLING, 32),
+                                    (O.RING_CHUNKED, 15), (O.RING_CHUNKED, 11)])
+@pytest.mark.parametrize("N", [0, 1, 64, 1000])
+def test_plan_replay_reference_test_sizes(algo, P, N):
+    """The largest context sizes of gloo/test/allreduce_test.cc:251-269
+    (HD up to 32 ranks, ring_chunked up to 15), value = rank pattern."""
+    ins = case_inputs(P, N, O.FLOAT32, 1, 2)
+    plans = [gloo_amd.plan(NAMES[algo], r, P, N) for r in range(P)]
+    got = replay_plans(plans, O.SUM, O.FLOAT32, [ins[r][0] for r in range(P)])
+    for r in range(P):
+        assert (got[r] == P * (P - 1) / 2).all()
+    exp = O.allreduce(algo, O.SUM, O.FLOAT32, ins)
+    for r in range(P):
+        assert same_bits(got[r], exp[r][0])
