@@ -53,6 +53,9 @@ def parse():
     p.add_argument("--staged", action="store_true", default=True,
                    help="also time the host-staged (H2D + op + D2H) rate")
     p.add_argument("--no-staged", dest="staged", action="store_false")
+    p.add_argument("--sweep", action="store_true", default=True,
+                   help="N>1: also time configs[2]'s 1K..16M element sweep")
+    p.add_argument("--no-sweep", dest="sweep", action="store_false")
     p.add_argument("--watchdog", type=float, default=900.0,
                    help="seconds before dumping stacks and exiting")
     p.add_argument("--kernel-only", action="store_true",
@@ -332,6 +335,26 @@ def host_endpoint_rate(torch, dist, gloo_amd, ctx, src, dev_result, algo, reps):
                     "overlapped with the schedule, per-range D2H after final writes"}
 
 
+SWEEP_ELEMS = [1 << 10, 1 << 12, 1 << 14, 1 << 16, 1 << 18, 1 << 20, 1 << 22, 1 << 24]
+
+
+def element_sweep(torch, dist, gloo_amd, ctx, dev, schedules, dtype):
+    """configs[2]'s element sweep (1K..16M elements per rank): per size and
+    schedule, us per allreduce (max over ranks) and algbw.  Iterations shrink
+    with size so the whole sweep stays within seconds."""
+    out = {}
+    for n in SWEEP_ELEMS:
+        x = synthetic(torch, n, dtype, dev, 77)
+        row = {}
+        for sched in schedules:
+            iters = 20 if n <= (1 << 20) else 5
+            t, _ = time_schedule(torch, dist, gloo_amd, ctx, x, sched, iters, 2)
+            row[sched] = {"us": round(t * 1e6, 1),
+                          "algbw_GBps": round(n * x.element_size() / t / 1e9, 3)}
+        out[str(n)] = row
+    return out
+
+
 def bench_multi(args):
     import torch
     import torch.distributed as dist
@@ -451,6 +474,9 @@ def bench_multi(args):
     if args.staged:
         staged = host_endpoint_rate(torch, dist, gloo_amd, ctx, src, dev_result, chosen,
                                     reps=min(steps, 5))
+    sweep = None
+    if args.sweep:
+        sweep = element_sweep(torch, dist, gloo_amd, ctx, dev, candidates, args.dtype)
     res = None
     if rank == 0:
         chunk = max(256 * es, -(-S // (2 * world)))
@@ -489,6 +515,7 @@ def bench_multi(args):
                                       "(ring: everything on rank->rank+1; mesh: 1/(P-1) "
                                       "per peer link)"},
             "alt_schedules": alts,
+            "sweep": sweep,
             "verified": verified,
         }
         if staged is not None:

@@ -116,7 +116,9 @@ def _stream_ptr(s):
 
 ALGO_CODES = {"ring_chunked": 0, "halving_doubling": 1, "ring_chunked_mesh": 2,
               # schedules of gloo_amd.allreduce (plan introspection)
-              "fn_ring": 3, "fn_ring_mesh": 4, "fn_bcube": 5}
+              "fn_ring": 3, "fn_ring_mesh": 4, "fn_bcube": 5,
+              # one-round variants for small buffers
+              "ring_chunked_repl": 6, "fn_ring_repl": 7}
 
 
 class Algorithm:
@@ -180,13 +182,18 @@ class AllreduceRingChunked(Algorithm):
     schedule="ring" (default) moves chunks around the ring exactly as the
     reference does (one link per direction); schedule="mesh" computes the
     identical result (same chunks, same reduction chain and operand order)
-    with every rank exchanging directly with every peer over all links."""
+    with every rank exchanging directly with every peer over all links;
+    schedule="replicated" (small buffers) computes it in one round: every
+    rank receives every peer's buffer and evaluates all chains itself."""
+
+    SCHEDULES = {"ring": "ring_chunked", "mesh": "ring_chunked_mesh",
+                 "replicated": "ring_chunked_repl"}
 
     def __init__(self, context, ptrs, count=None, fn=None, streams=None, dtype=None,
                  schedule="ring"):
-        if schedule not in ("ring", "mesh"):
-            raise ValueError("schedule must be 'ring' or 'mesh'")
-        self._algo = ALGO_CODES["ring_chunked_mesh" if schedule == "mesh" else "ring_chunked"]
+        if schedule not in self.SCHEDULES:
+            raise ValueError("schedule must be one of %s" % sorted(self.SCHEDULES))
+        self._algo = ALGO_CODES[self.SCHEDULES[schedule]]
         self.schedule = schedule
         super().__init__(context, ptrs, count, fn, streams, dtype)
 

@@ -784,24 +784,51 @@ void HipPlanExecutor::exchange(char* ptr0) {
         break;
       }
       case glx::FOLD: {
-        waitWar(s.off, s.len);
-        if (hostMode_) waitH2D(compute_, computeH2dWaited_, s.off, s.len);
-        char* dst = ptr0 + (size_t)s.off * esize_;
-        const auto& regions = plan_.folds[(size_t)s.boff];
-        std::vector<const void*> srcs;
-        for (int64_t r : regions) {
-          srcs.push_back(r < 0 ? (const void*)dst
-                               : (const void*)landing(blocks_, r, s.off));
+        // consecutive FOLD steps of the same kind go out as one batched launch
+        size_t last = i;
+        while (last + 1 < steps.size() && steps[last + 1].kind == glx::FOLD &&
+               steps[last + 1].flags == s.flags) {
+          last++;
         }
         const bool rev = (s.flags & glx::kFoldLeft) == 0;  // ring chain vs left fold
-        GLX_HIP_CHECK(glx::launch_reduce_n(op_, dtype_, dst, srcs.data(), (int)srcs.size(),
-                                           (size_t)s.len, compute_, rev));
-        computeSinceMark = true;
-        if (hostMode_ && !stage_.d2h[i].empty()) {  // final values: copy back now
-          GLX_HIP_CHECK(hipEventRecord(d2hEvents_[i], compute_));
-          GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, d2hEvents_[i], 0));
-          copyBack(stage_.d2h[i]);
+        const bool whole = (s.flags & glx::kFoldWhole) != 0;
+        std::vector<glx::FoldSpec> specs;
+        for (size_t q = i; q <= last; q++) {
+          const glx::Step& f = steps[q];
+          waitWar(f.off, f.len);
+          if (hostMode_) waitH2D(compute_, computeH2dWaited_, f.off, f.len);
+          char* dst = ptr0 + (size_t)f.off * esize_;
+          glx::FoldSpec spec;
+          spec.dst = dst;
+          spec.n = (size_t)f.len;
+          for (int64_t r : plan_.folds[(size_t)f.boff]) {
+            if (r < 0) {
+              spec.srcs.push_back(dst);
+            } else if (whole) {  // whole-buffer message: element off is off into it
+              spec.srcs.push_back(landing(blocks_, r, 0) + (size_t)f.off * esize_);
+            } else {
+              spec.srcs.push_back(landing(blocks_, r, f.off));
+            }
+          }
+          spec.k = (int)spec.srcs.size();
+          specs.push_back(std::move(spec));
         }
+        if (specs.size() == 1) {
+          const glx::FoldSpec& f = specs[0];
+          GLX_HIP_CHECK(glx::launch_reduce_n(op_, dtype_, f.dst, f.srcs.data(), f.k, f.n,
+                                             compute_, rev));
+        } else {
+          GLX_HIP_CHECK(glx::launch_reduce_n_batch(op_, dtype_, specs, compute_, rev));
+        }
+        computeSinceMark = true;
+        for (size_t q = i; q <= last; q++) {
+          if (hostMode_ && !stage_.d2h[q].empty()) {  // final values: copy back now
+            GLX_HIP_CHECK(hipEventRecord(d2hEvents_[q], compute_));
+            GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, d2hEvents_[q], 0));
+            copyBack(stage_.d2h[q]);
+          }
+        }
+        i = last;
         break;
       }
       case glx::COPY: {

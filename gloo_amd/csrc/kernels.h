@@ -4,6 +4,8 @@
 #include <hip/hip_runtime_api.h>
 #include <stddef.h>
 
+#include <vector>
+
 namespace glx {
 
 // dst = op(a, b), n elements of dtype, on stream s.  Never synchronises.
@@ -15,6 +17,16 @@ hipError_t launch_reduce(int op, int dtype, void* dst, const void* a,
 // (rev = true, the ring's chain order).  dst may alias srcs[0].
 hipError_t launch_reduce_n(int op, int dtype, void* dst, const void* const* srcs,
                            int k, size_t n, hipStream_t s, bool rev = false);
+
+// Several independent folds (same op/dtype/order) in one launch.
+struct FoldSpec {
+  void* dst;
+  std::vector<const void*> srcs;
+  int k;
+  size_t n;
+};
+hipError_t launch_reduce_n_batch(int op, int dtype, const std::vector<FoldSpec>& specs,
+                                 hipStream_t s, bool rev);
 
 // Byte copy dst <- src as a kernel on stream s (dst may be a peer GPU's
 // IPC-mapped memory: the stores then travel over xGMI).  Never synchronises.

@@ -350,6 +350,37 @@ Plan meshPlan(int rank, int size, Range range, Chain chain) {
 
 }  // namespace
 
+// Replicated: every rank folds every owner's range from all P copies.
+template <typename Range, typename Chain>
+Plan replicatedPlan(int rank, int size, int64_t count, Range range, Chain chain) {
+  Plan p;
+  const int64_t region = count + kPadElems;
+  p.scratch_elems = (int64_t)size * region;  // one whole-buffer region per source rank
+  for (int d = 1; d < size; d++) {
+    const int j = (rank + d) % size;
+    p.steps.push_back({SEND, j, 2, 0, count, 0, (int64_t)rank * region, 0});
+    p.bytes_sent += count;
+  }
+  for (int d = 1; d < size; d++) {
+    const int k = (rank - d + size) % size;
+    p.steps.push_back({RECV, k, 2, 0, count, (int64_t)k * region, 0, 0});
+  }
+  for (int c = 0; c < size; c++) {
+    int64_t off, len;
+    range(c, &off, &len);
+    if (len == 0) continue;
+    std::vector<int64_t> srcs;
+    for (int from : chain(c)) srcs.push_back(from == rank ? -1 : (int64_t)from * region);
+    p.folds.push_back(srcs);
+    p.steps.push_back({FOLD, -1, (int64_t)srcs.size(), off, len,
+                       (int64_t)p.folds.size() - 1, 0, kFoldWhole});
+  }
+  for (int d = 1; d < size; d++) {
+    p.steps.push_back({RELEASE, (rank - d + size) % size, 2, 0, 0, 0, 0, 0});
+  }
+  return p;
+}
+
 // ring_chunked (gloo/allreduce_ring_chunked.h:106-158) reduces chunk pair j
 // (chunks 2j, 2j+1) along ranks j, j+1, ..., j+P-1: rank j+k computes
 // op(x[j+k], partial) in place.  The broadcast pass (:163-200) becomes the
@@ -369,6 +400,23 @@ Plan planRingChunkedMesh(int rank, int size, int64_t count) {
     return v;
   };
   return meshPlan(rank, size, pair, chain);
+}
+
+Plan planRingChunkedReplicated(int rank, int size, int64_t count) {
+  if (count == 0 || size == 1) return Plan();
+  const int64_t chunks = 2 * (int64_t)size;
+  const int64_t chunkSize = std::max<int64_t>(256, (count + chunks - 1) / chunks);
+  auto pair = [&](int j, int64_t* off, int64_t* len) {
+    int64_t o = 2 * (int64_t)j * chunkSize;
+    *off = o;
+    *len = o < count ? std::min(2 * chunkSize, count - o) : 0;
+  };
+  auto chain = [&](int j) {
+    std::vector<int> v;
+    for (int k = 0; k < size; k++) v.push_back((j + k) % size);
+    return v;
+  };
+  return replicatedPlan(rank, size, count, pair, chain);
 }
 
 // ---------------------------------------------------------------------------
@@ -503,6 +551,22 @@ Plan planFnRingMesh(int rank, int size, int64_t count, const PlanParams& prm) {
     return v;
   };
   return meshPlan(rank, size, range, chain);
+}
+
+Plan planFnRingReplicated(int rank, int size, int64_t count, const PlanParams& prm) {
+  if (count == 0 || size == 1) return Plan();
+  const FnRingGeom g = fnRingGeom(size, count, prm);
+  auto range = [&](int c, int64_t* off, int64_t* len) {
+    const int64_t o = (int64_t)c * g.chunkE;
+    *off = o;
+    *len = o < count ? std::min(g.chunkE, count - o) : 0;
+  };
+  auto chain = [&](int c) {
+    std::vector<int> v;
+    for (int k = 1; k <= size; k++) v.push_back((c - k + 2 * size) % size);
+    return v;
+  };
+  return replicatedPlan(rank, size, count, range, chain);
 }
 
 // ---------------------------------------------------------------------------
@@ -646,6 +710,8 @@ Plan makePlan(int algo, int rank, int size, int64_t count, const PlanParams& prm
     case ALGO_FN_RING: return planFnRing(rank, size, count, prm);
     case ALGO_FN_RING_MESH: return planFnRingMesh(rank, size, count, prm);
     case ALGO_FN_BCUBE: return planFnBcube(rank, size, count);
+    case ALGO_RING_CHUNKED_REPL: return planRingChunkedReplicated(rank, size, count);
+    case ALGO_FN_RING_REPL: return planFnRingReplicated(rank, size, count, prm);
   }
   fail("unknown algorithm");
   return Plan();

@@ -58,9 +58,14 @@ enum Algo {
   ALGO_FN_RING = 3,            // gloo::allreduce(opts), Algorithm::RING
   ALGO_FN_RING_MESH = 4,       // its result over all links
   ALGO_FN_BCUBE = 5,           // gloo::allreduce(opts), Algorithm::BCUBE
+  ALGO_RING_CHUNKED_REPL = 6,  // ring_chunked's result in one round (small buffers)
+  ALGO_FN_RING_REPL = 7,       // RING's result in one round (small buffers)
 };
 
 constexpr int64_t kFoldLeft = 1;  // FOLD flag, see above
+// FOLD flag: the source regions hold whole-buffer messages (sent from
+// element 0), so s[i] for ptr0[off...] sits `off` elements into region i.
+constexpr int64_t kFoldWhole = 2;
 
 // gloo/allreduce.h:80 (AllreduceOptionsImpl::kMaxSegmentSize)
 constexpr int64_t kMaxSegmentBytes = 1 << 20;
@@ -96,6 +101,13 @@ Plan planFnRing(int rank, int size, int64_t count, const PlanParams& prm);
 // The same chunks and reduction chains, each owner folding its chunk from
 // all peers at once.
 Plan planFnRingMesh(int rank, int size, int64_t count, const PlanParams& prm);
+// One-round ("replicated") variants for small buffers: every rank sends its
+// whole buffer to every peer and evaluates every chunk's reduction chain
+// itself (one batched fold launch).  Same chains as the ring, so the same
+// bits; (P-1)·S bytes out per rank, one dependent round instead of 4P-4.
+Plan planRingChunkedReplicated(int rank, int size, int64_t count);
+Plan planFnRingReplicated(int rank, int size, int64_t count, const PlanParams& prm);
+
 // gloo/allreduce.cc:395-669 (bcube, n = 2)
 Plan planFnBcube(int rank, int size, int64_t count);
 

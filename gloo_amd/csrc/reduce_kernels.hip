@@ -356,6 +356,46 @@ __global__ __launch_bounds__(kBlock) void reduce_n_kernel(
   }
 }
 
+// Several independent folds in one launch (blockIdx.y = job): the
+// replicated schedule folds every chunk of the buffer, each in its own
+// operand order, and one launch costs less than P back-to-back ones.
+constexpr int kMaxJobs = 8;
+struct FoldJob {
+  void* dst;
+  const void* p[kMaxSrc];
+  int k;
+  size_t head, nvec, tail;  // head/tail elements done scalar (head = n: all scalar)
+};
+struct FoldJobs { FoldJob j[kMaxJobs]; };
+
+template <typename T, int OP, bool REV>
+__global__ __launch_bounds__(kBlock) void reduce_n_batch_kernel(FoldJobs jobs) {
+  using E = Elem<T, OP>;
+  using S = typename E::S;
+  constexpr int V = 16 / sizeof(S);
+  const FoldJob& jb = jobs.j[blockIdx.y];
+  S* dst = reinterpret_cast<S*>(jb.dst);
+  auto src = [&](int j) { return reinterpret_cast<const S*>(jb.p[j]); };
+  const size_t gstep = (size_t)gridDim.x * kBlock;
+  const size_t gtid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  const size_t tail_at = jb.head + jb.nvec * V;
+  for (size_t t = gtid; t < jb.head + jb.tail; t += gstep) {
+    const size_t i = t < jb.head ? t : tail_at + (t - jb.head);
+    S acc = src(0)[i];
+    for (int j = 1; j < jb.k; j++) acc = fold_step<T, OP, REV>(acc, src(j)[i]);
+    dst[i] = acc;
+  }
+  v4u* vd = reinterpret_cast<v4u*>(dst + jb.head);
+  for (size_t i = gtid; i < jb.nvec; i += gstep) {
+    v4u acc = ld16<true>(reinterpret_cast<const v4u*>(src(0) + jb.head) + i);
+    for (int j = 1; j < jb.k; j++) {
+      v4u y = ld16<true>(reinterpret_cast<const v4u*>(src(j) + jb.head) + i);
+      acc = REV ? vec_apply<T, OP>(y, acc) : vec_apply<T, OP>(acc, y);
+    }
+    st16<true>(vd + i, acc);
+  }
+}
+
 template <typename T, int OP, bool REV>
 __global__ __launch_bounds__(kBlock) void reduce_n_scalar_kernel(
     typename Elem<T, OP>::S* dst, SrcPtrs srcs, int k, size_t n) {
@@ -553,6 +593,70 @@ hipError_t launch_n_typed(void* dst, const void* const* srcs, int k, size_t n,
   return e;
 }
 
+template <typename T, int OP>
+hipError_t launch_batch_typed(const FoldJobs& jobs, int njobs, size_t max_work, bool rev,
+                              hipStream_t s) {
+  size_t bx = (max_work + kBlock - 1) / kBlock;
+  size_t cap = (size_t)num_cus() * 8;
+  if (bx > cap) bx = cap;
+  if (bx == 0) bx = 1;
+  dim3 grid((unsigned)bx, (unsigned)njobs);
+  if (rev) {
+    hipLaunchKernelGGL((reduce_n_batch_kernel<T, OP, true>), grid, dim3(kBlock), 0, s, jobs);
+  } else {
+    hipLaunchKernelGGL((reduce_n_batch_kernel<T, OP, false>), grid, dim3(kBlock), 0, s, jobs);
+  }
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_batch_op(int op, const std::vector<FoldSpec>& specs, bool rev,
+                           hipStream_t s) {
+  using S = typename Elem<T, GLX_SUM>::S;
+  constexpr size_t es = sizeof(S);
+  constexpr size_t V = 16 / es;
+  for (size_t at = 0; at < specs.size(); at += kMaxJobs) {
+    FoldJobs jobs{};
+    int nj = 0;
+    size_t max_work = 1;
+    for (size_t q = at; q < specs.size() && q < at + kMaxJobs; q++) {
+      const FoldSpec& f = specs[q];
+      if (f.n == 0) continue;
+      if (f.k < 1 || f.k > kMaxSrc) return hipErrorInvalidValue;
+      FoldJob& jb = jobs.j[nj++];
+      jb.dst = f.dst;
+      jb.k = f.k;
+      uintptr_t phase = (uintptr_t)f.dst % 16;
+      bool same = ((uintptr_t)f.dst % es) == 0;
+      for (int j = 0; j < f.k; j++) {
+        jb.p[j] = f.srcs[j];
+        same = same && ((uintptr_t)f.srcs[j] % 16) == phase;
+      }
+      if (same) {
+        jb.head = ((16 - phase) % 16) / es;
+        if (jb.head > f.n) jb.head = f.n;
+        jb.nvec = (f.n - jb.head) / V;
+        jb.tail = f.n - jb.head - jb.nvec * V;
+      } else {
+        jb.head = f.n;
+        jb.nvec = 0;
+        jb.tail = 0;
+      }
+      max_work = std::max(max_work, std::max(jb.nvec, jb.head + jb.tail));
+    }
+    if (nj == 0) continue;
+    hipError_t e = hipErrorInvalidValue;
+    switch (op) {
+      case GLX_SUM: e = launch_batch_typed<T, GLX_SUM>(jobs, nj, max_work, rev, s); break;
+      case GLX_PRODUCT: e = launch_batch_typed<T, GLX_PRODUCT>(jobs, nj, max_work, rev, s); break;
+      case GLX_MAX: e = launch_batch_typed<T, GLX_MAX>(jobs, nj, max_work, rev, s); break;
+      case GLX_MIN: e = launch_batch_typed<T, GLX_MIN>(jobs, nj, max_work, rev, s); break;
+    }
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 template <typename T>
 hipError_t launch_n_op(int op, void* dst, const void* const* srcs, int k,
                        size_t n, hipStream_t s, bool rev) {
@@ -604,6 +708,31 @@ hipError_t launch_reduce(int op, int dtype, void* dst, const void* a,
     case GLX_FLOAT64: return launch_op<double>(op, dst, a, b, n, s);
     case GLX_FLOAT16: return launch_op<f16_t>(op, dst, a, b, n, s);
     case GLX_BFLOAT16: return launch_op<bf16_t>(op, dst, a, b, n, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_reduce_n_batch(int op, int dtype, const std::vector<FoldSpec>& specs,
+                                 hipStream_t s, bool rev) {
+  for (const FoldSpec& f : specs) {
+    if (f.k > kMaxSrc) {  // rare: fall back to one multi-pass fold each
+      for (const FoldSpec& g : specs) {
+        hipError_t e = launch_reduce_n(op, dtype, g.dst, g.srcs.data(), g.k, g.n, s, rev);
+        if (e != hipSuccess) return e;
+      }
+      return hipSuccess;
+    }
+  }
+  switch (dtype) {
+    case GLX_INT8: return launch_batch_op<int8_t>(op, specs, rev, s);
+    case GLX_UINT8: return launch_batch_op<uint8_t>(op, specs, rev, s);
+    case GLX_INT32: return launch_batch_op<int32_t>(op, specs, rev, s);
+    case GLX_INT64: return launch_batch_op<int64_t>(op, specs, rev, s);
+    case GLX_UINT64: return launch_batch_op<uint64_t>(op, specs, rev, s);
+    case GLX_FLOAT32: return launch_batch_op<float>(op, specs, rev, s);
+    case GLX_FLOAT64: return launch_batch_op<double>(op, specs, rev, s);
+    case GLX_FLOAT16: return launch_batch_op<f16_t>(op, specs, rev, s);
+    case GLX_BFLOAT16: return launch_batch_op<bf16_t>(op, specs, rev, s);
   }
   return hipErrorInvalidValue;
 }

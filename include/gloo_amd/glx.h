@@ -200,7 +200,11 @@ enum glx_algo {
   /* schedules of glx_allreduce (plan introspection only) */
   GLX_ALGO_FN_RING = 3,
   GLX_ALGO_FN_RING_MESH = 4,
-  GLX_ALGO_FN_BCUBE = 5
+  GLX_ALGO_FN_BCUBE = 5,
+  /* one round for small buffers: every rank receives every peer's whole
+   * buffer and folds every chunk in the ring's own order (bit-identical) */
+  GLX_ALGO_RING_CHUNKED_REPL = 6,
+  GLX_ALGO_FN_RING_REPL = 7
 };
 glx_algorithm* glx_allreduce_create(glx_context* ctx, int algo, void* const* ptrs,
                                     int nptrs, int count, int dtype, int op,

@@ -127,11 +127,13 @@ def replay_plans(plans, op, dtype, inputs):
                 elif kind == 5:  # FOLD: acc = s0; acc = op(s_k, acc) (or op(acc, s_k))
                     srcs = plans[r][2][boff]
                     left = bool(steps[pc[r]][7] & 1)
+                    whole = bool(steps[pc[r]][7] & 2)  # whole-buffer source regions
 
-                    def val(reg, r=r, off=off, ln=ln):
+                    def val(reg, r=r, off=off, ln=ln, whole=whole):
                         if reg == -1:
                             return np.array(data[r][off:off + ln], copy=True)
-                        return scratch[r][reg:reg + ln]
+                        at = reg + off if whole else reg
+                        return scratch[r][at:at + ln]
                     acc = np.array(val(srcs[0]), copy=True)
                     for reg in srcs[1:]:
                         acc = (O.reduce(op, dtype, acc, val(reg)) if left

@@ -26,6 +26,7 @@ ALGOS = {O.RING_CHUNKED: "AllreduceRingChunked", O.HALVING_DOUBLING: "AllreduceH
 
 
 MESH = 2  # ring_chunked semantics, mesh schedule
+REPL = 6  # ring_chunked semantics, one-round replicated schedule
 
 
 def gpu_allreduce(algo, op, dtype, inputs, runs=1, streams=False, timeout_s=60,
@@ -39,9 +40,10 @@ def gpu_allreduce(algo, op, dtype, inputs, runs=1, streams=False, timeout_s=60,
     torch.cuda.synchronize()
     fn = {O.SUM: gloo_amd.ReductionFunction.sum, O.PRODUCT: gloo_amd.ReductionFunction.product,
           O.MAX: gloo_amd.ReductionFunction.max, O.MIN: gloo_amd.ReductionFunction.min}[op]
-    if algo == MESH:
+    if algo in (MESH, REPL):
         def cls(*a, **kw):
-            return gloo_amd.AllreduceRingChunked(*a, schedule="mesh", **kw)
+            return gloo_amd.AllreduceRingChunked(
+                *a, schedule="mesh" if algo == MESH else "replicated", **kw)
     else:
         cls = getattr(gloo_amd, ALGOS[algo])
 
@@ -321,3 +323,22 @@ def test_multi_device_pointers_in_one_rank(algo):
     for r in range(P):
         for i in range(nptrs):
             assert_same(bufs[r][i].cpu().numpy(), exp[r][i], O.FLOAT32, O.SUM)
+
+
+@pytest.mark.parametrize("P", [2, 3, 4, 8])
+@pytest.mark.parametrize("N", [1, 255, 1000, 4099, 100003])
+def test_replicated_schedule_matches_ring_chunked_oracle(P, N):
+    import gloo_amd  # noqa: F401
+    ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=18)
+    out = gpu_allreduce(REPL, O.SUM, O.FLOAT32, ins, runs=2)
+    check_all(out, O.allreduce(O.RING_CHUNKED, O.SUM, O.FLOAT32, ins), O.FLOAT32, O.SUM)
+
+
+@pytest.mark.parametrize("dtype,op", [(O.FLOAT16, O.SUM), (O.FLOAT32, O.MAX),
+                                      (O.INT64, O.PRODUCT), (O.BFLOAT16, O.MIN)],
+                         ids=lambda x: str(x))
+def test_replicated_schedule_dtypes_multi_pointer(dtype, op):
+    P, N = 5, 20011
+    ins = case_inputs(P, N, dtype, 2, 0, seed=19)
+    out = gpu_allreduce(REPL, op, dtype, ins, streams=True)
+    check_all(out, O.allreduce(O.RING_CHUNKED, op, dtype, ins), dtype, op)

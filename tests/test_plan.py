@@ -130,3 +130,34 @@ def test_plan_replay_reference_test_sizes(algo, P, N):
     exp = O.allreduce(algo, O.SUM, O.FLOAT32, ins)
     for r in range(P):
         assert same_bits(got[r], exp[r][0])
+
+
+@pytest.mark.parametrize("P", [2, 3, 4, 5, 8])
+@pytest.mark.parametrize("N", [1, 255, 1000, 4099, 65537])
+@pytest.mark.parametrize("dtype,op", [(O.FLOAT32, O.SUM), (O.FLOAT16, O.SUM),
+                                      (O.FLOAT32, O.MAX), (O.INT32, O.PRODUCT)])
+def test_replicated_ring_chunked_is_bit_identical(P, N, dtype, op):
+    ins = case_inputs(P, N, dtype, 1, 0, seed=41)
+    plans = [gloo_amd.plan("ring_chunked_repl", r, P, N, with_folds=True) for r in range(P)]
+    got = replay_plans(plans, op, dtype, [ins[r][0] for r in range(P)])
+    exp = O.allreduce(O.RING_CHUNKED, op, dtype, ins)
+    for r in range(P):
+        assert same_bits(got[r], exp[r][0]), r
+    # one dependent round: all sends precede every receive
+    steps = plans[0][0]
+    kinds = [s[0] for s in steps]
+    assert kinds.index(1) > max(i for i, k in enumerate(kinds) if k == 0)
+
+
+@pytest.mark.parametrize("P", [2, 3, 7, 8])
+@pytest.mark.parametrize("N", [1, 1000, 4099])
+@pytest.mark.parametrize("max_seg", [128, 0])
+def test_replicated_fn_ring_is_bit_identical(P, N, max_seg):
+    ins = [O.fill(O.FLOAT32, N, 0, seed=5, rank=r) for r in range(P)]
+    plans = [gloo_amd.plan("fn_ring_repl", r, P, N, with_folds=True, max_segment_size=max_seg)
+             for r in range(P)]
+    got = replay_plans(plans, O.SUM, O.FLOAT32, ins)
+    exp = O.allreduce_fn(O.FN_RING, O.SUM, O.FLOAT32, [[] for _ in range(P)],
+                         [[x] for x in ins], max_seg)
+    for r in range(P):
+        assert same_bits(got[r], exp[r][0]), r

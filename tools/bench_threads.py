@@ -21,7 +21,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--P", default="2,4,8")
     ap.add_argument("--elems", default="1024,16384,262144,1048576,4194304,16777216,67108864")
-    ap.add_argument("--algos", default="ring_chunked,ring_chunked_mesh,halving_doubling")
+    ap.add_argument("--algos", default="ring_chunked,ring_chunked_mesh,ring_chunked_repl,"
+                                       "halving_doubling")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     args = ap.parse_args()
@@ -31,8 +32,9 @@ def main():
         def cls(ctx, bufs_, algo=algo):
             if algo == "halving_doubling":
                 return gloo_amd.AllreduceHalvingDoubling(ctx, bufs_)
-            return gloo_amd.AllreduceRingChunked(
-                ctx, bufs_, schedule="mesh" if algo == "ring_chunked_mesh" else "ring")
+            sched = {"ring_chunked_mesh": "mesh", "ring_chunked_repl": "replicated"}.get(
+                algo, "ring")
+            return gloo_amd.AllreduceRingChunked(ctx, bufs_, schedule=sched)
         for P in [int(x) for x in args.P.split(",")]:
             for n in [int(x) for x in args.elems.split(",")]:
                 iters = args.iters if n <= (1 << 22) else max(3, args.iters // 4)
