@@ -9,8 +9,9 @@ buffers (gloo/allreduce.h:89-193, gloo/allreduce.cc:97-146).
 
 Differences forced by the device: the reduce function is one of the
 gloo/math.h ops (ReductionFunction / ReductionType / gloo_amd.math.sum ...),
-not an arbitrary host callable; buffers are device tensors (or raw device
-pointers with an explicit dtype).  Results are bit-identical to the
+not an arbitrary host callable.  Buffers are device tensors, or host memory
+as in the reference (numpy arrays, CPU tensors: staged through the GPU per
+call), or raw pointers with an explicit dtype.  Results are bit-identical to the
 reference's for the same inputs, ring and bcube.
 """
 import ctypes
@@ -66,8 +67,7 @@ class AllreduceOptions:
         self._sizes(self.outputs, elements, dtype)
 
     def _sizes(self, bufs, elements, dtype):
-        _, dt, numel = _as_ptrs(bufs, dtype if dtype is not None else self.dtype,
-                                allow_host=False)
+        _, dt, numel = _as_ptrs(bufs, dtype if dtype is not None else self.dtype)
         if self.dtype is not None and dt != self.dtype:
             raise TypeError("inputs and outputs must share one dtype")
         self.dtype = dt
@@ -117,14 +117,14 @@ def allreduce(opts):
     if not opts.outputs:
         raise EnforceNotMet("allreduce: at least one output is required")
     op = opts.op if opts.op is not None else 1
-    inp, _, _ = (_as_ptrs(opts.inputs, opts.dtype, allow_host=False) if opts.inputs
-                 else ([], None, None))
-    outp, _, _ = _as_ptrs(opts.outputs, opts.dtype, allow_host=False)
+    inp, _, _ = _as_ptrs(opts.inputs, opts.dtype) if opts.inputs else ([], None, None)
+    outp, _, _ = _as_ptrs(opts.outputs, opts.dtype)
     iarr = (ctypes.c_void_p * max(len(inp), 1))(*inp)
     oarr = (ctypes.c_void_p * len(outp))(*outp)
     sync = None
     stream = _stream_ptr(opts.stream)
-    if stream is None and any(not isinstance(b, int) for b in opts.outputs + opts.inputs):
+    if stream is None and any(getattr(b, "is_cuda", False)
+                              for b in opts.outputs + opts.inputs):
         import torch
         cur = torch.cuda.current_stream()
         if cur.cuda_stream:

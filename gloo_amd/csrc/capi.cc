@@ -315,7 +315,8 @@ glx_algorithm* glx_allreduce_halving_doubling_create(glx_context* ctx, void* con
 glx_algorithm* glx_allreduce_create(glx_context* ctx, int algo, void* const* ptrs, int nptrs,
                                     int count, int dtype, int op, const glx_stream_t* streams,
                                     int nstreams) {
-  if (algo < GLX_ALGO_RING_CHUNKED || algo > GLX_ALGO_RING_CHUNKED_MESH) {
+  if (algo != GLX_ALGO_RING_CHUNKED && algo != GLX_ALGO_HALVING_DOUBLING &&
+      algo != GLX_ALGO_RING_CHUNKED_MESH && algo != GLX_ALGO_RING_CHUNKED_REPL) {
     fail(GLX_ERR_INVALID, "glx_allreduce_create: unknown algorithm");
     return nullptr;
   }

@@ -241,6 +241,7 @@ HipPlanExecutor::~HipPlanExecutor() noexcept(false) {
   }
   if (hostDone_) hipEventDestroy(hostDone_);
   for (char* d : devBufs_) hipFree(d);
+  for (char* d : fnStage_) hipFree(d);
   for (void* p : registered_) hipHostUnregister(p);
   for (void* p : ipcOpened_) hipIpcCloseMemHandle(p);
   for (auto& e : events_) hipEventDestroy(e);
@@ -575,14 +576,18 @@ void HipPlanExecutor::runFn(const FnCall& call) {
   for (void* p : call.out) GLX_ENFORCE(p != nullptr || count_ == 0, "null output pointer");
   for (void* p : call.in) GLX_ENFORCE(p != nullptr || count_ == 0, "null input pointer");
   if (count_ == 0) return;  // gloo/allreduce.cc:98-100
+  const bool host = isHostPointer(call.out[0]);
   for (void* p : call.out) {
-    GLX_ENFORCE(!isHostPointer(p), "allreduce(opts) takes device buffers; host-memory "
-                "buffers are staged by the class algorithms (AllreduceRingChunked, ...)");
+    GLX_ENFORCE(isHostPointer(p) == host, "buffers must be all device or all host memory");
   }
   for (void* p : call.in) {
-    GLX_ENFORCE(!isHostPointer(p), "allreduce(opts) takes device buffers");
+    GLX_ENFORCE(isHostPointer(p) == host, "buffers must be all device or all host memory");
   }
   GLX_HIP_CHECK(hipSetDevice(device_));
+  if (host) {
+    runFnHost(call);
+    return;
+  }
   // per-call stream and timeout (opts.timeout, gloo/allreduce.h:50)
   struct Restore {
     HipPlanExecutor* e;
@@ -602,6 +607,54 @@ void HipPlanExecutor::runFn(const FnCall& call) {
                                  hipMemcpyDeviceToDevice, compute_));
   }
   if (call.stream == nullptr) GLX_HIP_CHECK(hipStreamSynchronize(compute_));
+}
+
+// gloo::allreduce(opts) on host buffers (the reference's own calling
+// convention, e.g. CPU tensors): the buffers change from call to call, so
+// they are not pinned; they are copied into device staging buffers owned by
+// this executor, the device path runs there, and the result is copied back
+// to every output.  Blocking, like the reference.
+void HipPlanExecutor::runFnHost(const FnCall& call) {
+  GLX_ENFORCE(call.stream == nullptr, "a stream cannot be used with host-memory buffers");
+  const size_t bytes = (size_t)count_ * esize_;
+  // device staging: out[0], and the inputs (or, with no inputs, the outputs,
+  // which are then folded into out[0])
+  const std::vector<void*>& srcs = call.in.empty() ? call.out : call.in;
+  const size_t need = 1 + srcs.size();
+  while (fnStage_.size() < need) {
+    char* d = nullptr;
+    GLX_HIP_CHECK(hipMalloc((void**)&d, bytes));
+    fnStage_.push_back(d);
+  }
+  timeout_ = call.timeout;
+  struct Restore {
+    HipPlanExecutor* e;
+    ~Restore() { e->timeout_ = std::chrono::milliseconds(0); }
+  } restore{this};
+  for (size_t i = 0; i < srcs.size(); i++) {
+    GLX_HIP_CHECK(hipMemcpyAsync(fnStage_[1 + i], srcs[i], bytes, hipMemcpyHostToDevice,
+                                 compute_));
+  }
+  std::vector<void*> din, dout;
+  char* out0;
+  if (call.in.empty()) {  // the staged outputs are the data; out[0]'s copy gets the result
+    dout.assign(fnStage_.begin() + 1, fnStage_.begin() + 1 + (long)srcs.size());
+    out0 = fnStage_[1];
+  } else {
+    din.assign(fnStage_.begin() + 1, fnStage_.begin() + 1 + (long)srcs.size());
+    dout.push_back(fnStage_[0]);
+    out0 = fnStage_[0];
+    if (dtype_ == GLX_FLOAT16 && din.size() >= 2) {
+      // float16's assignment reads out[0]'s old value
+      GLX_HIP_CHECK(hipMemcpyAsync(out0, call.out[0], bytes, hipMemcpyHostToDevice, compute_));
+    }
+  }
+  localReduce(din, dout);
+  if (contextSize_ > 1) exchange(out0);
+  for (void* p : call.out) {
+    GLX_HIP_CHECK(hipMemcpyAsync(p, out0, bytes, hipMemcpyDeviceToHost, compute_));
+  }
+  GLX_HIP_CHECK(hipStreamSynchronize(compute_));
 }
 
 void HipPlanExecutor::setupHostMode() {

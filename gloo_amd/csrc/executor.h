@@ -177,6 +177,8 @@ class HipPlanExecutor : public Algorithm {
   void waitH2D(hipStream_t s, int& waited, int64_t off, int64_t len);
   void copyBack(const std::vector<glx::Range>& ranges);
   void runHost();
+  std::vector<char*> fnStage_;  // device staging of function-style host buffers
+  void runFnHost(const FnCall& call);
   std::vector<OutChan> out_;
   std::vector<InChan> in_;
   std::vector<int> stepChan_;        // channel index per step

@@ -238,3 +238,48 @@ def test_multiprocess_ipc(algo):
         for r, p in enumerate(procs):
             assert p.returncode == 0, "rank %d failed:\n%s" % (r, outs[r])
             assert "OK" in outs[r]
+
+
+def host_allreduce_fn(algo, op, dtype, ins, outs, max_seg=0, runs=1):
+    """gloo_amd.allreduce on host (numpy) buffers, the reference's calling
+    convention; every call gets fresh arrays."""
+    import gloo_amd
+    P = len(outs)
+    N = outs[0][0].size
+    store = gloo_amd.rendezvous.HashStore()
+    result = [None] * P
+
+    def rank_fn(r):
+        ctx = gloo_amd.rendezvous.Context(r, P, 0)
+        ctx.setTimeout(60)
+        ctx.connectFullMesh(store)
+        for _ in range(runs):
+            hi = [np.array(x, copy=True) for x in ins[r]]
+            ho = [np.array(x, copy=True) for x in outs[r]]
+            opts = gloo_amd.AllreduceOptions(ctx)
+            opts.setAlgorithm(algo)
+            if hi:
+                opts.setInputs(hi, N)
+            opts.setOutputs(ho, N)
+            opts.setReduceFunction(op)
+            opts.setMaxSegmentSize(max_seg)
+            gloo_amd.allreduce(opts)
+        result[r] = ho
+        ctx.close()
+        return True
+
+    run_ranks(P, rank_fn, timeout=120)
+    return result
+
+
+HOST_GOLDEN = [r for r in INDEX if r["dtype"] != O.UINT64 or r["N"] in (0, 1000)]
+
+
+@pytest.mark.parametrize("rec", HOST_GOLDEN, ids=[r["name"] for r in HOST_GOLDEN])
+def test_allreduce_fn_host_buffers_vs_reference_golden(rec):
+    ins, outs = fn_case_buffers(rec)
+    got = host_allreduce_fn(rec["algo"], rec["op"], rec["dtype"], ins, outs,
+                            rec["max_segment_size"], runs=2)
+    for r in range(rec["P"]):
+        for i in range(rec["nout"]):
+            check_against_golden(rec, DATA, got[r][i])
