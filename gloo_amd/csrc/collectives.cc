@@ -82,7 +82,8 @@ void allreduce(const AllreduceOptions& opts) {
       alg = std::make_shared<HipPlanExecutor>(opts.context, schedule,
                                               std::vector<void*>{opts.out[0]},
                                               (int64_t)opts.elements, opts.dtype, opts.op,
-                                              std::vector<hipStream_t>(), prm);
+                                              std::vector<hipStream_t>(), prm,
+                                              /*perCallBuffers=*/true);
       ctx.ops.emplace(key, alg);
     }
   }

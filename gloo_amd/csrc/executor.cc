@@ -109,7 +109,7 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
                                  const std::vector<void*>& ptrs, int64_t count,
                                  int dtype, int op,
                                  const std::vector<hipStream_t>& streams,
-                                 const glx::PlanParams& prm)
+                                 const glx::PlanParams& prm, bool perCallBuffers)
     : Algorithm(ctx), algo_(algo), ptrs_(ptrs), count_(count), dtype_(dtype), op_(op) {
   GLX_ENFORCE(!ptrs.empty(), "at least one buffer pointer is required");
   GLX_ENFORCE(count >= 0 && count <= (int64_t(1) << 40), "count out of range: ", count);
@@ -140,14 +140,16 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
   split_ = std::max(1, std::min(copySplit(), (int)kMaxSplit));
   copyEngine_ = copyEngine();
 
-  hostMode_ = count_ > 0 && isHostPointer(ptrs[0]);
+  // perCallBuffers (function style): ptrs only describe the first call; the
+  // buffers of every call come with runFn, host ones staged per call there
+  hostMode_ = !perCallBuffers && count_ > 0 && isHostPointer(ptrs[0]);
   for (void* p : ptrs) {
-    GLX_ENFORCE(count_ == 0 || isHostPointer(p) == hostMode_,
+    GLX_ENFORCE(perCallBuffers || count_ == 0 || isHostPointer(p) == hostMode_,
                 "buffers must be all device memory or all host memory");
   }
   GLX_ENFORCE(!hostMode_ || !userStream_, "streams cannot be used with host-memory buffers");
   if (hostMode_) setupHostMode();
-  if (!hostMode_ && count_ > 0) {
+  if (!hostMode_ && !perCallBuffers && count_ > 0) {
     // pointers on other GPUs of this rank (the reference's multi-device
     // ranks, gloo/cuda_allreduce_ring_chunked.cc): the fold kernel reads them
     // and the broadcast writes them over xGMI from this rank's device

@@ -45,7 +45,7 @@ class HipPlanExecutor : public Algorithm {
   HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
                   const std::vector<void*>& ptrs, int64_t count, int dtype,
                   int op, const std::vector<hipStream_t>& streams,
-                  const glx::PlanParams& prm = glx::PlanParams());
+                  const glx::PlanParams& prm = glx::PlanParams(), bool perCallBuffers = false);
   ~HipPlanExecutor() noexcept(false) override;
 
   // Class-style run (gloo/allreduce_ring_chunked.h:83-212): fold ptrs into
