@@ -118,7 +118,9 @@ ALGO_CODES = {"ring_chunked": 0, "halving_doubling": 1, "ring_chunked_mesh": 2,
               # schedules of gloo_amd.allreduce (plan introspection)
               "fn_ring": 3, "fn_ring_mesh": 4, "fn_bcube": 5,
               # one-round variants for small buffers
-              "ring_chunked_repl": 6, "fn_ring_repl": 7}
+              "ring_chunked_repl": 6, "fn_ring_repl": 7,
+              # creation-time choice among the ring_chunked schedules
+              "ring_chunked_auto": 8}
 
 
 class Algorithm:
@@ -179,7 +181,9 @@ class AllreduceRingChunked(Algorithm):
     """gloo::AllreduceRingChunked<T> (gloo/allreduce_ring_chunked.h:19) on
     MI355X: xGMI peer copies + HIP reduce kernel, same chunking and order.
 
-    schedule="ring" (default) moves chunks around the ring exactly as the
+    schedule="auto" (default) picks the data movement by size (replicated up
+    to 256 KiB per rank, mesh above; env GLOO_AMD_RING_SCHEDULE forces one).
+    schedule="ring" moves chunks around the ring exactly as the
     reference does (one link per direction); schedule="mesh" computes the
     identical result (same chunks, same reduction chain and operand order)
     with every rank exchanging directly with every peer over all links;
@@ -187,10 +191,10 @@ class AllreduceRingChunked(Algorithm):
     rank receives every peer's buffer and evaluates all chains itself."""
 
     SCHEDULES = {"ring": "ring_chunked", "mesh": "ring_chunked_mesh",
-                 "replicated": "ring_chunked_repl"}
+                 "replicated": "ring_chunked_repl", "auto": "ring_chunked_auto"}
 
     def __init__(self, context, ptrs, count=None, fn=None, streams=None, dtype=None,
-                 schedule="ring"):
+                 schedule="auto"):
         if schedule not in self.SCHEDULES:
             raise ValueError("schedule must be one of %s" % sorted(self.SCHEDULES))
         self._algo = ALGO_CODES[self.SCHEDULES[schedule]]

@@ -30,11 +30,12 @@ _MATH_FUNCS = {_math.sum: 1, _math.product: 2, _math.max: 3, _math.min: 4}
 class AllreduceOptions:
     """gloo::AllreduceOptions (gloo/allreduce.h:89-193)."""
 
-    class Algorithm:  # gloo/allreduce.h:38-42 (+ RING_MESH: RING's result over all links)
-        UNSPECIFIED = 0
+    class Algorithm:  # gloo/allreduce.h:38-42 (+ RING's result over all links / in one round)
+        UNSPECIFIED = 0  # RING's result, data movement chosen by size
         RING = 1
         BCUBE = 2
         RING_MESH = 3
+        RING_REPLICATED = 4
 
     def __init__(self, context):
         self.context = context

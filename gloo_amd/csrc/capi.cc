@@ -315,6 +315,10 @@ glx_algorithm* glx_allreduce_halving_doubling_create(glx_context* ctx, void* con
 glx_algorithm* glx_allreduce_create(glx_context* ctx, int algo, void* const* ptrs, int nptrs,
                                     int count, int dtype, int op, const glx_stream_t* streams,
                                     int nstreams) {
+  if (algo == GLX_ALGO_RING_CHUNKED_AUTO && ctx != nullptr && count >= 0) {
+    algo = glx::autoRingSchedule(ctx->c->size, (int64_t)count * (int64_t)glx_dtype_size(dtype),
+                                 /*fn=*/false);
+  }
   if (algo != GLX_ALGO_RING_CHUNKED && algo != GLX_ALGO_HALVING_DOUBLING &&
       algo != GLX_ALGO_RING_CHUNKED_MESH && algo != GLX_ALGO_RING_CHUNKED_REPL) {
     fail(GLX_ERR_INVALID, "glx_allreduce_create: unknown algorithm");

@@ -31,15 +31,14 @@ int64_t envBytes(const char* name, int64_t dflt) {
   return (end != e && v >= 0) ? (int64_t)v : dflt;
 }
 
-int scheduleFor(int algorithm) {
+int scheduleFor(int algorithm, int size, int64_t bytes) {
   switch (algorithm) {
-    case AllreduceOptions::UNSPECIFIED: {
-      const char* e = std::getenv("GLOO_AMD_ALLREDUCE_SCHEDULE");
-      if (e != nullptr && std::strcmp(e, "mesh") == 0) return glx::ALGO_FN_RING_MESH;
-      return glx::ALGO_FN_RING;  // gloo/allreduce.cc:134-137
-    }
+    case AllreduceOptions::UNSPECIFIED:
+      // RING's result (gloo/allreduce.cc:134-137) moved the fastest way
+      return glx::autoRingSchedule(size, bytes, /*fn=*/true);
     case AllreduceOptions::RING: return glx::ALGO_FN_RING;
     case AllreduceOptions::RING_MESH: return glx::ALGO_FN_RING_MESH;
+    case AllreduceOptions::RING_REPLICATED: return glx::ALGO_FN_RING_REPL;
     case AllreduceOptions::BCUBE: return glx::ALGO_FN_BCUBE;
   }
   GLX_ENFORCE(false, "Algorithm not handled.");  // :141-142
@@ -50,7 +49,9 @@ int scheduleFor(int algorithm) {
 
 void allreduce(const AllreduceOptions& opts) {
   GLX_ENFORCE(opts.context != nullptr, "allreduce: null context");
-  const int schedule = scheduleFor(opts.algorithm);
+  GLX_ENFORCE(opts.algorithm >= AllreduceOptions::UNSPECIFIED &&
+                  opts.algorithm <= AllreduceOptions::RING_REPLICATED,
+              "Algorithm not handled.");  // :141-142
   if (opts.elements == 0) return;  // :98-100
   // sanity checks (:107-122)
   GLX_ENFORCE(!opts.out.empty(), "allreduce: at least one output is required");
@@ -63,6 +64,7 @@ void allreduce(const AllreduceOptions& opts) {
   GLX_ENFORCE(ctx.size == 1 || ctx.connected(),
               "allreduce: context must be connected (connectFullMesh)");
 
+  const int schedule = scheduleFor(opts.algorithm, ctx.size, (int64_t)(opts.elements * es));
   const size_t maxSeg = opts.maxSegmentSize == 0 ? (size_t)glx::kMaxSegmentBytes
                                                  : opts.maxSegmentSize;
   const std::string key = std::to_string(schedule) + "/" + std::to_string(opts.dtype) + "/" +

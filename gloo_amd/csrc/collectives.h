@@ -17,7 +17,7 @@ namespace gloo {
 // detail::AllreduceOptionsImpl (gloo/allreduce.h:22-84) with the reduce
 // function named by (dtype, op) instead of a host std::function.
 struct AllreduceOptions {
-  enum Algorithm { UNSPECIFIED = 0, RING = 1, BCUBE = 2, RING_MESH = 3 };
+  enum Algorithm { UNSPECIFIED = 0, RING = 1, BCUBE = 2, RING_MESH = 3, RING_REPLICATED = 4 };
 
   explicit AllreduceOptions(const std::shared_ptr<Context>& c) : context(c) {}
 

@@ -8,6 +8,7 @@
 #include "plan.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -699,6 +700,22 @@ Plan planFnBcube(int rank, int size, int64_t count) {
     }
   }
   return p;
+}
+
+int autoRingSchedule(int size, int64_t bytes, bool fn) {
+  const int ring = fn ? ALGO_FN_RING : ALGO_RING_CHUNKED;
+  const int mesh = fn ? ALGO_FN_RING_MESH : ALGO_RING_CHUNKED_MESH;
+  const int repl = fn ? ALGO_FN_RING_REPL : ALGO_RING_CHUNKED_REPL;
+  if (const char* e = std::getenv("GLOO_AMD_RING_SCHEDULE")) {
+    const std::string v(e);
+    if (v == "ring") return ring;
+    if (v == "mesh") return mesh;
+    if (v == "replicated") return repl;
+  }
+  int64_t maxRepl = int64_t(256) << 10;  // the reference's kOnDeviceThreshold (algorithm.cc:16)
+  if (const char* e = std::getenv("GLOO_AMD_REPLICATED_MAX_BYTES")) maxRepl = std::atoll(e);
+  if (size <= 1) return ring;
+  return bytes <= maxRepl ? repl : mesh;
 }
 
 Plan makePlan(int algo, int rank, int size, int64_t count, const PlanParams& prm) {

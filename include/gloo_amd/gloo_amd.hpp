@@ -227,8 +227,10 @@ class DeviceAllreduce : public Algorithm {
 
 // Data movement of HipAllreduceRingChunked (results are bit-identical):
 // RING = the reference's ring (one link per direction); MESH = each rank
-// folds its chunk pair from every peer directly (all links at once).
-enum class Schedule { RING, MESH };
+// folds its chunk pair from every peer directly (all links at once);
+// REPLICATED = one round, every rank folds everything (small buffers);
+// AUTO = REPLICATED up to 256 KiB per rank, MESH above.
+enum class Schedule { RING, MESH, REPLICATED, AUTO };
 
 namespace detail {
 inline glx_algorithm* createRing(glx_context* c, void* const* p, int n, int count, int dt,
@@ -239,6 +241,14 @@ inline glx_algorithm* createMesh(glx_context* c, void* const* p, int n, int coun
                                  int op, const glx_stream_t* s, int ns) {
   return glx_allreduce_create(c, GLX_ALGO_RING_CHUNKED_MESH, p, n, count, dt, op, s, ns);
 }
+inline glx_algorithm* createRepl(glx_context* c, void* const* p, int n, int count, int dt,
+                                 int op, const glx_stream_t* s, int ns) {
+  return glx_allreduce_create(c, GLX_ALGO_RING_CHUNKED_REPL, p, n, count, dt, op, s, ns);
+}
+inline glx_algorithm* createAuto(glx_context* c, void* const* p, int n, int count, int dt,
+                                 int op, const glx_stream_t* s, int ns) {
+  return glx_allreduce_create(c, GLX_ALGO_RING_CHUNKED_AUTO, p, n, count, dt, op, s, ns);
+}
 }  // namespace detail
 
 // gloo::CudaAllreduceRingChunked<T> analog (gloo/cuda_allreduce_ring_chunked.h:22-26).
@@ -248,10 +258,12 @@ class HipAllreduceRingChunked : public detail::DeviceAllreduce<T> {
   HipAllreduceRingChunked(const std::shared_ptr<Context>& ctx, const std::vector<T*>& ptrs,
                           int count, const std::vector<glx_stream_t>& streams = {},
                           const ReductionFunction<T>* fn = ReductionFunction<T>::sum,
-                          Schedule schedule = Schedule::RING)
-      : detail::DeviceAllreduce<T>(
-            schedule == Schedule::MESH ? &detail::createMesh : &detail::createRing, ctx, ptrs,
-            count, streams, fn) {}
+                          Schedule schedule = Schedule::AUTO)
+      : detail::DeviceAllreduce<T>(schedule == Schedule::MESH         ? &detail::createMesh
+                                   : schedule == Schedule::REPLICATED ? &detail::createRepl
+                                   : schedule == Schedule::RING       ? &detail::createRing
+                                                                      : &detail::createAuto,
+                                   ctx, ptrs, count, streams, fn) {}
 };
 
 // gloo::CudaAllreduceHalvingDoubling<T> analog (gloo/cuda_allreduce_halving_doubling.h:25-30).
@@ -317,6 +329,7 @@ class AllreduceOptions {
     RING = GLX_ALLREDUCE_RING,
     BCUBE = GLX_ALLREDUCE_BCUBE,
     RING_MESH = GLX_ALLREDUCE_RING_MESH,  // RING's result over all links
+    RING_REPLICATED = GLX_ALLREDUCE_RING_REPLICATED,  // RING's result in one round
   };
 
   explicit AllreduceOptions(const std::shared_ptr<Context>& context) : context_(context) {}

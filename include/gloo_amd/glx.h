@@ -204,7 +204,11 @@ enum glx_algo {
   /* one round for small buffers: every rank receives every peer's whole
    * buffer and folds every chunk in the ring's own order (bit-identical) */
   GLX_ALGO_RING_CHUNKED_REPL = 6,
-  GLX_ALGO_FN_RING_REPL = 7
+  GLX_ALGO_FN_RING_REPL = 7,
+  /* AllreduceRingChunked's result, data movement chosen at creation:
+   * replicated up to 256 KiB per rank, mesh above (GLOO_AMD_RING_SCHEDULE /
+   * GLOO_AMD_REPLICATED_MAX_BYTES override) */
+  GLX_ALGO_RING_CHUNKED_AUTO = 8
 };
 glx_algorithm* glx_allreduce_create(glx_context* ctx, int algo, void* const* ptrs,
                                     int nptrs, int count, int dtype, int op,
@@ -226,7 +230,8 @@ enum glx_allreduce_algorithm {
   GLX_ALLREDUCE_UNSPECIFIED = 0,
   GLX_ALLREDUCE_RING = 1,
   GLX_ALLREDUCE_BCUBE = 2,
-  GLX_ALLREDUCE_RING_MESH = 3
+  GLX_ALLREDUCE_RING_MESH = 3,
+  GLX_ALLREDUCE_RING_REPLICATED = 4  /* RING's result in one round (small buffers) */
 };
 /* gloo::allreduce(const AllreduceOptions&) (gloo/allreduce.cc:97-146,
  * gloo/allreduce.h:89-193) on device buffers.  The reduce function is one of
@@ -246,7 +251,9 @@ enum glx_allreduce_algorithm {
  * Every rank calls with the same algorithm/dtype/op/elements/tag/
  * max_segment_size.  The first call with a given combination sets up and
  * exchanges receive buffers with the peers (once; later calls reuse them).
- * UNSPECIFIED means RING, or RING_MESH with GLOO_AMD_ALLREDUCE_SCHEDULE=mesh. */
+ * UNSPECIFIED computes RING's result with the data movement chosen per
+ * size (replicated up to 256 KiB per rank, mesh above; GLOO_AMD_RING_SCHEDULE
+ * forces ring|mesh|replicated). */
 int glx_allreduce(glx_context* ctx, int algorithm, int dtype, int op,
                   void* const* inputs, int num_inputs, void* const* outputs,
                   int num_outputs, size_t elements, uint32_t tag,

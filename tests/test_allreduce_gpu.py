@@ -27,6 +27,7 @@ ALGOS = {O.RING_CHUNKED: "AllreduceRingChunked", O.HALVING_DOUBLING: "AllreduceH
 
 MESH = 2  # ring_chunked semantics, mesh schedule
 REPL = 6  # ring_chunked semantics, one-round replicated schedule
+AUTO = 8  # ring_chunked semantics, schedule chosen by size
 
 
 def gpu_allreduce(algo, op, dtype, inputs, runs=1, streams=False, timeout_s=60,
@@ -44,6 +45,11 @@ def gpu_allreduce(algo, op, dtype, inputs, runs=1, streams=False, timeout_s=60,
         def cls(*a, **kw):
             return gloo_amd.AllreduceRingChunked(
                 *a, schedule="mesh" if algo == MESH else "replicated", **kw)
+    elif algo == O.RING_CHUNKED:
+        def cls(*a, **kw):
+            return gloo_amd.AllreduceRingChunked(*a, schedule="ring", **kw)
+    elif algo == AUTO:
+        cls = gloo_amd.AllreduceRingChunked
     else:
         cls = getattr(gloo_amd, ALGOS[algo])
 
@@ -342,3 +348,12 @@ def test_replicated_schedule_dtypes_multi_pointer(dtype, op):
     ins = case_inputs(P, N, dtype, 2, 0, seed=19)
     out = gpu_allreduce(REPL, op, dtype, ins, streams=True)
     check_all(out, O.allreduce(O.RING_CHUNKED, op, dtype, ins), dtype, op)
+
+
+@pytest.mark.parametrize("P,N", [(2, 1000), (3, 70000), (4, 100003), (8, 4099)])
+def test_auto_schedule_is_ring_chunked(P, N):
+    """The default AllreduceRingChunked picks its data movement by size; the
+    bits are the reference's whatever it picks."""
+    ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=23)
+    out = gpu_allreduce(AUTO, O.SUM, O.FLOAT32, ins, runs=2)
+    check_all(out, O.allreduce(O.RING_CHUNKED, O.SUM, O.FLOAT32, ins), O.FLOAT32, O.SUM)
