@@ -254,8 +254,12 @@ def host_allreduce_fn(algo, op, dtype, ins, outs, max_seg=0, runs=1):
         ctx.setTimeout(60)
         ctx.connectFullMesh(store)
         for _ in range(runs):
-            hi = [np.array(x, copy=True) for x in ins[r]]
-            ho = [np.array(x, copy=True) for x in outs[r]]
+            # the oracle keeps float16 as raw uint16 bits: hand numpy float16
+            hv = np.float16 if dtype == O.FLOAT16 else None
+            hi = [np.array(x, copy=True).view(hv) if hv else np.array(x, copy=True)
+                  for x in ins[r]]
+            ho = [np.array(x, copy=True).view(hv) if hv else np.array(x, copy=True)
+                  for x in outs[r]]
             opts = gloo_amd.AllreduceOptions(ctx)
             opts.setAlgorithm(algo)
             if hi:
@@ -264,7 +268,7 @@ def host_allreduce_fn(algo, op, dtype, ins, outs, max_seg=0, runs=1):
             opts.setReduceFunction(op)
             opts.setMaxSegmentSize(max_seg)
             gloo_amd.allreduce(opts)
-        result[r] = ho
+        result[r] = [x.view(np.uint16) for x in ho] if dtype == O.FLOAT16 else ho
         ctx.close()
         return True
 
