@@ -258,11 +258,14 @@ def reduce_kernel_roofline(torch, gloo_amd, dev, chunk_bytes, reps=50):
             "algorithmic_bytes_per_launch": 3 * chunk_bytes}
 
 
+RING_SCHEDULES = {"ring_chunked": "ring", "ring_chunked_mesh": "mesh",
+                  "ring_chunked_repl": "replicated", "ring_chunked_auto": "auto"}
+
+
 def make_alg(gloo_amd, ctx, buf, algo):
     if algo == "halving_doubling":
         return gloo_amd.AllreduceHalvingDoubling(ctx, [buf])
-    return gloo_amd.AllreduceRingChunked(ctx, [buf],
-                                        schedule="mesh" if algo == "ring_chunked_mesh" else "ring")
+    return gloo_amd.AllreduceRingChunked(ctx, [buf], schedule=RING_SCHEDULES[algo])
 
 
 def busiest_link_bytes(gloo_amd, algo, rank, world, count, es):
@@ -346,11 +349,20 @@ def element_sweep(torch, dist, gloo_amd, ctx, dev, schedules, dtype):
     for n in SWEEP_ELEMS:
         x = synthetic(torch, n, dtype, dev, 77)
         row = {}
-        for sched in schedules:
+        scheds = list(schedules)
+        if "ring_chunked" in scheds and n * x.element_size() <= (4 << 20):
+            # one round, every rank folds everything: the one-shot kernel when
+            # the ranks are on distinct devices (host-mediated steps otherwise)
+            scheds.append("ring_chunked_repl")
+        for sched in scheds:
             iters = 20 if n <= (1 << 20) else 5
             t, _ = time_schedule(torch, dist, gloo_amd, ctx, x, sched, iters, 2)
             row[sched] = {"us": round(t * 1e6, 1),
                           "algbw_GBps": round(n * x.element_size() / t / 1e9, 3)}
+            if sched == "ring_chunked_repl":
+                alg = make_alg(gloo_amd, ctx, x, sched)
+                row[sched]["engine"] = alg.engine()
+                alg.close()
         out[str(n)] = row
     return out
 

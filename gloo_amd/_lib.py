@@ -64,6 +64,7 @@ SIGNATURES = [
      [_vp, _i, ctypes.POINTER(_vp), _i, _i, _i, _i, ctypes.POINTER(_vp), _i]),
     ("glx_algorithm_run", _i, [_vp]),
     ("glx_algorithm_bytes_sent", _i64, [_vp]),
+    ("glx_algorithm_engine", _i, [_vp]),
     ("glx_algorithm_destroy", None, [_vp]),
     ("glx_plan", _i64, [_i, _i, _i, _i64, ctypes.POINTER(_i64), _i64,
                         ctypes.POINTER(_i64)]),

@@ -99,7 +99,9 @@ def _as_ptrs(bufs, dtype, allow_host=True):
         code = torch_dtype_code(b)
         if dtype is None:
             dtype = code
-        elif dtype != code:
+        elif dtype != code and lib.glx_dtype_size(dtype) != b.element_size():
+            # an explicit dtype may reinterpret a tensor of the same element
+            # size (e.g. uint64 data held in an int64 tensor)
             raise TypeError("all buffers must share one dtype")
         ptrs.append(b.data_ptr())
         numel = b.numel() if numel is None else min(numel, b.numel())
@@ -166,6 +168,11 @@ class Algorithm:
     def bytes_sent(self):
         """Bytes this rank moves over peer links per run()."""
         return lib.glx_algorithm_bytes_sent(self._h)
+
+    def engine(self):
+        """"steps" (host-issued schedule steps) or "oneshot" (the replicated
+        schedule as one device-driven kernel per rank)."""
+        return {0: "steps", 1: "oneshot"}[lib.glx_algorithm_engine(self._h)]
 
     def close(self):
         h = getattr(self, "_h", None)

@@ -317,7 +317,7 @@ glx_algorithm* glx_allreduce_create(glx_context* ctx, int algo, void* const* ptr
                                     int nstreams) {
   if (algo == GLX_ALGO_RING_CHUNKED_AUTO && ctx != nullptr && count >= 0) {
     algo = glx::autoRingSchedule(ctx->c->size, (int64_t)count * (int64_t)glx_dtype_size(dtype),
-                                 /*fn=*/false);
+                                 /*fn=*/false, gloo::HipPlanExecutor::oneShotAvailable(*ctx->c));
   }
   if (algo != GLX_ALGO_RING_CHUNKED && algo != GLX_ALGO_HALVING_DOUBLING &&
       algo != GLX_ALGO_RING_CHUNKED_MESH && algo != GLX_ALGO_RING_CHUNKED_REPL) {
@@ -361,6 +361,11 @@ int glx_algorithm_run(glx_algorithm* alg) {
 
 int64_t glx_algorithm_bytes_sent(glx_algorithm* alg) {
   return alg ? alg->a->bytesSentPerRun() : -1;
+}
+
+int glx_algorithm_engine(glx_algorithm* alg) {
+  if (alg == nullptr) return -1;
+  return alg->a->oneShot() ? GLX_ENGINE_ONESHOT : GLX_ENGINE_STEPS;
 }
 
 void glx_algorithm_destroy(glx_algorithm* alg) {

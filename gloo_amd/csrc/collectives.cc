@@ -31,11 +31,12 @@ int64_t envBytes(const char* name, int64_t dflt) {
   return (end != e && v >= 0) ? (int64_t)v : dflt;
 }
 
-int scheduleFor(int algorithm, int size, int64_t bytes) {
+int scheduleFor(int algorithm, const Context& ctx, int64_t bytes) {
   switch (algorithm) {
     case AllreduceOptions::UNSPECIFIED:
       // RING's result (gloo/allreduce.cc:134-137) moved the fastest way
-      return glx::autoRingSchedule(size, bytes, /*fn=*/true);
+      return glx::autoRingSchedule(ctx.size, bytes, /*fn=*/true,
+                                   HipPlanExecutor::oneShotAvailable(ctx));
     case AllreduceOptions::RING: return glx::ALGO_FN_RING;
     case AllreduceOptions::RING_MESH: return glx::ALGO_FN_RING_MESH;
     case AllreduceOptions::RING_REPLICATED: return glx::ALGO_FN_RING_REPL;
@@ -64,7 +65,7 @@ void allreduce(const AllreduceOptions& opts) {
   GLX_ENFORCE(ctx.size == 1 || ctx.connected(),
               "allreduce: context must be connected (connectFullMesh)");
 
-  const int schedule = scheduleFor(opts.algorithm, ctx.size, (int64_t)(opts.elements * es));
+  const int schedule = scheduleFor(opts.algorithm, ctx, (int64_t)(opts.elements * es));
   const size_t maxSeg = opts.maxSegmentSize == 0 ? (size_t)glx::kMaxSegmentBytes
                                                  : opts.maxSegmentSize;
   const std::string key = std::to_string(schedule) + "/" + std::to_string(opts.dtype) + "/" +

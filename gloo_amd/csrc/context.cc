@@ -234,6 +234,15 @@ void Context::connectFullMesh(std::shared_ptr<rendezvous::Store> store) {
   connected_ = true;
 }
 
+bool Context::ranksShareDevice() const {
+  for (size_t a = 0; a < peers_.size(); a++) {
+    for (size_t b = a + 1; b < peers_.size(); b++) {
+      if (peers_[a].pid == peers_[b].pid && peers_[a].device == peers_[b].device) return true;
+    }
+  }
+  return false;
+}
+
 void Context::checkPeersAlive() {
   for (const auto& p : peers_) {
     if (p.rank == rank || p.sameProcess || p.pid <= 0) continue;

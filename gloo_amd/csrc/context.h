@@ -101,6 +101,12 @@ class Context {
   ControlBlock& localControl() { return local_; }
   PeerEndpoint& peer(int r) { return peers_.at(r); }
 
+  // True when two ranks of the context are threads of one process on one
+  // device (the same answer on every rank: it is computed from all
+  // endpoints).  Their streams may share a hardware queue, so kernels that
+  // wait for each other on the device could not both run.
+  bool ranksShareDevice() const;
+
   // Throws IoException if a peer process has exited.
   void checkPeersAlive();
 

@@ -174,12 +174,17 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
     }
   }
 
-  allocScratch();
+  oneShot_ = oneShotWanted(*ctx, algo, count_);
+  if (oneShot_) {
+    setupOneShot();
+  } else {
+    allocScratch();
+  }
 
   // Channels named by the plan; allocate our counter words.
   auto& ctl = ctx->localControl();
   stepChan_.assign(plan_.steps.size(), -1);
-  for (size_t i = 0; i < plan_.steps.size(); i++) {
+  for (size_t i = 0; i < plan_.steps.size() && !oneShot_; i++) {
     const auto& s = plan_.steps[i];
     if (s.kind == glx::SEND) {
       int idx = outIndex((int)s.peer, (int)s.channel);
@@ -249,6 +254,9 @@ HipPlanExecutor::~HipPlanExecutor() noexcept(false) {
   for (auto& e : events_) hipEventDestroy(e);
   if (computeMark_) hipEventDestroy(computeMark_);
   for (auto& b : blocks_) hipFree(b.ptr);
+  if (osBase_) hipFree(osBase_);
+  if (osStatus_) hipHostFree(osStatus_);
+  if (osDone_) hipEventDestroy(osDone_);
   for (auto& c : copies_) hipStreamDestroy(c.s);
   if (ownCompute_ && compute_) hipStreamDestroy(compute_);
   auto& ctl = context_->localControl();
@@ -300,6 +308,16 @@ void HipPlanExecutor::publish() {
     putPod<int32_t>(b, DIR_OUT);
     putPod<int32_t>(b, (int32_t)oc.creditWord);
   }
+  putPod<int32_t>(b, oneShot_ ? 1 : 0);
+  if (oneShot_) {
+    putPod<uint64_t>(b, (uint64_t)(uintptr_t)osBase_);
+    hipIpcMemHandle_t h;
+    memset(&h, 0, sizeof(h));
+    int32_t haveIpc = hipIpcGetMemHandle(&h, osBase_) == hipSuccess ? 1 : 0;
+    (void)hipGetLastError();
+    putPod<int32_t>(b, haveIpc);
+    putPod(b, h);
+  }
   context_->store().set(
       "glx/alg/" + std::to_string(slot_) + "/" + std::to_string(contextRank_), b);
 }
@@ -308,6 +326,9 @@ void HipPlanExecutor::resolvePeers() {
   std::map<int, bool> peers;
   for (auto& oc : out_) peers[oc.peer] = true;
   for (auto& ic : in_) peers[ic.peer] = true;
+  for (int r = 0; r < contextSize_ && oneShot_; r++) {
+    if (r != contextRank_) peers[r] = true;
+  }
   for (auto& kv : peers) {
     const int r = kv.first;
     PeerEndpoint& pe = context_->peer(r);
@@ -362,6 +383,23 @@ void HipPlanExecutor::resolvePeers() {
       } else {  // peer sends to us on `tag`: its credit word
         int idx = inIndex(r, tag);
         if (idx >= 0) in_[idx].credit = pe.ctl->word((uint32_t)word);
+      }
+    }
+    const int32_t peerOneShot = getPod<int32_t>(b, at);
+    GLX_ENFORCE(peerOneShot == (oneShot_ ? 1 : 0), "rank ", r,
+                " chose a different replicated-schedule engine (schedules disagree)");
+    if (oneShot_) {
+      const uint64_t ptr = getPod<uint64_t>(b, at);
+      const int32_t haveIpc = getPod<int32_t>(b, at);
+      const hipIpcMemHandle_t h = getPod<hipIpcMemHandle_t>(b, at);
+      if (pe.sameProcess) {
+        osPeer_[r] = reinterpret_cast<char*>((uintptr_t)ptr);
+      } else {
+        GLX_ENFORCE(haveIpc, "rank ", r, " could not export its one-shot regions");
+        void* p = nullptr;
+        GLX_HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+        ipcOpened_.push_back(p);
+        osPeer_[r] = static_cast<char*>(p);
       }
     }
   }
@@ -534,7 +572,10 @@ void HipPlanExecutor::run() {
     GLX_HIP_CHECK(hipMemcpyAsync(ptrs_[i], ptr0, bytes, hipMemcpyDeviceToDevice, compute_));
   }
   GLX_TRACE("r%d sync", contextRank_);
-  if (!userStream_) GLX_HIP_CHECK(hipStreamSynchronize(compute_));
+  if (!userStream_) {
+    GLX_HIP_CHECK(hipStreamSynchronize(compute_));
+    checkOneShot();
+  }
   GLX_TRACE("r%d done", contextRank_);
 }
 
@@ -608,7 +649,10 @@ void HipPlanExecutor::runFn(const FnCall& call) {
     GLX_HIP_CHECK(hipMemcpyAsync(call.out[i], out0, (size_t)count_ * esize_,
                                  hipMemcpyDeviceToDevice, compute_));
   }
-  if (call.stream == nullptr) GLX_HIP_CHECK(hipStreamSynchronize(compute_));
+  if (call.stream == nullptr) {
+    GLX_HIP_CHECK(hipStreamSynchronize(compute_));
+    checkOneShot();
+  }
 }
 
 // gloo::allreduce(opts) on host buffers (the reference's own calling
@@ -657,6 +701,7 @@ void HipPlanExecutor::runFnHost(const FnCall& call) {
     GLX_HIP_CHECK(hipMemcpyAsync(p, out0, bytes, hipMemcpyDeviceToHost, compute_));
   }
   GLX_HIP_CHECK(hipStreamSynchronize(compute_));
+  checkOneShot();
 }
 
 void HipPlanExecutor::setupHostMode() {
@@ -746,9 +791,14 @@ void HipPlanExecutor::runHost() {
   GLX_HIP_CHECK(hipStreamSynchronize(d2h_));
   GLX_HIP_CHECK(hipStreamSynchronize(compute_));
   GLX_HIP_CHECK(hipStreamSynchronize(h2d_));
+  checkOneShot();
 }
 
 void HipPlanExecutor::exchange(char* ptr0) {
+  if (oneShot_) {
+    runOneShot(ptr0);
+    return;
+  }
   if (!resolved_) resolvePeers();
   bool computeSinceMark = true;  // the caller's writes to ptr0 count as compute
   for (auto& c : copies_) c.last = nullptr;
@@ -927,6 +977,125 @@ void HipPlanExecutor::exchange(char* ptr0) {
     if (c.last != nullptr) GLX_HIP_CHECK(hipStreamWaitEvent(compute_, c.last, 0));
   }
   inflight_.clear();
+}
+
+// ---------------------------------------------------------------------------
+// One-shot replicated schedule
+// ---------------------------------------------------------------------------
+
+// GLOO_AMD_ONESHOT=0 keeps the replicated schedule host-mediated, =1 forces
+// the device-driven kernel; by default it is used whenever no two ranks are
+// threads sharing one device (their kernels might not be co-resident).  The
+// inputs are the same on every rank, so every rank makes the same choice.
+bool HipPlanExecutor::oneShotWanted(const Context& ctx, int algo, int64_t count) {
+  if (algo != glx::ALGO_RING_CHUNKED_REPL && algo != glx::ALGO_FN_RING_REPL) return false;
+  return count > 0 && oneShotAvailable(ctx);
+}
+
+bool HipPlanExecutor::oneShotAvailable(const Context& ctx) {
+  if (ctx.size < 2 || ctx.size > glx::kOsMaxRanks) return false;
+  const char* e = std::getenv("GLOO_AMD_ONESHOT");
+  if (e != nullptr && e[0] == '0') return false;
+  if (e != nullptr && e[0] == '1') return true;
+  return !ctx.ranksShareDevice();
+}
+
+void HipPlanExecutor::setupOneShot() {
+  const int P = contextSize_;
+  glx::OneShotParams& p = os_;
+  p.P = P;
+  p.rank = contextRank_;
+  p.count = (size_t)count_;
+  // slices: >= 4 KiB, a whole number of 16-byte vectors, <= kOsMaxSlices
+  const size_t V = 16 / esize_;
+  const size_t minSlice = 4096 / esize_;
+  size_t slice = ((size_t)count_ + glx::kOsMaxSlices - 1) / glx::kOsMaxSlices;
+  slice = (std::max(slice, minSlice) + V - 1) / V * V;
+  p.slice = slice;
+  p.G = (int)(((size_t)count_ + slice - 1) / slice);
+  // chunk ranges and their chains, read off the replicated plan's folds
+  const int64_t region = count_ + glx::kPadElems;
+  p.njobs = 0;
+  for (const auto& s : plan_.steps) {
+    if (s.kind != glx::FOLD) continue;
+    GLX_ENFORCE(p.njobs < glx::kOsMaxRanks, "one-shot: too many chunk ranges");
+    const auto& f = plan_.folds[(size_t)s.boff];
+    GLX_ENFORCE((int)f.size() == P, "one-shot: fold of ", f.size(), " sources for ", P, " ranks");
+    for (int i = 0; i < P; i++) {
+      const int64_t r = f[(size_t)i];
+      GLX_ENFORCE(r < 0 || r % region == 0, "one-shot: unexpected fold source");
+      p.chain[p.njobs][i] = (uint8_t)(r < 0 ? contextRank_ : (int)(r / region));
+    }
+    p.jobOff[p.njobs] = (size_t)s.off;
+    p.jobLen[p.njobs] = (size_t)s.len;
+    p.njobs++;
+  }
+  osRegion_ = ((size_t)count_ * esize_ + 255) & ~(size_t)255;
+  const size_t flagBytes = (size_t)P * (size_t)p.G * sizeof(uint64_t);
+  const size_t bytes = 2 * (size_t)P * osRegion_ + flagBytes;
+  // uncached: peers' stores land in our HBM behind our caches' back
+  GLX_HIP_CHECK(hipExtMallocWithFlags((void**)&osBase_, bytes, hipDeviceMallocUncached));
+  GLX_HIP_CHECK(hipMemset(osBase_, 0, bytes));
+  p.flagIn = reinterpret_cast<const uint64_t*>(osBase_ + 2 * (size_t)P * osRegion_);
+  GLX_HIP_CHECK(hipHostMalloc((void**)&osStatus_, sizeof(int),
+                              hipHostMallocMapped | hipHostMallocCoherent));
+  *reinterpret_cast<volatile int*>(osStatus_) = 0;
+  GLX_HIP_CHECK(hipHostGetDevicePointer((void**)&osStatusDev_, osStatus_, 0));
+  p.status = osStatusDev_;
+  GLX_HIP_CHECK(hipEventCreateWithFlags(&osDone_, hipEventDisableTiming));
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) == hipSuccess &&
+      khz > 0) {
+    clockKhz_ = khz;
+  }
+  GLX_HIP_CHECK(hipDeviceSynchronize());
+}
+
+void HipPlanExecutor::checkOneShot() {
+  if (!oneShot_) return;
+  const int st = *reinterpret_cast<volatile int*>(osStatus_);
+  if (st != 0) {
+    GLX_THROW_TIMEOUT("Timed out waiting for data from rank ", st - 1, " (rank ",
+                      contextRank_, ", one-shot allreduce, timeout ",
+                      effectiveTimeout().count(), " ms)");
+  }
+}
+
+void HipPlanExecutor::runOneShot(char* ptr0) {
+  if (!resolved_) resolvePeers();
+  checkOneShot();  // an earlier asynchronous call that timed out
+  const int P = contextSize_;
+  const uint64_t e = ++osEpoch_;
+  const size_t parity = (size_t)(e & 1) * (size_t)P * osRegion_;
+  glx::OneShotParams p = os_;
+  p.buf = ptr0;
+  p.epoch = e;
+  p.timeoutTicks = (uint64_t)effectiveTimeout().count() * (uint64_t)clockKhz_;
+  for (int j = 0; j < P; j++) {
+    if (j == contextRank_) {
+      p.push[j] = nullptr;
+      p.land[j] = ptr0;
+      p.flagOut[j] = nullptr;
+      continue;
+    }
+    char* peer = osPeer_.at(j);
+    p.push[j] = peer + parity + (size_t)contextRank_ * osRegion_;
+    p.land[j] = osBase_ + parity + (size_t)j * osRegion_;
+    p.flagOut[j] = reinterpret_cast<uint64_t*>(peer + 2 * (size_t)P * osRegion_) +
+                   (size_t)contextRank_ * (size_t)p.G;
+  }
+  // epochs stay ordered even when calls come on different streams
+  if (osLaunched_) GLX_HIP_CHECK(hipStreamWaitEvent(compute_, osDone_, 0));
+  if (hostMode_) waitH2D(compute_, computeH2dWaited_, 0, count_);
+  GLX_TRACE("r%d one-shot epoch %lu (G=%d slice=%zu)", contextRank_, (unsigned long)e, p.G,
+            p.slice);
+  GLX_HIP_CHECK(glx::launch_oneshot(op_, dtype_, p, compute_));
+  GLX_HIP_CHECK(hipEventRecord(osDone_, compute_));
+  osLaunched_ = true;
+  if (hostMode_) {
+    GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, osDone_, 0));
+    copyBack({glx::Range{0, count_}});
+  }
 }
 
 }  // namespace gloo

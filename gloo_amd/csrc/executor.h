@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "context.h"
+#include "kernels.h"
 #include "plan.h"
 
 namespace gloo {
@@ -77,6 +78,9 @@ class HipPlanExecutor : public Algorithm {
   static void setCopyEngine(int engine);
   static int copyEngine();
   const glx::Plan& plan() const { return plan_; }
+  // True when the replicated schedule runs as one device-driven kernel per
+  // rank (oneshot_kernels.hip) instead of host-mediated steps.
+  bool oneShot() const { return oneShot_; }
 
  private:
   struct OutChan {  // this rank -> peer
@@ -188,6 +192,32 @@ class HipPlanExecutor : public Algorithm {
   std::vector<Pending> pending_;
   std::vector<InflightSend> inflight_;
   std::vector<void*> ipcOpened_;
+
+  // One-shot replicated schedule (oneshot_kernels.hip): no channels, no
+  // scratch blocks; one uncached allocation per rank holding the landing
+  // regions [2 parities][P ranks][osRegion_ bytes] and the flags [P][G].
+  bool oneShot_ = false;
+  char* osBase_ = nullptr;
+  size_t osRegion_ = 0;
+  std::map<int, char*> osPeer_;  // peers' osBase_ (IPC-mapped)
+  glx::OneShotParams os_{};      // fixed part of the kernel's parameters
+  uint64_t osEpoch_ = 0;
+  int* osStatus_ = nullptr;      // pinned host word the kernel flags timeouts in
+  int* osStatusDev_ = nullptr;
+  hipEvent_t osDone_ = nullptr;
+  bool osLaunched_ = false;
+  int clockKhz_ = 100000;        // s_memrealtime rate
+  static bool oneShotWanted(const Context& ctx, int algo, int64_t count);
+
+ public:
+  // Whether replicated-schedule executors on this context will run as the
+  // one-shot kernel (GLOO_AMD_ONESHOT, ranks on distinct devices/processes).
+  static bool oneShotAvailable(const Context& ctx);
+
+ private:
+  void setupOneShot();
+  void runOneShot(char* ptr0);
+  void checkOneShot();
 };
 
 }  // namespace gloo

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime_api.h>
 #include <stddef.h>
+#include <stdint.h>
 
 #include <vector>
 
@@ -34,6 +35,30 @@ hipError_t launch_copy(void* dst, const void* src, size_t bytes, hipStream_t s);
 // Grid (workgroups) of the copy kernel.
 void set_copy_blocks(int blocks);
 int copy_blocks();
+
+// One-shot replicated allreduce (oneshot_kernels.hip): one kernel per rank
+// pushes the buffer to every peer, waits on per-slice flags and folds every
+// chunk along its ring chain.  All pointers are device-accessible; push/land
+// regions and flags are uncached device memory (peers' via IPC).
+constexpr int kOsMaxRanks = 8;
+constexpr int kOsMaxSlices = 256;  // workgroups (= slices) per launch
+struct OneShotParams {
+  char* buf;                        // this rank's buffer: input and result
+  char* push[kOsMaxRanks];          // this rank's landing region in peer j (j != rank)
+  const char* land[kOsMaxRanks];    // rank k's landing region here (k != rank)
+  uint64_t* flagOut[kOsMaxRanks];   // peer j's flag row for this rank ([G] words)
+  const uint64_t* flagIn;           // this rank's flags: [P][G] words
+  int* status;                      // host-visible: 1 + rank that never arrived
+  uint64_t epoch;                   // >= 1, +1 per call, equal on all ranks
+  uint64_t timeoutTicks;            // s_memrealtime ticks
+  size_t count;                     // elements
+  size_t slice;                     // elements per workgroup, multiple of 16 / esize
+  int P, rank, G;
+  int njobs;                        // chunk ranges with their own chain
+  size_t jobOff[kOsMaxRanks], jobLen[kOsMaxRanks];
+  uint8_t chain[kOsMaxRanks][kOsMaxRanks];  // fold order: acc = op(x[chain[i]], acc)
+};
+hipError_t launch_oneshot(int op, int dtype, const OneShotParams& p, hipStream_t s);
 
 // Tuning knobs of the vector kernel (lanes' unroll depth, grid cap per CU,
 // nontemporal loads/stores: 0/1, -1 = keep).

@@ -702,7 +702,7 @@ Plan planFnBcube(int rank, int size, int64_t count) {
   return p;
 }
 
-int autoRingSchedule(int size, int64_t bytes, bool fn) {
+int autoRingSchedule(int size, int64_t bytes, bool fn, bool deviceDriven) {
   const int ring = fn ? ALGO_FN_RING : ALGO_RING_CHUNKED;
   const int mesh = fn ? ALGO_FN_RING_MESH : ALGO_RING_CHUNKED_MESH;
   const int repl = fn ? ALGO_FN_RING_REPL : ALGO_RING_CHUNKED_REPL;
@@ -712,7 +712,10 @@ int autoRingSchedule(int size, int64_t bytes, bool fn) {
     if (v == "mesh") return mesh;
     if (v == "replicated") return repl;
   }
-  int64_t maxRepl = int64_t(256) << 10;  // the reference's kOnDeviceThreshold (algorithm.cc:16)
+  // host-mediated: the reference's kOnDeviceThreshold (algorithm.cc:16);
+  // one-shot kernel: where its (P-1)·S per-link bytes start to cost more than
+  // the mesh's two host-mediated rounds
+  int64_t maxRepl = deviceDriven ? (int64_t(2) << 20) : (int64_t(256) << 10);
   if (const char* e = std::getenv("GLOO_AMD_REPLICATED_MAX_BYTES")) maxRepl = std::atoll(e);
   if (size <= 1) return ring;
   return bytes <= maxRepl ? repl : mesh;

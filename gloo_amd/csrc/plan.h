@@ -115,11 +115,13 @@ Plan makePlan(int algo, int rank, int size, int64_t count,
               const PlanParams& prm = PlanParams());
 
 // Automatic data movement for the ring's result (all bit-identical): the
-// one-round replicated schedule up to `replicatedMaxBytes` per rank, the
-// all-links mesh above.  fn: the function-style RING family instead of the
-// class ring_chunked one.  Env GLOO_AMD_RING_SCHEDULE=ring|mesh|replicated
-// forces one; GLOO_AMD_REPLICATED_MAX_BYTES moves the threshold.
-int autoRingSchedule(int size, int64_t bytes, bool fn);
+// one-round replicated schedule up to a threshold per rank, the all-links
+// mesh above.  fn: the function-style RING family instead of the class
+// ring_chunked one.  deviceDriven: the replicated schedule will run as the
+// one-shot kernel (no host round trips), which moves the threshold from
+// 256 KiB to 2 MiB.  Env GLOO_AMD_RING_SCHEDULE=ring|mesh|replicated forces
+// one; GLOO_AMD_REPLICATED_MAX_BYTES sets the threshold.
+int autoRingSchedule(int size, int64_t bytes, bool fn, bool deviceDriven = false);
 
 // Host-memory endpoints: when the user's buffer is in host
 // memory the executor stages it through a device buffer.  This derives from

@@ -263,6 +263,13 @@ int glx_allreduce(glx_context* ctx, int algorithm, int dtype, int op,
 int glx_algorithm_run(glx_algorithm* alg);
 /* Number of bytes moved over the peer links by this rank in one run(). */
 int64_t glx_algorithm_bytes_sent(glx_algorithm* alg);
+/* How run() executes: GLX_ENGINE_STEPS = the schedule's steps issued by the
+ * host (copies, reduce kernels, control-block counters); GLX_ENGINE_ONESHOT =
+ * the replicated schedule as one device-driven kernel per rank (small
+ * buffers, ranks on distinct devices or processes).  Results are identical. */
+#define GLX_ENGINE_STEPS 0
+#define GLX_ENGINE_ONESHOT 1
+int glx_algorithm_engine(glx_algorithm* alg);
 void glx_algorithm_destroy(glx_algorithm* alg);
 
 /* ---- schedule introspection (host logic; no GPU needed) ----------------- */

@@ -5,6 +5,9 @@
 algo: ring_chunked | halving_doubling | ring_chunked_mesh (class algorithms)
       fn_ring | fn_bcube | fn_ring_mesh (gloo_amd.allreduce, two calls with
       different buffers, the second out of place)
+      oneshot (the replicated schedule as one device-driven kernel per rank:
+      class and function style, dtypes x ops x sizes, device and host
+      buffers, repeated runs; prints per-op latencies)
 
 Checks its result against the oracle and prints OK."""
 import os
@@ -25,6 +28,8 @@ def main():
     from oracle import oracle as O
 
     N = 100003
+    if algo == "oneshot":
+        return run_oneshot(store_dir, rank, size)
     if algo.startswith("fn_"):
         return run_fn(store_dir, rank, size, algo, N)
     code = O.HALVING_DOUBLING if algo == "halving_doubling" else O.RING_CHUNKED
@@ -98,6 +103,100 @@ def run_fn(store_dir, rank, size, algo, N):
     ctx.close()
     if not ok:
         print("MISMATCH rank", rank)
+        sys.exit(1)
+    print("OK")
+
+
+def run_oneshot(store_dir, rank, size):
+    import time
+
+    import numpy as np
+    import torch
+
+    import gloo_amd
+    from helpers import case_inputs
+    from oracle import oracle as O
+
+    store = gloo_amd.rendezvous.FileStore(store_dir)
+    ctx = gloo_amd.rendezvous.Context(rank, size, 0)
+    ctx.setTimeout(20)
+    ctx.connectFullMesh(store)
+    bad = []
+
+    def same(got, exp):
+        return np.array_equal(np.ascontiguousarray(got).view(np.uint8),
+                              np.ascontiguousarray(exp).view(np.uint8))
+
+    from test_reduce_gpu import from_dev, to_dev
+
+    cases = []
+    for n in (1, 3, 255, 256, 1024, 4099, 65539, 262144, 1 << 20):
+        cases.append((n, O.FLOAT32, O.SUM))
+    for dt in (O.FLOAT16, O.INT32, O.FLOAT64, O.INT8, O.UINT64):
+        for op in (O.SUM, O.PRODUCT, O.MAX, O.MIN):
+            cases.append((4099, dt, op))
+    cases.append((77777, O.FLOAT16, O.SUM))
+    for seed, (n, dt, op) in enumerate(cases):
+        ins = case_inputs(size, n, dt, 1, 0, seed=100 + seed)
+        exp = O.allreduce(O.RING_CHUNKED, op, dt, ins)[rank][0]
+        buf = to_dev(ins[rank][0], dt)
+        alg = gloo_amd.AllreduceRingChunked(ctx, [buf], fn=gloo_amd.ReductionFunction(op),
+                                           schedule="replicated", dtype=dt)
+        if alg.engine() != "oneshot":
+            bad.append(("engine", n, dt, op, alg.engine()))
+        for it in range(3):
+            buf.copy_(to_dev(ins[rank][0], dt))
+            torch.cuda.synchronize()
+            alg.run()
+            got = from_dev(buf, dt)
+            if not same(got, exp):
+                bad.append(("class", n, dt, op, it))
+        alg.close()
+    # host buffers (numpy): staged H2D, kernel, D2H
+    n = 4099
+    ins = case_inputs(size, n, O.FLOAT32, 1, 0, seed=7)
+    exp = O.allreduce(O.RING_CHUNKED, O.SUM, O.FLOAT32, ins)[rank][0]
+    host = ins[rank][0].copy()
+    alg = gloo_amd.AllreduceRingChunked(ctx, [host], schedule="replicated")
+    for it in range(2):
+        host[:] = ins[rank][0]
+        alg.run()
+        if not same(host, exp):
+            bad.append(("host", n, it))
+    alg.close()
+    # function style: UNSPECIFIED at a small size -> RING's replicated schedule
+    for n in (1000, 65536):
+        data = case_inputs(size, n, O.FLOAT32, 1, 0, seed=11)
+        exp = O.allreduce_fn(O.FN_RING, O.SUM, O.FLOAT32, [[] for _ in range(size)],
+                             data)[rank][0]
+        for it in range(2):
+            out = torch.from_numpy(data[rank][0].copy()).cuda()
+            opts = gloo_amd.AllreduceOptions(ctx)
+            opts.setAlgorithm(gloo_amd.AllreduceOptions.Algorithm.UNSPECIFIED)
+            opts.setOutput(out)
+            opts.setReduceFunction(gloo_amd.ReductionFunction.sum)
+            gloo_amd.allreduce(opts)
+            if not same(out.cpu().numpy(), exp):
+                bad.append(("fn", n, it))
+    # latency: one-shot vs the host-mediated replicated steps (same bits)
+    for n in (1024, 65536, 262144):
+        buf = torch.zeros(n, device="cuda")
+        alg = gloo_amd.AllreduceRingChunked(ctx, [buf], schedule="replicated")
+        for _ in range(5):
+            alg.run()
+        iters = 50
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            alg.run()
+        us = (time.perf_counter() - t0) / iters * 1e6
+        print("LAT rank %d P %d elems %d engine %s us %.1f" % (rank, size, n, alg.engine(), us))
+        alg.close()
+    store.set("done/%d" % rank, b"1")
+    for r in range(size):
+        store.get("done/%d" % r, timeout_ms=60000)
+    ctx.close()
+    if bad:
+        print("MISMATCH rank", rank, bad[:10])
         sys.exit(1)
     print("OK")
 

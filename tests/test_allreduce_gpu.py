@@ -257,6 +257,33 @@ def test_multiprocess_ipc(algo):
             assert "OK" in outs[r]
 
 
+@pytest.mark.parametrize("P", [2, 4])
+def test_oneshot_multiprocess(P):
+    """The replicated schedule as one device-driven kernel per rank
+    (oneshot_kernels.hip), one process per rank: peers' kernels push into
+    each other's IPC-mapped uncached regions and wait on flags.  Bit-exact
+    with the reference ring's chains for every dtype/op, device and host
+    buffers, class and function style, repeated runs (mp_worker.py)."""
+    with tempfile.TemporaryDirectory() as d:
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), "oneshot"],
+                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                 for r in range(P)]
+        outs = []
+        for p in procs:
+            try:
+                o, _ = p.communicate(timeout=240)
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+            outs.append(o.decode(errors="replace"))
+        for r, p in enumerate(procs):
+            print(outs[r])
+            assert p.returncode == 0, "rank %d failed:\n%s" % (r, outs[r])
+            assert "OK" in outs[r]
+
+
 @pytest.mark.parametrize("split", [2, 4])
 @pytest.mark.parametrize("algo", [O.RING_CHUNKED, O.HALVING_DOUBLING, MESH],
                          ids=["ring_chunked", "halving_doubling", "mesh"])
