@@ -41,6 +41,15 @@ def set_copy_engine(engine, blocks=0):
     errors.check(_lib.lib.glx_set_copy_engine(code, int(blocks)), "set_copy_engine")
 
 
+def set_mesh_engine(engine):
+    """Engine of mesh-schedule algorithms created afterwards when the ranks
+    are on distinct devices or processes: "device" (the two-shot kernel, one
+    device-driven launch per rank; default) or "steps" (host-issued copies
+    and fold kernels).  Same results either way."""
+    code = {"steps": 0, "device": 2}[engine]
+    errors.check(_lib.lib.glx_set_mesh_engine(code), "set_mesh_engine")
+
+
 def device_count():
     import ctypes
     n = ctypes.c_int(0)

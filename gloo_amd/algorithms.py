@@ -170,9 +170,10 @@ class Algorithm:
         return lib.glx_algorithm_bytes_sent(self._h)
 
     def engine(self):
-        """"steps" (host-issued schedule steps) or "oneshot" (the replicated
+        """"steps" (host-issued schedule steps), "oneshot" (the replicated
+        schedule as one device-driven kernel per rank) or "twoshot" (the mesh
         schedule as one device-driven kernel per rank)."""
-        return {0: "steps", 1: "oneshot"}[lib.glx_algorithm_engine(self._h)]
+        return {0: "steps", 1: "oneshot", 2: "twoshot"}[lib.glx_algorithm_engine(self._h)]
 
     def close(self):
         h = getattr(self, "_h", None)

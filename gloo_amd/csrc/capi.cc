@@ -173,6 +173,14 @@ int glx_set_copy_engine(int engine, int blocks) {
   return GLX_OK;
 }
 
+int glx_set_mesh_engine(int engine) {
+  if (engine != GLX_ENGINE_STEPS && engine != GLX_ENGINE_TWOSHOT) {
+    return fail(GLX_ERR_INVALID, "mesh engine must be GLX_ENGINE_STEPS or GLX_ENGINE_TWOSHOT");
+  }
+  gloo::HipPlanExecutor::setMeshEngine(engine);
+  return GLX_OK;
+}
+
 int glx_set_copy_split(int k) {
   if (k < 1 || k > 8) return fail(GLX_ERR_INVALID, "glx_set_copy_split: k must be in [1, 8]");
   gloo::HipPlanExecutor::setCopySplit(k);
@@ -317,7 +325,7 @@ glx_algorithm* glx_allreduce_create(glx_context* ctx, int algo, void* const* ptr
                                     int nstreams) {
   if (algo == GLX_ALGO_RING_CHUNKED_AUTO && ctx != nullptr && count >= 0) {
     algo = glx::autoRingSchedule(ctx->c->size, (int64_t)count * (int64_t)glx_dtype_size(dtype),
-                                 /*fn=*/false, gloo::HipPlanExecutor::oneShotAvailable(*ctx->c));
+                                 /*fn=*/false, gloo::HipPlanExecutor::deviceEnginesAvailable(*ctx->c));
   }
   if (algo != GLX_ALGO_RING_CHUNKED && algo != GLX_ALGO_HALVING_DOUBLING &&
       algo != GLX_ALGO_RING_CHUNKED_MESH && algo != GLX_ALGO_RING_CHUNKED_REPL) {
@@ -365,7 +373,7 @@ int64_t glx_algorithm_bytes_sent(glx_algorithm* alg) {
 
 int glx_algorithm_engine(glx_algorithm* alg) {
   if (alg == nullptr) return -1;
-  return alg->a->oneShot() ? GLX_ENGINE_ONESHOT : GLX_ENGINE_STEPS;
+  return alg->a->engine();
 }
 
 void glx_algorithm_destroy(glx_algorithm* alg) {

@@ -36,7 +36,7 @@ int scheduleFor(int algorithm, const Context& ctx, int64_t bytes) {
     case AllreduceOptions::UNSPECIFIED:
       // RING's result (gloo/allreduce.cc:134-137) moved the fastest way
       return glx::autoRingSchedule(ctx.size, bytes, /*fn=*/true,
-                                   HipPlanExecutor::oneShotAvailable(ctx));
+                                   HipPlanExecutor::deviceEnginesAvailable(ctx));
     case AllreduceOptions::RING: return glx::ALGO_FN_RING;
     case AllreduceOptions::RING_MESH: return glx::ALGO_FN_RING_MESH;
     case AllreduceOptions::RING_REPLICATED: return glx::ALGO_FN_RING_REPL;

@@ -1,5 +1,5 @@
 // elem_ops.h -- device-side element operations shared by the HIP kernels
-// (reduce_kernels.hip, oneshot_kernels.hip): the reference CPU path's
+// (reduce_kernels.hip, xgmi_kernels.hip): the reference CPU path's
 // semantics, bit for bit (see reduce_kernels.hip's header for the rules).
 #pragma once
 

@@ -174,9 +174,9 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
     }
   }
 
-  oneShot_ = oneShotWanted(*ctx, algo, count_);
-  if (oneShot_) {
-    setupOneShot();
+  engine_ = engineFor(*ctx, algo, count_);
+  if (engine_ != kEngineSteps) {
+    setupDevice();
   } else {
     allocScratch();
   }
@@ -184,7 +184,7 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
   // Channels named by the plan; allocate our counter words.
   auto& ctl = ctx->localControl();
   stepChan_.assign(plan_.steps.size(), -1);
-  for (size_t i = 0; i < plan_.steps.size() && !oneShot_; i++) {
+  for (size_t i = 0; i < plan_.steps.size() && engine_ == kEngineSteps; i++) {
     const auto& s = plan_.steps[i];
     if (s.kind == glx::SEND) {
       int idx = outIndex((int)s.peer, (int)s.channel);
@@ -254,9 +254,9 @@ HipPlanExecutor::~HipPlanExecutor() noexcept(false) {
   for (auto& e : events_) hipEventDestroy(e);
   if (computeMark_) hipEventDestroy(computeMark_);
   for (auto& b : blocks_) hipFree(b.ptr);
-  if (osBase_) hipFree(osBase_);
-  if (osStatus_) hipHostFree(osStatus_);
-  if (osDone_) hipEventDestroy(osDone_);
+  for (char* d : ddBlocks_) hipFree(d);
+  if (ddStatus_) hipHostFree(ddStatus_);
+  if (ddDone_) hipEventDestroy(ddDone_);
   for (auto& c : copies_) hipStreamDestroy(c.s);
   if (ownCompute_ && compute_) hipStreamDestroy(compute_);
   auto& ctl = context_->localControl();
@@ -308,12 +308,13 @@ void HipPlanExecutor::publish() {
     putPod<int32_t>(b, DIR_OUT);
     putPod<int32_t>(b, (int32_t)oc.creditWord);
   }
-  putPod<int32_t>(b, oneShot_ ? 1 : 0);
-  if (oneShot_) {
-    putPod<uint64_t>(b, (uint64_t)(uintptr_t)osBase_);
+  putPod<int32_t>(b, engine_);
+  putPod<int32_t>(b, (int32_t)ddBlocks_.size());
+  for (char* d : ddBlocks_) {
+    putPod<uint64_t>(b, (uint64_t)(uintptr_t)d);
     hipIpcMemHandle_t h;
     memset(&h, 0, sizeof(h));
-    int32_t haveIpc = hipIpcGetMemHandle(&h, osBase_) == hipSuccess ? 1 : 0;
+    int32_t haveIpc = hipIpcGetMemHandle(&h, d) == hipSuccess ? 1 : 0;
     (void)hipGetLastError();
     putPod<int32_t>(b, haveIpc);
     putPod(b, h);
@@ -326,7 +327,7 @@ void HipPlanExecutor::resolvePeers() {
   std::map<int, bool> peers;
   for (auto& oc : out_) peers[oc.peer] = true;
   for (auto& ic : in_) peers[ic.peer] = true;
-  for (int r = 0; r < contextSize_ && oneShot_; r++) {
+  for (int r = 0; r < contextSize_ && engine_ != kEngineSteps; r++) {
     if (r != contextRank_) peers[r] = true;
   }
   for (auto& kv : peers) {
@@ -385,23 +386,26 @@ void HipPlanExecutor::resolvePeers() {
         if (idx >= 0) in_[idx].credit = pe.ctl->word((uint32_t)word);
       }
     }
-    const int32_t peerOneShot = getPod<int32_t>(b, at);
-    GLX_ENFORCE(peerOneShot == (oneShot_ ? 1 : 0), "rank ", r,
-                " chose a different replicated-schedule engine (schedules disagree)");
-    if (oneShot_) {
+    const int32_t peerEngine = getPod<int32_t>(b, at);
+    GLX_ENFORCE(peerEngine == engine_, "rank ", r, " runs engine ", peerEngine, ", rank ",
+                contextRank_, " engine ", engine_, " (schedules disagree)");
+    const int32_t nb = getPod<int32_t>(b, at);
+    std::vector<char*> blocks;
+    for (int32_t k = 0; k < nb; k++) {
       const uint64_t ptr = getPod<uint64_t>(b, at);
       const int32_t haveIpc = getPod<int32_t>(b, at);
       const hipIpcMemHandle_t h = getPod<hipIpcMemHandle_t>(b, at);
       if (pe.sameProcess) {
-        osPeer_[r] = reinterpret_cast<char*>((uintptr_t)ptr);
+        blocks.push_back(reinterpret_cast<char*>((uintptr_t)ptr));
       } else {
-        GLX_ENFORCE(haveIpc, "rank ", r, " could not export its one-shot regions");
+        GLX_ENFORCE(haveIpc, "rank ", r, " could not export its device-engine block ", k);
         void* p = nullptr;
         GLX_HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
         ipcOpened_.push_back(p);
-        osPeer_[r] = static_cast<char*>(p);
+        blocks.push_back(static_cast<char*>(p));
       }
     }
+    if (engine_ != kEngineSteps) ddPeer_[r] = blocks;
   }
   for (auto& oc : out_) {
     GLX_ENFORCE(oc.delivery != nullptr, "rank ", oc.peer, " has no receive channel ",
@@ -574,7 +578,7 @@ void HipPlanExecutor::run() {
   GLX_TRACE("r%d sync", contextRank_);
   if (!userStream_) {
     GLX_HIP_CHECK(hipStreamSynchronize(compute_));
-    checkOneShot();
+    checkDevice();
   }
   GLX_TRACE("r%d done", contextRank_);
 }
@@ -651,7 +655,7 @@ void HipPlanExecutor::runFn(const FnCall& call) {
   }
   if (call.stream == nullptr) {
     GLX_HIP_CHECK(hipStreamSynchronize(compute_));
-    checkOneShot();
+    checkDevice();
   }
 }
 
@@ -701,7 +705,7 @@ void HipPlanExecutor::runFnHost(const FnCall& call) {
     GLX_HIP_CHECK(hipMemcpyAsync(p, out0, bytes, hipMemcpyDeviceToHost, compute_));
   }
   GLX_HIP_CHECK(hipStreamSynchronize(compute_));
-  checkOneShot();
+  checkDevice();
 }
 
 void HipPlanExecutor::setupHostMode() {
@@ -791,12 +795,12 @@ void HipPlanExecutor::runHost() {
   GLX_HIP_CHECK(hipStreamSynchronize(d2h_));
   GLX_HIP_CHECK(hipStreamSynchronize(compute_));
   GLX_HIP_CHECK(hipStreamSynchronize(h2d_));
-  checkOneShot();
+  checkDevice();
 }
 
 void HipPlanExecutor::exchange(char* ptr0) {
-  if (oneShot_) {
-    runOneShot(ptr0);
+  if (engine_ != kEngineSteps) {
+    runDevice(ptr0);
     return;
   }
   if (!resolved_) resolvePeers();
@@ -980,24 +984,76 @@ void HipPlanExecutor::exchange(char* ptr0) {
 }
 
 // ---------------------------------------------------------------------------
-// One-shot replicated schedule
+// Device-driven engines (xgmi_kernels.hip)
 // ---------------------------------------------------------------------------
 
-// GLOO_AMD_ONESHOT=0 keeps the replicated schedule host-mediated, =1 forces
-// the device-driven kernel; by default it is used whenever no two ranks are
-// threads sharing one device (their kernels might not be co-resident).  The
-// inputs are the same on every rank, so every rank makes the same choice.
-bool HipPlanExecutor::oneShotWanted(const Context& ctx, int algo, int64_t count) {
-  if (algo != glx::ALGO_RING_CHUNKED_REPL && algo != glx::ALGO_FN_RING_REPL) return false;
-  return count > 0 && oneShotAvailable(ctx);
+namespace {
+
+int initialMeshEngine() {
+  const char* e = std::getenv("GLOO_AMD_MESH_ENGINE");
+  return (e != nullptr && std::strcmp(e, "steps") == 0) ? HipPlanExecutor::kEngineSteps
+                                                        : HipPlanExecutor::kEngineTwoShot;
 }
 
-bool HipPlanExecutor::oneShotAvailable(const Context& ctx) {
+std::atomic<int> g_mesh_engine{initialMeshEngine()};
+
+}  // namespace
+
+void HipPlanExecutor::setMeshEngine(int engine) {
+  g_mesh_engine.store(engine == kEngineSteps ? kEngineSteps : kEngineTwoShot);
+}
+
+int HipPlanExecutor::meshEngine() { return g_mesh_engine.load(); }
+
+bool HipPlanExecutor::deviceEnginesAvailable(const Context& ctx) {
   if (ctx.size < 2 || ctx.size > glx::kOsMaxRanks) return false;
   const char* e = std::getenv("GLOO_AMD_ONESHOT");
   if (e != nullptr && e[0] == '0') return false;
   if (e != nullptr && e[0] == '1') return true;
   return !ctx.ranksShareDevice();
+}
+
+// The inputs are the same on every rank, so every rank makes the same choice
+// (and publish/resolve checks that they did).
+int HipPlanExecutor::engineFor(const Context& ctx, int algo, int64_t count) {
+  if (count <= 0 || !deviceEnginesAvailable(ctx)) return kEngineSteps;
+  if (algo == glx::ALGO_RING_CHUNKED_REPL || algo == glx::ALGO_FN_RING_REPL) {
+    return kEngineOneShot;
+  }
+  if (algo == glx::ALGO_RING_CHUNKED_MESH || algo == glx::ALGO_FN_RING_MESH) {
+    return meshEngine();
+  }
+  return kEngineSteps;
+}
+
+// Uncached: peers' stores land in our HBM behind our caches' back.
+char* HipPlanExecutor::ddAlloc(size_t bytes) {
+  char* d = nullptr;
+  GLX_HIP_CHECK(hipExtMallocWithFlags((void**)&d, bytes, hipDeviceMallocUncached));
+  ddBlocks_.push_back(d);
+  GLX_HIP_CHECK(hipMemset(d, 0, bytes));
+  return d;
+}
+
+void HipPlanExecutor::setupDevice() {
+  if (engine_ == kEngineOneShot) {
+    setupOneShot();
+  } else {
+    setupTwoShot();
+  }
+  GLX_HIP_CHECK(hipHostMalloc((void**)&ddStatus_, sizeof(int),
+                              hipHostMallocMapped | hipHostMallocCoherent));
+  *reinterpret_cast<volatile int*>(ddStatus_) = 0;
+  GLX_HIP_CHECK(hipHostGetDevicePointer((void**)&ddStatusDev_, ddStatus_, 0));
+  os_.status = ddStatusDev_;
+  ts_.status = ddStatusDev_;
+  GLX_HIP_CHECK(hipEventCreateWithFlags(&ddDone_, hipEventDisableTiming));
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) == hipSuccess &&
+      khz > 0) {
+    clockKhz_ = khz;
+  }
+  GLX_HIP_CHECK(hipDeviceSynchronize());
 }
 
 void HipPlanExecutor::setupOneShot() {
@@ -1030,70 +1086,142 @@ void HipPlanExecutor::setupOneShot() {
     p.jobLen[p.njobs] = (size_t)s.len;
     p.njobs++;
   }
-  osRegion_ = ((size_t)count_ * esize_ + 255) & ~(size_t)255;
-  const size_t flagBytes = (size_t)P * (size_t)p.G * sizeof(uint64_t);
-  const size_t bytes = 2 * (size_t)P * osRegion_ + flagBytes;
-  // uncached: peers' stores land in our HBM behind our caches' back
-  GLX_HIP_CHECK(hipExtMallocWithFlags((void**)&osBase_, bytes, hipDeviceMallocUncached));
-  GLX_HIP_CHECK(hipMemset(osBase_, 0, bytes));
-  p.flagIn = reinterpret_cast<const uint64_t*>(osBase_ + 2 * (size_t)P * osRegion_);
-  GLX_HIP_CHECK(hipHostMalloc((void**)&osStatus_, sizeof(int),
-                              hipHostMallocMapped | hipHostMallocCoherent));
-  *reinterpret_cast<volatile int*>(osStatus_) = 0;
-  GLX_HIP_CHECK(hipHostGetDevicePointer((void**)&osStatusDev_, osStatus_, 0));
-  p.status = osStatusDev_;
-  GLX_HIP_CHECK(hipEventCreateWithFlags(&osDone_, hipEventDisableTiming));
-  int khz = 0;
-  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) == hipSuccess &&
-      khz > 0) {
-    clockKhz_ = khz;
-  }
-  GLX_HIP_CHECK(hipDeviceSynchronize());
+  ddSlot_ = ((size_t)count_ * esize_ + 255) & ~(size_t)255;
+  ddAlloc((size_t)P * ddSlot_);
+  ddAlloc((size_t)P * ddSlot_);
+  p.flagIn = reinterpret_cast<const uint64_t*>(
+      ddAlloc((size_t)P * (size_t)p.G * sizeof(uint64_t)));
 }
 
-void HipPlanExecutor::checkOneShot() {
-  if (!oneShot_) return;
-  const int st = *reinterpret_cast<volatile int*>(osStatus_);
+void HipPlanExecutor::setupTwoShot() {
+  const int P = contextSize_;
+  glx::TwoShotParams& p = ts_;
+  p.P = P;
+  p.rank = contextRank_;
+  // owners' ranges and this rank's chain, read off the mesh plan: channel-0
+  // SENDs carry this rank's copy of range j to owner j, the FOLD our own range
+  for (int c = 0; c < glx::kOsMaxRanks; c++) p.rangeOff[c] = p.rangeLen[c] = 0;
+  for (int i = 0; i < P; i++) p.chain[i] = (uint8_t)i;
+  size_t maxLen = 0;
+  for (const auto& s : plan_.steps) {
+    if (s.kind == glx::SEND && s.channel == 0) {
+      p.rangeOff[s.peer] = (size_t)s.off;
+      p.rangeLen[s.peer] = (size_t)s.len;
+      maxLen = std::max(maxLen, (size_t)s.len);
+    }
+  }
+  const glx::Step* fold = nullptr;
+  for (const auto& s : plan_.steps) {
+    if (s.kind == glx::FOLD) fold = &s;
+  }
+  if (fold != nullptr) {
+    p.rangeOff[contextRank_] = (size_t)fold->off;
+    p.rangeLen[contextRank_] = (size_t)fold->len;
+    maxLen = std::max(maxLen, (size_t)fold->len);
+  }
+  // every non-empty range is a channel-0 SEND target or our own FOLD, so
+  // maxLen is the plan's largest range: FOLD sources are multiples of it + pad
+  if (fold != nullptr) {
+    const auto& f = plan_.folds[(size_t)fold->boff];
+    GLX_ENFORCE((int)f.size() == P, "two-shot: fold of ", f.size(), " sources for ", P,
+                " ranks");
+    const int64_t region = (int64_t)maxLen + glx::kPadElems;
+    for (int i = 0; i < P; i++) {
+      const int64_t r = f[(size_t)i];
+      GLX_ENFORCE(r < 0 || r % region == 0, "two-shot: unexpected fold source");
+      p.chain[i] = (uint8_t)(r < 0 ? contextRank_ : (int)(r / region));
+    }
+  }
+  const size_t V = 16 / esize_;
+  const size_t minSlice = 4096 / esize_;
+  size_t slice = (maxLen + glx::kOsMaxSlices - 1) / glx::kOsMaxSlices;
+  slice = (std::max(slice, minSlice) + V - 1) / V * V;
+  p.slice = slice;
+  p.G = (int)std::max<size_t>(1, (maxLen + slice - 1) / slice);
+  ddSlot_ = (maxLen * esize_ + 16 + 255) & ~(size_t)255;
+  for (int k = 0; k < 4; k++) ddAlloc((size_t)P * ddSlot_);  // RS 0/1, AG 0/1
+  char* flags = ddAlloc(2 * (size_t)P * (size_t)p.G * sizeof(uint64_t));
+  p.flagAIn = reinterpret_cast<const uint64_t*>(flags);
+  p.flagBIn = reinterpret_cast<const uint64_t*>(flags) + (size_t)P * (size_t)p.G;
+}
+
+void HipPlanExecutor::checkDevice() {
+  if (engine_ == kEngineSteps) return;
+  const int st = *reinterpret_cast<volatile int*>(ddStatus_);
   if (st != 0) {
     GLX_THROW_TIMEOUT("Timed out waiting for data from rank ", st - 1, " (rank ",
-                      contextRank_, ", one-shot allreduce, timeout ",
+                      contextRank_, ", device-driven allreduce, timeout ",
                       effectiveTimeout().count(), " ms)");
   }
 }
 
-void HipPlanExecutor::runOneShot(char* ptr0) {
+void HipPlanExecutor::runDevice(char* ptr0) {
   if (!resolved_) resolvePeers();
-  checkOneShot();  // an earlier asynchronous call that timed out
+  checkDevice();  // an earlier asynchronous call that timed out
   const int P = contextSize_;
-  const uint64_t e = ++osEpoch_;
-  const size_t parity = (size_t)(e & 1) * (size_t)P * osRegion_;
-  glx::OneShotParams p = os_;
-  p.buf = ptr0;
-  p.epoch = e;
-  p.timeoutTicks = (uint64_t)effectiveTimeout().count() * (uint64_t)clockKhz_;
-  for (int j = 0; j < P; j++) {
-    if (j == contextRank_) {
-      p.push[j] = nullptr;
-      p.land[j] = ptr0;
-      p.flagOut[j] = nullptr;
-      continue;
-    }
-    char* peer = osPeer_.at(j);
-    p.push[j] = peer + parity + (size_t)contextRank_ * osRegion_;
-    p.land[j] = osBase_ + parity + (size_t)j * osRegion_;
-    p.flagOut[j] = reinterpret_cast<uint64_t*>(peer + 2 * (size_t)P * osRegion_) +
-                   (size_t)contextRank_ * (size_t)p.G;
-  }
+  const uint64_t e = ++ddEpoch_;
+  const int par = (int)(e & 1);
+  const uint64_t ticks = (uint64_t)effectiveTimeout().count() * (uint64_t)clockKhz_;
   // epochs stay ordered even when calls come on different streams
-  if (osLaunched_) GLX_HIP_CHECK(hipStreamWaitEvent(compute_, osDone_, 0));
+  if (ddLaunched_) GLX_HIP_CHECK(hipStreamWaitEvent(compute_, ddDone_, 0));
   if (hostMode_) waitH2D(compute_, computeH2dWaited_, 0, count_);
-  GLX_TRACE("r%d one-shot epoch %lu (G=%d slice=%zu)", contextRank_, (unsigned long)e, p.G,
-            p.slice);
-  GLX_HIP_CHECK(glx::launch_oneshot(op_, dtype_, p, compute_));
-  GLX_HIP_CHECK(hipEventRecord(osDone_, compute_));
-  osLaunched_ = true;
+  if (engine_ == kEngineOneShot) {
+    glx::OneShotParams p = os_;
+    p.buf = ptr0;
+    p.epoch = e;
+    p.timeoutTicks = ticks;
+    for (int j = 0; j < P; j++) {
+      if (j == contextRank_) {
+        p.push[j] = nullptr;
+        p.land[j] = ptr0;
+        p.flagOut[j] = nullptr;
+        continue;
+      }
+      const auto& pb = ddPeer_.at(j);
+      p.push[j] = pb[(size_t)par] + (size_t)contextRank_ * ddSlot_;
+      p.land[j] = ddBlocks_[(size_t)par] + (size_t)j * ddSlot_;
+      p.flagOut[j] = reinterpret_cast<uint64_t*>(pb[2]) + (size_t)contextRank_ * (size_t)p.G;
+    }
+    GLX_TRACE("r%d one-shot epoch %lu (G=%d slice=%zu)", contextRank_, (unsigned long)e, p.G,
+              p.slice);
+    GLX_HIP_CHECK(glx::launch_oneshot(op_, dtype_, p, compute_));
+  } else {
+    glx::TwoShotParams p = ts_;
+    p.buf = ptr0;
+    p.epoch = e;
+    p.timeoutTicks = ticks;
+    const size_t G = (size_t)p.G;
+    // element i of range c at vbase + i*es: the 16-byte phase of a 16-byte
+    // aligned buffer (see xgmi_kernels.hip)
+    auto vbase = [&](char* slot, int c) {
+      const size_t off = p.rangeOff[c] * esize_;
+      return slot + (off % 16) - off;
+    };
+    for (int j = 0; j < P; j++) {
+      if (j == contextRank_) {
+        p.rsPush[j] = p.agPush[j] = nullptr;
+        p.rsLand[j] = p.agLand[j] = nullptr;
+        p.flagAOut[j] = p.flagBOut[j] = nullptr;
+        continue;
+      }
+      const auto& pb = ddPeer_.at(j);
+      const size_t mine = (size_t)contextRank_ * ddSlot_, theirs = (size_t)j * ddSlot_;
+      p.rsPush[j] = vbase(pb[(size_t)par] + mine, j);             // my copy of range j
+      p.rsLand[j] = vbase(ddBlocks_[(size_t)par] + theirs, contextRank_);  // j's copy of mine
+      p.agPush[j] = vbase(pb[2 + (size_t)par] + mine, contextRank_);       // my result
+      p.agLand[j] = vbase(ddBlocks_[2 + (size_t)par] + theirs, j);         // j's result
+      uint64_t* pf = reinterpret_cast<uint64_t*>(pb[4]);
+      p.flagAOut[j] = pf + (size_t)contextRank_ * G;
+      p.flagBOut[j] = pf + (size_t)P * G + (size_t)contextRank_ * G;
+    }
+    GLX_TRACE("r%d two-shot epoch %lu (G=%d slice=%zu)", contextRank_, (unsigned long)e, p.G,
+              p.slice);
+    GLX_HIP_CHECK(glx::launch_twoshot(op_, dtype_, p, compute_));
+  }
+  GLX_HIP_CHECK(hipEventRecord(ddDone_, compute_));
+  ddLaunched_ = true;
   if (hostMode_) {
-    GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, osDone_, 0));
+    GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, ddDone_, 0));
     copyBack({glx::Range{0, count_}});
   }
 }

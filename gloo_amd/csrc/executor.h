@@ -78,9 +78,9 @@ class HipPlanExecutor : public Algorithm {
   static void setCopyEngine(int engine);
   static int copyEngine();
   const glx::Plan& plan() const { return plan_; }
-  // True when the replicated schedule runs as one device-driven kernel per
-  // rank (oneshot_kernels.hip) instead of host-mediated steps.
-  bool oneShot() const { return oneShot_; }
+  // How run() executes: kEngineSteps (host-issued schedule steps),
+  // kEngineOneShot / kEngineTwoShot (one device-driven kernel per rank).
+  int engine() const { return engine_; }
 
  private:
   struct OutChan {  // this rank -> peer
@@ -193,31 +193,43 @@ class HipPlanExecutor : public Algorithm {
   std::vector<InflightSend> inflight_;
   std::vector<void*> ipcOpened_;
 
-  // One-shot replicated schedule (oneshot_kernels.hip): no channels, no
-  // scratch blocks; one uncached allocation per rank holding the landing
-  // regions [2 parities][P ranks][osRegion_ bytes] and the flags [P][G].
-  bool oneShot_ = false;
-  char* osBase_ = nullptr;
-  size_t osRegion_ = 0;
-  std::map<int, char*> osPeer_;  // peers' osBase_ (IPC-mapped)
-  glx::OneShotParams os_{};      // fixed part of the kernel's parameters
-  uint64_t osEpoch_ = 0;
-  int* osStatus_ = nullptr;      // pinned host word the kernel flags timeouts in
-  int* osStatusDev_ = nullptr;
-  hipEvent_t osDone_ = nullptr;
-  bool osLaunched_ = false;
-  int clockKhz_ = 100000;        // s_memrealtime rate
-  static bool oneShotWanted(const Context& ctx, int algo, int64_t count);
+  // Device-driven engines (xgmi_kernels.hip): the replicated schedule as the
+  // one-shot kernel, the mesh schedule as the two-shot kernel.  No channels,
+  // no scratch blocks; uncached blocks (IPC-exported, each its own handle):
+  //   one-shot: [0],[1] landing slots [P][ddSlot_] of parity 0/1; [2] flags [P][G]
+  //   two-shot: [0],[1] RS slots, [2],[3] AG slots of parity 0/1;
+  //             [4] flags: A [P][G], then B [P][G]
+  int engine_ = kEngineSteps;
+  std::vector<char*> ddBlocks_;
+  std::map<int, std::vector<char*>> ddPeer_;  // peers' blocks (IPC-mapped)
+  size_t ddSlot_ = 0;                         // bytes per landing slot
+  glx::OneShotParams os_{};                   // fixed parts of the kernels' parameters
+  glx::TwoShotParams ts_{};
+  uint64_t ddEpoch_ = 0;
+  int* ddStatus_ = nullptr;  // pinned host word the kernels flag timeouts in
+  int* ddStatusDev_ = nullptr;
+  hipEvent_t ddDone_ = nullptr;
+  bool ddLaunched_ = false;
+  int clockKhz_ = 100000;  // s_memrealtime rate
+  static int engineFor(const Context& ctx, int algo, int64_t count);
+  char* ddAlloc(size_t bytes);
+  void setupDevice();
+  void setupOneShot();
+  void setupTwoShot();
+  void runDevice(char* ptr0);
+  void checkDevice();
 
  public:
-  // Whether replicated-schedule executors on this context will run as the
-  // one-shot kernel (GLOO_AMD_ONESHOT, ranks on distinct devices/processes).
-  static bool oneShotAvailable(const Context& ctx);
-
- private:
-  void setupOneShot();
-  void runOneShot(char* ptr0);
-  void checkOneShot();
+  static constexpr int kEngineSteps = 0, kEngineOneShot = 1, kEngineTwoShot = 2;
+  // Whether device-driven engines can run on this context: GLOO_AMD_ONESHOT
+  // (0 = never, 1 = always), by default when no two ranks are threads sharing
+  // one device (their kernels might not be co-resident).  P <= 8.
+  static bool deviceEnginesAvailable(const Context& ctx);
+  // Engine of the mesh schedule when available: kEngineTwoShot (default,
+  // env GLOO_AMD_MESH_ENGINE=steps overrides) or kEngineSteps.  Read at
+  // construction.
+  static void setMeshEngine(int engine);
+  static int meshEngine();
 };
 
 }  // namespace gloo

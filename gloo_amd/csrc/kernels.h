@@ -36,7 +36,7 @@ hipError_t launch_copy(void* dst, const void* src, size_t bytes, hipStream_t s);
 void set_copy_blocks(int blocks);
 int copy_blocks();
 
-// One-shot replicated allreduce (oneshot_kernels.hip): one kernel per rank
+// One-shot replicated allreduce (xgmi_kernels.hip): one kernel per rank
 // pushes the buffer to every peer, waits on per-slice flags and folds every
 // chunk along its ring chain.  All pointers are device-accessible; push/land
 // regions and flags are uncached device memory (peers' via IPC).
@@ -59,6 +59,29 @@ struct OneShotParams {
   uint8_t chain[kOsMaxRanks][kOsMaxRanks];  // fold order: acc = op(x[chain[i]], acc)
 };
 hipError_t launch_oneshot(int op, int dtype, const OneShotParams& p, hipStream_t s);
+
+// Two-shot mesh allreduce (xgmi_kernels.hip): rank j owns range j; every
+// rank pushes its copy of range j to owner j, the owner folds it along its
+// chain and pushes the result to everyone.  Slot pointers are "virtual
+// buffers": element i of range c at ptr + i * esize.
+struct TwoShotParams {
+  char* buf;
+  char* rsPush[kOsMaxRanks];        // owner j's RS slot for this rank's copy of range j
+  const char* rsLand[kOsMaxRanks];  // this rank's RS slot holding rank k's copy of range rank
+  char* agPush[kOsMaxRanks];        // peer j's AG slot for this rank's finished range
+  const char* agLand[kOsMaxRanks];  // this rank's AG slot holding owner j's finished range
+  uint64_t* flagAOut[kOsMaxRanks];  // owner j's A-flag row for this rank ([G] words)
+  const uint64_t* flagAIn;          // [P][G]: rank k's copy of my range slice landed
+  uint64_t* flagBOut[kOsMaxRanks];  // peer j's B-flag row for this rank as owner
+  const uint64_t* flagBIn;          // [P][G]: owner j's finished slice landed
+  int* status;
+  uint64_t epoch, timeoutTicks;
+  size_t rangeOff[kOsMaxRanks], rangeLen[kOsMaxRanks];  // by owner
+  uint8_t chain[kOsMaxRanks];       // this rank's fold order
+  size_t slice;                     // elements per workgroup per range, multiple of 16 / esize
+  int P, rank, G;
+};
+hipError_t launch_twoshot(int op, int dtype, const TwoShotParams& p, hipStream_t s);
 
 // Tuning knobs of the vector kernel (lanes' unroll depth, grid cap per CU,
 // nontemporal loads/stores: 0/1, -1 = keep).

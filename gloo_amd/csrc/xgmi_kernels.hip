@@ -1,0 +1,411 @@
+// xgmi_kernels.hip -- device-driven allreduce engines: a whole schedule as
+// ONE kernel per rank, the ranks' kernels handing data to each other through
+// IPC-mapped uncached device memory over xGMI and synchronising on flag
+// words, with no host round trip between steps.  Two engines, both
+// bit-identical to the reference's ring (same chunks, same per-element
+// reduction chains, acc = op(newer rank's value, acc)):
+//
+//  one-shot (the replicated schedule, plan.h planRingChunkedReplicated /
+//  planFnRingReplicated; small buffers).  Workgroup w of rank r:
+//    1. push  slice w of r's buffer to every peer's landing slot [r];
+//             system-scope release; flagOut[peer][r][w] = epoch
+//    2. wait  one lane polls flagIn[k][w] >= epoch for every peer k
+//    3. fold  slice w of every chunk along that chunk's chain, in place.
+//
+//  two-shot (the all-links mesh, plan.h planRingChunkedMesh /
+//  planFnRingMesh; medium and large buffers).  Rank j owns range j.
+//  Workgroup w of rank r:
+//    1. push  slice w of every range j != r to owner j's RS slot [r]; flag A
+//    2. fold  slice w of range r once every peer's A flag is up, along the
+//             range's chain; the result goes to r's buffer AND to every
+//             peer's AG slot [r] in the same pass; flag B
+//    3. take  slice w of every range j != r from AG slot [j] once owner j's
+//             B flag is up.
+//
+// Waits are bounded: a peer that never arrives sets *status (1 + its rank)
+// and the workgroup exits, so every wave reaches the end.  Landing slots are
+// double-buffered by epoch parity: a rank writes epoch e into a peer's slot
+// only after its epoch e-1 kernel saw that peer's epoch e-1 flags, i.e. after
+// the peer finished epoch e-2, the last reader of that parity.
+//
+// Slots use a "virtual buffer" layout: element i of range c lives at
+// vbase + i*es with vbase = slot + (off_c*es mod 16) - off_c*es, so it has
+// the 16-byte phase it has in a 16-byte-aligned user buffer and the body of
+// every span runs on 16-byte vectors (an unaligned user buffer takes the
+// scalar path on its own side; the slot layout never depends on it).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+#include "elem_ops.h"
+#include "kernels.h"
+
+namespace glx {
+namespace {
+
+// [a, b) as scalar head [a, hs), 16-byte vectors [va, vb) (elements
+// [hs, ts)) and scalar tail [ts, b); all scalar when the buffer is not
+// 16-byte aligned or the span holds no whole vector.
+struct Span {
+  size_t a, b, hs, ts, va, vb;
+  __device__ __forceinline__ size_t nedge() const { return (hs - a) + (b - ts); }
+  __device__ __forceinline__ size_t edge(size_t t) const {
+    return t < hs - a ? a + t : ts + (t - (hs - a));
+  }
+};
+
+template <int V>
+__device__ __forceinline__ Span split_span(size_t a, size_t b, bool aligned) {
+  Span s{a, b, b, b, 0, 0};
+  if (aligned) {
+    const size_t va = (a + V - 1) / V, vb = b / V;
+    if (va < vb) {
+      s.va = va;
+      s.vb = vb;
+      s.hs = va * V;
+      s.ts = vb * V;
+    }
+  }
+  return s;
+}
+
+// Copy [a, b) of src to dst (virtual-buffer pointers with equal phases).
+template <typename S>
+__device__ __forceinline__ void copy_span(S* dst, const S* src, size_t a, size_t b,
+                                          bool aligned) {
+  const Span sp = split_span<16 / sizeof(S)>(a, b, aligned);
+  const size_t va = sp.va, vb = sp.vb;
+  for (size_t t = threadIdx.x; t < sp.nedge(); t += kBlock) {
+    const size_t i = sp.edge(t);
+    dst[i] = src[i];
+  }
+  const v4u* vs = reinterpret_cast<const v4u*>(src);
+  v4u* vd = reinterpret_cast<v4u*>(dst);
+  size_t i = va + threadIdx.x;
+  for (; i + 3 * kBlock < vb; i += 4 * kBlock) {  // 4 vectors in flight per lane
+    const v4u x0 = vs[i], x1 = vs[i + kBlock], x2 = vs[i + 2 * kBlock],
+              x3 = vs[i + 3 * kBlock];
+    vd[i] = x0;
+    vd[i + kBlock] = x1;
+    vd[i + 2 * kBlock] = x2;
+    vd[i + 3 * kBlock] = x3;
+  }
+  for (; i < vb; i += kBlock) vd[i] = vs[i];
+}
+
+// Copy [a, b) of src to every dsts[d] for d < n (one load, n stores).
+template <typename S>
+__device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* src, size_t a,
+                                             size_t b, bool aligned) {
+  const Span sp = split_span<16 / sizeof(S)>(a, b, aligned);
+  const size_t va = sp.va, vb = sp.vb;
+  for (size_t t = threadIdx.x; t < sp.nedge(); t += kBlock) {
+    const size_t i = sp.edge(t);
+    const S x = src[i];
+#pragma unroll
+    for (int d = 0; d < kOsMaxRanks - 1; d++) {
+      if (d < n) reinterpret_cast<S*>(dsts[d])[i] = x;
+    }
+  }
+  const v4u* vs = reinterpret_cast<const v4u*>(src);
+  size_t i = va + threadIdx.x;
+  for (; i + kBlock < vb; i += 2 * kBlock) {
+    const v4u x0 = vs[i], x1 = vs[i + kBlock];
+#pragma unroll
+    for (int d = 0; d < kOsMaxRanks - 1; d++) {
+      if (d < n) {
+        reinterpret_cast<v4u*>(dsts[d])[i] = x0;
+        reinterpret_cast<v4u*>(dsts[d])[i + kBlock] = x1;
+      }
+    }
+  }
+  for (; i < vb; i += kBlock) {
+    const v4u x = vs[i];
+#pragma unroll
+    for (int d = 0; d < kOsMaxRanks - 1; d++) {
+      if (d < n) reinterpret_cast<v4u*>(dsts[d])[i] = x;
+    }
+  }
+}
+
+// [a, b) of dst = chain fold of srcs[0..P-1]: acc = s0; acc = op(s_k, acc).
+// The result also goes to every outs[d], d < nout.
+template <typename T, int OP>
+__device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
+                                          const typename Elem<T, OP>::S* const* srcs, int P,
+                                          char* const* outs, int nout, size_t a, size_t b,
+                                          bool aligned) {
+  using E = Elem<T, OP>;
+  using S = typename E::S;
+  const Span sp = split_span<16 / sizeof(S)>(a, b, aligned);
+  const size_t va = sp.va, vb = sp.vb;
+  for (size_t t = threadIdx.x; t < sp.nedge(); t += kBlock) {
+    const size_t i = sp.edge(t);
+    S y[kOsMaxRanks];
+#pragma unroll
+    for (int k = 0; k < kOsMaxRanks; k++) {
+      if (k < P) y[k] = srcs[k][i];
+    }
+    S acc = y[0];
+#pragma unroll
+    for (int k = 1; k < kOsMaxRanks; k++) {
+      if (k < P) acc = E::apply(y[k], acc);
+    }
+    dst[i] = acc;
+#pragma unroll
+    for (int d = 0; d < kOsMaxRanks - 1; d++) {
+      if (d < nout) reinterpret_cast<S*>(outs[d])[i] = acc;
+    }
+  }
+  for (size_t v = va + threadIdx.x; v < vb; v += kBlock) {
+    v4u y[kOsMaxRanks];  // all P loads in flight before the chain
+#pragma unroll
+    for (int k = 0; k < kOsMaxRanks; k++) {
+      if (k < P) y[k] = reinterpret_cast<const v4u*>(srcs[k])[v];
+    }
+    v4u acc = y[0];
+#pragma unroll
+    for (int k = 1; k < kOsMaxRanks; k++) {
+      if (k < P) acc = vec_apply<T, OP>(y[k], acc);
+    }
+    reinterpret_cast<v4u*>(dst)[v] = acc;
+#pragma unroll
+    for (int d = 0; d < kOsMaxRanks - 1; d++) {
+      if (d < nout) reinterpret_cast<v4u*>(outs[d])[v] = acc;
+    }
+  }
+}
+
+// Every wave's stores complete and visible system-wide, then (by lanes
+// 0..P-1, lane r excluded, where want(lane)) flag words set to epoch.
+template <typename Want>
+__device__ __forceinline__ void release_flags(uint64_t* const* rows, int P, int rank, int w,
+                                              uint64_t epoch, Want want) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __syncthreads();
+  const int t = (int)threadIdx.x;
+  if (t < P && t != rank && want(t)) {
+    __hip_atomic_store(rows[t] + w, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// Lane 0 waits until word >= epoch (bounded); the whole workgroup learns
+// the outcome.  Returns false after a timeout (status already set).
+__device__ __forceinline__ bool wait_flag(const uint64_t* word, uint64_t epoch, int peer,
+                                          uint64_t start, uint64_t timeoutTicks, int* status,
+                                          int* s_ok) {
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+      if (__builtin_amdgcn_s_memrealtime() - start > timeoutTicks) {
+        ok = 0;
+        __hip_atomic_store(status, 1 + peer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    // drop any stale copy of the landing lines before anyone reads them
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    *s_ok = ok;
+  }
+  __syncthreads();
+  return *s_ok != 0;
+}
+
+// ---- one-shot ---------------------------------------------------------------
+
+template <typename T, int OP>
+__global__ __launch_bounds__(kBlock) void oneshot_kernel(OneShotParams p) {
+  using S = typename Elem<T, OP>::S;
+  __shared__ int s_ok;
+  const int w = blockIdx.x;
+  const size_t e0 = (size_t)w * p.slice;
+  const size_t e1 = e0 + p.slice < p.count ? e0 + p.slice : p.count;
+  S* buf = reinterpret_cast<S*>(p.buf);
+  const bool aligned = ((uintptr_t)p.buf % 16) == 0;
+
+  // 1. push (peers in ring order from rank+1)
+  char* to[kOsMaxRanks - 1];
+#pragma unroll
+  for (int d = 1; d < kOsMaxRanks; d++) {
+    int j = p.rank + d;
+    if (j >= p.P) j -= p.P;
+    to[d - 1] = d < p.P ? p.push[j] : nullptr;
+  }
+  scatter_span<S>(to, p.P - 1, buf, e0, e1, aligned);
+  release_flags(p.flagOut, p.P, p.rank, w, p.epoch, [](int) { return true; });
+
+  // 2. wait
+  const uint64_t start = __builtin_amdgcn_s_memrealtime();
+  for (int k = 0; k < p.P; k++) {
+    if (k == p.rank) continue;
+    if (!wait_flag(p.flagIn + (size_t)k * p.G + w, p.epoch, k, start, p.timeoutTicks,
+                   p.status, &s_ok)) {
+      return;
+    }
+  }
+
+  // 3. fold every chunk's part of this slice along its chain
+  for (int q = 0; q < p.njobs; q++) {
+    const size_t jb = p.jobOff[q], je = p.jobOff[q] + p.jobLen[q];
+    const size_t a = jb > e0 ? jb : e0, b = je < e1 ? je : e1;
+    if (a >= b) continue;
+    const S* src[kOsMaxRanks];
+#pragma unroll
+    for (int i = 0; i < kOsMaxRanks; i++) {
+      const int r = p.chain[q][i];
+      src[i] = i < p.P ? (r == p.rank ? buf : reinterpret_cast<const S*>(p.land[r])) : nullptr;
+    }
+    fold_span<T, OP>(buf, src, p.P, nullptr, 0, a, b, aligned);
+  }
+}
+
+// ---- two-shot ---------------------------------------------------------------
+
+template <typename T, int OP>
+__global__ __launch_bounds__(kBlock) void twoshot_kernel(TwoShotParams p) {
+  using S = typename Elem<T, OP>::S;
+  __shared__ int s_ok;
+  const int w = blockIdx.x;
+  S* buf = reinterpret_cast<S*>(p.buf);
+  const bool aligned = ((uintptr_t)p.buf % 16) == 0;
+  auto span = [&](int c, size_t& a, size_t& b) {  // slice w of range c
+    const size_t off = p.rangeOff[c], len = p.rangeLen[c];
+    const size_t s0 = (size_t)w * p.slice;
+    a = off + (s0 < len ? s0 : len);
+    b = off + (s0 + p.slice < len ? s0 + p.slice : len);
+    return a < b;
+  };
+
+  // 1. push my copy of every other range's slice to its owner
+  for (int d = 1; d < p.P; d++) {
+    int j = p.rank + d;
+    if (j >= p.P) j -= p.P;
+    size_t a, b;
+    if (span(j, a, b)) copy_span<S>(reinterpret_cast<S*>(p.rsPush[j]), buf, a, b, aligned);
+  }
+  release_flags(p.flagAOut, p.P, p.rank, w, p.epoch, [&](int j) {
+    size_t a, b;
+    return span(j, a, b);
+  });
+
+  // 2. fold my range's slice from every peer's copy; result to my buffer
+  //    and to every peer's AG slot in the same pass
+  const uint64_t start = __builtin_amdgcn_s_memrealtime();
+  size_t a, b;
+  if (span(p.rank, a, b)) {
+    for (int k = 0; k < p.P; k++) {
+      if (k == p.rank) continue;
+      if (!wait_flag(p.flagAIn + (size_t)k * p.G + w, p.epoch, k, start, p.timeoutTicks,
+                     p.status, &s_ok)) {
+        return;
+      }
+    }
+    const S* src[kOsMaxRanks];
+#pragma unroll
+    for (int i = 0; i < kOsMaxRanks; i++) {
+      const int r = p.chain[i];
+      src[i] = i < p.P ? (r == p.rank ? buf : reinterpret_cast<const S*>(p.rsLand[r])) : nullptr;
+    }
+    char* outs[kOsMaxRanks - 1];
+#pragma unroll
+    for (int d = 1; d < kOsMaxRanks; d++) {
+      int j = p.rank + d;
+      if (j >= p.P) j -= p.P;
+      outs[d - 1] = d < p.P ? p.agPush[j] : nullptr;
+    }
+    fold_span<T, OP>(buf, src, p.P, outs, p.P - 1, a, b, aligned);
+    release_flags(p.flagBOut, p.P, p.rank, w, p.epoch, [](int) { return true; });
+  }
+
+  // 3. take every other owner's finished slice
+  for (int d = 1; d < p.P; d++) {
+    int j = p.rank - d;
+    if (j < 0) j += p.P;
+    if (!span(j, a, b)) continue;
+    if (!wait_flag(p.flagBIn + (size_t)j * p.G + w, p.epoch, j, start, p.timeoutTicks,
+                   p.status, &s_ok)) {
+      return;
+    }
+    copy_span<S>(buf, reinterpret_cast<const S*>(p.agLand[j]), a, b, aligned);
+  }
+}
+
+// ---- launch -------------------------------------------------------------------
+
+template <typename T>
+hipError_t launch_os_op(int op, const OneShotParams& p, hipStream_t s) {
+  const dim3 grid((unsigned)p.G), block(kBlock);
+  switch (op) {
+    case GLX_SUM: hipLaunchKernelGGL((oneshot_kernel<T, GLX_SUM>), grid, block, 0, s, p); break;
+    case GLX_PRODUCT:
+      hipLaunchKernelGGL((oneshot_kernel<T, GLX_PRODUCT>), grid, block, 0, s, p);
+      break;
+    case GLX_MAX: hipLaunchKernelGGL((oneshot_kernel<T, GLX_MAX>), grid, block, 0, s, p); break;
+    case GLX_MIN: hipLaunchKernelGGL((oneshot_kernel<T, GLX_MIN>), grid, block, 0, s, p); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_ts_op(int op, const TwoShotParams& p, hipStream_t s) {
+  const dim3 grid((unsigned)p.G), block(kBlock);
+  switch (op) {
+    case GLX_SUM: hipLaunchKernelGGL((twoshot_kernel<T, GLX_SUM>), grid, block, 0, s, p); break;
+    case GLX_PRODUCT:
+      hipLaunchKernelGGL((twoshot_kernel<T, GLX_PRODUCT>), grid, block, 0, s, p);
+      break;
+    case GLX_MAX: hipLaunchKernelGGL((twoshot_kernel<T, GLX_MAX>), grid, block, 0, s, p); break;
+    case GLX_MIN: hipLaunchKernelGGL((twoshot_kernel<T, GLX_MIN>), grid, block, 0, s, p); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_oneshot(int op, int dtype, const OneShotParams& p, hipStream_t s) {
+  if (p.P < 2 || p.P > kOsMaxRanks || p.G < 1 || p.G > kOsMaxSlices || p.njobs < 0 ||
+      p.njobs > kOsMaxRanks || p.count == 0 || p.slice == 0 ||
+      (size_t)p.G * p.slice < p.count || (size_t)(p.G - 1) * p.slice >= p.count) {
+    return hipErrorInvalidValue;  // the grid must cover the buffer exactly
+  }
+  switch (dtype) {
+    case GLX_INT8: return launch_os_op<int8_t>(op, p, s);
+    case GLX_UINT8: return launch_os_op<uint8_t>(op, p, s);
+    case GLX_INT32: return launch_os_op<int32_t>(op, p, s);
+    case GLX_INT64: return launch_os_op<int64_t>(op, p, s);
+    case GLX_UINT64: return launch_os_op<uint64_t>(op, p, s);
+    case GLX_FLOAT32: return launch_os_op<float>(op, p, s);
+    case GLX_FLOAT64: return launch_os_op<double>(op, p, s);
+    case GLX_FLOAT16: return launch_os_op<f16_t>(op, p, s);
+    case GLX_BFLOAT16: return launch_os_op<bf16_t>(op, p, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_twoshot(int op, int dtype, const TwoShotParams& p, hipStream_t s) {
+  size_t maxLen = 0;
+  for (int c = 0; c < p.P && c < kOsMaxRanks; c++) {
+    maxLen = p.rangeLen[c] > maxLen ? p.rangeLen[c] : maxLen;
+  }
+  if (p.P < 2 || p.P > kOsMaxRanks || p.G < 1 || p.G > kOsMaxSlices || p.slice == 0 ||
+      (size_t)p.G * p.slice < maxLen) {
+    return hipErrorInvalidValue;  // the slices must cover every range
+  }
+  switch (dtype) {
+    case GLX_INT8: return launch_ts_op<int8_t>(op, p, s);
+    case GLX_UINT8: return launch_ts_op<uint8_t>(op, p, s);
+    case GLX_INT32: return launch_ts_op<int32_t>(op, p, s);
+    case GLX_INT64: return launch_ts_op<int64_t>(op, p, s);
+    case GLX_UINT64: return launch_ts_op<uint64_t>(op, p, s);
+    case GLX_FLOAT32: return launch_ts_op<float>(op, p, s);
+    case GLX_FLOAT64: return launch_ts_op<double>(op, p, s);
+    case GLX_FLOAT16: return launch_ts_op<f16_t>(op, p, s);
+    case GLX_BFLOAT16: return launch_ts_op<bf16_t>(op, p, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace glx

@@ -113,6 +113,12 @@ int glx_set_copy_split(int k);
  * into the peer's memory over xGMI, with `blocks` workgroups (<= 0: keep).
  * Env GLOO_AMD_COPY_ENGINE=kernel selects 1 at load time. */
 int glx_set_copy_engine(int engine, int blocks);
+/* Engine of the mesh schedule (ring_chunked's result over all links) for
+ * algorithms created afterwards, when device-driven engines are available
+ * (ranks on distinct devices or processes, P <= 8): GLX_ENGINE_TWOSHOT (one
+ * device-driven kernel per rank, default) or GLX_ENGINE_STEPS (host-issued
+ * copies and fold kernels).  Env GLOO_AMD_MESH_ENGINE=steps at load time. */
+int glx_set_mesh_engine(int engine);
 
 /* Number of visible HIP devices (0 when no GPU). */
 int glx_device_count(int* count);
@@ -266,9 +272,12 @@ int64_t glx_algorithm_bytes_sent(glx_algorithm* alg);
 /* How run() executes: GLX_ENGINE_STEPS = the schedule's steps issued by the
  * host (copies, reduce kernels, control-block counters); GLX_ENGINE_ONESHOT =
  * the replicated schedule as one device-driven kernel per rank (small
- * buffers, ranks on distinct devices or processes).  Results are identical. */
+ * buffers); GLX_ENGINE_TWOSHOT = the mesh schedule as one device-driven
+ * kernel per rank.  Device-driven engines need the ranks on distinct devices
+ * or processes.  Results are identical. */
 #define GLX_ENGINE_STEPS 0
 #define GLX_ENGINE_ONESHOT 1
+#define GLX_ENGINE_TWOSHOT 2
 int glx_algorithm_engine(glx_algorithm* alg);
 void glx_algorithm_destroy(glx_algorithm* alg);
 

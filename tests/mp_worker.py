@@ -5,9 +5,9 @@
 algo: ring_chunked | halving_doubling | ring_chunked_mesh (class algorithms)
       fn_ring | fn_bcube | fn_ring_mesh (gloo_amd.allreduce, two calls with
       different buffers, the second out of place)
-      oneshot (the replicated schedule as one device-driven kernel per rank:
-      class and function style, dtypes x ops x sizes, device and host
-      buffers, repeated runs; prints per-op latencies)
+      oneshot | twoshot (the replicated / mesh schedule as one device-driven
+      kernel per rank: class and function style, dtypes x ops x sizes,
+      device and host buffers, repeated runs; prints per-op latencies)
 
 Checks its result against the oracle and prints OK."""
 import os
@@ -28,8 +28,8 @@ def main():
     from oracle import oracle as O
 
     N = 100003
-    if algo == "oneshot":
-        return run_oneshot(store_dir, rank, size)
+    if algo in ("oneshot", "twoshot"):
+        return run_device(store_dir, rank, size, algo)
     if algo.startswith("fn_"):
         return run_fn(store_dir, rank, size, algo, N)
     code = O.HALVING_DOUBLING if algo == "halving_doubling" else O.RING_CHUNKED
@@ -107,7 +107,7 @@ def run_fn(store_dir, rank, size, algo, N):
     print("OK")
 
 
-def run_oneshot(store_dir, rank, size):
+def run_device(store_dir, rank, size, mode):
     import time
 
     import numpy as np
@@ -129,8 +129,12 @@ def run_oneshot(store_dir, rank, size):
 
     from test_reduce_gpu import from_dev, to_dev
 
+    sched = "replicated" if mode == "oneshot" else "mesh"
     cases = []
-    for n in (1, 3, 255, 256, 1024, 4099, 65539, 262144, 1 << 20):
+    sizes = [1, 3, 255, 256, 1024, 4099, 65539, 262144, 1 << 20]
+    if mode == "twoshot":
+        sizes += [(1 << 22) + 5, 3 << 22]
+    for n in sizes:
         cases.append((n, O.FLOAT32, O.SUM))
     for dt in (O.FLOAT16, O.INT32, O.FLOAT64, O.INT8, O.UINT64):
         for op in (O.SUM, O.PRODUCT, O.MAX, O.MIN):
@@ -141,8 +145,8 @@ def run_oneshot(store_dir, rank, size):
         exp = O.allreduce(O.RING_CHUNKED, op, dt, ins)[rank][0]
         buf = to_dev(ins[rank][0], dt)
         alg = gloo_amd.AllreduceRingChunked(ctx, [buf], fn=gloo_amd.ReductionFunction(op),
-                                           schedule="replicated", dtype=dt)
-        if alg.engine() != "oneshot":
+                                           schedule=sched, dtype=dt)
+        if alg.engine() != mode:
             bad.append(("engine", n, dt, op, alg.engine()))
         for it in range(3):
             buf.copy_(to_dev(ins[rank][0], dt))
@@ -157,40 +161,51 @@ def run_oneshot(store_dir, rank, size):
     ins = case_inputs(size, n, O.FLOAT32, 1, 0, seed=7)
     exp = O.allreduce(O.RING_CHUNKED, O.SUM, O.FLOAT32, ins)[rank][0]
     host = ins[rank][0].copy()
-    alg = gloo_amd.AllreduceRingChunked(ctx, [host], schedule="replicated")
+    alg = gloo_amd.AllreduceRingChunked(ctx, [host], schedule=sched)
     for it in range(2):
         host[:] = ins[rank][0]
         alg.run()
         if not same(host, exp):
             bad.append(("host", n, it))
     alg.close()
-    # function style: UNSPECIFIED at a small size -> RING's replicated schedule
-    for n in (1000, 65536):
+    # function style: RING's result, one round (UNSPECIFIED at a small size)
+    # or over all links (RING_MESH)
+    fn_algo = (gloo_amd.AllreduceOptions.Algorithm.UNSPECIFIED if mode == "oneshot"
+               else gloo_amd.AllreduceOptions.Algorithm.RING_MESH)
+    for n in (1000, 65536, 1 << 20):
         data = case_inputs(size, n, O.FLOAT32, 1, 0, seed=11)
         exp = O.allreduce_fn(O.FN_RING, O.SUM, O.FLOAT32, [[] for _ in range(size)],
                              data)[rank][0]
         for it in range(2):
             out = torch.from_numpy(data[rank][0].copy()).cuda()
             opts = gloo_amd.AllreduceOptions(ctx)
-            opts.setAlgorithm(gloo_amd.AllreduceOptions.Algorithm.UNSPECIFIED)
+            opts.setAlgorithm(fn_algo)
             opts.setOutput(out)
             opts.setReduceFunction(gloo_amd.ReductionFunction.sum)
             gloo_amd.allreduce(opts)
             if not same(out.cpu().numpy(), exp):
                 bad.append(("fn", n, it))
-    # latency: one-shot vs the host-mediated replicated steps (same bits)
-    for n in (1024, 65536, 262144):
-        buf = torch.zeros(n, device="cuda")
-        alg = gloo_amd.AllreduceRingChunked(ctx, [buf], schedule="replicated")
-        for _ in range(5):
-            alg.run()
-        iters = 50
-        t0 = time.perf_counter()
-        for _ in range(iters):
-            alg.run()
-        us = (time.perf_counter() - t0) / iters * 1e6
-        print("LAT rank %d P %d elems %d engine %s us %.1f" % (rank, size, n, alg.engine(), us))
-        alg.close()
+    # latency of the device-driven engine vs the host-issued steps (same bits)
+    lat_sizes = (1024, 65536, 262144) if mode == "oneshot" else (65536, 1 << 20, 1 << 24)
+    for n in lat_sizes:
+        for eng in ("device", "steps"):
+            if mode == "twoshot":
+                gloo_amd.set_mesh_engine(eng)
+            elif eng == "steps":
+                continue
+            buf = torch.zeros(n, device="cuda")
+            alg = gloo_amd.AllreduceRingChunked(ctx, [buf], schedule=sched)
+            for _ in range(5):
+                alg.run()
+            iters = 50 if n <= (1 << 20) else 10
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                alg.run()
+            us = (time.perf_counter() - t0) / iters * 1e6
+            print("LAT rank %d P %d elems %d engine %s us %.1f" % (rank, size, n, alg.engine(),
+                                                                    us))
+            alg.close()
+    gloo_amd.set_mesh_engine("device")
     store.set("done/%d" % rank, b"1")
     for r in range(size):
         store.get("done/%d" % r, timeout_ms=60000)

@@ -257,16 +257,18 @@ def test_multiprocess_ipc(algo):
             assert "OK" in outs[r]
 
 
+@pytest.mark.parametrize("mode", ["oneshot", "twoshot"])
 @pytest.mark.parametrize("P", [2, 4])
-def test_oneshot_multiprocess(P):
-    """The replicated schedule as one device-driven kernel per rank
-    (oneshot_kernels.hip), one process per rank: peers' kernels push into
-    each other's IPC-mapped uncached regions and wait on flags.  Bit-exact
-    with the reference ring's chains for every dtype/op, device and host
-    buffers, class and function style, repeated runs (mp_worker.py)."""
+def test_device_engine_multiprocess(P, mode):
+    """The replicated (one-shot) and mesh (two-shot) schedules as one
+    device-driven kernel per rank (xgmi_kernels.hip), one process per rank:
+    peers' kernels push into each other's IPC-mapped uncached regions and
+    wait on flags.  Bit-exact with the reference ring's chains for every
+    dtype/op, device and host buffers, class and function style, repeated
+    runs, ranges left empty at small sizes (mp_worker.py)."""
     with tempfile.TemporaryDirectory() as d:
         env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-        procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), "oneshot"],
+        procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), mode],
                                   env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
                  for r in range(P)]
         outs = []
