@@ -259,12 +259,29 @@ def reduce_kernel_roofline(torch, gloo_amd, dev, chunk_bytes, reps=50):
 
 
 RING_SCHEDULES = {"ring_chunked": "ring", "ring_chunked_mesh": "mesh",
-                  "ring_chunked_repl": "replicated", "ring_chunked_auto": "auto"}
+                  "ring_chunked_mesh_steps": "mesh", "ring_chunked_repl": "replicated",
+                  "ring_chunked_auto": "auto"}
+ENGINES = {}  # bench name -> engine the product chose ("steps", "oneshot", "twoshot")
+
+
+def plan_name(algo):
+    """Schedule name of a bench candidate for gloo_amd.plan()."""
+    return {"ring_chunked_mesh_steps": "ring_chunked_mesh",
+            "ring_chunked_repl": "ring_chunked_repl"}.get(algo, algo)
 
 
 def make_alg(gloo_amd, ctx, buf, algo):
+    """ring_chunked_mesh runs on the two-shot device engine when the ranks are
+    on distinct devices/processes; ring_chunked_mesh_steps is the same
+    schedule with host-issued steps (calibrated peer-copy transport)."""
     if algo == "halving_doubling":
         return gloo_amd.AllreduceHalvingDoubling(ctx, [buf])
+    if algo == "ring_chunked_mesh_steps":
+        gloo_amd.set_mesh_engine("steps")
+        try:
+            return gloo_amd.AllreduceRingChunked(ctx, [buf], schedule="mesh")
+        finally:
+            gloo_amd.set_mesh_engine("device")
     return gloo_amd.AllreduceRingChunked(ctx, [buf], schedule=RING_SCHEDULES[algo])
 
 
@@ -272,7 +289,7 @@ def busiest_link_bytes(gloo_amd, algo, rank, world, count, es):
     """Bytes this rank sends to its most-loaded destination per run (from the
     compiled step program): the per-link load that bounds the step on a
     point-to-point xGMI fabric."""
-    steps, _ = gloo_amd.plan(algo, rank, world, count)
+    steps, _ = gloo_amd.plan(plan_name(algo), rank, world, count)
     per_peer = {}
     for st in steps:
         if st[0] == 0:
@@ -284,7 +301,8 @@ def time_schedule(torch, dist, gloo_amd, ctx, buf, algo, steps, warmup):
     """warmup untimed runs, then `steps` timed runs between barriers +
     device syncs; returns (max-over-ranks seconds per step, link bytes/run)."""
     alg = make_alg(gloo_amd, ctx, buf, algo)
-    log("%s: created, warmup %d" % (algo, warmup))
+    ENGINES[algo] = alg.engine()
+    log("%s: created (engine %s), warmup %d" % (algo, ENGINES[algo], warmup))
     for _ in range(warmup):
         alg.run()
     log("%s: warm, timing %d steps" % (algo, steps))
@@ -341,6 +359,51 @@ def host_endpoint_rate(torch, dist, gloo_amd, ctx, src, dev_result, algo, reps):
 SWEEP_ELEMS = [1 << 10, 1 << 12, 1 << 14, 1 << 16, 1 << 18, 1 << 20, 1 << 22, 1 << 24]
 
 
+def probe_device_engines(torch, dist, gloo_amd, ctx, dev, dtype):
+    """Before timing them, check the device-driven engines (one-shot and
+    two-shot kernels) on this machine: short timeout, results bit-identical to
+    the host-issued steps engine over three refilled runs.  If any rank fails,
+    every rank turns them off for the rest of the run (the host-issued
+    schedules remain) and the JSON says why."""
+    ok, note = 1, "ok"
+    ctx.setTimeout(15)
+    try:
+        for algo, n in (("ring_chunked_repl", 65536 + 3), ("ring_chunked_mesh", (1 << 20) + 5)):
+            x = synthetic(torch, n, dtype, dev, 99 + int(os.environ.get("RANK", "0")))
+            ref = x.clone()
+            torch.cuda.synchronize()  # run() does not order itself after torch's stream
+            gloo_amd.set_device_engines("off")
+            try:
+                a = make_alg(gloo_amd, ctx, ref, algo)
+            finally:
+                gloo_amd.set_device_engines("auto")
+            a.run()
+            a.close()
+            y = x.clone()
+            a = make_alg(gloo_amd, ctx, y, algo)
+            eng = a.engine()
+            for _ in range(3):
+                y.copy_(x)
+                torch.cuda.synchronize()
+                a.run()
+                torch.cuda.synchronize()
+                if not torch.equal(y.view(torch.uint8), ref.view(torch.uint8)):
+                    ok, note = 0, "%s (%s) differs from the steps engine" % (algo, eng)
+            a.close()
+    except Exception as e:  # timeout (IoException) or HIP error on this rank
+        ok, note = 0, "%s: %s" % (type(e).__name__, str(e)[:200])
+    ctx.setTimeout(120)
+    flag = torch.tensor([ok], dtype=torch.int64)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    enabled = bool(flag.item())
+    if not enabled:
+        gloo_amd.set_device_engines("off")
+        if note == "ok":
+            note = "failed on another rank"
+    log("device engines: %s (%s)" % ("enabled" if enabled else "DISABLED", note))
+    return {"enabled": enabled, "probe": note}
+
+
 def element_sweep(torch, dist, gloo_amd, ctx, dev, schedules, dtype):
     """configs[2]'s element sweep (1K..16M elements per rank): per size and
     schedule, us per allreduce (max over ranks) and algbw.  Iterations shrink
@@ -393,6 +456,7 @@ def bench_multi(args):
     ctx.setTimeout(120)
     ctx.connectFullMesh(store)
     log("connected (world %d, device %d)" % (world, local))
+    device_engines = probe_device_engines(torch, dist, gloo_amd, ctx, dev, args.dtype)
     # Transport calibration: peer copies by the DMA engines split over 1/2/4
     # streams, or by the xGMI copy kernel (32/128 workgroups); a few runs
     # each, max over ranks (every rank sees the same times and picks alike).
@@ -409,14 +473,17 @@ def bench_multi(args):
 
     def tuned(algo):
         calib = {}
-        if args.copy_split == "auto":
+        probe = make_alg(gloo_amd, ctx, buf, algo)
+        device_engine = probe.engine() != "steps"  # no peer-copy transport to tune
+        probe.close()
+        if args.copy_split == "auto" and not device_engine:
             for tr in TRANSPORTS:
                 set_transport(tr)
                 buf.copy_(src)
                 calib[tr], _ = time_schedule(torch, dist, gloo_amd, ctx, buf, algo, 3, 1)
             best = min(calib, key=lambda k: calib[k])
         else:
-            best = ("dma", int(args.copy_split), 0)
+            best = ("dma", 1 if args.copy_split == "auto" else int(args.copy_split), 0)
         set_transport(best)
         buf.copy_(src)
         torch.cuda.synchronize()
@@ -430,7 +497,9 @@ def bench_multi(args):
         torch.cuda.synchronize()
         alg.close()
         result = buf.clone()
-        return {"t": t, "sent": sent, "transport": tname(best), "tr": best,
+        return {"t": t, "sent": sent,
+                "transport": ("device-driven kernel stores (%s)" % ENGINES[algo]
+                              if device_engine else tname(best)), "tr": best,
                 "calib_ms": {tname(k): round(v * 1e3, 3) for k, v in calib.items()},
                 "result": result}
 
@@ -438,9 +507,9 @@ def bench_multi(args):
         return int(t.view(torch.int16 if es == 2 else torch.int32).to(torch.int64).sum().item())
 
     if args.algo == "ring_chunked" and args.schedule == "auto":
-        candidates = ["ring_chunked", "ring_chunked_mesh"]
+        candidates = ["ring_chunked", "ring_chunked_mesh", "ring_chunked_mesh_steps"]
     elif args.algo == "ring_chunked" and args.schedule == "mesh":
-        candidates = ["ring_chunked_mesh"]
+        candidates = ["ring_chunked_mesh", "ring_chunked_mesh_steps"]
     else:
         candidates = [args.algo]
     runs = {a: tuned(a) for a in candidates}
@@ -466,6 +535,7 @@ def bench_multi(args):
                    "ms_per_step": round(runs[a]["t"] * 1e3, 4),
                    "algbw_GBps": round(S / runs[a]["t"] / 1e9, 3),
                    "bytes_sent_per_step": runs[a]["sent"], "transport": runs[a]["transport"],
+                   "engine": ENGINES.get(a),
                    "busiest_link_GBps": round(lm / runs[a]["t"] / 1e9, 2)}
     if not args.no_alt:
         for other in ("ring_chunked", "ring_chunked_mesh", "halving_doubling"):
@@ -506,7 +576,9 @@ def bench_multi(args):
                            args.algo, {"f32": "fp32"}.get(args.dtype, args.dtype), args.size_mib),
                        "algorithm": args.algo,
                        "schedule": {"ring_chunked": "ring", "ring_chunked_mesh": "mesh",
+                                    "ring_chunked_mesh_steps": "mesh",
                                     "halving_doubling": "halving_doubling"}[chosen],
+                       "engine": ENGINES.get(chosen),
                        "schedule_note": "ring_chunked's chunking and reduction order; ring = "
                                         "the reference's data movement, mesh = all links "
                                         "(bit-identical, checked)",
@@ -527,6 +599,7 @@ def bench_multi(args):
                                       "(ring: everything on rank->rank+1; mesh: 1/(P-1) "
                                       "per peer link)"},
             "alt_schedules": alts,
+            "device_engines": device_engines,
             "sweep": sweep,
             "verified": verified,
         }

@@ -50,6 +50,14 @@ def set_mesh_engine(engine):
     errors.check(_lib.lib.glx_set_mesh_engine(code), "set_mesh_engine")
 
 
+def set_device_engines(mode):
+    """Device-driven engines (one-shot / two-shot kernels) for algorithms
+    created afterwards: "auto" (default: when no two ranks are threads sharing
+    a device), "off" (host-issued steps only) or "on"."""
+    code = {"auto": -1, "off": 0, "on": 1}[mode]
+    errors.check(_lib.lib.glx_set_device_engines(code), "set_device_engines")
+
+
 def device_count():
     import ctypes
     n = ctypes.c_int(0)

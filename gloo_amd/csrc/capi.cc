@@ -181,6 +181,12 @@ int glx_set_mesh_engine(int engine) {
   return GLX_OK;
 }
 
+int glx_set_device_engines(int mode) {
+  if (mode < -1 || mode > 1) return fail(GLX_ERR_INVALID, "device engine mode must be -1, 0 or 1");
+  gloo::HipPlanExecutor::setDeviceEngines(mode);
+  return GLX_OK;
+}
+
 int glx_set_copy_split(int k) {
   if (k < 1 || k > 8) return fail(GLX_ERR_INVALID, "glx_set_copy_split: k must be in [1, 8]");
   gloo::HipPlanExecutor::setCopySplit(k);

@@ -1005,11 +1005,27 @@ void HipPlanExecutor::setMeshEngine(int engine) {
 
 int HipPlanExecutor::meshEngine() { return g_mesh_engine.load(); }
 
+namespace {
+
+int initialDeviceEngines() {
+  const char* e = std::getenv("GLOO_AMD_ONESHOT");
+  if (e != nullptr && e[0] == '0') return 0;
+  if (e != nullptr && e[0] == '1') return 1;
+  return -1;
+}
+
+std::atomic<int> g_device_engines{initialDeviceEngines()};
+
+}  // namespace
+
+void HipPlanExecutor::setDeviceEngines(int mode) {
+  g_device_engines.store(mode < 0 ? -1 : (mode > 0 ? 1 : 0));
+}
+
 bool HipPlanExecutor::deviceEnginesAvailable(const Context& ctx) {
   if (ctx.size < 2 || ctx.size > glx::kOsMaxRanks) return false;
-  const char* e = std::getenv("GLOO_AMD_ONESHOT");
-  if (e != nullptr && e[0] == '0') return false;
-  if (e != nullptr && e[0] == '1') return true;
+  const int mode = g_device_engines.load();
+  if (mode >= 0) return mode == 1;
   return !ctx.ranksShareDevice();
 }
 
@@ -1026,10 +1042,17 @@ int HipPlanExecutor::engineFor(const Context& ctx, int algo, int64_t count) {
   return kEngineSteps;
 }
 
-// Uncached: peers' stores land in our HBM behind our caches' back.
+// Peers' stores land in our HBM behind our caches' back: uncached memory
+// (default), or fine-grained memory (GLOO_AMD_DD_MEM=finegrained: cached
+// non-coherently, the kernels' system-scope acquire drops stale lines).
 char* HipPlanExecutor::ddAlloc(size_t bytes) {
+  static const unsigned flags = [] {
+    const char* e = std::getenv("GLOO_AMD_DD_MEM");
+    return (e != nullptr && std::strcmp(e, "finegrained") == 0) ? hipDeviceMallocFinegrained
+                                                                 : hipDeviceMallocUncached;
+  }();
   char* d = nullptr;
-  GLX_HIP_CHECK(hipExtMallocWithFlags((void**)&d, bytes, hipDeviceMallocUncached));
+  GLX_HIP_CHECK(hipExtMallocWithFlags((void**)&d, bytes, flags));
   ddBlocks_.push_back(d);
   GLX_HIP_CHECK(hipMemset(d, 0, bytes));
   return d;

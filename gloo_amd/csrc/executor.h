@@ -225,6 +225,9 @@ class HipPlanExecutor : public Algorithm {
   // (0 = never, 1 = always), by default when no two ranks are threads sharing
   // one device (their kernels might not be co-resident).  P <= 8.
   static bool deviceEnginesAvailable(const Context& ctx);
+  // Override for algorithms created afterwards: 0 = never, 1 = always
+  // (caller guarantees co-residency), -1 = automatic (the default).
+  static void setDeviceEngines(int mode);
   // Engine of the mesh schedule when available: kEngineTwoShot (default,
   // env GLOO_AMD_MESH_ENGINE=steps overrides) or kEngineSteps.  Read at
   // construction.

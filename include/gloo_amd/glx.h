@@ -119,6 +119,11 @@ int glx_set_copy_engine(int engine, int blocks);
  * device-driven kernel per rank, default) or GLX_ENGINE_STEPS (host-issued
  * copies and fold kernels).  Env GLOO_AMD_MESH_ENGINE=steps at load time. */
 int glx_set_mesh_engine(int engine);
+/* Device-driven engines for algorithms created afterwards: 0 = never (every
+ * schedule runs as host-issued steps), 1 = always (the caller guarantees the
+ * ranks' kernels can run concurrently), -1 = automatic (default: when no two
+ * ranks are threads sharing one device).  Env GLOO_AMD_ONESHOT=0/1. */
+int glx_set_device_engines(int mode);
 
 /* Number of visible HIP devices (0 when no GPU). */
 int glx_device_count(int* count);
