@@ -218,6 +218,8 @@ class DeviceAllreduce : public Algorithm {
   ~DeviceAllreduce() override { glx_algorithm_destroy(a_); }
   void run() override { check(glx_algorithm_run(a_), "run"); }
   int64_t bytesSentPerRun() const { return glx_algorithm_bytes_sent(a_); }
+  // GLX_ENGINE_STEPS / GLX_ENGINE_ONESHOT / GLX_ENGINE_TWOSHOT (glx.h)
+  int engine() const { return glx_algorithm_engine(a_); }
 
  private:
   std::shared_ptr<Context> ctx_;
@@ -229,8 +231,17 @@ class DeviceAllreduce : public Algorithm {
 // RING = the reference's ring (one link per direction); MESH = each rank
 // folds its chunk pair from every peer directly (all links at once);
 // REPLICATED = one round, every rank folds everything (small buffers);
-// AUTO = REPLICATED up to 256 KiB per rank, MESH above.
+// AUTO = REPLICATED up to a threshold per rank (2 MiB with the device-driven
+// engines, 256 KiB without), MESH above.  With the ranks on distinct devices
+// or processes REPLICATED and MESH run as one device-driven kernel per rank
+// (one-shot / two-shot; see setMeshEngine / setDeviceEngines).
 enum class Schedule { RING, MESH, REPLICATED, AUTO };
+
+// Engine knobs for algorithms created afterwards (process-wide; every rank
+// must set them alike).  mode: -1 automatic, 0 never, 1 always.
+inline void setDeviceEngines(int mode) { check(glx_set_device_engines(mode), "setDeviceEngines"); }
+// GLX_ENGINE_TWOSHOT (default) or GLX_ENGINE_STEPS for the MESH schedule.
+inline void setMeshEngine(int engine) { check(glx_set_mesh_engine(engine), "setMeshEngine"); }
 
 namespace detail {
 inline glx_algorithm* createRing(glx_context* c, void* const* p, int n, int count, int dt,
