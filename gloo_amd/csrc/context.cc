@@ -1,6 +1,8 @@
 // context.cc -- see context.h.
 #include "context.h"
 
+#include <algorithm>
+
 #include <errno.h>
 #include <fcntl.h>
 #include <signal.h>
@@ -185,6 +187,7 @@ void Context::connectFullMesh(std::shared_ptr<rendezvous::Store> store) {
       p.device = device_;
       p.localDevice = device_;
       p.sameProcess = true;
+      p.busId = busId_;
       p.shmName = shm;
       continue;
     }
@@ -196,6 +199,7 @@ void Context::connectFullMesh(std::shared_ptr<rendezvous::Store> store) {
     p.pid = (pid_t)rd.pod<int64_t>();
     p.device = rd.pod<int32_t>();
     std::string bus = rd.str();
+    p.busId = bus;
     p.shmName = rd.str();
     p.sameProcess = (p.pid == pid);
     if (p.sameProcess) {
@@ -241,6 +245,18 @@ bool Context::ranksShareDevice() const {
     }
   }
   return false;
+}
+
+int Context::maxRanksPerDevice() const {
+  std::map<std::string, int> n;
+  int most = 1;
+  for (const auto& p : peers_) {
+    const std::string key = !p.busId.empty()
+                                ? p.busId
+                                : std::to_string(p.pid) + ":" + std::to_string(p.device);
+    most = std::max(most, ++n[key]);
+  }
+  return most;
 }
 
 void Context::checkPeersAlive() {

@@ -74,6 +74,7 @@ struct PeerEndpoint {
   int device = -1;       // device ordinal in the peer's process
   int localDevice = -1;  // the same GPU's ordinal in this process (-1: unknown)
   bool sameProcess = false;
+  std::string busId;  // PCI bus id of the rank's GPU ("" if unknown)
   std::string shmName;
   std::unique_ptr<ControlBlock> ctl;  // mapped peer control block
 };
@@ -106,6 +107,8 @@ class Context {
   // endpoints).  Their streams may share a hardware queue, so kernels that
   // wait for each other on the device could not both run.
   bool ranksShareDevice() const;
+  // Largest number of ranks on one GPU (by PCI bus id; equal on every rank).
+  int maxRanksPerDevice() const;
 
   // Throws IoException if a peer process has exited.
   void checkPeersAlive();

@@ -1079,16 +1079,30 @@ void HipPlanExecutor::setupDevice() {
   GLX_HIP_CHECK(hipDeviceSynchronize());
 }
 
+// Workgroups (= slices) per launch: kOsMaxSlices, fewer if the kernel's
+// resident capacity shared by the ranks on the busiest GPU is smaller (ranks
+// spin on each other's workgroups, so every grid must be resident at once).
+// Same inputs on every rank -> same grid.
+size_t HipPlanExecutor::maxSlices(bool twoShot) const {
+  const int cap = glx::device_engine_resident_blocks(twoShot, op_, dtype_);
+  const int share = context_->maxRanksPerDevice();
+  size_t g = glx::kOsMaxSlices;
+  if (cap > 0) g = std::min(g, (size_t)std::max(1, cap / std::max(1, share)));
+  return g;
+}
+
 void HipPlanExecutor::setupOneShot() {
   const int P = contextSize_;
   glx::OneShotParams& p = os_;
   p.P = P;
   p.rank = contextRank_;
   p.count = (size_t)count_;
-  // slices: >= 4 KiB, a whole number of 16-byte vectors, <= kOsMaxSlices
+  // slices: >= 4 KiB, a whole number of 16-byte vectors, at most
+  // maxSlices() of them (the grid must be resident as a whole)
   const size_t V = 16 / esize_;
   const size_t minSlice = 4096 / esize_;
-  size_t slice = ((size_t)count_ + glx::kOsMaxSlices - 1) / glx::kOsMaxSlices;
+  const size_t gmax = maxSlices(false);
+  size_t slice = ((size_t)count_ + gmax - 1) / gmax;
   slice = (std::max(slice, minSlice) + V - 1) / V * V;
   p.slice = slice;
   p.G = (int)(((size_t)count_ + slice - 1) / slice);
@@ -1157,7 +1171,8 @@ void HipPlanExecutor::setupTwoShot() {
   }
   const size_t V = 16 / esize_;
   const size_t minSlice = 4096 / esize_;
-  size_t slice = (maxLen + glx::kOsMaxSlices - 1) / glx::kOsMaxSlices;
+  const size_t gmax = maxSlices(true);
+  size_t slice = (maxLen + gmax - 1) / gmax;
   slice = (std::max(slice, minSlice) + V - 1) / V * V;
   p.slice = slice;
   p.G = (int)std::max<size_t>(1, (maxLen + slice - 1) / slice);

@@ -214,6 +214,7 @@ class HipPlanExecutor : public Algorithm {
   static int engineFor(const Context& ctx, int algo, int64_t count);
   char* ddAlloc(size_t bytes);
   void setupDevice();
+  size_t maxSlices(bool twoShot) const;
   void setupOneShot();
   void setupTwoShot();
   void runDevice(char* ptr0);

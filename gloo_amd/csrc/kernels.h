@@ -82,6 +82,10 @@ struct TwoShotParams {
   int P, rank, G;
 };
 hipError_t launch_twoshot(int op, int dtype, const TwoShotParams& p, hipStream_t s);
+// Workgroups of the one-shot (twoShot = false) / two-shot kernel for (op,
+// dtype) that fit on the current device at once (occupancy x CUs).  A grid
+// of peers waiting on each other must be resident as a whole.
+int device_engine_resident_blocks(bool twoShot, int op, int dtype);
 
 // Tuning knobs of the vector kernel (lanes' unroll depth, grid cap per CU,
 // nontemporal loads/stores: 0/1, -1 = keep).

@@ -81,14 +81,14 @@ __device__ __forceinline__ void copy_span(S* dst, const S* src, size_t a, size_t
   }
   const v4u* vs = reinterpret_cast<const v4u*>(src);
   v4u* vd = reinterpret_cast<v4u*>(dst);
+  constexpr int U = 8;  // vectors in flight per lane
   size_t i = va + threadIdx.x;
-  for (; i + 3 * kBlock < vb; i += 4 * kBlock) {  // 4 vectors in flight per lane
-    const v4u x0 = vs[i], x1 = vs[i + kBlock], x2 = vs[i + 2 * kBlock],
-              x3 = vs[i + 3 * kBlock];
-    vd[i] = x0;
-    vd[i + kBlock] = x1;
-    vd[i + 2 * kBlock] = x2;
-    vd[i + 3 * kBlock] = x3;
+  for (; i + (U - 1) * kBlock < vb; i += U * kBlock) {
+    v4u x[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) x[u] = vs[i + u * kBlock];
+#pragma unroll
+    for (int u = 0; u < U; u++) vd[i + u * kBlock] = x[u];
   }
   for (; i < vb; i += kBlock) vd[i] = vs[i];
 }
@@ -157,8 +157,38 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
       if (d < nout) reinterpret_cast<S*>(outs[d])[i] = acc;
     }
   }
-  for (size_t v = va + threadIdx.x; v < vb; v += kBlock) {
-    v4u y[kOsMaxRanks];  // all P loads in flight before the chain
+  // two vectors per lane, all 2P loads in flight before the chains (not for
+  // 1-byte types: 16 lanes of byte ops per vector already fill the registers)
+  size_t v = va + threadIdx.x;
+  for (; sizeof(S) > 1 && v + kBlock < vb; v += 2 * kBlock) {
+    v4u y[kOsMaxRanks], z[kOsMaxRanks];
+#pragma unroll
+    for (int k = 0; k < kOsMaxRanks; k++) {
+      if (k < P) {
+        y[k] = reinterpret_cast<const v4u*>(srcs[k])[v];
+        z[k] = reinterpret_cast<const v4u*>(srcs[k])[v + kBlock];
+      }
+    }
+    v4u acc = y[0], acc2 = z[0];
+#pragma unroll
+    for (int k = 1; k < kOsMaxRanks; k++) {
+      if (k < P) {
+        acc = vec_apply<T, OP>(y[k], acc);
+        acc2 = vec_apply<T, OP>(z[k], acc2);
+      }
+    }
+    reinterpret_cast<v4u*>(dst)[v] = acc;
+    reinterpret_cast<v4u*>(dst)[v + kBlock] = acc2;
+#pragma unroll
+    for (int d = 0; d < kOsMaxRanks - 1; d++) {
+      if (d < nout) {
+        reinterpret_cast<v4u*>(outs[d])[v] = acc;
+        reinterpret_cast<v4u*>(outs[d])[v + kBlock] = acc2;
+      }
+    }
+  }
+  for (; v < vb; v += kBlock) {
+    v4u y[kOsMaxRanks];
 #pragma unroll
     for (int k = 0; k < kOsMaxRanks; k++) {
       if (k < P) y[k] = reinterpret_cast<const v4u*>(srcs[k])[v];
@@ -215,7 +245,9 @@ __device__ __forceinline__ bool wait_flag(const uint64_t* word, uint64_t epoch, 
 // ---- one-shot ---------------------------------------------------------------
 
 template <typename T, int OP>
-__global__ __launch_bounds__(kBlock) void oneshot_kernel(OneShotParams p) {
+// >= 2 waves per SIMD: every rank's grid (<= kOsMaxSlices workgroups) stays
+// resident even when a few ranks share one GPU
+__global__ __launch_bounds__(kBlock, 2) void oneshot_kernel(OneShotParams p) {
   using S = typename Elem<T, OP>::S;
   __shared__ int s_ok;
   const int w = blockIdx.x;
@@ -263,7 +295,7 @@ __global__ __launch_bounds__(kBlock) void oneshot_kernel(OneShotParams p) {
 // ---- two-shot ---------------------------------------------------------------
 
 template <typename T, int OP>
-__global__ __launch_bounds__(kBlock) void twoshot_kernel(TwoShotParams p) {
+__global__ __launch_bounds__(kBlock, 2) void twoshot_kernel(TwoShotParams p) {
   using S = typename Elem<T, OP>::S;
   __shared__ int s_ok;
   const int w = blockIdx.x;
@@ -277,9 +309,11 @@ __global__ __launch_bounds__(kBlock) void twoshot_kernel(TwoShotParams p) {
     return a < b;
   };
 
-  // 1. push my copy of every other range's slice to its owner
-  for (int d = 1; d < p.P; d++) {
-    int j = p.rank + d;
+  // 1. push my copy of every other range's slice to its owner.  Workgroups
+  //    start at different owners (w mod P-1) so that at any moment the
+  //    grid's stores spread over all P-1 links instead of queueing on one.
+  for (int q = 0; q < p.P - 1; q++) {
+    int j = p.rank + 1 + (q + w) % (p.P - 1);
     if (j >= p.P) j -= p.P;
     size_t a, b;
     if (span(j, a, b)) copy_span<S>(reinterpret_cast<S*>(p.rsPush[j]), buf, a, b, aligned);
@@ -363,7 +397,51 @@ hipError_t launch_ts_op(int op, const TwoShotParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <typename T>
+int resident_typed(bool twoShot, int op) {
+  const void* k = nullptr;
+  switch (op) {
+    case GLX_SUM:
+      k = twoShot ? (const void*)twoshot_kernel<T, GLX_SUM> : (const void*)oneshot_kernel<T, GLX_SUM>;
+      break;
+    case GLX_PRODUCT:
+      k = twoShot ? (const void*)twoshot_kernel<T, GLX_PRODUCT>
+                  : (const void*)oneshot_kernel<T, GLX_PRODUCT>;
+      break;
+    case GLX_MAX:
+      k = twoShot ? (const void*)twoshot_kernel<T, GLX_MAX> : (const void*)oneshot_kernel<T, GLX_MAX>;
+      break;
+    case GLX_MIN:
+      k = twoShot ? (const void*)twoshot_kernel<T, GLX_MIN> : (const void*)oneshot_kernel<T, GLX_MIN>;
+      break;
+    default: return 0;
+  }
+  int perCu = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCu, k, kBlock, 0) != hipSuccess ||
+      hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return perCu * cus;
+}
+
 }  // namespace
+
+int device_engine_resident_blocks(bool twoShot, int op, int dtype) {
+  switch (dtype) {
+    case GLX_INT8: return resident_typed<int8_t>(twoShot, op);
+    case GLX_UINT8: return resident_typed<uint8_t>(twoShot, op);
+    case GLX_INT32: return resident_typed<int32_t>(twoShot, op);
+    case GLX_INT64: return resident_typed<int64_t>(twoShot, op);
+    case GLX_UINT64: return resident_typed<uint64_t>(twoShot, op);
+    case GLX_FLOAT32: return resident_typed<float>(twoShot, op);
+    case GLX_FLOAT64: return resident_typed<double>(twoShot, op);
+    case GLX_FLOAT16: return resident_typed<f16_t>(twoShot, op);
+    case GLX_BFLOAT16: return resident_typed<bf16_t>(twoShot, op);
+  }
+  return 0;
+}
 
 hipError_t launch_oneshot(int op, int dtype, const OneShotParams& p, hipStream_t s) {
   if (p.P < 2 || p.P > kOsMaxRanks || p.G < 1 || p.G > kOsMaxSlices || p.njobs < 0 ||
