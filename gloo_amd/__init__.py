@@ -18,6 +18,7 @@ from .algorithms import (  # noqa: F401
     HipAllreduceRingChunked,
     ReductionFunction,
     ReductionType,
+    device_layout,
     plan,
 )
 from .collectives import AllreduceOptions, allreduce  # noqa: F401

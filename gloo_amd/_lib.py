@@ -66,6 +66,7 @@ SIGNATURES = [
     ("glx_algorithm_bytes_sent", _i64, [_vp]),
     ("glx_algorithm_engine", _i, [_vp]),
     ("glx_algorithm_destroy", None, [_vp]),
+    ("glx_device_layout", _i64, [_i, _i, _i, _i64, _i, _i64, ctypes.POINTER(_i64), _i64]),
     ("glx_plan", _i64, [_i, _i, _i, _i64, ctypes.POINTER(_i64), _i64,
                         ctypes.POINTER(_i64)]),
     ("glx_plan_fold", _i64, [_i, _i, _i, _i64, _i64, ctypes.POINTER(_i64), _i64]),

@@ -251,6 +251,33 @@ def plan(algo, rank, size, count, with_folds=False, esize=4, max_segment_size=0,
     return steps, scratch.value, folds
 
 
+def device_layout(algo, rank, size, count, esize=4, max_slices=256):
+    """Geometry the device-driven engines (one-shot: replicated schedules,
+    two-shot: mesh schedules) derive from the compiled plan (host logic, no
+    GPU): dict with G, slice, max_len, jobs [(off, len, chain)] (one-shot),
+    ranges [(off, len)] by owner and my_chain (two-shot)."""
+    code = ALGO_CODES[algo]
+    n = lib.glx_device_layout(code, rank, size, count, esize, max_slices, None, 0)
+    if n < 0:
+        check(_lib.ERR_INVALID, "device_layout")
+    b = (ctypes.c_int64 * n)()
+    lib.glx_device_layout(code, rank, size, count, esize, max_slices, b, n)
+    v = list(b)
+    K = 8
+    G, slice_, max_len, njobs = v[:4]
+    at = 4
+    job_off, job_len = v[at:at + K], v[at + K:at + 2 * K]
+    at += 2 * K
+    chains = [v[at + q * K: at + q * K + size] for q in range(K)]
+    at += K * K
+    r_off, r_len = v[at:at + K], v[at + K:at + 2 * K]
+    at += 2 * K
+    my_chain = v[at:at + size]
+    return {"G": G, "slice": slice_, "max_len": max_len,
+            "jobs": [(job_off[q], job_len[q], chains[q]) for q in range(njobs)],
+            "ranges": [(r_off[c], r_len[c]) for c in range(size)], "my_chain": my_chain}
+
+
 def stage_plan(algo, rank, size, count, esize=4, max_piece=None):
     """Host-memory staging of a plan (glx_plan_stage): (h2d pieces [(off,
     len)] in issue order, copy-backs [(step, off, len)], step -1 = after the

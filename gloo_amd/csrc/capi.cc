@@ -455,6 +455,35 @@ int64_t glx_plan_stage(int algo, int rank, int size, int64_t count, int esize,
   return n;
 }
 
+int64_t glx_device_layout(int algo, int rank, int size, int64_t count, int esize,
+                          int64_t max_slices, int64_t* out, int64_t cap) {
+  int64_t n = -1;
+  guarded([&]() -> int {
+    const bool oneShot = algo == GLX_ALGO_RING_CHUNKED_REPL || algo == glx::ALGO_FN_RING_REPL;
+    const bool twoShot = algo == GLX_ALGO_RING_CHUNKED_MESH || algo == glx::ALGO_FN_RING_MESH;
+    GLX_ENFORCE(oneShot || twoShot, "glx_device_layout: not a replicated or mesh schedule");
+    GLX_ENFORCE(esize == 1 || esize == 2 || esize == 4 || esize == 8, "bad element size");
+    glx::Plan p = glx::makePlan(algo, rank, size, count,
+                                planParams(esize, 0, glx::PlanParams().minPieceBytes));
+    const glx::DeviceLayout d =
+        oneShot ? glx::oneShotLayout(p, rank, size, count, esize, max_slices)
+                : glx::twoShotLayout(p, rank, size, count, esize, max_slices);
+    std::vector<int64_t> v = {d.G, d.slice, d.maxLen, d.njobs};
+    const int K = glx::kDevMaxRanks;
+    for (int q = 0; q < K; q++) v.push_back(d.jobOff[q]);
+    for (int q = 0; q < K; q++) v.push_back(d.jobLen[q]);
+    for (int q = 0; q < K; q++)
+      for (int i = 0; i < K; i++) v.push_back(d.chain[q][i]);
+    for (int c = 0; c < K; c++) v.push_back(d.rangeOff[c]);
+    for (int c = 0; c < K; c++) v.push_back(d.rangeLen[c]);
+    for (int i = 0; i < K; i++) v.push_back(d.myChain[i]);
+    n = (int64_t)v.size();
+    for (int64_t i = 0; i < n && i < cap && out != nullptr; i++) out[i] = v[(size_t)i];
+    return GLX_OK;
+  });
+  return n;
+}
+
 int64_t glx_plan_fold(int algo, int rank, int size, int64_t count, int64_t fold,
                       int64_t* srcs, int64_t cap) {
   return glx_plan_fold_ex(algo, rank, size, count, 4, 0, glx::PlanParams().minPieceBytes,

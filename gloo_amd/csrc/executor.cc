@@ -1093,35 +1093,19 @@ size_t HipPlanExecutor::maxSlices(bool twoShot) const {
 
 void HipPlanExecutor::setupOneShot() {
   const int P = contextSize_;
+  const glx::DeviceLayout d =
+      glx::oneShotLayout(plan_, contextRank_, P, count_, (int)esize_, (int64_t)maxSlices(false));
   glx::OneShotParams& p = os_;
   p.P = P;
   p.rank = contextRank_;
   p.count = (size_t)count_;
-  // slices: >= 4 KiB, a whole number of 16-byte vectors, at most
-  // maxSlices() of them (the grid must be resident as a whole)
-  const size_t V = 16 / esize_;
-  const size_t minSlice = 4096 / esize_;
-  const size_t gmax = maxSlices(false);
-  size_t slice = ((size_t)count_ + gmax - 1) / gmax;
-  slice = (std::max(slice, minSlice) + V - 1) / V * V;
-  p.slice = slice;
-  p.G = (int)(((size_t)count_ + slice - 1) / slice);
-  // chunk ranges and their chains, read off the replicated plan's folds
-  const int64_t region = count_ + glx::kPadElems;
-  p.njobs = 0;
-  for (const auto& s : plan_.steps) {
-    if (s.kind != glx::FOLD) continue;
-    GLX_ENFORCE(p.njobs < glx::kOsMaxRanks, "one-shot: too many chunk ranges");
-    const auto& f = plan_.folds[(size_t)s.boff];
-    GLX_ENFORCE((int)f.size() == P, "one-shot: fold of ", f.size(), " sources for ", P, " ranks");
-    for (int i = 0; i < P; i++) {
-      const int64_t r = f[(size_t)i];
-      GLX_ENFORCE(r < 0 || r % region == 0, "one-shot: unexpected fold source");
-      p.chain[p.njobs][i] = (uint8_t)(r < 0 ? contextRank_ : (int)(r / region));
-    }
-    p.jobOff[p.njobs] = (size_t)s.off;
-    p.jobLen[p.njobs] = (size_t)s.len;
-    p.njobs++;
+  p.slice = (size_t)d.slice;
+  p.G = d.G;
+  p.njobs = d.njobs;
+  for (int q = 0; q < d.njobs; q++) {
+    p.jobOff[q] = (size_t)d.jobOff[q];
+    p.jobLen[q] = (size_t)d.jobLen[q];
+    for (int i = 0; i < P; i++) p.chain[q][i] = (uint8_t)d.chain[q][i];
   }
   ddSlot_ = ((size_t)count_ * esize_ + 255) & ~(size_t)255;
   ddAlloc((size_t)P * ddSlot_);
@@ -1132,51 +1116,19 @@ void HipPlanExecutor::setupOneShot() {
 
 void HipPlanExecutor::setupTwoShot() {
   const int P = contextSize_;
+  const glx::DeviceLayout d =
+      glx::twoShotLayout(plan_, contextRank_, P, count_, (int)esize_, (int64_t)maxSlices(true));
   glx::TwoShotParams& p = ts_;
   p.P = P;
   p.rank = contextRank_;
-  // owners' ranges and this rank's chain, read off the mesh plan: channel-0
-  // SENDs carry this rank's copy of range j to owner j, the FOLD our own range
-  for (int c = 0; c < glx::kOsMaxRanks; c++) p.rangeOff[c] = p.rangeLen[c] = 0;
-  for (int i = 0; i < P; i++) p.chain[i] = (uint8_t)i;
-  size_t maxLen = 0;
-  for (const auto& s : plan_.steps) {
-    if (s.kind == glx::SEND && s.channel == 0) {
-      p.rangeOff[s.peer] = (size_t)s.off;
-      p.rangeLen[s.peer] = (size_t)s.len;
-      maxLen = std::max(maxLen, (size_t)s.len);
-    }
+  for (int c = 0; c < glx::kOsMaxRanks; c++) {
+    p.rangeOff[c] = (size_t)d.rangeOff[c];
+    p.rangeLen[c] = (size_t)d.rangeLen[c];
+    p.chain[c] = (uint8_t)d.myChain[c];
   }
-  const glx::Step* fold = nullptr;
-  for (const auto& s : plan_.steps) {
-    if (s.kind == glx::FOLD) fold = &s;
-  }
-  if (fold != nullptr) {
-    p.rangeOff[contextRank_] = (size_t)fold->off;
-    p.rangeLen[contextRank_] = (size_t)fold->len;
-    maxLen = std::max(maxLen, (size_t)fold->len);
-  }
-  // every non-empty range is a channel-0 SEND target or our own FOLD, so
-  // maxLen is the plan's largest range: FOLD sources are multiples of it + pad
-  if (fold != nullptr) {
-    const auto& f = plan_.folds[(size_t)fold->boff];
-    GLX_ENFORCE((int)f.size() == P, "two-shot: fold of ", f.size(), " sources for ", P,
-                " ranks");
-    const int64_t region = (int64_t)maxLen + glx::kPadElems;
-    for (int i = 0; i < P; i++) {
-      const int64_t r = f[(size_t)i];
-      GLX_ENFORCE(r < 0 || r % region == 0, "two-shot: unexpected fold source");
-      p.chain[i] = (uint8_t)(r < 0 ? contextRank_ : (int)(r / region));
-    }
-  }
-  const size_t V = 16 / esize_;
-  const size_t minSlice = 4096 / esize_;
-  const size_t gmax = maxSlices(true);
-  size_t slice = (maxLen + gmax - 1) / gmax;
-  slice = (std::max(slice, minSlice) + V - 1) / V * V;
-  p.slice = slice;
-  p.G = (int)std::max<size_t>(1, (maxLen + slice - 1) / slice);
-  ddSlot_ = (maxLen * esize_ + 16 + 255) & ~(size_t)255;
+  p.slice = (size_t)d.slice;
+  p.G = d.G;
+  ddSlot_ = ((size_t)d.maxLen * esize_ + 16 + 255) & ~(size_t)255;
   for (int k = 0; k < 4; k++) ddAlloc((size_t)P * ddSlot_);  // RS 0/1, AG 0/1
   char* flags = ddAlloc(2 * (size_t)P * (size_t)p.G * sizeof(uint64_t));
   p.flagAIn = reinterpret_cast<const uint64_t*>(flags);

@@ -738,6 +738,80 @@ Plan makePlan(int algo, int rank, int size, int64_t count, const PlanParams& prm
 }
 
 // ---------------------------------------------------------------------------
+// Geometry of the device-driven engines
+// ---------------------------------------------------------------------------
+namespace {
+
+// slices: >= 4 KiB, a whole number of 16-byte vectors, at most maxSlices
+void sliceUp(DeviceLayout& d, int64_t len, int esize, int64_t maxSlices) {
+  const int64_t V = 16 / esize, minSlice = 4096 / esize;
+  const int64_t gmax = std::max<int64_t>(1, std::min<int64_t>(maxSlices, 1 << 20));
+  int64_t slice = (len + gmax - 1) / gmax;
+  slice = (std::max(slice, minSlice) + V - 1) / V * V;
+  d.slice = slice;
+  d.G = (int)std::max<int64_t>(1, (len + slice - 1) / slice);
+}
+
+// FOLD sources are region offsets (multiples of `region`) or -1 (ptr0)
+void chainOf(const std::vector<int64_t>& f, int64_t region, int rank, int size, int* out) {
+  if ((int)f.size() != size) fail("device layout: fold of " + std::to_string(f.size()) +
+                                  " sources for " + std::to_string(size) + " ranks");
+  for (int i = 0; i < size; i++) {
+    const int64_t r = f[(size_t)i];
+    if (r >= 0 && r % region != 0) fail("device layout: unexpected fold source");
+    out[i] = r < 0 ? rank : (int)(r / region);
+  }
+}
+
+}  // namespace
+
+DeviceLayout oneShotLayout(const Plan& plan, int rank, int size, int64_t count, int esize,
+                           int64_t maxSlices) {
+  if (size < 2 || size > kDevMaxRanks || count <= 0) fail("device layout: bad geometry");
+  DeviceLayout d;
+  sliceUp(d, count, esize, maxSlices);
+  const int64_t region = count + kPadElems;  // replicatedPlan's regions
+  for (const auto& st : plan.steps) {
+    if (st.kind != FOLD) continue;
+    if (d.njobs >= kDevMaxRanks) fail("device layout: too many chunk ranges");
+    chainOf(plan.folds[(size_t)st.boff], region, rank, size, d.chain[d.njobs]);
+    d.jobOff[d.njobs] = st.off;
+    d.jobLen[d.njobs] = st.len;
+    d.njobs++;
+  }
+  d.maxLen = count;
+  return d;
+}
+
+DeviceLayout twoShotLayout(const Plan& plan, int rank, int size, int64_t count, int esize,
+                           int64_t maxSlices) {
+  if (size < 2 || size > kDevMaxRanks || count <= 0) fail("device layout: bad geometry");
+  DeviceLayout d;
+  // channel-0 SENDs carry this rank's copy of range j to owner j; the FOLD
+  // is our own range.  Every non-empty range is one or the other, so maxLen
+  // is the plan's largest range (meshPlan's region = maxLen + pad).
+  for (int i = 0; i < size; i++) d.myChain[i] = i;
+  const Step* fold = nullptr;
+  for (const auto& st : plan.steps) {
+    if (st.kind == SEND && st.channel == 0) {
+      d.rangeOff[st.peer] = st.off;
+      d.rangeLen[st.peer] = st.len;
+      d.maxLen = std::max(d.maxLen, st.len);
+    } else if (st.kind == FOLD) {
+      fold = &st;
+    }
+  }
+  if (fold != nullptr) {
+    d.rangeOff[rank] = fold->off;
+    d.rangeLen[rank] = fold->len;
+    d.maxLen = std::max(d.maxLen, fold->len);
+    chainOf(plan.folds[(size_t)fold->boff], d.maxLen + kPadElems, rank, size, d.myChain);
+  }
+  sliceUp(d, std::max<int64_t>(1, d.maxLen), esize, maxSlices);
+  return d;
+}
+
+// ---------------------------------------------------------------------------
 // Staging of host-memory buffers
 // ---------------------------------------------------------------------------
 namespace {

@@ -123,6 +123,30 @@ Plan makePlan(int algo, int rank, int size, int64_t count,
 // one; GLOO_AMD_REPLICATED_MAX_BYTES sets the threshold.
 int autoRingSchedule(int size, int64_t bytes, bool fn, bool deviceDriven = false);
 
+// Geometry of the device-driven engines (xgmi_kernels.hip), read off a
+// compiled replicated plan (one-shot) or mesh plan (two-shot): the same
+// ranges and chains as the plan's FOLD steps, so the kernels compute exactly
+// what the steps engine computes.  One workgroup per slice index; slices are
+// >= 4 KiB, whole 16-byte vectors, at most maxSlices of them.
+constexpr int kDevMaxRanks = 8;
+struct DeviceLayout {
+  int G = 0;            // workgroups = slices
+  int64_t slice = 0;    // elements per slice (one-shot: of the buffer;
+                        // two-shot: of every owner's range)
+  // one-shot: chunk ranges and each one's chain (fold order of ranks)
+  int njobs = 0;
+  int64_t jobOff[kDevMaxRanks] = {}, jobLen[kDevMaxRanks] = {};
+  int chain[kDevMaxRanks][kDevMaxRanks] = {};
+  // two-shot: owner j's range, and this rank's own chain
+  int64_t rangeOff[kDevMaxRanks] = {}, rangeLen[kDevMaxRanks] = {};
+  int myChain[kDevMaxRanks] = {};
+  int64_t maxLen = 0;   // largest range (two-shot slot size)
+};
+DeviceLayout oneShotLayout(const Plan& plan, int rank, int size, int64_t count, int esize,
+                           int64_t maxSlices);
+DeviceLayout twoShotLayout(const Plan& plan, int rank, int size, int64_t count, int esize,
+                           int64_t maxSlices);
+
 // Host-memory endpoints: when the user's buffer is in host
 // memory the executor stages it through a device buffer.  This derives from
 // a plan (1) the order to copy the buffer in: pieces in the order the steps

@@ -294,6 +294,14 @@ void glx_algorithm_destroy(glx_algorithm* alg);
  * per-rank receive-buffer size. */
 int64_t glx_plan(int algo, int rank, int size, int64_t count, int64_t* steps,
                  int64_t cap, int64_t* scratch_elems);
+/* Geometry the device-driven engines derive from a replicated (one-shot)
+ * or mesh (two-shot) schedule, for host-side replay in tests: writes
+ * [G, slice, maxLen, njobs, jobOff[8], jobLen[8], chain[8][8], rangeOff[8],
+ * rangeLen[8], myChain[8]] (up to cap values) and returns their number, or
+ * -1 (glx_last_error()).  max_slices bounds G (the launch uses the kernel's
+ * resident capacity per rank). */
+int64_t glx_device_layout(int algo, int rank, int size, int64_t count, int esize,
+                          int64_t max_slices, int64_t* out, int64_t cap);
 /* Sources of FOLD step number `fold` (its boff field): region offsets, -1 =
  * the rank's own buffer.  Returns the count (writes at most cap) or -1. */
 int64_t glx_plan_fold(int algo, int rank, int size, int64_t count, int64_t fold,
