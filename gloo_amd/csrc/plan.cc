@@ -712,10 +712,15 @@ int autoRingSchedule(int size, int64_t bytes, bool fn, bool deviceDriven) {
     if (v == "mesh") return mesh;
     if (v == "replicated") return repl;
   }
-  // host-mediated: the reference's kOnDeviceThreshold (algorithm.cc:16);
-  // one-shot kernel: where its (P-1)·S per-link bytes start to cost more than
-  // the mesh's two host-mediated rounds
-  int64_t maxRepl = deviceDriven ? (int64_t(2) << 20) : (int64_t(256) << 10);
+  // host-mediated: the reference's kOnDeviceThreshold (algorithm.cc:16).
+  // Device-driven: one-shot moves S per link in one round, two-shot 2S/P per
+  // link in two; with a round costing L and links B, one-shot wins below
+  // S* = L·B / (1 - 2/P): always at P = 2, ~1-2 MiB at P = 4, less at P = 8.
+  int64_t maxRepl = int64_t(256) << 10;
+  if (deviceDriven) {
+    maxRepl = size <= 2 ? (int64_t(16) << 20) : size <= 4 ? (int64_t(2) << 20)
+                                                          : (int64_t(1) << 20);
+  }
   if (const char* e = std::getenv("GLOO_AMD_REPLICATED_MAX_BYTES")) maxRepl = std::atoll(e);
   if (size <= 1) return ring;
   return bytes <= maxRepl ? repl : mesh;

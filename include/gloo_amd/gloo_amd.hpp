@@ -231,8 +231,9 @@ class DeviceAllreduce : public Algorithm {
 // RING = the reference's ring (one link per direction); MESH = each rank
 // folds its chunk pair from every peer directly (all links at once);
 // REPLICATED = one round, every rank folds everything (small buffers);
-// AUTO = REPLICATED up to a threshold per rank (2 MiB with the device-driven
-// engines, 256 KiB without), MESH above.  With the ranks on distinct devices
+// AUTO = REPLICATED up to a threshold per rank (with the device-driven
+// engines 16 MiB at P = 2, 2 MiB at P <= 4, 1 MiB above; 256 KiB without),
+// MESH above.  With the ranks on distinct devices
 // or processes REPLICATED and MESH run as one device-driven kernel per rank
 // (one-shot / two-shot; see setMeshEngine / setDeviceEngines).
 enum class Schedule { RING, MESH, REPLICATED, AUTO };

@@ -8,6 +8,9 @@ algo: ring_chunked | halving_doubling | ring_chunked_mesh (class algorithms)
       oneshot | twoshot (the replicated / mesh schedule as one device-driven
       kernel per rank: class and function style, dtypes x ops x sizes,
       device and host buffers, repeated runs; prints per-op latencies)
+      devtimeout (rank 0 runs both device engines while the other ranks never
+      call run(): its kernels must give up after the timeout and run() must
+      raise IoException)
 
 Checks its result against the oracle and prints OK."""
 import os
@@ -30,6 +33,8 @@ def main():
     N = 100003
     if algo in ("oneshot", "twoshot"):
         return run_device(store_dir, rank, size, algo)
+    if algo == "devtimeout":
+        return run_device_timeout(store_dir, rank, size)
     if algo.startswith("fn_"):
         return run_fn(store_dir, rank, size, algo, N)
     code = O.HALVING_DOUBLING if algo == "halving_doubling" else O.RING_CHUNKED
@@ -100,6 +105,44 @@ def run_fn(store_dir, rank, size, algo, N):
     store.set("done/%d" % rank, b"1")
     for r in range(size):
         store.get("done/%d" % r, timeout_ms=60000)
+    ctx.close()
+    if not ok:
+        print("MISMATCH rank", rank)
+        sys.exit(1)
+    print("OK")
+
+
+def run_device_timeout(store_dir, rank, size):
+    import time
+
+    import torch
+
+    import gloo_amd
+
+    store = gloo_amd.rendezvous.FileStore(store_dir)
+    ctx = gloo_amd.rendezvous.Context(rank, size, 0)
+    ctx.setTimeout(3)
+    ctx.connectFullMesh(store)
+    ok = True
+    for sched, eng, n in (("replicated", "oneshot", 4099), ("mesh", "twoshot", 1 << 20)):
+        buf = torch.ones(n, device="cuda")
+        alg = gloo_amd.AllreduceRingChunked(ctx, [buf], schedule=sched)
+        ok = ok and alg.engine() == eng
+        if rank == 0:
+            t0 = time.time()
+            try:
+                alg.run()
+                print("NO TIMEOUT", sched)
+                ok = False
+            except gloo_amd.IoException as e:
+                dt = time.time() - t0
+                print("timed out as expected after %.1f s: %s" % (dt, e))
+                ok = ok and "Timed out" in str(e) and dt < 30
+            store.set("timeout_done/%s" % sched, b"1")
+        else:
+            store.get("timeout_done/%s" % sched, timeout_ms=120000)
+        torch.cuda.synchronize()  # the kernels that gave up have exited
+        alg.close()
     ctx.close()
     if not ok:
         print("MISMATCH rank", rank)

@@ -286,6 +286,30 @@ def test_device_engine_multiprocess(P, mode):
             assert "OK" in outs[r]
 
 
+def test_device_engine_timeout_raises_io_exception():
+    """A device-driven kernel whose peers never arrive gives up after the
+    context timeout (every wave exits), and run() raises IoException."""
+    P = 2
+    with tempfile.TemporaryDirectory() as d:
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), "devtimeout"],
+                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                 for r in range(P)]
+        outs = []
+        for p in procs:
+            try:
+                o, _ = p.communicate(timeout=120)
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+            outs.append(o.decode(errors="replace"))
+        for r, p in enumerate(procs):
+            print(outs[r])
+            assert p.returncode == 0, "rank %d failed:\n%s" % (r, outs[r])
+            assert "OK" in outs[r]
+
+
 @pytest.mark.parametrize("split", [2, 4])
 @pytest.mark.parametrize("algo", [O.RING_CHUNKED, O.HALVING_DOUBLING, MESH],
                          ids=["ring_chunked", "halving_doubling", "mesh"])
