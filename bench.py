@@ -261,19 +261,29 @@ def reduce_kernel_roofline(torch, gloo_amd, dev, chunk_bytes, reps=50):
 RING_SCHEDULES = {"ring_chunked": "ring", "ring_chunked_mesh": "mesh",
                   "ring_chunked_mesh_steps": "mesh", "ring_chunked_repl": "replicated",
                   "ring_chunked_auto": "auto"}
-ENGINES = {}  # bench name -> engine the product chose ("steps", "oneshot", "twoshot")
+ENGINES = {}  # bench name -> engine the product chose (steps/oneshot/twoshot/devsteps)
 
 
 def plan_name(algo):
     """Schedule name of a bench candidate for gloo_amd.plan()."""
+    if algo.endswith("_host"):
+        algo = algo[:-len("_host")]
     return {"ring_chunked_mesh_steps": "ring_chunked_mesh",
             "ring_chunked_repl": "ring_chunked_repl"}.get(algo, algo)
 
 
 def make_alg(gloo_amd, ctx, buf, algo):
-    """ring_chunked_mesh runs on the two-shot device engine when the ranks are
-    on distinct devices/processes; ring_chunked_mesh_steps is the same
-    schedule with host-issued steps (calibrated peer-copy transport)."""
+    """With the ranks on distinct devices/processes: ring_chunked and
+    halving_doubling run their step programs in the plan kernel (devsteps),
+    ring_chunked_mesh on the two-shot kernel, ring_chunked_repl on the
+    one-shot kernel.  *_host and ring_chunked_mesh_steps are the same
+    schedules with host-issued steps (calibrated peer-copy transport)."""
+    if algo.endswith("_host"):
+        gloo_amd.set_steps_engine("host")
+        try:
+            return make_alg(gloo_amd, ctx, buf, algo[:-len("_host")])
+        finally:
+            gloo_amd.set_steps_engine("device")
     if algo == "halving_doubling":
         return gloo_amd.AllreduceHalvingDoubling(ctx, [buf])
     if algo == "ring_chunked_mesh_steps":
@@ -368,7 +378,8 @@ def probe_device_engines(torch, dist, gloo_amd, ctx, dev, dtype):
     ok, note = 1, "ok"
     ctx.setTimeout(15)
     try:
-        for algo, n in (("ring_chunked_repl", 65536 + 3), ("ring_chunked_mesh", (1 << 20) + 5)):
+        for algo, n in (("ring_chunked_repl", 65536 + 3), ("ring_chunked_mesh", (1 << 20) + 5),
+                        ("ring_chunked", 1 << 20), ("halving_doubling", 1 << 20)):
             x = synthetic(torch, n, dtype, dev, 99 + int(os.environ.get("RANK", "0")))
             ref = x.clone()
             torch.cuda.synchronize()  # run() does not order itself after torch's stream
@@ -421,11 +432,8 @@ def element_sweep(torch, dist, gloo_amd, ctx, dev, schedules, dtype):
             iters = 20 if n <= (1 << 20) else 5
             t, _ = time_schedule(torch, dist, gloo_amd, ctx, x, sched, iters, 2)
             row[sched] = {"us": round(t * 1e6, 1),
-                          "algbw_GBps": round(n * x.element_size() / t / 1e9, 3)}
-            if sched == "ring_chunked_repl":
-                alg = make_alg(gloo_amd, ctx, x, sched)
-                row[sched]["engine"] = alg.engine()
-                alg.close()
+                          "algbw_GBps": round(n * x.element_size() / t / 1e9, 3),
+                          "engine": ENGINES.get(sched)}
         out[str(n)] = row
     return out
 
@@ -507,7 +515,8 @@ def bench_multi(args):
         return int(t.view(torch.int16 if es == 2 else torch.int32).to(torch.int64).sum().item())
 
     if args.algo == "ring_chunked" and args.schedule == "auto":
-        candidates = ["ring_chunked", "ring_chunked_mesh", "ring_chunked_mesh_steps"]
+        candidates = ["ring_chunked", "ring_chunked_host", "ring_chunked_mesh",
+                      "ring_chunked_mesh_steps"]
     elif args.algo == "ring_chunked" and args.schedule == "mesh":
         candidates = ["ring_chunked_mesh", "ring_chunked_mesh_steps"]
     else:
@@ -538,7 +547,8 @@ def bench_multi(args):
                    "engine": ENGINES.get(a),
                    "busiest_link_GBps": round(lm / runs[a]["t"] / 1e9, 2)}
     if not args.no_alt:
-        for other in ("ring_chunked", "ring_chunked_mesh", "halving_doubling"):
+        for other in ("ring_chunked", "ring_chunked_mesh", "halving_doubling",
+                      "halving_doubling_host"):
             if other in runs:
                 continue
             buf.copy_(src)
@@ -575,13 +585,17 @@ def bench_multi(args):
             "config": {"workload": "allreduce_%s_%s_%dMiB_per_rank" % (
                            args.algo, {"f32": "fp32"}.get(args.dtype, args.dtype), args.size_mib),
                        "algorithm": args.algo,
-                       "schedule": {"ring_chunked": "ring", "ring_chunked_mesh": "mesh",
+                       "schedule": {"ring_chunked": "ring", "ring_chunked_host": "ring",
+                                    "ring_chunked_mesh": "mesh",
                                     "ring_chunked_mesh_steps": "mesh",
-                                    "halving_doubling": "halving_doubling"}[chosen],
+                                    "halving_doubling": "halving_doubling",
+                                    "halving_doubling_host": "halving_doubling"}[chosen],
                        "engine": ENGINES.get(chosen),
                        "schedule_note": "ring_chunked's chunking and reduction order; ring = "
                                         "the reference's data movement, mesh = all links "
-                                        "(bit-identical, checked)",
+                                        "(bit-identical, checked); engine: devsteps = the "
+                                        "step program in one kernel, twoshot = the mesh in "
+                                        "one kernel, steps = host-issued",
                        "bytes_per_rank": S, "elements": n,
                        "parallelism": "dp%d" % world,
                        "transport": "xGMI peer copies: " + runs[chosen]["transport"],

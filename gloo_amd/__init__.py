@@ -20,6 +20,7 @@ from .algorithms import (  # noqa: F401
     ReductionType,
     device_layout,
     plan,
+    plan_sync,
 )
 from .collectives import AllreduceOptions, allreduce  # noqa: F401
 from . import errors  # noqa: F401
@@ -49,6 +50,15 @@ def set_mesh_engine(engine):
     and fold kernels).  Same results either way."""
     code = {"steps": 0, "device": 2}[engine]
     errors.check(_lib.lib.glx_set_mesh_engine(code), "set_mesh_engine")
+
+
+def set_steps_engine(engine):
+    """Engine of ring / halving-doubling / bcube / function-style ring
+    algorithms created afterwards when the ranks are on distinct devices or
+    processes: "device" (the plan kernel, one device-driven launch per rank;
+    default) or "host" (host-issued steps).  Same results either way."""
+    code = {"host": 0, "device": 3}[engine]
+    errors.check(_lib.lib.glx_set_steps_engine(code), "set_steps_engine")
 
 
 def set_device_engines(mode):

@@ -67,6 +67,9 @@ SIGNATURES = [
     ("glx_algorithm_engine", _i, [_vp]),
     ("glx_algorithm_destroy", None, [_vp]),
     ("glx_device_layout", _i64, [_i, _i, _i, _i64, _i, _i64, ctypes.POINTER(_i64), _i64]),
+    ("glx_plan_sync", _i64, [_i, _i, _i, _i64, _i, _i64, _i64, _i, ctypes.POINTER(_i64),
+                             _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
+                             ctypes.POINTER(_i64), _i64]),
     ("glx_plan", _i64, [_i, _i, _i, _i64, ctypes.POINTER(_i64), _i64,
                         ctypes.POINTER(_i64)]),
     ("glx_plan_fold", _i64, [_i, _i, _i, _i64, _i64, ctypes.POINTER(_i64), _i64]),
@@ -79,6 +82,7 @@ SIGNATURES = [
     ("glx_set_copy_engine", _i, [_i, _i]),
     ("glx_set_mesh_engine", _i, [_i]),
     ("glx_set_device_engines", _i, [_i]),
+    ("glx_set_steps_engine", _i, [_i]),
     ("glx_allreduce", _i, [_vp, _i, _i, _i, ctypes.POINTER(_vp), _i, ctypes.POINTER(_vp), _i,
                            ctypes.c_size_t, ctypes.c_uint32, ctypes.c_size_t, _i64, _vp]),
 ]

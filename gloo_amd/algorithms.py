@@ -171,9 +171,12 @@ class Algorithm:
 
     def engine(self):
         """"steps" (host-issued schedule steps), "oneshot" (the replicated
-        schedule as one device-driven kernel per rank) or "twoshot" (the mesh
-        schedule as one device-driven kernel per rank)."""
-        return {0: "steps", 1: "oneshot", 2: "twoshot"}[lib.glx_algorithm_engine(self._h)]
+        schedule as one device-driven kernel per rank), "twoshot" (the mesh
+        schedule as one device-driven kernel per rank) or "devsteps" (any
+        other schedule's step program walked by one device-driven kernel per
+        rank)."""
+        return {0: "steps", 1: "oneshot", 2: "twoshot",
+                3: "devsteps"}[lib.glx_algorithm_engine(self._h)]
 
     def close(self):
         h = getattr(self, "_h", None)
@@ -276,6 +279,25 @@ def device_layout(algo, rank, size, count, esize=4, max_slices=256):
     return {"G": G, "slice": slice_, "max_len": max_len,
             "jobs": [(job_off[q], job_len[q], chains[q]) for q in range(njobs)],
             "ranges": [(r_off[c], r_len[c]) for c in range(size)], "my_chain": my_chain}
+
+
+def plan_sync(algo, rank, size, count, G, esize=4, max_segment_size=0,
+              min_piece_bytes=DEFAULT_MIN_PIECE_BYTES):
+    """The plan kernel's bookkeeping for one rank with G workgroups
+    (glx_plan_sync, host logic): dict with bounds (segment bounds), slice,
+    safe, steps [(channel, seg0, seg1, seq, per_run)]."""
+    code = ALGO_CODES[algo]
+    args = (code, rank, size, count, esize, max_segment_size, min_piece_bytes, G)
+    nb = ctypes.c_int64(0)
+    info = (ctypes.c_int64 * 2)()
+    n = lib.glx_plan_sync(*args, None, 0, ctypes.byref(nb), info, None, 0)
+    if n < 0:
+        check(_lib.ERR_INVALID, "plan_sync")
+    bb = (ctypes.c_int64 * max(nb.value, 1))()
+    sb = (ctypes.c_int64 * max(5 * n, 1))()
+    lib.glx_plan_sync(*args, bb, nb.value, ctypes.byref(nb), info, sb, n)
+    return {"bounds": list(bb[:nb.value]), "slice": info[0], "safe": bool(info[1]),
+            "steps": [tuple(sb[5 * i:5 * i + 5]) for i in range(n)]}
 
 
 def stage_plan(algo, rank, size, count, esize=4, max_piece=None):

@@ -181,6 +181,14 @@ int glx_set_mesh_engine(int engine) {
   return GLX_OK;
 }
 
+int glx_set_steps_engine(int engine) {
+  if (engine != GLX_ENGINE_STEPS && engine != GLX_ENGINE_DEVSTEPS) {
+    return fail(GLX_ERR_INVALID, "steps engine must be GLX_ENGINE_STEPS or GLX_ENGINE_DEVSTEPS");
+  }
+  gloo::HipPlanExecutor::setStepsEngine(engine);
+  return GLX_OK;
+}
+
 int glx_set_device_engines(int mode) {
   if (mode < -1 || mode > 1) return fail(GLX_ERR_INVALID, "device engine mode must be -1, 0 or 1");
   gloo::HipPlanExecutor::setDeviceEngines(mode);
@@ -450,6 +458,38 @@ int64_t glx_plan_stage(int algo, int rank, int size, int64_t count, int esize,
     }
     for (const auto& r : sp.d2hRest) put(-1, r);
     if (n_d2h) *n_d2h = k;
+    return GLX_OK;
+  });
+  return n;
+}
+
+int64_t glx_plan_sync(int algo, int rank, int size, int64_t count, int esize,
+                      int64_t max_segment_bytes, int64_t min_piece_bytes, int G,
+                      int64_t* bounds, int64_t bounds_cap, int64_t* nbounds, int64_t* info,
+                      int64_t* steps, int64_t cap) {
+  int64_t n = -1;
+  guarded([&]() -> int {
+    const glx::SyncTable t = glx::syncTable(
+        algo, rank, size, count, planParams(esize, max_segment_bytes, min_piece_bytes), G);
+    n = (int64_t)t.steps.size();
+    if (info) {
+      info[0] = t.slice;
+      info[1] = t.safe ? 1 : 0;
+    }
+    if (nbounds) *nbounds = (int64_t)t.bounds.size();
+    for (int64_t i = 0; i < (int64_t)t.bounds.size() && i < bounds_cap && bounds != nullptr;
+         i++) {
+      bounds[i] = t.bounds[(size_t)i];
+    }
+    for (int64_t i = 0; i < n && i < cap && steps != nullptr; i++) {
+      const glx::StepSync& y = t.steps[(size_t)i];
+      int64_t* o = steps + 5 * i;
+      o[0] = y.chan;
+      o[1] = y.seg0;
+      o[2] = y.seg1;
+      o[3] = (int64_t)y.seq;
+      o[4] = (int64_t)y.perRun;
+    }
     return GLX_OK;
   });
   return n;

@@ -129,6 +129,7 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
   glx::PlanParams pp = prm;
   pp.esize = (int)esize_;
   plan_ = glx::makePlan(algo, contextRank_, contextSize_, count, pp);
+  prm_ = pp;
 
   userStream_ = !streams.empty();
   if (userStream_) {
@@ -175,16 +176,33 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
   }
 
   engine_ = engineFor(*ctx, algo, count_);
-  if (engine_ != kEngineSteps) {
+  if (engine_ == kEngineDevSteps) {
+    // the plan kernel's grid and bookkeeping; when a landing region would be
+    // shared by two workgroups across messages, keep the host-issued steps
+    // (every rank computes the same from every rank's program)
+    const size_t minSlice = 4096 / esize_;
+    const glx::SyncTable probe = glx::syncTable(algo, contextRank_, contextSize_, count_, pp, 1);
+    int64_t maxSeg = 1;
+    for (size_t k = 0; k + 1 < probe.bounds.size(); k++) {
+      maxSeg = std::max(maxSeg, probe.bounds[k + 1] - probe.bounds[k]);
+    }
+    const size_t G = std::max<size_t>(
+        1, std::min(maxSlices(2), ((size_t)maxSeg + minSlice - 1) / minSlice));
+    sync_ = glx::syncTable(algo, contextRank_, contextSize_, count_, pp, (int)G);
+    pk_.G = (int)G;
+    if (!sync_.safe) engine_ = kEngineSteps;
+  }
+  if (engine_ == kEngineOneShot || engine_ == kEngineTwoShot) {
     setupDevice();
   } else {
-    allocScratch();
+    allocScratch(engine_ == kEngineDevSteps);  // the plan kernel's peers store into it
   }
 
   // Channels named by the plan; allocate our counter words.
   auto& ctl = ctx->localControl();
   stepChan_.assign(plan_.steps.size(), -1);
-  for (size_t i = 0; i < plan_.steps.size() && engine_ == kEngineSteps; i++) {
+  const bool hostSteps = engine_ == kEngineSteps;
+  for (size_t i = 0; i < plan_.steps.size() && (hostSteps || engine_ == kEngineDevSteps); i++) {
     const auto& s = plan_.steps[i];
     if (s.kind == glx::SEND) {
       int idx = outIndex((int)s.peer, (int)s.channel);
@@ -192,13 +210,15 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
         OutChan oc;
         oc.peer = (int)s.peer;
         oc.tag = (int)s.channel;
-        oc.creditWord = ctl.allocWord();
-        oc.credit = ctl.word(oc.creditWord);
+        // plan kernel: no control-block words or copy streams (flag rows
+        // are assigned in setupDevSteps)
+        oc.creditWord = hostSteps ? ctl.allocWord() : 0;
+        oc.credit = hostSteps ? ctl.word(oc.creditWord) : nullptr;
         // one copy stream per destination peer: copies to different peers
         // run concurrently on different xGMI links
-        oc.stream = -1;
+        oc.stream = hostSteps ? -1 : 0;
         for (const auto& o : out_) {
-          if (o.peer == oc.peer) oc.stream = o.stream;
+          if (hostSteps && o.peer == oc.peer) oc.stream = o.stream;
         }
         if (oc.stream < 0) {
           oc.stream = (int)copies_.size();
@@ -218,14 +238,15 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
         InChan ic;
         ic.peer = (int)s.peer;
         ic.tag = (int)s.channel;
-        ic.deliveryWord = ctl.allocWord();
-        ic.delivery = ctl.word(ic.deliveryWord);
+        ic.deliveryWord = hostSteps ? ctl.allocWord() : 0;
+        ic.delivery = hostSteps ? ctl.word(ic.deliveryWord) : nullptr;
         in_.push_back(ic);
         idx = (int)in_.size() - 1;
       }
       stepChan_[i] = idx;
     }
   }
+  if (engine_ == kEngineDevSteps) setupDevice();
   events_.resize(plan_.steps.size() * (size_t)split_, nullptr);
   for (auto& e : events_) GLX_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   GLX_HIP_CHECK(hipEventCreateWithFlags(&computeMark_, hipEventDisableTiming));
@@ -259,9 +280,14 @@ HipPlanExecutor::~HipPlanExecutor() noexcept(false) {
   if (ddDone_) hipEventDestroy(ddDone_);
   for (auto& c : copies_) hipStreamDestroy(c.s);
   if (ownCompute_ && compute_) hipStreamDestroy(compute_);
-  auto& ctl = context_->localControl();
-  for (auto& oc : out_) ctl.freeWord(oc.creditWord);
-  for (auto& ic : in_) ctl.freeWord(ic.deliveryWord);
+  if (devSteps_) hipFree(devSteps_);
+  if (devSegs_) hipFree(devSegs_);
+  if (devFoldSrc_) hipFree(devFoldSrc_);
+  if (engine_ == kEngineSteps) {
+    auto& ctl = context_->localControl();
+    for (auto& oc : out_) ctl.freeWord(oc.creditWord);
+    for (auto& ic : in_) ctl.freeWord(ic.deliveryWord);
+  }
 }
 
 int HipPlanExecutor::outIndex(int peer, int tag) {
@@ -378,12 +404,16 @@ void HipPlanExecutor::resolvePeers() {
       if (dir == DIR_IN) {  // peer receives from us on `tag`
         int idx = outIndex(r, tag);
         if (idx >= 0) {
-          out_[idx].delivery = pe.ctl->word((uint32_t)word);
+          if (engine_ == kEngineSteps) out_[idx].delivery = pe.ctl->word((uint32_t)word);
+          out_[idx].peerRow = word;
           out_[idx].peerDevice = pe.localDevice;
         }
       } else {  // peer sends to us on `tag`: its credit word
         int idx = inIndex(r, tag);
-        if (idx >= 0) in_[idx].credit = pe.ctl->word((uint32_t)word);
+        if (idx >= 0) {
+          if (engine_ == kEngineSteps) in_[idx].credit = pe.ctl->word((uint32_t)word);
+          in_[idx].peerRow = word;
+        }
       }
     }
     const int32_t peerEngine = getPod<int32_t>(b, at);
@@ -406,14 +436,28 @@ void HipPlanExecutor::resolvePeers() {
       }
     }
     if (engine_ != kEngineSteps) ddPeer_[r] = blocks;
+    if (engine_ == kEngineDevSteps) {  // the peer's flag rows for our channels
+      GLX_ENFORCE(!blocks.empty(), "rank ", r, " published no flag rows");
+      uint64_t* rows = reinterpret_cast<uint64_t*>(blocks[0]);
+      const size_t G = (size_t)pk_.G;
+      for (auto& oc : out_) {
+        if (oc.peer == r && oc.peerRow >= 0) oc.devDelivery = rows + (size_t)oc.peerRow * G;
+      }
+      for (auto& ic : in_) {
+        if (ic.peer == r && ic.peerRow >= 0) ic.devCredit = rows + (size_t)ic.peerRow * G;
+      }
+    }
   }
+  const bool dev = engine_ == kEngineDevSteps;
   for (auto& oc : out_) {
-    GLX_ENFORCE(oc.delivery != nullptr, "rank ", oc.peer, " has no receive channel ",
-                oc.tag, " from rank ", contextRank_, " (schedules disagree)");
+    GLX_ENFORCE(dev ? oc.devDelivery != nullptr : oc.delivery != nullptr, "rank ", oc.peer,
+                " has no receive channel ", oc.tag, " from rank ", contextRank_,
+                " (schedules disagree)");
   }
   for (auto& ic : in_) {
-    GLX_ENFORCE(ic.credit != nullptr, "rank ", ic.peer, " has no send channel ", ic.tag,
-                " to rank ", contextRank_, " (schedules disagree)");
+    GLX_ENFORCE(dev ? ic.devCredit != nullptr : ic.credit != nullptr, "rank ", ic.peer,
+                " has no send channel ", ic.tag, " to rank ", contextRank_,
+                " (schedules disagree)");
   }
   resolved_ = true;
 }
@@ -437,7 +481,7 @@ char* HipPlanExecutor::landing(const std::vector<ScratchBlock>& blocks, int64_t 
   return blk->ptr + at;
 }
 
-void HipPlanExecutor::allocScratch() {
+void HipPlanExecutor::allocScratch(bool uncached) {
   if (plan_.scratch_elems <= 0) return;
   // region starts = where messages land
   std::vector<int64_t> starts;
@@ -463,7 +507,11 @@ void HipPlanExecutor::allocScratch() {
   if (cur.elems > 0) blocks_.push_back(cur);
   for (auto& b : blocks_) {
     const size_t bytes = (size_t)b.elems * esize_ + 64;
-    GLX_HIP_CHECK(hipMalloc((void**)&b.ptr, bytes));
+    if (uncached) {
+      GLX_HIP_CHECK(hipExtMallocWithFlags((void**)&b.ptr, bytes, hipDeviceMallocUncached));
+    } else {
+      GLX_HIP_CHECK(hipMalloc((void**)&b.ptr, bytes));
+    }
     GLX_HIP_CHECK(hipMemset(b.ptr, 0, bytes));
   }
   GLX_HIP_CHECK(hipDeviceSynchronize());
@@ -997,6 +1045,14 @@ int initialMeshEngine() {
 
 std::atomic<int> g_mesh_engine{initialMeshEngine()};
 
+int initialStepsEngine() {
+  const char* e = std::getenv("GLOO_AMD_STEPS_ENGINE");
+  return (e != nullptr && std::strcmp(e, "host") == 0) ? HipPlanExecutor::kEngineSteps
+                                                       : HipPlanExecutor::kEngineDevSteps;
+}
+
+std::atomic<int> g_steps_engine{initialStepsEngine()};
+
 }  // namespace
 
 void HipPlanExecutor::setMeshEngine(int engine) {
@@ -1004,6 +1060,12 @@ void HipPlanExecutor::setMeshEngine(int engine) {
 }
 
 int HipPlanExecutor::meshEngine() { return g_mesh_engine.load(); }
+
+void HipPlanExecutor::setStepsEngine(int engine) {
+  g_steps_engine.store(engine == kEngineSteps ? kEngineSteps : kEngineDevSteps);
+}
+
+int HipPlanExecutor::stepsEngine() { return g_steps_engine.load(); }
 
 namespace {
 
@@ -1039,6 +1101,10 @@ int HipPlanExecutor::engineFor(const Context& ctx, int algo, int64_t count) {
   if (algo == glx::ALGO_RING_CHUNKED_MESH || algo == glx::ALGO_FN_RING_MESH) {
     return meshEngine();
   }
+  if (algo == glx::ALGO_RING_CHUNKED || algo == glx::ALGO_HALVING_DOUBLING ||
+      algo == glx::ALGO_FN_RING || algo == glx::ALGO_FN_BCUBE) {
+    return stepsEngine();
+  }
   return kEngineSteps;
 }
 
@@ -1061,8 +1127,10 @@ char* HipPlanExecutor::ddAlloc(size_t bytes) {
 void HipPlanExecutor::setupDevice() {
   if (engine_ == kEngineOneShot) {
     setupOneShot();
-  } else {
+  } else if (engine_ == kEngineTwoShot) {
     setupTwoShot();
+  } else {
+    setupDevSteps();
   }
   GLX_HIP_CHECK(hipHostMalloc((void**)&ddStatus_, sizeof(int),
                               hipHostMallocMapped | hipHostMallocCoherent));
@@ -1070,6 +1138,7 @@ void HipPlanExecutor::setupDevice() {
   GLX_HIP_CHECK(hipHostGetDevicePointer((void**)&ddStatusDev_, ddStatus_, 0));
   os_.status = ddStatusDev_;
   ts_.status = ddStatusDev_;
+  pk_.status = ddStatusDev_;
   GLX_HIP_CHECK(hipEventCreateWithFlags(&ddDone_, hipEventDisableTiming));
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) == hipSuccess &&
@@ -1083,8 +1152,8 @@ void HipPlanExecutor::setupDevice() {
 // resident capacity shared by the ranks on the busiest GPU is smaller (ranks
 // spin on each other's workgroups, so every grid must be resident at once).
 // Same inputs on every rank -> same grid.
-size_t HipPlanExecutor::maxSlices(bool twoShot) const {
-  const int cap = glx::device_engine_resident_blocks(twoShot, op_, dtype_);
+size_t HipPlanExecutor::maxSlices(int kernel) const {
+  const int cap = glx::device_engine_resident_blocks(kernel, op_, dtype_);
   const int share = context_->maxRanksPerDevice();
   size_t g = glx::kOsMaxSlices;
   if (cap > 0) g = std::min(g, (size_t)std::max(1, cap / std::max(1, share)));
@@ -1094,7 +1163,7 @@ size_t HipPlanExecutor::maxSlices(bool twoShot) const {
 void HipPlanExecutor::setupOneShot() {
   const int P = contextSize_;
   const glx::DeviceLayout d =
-      glx::oneShotLayout(plan_, contextRank_, P, count_, (int)esize_, (int64_t)maxSlices(false));
+      glx::oneShotLayout(plan_, contextRank_, P, count_, (int)esize_, (int64_t)maxSlices(0));
   glx::OneShotParams& p = os_;
   p.P = P;
   p.rank = contextRank_;
@@ -1117,7 +1186,7 @@ void HipPlanExecutor::setupOneShot() {
 void HipPlanExecutor::setupTwoShot() {
   const int P = contextSize_;
   const glx::DeviceLayout d =
-      glx::twoShotLayout(plan_, contextRank_, P, count_, (int)esize_, (int64_t)maxSlices(true));
+      glx::twoShotLayout(plan_, contextRank_, P, count_, (int)esize_, (int64_t)maxSlices(1));
   glx::TwoShotParams& p = ts_;
   p.P = P;
   p.rank = contextRank_;
@@ -1133,6 +1202,111 @@ void HipPlanExecutor::setupTwoShot() {
   char* flags = ddAlloc(2 * (size_t)P * (size_t)p.G * sizeof(uint64_t));
   p.flagAIn = reinterpret_cast<const uint64_t*>(flags);
   p.flagBIn = reinterpret_cast<const uint64_t*>(flags) + (size_t)P * (size_t)p.G;
+}
+
+// The plan kernel: segments from every rank's program (plan.cc syncTable),
+// G workgroups, flag rows [our in-channels' deliveries, then our
+// out-channels' credits][G] in one uncached block.
+void HipPlanExecutor::setupDevSteps() {
+  GLX_ENFORCE(sync_.outChans.size() == out_.size() && sync_.inChans.size() == in_.size(),
+              "plan kernel: channel tables disagree");
+  const size_t G = (size_t)pk_.G;
+  std::vector<glx::DevSegment> segs;
+  for (size_t k = 0; k + 1 < sync_.bounds.size(); k++) {
+    glx::DevSegment sg;
+    sg.off = sync_.bounds[k];
+    sg.len = sync_.bounds[k + 1] - sync_.bounds[k];
+    sg.slice = sync_.slice;  // one slice size for every segment (SyncTable::safe)
+    segs.push_back(sg);
+  }
+  if (segs.empty()) segs.push_back(glx::DevSegment{0, 0, (int64_t)(16 / esize_)});
+  GLX_HIP_CHECK(hipMalloc((void**)&devSegs_, segs.size() * sizeof(glx::DevSegment)));
+  GLX_HIP_CHECK(hipMemcpy(devSegs_, segs.data(), segs.size() * sizeof(glx::DevSegment),
+                          hipMemcpyHostToDevice));
+  pk_.segs = devSegs_;
+  for (size_t k = 0; k < in_.size(); k++) in_[k].deliveryWord = (uint32_t)k;
+  for (size_t k = 0; k < out_.size(); k++) out_[k].creditWord = (uint32_t)(in_.size() + k);
+  const size_t rows = std::max<size_t>(1, in_.size() + out_.size());
+  ddAlloc(rows * G * sizeof(uint64_t));
+}
+
+// After resolvePeers: the step table with every address the kernel needs.
+void HipPlanExecutor::buildDevSteps() {
+  const size_t G = (size_t)pk_.G;
+  uint64_t* rows = reinterpret_cast<uint64_t*>(ddBlocks_[0]);
+  // element i of a message for ptr0[off...] sits at landing + (i - off)*es
+  auto vbase = [&](char* at, int64_t off) {
+    return reinterpret_cast<char*>(reinterpret_cast<uintptr_t>(at) -
+                                   (uintptr_t)off * (uintptr_t)esize_);
+  };
+  std::vector<glx::DevStep> ds;
+  std::vector<const char*> fs;
+  for (size_t i = 0; i < plan_.steps.size(); i++) {
+    const glx::Step& s = plan_.steps[i];
+    const glx::StepSync& y = sync_.steps[i];
+    glx::DevStep d{};
+    d.kind = (int32_t)s.kind;
+    d.peer = (int32_t)s.peer;
+    d.seg0 = y.seg0;
+    d.seg1 = y.seg1;
+    d.seq = y.seq;
+    d.perRun = y.perRun;
+    switch (s.kind) {
+      case glx::SEND: {
+        GLX_ENFORCE(y.chan == stepChan_[i], "plan kernel: channel numbering disagrees");
+        const OutChan& oc = out_[(size_t)y.chan];
+        d.dst = s.len > 0 ? vbase(landing(peerBlocks_[oc.peer], s.dst_off, s.off), s.off)
+                          : nullptr;
+        d.flag = oc.devDelivery;
+        d.credit = rows + (size_t)oc.creditWord * G;
+        break;
+      }
+      case glx::RECV:
+      case glx::RELEASE: {
+        GLX_ENFORCE(y.chan == stepChan_[i], "plan kernel: channel numbering disagrees");
+        const InChan& ic = in_[(size_t)y.chan];
+        d.flag = s.kind == glx::RECV ? rows + (size_t)ic.deliveryWord * G : ic.devCredit;
+        break;
+      }
+      case glx::REDUCE:
+      case glx::COPY:
+        d.src = vbase(landing(blocks_, s.boff, s.off), s.off);
+        break;
+      case glx::FOLD: {
+        const auto& f = plan_.folds[(size_t)s.boff];
+        GLX_ENFORCE(f.size() <= (size_t)glx::kOsMaxRanks, "plan kernel: fold of ", f.size(),
+                    " sources");
+        d.nsrc = (int32_t)f.size();
+        d.left = (s.flags & glx::kFoldLeft) != 0 ? 1 : 0;
+        d.srcIndex = (int64_t)fs.size();
+        const bool whole = (s.flags & glx::kFoldWhole) != 0;
+        for (int64_t r : f) {
+          if (r < 0) {
+            fs.push_back(nullptr);
+          } else if (whole) {  // whole-buffer message: element i at landing(r, 0) + i*es
+            fs.push_back(landing(blocks_, r, 0));
+          } else {
+            fs.push_back(vbase(landing(blocks_, r, s.off), s.off));
+          }
+        }
+        break;
+      }
+      default:
+        GLX_ENFORCE(false, "bad plan step kind ", s.kind);
+    }
+    ds.push_back(d);
+  }
+  if (fs.empty()) fs.push_back(nullptr);
+  if (ds.empty()) ds.push_back(glx::DevStep{});  // never walked (nsteps = 0)
+  GLX_HIP_CHECK(hipMalloc((void**)&devSteps_, ds.size() * sizeof(glx::DevStep)));
+  GLX_HIP_CHECK(hipMemcpy(devSteps_, ds.data(), ds.size() * sizeof(glx::DevStep),
+                          hipMemcpyHostToDevice));
+  GLX_HIP_CHECK(hipMalloc((void**)&devFoldSrc_, fs.size() * sizeof(char*)));
+  GLX_HIP_CHECK(hipMemcpy(devFoldSrc_, fs.data(), fs.size() * sizeof(char*),
+                          hipMemcpyHostToDevice));
+  pk_.steps = devSteps_;
+  pk_.foldSrc = devFoldSrc_;
+  pk_.nsteps = (int)plan_.steps.size();
 }
 
 void HipPlanExecutor::checkDevice() {
@@ -1175,6 +1349,15 @@ void HipPlanExecutor::runDevice(char* ptr0) {
     GLX_TRACE("r%d one-shot epoch %lu (G=%d slice=%zu)", contextRank_, (unsigned long)e, p.G,
               p.slice);
     GLX_HIP_CHECK(glx::launch_oneshot(op_, dtype_, p, compute_));
+  } else if (engine_ == kEngineDevSteps) {
+    if (devSteps_ == nullptr) buildDevSteps();
+    glx::PlanKernelParams p = pk_;
+    p.buf = ptr0;
+    p.run = devRuns_++;
+    p.timeoutTicks = ticks;
+    GLX_TRACE("r%d plan kernel run %lu (G=%d, %d steps)", contextRank_, (unsigned long)p.run,
+              p.G, p.nsteps);
+    GLX_HIP_CHECK(glx::launch_plan_kernel(op_, dtype_, p, compute_));
   } else {
     glx::TwoShotParams p = ts_;
     p.buf = ptr0;

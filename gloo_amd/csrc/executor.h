@@ -90,7 +90,9 @@ class HipPlanExecutor : public Algorithm {
     std::atomic<uint64_t>* delivery = nullptr;  // in peer's block
     uint64_t sent = 0;
     int peerDevice = -1;
-    int stream = 0;     // index into copies_ (one copy stream per destination peer)
+    int stream = 0;
+    int peerRow = -1;                 // plan kernel: the receiver's delivery row
+    uint64_t* devDelivery = nullptr;  // plan kernel: that row (peer memory)     // index into copies_ (one copy stream per destination peer)
   };
   struct CopyStream {
     hipStream_t s = nullptr;
@@ -104,6 +106,8 @@ class HipPlanExecutor : public Algorithm {
     std::atomic<uint64_t>* delivery;  // our word, written by peer
     std::atomic<uint64_t>* credit = nullptr;  // in peer's block
     uint64_t received = 0, consumed = 0;
+    int peerRow = -1;               // plan kernel: the sender's credit row
+    uint64_t* devCredit = nullptr;  // plan kernel: that row (peer memory)
   };
   static constexpr int kMaxSplit = 8;
   struct Pending {  // fire `value` into `word` once all `ev` (maybe none) complete
@@ -140,7 +144,7 @@ class HipPlanExecutor : public Algorithm {
     return timeout_.count() > 0 ? timeout_ : context_->getTimeout();
   }  // the plan's steps on ptr0 (contextSize_ > 1)
   void localReduce(const std::vector<void*>& in, const std::vector<void*>& out);
-  void allocScratch();
+  void allocScratch(bool uncached = false);
   void waitWar(int64_t off, int64_t len);
 
   glx::Plan plan_;
@@ -205,6 +209,15 @@ class HipPlanExecutor : public Algorithm {
   size_t ddSlot_ = 0;                         // bytes per landing slot
   glx::OneShotParams os_{};                   // fixed parts of the kernels' parameters
   glx::TwoShotParams ts_{};
+  // plan kernel (engine devsteps): step table, segments and fold sources in
+  // device memory, built at the first run (they hold peers' addresses)
+  glx::PlanKernelParams pk_{};
+  glx::PlanParams prm_;
+  glx::SyncTable sync_;
+  glx::DevStep* devSteps_ = nullptr;
+  glx::DevSegment* devSegs_ = nullptr;
+  const char** devFoldSrc_ = nullptr;
+  uint64_t devRuns_ = 0;
   uint64_t ddEpoch_ = 0;
   int* ddStatus_ = nullptr;  // pinned host word the kernels flag timeouts in
   int* ddStatusDev_ = nullptr;
@@ -214,14 +227,17 @@ class HipPlanExecutor : public Algorithm {
   static int engineFor(const Context& ctx, int algo, int64_t count);
   char* ddAlloc(size_t bytes);
   void setupDevice();
-  size_t maxSlices(bool twoShot) const;
+  size_t maxSlices(int kernel) const;
   void setupOneShot();
   void setupTwoShot();
+  void setupDevSteps();
+  void buildDevSteps();
   void runDevice(char* ptr0);
   void checkDevice();
 
  public:
-  static constexpr int kEngineSteps = 0, kEngineOneShot = 1, kEngineTwoShot = 2;
+  static constexpr int kEngineSteps = 0, kEngineOneShot = 1, kEngineTwoShot = 2,
+                       kEngineDevSteps = 3;
   // Whether device-driven engines can run on this context: GLOO_AMD_ONESHOT
   // (0 = never, 1 = always), by default when no two ranks are threads sharing
   // one device (their kernels might not be co-resident).  P <= 8.
@@ -234,6 +250,11 @@ class HipPlanExecutor : public Algorithm {
   // construction.
   static void setMeshEngine(int engine);
   static int meshEngine();
+  // Engine of the ring, halving-doubling, bcube and function-style ring
+  // schedules when available: kEngineDevSteps (the plan kernel, default;
+  // env GLOO_AMD_STEPS_ENGINE=host overrides) or kEngineSteps.
+  static void setStepsEngine(int engine);
+  static int stepsEngine();
 };
 
 }  // namespace gloo

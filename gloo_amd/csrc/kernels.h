@@ -41,7 +41,7 @@ int copy_blocks();
 // chunk along its ring chain.  All pointers are device-accessible; push/land
 // regions and flags are uncached device memory (peers' via IPC).
 constexpr int kOsMaxRanks = 8;
-constexpr int kOsMaxSlices = 256;  // workgroups (= slices) per launch
+constexpr int kOsMaxSlices = 512;  // workgroups (= slices) per launch
 struct OneShotParams {
   char* buf;                        // this rank's buffer: input and result
   char* push[kOsMaxRanks];          // this rank's landing region in peer j (j != rank)
@@ -82,10 +82,48 @@ struct TwoShotParams {
   int P, rank, G;
 };
 hipError_t launch_twoshot(int op, int dtype, const TwoShotParams& p, hipStream_t s);
-// Workgroups of the one-shot (twoShot = false) / two-shot kernel for (op,
-// dtype) that fit on the current device at once (occupancy x CUs).  A grid
-// of peers waiting on each other must be resident as a whole.
-int device_engine_resident_blocks(bool twoShot, int op, int dtype);
+// Plan kernel (xgmi_kernels.hip): ANY compiled schedule (a plan.h step
+// program) as one device-driven kernel per rank.  The buffer is cut into
+// segments at every step boundary of every rank's program and every segment
+// into G slices; workgroup w owns slice w of every segment on every rank, so
+// each step gives every workgroup a share and an element is always handled
+// by the same workgroup index: workgroups of one rank never wait for each
+// other, workgroup w only for workgroup w of its peers.  Per (channel,
+// workgroup) flag rows carry the host executor's delivery / credit counts.
+struct DevSegment {
+  int64_t off, len, slice;  // slice: elements per workgroup, whole 16-byte vectors
+};
+struct DevStep {
+  int32_t kind;            // glx::StepKind
+  int32_t peer;            // reported on timeout
+  int32_t seg0, seg1;      // the step's element range = segments [seg0, seg1)
+  int32_t nsrc;            // FOLD: number of sources, first at foldSrc[srcIndex]
+  int32_t left;            // FOLD: 1 = left fold (plan.h kFoldLeft), 0 = the ring's chain
+  int64_t srcIndex;
+  const char* src;         // REDUCE / COPY: landing region as a virtual buffer
+  char* dst;               // SEND: the peer's landing region as a virtual buffer
+  uint64_t* flag;          // SEND: peer's delivery row; RECV: my delivery row;
+                           // RELEASE: peer's credit row
+  const uint64_t* credit;  // SEND: my credit row
+  uint64_t seq, perRun;    // message number within a run (1-based), messages per run
+};
+struct PlanKernelParams {
+  char* buf;
+  const DevStep* steps;        // device memory
+  const DevSegment* segs;      // device memory
+  const char* const* foldSrc;  // device memory; nullptr = buf
+  int nsteps, G;
+  uint64_t run;                // runs completed before this one
+  uint64_t timeoutTicks;
+  int* status;
+};
+hipError_t launch_plan_kernel(int op, int dtype, const PlanKernelParams& p, hipStream_t s);
+
+// Workgroups of a device-engine kernel (kernel 0 = one-shot, 1 = two-shot,
+// 2 = plan kernel) for (op, dtype) that fit on the current device at once
+// (occupancy x CUs).  A grid of peers waiting on each other must be
+// resident as a whole.
+int device_engine_resident_blocks(int kernel, int op, int dtype);
 
 // Tuning knobs of the vector kernel (lanes' unroll depth, grid cap per CU,
 // nontemporal loads/stores: 0/1, -1 = keep).

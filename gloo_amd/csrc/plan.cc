@@ -8,6 +8,7 @@
 #include "plan.h"
 
 #include <algorithm>
+#include <map>
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
@@ -740,6 +741,167 @@ Plan makePlan(int algo, int rank, int size, int64_t count, const PlanParams& prm
   }
   fail("unknown algorithm");
   return Plan();
+}
+
+// ---------------------------------------------------------------------------
+// The plan kernel's segments, channels and message numbers
+// ---------------------------------------------------------------------------
+namespace {
+
+bool dataStep(const Step& s) {
+  return (s.kind == SEND && s.len > 0) || s.kind == REDUCE || s.kind == COPY || s.kind == FOLD;
+}
+
+int chanOf(std::vector<std::pair<int, int>>& v, int peer, int tag) {
+  for (size_t i = 0; i < v.size(); i++) {
+    if (v[i].first == peer && v[i].second == tag) return (int)i;
+  }
+  v.emplace_back(peer, tag);
+  return (int)v.size() - 1;
+}
+
+// See SyncTable::safe.  Byte ownership of message [a, a+len) in its landing
+// region: element x sits at byte (a*es mod 16) + (x - a)*es and belongs to
+// workgroup w when it lies in slice w of its segment.
+bool regionsSafe(const std::vector<Plan>& all, const std::vector<int64_t>& bounds, int64_t sl,
+                 int G, int es) {
+  struct Iv {
+    int64_t b0, b1;
+    int w;
+  };
+  auto owners = [&](int64_t a, int64_t len) {
+    std::vector<Iv> v;
+    const int64_t ph = (a * es) % 16;
+    auto it = std::upper_bound(bounds.begin(), bounds.end(), a) - 1;
+    for (; it + 1 != bounds.end() && *it < a + len; ++it) {
+      const int64_t s0 = *it, s1 = *(it + 1);
+      for (int w = 0; w < G; w++) {
+        const int64_t x = std::max(a, s0 + (int64_t)w * sl);
+        const int64_t y = std::min(std::min(a + len, s1), s0 + (int64_t)(w + 1) * sl);
+        if (x < y) v.push_back({ph + (x - a) * es, ph + (y - a) * es, w});
+      }
+    }
+    std::sort(v.begin(), v.end(), [](const Iv& p, const Iv& q) { return p.b0 < q.b0; });
+    return v;
+  };
+  auto agree = [](const std::vector<Iv>& m, const std::vector<Iv>& n) {
+    size_t i = 0, j = 0;
+    while (i < m.size() && j < n.size()) {
+      const int64_t lo = std::max(m[i].b0, n[j].b0), hi = std::min(m[i].b1, n[j].b1);
+      if (lo < hi && m[i].w != n[j].w) return false;
+      if (m[i].b1 < n[j].b1) {
+        i++;
+      } else {
+        j++;
+      }
+    }
+    return true;
+  };
+  const int size = (int)all.size();
+  for (int q = 0; q < size; q++) {
+    // the messages landing in each of q's regions: the k-th RECV of (p, tag)
+    // is the k-th SEND of p to q on tag
+    std::map<int64_t, std::vector<std::pair<int64_t, int64_t>>> byRegion;
+    std::map<std::pair<int, int>, int> nrecv;
+    for (const auto& s : all[(size_t)q].steps) {
+      if (s.kind != RECV) continue;
+      const int p = (int)s.peer, tag = (int)s.channel;
+      const int k = nrecv[{p, tag}]++;
+      const Step* snd = nullptr;
+      int seen = 0;
+      for (const auto& u : all[(size_t)p].steps) {
+        if (u.kind == SEND && u.peer == q && u.channel == tag && seen++ == k) {
+          snd = &u;
+          break;
+        }
+      }
+      if (snd == nullptr) return false;  // programs disagree: never run the kernel on them
+      if (snd->len == 0) continue;
+      auto& v = byRegion[s.boff];
+      const std::pair<int64_t, int64_t> m{snd->off, snd->len};
+      if (std::find(v.begin(), v.end(), m) == v.end()) v.push_back(m);
+    }
+    for (const auto& kv : byRegion) {
+      const auto& ms = kv.second;
+      std::vector<std::vector<Iv>> own;
+      for (const auto& m : ms) own.push_back(owners(m.first, m.second));
+      for (size_t i = 0; i < ms.size(); i++) {
+        for (size_t j = i + 1; j < ms.size(); j++) {
+          if (!agree(own[i], own[j])) return false;
+        }
+      }
+    }
+  }
+  return true;
+}
+
+}  // namespace
+
+SyncTable syncTable(int algo, int rank, int size, int64_t count, const PlanParams& prm,
+                    int G) {
+  SyncTable t;
+  t.bounds = {0, count};
+  Plan mine;
+  std::vector<Plan> all;
+  for (int q = 0; q < size; q++) {
+    Plan p = makePlan(algo, q, size, count, prm);
+    for (const auto& s : p.steps) {
+      if (!dataStep(s)) continue;
+      if (s.off < 0 || s.off + s.len > count) fail("sync table: step range outside the buffer");
+      t.bounds.push_back(s.off);
+      t.bounds.push_back(s.off + s.len);
+    }
+    if (q == rank) mine = p;
+    all.push_back(std::move(p));
+  }
+  std::sort(t.bounds.begin(), t.bounds.end());
+  t.bounds.erase(std::unique(t.bounds.begin(), t.bounds.end()), t.bounds.end());
+  if (G < 1) fail("sync table: G must be >= 1");
+  const int64_t V = 16 / std::max(1, prm.esize);
+  int64_t maxSeg = 1;
+  for (size_t k = 0; k + 1 < t.bounds.size(); k++) {
+    maxSeg = std::max(maxSeg, t.bounds[k + 1] - t.bounds[k]);
+  }
+  t.slice = ((maxSeg + G - 1) / G + V - 1) / V * V;
+  t.safe = regionsSafe(all, t.bounds, t.slice, G, prm.esize);
+  auto segIndex = [&](int64_t x) {
+    auto it = std::lower_bound(t.bounds.begin(), t.bounds.end(), x);
+    if (it == t.bounds.end() || *it != x) fail("sync table: not a segment bound");
+    return (int32_t)(it - t.bounds.begin());
+  };
+  std::vector<uint64_t> sent, recvd, released;
+  t.steps.resize(mine.steps.size());
+  for (size_t i = 0; i < mine.steps.size(); i++) {
+    const Step& s = mine.steps[i];
+    StepSync& y = t.steps[i];
+    if (s.kind == SEND) {
+      y.chan = chanOf(t.outChans, (int)s.peer, (int)s.channel);
+      sent.resize(t.outChans.size());
+      y.seq = ++sent[(size_t)y.chan];
+    } else if (s.kind == RECV) {
+      y.chan = chanOf(t.inChans, (int)s.peer, (int)s.channel);
+      recvd.resize(t.inChans.size());
+      y.seq = ++recvd[(size_t)y.chan];
+    } else if (s.kind == RELEASE) {
+      y.chan = chanOf(t.inChans, (int)s.peer, (int)s.channel);
+      released.resize(t.inChans.size());
+      y.seq = ++released[(size_t)y.chan];
+    }
+    if (dataStep(s)) {
+      y.seg0 = segIndex(s.off);
+      y.seg1 = segIndex(s.off + s.len);
+    }
+  }
+  recvd.resize(t.inChans.size());
+  released.resize(t.inChans.size());
+  if (recvd != released) fail("sync table: RECV and RELEASE counts differ");
+  for (size_t i = 0; i < mine.steps.size(); i++) {
+    const Step& s = mine.steps[i];
+    StepSync& y = t.steps[i];
+    if (s.kind == SEND) y.perRun = sent[(size_t)y.chan];
+    if (s.kind == RECV || s.kind == RELEASE) y.perRun = recvd[(size_t)y.chan];
+  }
+  return t;
 }
 
 // ---------------------------------------------------------------------------

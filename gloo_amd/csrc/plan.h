@@ -27,6 +27,7 @@
 #pragma once
 
 #include <cstdint>
+#include <utility>
 #include <vector>
 
 namespace glx {
@@ -147,6 +148,35 @@ DeviceLayout oneShotLayout(const Plan& plan, int rank, int size, int64_t count, 
                            int64_t maxSlices);
 DeviceLayout twoShotLayout(const Plan& plan, int rank, int size, int64_t count, int esize,
                            int64_t maxSlices);
+
+// The plan kernel's bookkeeping for one rank's program: segment bounds (0,
+// count and both ends of every data step of EVERY rank's program, so all
+// ranks cut alike and every step range is a union of segments), the slice
+// (every segment is cut into G slices of this many elements, a whole number
+// of 16-byte vectors; workgroup w owns slice w of every segment), and per
+// step its channel (out-channel index for SEND, in-channel index for RECV /
+// RELEASE, numbered by first use -- the executor's numbering), its segments
+// and its message number within a run (1-based) out of perRun.
+//
+// safe: the kernel's credits are per (channel, workgroup), so a landing
+// region is protected only if every two messages landing in it give every
+// byte they both cover to the same workgroup (a workgroup may run several
+// messages ahead of another).  Checked over every region of every rank;
+// when it fails the executor keeps the host-issued steps.
+struct StepSync {
+  int32_t chan = -1;
+  int32_t seg0 = 0, seg1 = 0;
+  uint64_t seq = 0, perRun = 0;
+};
+struct SyncTable {
+  std::vector<int64_t> bounds;
+  int64_t slice = 0;
+  bool safe = true;
+  std::vector<std::pair<int, int>> outChans, inChans;  // (peer, tag)
+  std::vector<StepSync> steps;
+};
+SyncTable syncTable(int algo, int rank, int size, int64_t count, const PlanParams& prm,
+                    int G);
 
 // Host-memory endpoints: when the user's buffer is in host
 // memory the executor stages it through a device buffer.  This derives from

@@ -128,9 +128,11 @@ __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* 
   }
 }
 
-// [a, b) of dst = chain fold of srcs[0..P-1]: acc = s0; acc = op(s_k, acc).
+// [a, b) of dst = fold of srcs[0..P-1]: acc = s0, then acc = op(s_k, acc)
+// (the ring's chain: the newer rank's value is the in-place destination)
+// or, LEFT, acc = op(acc, s_k) (a left fold, out = op(out, peer)).
 // The result also goes to every outs[d], d < nout.
-template <typename T, int OP>
+template <typename T, int OP, bool LEFT = false>
 __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
                                           const typename Elem<T, OP>::S* const* srcs, int P,
                                           char* const* outs, int nout, size_t a, size_t b,
@@ -149,7 +151,7 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
     S acc = y[0];
 #pragma unroll
     for (int k = 1; k < kOsMaxRanks; k++) {
-      if (k < P) acc = E::apply(y[k], acc);
+      if (k < P) acc = LEFT ? E::apply(acc, y[k]) : E::apply(y[k], acc);
     }
     dst[i] = acc;
 #pragma unroll
@@ -173,8 +175,8 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
 #pragma unroll
     for (int k = 1; k < kOsMaxRanks; k++) {
       if (k < P) {
-        acc = vec_apply<T, OP>(y[k], acc);
-        acc2 = vec_apply<T, OP>(z[k], acc2);
+        acc = LEFT ? vec_apply<T, OP>(acc, y[k]) : vec_apply<T, OP>(y[k], acc);
+        acc2 = LEFT ? vec_apply<T, OP>(acc2, z[k]) : vec_apply<T, OP>(z[k], acc2);
       }
     }
     reinterpret_cast<v4u*>(dst)[v] = acc;
@@ -196,7 +198,7 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
     v4u acc = y[0];
 #pragma unroll
     for (int k = 1; k < kOsMaxRanks; k++) {
-      if (k < P) acc = vec_apply<T, OP>(y[k], acc);
+      if (k < P) acc = LEFT ? vec_apply<T, OP>(acc, y[k]) : vec_apply<T, OP>(y[k], acc);
     }
     reinterpret_cast<v4u*>(dst)[v] = acc;
 #pragma unroll
@@ -219,11 +221,21 @@ __device__ __forceinline__ void release_flags(uint64_t* const* rows, int P, int 
   }
 }
 
+// Every wave's stores complete and visible system-wide, then lane 0 stores
+// `value` into `word` (a flag in a peer's memory).
+__device__ __forceinline__ void signal_flag(uint64_t* word, uint64_t value) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(word, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // Lane 0 waits until word >= epoch (bounded); the whole workgroup learns
 // the outcome.  Returns false after a timeout (status already set).
 __device__ __forceinline__ bool wait_flag(const uint64_t* word, uint64_t epoch, int peer,
                                           uint64_t start, uint64_t timeoutTicks, int* status,
-                                          int* s_ok) {
+                                          int* s_ok, bool acquire = true) {
   if (threadIdx.x == 0) {
     int ok = 1;
     while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
@@ -235,7 +247,7 @@ __device__ __forceinline__ bool wait_flag(const uint64_t* word, uint64_t epoch, 
       __builtin_amdgcn_s_sleep(2);
     }
     // drop any stale copy of the landing lines before anyone reads them
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (acquire) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     *s_ok = ok;
   }
   __syncthreads();
@@ -365,6 +377,90 @@ __global__ __launch_bounds__(kBlock, 2) void twoshot_kernel(TwoShotParams p) {
   }
 }
 
+// ---- plan kernel --------------------------------------------------------------
+
+// Workgroup w's part [a, b) of a segment.
+__device__ __forceinline__ bool seg_part(const DevSegment& sg, int w, size_t& a, size_t& b) {
+  const size_t off = (size_t)sg.off, len = (size_t)sg.len, sl = (size_t)sg.slice;
+  const size_t s0 = (size_t)w * sl;
+  a = off + (s0 < len ? s0 : len);
+  b = off + (s0 + sl < len ? s0 + sl : len);
+  return a < b;
+}
+
+template <typename T, int OP>
+__global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
+  using S = typename Elem<T, OP>::S;
+  __shared__ int s_ok;
+  const int w = blockIdx.x;
+  S* buf = reinterpret_cast<S*>(p.buf);
+  const bool aligned = ((uintptr_t)p.buf % 16) == 0;
+  for (int i = 0; i < p.nsteps; i++) {
+    const DevStep st = p.steps[i];
+    const uint64_t seq = p.run * st.perRun + st.seq;
+    switch (st.kind) {
+      case 0: {  // SEND, once the receiver has consumed message seq-1 of this slice
+        if (seq > 1 && !wait_flag(st.credit + w, seq - 1, st.peer,
+                                  __builtin_amdgcn_s_memrealtime(), p.timeoutTicks, p.status,
+                                  &s_ok, /*acquire=*/false)) {
+          return;
+        }
+        for (int g = st.seg0; g < st.seg1; g++) {
+          size_t a, b;
+          if (seg_part(p.segs[g], w, a, b)) {
+            copy_span<S>(reinterpret_cast<S*>(st.dst), buf, a, b, aligned);
+          }
+        }
+        signal_flag(st.flag + w, seq);
+        break;
+      }
+      case 1:  // RECV
+        if (!wait_flag(st.flag + w, seq, st.peer, __builtin_amdgcn_s_memrealtime(),
+                       p.timeoutTicks, p.status, &s_ok)) {
+          return;
+        }
+        break;
+      case 2:    // REDUCE: buf = op(buf, region), in place
+      case 3:    // COPY:   buf = region
+      case 5: {  // FOLD
+        const S* srcs[kOsMaxRanks];
+#pragma unroll
+        for (int k = 0; k < kOsMaxRanks; k++) srcs[k] = buf;
+        int n = 2;
+        if (st.kind == 5) {
+          n = st.nsrc;
+          for (int k = 0; k < n && k < kOsMaxRanks; k++) {
+            const char* q = p.foldSrc[st.srcIndex + k];
+            if (q != nullptr) srcs[k] = reinterpret_cast<const S*>(q);
+          }
+        } else {
+          srcs[1] = reinterpret_cast<const S*>(st.src);
+        }
+        for (int g = st.seg0; g < st.seg1; g++) {
+          size_t a, b;
+          if (!seg_part(p.segs[g], w, a, b)) continue;
+          if (st.kind == 3) {
+            copy_span<S>(buf, srcs[1], a, b, aligned);
+          } else if (st.kind == 2 || st.left) {
+            fold_span<T, OP, true>(buf, srcs, n, nullptr, 0, a, b, aligned);
+          } else {
+            fold_span<T, OP, false>(buf, srcs, n, nullptr, 0, a, b, aligned);
+          }
+        }
+        break;
+      }
+      case 4:  // RELEASE: every wave is done reading the region
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          __hip_atomic_store(st.flag + w, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        break;
+      default:
+        break;
+    }
+  }
+}
+
 // ---- launch -------------------------------------------------------------------
 
 template <typename T>
@@ -397,23 +493,21 @@ hipError_t launch_ts_op(int op, const TwoShotParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <typename T, int OP>
+const void* engine_kernel(int kernel) {
+  if (kernel == 0) return (const void*)oneshot_kernel<T, OP>;
+  if (kernel == 1) return (const void*)twoshot_kernel<T, OP>;
+  return (const void*)plan_kernel<T, OP>;
+}
+
 template <typename T>
-int resident_typed(bool twoShot, int op) {
+int resident_typed(int kernel, int op) {
   const void* k = nullptr;
   switch (op) {
-    case GLX_SUM:
-      k = twoShot ? (const void*)twoshot_kernel<T, GLX_SUM> : (const void*)oneshot_kernel<T, GLX_SUM>;
-      break;
-    case GLX_PRODUCT:
-      k = twoShot ? (const void*)twoshot_kernel<T, GLX_PRODUCT>
-                  : (const void*)oneshot_kernel<T, GLX_PRODUCT>;
-      break;
-    case GLX_MAX:
-      k = twoShot ? (const void*)twoshot_kernel<T, GLX_MAX> : (const void*)oneshot_kernel<T, GLX_MAX>;
-      break;
-    case GLX_MIN:
-      k = twoShot ? (const void*)twoshot_kernel<T, GLX_MIN> : (const void*)oneshot_kernel<T, GLX_MIN>;
-      break;
+    case GLX_SUM: k = engine_kernel<T, GLX_SUM>(kernel); break;
+    case GLX_PRODUCT: k = engine_kernel<T, GLX_PRODUCT>(kernel); break;
+    case GLX_MAX: k = engine_kernel<T, GLX_MAX>(kernel); break;
+    case GLX_MIN: k = engine_kernel<T, GLX_MIN>(kernel); break;
     default: return 0;
   }
   int perCu = 0, dev = 0, cus = 0;
@@ -426,19 +520,34 @@ int resident_typed(bool twoShot, int op) {
   return perCu * cus;
 }
 
+template <typename T>
+hipError_t launch_pk_op(int op, const PlanKernelParams& p, hipStream_t s) {
+  const dim3 grid((unsigned)p.G), block(kBlock);
+  switch (op) {
+    case GLX_SUM: hipLaunchKernelGGL((plan_kernel<T, GLX_SUM>), grid, block, 0, s, p); break;
+    case GLX_PRODUCT:
+      hipLaunchKernelGGL((plan_kernel<T, GLX_PRODUCT>), grid, block, 0, s, p);
+      break;
+    case GLX_MAX: hipLaunchKernelGGL((plan_kernel<T, GLX_MAX>), grid, block, 0, s, p); break;
+    case GLX_MIN: hipLaunchKernelGGL((plan_kernel<T, GLX_MIN>), grid, block, 0, s, p); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 }  // namespace
 
-int device_engine_resident_blocks(bool twoShot, int op, int dtype) {
+int device_engine_resident_blocks(int kernel, int op, int dtype) {
   switch (dtype) {
-    case GLX_INT8: return resident_typed<int8_t>(twoShot, op);
-    case GLX_UINT8: return resident_typed<uint8_t>(twoShot, op);
-    case GLX_INT32: return resident_typed<int32_t>(twoShot, op);
-    case GLX_INT64: return resident_typed<int64_t>(twoShot, op);
-    case GLX_UINT64: return resident_typed<uint64_t>(twoShot, op);
-    case GLX_FLOAT32: return resident_typed<float>(twoShot, op);
-    case GLX_FLOAT64: return resident_typed<double>(twoShot, op);
-    case GLX_FLOAT16: return resident_typed<f16_t>(twoShot, op);
-    case GLX_BFLOAT16: return resident_typed<bf16_t>(twoShot, op);
+    case GLX_INT8: return resident_typed<int8_t>(kernel, op);
+    case GLX_UINT8: return resident_typed<uint8_t>(kernel, op);
+    case GLX_INT32: return resident_typed<int32_t>(kernel, op);
+    case GLX_INT64: return resident_typed<int64_t>(kernel, op);
+    case GLX_UINT64: return resident_typed<uint64_t>(kernel, op);
+    case GLX_FLOAT32: return resident_typed<float>(kernel, op);
+    case GLX_FLOAT64: return resident_typed<double>(kernel, op);
+    case GLX_FLOAT16: return resident_typed<f16_t>(kernel, op);
+    case GLX_BFLOAT16: return resident_typed<bf16_t>(kernel, op);
   }
   return 0;
 }
@@ -459,6 +568,25 @@ hipError_t launch_oneshot(int op, int dtype, const OneShotParams& p, hipStream_t
     case GLX_FLOAT64: return launch_os_op<double>(op, p, s);
     case GLX_FLOAT16: return launch_os_op<f16_t>(op, p, s);
     case GLX_BFLOAT16: return launch_os_op<bf16_t>(op, p, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_plan_kernel(int op, int dtype, const PlanKernelParams& p, hipStream_t s) {
+  if (p.G < 1 || p.G > kOsMaxSlices || p.nsteps < 0 || p.steps == nullptr ||
+      p.segs == nullptr || p.foldSrc == nullptr) {
+    return hipErrorInvalidValue;
+  }
+  switch (dtype) {
+    case GLX_INT8: return launch_pk_op<int8_t>(op, p, s);
+    case GLX_UINT8: return launch_pk_op<uint8_t>(op, p, s);
+    case GLX_INT32: return launch_pk_op<int32_t>(op, p, s);
+    case GLX_INT64: return launch_pk_op<int64_t>(op, p, s);
+    case GLX_UINT64: return launch_pk_op<uint64_t>(op, p, s);
+    case GLX_FLOAT32: return launch_pk_op<float>(op, p, s);
+    case GLX_FLOAT64: return launch_pk_op<double>(op, p, s);
+    case GLX_FLOAT16: return launch_pk_op<f16_t>(op, p, s);
+    case GLX_BFLOAT16: return launch_pk_op<bf16_t>(op, p, s);
   }
   return hipErrorInvalidValue;
 }

@@ -218,7 +218,7 @@ class DeviceAllreduce : public Algorithm {
   ~DeviceAllreduce() override { glx_algorithm_destroy(a_); }
   void run() override { check(glx_algorithm_run(a_), "run"); }
   int64_t bytesSentPerRun() const { return glx_algorithm_bytes_sent(a_); }
-  // GLX_ENGINE_STEPS / GLX_ENGINE_ONESHOT / GLX_ENGINE_TWOSHOT (glx.h)
+  // GLX_ENGINE_STEPS / _ONESHOT / _TWOSHOT / _DEVSTEPS (glx.h)
   int engine() const { return glx_algorithm_engine(a_); }
 
  private:
@@ -243,6 +243,9 @@ enum class Schedule { RING, MESH, REPLICATED, AUTO };
 inline void setDeviceEngines(int mode) { check(glx_set_device_engines(mode), "setDeviceEngines"); }
 // GLX_ENGINE_TWOSHOT (default) or GLX_ENGINE_STEPS for the MESH schedule.
 inline void setMeshEngine(int engine) { check(glx_set_mesh_engine(engine), "setMeshEngine"); }
+// GLX_ENGINE_DEVSTEPS (default) or GLX_ENGINE_STEPS for RING, halving-doubling,
+// bcube and the function-style ring.
+inline void setStepsEngine(int engine) { check(glx_set_steps_engine(engine), "setStepsEngine"); }
 
 namespace detail {
 inline glx_algorithm* createRing(glx_context* c, void* const* p, int n, int count, int dt,

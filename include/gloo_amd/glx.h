@@ -124,6 +124,11 @@ int glx_set_mesh_engine(int engine);
  * ranks' kernels can run concurrently), -1 = automatic (default: when no two
  * ranks are threads sharing one device).  Env GLOO_AMD_ONESHOT=0/1. */
 int glx_set_device_engines(int mode);
+/* Engine of the ring, halving-doubling, bcube and function-style ring
+ * schedules for algorithms created afterwards, when device-driven engines
+ * are available: GLX_ENGINE_DEVSTEPS (the plan kernel, default) or
+ * GLX_ENGINE_STEPS (host-issued steps).  Env GLOO_AMD_STEPS_ENGINE=host. */
+int glx_set_steps_engine(int engine);
 
 /* Number of visible HIP devices (0 when no GPU). */
 int glx_device_count(int* count);
@@ -283,6 +288,10 @@ int64_t glx_algorithm_bytes_sent(glx_algorithm* alg);
 #define GLX_ENGINE_STEPS 0
 #define GLX_ENGINE_ONESHOT 1
 #define GLX_ENGINE_TWOSHOT 2
+/* GLX_ENGINE_DEVSTEPS = any other schedule (ring, halving-doubling, bcube,
+ * function-style ring) run as ONE device-driven kernel per rank that walks
+ * the schedule's step program (the plan kernel). */
+#define GLX_ENGINE_DEVSTEPS 3
 int glx_algorithm_engine(glx_algorithm* alg);
 void glx_algorithm_destroy(glx_algorithm* alg);
 
@@ -302,6 +311,18 @@ int64_t glx_plan(int algo, int rank, int size, int64_t count, int64_t* steps,
  * resident capacity per rank). */
 int64_t glx_device_layout(int algo, int rank, int size, int64_t count, int esize,
                           int64_t max_slices, int64_t* out, int64_t cap);
+/* The plan kernel's bookkeeping for one rank's step program with G
+ * workgroups (host logic): segment bounds (written to bounds, *nbounds =
+ * their number), info = {slice, safe} (elements per workgroup slice; 1 if
+ * no landing region is shared by two workgroups across messages, else the
+ * executor keeps host-issued steps), and per step 5 int64 {channel, seg0,
+ * seg1, seq, perRun} (channel = out-channel index for SEND, in-channel index
+ * for RECV/RELEASE, -1 otherwise; seq = message number within a run,
+ * 1-based).  Returns the number of steps or -1. */
+int64_t glx_plan_sync(int algo, int rank, int size, int64_t count, int esize,
+                      int64_t max_segment_bytes, int64_t min_piece_bytes, int G,
+                      int64_t* bounds, int64_t bounds_cap, int64_t* nbounds, int64_t* info,
+                      int64_t* steps, int64_t cap);
 /* Sources of FOLD step number `fold` (its boff field): region offsets, -1 =
  * the rank's own buffer.  Returns the count (writes at most cap) or -1. */
 int64_t glx_plan_fold(int algo, int rank, int size, int64_t count, int64_t fold,

@@ -8,6 +8,10 @@ algo: ring_chunked | halving_doubling | ring_chunked_mesh (class algorithms)
       oneshot | twoshot (the replicated / mesh schedule as one device-driven
       kernel per rank: class and function style, dtypes x ops x sizes,
       device and host buffers, repeated runs; prints per-op latencies)
+      devsteps (ring_chunked, halving_doubling, function-style ring and bcube
+      through the plan kernel: dtypes x ops x sizes, device and host buffers,
+      repeated runs; prints per-op latencies of the plan kernel vs the
+      host-issued steps)
       devtimeout (rank 0 runs both device engines while the other ranks never
       call run(): its kernels must give up after the timeout and run() must
       raise IoException)
@@ -35,6 +39,8 @@ def main():
         return run_device(store_dir, rank, size, algo)
     if algo == "devtimeout":
         return run_device_timeout(store_dir, rank, size)
+    if algo == "devsteps":
+        return run_devsteps(store_dir, rank, size)
     if algo.startswith("fn_"):
         return run_fn(store_dir, rank, size, algo, N)
     code = O.HALVING_DOUBLING if algo == "halving_doubling" else O.RING_CHUNKED
@@ -146,6 +152,117 @@ def run_device_timeout(store_dir, rank, size):
     ctx.close()
     if not ok:
         print("MISMATCH rank", rank)
+        sys.exit(1)
+    print("OK")
+
+
+def run_devsteps(store_dir, rank, size):
+    import time
+
+    import numpy as np
+    import torch
+
+    import gloo_amd
+    from helpers import case_inputs
+    from oracle import oracle as O
+    from test_reduce_gpu import from_dev, to_dev
+
+    store = gloo_amd.rendezvous.FileStore(store_dir)
+    ctx = gloo_amd.rendezvous.Context(rank, size, 0)
+    ctx.setTimeout(20)
+    ctx.connectFullMesh(store)
+    bad = []
+
+    def same(got, exp):
+        return np.array_equal(np.ascontiguousarray(got).view(np.uint8),
+                              np.ascontiguousarray(exp).view(np.uint8))
+
+    def make(kind, buf, op=O.SUM, dt=None):
+        fn = gloo_amd.ReductionFunction(op)
+        if kind == O.HALVING_DOUBLING:
+            return gloo_amd.AllreduceHalvingDoubling(ctx, [buf], fn=fn, dtype=dt)
+        return gloo_amd.AllreduceRingChunked(ctx, [buf], fn=fn, schedule="ring", dtype=dt)
+
+    cases = []
+    for kind in (O.RING_CHUNKED, O.HALVING_DOUBLING):
+        for n in (1, 3, 255, 256, 1000, 4099, 65539, 1 << 20, (1 << 22) + 5):
+            cases.append((kind, n, O.FLOAT32, O.SUM))
+        for dt in (O.FLOAT16, O.INT32, O.FLOAT64, O.INT8, O.UINT64):
+            for op in (O.SUM, O.PRODUCT, O.MAX, O.MIN):
+                cases.append((kind, 4099, dt, op))
+    engines = set()
+    for seed, (kind, n, dt, op) in enumerate(cases):
+        ins = case_inputs(size, n, dt, 1, 0, seed=200 + seed)
+        exp = O.allreduce(kind, op, dt, ins)[rank][0]
+        buf = to_dev(ins[rank][0], dt)
+        alg = make(kind, buf, op, dt)
+        # the plan kernel, or host-issued steps where a landing region would
+        # be shared across workgroups (glx_plan_sync "safe")
+        engines.add(alg.engine())
+        if alg.engine() not in ("devsteps", "steps"):
+            bad.append(("engine", kind, n, alg.engine()))
+        for it in range(3):
+            buf.copy_(to_dev(ins[rank][0], dt))
+            torch.cuda.synchronize()
+            alg.run()
+            if not same(from_dev(buf, dt), exp):
+                bad.append(("class", kind, n, dt, op, it))
+        alg.close()
+    if "devsteps" not in engines:
+        bad.append(("engine", "the plan kernel never ran"))
+    n = 65536  # host buffers: staged H2D, kernel, D2H
+    ins = case_inputs(size, n, O.FLOAT32, 1, 0, seed=8)
+    for kind in (O.RING_CHUNKED, O.HALVING_DOUBLING):
+        exp = O.allreduce(kind, O.SUM, O.FLOAT32, ins)[rank][0]
+        host = ins[rank][0].copy()
+        alg = make(kind, host)
+        for it in range(2):
+            host[:] = ins[rank][0]
+            alg.run()
+            if not same(host, exp):
+                bad.append(("host", kind, it))
+        alg.close()
+    A = gloo_amd.AllreduceOptions.Algorithm
+    for algo, code in ((A.RING, O.FN_RING), (A.BCUBE, O.FN_BCUBE)):
+        for n in (1000, 65536, 1 << 20):
+            data = case_inputs(size, n, O.FLOAT32, 1, 0, seed=12)
+            exp = O.allreduce_fn(code, O.SUM, O.FLOAT32, [[] for _ in range(size)],
+                                 data)[rank][0]
+            for it in range(2):
+                out = torch.from_numpy(data[rank][0].copy()).cuda()
+                torch.cuda.synchronize()
+                opts = gloo_amd.AllreduceOptions(ctx)
+                opts.setAlgorithm(algo)
+                opts.setOutput(out)
+                opts.setReduceFunction(gloo_amd.ReductionFunction.sum)
+                gloo_amd.allreduce(opts)
+                if not same(out.cpu().numpy(), exp):
+                    bad.append(("fn", code, n, it))
+    # latency: the plan kernel vs the host-issued steps (same bits)
+    for kind, label in ((O.RING_CHUNKED, "ring"), (O.HALVING_DOUBLING, "hd")):
+        for n in (1024, 65536, 1 << 20, 3 << 22):
+            for eng in ("device", "host"):
+                gloo_amd.set_steps_engine(eng)
+                buf = torch.zeros(n, device="cuda")
+                torch.cuda.synchronize()
+                alg = make(kind, buf)
+                for _ in range(3):
+                    alg.run()
+                iters = 20 if n <= (1 << 20) else 5
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    alg.run()
+                us = (time.perf_counter() - t0) / iters * 1e6
+                print("LAT rank %d P %d %s elems %d engine %s us %.1f"
+                      % (rank, size, label, n, alg.engine(), us), flush=True)
+                alg.close()
+    gloo_amd.set_steps_engine("device")
+    store.set("done/%d" % rank, b"1")
+    for r in range(size):
+        store.get("done/%d" % r, timeout_ms=60000)
+    ctx.close()
+    if bad:
+        print("MISMATCH rank", rank, bad[:10])
         sys.exit(1)
     print("OK")
 

@@ -257,10 +257,11 @@ def test_multiprocess_ipc(algo):
             assert "OK" in outs[r]
 
 
-@pytest.mark.parametrize("mode", ["oneshot", "twoshot"])
-@pytest.mark.parametrize("P", [2, 4])
+@pytest.mark.parametrize("mode", ["oneshot", "twoshot", "devsteps"])
+@pytest.mark.parametrize("P", [2, 3, 4])
 def test_device_engine_multiprocess(P, mode):
-    """The replicated (one-shot) and mesh (two-shot) schedules as one
+    """The replicated (one-shot) and mesh (two-shot) schedules, and the ring,
+    halving-doubling and bcube step programs (plan kernel), as one
     device-driven kernel per rank (xgmi_kernels.hip), one process per rank:
     peers' kernels push into each other's IPC-mapped uncached regions and
     wait on flags.  Bit-exact with the reference ring's chains for every

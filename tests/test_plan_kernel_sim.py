@@ -1,0 +1,208 @@
+"""CPU: the plan kernel's protocol (xgmi_kernels.hip plan_kernel), simulated.
+
+Every (rank, workgroup) runs its rank's compiled step program on its slices
+of the segments, with the bookkeeping the executor hands the kernel
+(glx_plan_sync: segment bounds cut from every rank's program, one slice size,
+channel numbers, per-run message numbers), blocking exactly where the kernel
+blocks -- SEND on the channel's credit for its slice, RECV on the delivery --
+and signalling delivery / credit per slice.  A scheduler runs every
+(rank, workgroup) as far as it can before moving on (so workgroups drift
+apart, as they may on the GPU) for two runs, with the kernel boundary between
+runs per rank.  For every program glx_plan_sync calls safe it must finish
+without a stall, never overwrite a landing-region element another workgroup
+has not consumed yet, and reproduce the oracle bit for bit -- at every P up
+to 8, which the one-GPU boxes cannot run."""
+import numpy as np
+import pytest
+
+import gloo_amd
+from helpers import case_inputs, same_bits
+from oracle import oracle as O
+
+SEND, RECV, REDUCE, COPY, RELEASE, FOLD = range(6)
+FOLD_LEFT, FOLD_WHOLE = 1, 2
+
+
+class Clobber(Exception):
+    pass
+
+
+def simulate(name, P, N, G, op, ins, runs=2):
+    es = 4
+    progs = [gloo_amd.plan(name, r, P, N, with_folds=True) for r in range(P)]
+    syncs = [gloo_amd.plan_sync(name, r, P, N, G) for r in range(P)]
+    bounds, sl = syncs[0]["bounds"], syncs[0]["slice"]
+    assert all(s["bounds"] == bounds and s["slice"] == sl for s in syncs)
+    assert bounds[0] == 0 and bounds[-1] == N and bounds == sorted(set(bounds))
+    assert sl % (16 // es) == 0 and G * sl >= max(b - a for a, b in zip(bounds, bounds[1:]))
+
+    def parts(s0, s1, w):
+        for g in range(s0, s1):
+            lo, hi = bounds[g], bounds[g + 1]
+            a, b = min(lo + w * sl, hi), min(lo + (w + 1) * sl, hi)
+            if a < b:
+                yield a, b
+
+    out_ch, in_ch = [], []
+    for r in range(P):
+        oc, ic = {}, {}
+        for st, sy in zip(progs[r][0], syncs[r]["steps"]):
+            kind, peer, tag, off, ln = st[:5]
+            if kind == SEND:
+                assert oc.setdefault((peer, tag), len(oc)) == sy[0]
+            elif kind in (RECV, RELEASE):
+                assert ic.setdefault((peer, tag), len(ic)) == sy[0]
+            if kind in (REDUCE, COPY, FOLD) or (kind == SEND and ln > 0):
+                assert bounds[sy[1]] == off and bounds[sy[2]] == off + ln
+        out_ch.append(oc)
+        in_ch.append(ic)
+    bufs = [np.array(ins[r][0], copy=True) for r in range(P)]
+    # landing regions in element units; element x of a message for
+    # ptr0[a...] at region + (a mod 4) + (x - a), as the 16-byte landing rule
+    size = [progs[r][1] + N + 64 for r in range(P)]
+    scratch = [np.zeros(size[r], dtype=np.float32) for r in range(P)]
+    pending = [np.zeros(size[r], dtype=bool) for r in range(P)]  # written, not yet read
+    delivery = [[[0] * G for _ in in_ch[r]] for r in range(P)]
+    credit = [[[0] * G for _ in out_ch[r]] for r in range(P)]
+    pc = [[0] * G for _ in range(P)]
+    run = [[0] * G for _ in range(P)]
+
+    def pos(base, a, x):
+        return base + a % 4 + (x - a)
+
+    def read(r, base, a, lo, hi):
+        i, j = pos(base, a, lo), pos(base, a, hi)
+        pending[r][i:j] = False
+        return np.array(scratch[r][i:j])
+
+    def step(r, w):
+        """Advance (r, w) by one step; False if it is blocked or finished."""
+        if run[r][w] >= runs:
+            return False
+        steps = progs[r][0]
+        if pc[r][w] == len(steps):  # kernel boundary: the whole grid of r is done
+            if all(pc[r][x] == len(steps) and run[r][x] == run[r][w] for x in range(G)):
+                for x in range(G):
+                    pc[r][x] = 0
+                    run[r][x] += 1
+                return True
+            return False
+        i = pc[r][w]
+        kind, peer, tag, off, ln, boff, dst_off, flags = steps[i]
+        chan, s0, s1, seq, per = syncs[r]["steps"][i]
+        s = run[r][w] * per + seq
+        if kind == SEND:
+            if credit[r][chan][w] < s - 1:
+                return False
+            for a, b in parts(s0, s1, w):
+                p0, p1 = pos(dst_off, off, a), pos(dst_off, off, b)
+                if pending[peer][p0:p1].any():
+                    raise Clobber("rank %d wg %d overwrote unread data of rank %d" % (r, w, peer))
+                scratch[peer][p0:p1] = bufs[r][a:b]
+                pending[peer][p0:p1] = True
+            delivery[peer][in_ch[peer][(r, tag)]][w] = s
+        elif kind == RECV:
+            if delivery[r][chan][w] < s:
+                return False
+        elif kind == REDUCE:
+            for a, b in parts(s0, s1, w):
+                bufs[r][a:b] = O.reduce(op, O.FLOAT32, bufs[r][a:b], read(r, boff, off, a, b))
+        elif kind == COPY:
+            for a, b in parts(s0, s1, w):
+                bufs[r][a:b] = read(r, boff, off, a, b)
+        elif kind == FOLD:
+            for a, b in parts(s0, s1, w):
+                vals = []
+                for q in progs[r][2][boff]:
+                    if q < 0:
+                        vals.append(np.array(bufs[r][a:b]))
+                    elif flags & FOLD_WHOLE:
+                        vals.append(read(r, q, 0, a, b))
+                    else:
+                        vals.append(read(r, q, off, a, b))
+                acc = vals[0]
+                for v in vals[1:]:
+                    acc = (O.reduce(op, O.FLOAT32, acc, v) if flags & FOLD_LEFT
+                           else O.reduce(op, O.FLOAT32, v, acc))
+                bufs[r][a:b] = acc
+        elif kind == RELEASE:
+            credit[peer][out_ch[peer][(r, tag)]][w] = s
+        pc[r][w] += 1
+        return True
+
+    while not all(run[r][w] >= runs for r in range(P) for w in range(G)):
+        moved = False
+        for r in range(P):
+            for w in range(G):
+                while step(r, w):
+                    moved = True
+        assert moved, "stall at %s" % [[(run[r][w], pc[r][w]) for w in range(G)]
+                                       for r in range(P)]
+    return bufs
+
+
+def expected(name, P, op, ins, runs):
+    cur = ins
+    for _ in range(runs):
+        if name == "fn_ring":
+            cur = O.allreduce_fn(O.FN_RING, op, O.FLOAT32, [[] for _ in range(P)], cur)
+        elif name == "fn_bcube":
+            cur = O.allreduce_fn(O.FN_BCUBE, op, O.FLOAT32, [[] for _ in range(P)], cur)
+        elif name == "halving_doubling":
+            cur = O.allreduce(O.HALVING_DOUBLING, op, O.FLOAT32, cur)
+        else:
+            cur = O.allreduce(O.RING_CHUNKED, op, O.FLOAT32, cur)
+    return cur
+
+
+NAMES = ["ring_chunked", "halving_doubling", "fn_ring", "fn_bcube", "ring_chunked_mesh"]
+
+
+@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("P", [2, 3, 5, 8])
+@pytest.mark.parametrize("N", [1, 1024, 999, 4099])
+@pytest.mark.parametrize("G", [1, 4])
+def test_plan_kernel_protocol_matches_oracle(name, P, N, G):
+    if not all(gloo_amd.plan_sync(name, r, P, N, G)["safe"] for r in range(P)):
+        pytest.skip("the executor keeps host-issued steps for this program")
+    ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=91)
+    got = simulate(name, P, N, G, O.SUM, ins)
+    exp = expected(name, P, O.SUM, ins, 2)
+    for r in range(P):
+        assert same_bits(got[r], exp[r][0]), "rank %d" % r
+
+
+@pytest.mark.parametrize("name", ["ring_chunked", "halving_doubling"])
+@pytest.mark.parametrize("P", [4, 6, 7])
+def test_plan_kernel_protocol_max_and_odd_sizes(name, P):
+    # ring: 16-byte-aligned chunks and a shorter last one; HD: a size whose
+    # halvings stay aligned
+    N = 2 * P * 4000 - 4 if name == "ring_chunked" else 65536
+    assert all(gloo_amd.plan_sync(name, r, P, N, 7)["safe"] for r in range(P))
+    ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=92)
+    got = simulate(name, P, N, 7, O.MAX, ins, runs=1)
+    exp = expected(name, P, O.MAX, ins, 1)
+    for r in range(P):
+        assert same_bits(got[r], exp[r][0]), "rank %d" % r
+
+
+@pytest.mark.parametrize("P", [2, 8])
+def test_plan_kernel_runs_the_bench_shapes(P):
+    """The shapes the bench times (2^k elements, 256 MiB at 512 workgroups)
+    are ones the plan kernel takes."""
+    for name in ("ring_chunked", "halving_doubling"):
+        for n, G in ((1 << 10, 1), (1 << 20, 256), (1 << 26, 512)):
+            assert all(gloo_amd.plan_sync(name, r, P, n, G)["safe"] for r in range(P)), (name, n)
+
+
+def test_unsafe_program_is_detected_and_would_clobber():
+    """ring_chunked with a last chunk of another length AND a 16-byte phase
+    that differs between the chunks sharing a landing region: two workgroups
+    would own the same region bytes in different messages.  glx_plan_sync
+    calls it unsafe (the executor keeps host-issued steps), and running the
+    kernel protocol anyway does clobber unread data."""
+    P, N, G = 2, 10003, 4
+    assert not all(gloo_amd.plan_sync("ring_chunked", r, P, N, G)["safe"] for r in range(P))
+    ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=93)
+    with pytest.raises(Clobber):
+        simulate("ring_chunked", P, N, G, O.SUM, ins)
