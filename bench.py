@@ -274,25 +274,30 @@ def plan_name(algo):
 
 def make_alg(gloo_amd, ctx, buf, algo):
     """With the ranks on distinct devices/processes: ring_chunked and
-    halving_doubling run their step programs in the plan kernel (devsteps),
-    ring_chunked_mesh on the two-shot kernel, ring_chunked_repl on the
-    one-shot kernel.  *_host and ring_chunked_mesh_steps are the same
+    halving_doubling run their step programs in the plan kernel (devsteps) at
+    every size, ring_chunked_mesh on the two-shot kernel, ring_chunked_repl on
+    the one-shot kernel.  *_host and ring_chunked_mesh_steps are the same
     schedules with host-issued steps (calibrated peer-copy transport)."""
+    engine = None
     if algo.endswith("_host"):
-        gloo_amd.set_steps_engine("host")
-        try:
-            return make_alg(gloo_amd, ctx, buf, algo[:-len("_host")])
-        finally:
-            gloo_amd.set_steps_engine("device")
-    if algo == "halving_doubling":
-        return gloo_amd.AllreduceHalvingDoubling(ctx, [buf])
-    if algo == "ring_chunked_mesh_steps":
-        gloo_amd.set_mesh_engine("steps")
-        try:
-            return gloo_amd.AllreduceRingChunked(ctx, [buf], schedule="mesh")
-        finally:
-            gloo_amd.set_mesh_engine("device")
-    return gloo_amd.AllreduceRingChunked(ctx, [buf], schedule=RING_SCHEDULES[algo])
+        engine, algo = "host", algo[:-len("_host")]
+    elif algo in ("ring_chunked", "halving_doubling"):
+        engine = "device"
+    if engine is not None:
+        gloo_amd.set_steps_engine(engine)
+    try:
+        if algo == "halving_doubling":
+            return gloo_amd.AllreduceHalvingDoubling(ctx, [buf])
+        if algo == "ring_chunked_mesh_steps":
+            gloo_amd.set_mesh_engine("steps")
+            try:
+                return gloo_amd.AllreduceRingChunked(ctx, [buf], schedule="mesh")
+            finally:
+                gloo_amd.set_mesh_engine("device")
+        return gloo_amd.AllreduceRingChunked(ctx, [buf], schedule=RING_SCHEDULES[algo])
+    finally:
+        if engine is not None:
+            gloo_amd.set_steps_engine("auto")
 
 
 def busiest_link_bytes(gloo_amd, algo, rank, world, count, es):

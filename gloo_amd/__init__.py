@@ -55,9 +55,10 @@ def set_mesh_engine(engine):
 def set_steps_engine(engine):
     """Engine of ring / halving-doubling / bcube / function-style ring
     algorithms created afterwards when the ranks are on distinct devices or
-    processes: "device" (the plan kernel, one device-driven launch per rank;
-    default) or "host" (host-issued steps).  Same results either way."""
-    code = {"host": 0, "device": 3}[engine]
+    processes: "auto" (default: the plan kernel up to 32 MiB per rank,
+    host-issued steps above), "device" (the plan kernel, one device-driven
+    launch per rank) or "host" (host-issued steps).  Same results either way."""
+    code = {"host": 0, "device": 3, "auto": -1}[engine]
     errors.check(_lib.lib.glx_set_steps_engine(code), "set_steps_engine")
 
 

@@ -182,8 +182,9 @@ int glx_set_mesh_engine(int engine) {
 }
 
 int glx_set_steps_engine(int engine) {
-  if (engine != GLX_ENGINE_STEPS && engine != GLX_ENGINE_DEVSTEPS) {
-    return fail(GLX_ERR_INVALID, "steps engine must be GLX_ENGINE_STEPS or GLX_ENGINE_DEVSTEPS");
+  if (engine != GLX_ENGINE_STEPS && engine != GLX_ENGINE_DEVSTEPS && engine != -1) {
+    return fail(GLX_ERR_INVALID,
+                "steps engine must be GLX_ENGINE_STEPS, GLX_ENGINE_DEVSTEPS or -1 (by size)");
   }
   gloo::HipPlanExecutor::setStepsEngine(engine);
   return GLX_OK;

@@ -175,7 +175,7 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
     }
   }
 
-  engine_ = engineFor(*ctx, algo, count_);
+  engine_ = engineFor(*ctx, algo, count_, (int)esize_);
   if (engine_ == kEngineDevSteps) {
     // the plan kernel's grid and bookkeeping; when a landing region would be
     // shared by two workgroups across messages, keep the host-issued steps
@@ -1045,10 +1045,19 @@ int initialMeshEngine() {
 
 std::atomic<int> g_mesh_engine{initialMeshEngine()};
 
+// -1 = by size (the plan kernel up to kDevStepsMaxBytes per rank, where its
+// per-step flag round trips beat host-issued steps; host-issued steps with
+// their wide copy and reduce launches above), else a fixed engine.
 int initialStepsEngine() {
   const char* e = std::getenv("GLOO_AMD_STEPS_ENGINE");
-  return (e != nullptr && std::strcmp(e, "host") == 0) ? HipPlanExecutor::kEngineSteps
-                                                       : HipPlanExecutor::kEngineDevSteps;
+  if (e != nullptr && std::strcmp(e, "host") == 0) return HipPlanExecutor::kEngineSteps;
+  if (e != nullptr && std::strcmp(e, "device") == 0) return HipPlanExecutor::kEngineDevSteps;
+  return -1;
+}
+
+int64_t devStepsMaxBytes() {
+  const char* e = std::getenv("GLOO_AMD_DEVSTEPS_MAX_BYTES");
+  return e != nullptr ? std::atoll(e) : (int64_t(32) << 20);
 }
 
 std::atomic<int> g_steps_engine{initialStepsEngine()};
@@ -1062,7 +1071,7 @@ void HipPlanExecutor::setMeshEngine(int engine) {
 int HipPlanExecutor::meshEngine() { return g_mesh_engine.load(); }
 
 void HipPlanExecutor::setStepsEngine(int engine) {
-  g_steps_engine.store(engine == kEngineSteps ? kEngineSteps : kEngineDevSteps);
+  g_steps_engine.store(engine < 0 ? -1 : (engine == kEngineSteps ? kEngineSteps : kEngineDevSteps));
 }
 
 int HipPlanExecutor::stepsEngine() { return g_steps_engine.load(); }
@@ -1093,7 +1102,7 @@ bool HipPlanExecutor::deviceEnginesAvailable(const Context& ctx) {
 
 // The inputs are the same on every rank, so every rank makes the same choice
 // (and publish/resolve checks that they did).
-int HipPlanExecutor::engineFor(const Context& ctx, int algo, int64_t count) {
+int HipPlanExecutor::engineFor(const Context& ctx, int algo, int64_t count, int esize) {
   if (count <= 0 || !deviceEnginesAvailable(ctx)) return kEngineSteps;
   if (algo == glx::ALGO_RING_CHUNKED_REPL || algo == glx::ALGO_FN_RING_REPL) {
     return kEngineOneShot;
@@ -1103,7 +1112,9 @@ int HipPlanExecutor::engineFor(const Context& ctx, int algo, int64_t count) {
   }
   if (algo == glx::ALGO_RING_CHUNKED || algo == glx::ALGO_HALVING_DOUBLING ||
       algo == glx::ALGO_FN_RING || algo == glx::ALGO_FN_BCUBE) {
-    return stepsEngine();
+    const int e = stepsEngine();
+    if (e >= 0) return e;
+    return count * esize <= devStepsMaxBytes() ? kEngineDevSteps : kEngineSteps;
   }
   return kEngineSteps;
 }

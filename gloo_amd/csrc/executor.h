@@ -224,7 +224,7 @@ class HipPlanExecutor : public Algorithm {
   hipEvent_t ddDone_ = nullptr;
   bool ddLaunched_ = false;
   int clockKhz_ = 100000;  // s_memrealtime rate
-  static int engineFor(const Context& ctx, int algo, int64_t count);
+  static int engineFor(const Context& ctx, int algo, int64_t count, int esize);
   char* ddAlloc(size_t bytes);
   void setupDevice();
   size_t maxSlices(int kernel) const;
@@ -251,8 +251,10 @@ class HipPlanExecutor : public Algorithm {
   static void setMeshEngine(int engine);
   static int meshEngine();
   // Engine of the ring, halving-doubling, bcube and function-style ring
-  // schedules when available: kEngineDevSteps (the plan kernel, default;
-  // env GLOO_AMD_STEPS_ENGINE=host overrides) or kEngineSteps.
+  // schedules when available: -1 = by size (default: the plan kernel up to
+  // 32 MiB per rank, env GLOO_AMD_DEVSTEPS_MAX_BYTES; host-issued steps
+  // above), kEngineDevSteps or kEngineSteps (env GLOO_AMD_STEPS_ENGINE=
+  // device|host).
   static void setStepsEngine(int engine);
   static int stepsEngine();
 };

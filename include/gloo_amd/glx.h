@@ -126,8 +126,10 @@ int glx_set_mesh_engine(int engine);
 int glx_set_device_engines(int mode);
 /* Engine of the ring, halving-doubling, bcube and function-style ring
  * schedules for algorithms created afterwards, when device-driven engines
- * are available: GLX_ENGINE_DEVSTEPS (the plan kernel, default) or
- * GLX_ENGINE_STEPS (host-issued steps).  Env GLOO_AMD_STEPS_ENGINE=host. */
+ * are available: -1 = by size (default: the plan kernel up to 32 MiB per
+ * rank, env GLOO_AMD_DEVSTEPS_MAX_BYTES, host-issued steps above),
+ * GLX_ENGINE_DEVSTEPS (the plan kernel) or GLX_ENGINE_STEPS (host-issued
+ * steps).  Env GLOO_AMD_STEPS_ENGINE=device|host. */
 int glx_set_steps_engine(int engine);
 
 /* Number of visible HIP devices (0 when no GPU). */

@@ -190,6 +190,7 @@ def run_devsteps(store_dir, rank, size):
         for dt in (O.FLOAT16, O.INT32, O.FLOAT64, O.INT8, O.UINT64):
             for op in (O.SUM, O.PRODUCT, O.MAX, O.MIN):
                 cases.append((kind, 4099, dt, op))
+    gloo_amd.set_steps_engine("device")
     engines = set()
     for seed, (kind, n, dt, op) in enumerate(cases):
         ins = case_inputs(size, n, dt, 1, 0, seed=200 + seed)
@@ -256,7 +257,7 @@ def run_devsteps(store_dir, rank, size):
                 print("LAT rank %d P %d %s elems %d engine %s us %.1f"
                       % (rank, size, label, n, alg.engine(), us), flush=True)
                 alg.close()
-    gloo_amd.set_steps_engine("device")
+    gloo_amd.set_steps_engine("auto")
     store.set("done/%d" % rank, b"1")
     for r in range(size):
         store.get("done/%d" % r, timeout_ms=60000)
