@@ -89,6 +89,20 @@ bool isPinnedHost(const void* p) {
   return a.type == hipMemoryTypeHost;
 }
 
+// Blocking wait for a stream with a short wake-up: poll for up to 200 us
+// (a device-driven small allreduce finishes in a few us; the runtime's
+// blocking wait adds several us of wake-up), then block.
+hipError_t spinSync(hipStream_t s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e != hipErrorNotReady) return e;
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) break;
+    _mm_pause();
+  }
+  return hipStreamSynchronize(s);
+}
+
 // H2D pieces of host-mode staging: small enough that the schedule starts
 // early, large enough to run the PCIe link at full rate.
 constexpr int64_t kStagePieceBytes = int64_t(8) << 20;
@@ -625,7 +639,7 @@ void HipPlanExecutor::run() {
   }
   GLX_TRACE("r%d sync", contextRank_);
   if (!userStream_) {
-    GLX_HIP_CHECK(hipStreamSynchronize(compute_));
+    GLX_HIP_CHECK(spinSync(compute_));
     checkDevice();
   }
   GLX_TRACE("r%d done", contextRank_);
@@ -702,7 +716,7 @@ void HipPlanExecutor::runFn(const FnCall& call) {
                                  hipMemcpyDeviceToDevice, compute_));
   }
   if (call.stream == nullptr) {
-    GLX_HIP_CHECK(hipStreamSynchronize(compute_));
+    GLX_HIP_CHECK(spinSync(compute_));
     checkDevice();
   }
 }

@@ -187,7 +187,7 @@ def run_devsteps(store_dir, rank, size):
     for kind in (O.RING_CHUNKED, O.HALVING_DOUBLING):
         for n in (1, 3, 255, 256, 1000, 4099, 65539, 1 << 20, (1 << 22) + 5):
             cases.append((kind, n, O.FLOAT32, O.SUM))
-        for dt in (O.FLOAT16, O.INT32, O.FLOAT64, O.INT8, O.UINT64):
+        for dt in (O.FLOAT16, O.BFLOAT16, O.INT32, O.FLOAT64, O.INT8, O.UINT64):
             for op in (O.SUM, O.PRODUCT, O.MAX, O.MIN):
                 cases.append((kind, 4099, dt, op))
     gloo_amd.set_steps_engine("device")
@@ -297,7 +297,7 @@ def run_device(store_dir, rank, size, mode):
         sizes += [(1 << 22) + 5, 3 << 22]
     for n in sizes:
         cases.append((n, O.FLOAT32, O.SUM))
-    for dt in (O.FLOAT16, O.INT32, O.FLOAT64, O.INT8, O.UINT64):
+    for dt in (O.FLOAT16, O.BFLOAT16, O.INT32, O.FLOAT64, O.INT8, O.UINT64):
         for op in (O.SUM, O.PRODUCT, O.MAX, O.MIN):
             cases.append((4099, dt, op))
     cases.append((77777, O.FLOAT16, O.SUM))
