@@ -235,12 +235,13 @@ def bench_single(args):
     return res
 
 
-def reduce_kernel_roofline(torch, gloo_amd, dev, chunk_bytes, reps=50):
-    """Live HBM roofline of the reduce kernel at the ring's chunk size, timed
-    with HIP events on the stream it is launched on."""
-    n = chunk_bytes // 4
-    a = torch.rand(n, device=dev)
-    b = torch.rand(n, device=dev)
+def reduce_kernel_roofline(torch, gloo_amd, dev, chunk_bytes, dtype="f32", reps=50):
+    """Live HBM roofline of the reduce kernel at the ring's chunk size and the
+    run's dtype, timed with HIP events on the stream it is launched on."""
+    name, es = DTYPES[dtype]
+    n = chunk_bytes // es
+    a = torch.rand(n, device=dev).to(getattr(torch, name))
+    b = torch.rand(n, device=dev).to(getattr(torch, name))
     s = torch.cuda.current_stream(dev)
     for _ in range(5):
         gloo_amd.math.reduce(gloo_amd.ReductionType.SUM, a, a, b, stream=s)
@@ -254,7 +255,7 @@ def reduce_kernel_roofline(torch, gloo_amd, dev, chunk_bytes, reps=50):
     ach = 3 * chunk_bytes / t / 1e9
     return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
-            "kernel": "reduce in place, %d MiB chunk" % (chunk_bytes >> 20),
+            "kernel": "reduce in place, %d MiB %s chunk" % (chunk_bytes >> 20, dtype),
             "algorithmic_bytes_per_launch": 3 * chunk_bytes}
 
 
@@ -608,7 +609,7 @@ def bench_multi(args):
                        "baseline_config": "configs[3]" if args.algo == "halving_doubling"
                        else "configs[2]"},
             "algbw_GBps": round(algbw, 3), "busbw_GBps": round(busbw, 3),
-            "roofline": reduce_kernel_roofline(torch, gloo_amd, dev, chunk),
+            "roofline": reduce_kernel_roofline(torch, gloo_amd, dev, chunk, args.dtype),
             "link_roofline": {"bound": "xgmi_link", "achieved": round(link_ach, 2),
                               "peak": XGMI_LINK_GBPS, "unit": "GB/s",
                               "frac": round(link_ach / XGMI_LINK_GBPS, 4),
