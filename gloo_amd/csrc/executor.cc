@@ -125,6 +125,20 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
                                  const std::vector<hipStream_t>& streams,
                                  const glx::PlanParams& prm, bool perCallBuffers)
     : Algorithm(ctx), algo_(algo), ptrs_(ptrs), count_(count), dtype_(dtype), op_(op) {
+  try {
+    construct(ctx, ptrs, streams, prm, perCallBuffers);
+  } catch (...) {
+    release();
+    throw;
+  }
+}
+
+void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
+                                const std::vector<void*>& ptrs,
+                                const std::vector<hipStream_t>& streams,
+                                const glx::PlanParams& prm, bool perCallBuffers) {
+  const int algo = algo_, dtype = dtype_, op = op_;
+  const int64_t count = count_;
   GLX_ENFORCE(!ptrs.empty(), "at least one buffer pointer is required");
   GLX_ENFORCE(count >= 0 && count <= (int64_t(1) << 40), "count out of range: ", count);
   esize_ = glx_dtype_size(dtype);
@@ -267,7 +281,10 @@ HipPlanExecutor::HipPlanExecutor(const std::shared_ptr<Context>& ctx, int algo,
   if (contextSize_ > 1 && count_ > 0) publish();
 }
 
-HipPlanExecutor::~HipPlanExecutor() noexcept(false) {
+HipPlanExecutor::~HipPlanExecutor() noexcept(false) { release(); }
+
+void HipPlanExecutor::release() noexcept {
+  if (device_ < 0) return;  // nothing was acquired
   hipSetDevice(device_);
   if (compute_ != nullptr) hipStreamSynchronize(compute_);
   for (auto& c : copies_) hipStreamSynchronize(c.s);
@@ -277,7 +294,9 @@ HipPlanExecutor::~HipPlanExecutor() noexcept(false) {
       hipStreamDestroy(st);
     }
   }
-  for (auto& e : h2dEvents_) hipEventDestroy(e);
+  for (auto& e : h2dEvents_) {
+    if (e != nullptr) hipEventDestroy(e);
+  }
   for (auto& e : d2hEvents_) {
     if (e != nullptr) hipEventDestroy(e);
   }
@@ -286,7 +305,9 @@ HipPlanExecutor::~HipPlanExecutor() noexcept(false) {
   for (char* d : fnStage_) hipFree(d);
   for (void* p : registered_) hipHostUnregister(p);
   for (void* p : ipcOpened_) hipIpcCloseMemHandle(p);
-  for (auto& e : events_) hipEventDestroy(e);
+  for (auto& e : events_) {
+    if (e != nullptr) hipEventDestroy(e);
+  }
   if (computeMark_) hipEventDestroy(computeMark_);
   for (auto& b : blocks_) hipFree(b.ptr);
   for (char* d : ddBlocks_) hipFree(d);

@@ -146,6 +146,12 @@ class HipPlanExecutor : public Algorithm {
   void localReduce(const std::vector<void*>& in, const std::vector<void*>& out);
   void allocScratch(bool uncached = false);
   void waitWar(int64_t off, int64_t len);
+  // The constructor's work; on a throw the constructor releases whatever it
+  // had acquired (the destructor never runs for a half-built object).
+  void construct(const std::shared_ptr<Context>& ctx, const std::vector<void*>& ptrs,
+                 const std::vector<hipStream_t>& streams, const glx::PlanParams& prm,
+                 bool perCallBuffers);
+  void release() noexcept;
 
   glx::Plan plan_;
   int algo_;
@@ -153,9 +159,9 @@ class HipPlanExecutor : public Algorithm {
   int64_t count_;
   int dtype_, op_;
   size_t esize_;
-  int device_;
-  int slot_;
-  bool userStream_;
+  int device_ = -1;
+  int slot_ = 0;
+  bool userStream_ = false;
   hipStream_t compute_ = nullptr;
   std::vector<CopyStream> copies_;
   uint64_t markEpoch_ = 0;
