@@ -312,6 +312,7 @@ void HipPlanExecutor::release() noexcept {
   for (auto& b : blocks_) hipFree(b.ptr);
   for (char* d : ddBlocks_) hipFree(d);
   if (ddStatus_) hipHostFree(ddStatus_);
+  if (trace_) hipHostFree(trace_);
   if (ddDone_) hipEventDestroy(ddDone_);
   for (auto& c : copies_) hipStreamDestroy(c.s);
   if (ownCompute_ && compute_) hipStreamDestroy(compute_);
@@ -1236,6 +1237,7 @@ void HipPlanExecutor::setupTwoShot() {
   glx::TwoShotParams& p = ts_;
   p.P = P;
   p.rank = contextRank_;
+  p.trace = nullptr;
   for (int c = 0; c < glx::kOsMaxRanks; c++) {
     p.rangeOff[c] = (size_t)d.rangeOff[c];
     p.rangeLen[c] = (size_t)d.rangeLen[c];
@@ -1243,6 +1245,12 @@ void HipPlanExecutor::setupTwoShot() {
   }
   p.slice = (size_t)d.slice;
   p.G = d.G;
+  if (devTrace()) {
+    const size_t n = (size_t)std::max<int64_t>(1, maxSlices(1)) * glx::kTsTrace;
+    GLX_HIP_CHECK(hipHostMalloc((void**)&trace_, n * sizeof(uint64_t), hipHostMallocDefault));
+    std::memset(trace_, 0, n * sizeof(uint64_t));
+    p.trace = trace_;
+  }
   ddSlot_ = ((size_t)d.maxLen * esize_ + 16 + 255) & ~(size_t)255;
   for (int k = 0; k < 4; k++) ddAlloc((size_t)P * ddSlot_);  // RS 0/1, AG 0/1
   char* flags = ddAlloc(2 * (size_t)P * (size_t)p.G * sizeof(uint64_t));
@@ -1365,6 +1373,52 @@ void HipPlanExecutor::checkDevice() {
   }
 }
 
+bool HipPlanExecutor::devTrace() {
+  static const bool on = [] {
+    const char* e = std::getenv("GLOO_AMD_DEVTRACE");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+
+// Diagnostics (GLOO_AMD_DEVTRACE=1): wait for the launch just issued and
+// print, per phase, the mean and max over workgroups of the time since the
+// workgroup started (s_memrealtime), plus the grid's span.
+void HipPlanExecutor::traceTwoShot(const glx::TwoShotParams& launched) {
+  (void)launched;
+  GLX_HIP_CHECK(hipStreamSynchronize(compute_));
+  const int G = ts_.G;
+  const uint64_t* t = trace_;
+  const double us = 1e3 / (double)clockKhz_;
+  uint64_t t0min = ~uint64_t(0), t5max = 0;
+  double mean[glx::kTsTrace] = {0}, mx[glx::kTsTrace] = {0};
+  for (int w = 0; w < G; w++) {
+    const uint64_t* r = t + (size_t)w * glx::kTsTrace;
+    t0min = std::min(t0min, r[0]);
+    t5max = std::max(t5max, r[5]);
+    for (int k = 1; k < glx::kTsTrace; k++) {
+      const double d = r[k] >= r[0] ? (double)(r[k] - r[0]) * us : 0.0;
+      mean[k] += d / G;
+      mx[k] = std::max(mx[k], d);
+    }
+  }
+  double st = 0, stmax = 0;  // start skew within the grid
+  for (int w = 0; w < G; w++) {
+    const double d = (double)(t[(size_t)w * glx::kTsTrace] - t0min) * us;
+    st += d / G;
+    stmax = std::max(stmax, d);
+  }
+  std::fprintf(stderr, "[devtrace r%d] resident capacity %d, ranks on the busiest device %d\n",
+               contextRank_, glx::device_engine_resident_blocks(1, op_, dtype_),
+               context_->maxRanksPerDevice());
+  std::fprintf(stderr,
+               "[devtrace r%d two-shot G=%d slice=%zu] span %.1f us | start skew mean %.1f max "
+               "%.1f | since start (mean/max): pushed %.1f/%.1f  copies-in %.1f/%.1f  "
+               "folded %.1f/%.1f  results-in %.1f/%.1f  end %.1f/%.1f\n",
+               contextRank_, G, ts_.slice, (double)(t5max - t0min) * us, st, stmax, mean[1],
+               mx[1], mean[2], mx[2], mean[3], mx[3], mean[4], mx[4], mean[5], mx[5]);
+}
+
 void HipPlanExecutor::runDevice(char* ptr0) {
   if (!resolved_) resolvePeers();
   checkDevice();  // an earlier asynchronous call that timed out
@@ -1436,6 +1490,7 @@ void HipPlanExecutor::runDevice(char* ptr0) {
     GLX_TRACE("r%d two-shot epoch %lu (G=%d slice=%zu)", contextRank_, (unsigned long)e, p.G,
               p.slice);
     GLX_HIP_CHECK(glx::launch_twoshot(op_, dtype_, p, compute_));
+    if (devTrace()) traceTwoShot(p);
   }
   GLX_HIP_CHECK(hipEventRecord(ddDone_, compute_));
   ddLaunched_ = true;

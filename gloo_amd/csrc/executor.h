@@ -230,6 +230,9 @@ class HipPlanExecutor : public Algorithm {
   hipEvent_t ddDone_ = nullptr;
   bool ddLaunched_ = false;
   int clockKhz_ = 100000;  // s_memrealtime rate
+  uint64_t* trace_ = nullptr;  // GLOO_AMD_DEVTRACE=1: two-shot phase stamps (pinned host)
+  static bool devTrace();
+  void traceTwoShot(const glx::TwoShotParams& launched);
   static int engineFor(const Context& ctx, int algo, int64_t count, int esize);
   char* ddAlloc(size_t bytes);
   void setupDevice();

@@ -80,7 +80,11 @@ struct TwoShotParams {
   uint8_t chain[kOsMaxRanks];       // this rank's fold order
   size_t slice;                     // elements per workgroup per range, multiple of 16 / esize
   int P, rank, G;
+  // diagnostics (GLOO_AMD_DEVTRACE=1): per workgroup [G][kTsTrace] s_memrealtime
+  // stamps: start, pushed, peers' copies landed, folded, results landed, end
+  uint64_t* trace;
 };
+constexpr int kTsTrace = 6;
 hipError_t launch_twoshot(int op, int dtype, const TwoShotParams& p, hipStream_t s);
 // Plan kernel (xgmi_kernels.hip): ANY compiled schedule (a plan.h step
 // program) as one device-driven kernel per rank.  The buffer is cut into

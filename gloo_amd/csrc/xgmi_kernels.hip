@@ -311,6 +311,12 @@ __global__ __launch_bounds__(kBlock, 2) void twoshot_kernel(TwoShotParams p) {
   using S = typename Elem<T, OP>::S;
   __shared__ int s_ok;
   const int w = blockIdx.x;
+  auto stamp = [&](int k) {  // diagnostics only (p.trace is null otherwise)
+    if (p.trace != nullptr && threadIdx.x == 0) {
+      p.trace[(size_t)w * kTsTrace + k] = __builtin_amdgcn_s_memrealtime();
+    }
+  };
+  stamp(0);
   S* buf = reinterpret_cast<S*>(p.buf);
   const bool aligned = ((uintptr_t)p.buf % 16) == 0;
   auto span = [&](int c, size_t& a, size_t& b) {  // slice w of range c
@@ -334,6 +340,7 @@ __global__ __launch_bounds__(kBlock, 2) void twoshot_kernel(TwoShotParams p) {
     size_t a, b;
     return span(j, a, b);
   });
+  stamp(1);
 
   // 2. fold my range's slice from every peer's copy; result to my buffer
   //    and to every peer's AG slot in the same pass
@@ -347,6 +354,7 @@ __global__ __launch_bounds__(kBlock, 2) void twoshot_kernel(TwoShotParams p) {
         return;
       }
     }
+    stamp(2);
     const S* src[kOsMaxRanks];
 #pragma unroll
     for (int i = 0; i < kOsMaxRanks; i++) {
@@ -363,6 +371,7 @@ __global__ __launch_bounds__(kBlock, 2) void twoshot_kernel(TwoShotParams p) {
     fold_span<T, OP>(buf, src, p.P, outs, p.P - 1, a, b, aligned);
     release_flags(p.flagBOut, p.P, p.rank, w, p.epoch, [](int) { return true; });
   }
+  stamp(3);
 
   // 3. take every other owner's finished slice
   for (int d = 1; d < p.P; d++) {
@@ -373,8 +382,10 @@ __global__ __launch_bounds__(kBlock, 2) void twoshot_kernel(TwoShotParams p) {
                    p.status, &s_ok)) {
       return;
     }
+    if (d == 1) stamp(4);
     copy_span<S>(buf, reinterpret_cast<const S*>(p.agLand[j]), a, b, aligned);
   }
+  stamp(5);
 }
 
 // ---- plan kernel --------------------------------------------------------------
