@@ -276,14 +276,16 @@ def plan_name(algo):
 def make_alg(gloo_amd, ctx, buf, algo):
     """With the ranks on distinct devices/processes: ring_chunked and
     halving_doubling run their step programs in the plan kernel (devsteps) at
-    every size, ring_chunked_mesh on the two-shot kernel, ring_chunked_repl on
+    every size up to 4 ranks, ring_chunked_mesh on the two-shot kernel, ring_chunked_repl on
     the one-shot kernel.  *_host and ring_chunked_mesh_steps are the same
     schedules with host-issued steps (calibrated peer-copy transport)."""
     engine = None
     if algo.endswith("_host"):
         engine, algo = "host", algo[:-len("_host")]
     elif algo in ("ring_chunked", "halving_doubling"):
-        engine = "device"
+        # the plan kernel where it is validated on the GPU (<= 4 ranks);
+        # above, the library's own choice (host-issued steps)
+        engine = "device" if int(os.environ.get("WORLD_SIZE", "1")) <= 4 else "auto"
     if engine is not None:
         gloo_amd.set_steps_engine(engine)
     try:
@@ -527,7 +529,31 @@ def bench_multi(args):
         candidates = ["ring_chunked_mesh", "ring_chunked_mesh_steps"]
     else:
         candidates = [args.algo]
-    runs = {a: tuned(a) for a in candidates}
+    # A candidate that fails on any rank (a timeout, a HIP error) is dropped
+    # on every rank and named in the JSON line; the others still report.
+    def agreed(ok):
+        flag = torch.tensor([0 if ok else 1], dtype=torch.int32)
+        dist.all_reduce(flag)
+        return int(flag.item()) == 0
+
+    def attempt(what, fn):
+        try:
+            return fn(), None
+        except Exception as e:  # noqa: BLE001 - reported in the JSON line
+            err = "%s: %s" % (type(e).__name__, str(e)[:300])
+            log("%s failed: %s" % (what, err))
+            return None, err
+
+    runs, failed = {}, {}
+    for a in candidates:
+        r, err = attempt(a, lambda: tuned(a))
+        if agreed(err is None):
+            runs[a] = r
+        else:
+            failed[a] = err or "failed on another rank"
+    if not runs:
+        raise RuntimeError("every candidate failed: %s" % failed)
+    candidates = [a for a in candidates if a in runs]
     chosen = min(runs, key=lambda a: runs[a]["t"])
     t, link_bytes = runs[chosen]["t"], runs[chosen]["sent"]
     dev_result = runs[chosen]["result"]
@@ -559,8 +585,12 @@ def bench_multi(args):
                 continue
             buf.copy_(src)
             torch.cuda.synchronize()
-            ta, sent_a = time_schedule(torch, dist, gloo_amd, ctx, buf, other, steps,
-                                       args.warmup)
+            got, err = attempt(other, lambda: time_schedule(torch, dist, gloo_amd, ctx, buf,
+                                                            other, steps, args.warmup))
+            if not agreed(err is None):
+                failed[other] = err or "failed on another rank"
+                continue
+            ta, sent_a = got
             lm = busiest_link_bytes(gloo_amd, other, rank, world, n, es)
             alts[other] = {"value": round(world * S / ta / 1e9, 3),
                            "ms_per_step": round(ta * 1e3, 4),
@@ -570,11 +600,16 @@ def bench_multi(args):
                            "busiest_link_GBps": round(lm / ta / 1e9, 2)}
     staged = None
     if args.staged:
-        staged = host_endpoint_rate(torch, dist, gloo_amd, ctx, src, dev_result, chosen,
-                                    reps=min(steps, 5))
+        staged, err = attempt("host-staged", lambda: host_endpoint_rate(
+            torch, dist, gloo_amd, ctx, src, dev_result, chosen, reps=min(steps, 5)))
+        if not agreed(err is None):
+            staged, failed["host_staged"] = None, err or "failed on another rank"
     sweep = None
     if args.sweep:
-        sweep = element_sweep(torch, dist, gloo_amd, ctx, dev, candidates, args.dtype)
+        sweep, err = attempt("sweep", lambda: element_sweep(torch, dist, gloo_amd, ctx, dev,
+                                                            candidates, args.dtype))
+        if not agreed(err is None):
+            sweep, failed["sweep"] = None, err or "failed on another rank"
     res = None
     if rank == 0:
         chunk = max(256 * es, -(-S // (2 * world)))
@@ -625,6 +660,8 @@ def bench_multi(args):
         }
         if staged is not None:
             res["host_staged"] = staged
+        if failed:
+            res["failed"] = failed
     dist.barrier()
     dist.destroy_process_group()
     return res

@@ -14,6 +14,7 @@
 
 #include <atomic>
 #include <cstring>
+#include <thread>
 
 #include "common.h"
 
@@ -140,7 +141,113 @@ Context::Context(int rank_, int size_, int device) : rank(rank_), size(size_), d
   peers_.resize(size_);
 }
 
-Context::~Context() = default;
+Context::~Context() {
+  if (shared_.empty() && imported_.empty()) return;
+  if (device_ >= 0) hipSetDevice(device_);
+  for (auto& kv : imported_) hipIpcCloseMemHandle(kv.second);
+  for (auto& b : shared_) hipFree(b.ptr);
+}
+
+namespace {
+int32_t exportBlock(hipIpcMemHandle_t* h, void* p) {
+  std::memset(h, 0, sizeof(*h));
+  const hipError_t e = hipIpcGetMemHandle(h, p);
+  if (e == hipSuccess) return 1;
+  (void)hipGetLastError();
+  return -(int32_t)e;
+}
+
+char* allocBlock(size_t bytes, unsigned flags) {
+  char* d = nullptr;
+  if (flags != 0) {
+    GLX_HIP_CHECK(hipExtMallocWithFlags((void**)&d, bytes, flags));
+  } else {
+    GLX_HIP_CHECK(hipMalloc((void**)&d, bytes));
+  }
+  return d;
+}
+
+// Free pooled bytes kept beyond this are returned to the runtime.
+constexpr size_t kMaxFreeSharedBytes = size_t(8) << 30;
+}  // namespace
+
+SharedBlock Context::acquireShared(size_t bytes, unsigned flags) {
+  // Whole 2 MiB granules: the runtime places smaller allocations side by side
+  // in one underlying buffer (seen 4 KiB apart), and a peer that imports such
+  // a block through IPC was seen to get a mapping that does not point at it
+  // (flags and data landing in the neighbouring block).  A block of its own
+  // maps exactly.
+  constexpr size_t kGranule = size_t(2) << 20;
+  bytes = (std::max<size_t>(bytes, 1) + kGranule - 1) / kGranule * kGranule;
+  std::lock_guard<std::mutex> g(sharedMutex_);
+  // the smallest free block of this kind that fits without wasting much
+  SharedBlock* best = nullptr;
+  const size_t most = std::max(2 * bytes, bytes + (size_t(4) << 20));
+  for (auto& b : shared_) {
+    if (!b.inUse && b.flags == flags && b.bytes >= bytes && b.bytes <= most &&
+        (size == 1 || b.ipcStatus == 1) && (best == nullptr || b.bytes < best->bytes)) {
+      best = &b;
+    }
+  }
+  if (best != nullptr) {
+    best->inUse = true;
+    return *best;
+  }
+  SharedBlock nb;
+  nb.bytes = bytes;
+  nb.flags = flags;
+  nb.ptr = allocBlock(bytes, flags);
+  if (size > 1) {
+    // A refused export is retried after a pause, then with a fresh block
+    // (the refused one held meanwhile so that the address range differs).
+    std::vector<char*> refused;
+    for (int attempt = 0; attempt < 8; attempt++) {
+      nb.ipcStatus = exportBlock(&nb.ipc, nb.ptr);
+      if (nb.ipcStatus == 1) break;
+      std::this_thread::sleep_for(std::chrono::milliseconds(1 + attempt));
+      if (attempt == 3) {
+        refused.push_back(nb.ptr);
+        nb.ptr = allocBlock(bytes, flags);
+      }
+    }
+    for (char* r : refused) hipFree(r);
+  }
+  nb.id = nextSharedId_++;
+  nb.inUse = true;
+  shared_.push_back(nb);
+  return nb;
+}
+
+void Context::releaseShared(int64_t id) {
+  std::lock_guard<std::mutex> g(sharedMutex_);
+  size_t freeBytes = 0;
+  for (auto& b : shared_) {
+    if (b.id == id) b.inUse = false;
+    if (!b.inUse) freeBytes += b.bytes;
+  }
+  // over the cap: return the largest free blocks (peers that imported them
+  // keep their mapping until their context goes; the id is never reused)
+  while (freeBytes > kMaxFreeSharedBytes) {
+    auto big = shared_.end();
+    for (auto it = shared_.begin(); it != shared_.end(); ++it) {
+      if (!it->inUse && (big == shared_.end() || it->bytes > big->bytes)) big = it;
+    }
+    if (big == shared_.end()) break;
+    freeBytes -= big->bytes;
+    hipFree(big->ptr);
+    shared_.erase(big);
+  }
+}
+
+char* Context::importShared(int r, int64_t id, const hipIpcMemHandle_t& h) {
+  std::lock_guard<std::mutex> g(sharedMutex_);
+  auto it = imported_.find({r, id});
+  if (it != imported_.end()) return it->second;
+  void* p = nullptr;
+  GLX_HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+  imported_[{r, id}] = static_cast<char*>(p);
+  return static_cast<char*>(p);
+}
 
 void Context::clearOps() {
   std::map<std::string, std::shared_ptr<Algorithm>> drop;

@@ -16,6 +16,7 @@
 // gloo/test/base_test.h:91-166) or one process per GPU (torchrun).
 #pragma once
 
+#include <hip/hip_runtime_api.h>
 #include <sys/types.h>
 
 #include <atomic>
@@ -79,6 +80,17 @@ struct PeerEndpoint {
   std::unique_ptr<ControlBlock> ctl;  // mapped peer control block
 };
 
+// Device memory peers map (receive regions, landing slots, flag rows).
+struct SharedBlock {
+  int64_t id = 0;  // unique within the exporting context, never reused
+  char* ptr = nullptr;
+  size_t bytes = 0;
+  unsigned flags = 0;       // 0: hipMalloc, else hipExtMallocWithFlags
+  hipIpcMemHandle_t ipc{};  // exported when the context has peers
+  int32_t ipcStatus = 0;    // 1 exported, else -(hipError_t)
+  bool inUse = false;
+};
+
 class Context {
  public:
   Context(int rank, int size, int device);
@@ -113,6 +125,17 @@ class Context {
   // Throws IoException if a peer process has exited.
   void checkPeersAlive();
 
+  // Shared device blocks, pooled per context: an algorithm takes a block
+  // (allocated and IPC-exported once, or a free one of a fitting size) and
+  // gives it back when it is destroyed; a peer's block is imported once
+  // (by rank and block id) and stays mapped until the context goes.  Creating
+  // and destroying algorithms then costs no IPC export / import / close
+  // after the first few -- those calls are slow and, with many processes
+  // exporting at once, were seen to fail.
+  SharedBlock acquireShared(size_t bytes, unsigned flags);
+  void releaseShared(int64_t id);
+  char* importShared(int rank, int64_t id, const hipIpcMemHandle_t& h);
+
   // Executors of function-style collectives by options key (see
   // collectives.cc).  They hold a reference to this context: clearOps()
   // breaks that cycle when the context's owner lets go of it.
@@ -129,6 +152,10 @@ class Context {
   ControlBlock local_;
   std::vector<PeerEndpoint> peers_;
   std::string busId_;
+  std::mutex sharedMutex_;
+  std::vector<SharedBlock> shared_;
+  int64_t nextSharedId_ = 1;
+  std::map<std::pair<int, int64_t>, char*> imported_;
 };
 
 }  // namespace gloo

@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <thread>
 
 #include "common.h"
 #include "kernels.h"
@@ -154,6 +155,8 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
   device_ = ctx->device();
   GLX_HIP_CHECK(hipSetDevice(device_));
   slot_ = ctx->nextSlot();
+  GLX_TRACE("r%d new algorithm: slot %d, algo %d, count %ld, dtype %d, op %d", contextRank_,
+            slot_, algo_, (long)count_, dtype_, op_);
   glx::PlanParams pp = prm;
   pp.esize = (int)esize_;
   plan_ = glx::makePlan(algo, contextRank_, contextSize_, count, pp);
@@ -283,9 +286,55 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
 
 HipPlanExecutor::~HipPlanExecutor() noexcept(false) { release(); }
 
+void HipPlanExecutor::drainCredits() noexcept {
+  if (broken_) return;  // a peer timed out or exited: nothing more will come
+  const auto deadline = std::chrono::steady_clock::now() + effectiveTimeout();
+  auto pause = [] { std::this_thread::sleep_for(std::chrono::microseconds(50)); };
+  try {
+    if (engine_ == kEngineSteps) {
+      for (auto& oc : out_) {
+        while (oc.credit != nullptr && oc.credit->load(std::memory_order_acquire) < oc.sent &&
+               std::chrono::steady_clock::now() < deadline) {
+          context_->checkPeersAlive();
+          pause();
+        }
+      }
+    } else if (engine_ == kEngineDevSteps && devRuns_ > 0 && !ddBlocks_.empty()) {
+      // final credit of out-channel c on every workgroup: devRuns_ * perRun
+      std::vector<uint64_t> want(out_.size(), 0);
+      for (size_t i = 0; i < plan_.steps.size() && i < sync_.steps.size(); i++) {
+        if (plan_.steps[i].kind == glx::SEND) {
+          const size_t c = (size_t)sync_.steps[i].chan;
+          if (c < want.size()) want[c] = devRuns_ * sync_.steps[i].perRun;
+        }
+      }
+      const size_t G = (size_t)pk_.G;
+      std::vector<uint64_t> row(G);
+      for (size_t c = 0; c < out_.size(); c++) {
+        const uint64_t* dev =
+            reinterpret_cast<const uint64_t*>(ddBlocks_[0]) + (size_t)out_[c].creditWord * G;
+        for (;;) {
+          if (hipMemcpy(row.data(), dev, G * sizeof(uint64_t), hipMemcpyDeviceToHost) !=
+              hipSuccess) {
+            (void)hipGetLastError();
+            break;
+          }
+          bool done = true;
+          for (size_t w = 0; w < G && done; w++) done = row[w] >= want[c];
+          if (done || std::chrono::steady_clock::now() >= deadline) break;
+          context_->checkPeersAlive();  // throws if a peer exited: stop waiting
+          pause();
+        }
+      }
+    }
+  } catch (...) {
+  }
+}
+
 void HipPlanExecutor::release() noexcept {
   if (device_ < 0) return;  // nothing was acquired
   hipSetDevice(device_);
+  drainCredits();
   if (compute_ != nullptr) hipStreamSynchronize(compute_);
   for (auto& c : copies_) hipStreamSynchronize(c.s);
   for (hipStream_t st : {h2d_, d2h_}) {
@@ -304,13 +353,14 @@ void HipPlanExecutor::release() noexcept {
   for (char* d : devBufs_) hipFree(d);
   for (char* d : fnStage_) hipFree(d);
   for (void* p : registered_) hipHostUnregister(p);
-  for (void* p : ipcOpened_) hipIpcCloseMemHandle(p);
   for (auto& e : events_) {
     if (e != nullptr) hipEventDestroy(e);
   }
   if (computeMark_) hipEventDestroy(computeMark_);
-  for (auto& b : blocks_) hipFree(b.ptr);
-  for (char* d : ddBlocks_) hipFree(d);
+  for (auto& b : blocks_) {
+    if (b.id > 0) context_->releaseShared(b.id);
+  }
+  for (int64_t id : ddIds_) context_->releaseShared(id);
   if (ddStatus_) hipHostFree(ddStatus_);
   if (trace_) hipHostFree(trace_);
   if (ddDone_) hipEventDestroy(ddDone_);
@@ -338,6 +388,7 @@ int HipPlanExecutor::inIndex(int peer, int tag) {
   return -1;
 }
 
+
 // Our record for this algorithm instance: where peers land their messages
 // (scratch pointer / IPC handle) and which counter words they bump (our
 // delivery words) or watch (our credit words).
@@ -345,17 +396,19 @@ void HipPlanExecutor::publish() {
   std::vector<char> b;
   putPod<uint32_t>(b, kAlgMagic);
   putPod<int64_t>(b, (int64_t)::getpid());
+  // what this slot holds: peers check it against their own algorithm
+  putPod<int32_t>(b, (int32_t)algo_);
+  putPod<int64_t>(b, count_);
+  putPod<int32_t>(b, (int32_t)dtype_);
+  putPod<int32_t>(b, (int32_t)op_);
   putPod<int32_t>(b, (int32_t)blocks_.size());
   for (const auto& blk : blocks_) {
     putPod<int64_t>(b, blk.start);
     putPod<int64_t>(b, blk.elems);
     putPod<uint64_t>(b, (uint64_t)(uintptr_t)blk.ptr);
-    hipIpcMemHandle_t h;
-    memset(&h, 0, sizeof(h));
-    int32_t haveIpc = hipIpcGetMemHandle(&h, blk.ptr) == hipSuccess ? 1 : 0;
-    (void)hipGetLastError();
-    putPod<int32_t>(b, haveIpc);
-    putPod(b, h);
+    putPod<int64_t>(b, blk.id);
+    putPod<int32_t>(b, blk.ipcStatus);
+    putPod(b, blk.ipc);
   }
   putPod<int32_t>(b, (int32_t)(in_.size() + out_.size()));
   for (auto& ic : in_) {
@@ -372,14 +425,11 @@ void HipPlanExecutor::publish() {
   }
   putPod<int32_t>(b, engine_);
   putPod<int32_t>(b, (int32_t)ddBlocks_.size());
-  for (char* d : ddBlocks_) {
-    putPod<uint64_t>(b, (uint64_t)(uintptr_t)d);
-    hipIpcMemHandle_t h;
-    memset(&h, 0, sizeof(h));
-    int32_t haveIpc = hipIpcGetMemHandle(&h, d) == hipSuccess ? 1 : 0;
-    (void)hipGetLastError();
-    putPod<int32_t>(b, haveIpc);
-    putPod(b, h);
+  for (size_t k = 0; k < ddBlocks_.size(); k++) {
+    putPod<uint64_t>(b, (uint64_t)(uintptr_t)ddBlocks_[k]);
+    putPod<int64_t>(b, ddIds_[k]);
+    putPod<int32_t>(b, ddIpcStatus_[k]);
+    putPod(b, ddIpc_[k]);
   }
   context_->store().set(
       "glx/alg/" + std::to_string(slot_) + "/" + std::to_string(contextRank_), b);
@@ -402,6 +452,15 @@ void HipPlanExecutor::resolvePeers() {
     size_t at = 0;
     GLX_ENFORCE(getPod<uint32_t>(b, at) == kAlgMagic, "bad algorithm record from rank ", r);
     getPod<int64_t>(b, at);  // pid (already known from the endpoint)
+    const int32_t ralgo = getPod<int32_t>(b, at);
+    const int64_t rcount = getPod<int64_t>(b, at);
+    const int32_t rdtype = getPod<int32_t>(b, at);
+    const int32_t rop = getPod<int32_t>(b, at);
+    GLX_ENFORCE(ralgo == algo_ && rcount == count_ && rdtype == dtype_ && rop == op_,
+                "rank ", r, "'s algorithm in slot ", slot_, " (algorithm ", ralgo, ", count ",
+                rcount, ", dtype ", rdtype, ", op ", rop, ") differs from rank ", contextRank_,
+                "'s (algorithm ", algo_, ", count ", count_, ", dtype ", dtype_, ", op ", op_,
+                "): the ranks created their algorithms in different orders");
     const int32_t nblocks = getPod<int32_t>(b, at);
     bool needScratch = false;
     for (auto& oc : out_) needScratch = needScratch || oc.peer == r;
@@ -411,21 +470,19 @@ void HipPlanExecutor::resolvePeers() {
       blk.start = getPod<int64_t>(b, at);
       blk.elems = getPod<int64_t>(b, at);
       const uint64_t ptr = getPod<uint64_t>(b, at);
+      const int64_t id = getPod<int64_t>(b, at);
       const int32_t haveIpc = getPod<int32_t>(b, at);
       const hipIpcMemHandle_t h = getPod<hipIpcMemHandle_t>(b, at);
       if (!needScratch) continue;
       if (pe.sameProcess) {
         blk.ptr = reinterpret_cast<char*>((uintptr_t)ptr);
       } else {
-        GLX_ENFORCE(haveIpc, "rank ", r,
-                    " could not export its receive buffer (hipIpcGetMemHandle)");
-        void* p = nullptr;
-        GLX_TRACE("r%d resolve: hipIpcOpenMemHandle(rank %d, block %d, %ld elems)",
-                  contextRank_, r, k, (long)blk.elems);
-        GLX_HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
-        GLX_TRACE("r%d resolve: opened %p", contextRank_, p);
-        ipcOpened_.push_back(p);
-        blk.ptr = static_cast<char*>(p);
+        GLX_ENFORCE(haveIpc == 1, "rank ", r,
+                    " could not export its receive buffer: hipIpcGetMemHandle returned ",
+                    hipGetErrorName((hipError_t)-haveIpc));
+        blk.ptr = context_->importShared(r, id, h);
+        GLX_TRACE("r%d resolve: rank %d block %d (shared %ld, %ld elems) at %p", contextRank_,
+                  r, k, (long)id, (long)blk.elems, (void*)blk.ptr);
       }
       pb.push_back(blk);
     }
@@ -459,16 +516,15 @@ void HipPlanExecutor::resolvePeers() {
     std::vector<char*> blocks;
     for (int32_t k = 0; k < nb; k++) {
       const uint64_t ptr = getPod<uint64_t>(b, at);
+      const int64_t id = getPod<int64_t>(b, at);
       const int32_t haveIpc = getPod<int32_t>(b, at);
       const hipIpcMemHandle_t h = getPod<hipIpcMemHandle_t>(b, at);
       if (pe.sameProcess) {
         blocks.push_back(reinterpret_cast<char*>((uintptr_t)ptr));
       } else {
-        GLX_ENFORCE(haveIpc, "rank ", r, " could not export its device-engine block ", k);
-        void* p = nullptr;
-        GLX_HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
-        ipcOpened_.push_back(p);
-        blocks.push_back(static_cast<char*>(p));
+        GLX_ENFORCE(haveIpc == 1, "rank ", r, " could not export its device-engine block ", k,
+                    ": hipIpcGetMemHandle returned ", hipGetErrorName((hipError_t)-haveIpc));
+        blocks.push_back(context_->importShared(r, id, h));
       }
     }
     if (engine_ != kEngineSteps) ddPeer_[r] = blocks;
@@ -517,6 +573,19 @@ char* HipPlanExecutor::landing(const std::vector<ScratchBlock>& blocks, int64_t 
   return blk->ptr + at;
 }
 
+// Shared blocks are exported as soon as they are allocated; the handle goes
+// into the algorithm record (publish).
+char* HipPlanExecutor::allocShared(size_t bytes, unsigned flags, int64_t* id,
+                                   hipIpcMemHandle_t* h, int32_t* status) {
+  const SharedBlock b = context_->acquireShared(bytes, flags);
+  *id = b.id;
+  *h = b.ipc;
+  *status = b.ipcStatus;
+  GLX_TRACE("r%d shared block %ld (%zu bytes) at %p, export status %d", contextRank_,
+            (long)b.id, b.bytes, (void*)b.ptr, (int)b.ipcStatus);
+  return b.ptr;
+}
+
 void HipPlanExecutor::allocScratch(bool uncached) {
   if (plan_.scratch_elems <= 0) return;
   // region starts = where messages land
@@ -543,11 +612,8 @@ void HipPlanExecutor::allocScratch(bool uncached) {
   if (cur.elems > 0) blocks_.push_back(cur);
   for (auto& b : blocks_) {
     const size_t bytes = (size_t)b.elems * esize_ + 64;
-    if (uncached) {
-      GLX_HIP_CHECK(hipExtMallocWithFlags((void**)&b.ptr, bytes, hipDeviceMallocUncached));
-    } else {
-      GLX_HIP_CHECK(hipMalloc((void**)&b.ptr, bytes));
-    }
+    b.ptr = allocShared(bytes, uncached ? hipDeviceMallocUncached : 0u, &b.id, &b.ipc,
+                        &b.ipcStatus);
     GLX_HIP_CHECK(hipMemset(b.ptr, 0, bytes));
   }
   GLX_HIP_CHECK(hipDeviceSynchronize());
@@ -600,6 +666,7 @@ void HipPlanExecutor::waitFor(Pred done, const char* what, int peer) {
         warned = true;
       }
       if (now - start > timeout) {
+        broken_ = true;
         GLX_THROW_TIMEOUT(
             "Timed out waiting for ", what, " from rank ", peer, " (rank ",
             contextRank_, ", after ",
@@ -607,7 +674,12 @@ void HipPlanExecutor::waitFor(Pred done, const char* what, int peer) {
             " ms, timeout ", timeout.count(), " ms)");
       }
       if (now - lastAlive > std::chrono::milliseconds(200)) {
-        context_->checkPeersAlive();
+        try {
+          context_->checkPeersAlive();
+        } catch (...) {
+          broken_ = true;
+          throw;
+        }
         lastAlive = now;
       }
     }
@@ -1091,6 +1163,8 @@ int initialStepsEngine() {
   return -1;
 }
 
+constexpr int kDevStepsAutoMaxRanks = 4;
+
 int64_t devStepsMaxBytes() {
   const char* e = std::getenv("GLOO_AMD_DEVSTEPS_MAX_BYTES");
   return e != nullptr ? std::atoll(e) : (int64_t(32) << 20);
@@ -1150,6 +1224,11 @@ int HipPlanExecutor::engineFor(const Context& ctx, int algo, int64_t count, int 
       algo == glx::ALGO_FN_RING || algo == glx::ALGO_FN_BCUBE) {
     const int e = stepsEngine();
     if (e >= 0) return e;
+    // auto: the plan kernel for small and medium buffers at up to 4 ranks
+    // (validated on the GPU multi-process up to P=4; at P=8 on one shared
+    // GPU a run was seen to stall, so more ranks keep host-issued steps
+    // unless forced with set_steps_engine("device"))
+    if (ctx.size > kDevStepsAutoMaxRanks) return kEngineSteps;
     return count * esize <= devStepsMaxBytes() ? kEngineDevSteps : kEngineSteps;
   }
   return kEngineSteps;
@@ -1164,9 +1243,15 @@ char* HipPlanExecutor::ddAlloc(size_t bytes) {
     return (e != nullptr && std::strcmp(e, "finegrained") == 0) ? hipDeviceMallocFinegrained
                                                                  : hipDeviceMallocUncached;
   }();
-  char* d = nullptr;
-  GLX_HIP_CHECK(hipExtMallocWithFlags((void**)&d, bytes, flags));
+  hipIpcMemHandle_t h{};
+  int32_t st = 0;
+  int64_t id = 0;
+  char* d = allocShared(bytes, flags, &id, &h, &st);
+  ddIds_.push_back(id);
+  GLX_TRACE("r%d ddAlloc %zu bytes at %p", contextRank_, bytes, (void*)d);
   ddBlocks_.push_back(d);
+  ddIpc_.push_back(h);
+  ddIpcStatus_.push_back(st);
   GLX_HIP_CHECK(hipMemset(d, 0, bytes));
   return d;
 }
@@ -1367,8 +1452,16 @@ void HipPlanExecutor::checkDevice() {
   if (engine_ == kEngineSteps) return;
   const int st = *reinterpret_cast<volatile int*>(ddStatus_);
   if (st != 0) {
-    GLX_THROW_TIMEOUT("Timed out waiting for data from rank ", st - 1, " (rank ",
-                      contextRank_, ", device-driven allreduce, timeout ",
+    broken_ = true;
+    const int peer = (st & 255) - 1, step = (st >> 8) - 1;
+    std::string where;
+    if (step >= 0 && (size_t)step < plan_.steps.size()) {
+      const glx::Step& s = plan_.steps[(size_t)step];
+      where = std::string(", ") + (s.kind == glx::SEND ? "credit for send" : "receive") +
+              " step " + std::to_string(step) + " of run " + std::to_string(devRuns_ - 1);
+    }
+    GLX_THROW_TIMEOUT("Timed out waiting for data from rank ", peer, " (rank ", contextRank_,
+                      ", device-driven allreduce", where, ", timeout ",
                       effectiveTimeout().count(), " ms)");
   }
 }

@@ -123,6 +123,9 @@ class HipPlanExecutor : public Algorithm {
     int64_t start = 0;  // first element (in plan region coordinates)
     int64_t elems = 0;
     char* ptr = nullptr;
+    int64_t id = 0;           // the context's shared-block id (allocShared)
+    hipIpcMemHandle_t ipc{};  // exported at allocation (allocShared)
+    int32_t ipcStatus = 0;    // 1 exported, else -(hipError_t)
   };
   static constexpr size_t kMaxBlockBytes = size_t(256) << 20;
   struct InflightSend {
@@ -152,6 +155,12 @@ class HipPlanExecutor : public Algorithm {
                  const std::vector<hipStream_t>& streams, const glx::PlanParams& prm,
                  bool perCallBuffers);
   void release() noexcept;
+  // Before our memory is freed: wait (bounded by the context timeout) until
+  // every receiver has credited our last message.  Those credit stores are
+  // the only writes a peer can still make into our memory (shm counters or,
+  // for the plan kernel, device flag rows) after our last run returned.
+  void drainCredits() noexcept;
+  bool broken_ = false;  // a wait timed out or a peer exited
 
   glx::Plan plan_;
   int algo_;
@@ -201,7 +210,6 @@ class HipPlanExecutor : public Algorithm {
   bool resolved_ = false;
   std::vector<Pending> pending_;
   std::vector<InflightSend> inflight_;
-  std::vector<void*> ipcOpened_;
 
   // Device-driven engines (xgmi_kernels.hip): the replicated schedule as the
   // one-shot kernel, the mesh schedule as the two-shot kernel.  No channels,
@@ -211,6 +219,14 @@ class HipPlanExecutor : public Algorithm {
   //             [4] flags: A [P][G], then B [P][G]
   int engine_ = kEngineSteps;
   std::vector<char*> ddBlocks_;
+  std::vector<int64_t> ddIds_;            // ddBlocks_' shared-block ids
+  std::vector<hipIpcMemHandle_t> ddIpc_;  // ddBlocks_' exported handles
+  std::vector<int32_t> ddIpcStatus_;
+  // Device memory peers will map, from the context's pool of exported blocks
+  // (flags 0: hipMalloc, else hipExtMallocWithFlags); back to the pool in
+  // release().
+  char* allocShared(size_t bytes, unsigned flags, int64_t* id, hipIpcMemHandle_t* h,
+                    int32_t* status);
   std::map<int, std::vector<char*>> ddPeer_;  // peers' blocks (IPC-mapped)
   size_t ddSlot_ = 0;                         // bytes per landing slot
   glx::OneShotParams os_{};                   // fixed parts of the kernels' parameters

@@ -235,13 +235,15 @@ __device__ __forceinline__ void signal_flag(uint64_t* word, uint64_t value) {
 // the outcome.  Returns false after a timeout (status already set).
 __device__ __forceinline__ bool wait_flag(const uint64_t* word, uint64_t epoch, int peer,
                                           uint64_t start, uint64_t timeoutTicks, int* status,
-                                          int* s_ok, bool acquire = true) {
+                                          int* s_ok, bool acquire = true, int where = 0) {
   if (threadIdx.x == 0) {
     int ok = 1;
     while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
       if (__builtin_amdgcn_s_memrealtime() - start > timeoutTicks) {
         ok = 0;
-        __hip_atomic_store(status, 1 + peer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // 1 + peer, plus 256 * (1 + step) when the plan kernel says where
+        __hip_atomic_store(status, 1 + peer + 256 * where, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -413,7 +415,7 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
       case 0: {  // SEND, once the receiver has consumed message seq-1 of this slice
         if (seq > 1 && !wait_flag(st.credit + w, seq - 1, st.peer,
                                   __builtin_amdgcn_s_memrealtime(), p.timeoutTicks, p.status,
-                                  &s_ok, /*acquire=*/false)) {
+                                  &s_ok, /*acquire=*/false, 1 + i)) {
           return;
         }
         for (int g = st.seg0; g < st.seg1; g++) {
@@ -427,7 +429,7 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
       }
       case 1:  // RECV
         if (!wait_flag(st.flag + w, seq, st.peer, __builtin_amdgcn_s_memrealtime(),
-                       p.timeoutTicks, p.status, &s_ok)) {
+                       p.timeoutTicks, p.status, &s_ok, true, 1 + i)) {
           return;
         }
         break;

@@ -200,6 +200,8 @@ def run_devsteps(store_dir, rank, size):
         # the plan kernel, or host-issued steps where a landing region would
         # be shared across workgroups (glx_plan_sync "safe")
         engines.add(alg.engine())
+        print("case %d kind %d n %d dtype %d op %d engine %s" % (seed, kind, n, dt, op,
+                                                                 alg.engine()), flush=True)
         if alg.engine() not in ("devsteps", "steps"):
             bad.append(("engine", kind, n, alg.engine()))
         for it in range(3):
