@@ -27,14 +27,17 @@ class Clobber(Exception):
     pass
 
 
-def simulate(name, P, N, G, op, ins, runs=2):
-    es = 4
-    progs = [gloo_amd.plan(name, r, P, N, with_folds=True) for r in range(P)]
-    syncs = [gloo_amd.plan_sync(name, r, P, N, G) for r in range(P)]
+def simulate(name, P, N, G, op, ins, runs=2, es=4):
+    """es: the element size the programs and bookkeeping are compiled for
+    (chunk phases and the 16-byte landing rule depend on it); the values
+    themselves are simulated as float32."""
+    V = 16 // es
+    progs = [gloo_amd.plan(name, r, P, N, with_folds=True, esize=es) for r in range(P)]
+    syncs = [gloo_amd.plan_sync(name, r, P, N, G, esize=es) for r in range(P)]
     bounds, sl = syncs[0]["bounds"], syncs[0]["slice"]
     assert all(s["bounds"] == bounds and s["slice"] == sl for s in syncs)
     assert bounds[0] == 0 and bounds[-1] == N and bounds == sorted(set(bounds))
-    assert sl % (16 // es) == 0 and G * sl >= max(b - a for a, b in zip(bounds, bounds[1:]))
+    assert sl % V == 0 and G * sl >= max(b - a for a, b in zip(bounds, bounds[1:]))
 
     def parts(s0, s1, w):
         for g in range(s0, s1):
@@ -58,7 +61,7 @@ def simulate(name, P, N, G, op, ins, runs=2):
         in_ch.append(ic)
     bufs = [np.array(ins[r][0], copy=True) for r in range(P)]
     # landing regions in element units; element x of a message for
-    # ptr0[a...] at region + (a mod 4) + (x - a), as the 16-byte landing rule
+    # ptr0[a...] at region + (a mod V) + (x - a), as the 16-byte landing rule
     size = [progs[r][1] + N + 64 for r in range(P)]
     scratch = [np.zeros(size[r], dtype=np.float32) for r in range(P)]
     pending = [np.zeros(size[r], dtype=bool) for r in range(P)]  # written, not yet read
@@ -68,7 +71,7 @@ def simulate(name, P, N, G, op, ins, runs=2):
     run = [[0] * G for _ in range(P)]
 
     def pos(base, a, x):
-        return base + a % 4 + (x - a)
+        return base + a % V + (x - a)
 
     def read(r, base, a, lo, hi):
         i, j = pos(base, a, lo), pos(base, a, hi)
