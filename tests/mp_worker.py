@@ -41,6 +41,8 @@ def main():
         return run_device_timeout(store_dir, rank, size)
     if algo == "devsteps":
         return run_devsteps(store_dir, rank, size)
+    if algo == "churn":
+        return run_churn(store_dir, rank, size)
     if algo.startswith("fn_"):
         return run_fn(store_dir, rank, size, algo, N)
     code = O.HALVING_DOUBLING if algo == "halving_doubling" else O.RING_CHUNKED
@@ -152,6 +154,65 @@ def run_device_timeout(store_dir, rank, size):
     ctx.close()
     if not ok:
         print("MISMATCH rank", rank)
+        sys.exit(1)
+    print("OK")
+
+
+def run_churn(store_dir, rank, size):
+    """Many algorithms created, run and destroyed back to back on every
+    engine (shared blocks come from the context's pool and are reused while
+    peers may still be finishing the previous algorithm): every result
+    bit-exact, and no file descriptors accumulate (IPC in dmabuf mode passes
+    them)."""
+    import numpy as np
+    import torch
+
+    import gloo_amd
+    from helpers import case_inputs
+    from oracle import oracle as O
+
+    store = gloo_amd.rendezvous.FileStore(store_dir)
+    ctx = gloo_amd.rendezvous.Context(rank, size, 0)
+    ctx.setTimeout(30)
+    ctx.connectFullMesh(store)
+
+    def nfd():
+        return len(os.listdir("/proc/self/fd"))
+
+    kinds = [("replicated", "auto"), ("mesh", "auto"), ("ring", "device"), ("ring", "host"),
+             ("hd", "device"), ("hd", "host")]
+    sizes = [1000, 4096, 65539, 12345, 1 << 16, 777]
+    bad, fds = [], []
+    for it in range(36):
+        sched, eng = kinds[it % len(kinds)]
+        n = sizes[(it // len(kinds)) % len(sizes)]
+        ins = case_inputs(size, n, O.FLOAT32, 1, 0, seed=500 + it)
+        kind = O.HALVING_DOUBLING if sched == "hd" else O.RING_CHUNKED
+        exp = O.allreduce(kind, O.SUM, O.FLOAT32, ins)[rank][0]
+        buf = torch.from_numpy(ins[rank][0].copy()).cuda()
+        torch.cuda.synchronize()
+        gloo_amd.set_steps_engine(eng)
+        if sched == "hd":
+            alg = gloo_amd.AllreduceHalvingDoubling(ctx, [buf])
+        else:
+            alg = gloo_amd.AllreduceRingChunked(ctx, [buf], schedule=sched)
+        gloo_amd.set_steps_engine("auto")
+        for r in range(2):
+            buf.copy_(torch.from_numpy(ins[rank][0]))
+            torch.cuda.synchronize()
+            alg.run()
+            got = buf.cpu().numpy()
+            if not np.array_equal(got.view(np.uint32), exp.view(np.uint32)):
+                bad.append((it, sched, eng, n, alg.engine(), r))
+        alg.close()
+        fds.append(nfd())
+    ctx.close()
+    print("fds", fds[:3], "...", fds[-3:])
+    if bad:
+        print("MISMATCH rank", rank, bad[:10])
+        sys.exit(1)
+    if fds[-1] > fds[5] + 8:
+        print("FD LEAK rank", rank, fds)
         sys.exit(1)
     print("OK")
 

@@ -287,6 +287,33 @@ def test_device_engine_multiprocess(P, mode):
             assert "OK" in outs[r]
 
 
+@pytest.mark.parametrize("P", [2, 4])
+def test_algorithm_churn_multiprocess(P):
+    """36 algorithms created, run twice and destroyed back to back per rank
+    on every engine (one-shot, two-shot, plan kernel, host steps; ring and
+    halving-doubling): shared blocks are pooled and reused across them while
+    peers may still be finishing, so this checks the drain-before-reuse and
+    pooling rules: bit-exact results, no fd growth."""
+    with tempfile.TemporaryDirectory() as d:
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), "churn"],
+                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                 for r in range(P)]
+        outs = []
+        for p in procs:
+            try:
+                o, _ = p.communicate(timeout=240)
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+            outs.append(o.decode(errors="replace"))
+        for r, p in enumerate(procs):
+            print(outs[r])
+            assert p.returncode == 0, "rank %d failed:\n%s" % (r, outs[r])
+            assert "OK" in outs[r]
+
+
 def test_device_engine_timeout_raises_io_exception():
     """A device-driven kernel whose peers never arrive gives up after the
     context timeout (every wave exits), and run() raises IoException."""
