@@ -1264,9 +1264,11 @@ void HipPlanExecutor::setupDevice() {
   } else {
     setupDevSteps();
   }
-  GLX_HIP_CHECK(hipHostMalloc((void**)&ddStatus_, sizeof(int),
+  // status int, then (as 64-bit words 1..3) the flag value seen, the value
+  // awaited and the workgroup of a timed-out wait
+  GLX_HIP_CHECK(hipHostMalloc((void**)&ddStatus_, 4 * sizeof(uint64_t),
                               hipHostMallocMapped | hipHostMallocCoherent));
-  *reinterpret_cast<volatile int*>(ddStatus_) = 0;
+  std::memset(ddStatus_, 0, 4 * sizeof(uint64_t));
   GLX_HIP_CHECK(hipHostGetDevicePointer((void**)&ddStatusDev_, ddStatus_, 0));
   os_.status = ddStatusDev_;
   ts_.status = ddStatusDev_;
@@ -1460,9 +1462,10 @@ void HipPlanExecutor::checkDevice() {
       where = std::string(", ") + (s.kind == glx::SEND ? "credit for send" : "receive") +
               " step " + std::to_string(step) + " of run " + std::to_string(devRuns_ - 1);
     }
+    const volatile uint64_t* d = reinterpret_cast<const volatile uint64_t*>(ddStatus_);
     GLX_THROW_TIMEOUT("Timed out waiting for data from rank ", peer, " (rank ", contextRank_,
-                      ", device-driven allreduce", where, ", timeout ",
-                      effectiveTimeout().count(), " ms)");
+                      ", device-driven allreduce", where, ": workgroup ", d[3], " saw ", d[1],
+                      ", awaited ", d[2], ", timeout ", effectiveTimeout().count(), " ms)");
   }
 }
 

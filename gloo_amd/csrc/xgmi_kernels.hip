@@ -241,7 +241,15 @@ __device__ __forceinline__ bool wait_flag(const uint64_t* word, uint64_t epoch, 
     while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
       if (__builtin_amdgcn_s_memrealtime() - start > timeoutTicks) {
         ok = 0;
-        // 1 + peer, plus 256 * (1 + step) when the plan kernel says where
+        // 1 + peer, plus 256 * (1 + step) when the plan kernel says where;
+        // the words after it: the value seen, the value awaited, the workgroup
+        uint64_t* detail = reinterpret_cast<uint64_t*>(status);
+        __hip_atomic_store(detail + 1,
+                           __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(detail + 2, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(detail + 3, (uint64_t)blockIdx.x, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(status, 1 + peer + 256 * where, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
         break;
