@@ -32,13 +32,24 @@ def main():
     ctx.setTimeout(60)
     ctx.connectFullMesh(store)
     gloo_amd.set_steps_engine("device")
+    # EXTRA_STREAMS=k: k more streams with a kernel each before the cases
+    # (more hardware queues per process, as host-steps algorithms create)
+    keep = []
+    for _ in range(int(os.environ.get("EXTRA_STREAMS", "0"))):
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            keep.append(torch.ones(1024, device="cuda") * 2)
+        keep.append(st)
+    torch.cuda.synchronize()
+    reps = int(os.environ.get("REPEAT", "1"))
     cases = []
     if os.environ.get("WITH_F32") == "1":  # the worker's f32 series first
         for n in (1, 3, 255, 256, 1000, 4099, 65539, 1 << 20, (1 << 22) + 5):
             cases.append((n, O.FLOAT32, O.SUM))
-    for dt in (O.FLOAT16, O.BFLOAT16, O.INT32, O.FLOAT64):
-        for op in (O.SUM, O.PRODUCT, O.MAX, O.MIN):
-            cases.append((4099, dt, op))
+    for _ in range(reps):
+        for dt in (O.FLOAT16, O.BFLOAT16, O.INT32, O.FLOAT64):
+            for op in (O.SUM, O.PRODUCT, O.MAX, O.MIN):
+                cases.append((4099, dt, op))
     nbad = 0
     for seed, (n, dt, op) in enumerate(cases):
         ins = case_inputs(size, n, dt, 1, 0, seed=300 + seed)
