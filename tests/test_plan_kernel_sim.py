@@ -209,3 +209,20 @@ def test_unsafe_program_is_detected_and_would_clobber():
     ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=93)
     with pytest.raises(Clobber):
         simulate("ring_chunked", P, N, G, O.SUM, ins)
+
+
+@pytest.mark.parametrize("es", [2, 8])
+@pytest.mark.parametrize("name", ["ring_chunked", "halving_doubling"])
+@pytest.mark.parametrize("P", [3, 8])
+@pytest.mark.parametrize("N,G", [(4099, 1), (65536, 4), (77777, 1)])
+def test_plan_kernel_protocol_other_element_sizes(es, name, P, N, G):
+    """2- and 8-byte elements: other chunk phases and 16-byte landing offsets
+    (the values are simulated as float32; for these two schedules only the
+    bookkeeping depends on the element size, not the reduction order)."""
+    if not all(gloo_amd.plan_sync(name, r, P, N, G, esize=es)["safe"] for r in range(P)):
+        pytest.skip("the executor keeps host-issued steps for this program")
+    ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=94)
+    got = simulate(name, P, N, G, O.SUM, ins, es=es)
+    exp = expected(name, P, O.SUM, ins, 2)
+    for r in range(P):
+        assert same_bits(got[r], exp[r][0]), "rank %d" % r
