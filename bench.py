@@ -600,8 +600,14 @@ def bench_multi(args):
                            "busiest_link_GBps": round(lm / ta / 1e9, 2)}
     staged = None
     if args.staged:
+        # host buffers: the fastest host-issued schedule (its H2D / D2H
+        # overlap the steps); the device engines stage the whole buffer first
+        host_cands = [a for a in candidates if ENGINES.get(a) == "steps"] or [chosen]
+        staged_algo = min(host_cands, key=lambda a: runs[a]["t"])
         staged, err = attempt("host-staged", lambda: host_endpoint_rate(
-            torch, dist, gloo_amd, ctx, src, dev_result, chosen, reps=min(steps, 5)))
+            torch, dist, gloo_amd, ctx, src, dev_result, staged_algo, reps=min(steps, 5)))
+        if staged is not None:
+            staged["schedule"] = staged_algo
         if not agreed(err is None):
             staged, failed["host_staged"] = None, err or "failed on another rank"
     sweep = None
