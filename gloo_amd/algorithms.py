@@ -192,8 +192,10 @@ class AllreduceRingChunked(Algorithm):
     """gloo::AllreduceRingChunked<T> (gloo/allreduce_ring_chunked.h:19) on
     MI355X: xGMI peer copies + HIP reduce kernel, same chunking and order.
 
-    schedule="auto" (default) picks the data movement by size (replicated up
-    to 256 KiB per rank, mesh above; env GLOO_AMD_RING_SCHEDULE forces one).
+    schedule="auto" (default) picks the data movement by size: replicated
+    up to 16 MiB per rank at P=2, 2 MiB at P<=4, 1 MiB at P<=8 when the
+    device-driven engines are available (256 KiB otherwise), mesh above;
+    env GLOO_AMD_RING_SCHEDULE forces one.
     schedule="ring" moves chunks around the ring exactly as the
     reference does (one link per direction); schedule="mesh" computes the
     identical result (same chunks, same reduction chain and operand order)
