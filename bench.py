@@ -283,9 +283,7 @@ def make_alg(gloo_amd, ctx, buf, algo):
     if algo.endswith("_host"):
         engine, algo = "host", algo[:-len("_host")]
     elif algo in ("ring_chunked", "halving_doubling"):
-        # the plan kernel where it is validated on the GPU (<= 4 ranks);
-        # above, the library's own choice (host-issued steps)
-        engine = "device" if int(os.environ.get("WORLD_SIZE", "1")) <= 4 else "auto"
+        engine = "device"  # the plan kernel (the step program in one kernel per rank)
     if engine is not None:
         gloo_amd.set_steps_engine(engine)
     try:

@@ -14,6 +14,8 @@
 
 #include <atomic>
 #include <cstring>
+#include <chrono>
+#include <cstdlib>
 #include <thread>
 
 #include "common.h"
@@ -144,19 +146,11 @@ Context::Context(int rank_, int size_, int device) : rank(rank_), size(size_), d
 Context::~Context() {
   if (shared_.empty() && imported_.empty()) return;
   if (device_ >= 0) hipSetDevice(device_);
-  for (auto& kv : imported_) hipIpcCloseMemHandle(kv.second);
+  for (auto& kv : imported_) hipIpcCloseMemHandle(kv.second.opened);
   for (auto& b : shared_) hipFree(b.ptr);
 }
 
 namespace {
-int32_t exportBlock(hipIpcMemHandle_t* h, void* p) {
-  std::memset(h, 0, sizeof(*h));
-  const hipError_t e = hipIpcGetMemHandle(h, p);
-  if (e == hipSuccess) return 1;
-  (void)hipGetLastError();
-  return -(int32_t)e;
-}
-
 char* allocBlock(size_t bytes, unsigned flags) {
   char* d = nullptr;
   if (flags != 0) {
@@ -169,23 +163,50 @@ char* allocBlock(size_t bytes, unsigned flags) {
 
 // Free pooled bytes kept beyond this are returned to the runtime.
 constexpr size_t kMaxFreeSharedBytes = size_t(8) << 30;
+// The canary word's line, after a block's usable bytes.
+constexpr size_t kCanaryBytes = 128;
+
+// Allocation granule of a shared block (GLOO_AMD_SHARED_GRANULE, bytes;
+// default 2 MiB).  With a block of its own per allocation the exported
+// pointer is the allocation's base; smaller blocks may be placed by the
+// runtime inside a larger buffer -- the canary check and the
+// published base offset cover that case too.
+size_t sharedGranule() {
+  static const size_t g = [] {
+    const char* e = std::getenv("GLOO_AMD_SHARED_GRANULE");
+    const long long v = e != nullptr ? std::atoll(e) : 0;
+    return v >= 4096 ? (size_t)v : (size_t(2) << 20);
+  }();
+  return g;
+}
+
+std::atomic<uint64_t> g_canary_counter{0};
+
+uint64_t makeCanary(int rank, int64_t id) {
+  // splitmix64 of (pid, rank, id, a process-wide counter, the clock)
+  uint64_t x = ((uint64_t)::getpid() << 32) ^ ((uint64_t)rank << 20) ^ (uint64_t)id ^
+               (g_canary_counter.fetch_add(1) << 44) ^
+               (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+  x += 0x9e3779b97f4a7c15ull;
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+  x ^= x >> 31;
+  return x == 0 ? 1 : x;
+}
 }  // namespace
 
 SharedBlock Context::acquireShared(size_t bytes, unsigned flags) {
-  // Whole 2 MiB granules: the runtime places smaller allocations side by side
-  // in one underlying buffer (seen 4 KiB apart), and a peer that imports such
-  // a block through IPC was seen to get a mapping that does not point at it
-  // (flags and data landing in the neighbouring block).  A block of its own
-  // maps exactly.
-  constexpr size_t kGranule = size_t(2) << 20;
-  bytes = (std::max<size_t>(bytes, 1) + kGranule - 1) / kGranule * kGranule;
+  const size_t granule = sharedGranule();
+  const size_t alloc =
+      (std::max<size_t>(bytes, 1) + kCanaryBytes + granule - 1) / granule * granule;
+  bytes = alloc - kCanaryBytes;
   std::lock_guard<std::mutex> g(sharedMutex_);
   // the smallest free block of this kind that fits without wasting much
   SharedBlock* best = nullptr;
   const size_t most = std::max(2 * bytes, bytes + (size_t(4) << 20));
   for (auto& b : shared_) {
     if (!b.inUse && b.flags == flags && b.bytes >= bytes && b.bytes <= most &&
-        (size == 1 || b.ipcStatus == 1) && (best == nullptr || b.bytes < best->bytes)) {
+        (best == nullptr || b.bytes < best->bytes)) {
       best = &b;
     }
   }
@@ -196,23 +217,32 @@ SharedBlock Context::acquireShared(size_t bytes, unsigned flags) {
   SharedBlock nb;
   nb.bytes = bytes;
   nb.flags = flags;
-  nb.ptr = allocBlock(bytes, flags);
+  nb.ptr = allocBlock(alloc, flags);
+  nb.ref.ptr = (uint64_t)(uintptr_t)nb.ptr;
+  nb.ref.id = nextSharedId_++;
   if (size > 1) {
-    // A refused export is retried after a pause, then with a fresh block
-    // (the refused one held meanwhile so that the address range differs).
-    std::vector<char*> refused;
-    for (int attempt = 0; attempt < 8; attempt++) {
-      nb.ipcStatus = exportBlock(&nb.ipc, nb.ptr);
-      if (nb.ipcStatus == 1) break;
-      std::this_thread::sleep_for(std::chrono::milliseconds(1 + attempt));
-      if (attempt == 3) {
-        refused.push_back(nb.ptr);
-        nb.ptr = allocBlock(bytes, flags);
-      }
+    std::memset(&nb.ref.ipc, 0, sizeof(nb.ref.ipc));
+    const hipError_t e = hipIpcGetMemHandle(&nb.ref.ipc, nb.ptr);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      hipFree(nb.ptr);
+      GLX_ENFORCE(false, "rank ", rank, ": hipIpcGetMemHandle of a ", alloc,
+                  "-byte shared block refused: ", hipGetErrorName(e), " (", hipGetErrorString(e),
+                  ")");
     }
-    for (char* r : refused) hipFree(r);
+    nb.ref.ipcStatus = 1;
+    void* base = nullptr;
+    size_t range = 0;
+    if (hipMemGetAddressRange(&base, &range, nb.ptr) == hipSuccess && base != nullptr) {
+      nb.ref.baseOff = (uint64_t)(nb.ptr - static_cast<char*>(base));
+    } else {
+      (void)hipGetLastError();
+    }
+    nb.ref.canaryOff = bytes;
+    nb.ref.canary = makeCanary(rank, nb.ref.id);
+    GLX_HIP_CHECK(hipMemcpy(nb.ptr + nb.ref.canaryOff, &nb.ref.canary, sizeof(uint64_t),
+                            hipMemcpyHostToDevice));
   }
-  nb.id = nextSharedId_++;
   nb.inUse = true;
   shared_.push_back(nb);
   return nb;
@@ -222,7 +252,7 @@ void Context::releaseShared(int64_t id) {
   std::lock_guard<std::mutex> g(sharedMutex_);
   size_t freeBytes = 0;
   for (auto& b : shared_) {
-    if (b.id == id) b.inUse = false;
+    if (b.ref.id == id) b.inUse = false;
     if (!b.inUse) freeBytes += b.bytes;
   }
   // over the cap: return the largest free blocks (peers that imported them
@@ -239,14 +269,42 @@ void Context::releaseShared(int64_t id) {
   }
 }
 
-char* Context::importShared(int r, int64_t id, const hipIpcMemHandle_t& h) {
+char* Context::importShared(int r, const SharedRef& ref) {
   std::lock_guard<std::mutex> g(sharedMutex_);
-  auto it = imported_.find({r, id});
-  if (it != imported_.end()) return it->second;
+  auto it = imported_.find({r, ref.id});
+  if (it != imported_.end()) return it->second.ptr;
+  GLX_ENFORCE(ref.ipcStatus == 1, "rank ", r, " published shared block ", ref.id,
+              " without an IPC handle");
   void* p = nullptr;
-  GLX_HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
-  imported_[{r, id}] = static_cast<char*>(p);
-  return static_cast<char*>(p);
+  GLX_HIP_CHECK(hipIpcOpenMemHandle(&p, ref.ipc, hipIpcMemLazyEnablePeerAccess));
+  auto canaryAt = [&](const char* at) -> uint64_t {
+    uint64_t v = 0;
+    const hipError_t e = hipMemcpy(&v, at + ref.canaryOff, sizeof(v), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      return 0;
+    }
+    return v;
+  };
+  char* at = static_cast<char*>(p);
+  const uint64_t seen = canaryAt(at);
+  ipcImports_++;
+  if (seen != ref.canary) {
+    // the runtime may hand back the base of the exporter's allocation
+    // rather than the exported pointer inside it
+    if (ref.baseOff != 0 && canaryAt(at + ref.baseOff) == ref.canary) {
+      at += ref.baseOff;
+      ipcBaseFixups_++;
+    } else {
+      hipIpcCloseMemHandle(p);
+      GLX_ENFORCE(false, "rank ", rank, ": the IPC mapping of rank ", r, "'s shared block ",
+                  ref.id, " does not hold its canary (read 0x", std::hex, seen, ", expected 0x",
+                  ref.canary, std::dec, "; block at offset ", ref.baseOff,
+                  " in its allocation): the mapping is not the exporter's memory");
+    }
+  }
+  imported_[{r, ref.id}] = Imported{p, at};
+  return at;
 }
 
 void Context::clearOps() {

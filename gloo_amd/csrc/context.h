@@ -80,14 +80,25 @@ struct PeerEndpoint {
   std::unique_ptr<ControlBlock> ctl;  // mapped peer control block
 };
 
+// What a peer needs to map one of our shared device blocks (published in
+// algorithm records).
+struct SharedRef {
+  uint64_t ptr = 0;         // our address (threads of our process use it as is)
+  int64_t id = 0;           // unique within the exporting context, never reused
+  int32_t ipcStatus = 0;    // 1 exported (always, when the context has peers)
+  hipIpcMemHandle_t ipc{};  // hipIpcGetMemHandle(ptr)
+  uint64_t canaryOff = 0;   // the canary word sits at ptr + canaryOff
+  uint64_t canary = 0;      // its value, written by the exporter at allocation
+  uint64_t baseOff = 0;     // ptr - base of the runtime allocation holding it
+                            // (hipMemGetAddressRange)
+};
+
 // Device memory peers map (receive regions, landing slots, flag rows).
 struct SharedBlock {
-  int64_t id = 0;  // unique within the exporting context, never reused
   char* ptr = nullptr;
-  size_t bytes = 0;
-  unsigned flags = 0;       // 0: hipMalloc, else hipExtMallocWithFlags
-  hipIpcMemHandle_t ipc{};  // exported when the context has peers
-  int32_t ipcStatus = 0;    // 1 exported, else -(hipError_t)
+  size_t bytes = 0;     // usable bytes (the canary lies beyond them)
+  unsigned flags = 0;   // 0: hipMalloc, else hipExtMallocWithFlags
+  SharedRef ref;
   bool inUse = false;
 };
 
@@ -132,9 +143,19 @@ class Context {
   // and destroying algorithms then costs no IPC export / import / close
   // after the first few -- those calls are slow and, with many processes
   // exporting at once, were seen to fail.
+  //
+  // Every exported block carries a canary word beyond its usable bytes; an
+  // importer checks it before using the mapping and throws EnforceNotMet if
+  // the mapping does not hold it (a mapping of some other memory would
+  // otherwise corrupt data or lose flags silently).
   SharedBlock acquireShared(size_t bytes, unsigned flags);
   void releaseShared(int64_t id);
-  char* importShared(int rank, int64_t id, const hipIpcMemHandle_t& h);
+  char* importShared(int rank, const SharedRef& ref);
+  // Imports whose mapping the runtime returned at the base of the exporter's
+  // allocation instead of at the exported pointer (the canary was found at
+  // baseOff further on), and imports checked in all.
+  int64_t ipcBaseFixups() const { return ipcBaseFixups_; }
+  int64_t ipcImports() const { return ipcImports_; }
 
   // Executors of function-style collectives by options key (see
   // collectives.cc).  They hold a reference to this context: clearOps()
@@ -155,7 +176,12 @@ class Context {
   std::mutex sharedMutex_;
   std::vector<SharedBlock> shared_;
   int64_t nextSharedId_ = 1;
-  std::map<std::pair<int, int64_t>, char*> imported_;
+  struct Imported {
+    void* opened;  // what hipIpcOpenMemHandle returned (closed at the end)
+    char* ptr;     // the exporter's block
+  };
+  std::map<std::pair<int, int64_t>, Imported> imported_;
+  int64_t ipcBaseFixups_ = 0, ipcImports_ = 0;
 };
 
 }  // namespace gloo

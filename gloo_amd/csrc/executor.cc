@@ -37,6 +37,28 @@ T getPod(const std::vector<char>& b, size_t& at) {
   return v;
 }
 
+void putRef(std::vector<char>& b, const SharedRef& r) {
+  putPod(b, r.ptr);
+  putPod(b, r.id);
+  putPod(b, r.ipcStatus);
+  putPod(b, r.ipc);
+  putPod(b, r.canaryOff);
+  putPod(b, r.canary);
+  putPod(b, r.baseOff);
+}
+
+SharedRef getRef(const std::vector<char>& b, size_t& at) {
+  SharedRef r;
+  r.ptr = getPod<uint64_t>(b, at);
+  r.id = getPod<int64_t>(b, at);
+  r.ipcStatus = getPod<int32_t>(b, at);
+  r.ipc = getPod<hipIpcMemHandle_t>(b, at);
+  r.canaryOff = getPod<uint64_t>(b, at);
+  r.canary = getPod<uint64_t>(b, at);
+  r.baseOff = getPod<uint64_t>(b, at);
+  return r;
+}
+
 enum { DIR_IN = 0, DIR_OUT = 1 };
 
 // A SEND is split only when every part is at least this big.
@@ -309,18 +331,18 @@ void HipPlanExecutor::drainCredits() noexcept {
         }
       }
       const size_t G = (size_t)pk_.G;
-      std::vector<uint64_t> row(G);
+      std::vector<uint64_t> row(G * glx::kFlagStride);
       for (size_t c = 0; c < out_.size(); c++) {
-        const uint64_t* dev =
-            reinterpret_cast<const uint64_t*>(ddBlocks_[0]) + (size_t)out_[c].creditWord * G;
+        const uint64_t* dev = reinterpret_cast<const uint64_t*>(ddBlocks_[0]) +
+                              (size_t)out_[c].creditWord * G * glx::kFlagStride;
         for (;;) {
-          if (hipMemcpy(row.data(), dev, G * sizeof(uint64_t), hipMemcpyDeviceToHost) !=
+          if (hipMemcpy(row.data(), dev, G * glx::kFlagBytes, hipMemcpyDeviceToHost) !=
               hipSuccess) {
             (void)hipGetLastError();
             break;
           }
           bool done = true;
-          for (size_t w = 0; w < G && done; w++) done = row[w] >= want[c];
+          for (size_t w = 0; w < G && done; w++) done = row[w * glx::kFlagStride] >= want[c];
           if (done || std::chrono::steady_clock::now() >= deadline) break;
           context_->checkPeersAlive();  // throws if a peer exited: stop waiting
           pause();
@@ -358,10 +380,11 @@ void HipPlanExecutor::release() noexcept {
   }
   if (computeMark_) hipEventDestroy(computeMark_);
   for (auto& b : blocks_) {
-    if (b.id > 0) context_->releaseShared(b.id);
+    if (b.ref.id > 0) context_->releaseShared(b.ref.id);
   }
-  for (int64_t id : ddIds_) context_->releaseShared(id);
+  for (const SharedRef& r : ddRefs_) context_->releaseShared(r.id);
   if (ddStatus_) hipHostFree(ddStatus_);
+  if (ddClaim_) hipFree(ddClaim_);
   if (trace_) hipHostFree(trace_);
   if (ddDone_) hipEventDestroy(ddDone_);
   for (auto& c : copies_) hipStreamDestroy(c.s);
@@ -405,10 +428,7 @@ void HipPlanExecutor::publish() {
   for (const auto& blk : blocks_) {
     putPod<int64_t>(b, blk.start);
     putPod<int64_t>(b, blk.elems);
-    putPod<uint64_t>(b, (uint64_t)(uintptr_t)blk.ptr);
-    putPod<int64_t>(b, blk.id);
-    putPod<int32_t>(b, blk.ipcStatus);
-    putPod(b, blk.ipc);
+    putRef(b, blk.ref);
   }
   putPod<int32_t>(b, (int32_t)(in_.size() + out_.size()));
   for (auto& ic : in_) {
@@ -425,12 +445,7 @@ void HipPlanExecutor::publish() {
   }
   putPod<int32_t>(b, engine_);
   putPod<int32_t>(b, (int32_t)ddBlocks_.size());
-  for (size_t k = 0; k < ddBlocks_.size(); k++) {
-    putPod<uint64_t>(b, (uint64_t)(uintptr_t)ddBlocks_[k]);
-    putPod<int64_t>(b, ddIds_[k]);
-    putPod<int32_t>(b, ddIpcStatus_[k]);
-    putPod(b, ddIpc_[k]);
-  }
+  for (size_t k = 0; k < ddBlocks_.size(); k++) putRef(b, ddRefs_[k]);
   context_->store().set(
       "glx/alg/" + std::to_string(slot_) + "/" + std::to_string(contextRank_), b);
 }
@@ -469,20 +484,14 @@ void HipPlanExecutor::resolvePeers() {
       ScratchBlock blk;
       blk.start = getPod<int64_t>(b, at);
       blk.elems = getPod<int64_t>(b, at);
-      const uint64_t ptr = getPod<uint64_t>(b, at);
-      const int64_t id = getPod<int64_t>(b, at);
-      const int32_t haveIpc = getPod<int32_t>(b, at);
-      const hipIpcMemHandle_t h = getPod<hipIpcMemHandle_t>(b, at);
+      blk.ref = getRef(b, at);
       if (!needScratch) continue;
       if (pe.sameProcess) {
-        blk.ptr = reinterpret_cast<char*>((uintptr_t)ptr);
+        blk.ptr = reinterpret_cast<char*>((uintptr_t)blk.ref.ptr);
       } else {
-        GLX_ENFORCE(haveIpc == 1, "rank ", r,
-                    " could not export its receive buffer: hipIpcGetMemHandle returned ",
-                    hipGetErrorName((hipError_t)-haveIpc));
-        blk.ptr = context_->importShared(r, id, h);
+        blk.ptr = context_->importShared(r, blk.ref);
         GLX_TRACE("r%d resolve: rank %d block %d (shared %ld, %ld elems) at %p", contextRank_,
-                  r, k, (long)id, (long)blk.elems, (void*)blk.ptr);
+                  r, k, (long)blk.ref.id, (long)blk.elems, (void*)blk.ptr);
       }
       pb.push_back(blk);
     }
@@ -515,16 +524,11 @@ void HipPlanExecutor::resolvePeers() {
     const int32_t nb = getPod<int32_t>(b, at);
     std::vector<char*> blocks;
     for (int32_t k = 0; k < nb; k++) {
-      const uint64_t ptr = getPod<uint64_t>(b, at);
-      const int64_t id = getPod<int64_t>(b, at);
-      const int32_t haveIpc = getPod<int32_t>(b, at);
-      const hipIpcMemHandle_t h = getPod<hipIpcMemHandle_t>(b, at);
+      const SharedRef ref = getRef(b, at);
       if (pe.sameProcess) {
-        blocks.push_back(reinterpret_cast<char*>((uintptr_t)ptr));
+        blocks.push_back(reinterpret_cast<char*>((uintptr_t)ref.ptr));
       } else {
-        GLX_ENFORCE(haveIpc == 1, "rank ", r, " could not export its device-engine block ", k,
-                    ": hipIpcGetMemHandle returned ", hipGetErrorName((hipError_t)-haveIpc));
-        blocks.push_back(context_->importShared(r, id, h));
+        blocks.push_back(context_->importShared(r, ref));
       }
     }
     if (engine_ != kEngineSteps) ddPeer_[r] = blocks;
@@ -533,10 +537,14 @@ void HipPlanExecutor::resolvePeers() {
       uint64_t* rows = reinterpret_cast<uint64_t*>(blocks[0]);
       const size_t G = (size_t)pk_.G;
       for (auto& oc : out_) {
-        if (oc.peer == r && oc.peerRow >= 0) oc.devDelivery = rows + (size_t)oc.peerRow * G;
+        if (oc.peer == r && oc.peerRow >= 0) {
+          oc.devDelivery = rows + (size_t)oc.peerRow * G * glx::kFlagStride;
+        }
       }
       for (auto& ic : in_) {
-        if (ic.peer == r && ic.peerRow >= 0) ic.devCredit = rows + (size_t)ic.peerRow * G;
+        if (ic.peer == r && ic.peerRow >= 0) {
+          ic.devCredit = rows + (size_t)ic.peerRow * G * glx::kFlagStride;
+        }
       }
     }
   }
@@ -575,14 +583,11 @@ char* HipPlanExecutor::landing(const std::vector<ScratchBlock>& blocks, int64_t 
 
 // Shared blocks are exported as soon as they are allocated; the handle goes
 // into the algorithm record (publish).
-char* HipPlanExecutor::allocShared(size_t bytes, unsigned flags, int64_t* id,
-                                   hipIpcMemHandle_t* h, int32_t* status) {
+char* HipPlanExecutor::allocShared(size_t bytes, unsigned flags, SharedRef* ref) {
   const SharedBlock b = context_->acquireShared(bytes, flags);
-  *id = b.id;
-  *h = b.ipc;
-  *status = b.ipcStatus;
-  GLX_TRACE("r%d shared block %ld (%zu bytes) at %p, export status %d", contextRank_,
-            (long)b.id, b.bytes, (void*)b.ptr, (int)b.ipcStatus);
+  *ref = b.ref;
+  GLX_TRACE("r%d shared block %ld (%zu bytes) at %p, base offset %lu", contextRank_,
+            (long)b.ref.id, b.bytes, (void*)b.ptr, (unsigned long)b.ref.baseOff);
   return b.ptr;
 }
 
@@ -612,8 +617,7 @@ void HipPlanExecutor::allocScratch(bool uncached) {
   if (cur.elems > 0) blocks_.push_back(cur);
   for (auto& b : blocks_) {
     const size_t bytes = (size_t)b.elems * esize_ + 64;
-    b.ptr = allocShared(bytes, uncached ? hipDeviceMallocUncached : 0u, &b.id, &b.ipc,
-                        &b.ipcStatus);
+    b.ptr = allocShared(bytes, uncached ? hipDeviceMallocUncached : 0u, &b.ref);
     GLX_HIP_CHECK(hipMemset(b.ptr, 0, bytes));
   }
   GLX_HIP_CHECK(hipDeviceSynchronize());
@@ -1163,8 +1167,6 @@ int initialStepsEngine() {
   return -1;
 }
 
-constexpr int kDevStepsAutoMaxRanks = 4;
-
 int64_t devStepsMaxBytes() {
   const char* e = std::getenv("GLOO_AMD_DEVSTEPS_MAX_BYTES");
   return e != nullptr ? std::atoll(e) : (int64_t(32) << 20);
@@ -1224,11 +1226,7 @@ int HipPlanExecutor::engineFor(const Context& ctx, int algo, int64_t count, int 
       algo == glx::ALGO_FN_RING || algo == glx::ALGO_FN_BCUBE) {
     const int e = stepsEngine();
     if (e >= 0) return e;
-    // auto: the plan kernel for small and medium buffers at up to 4 ranks
-    // (validated on the GPU multi-process up to P=4; at P=8 on one shared
-    // GPU a run was seen to stall, so more ranks keep host-issued steps
-    // unless forced with set_steps_engine("device"))
-    if (ctx.size > kDevStepsAutoMaxRanks) return kEngineSteps;
+    // auto: the plan kernel for small and medium buffers
     return count * esize <= devStepsMaxBytes() ? kEngineDevSteps : kEngineSteps;
   }
   return kEngineSteps;
@@ -1243,15 +1241,11 @@ char* HipPlanExecutor::ddAlloc(size_t bytes) {
     return (e != nullptr && std::strcmp(e, "finegrained") == 0) ? hipDeviceMallocFinegrained
                                                                  : hipDeviceMallocUncached;
   }();
-  hipIpcMemHandle_t h{};
-  int32_t st = 0;
-  int64_t id = 0;
-  char* d = allocShared(bytes, flags, &id, &h, &st);
-  ddIds_.push_back(id);
+  SharedRef ref;
+  char* d = allocShared(bytes, flags, &ref);
+  ddRefs_.push_back(ref);
   GLX_TRACE("r%d ddAlloc %zu bytes at %p", contextRank_, bytes, (void*)d);
   ddBlocks_.push_back(d);
-  ddIpc_.push_back(h);
-  ddIpcStatus_.push_back(st);
   GLX_HIP_CHECK(hipMemset(d, 0, bytes));
   return d;
 }
@@ -1273,6 +1267,11 @@ void HipPlanExecutor::setupDevice() {
   os_.status = ddStatusDev_;
   ts_.status = ddStatusDev_;
   pk_.status = ddStatusDev_;
+  GLX_HIP_CHECK(hipMalloc((void**)&ddClaim_, sizeof(int)));
+  GLX_HIP_CHECK(hipMemset(ddClaim_, 0, sizeof(int)));
+  os_.claim = ddClaim_;
+  ts_.claim = ddClaim_;
+  pk_.claim = ddClaim_;
   GLX_HIP_CHECK(hipEventCreateWithFlags(&ddDone_, hipEventDisableTiming));
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) == hipSuccess &&
@@ -1314,7 +1313,7 @@ void HipPlanExecutor::setupOneShot() {
   ddAlloc((size_t)P * ddSlot_);
   ddAlloc((size_t)P * ddSlot_);
   p.flagIn = reinterpret_cast<const uint64_t*>(
-      ddAlloc((size_t)P * (size_t)p.G * sizeof(uint64_t)));
+      ddAlloc((size_t)P * (size_t)p.G * glx::kFlagBytes));
 }
 
 void HipPlanExecutor::setupTwoShot() {
@@ -1340,9 +1339,9 @@ void HipPlanExecutor::setupTwoShot() {
   }
   ddSlot_ = ((size_t)d.maxLen * esize_ + 16 + 255) & ~(size_t)255;
   for (int k = 0; k < 4; k++) ddAlloc((size_t)P * ddSlot_);  // RS 0/1, AG 0/1
-  char* flags = ddAlloc(2 * (size_t)P * (size_t)p.G * sizeof(uint64_t));
+  char* flags = ddAlloc(2 * (size_t)P * (size_t)p.G * glx::kFlagBytes);
   p.flagAIn = reinterpret_cast<const uint64_t*>(flags);
-  p.flagBIn = reinterpret_cast<const uint64_t*>(flags) + (size_t)P * (size_t)p.G;
+  p.flagBIn = reinterpret_cast<const uint64_t*>(flags) + (size_t)P * (size_t)p.G * glx::kFlagStride;
 }
 
 // The plan kernel: segments from every rank's program (plan.cc syncTable),
@@ -1368,7 +1367,7 @@ void HipPlanExecutor::setupDevSteps() {
   for (size_t k = 0; k < in_.size(); k++) in_[k].deliveryWord = (uint32_t)k;
   for (size_t k = 0; k < out_.size(); k++) out_[k].creditWord = (uint32_t)(in_.size() + k);
   const size_t rows = std::max<size_t>(1, in_.size() + out_.size());
-  ddAlloc(rows * G * sizeof(uint64_t));
+  ddAlloc(rows * G * glx::kFlagBytes);
 }
 
 // After resolvePeers: the step table with every address the kernel needs.
@@ -1399,14 +1398,15 @@ void HipPlanExecutor::buildDevSteps() {
         d.dst = s.len > 0 ? vbase(landing(peerBlocks_[oc.peer], s.dst_off, s.off), s.off)
                           : nullptr;
         d.flag = oc.devDelivery;
-        d.credit = rows + (size_t)oc.creditWord * G;
+        d.credit = rows + (size_t)oc.creditWord * G * glx::kFlagStride;
         break;
       }
       case glx::RECV:
       case glx::RELEASE: {
         GLX_ENFORCE(y.chan == stepChan_[i], "plan kernel: channel numbering disagrees");
         const InChan& ic = in_[(size_t)y.chan];
-        d.flag = s.kind == glx::RECV ? rows + (size_t)ic.deliveryWord * G : ic.devCredit;
+        d.flag = s.kind == glx::RECV ? rows + (size_t)ic.deliveryWord * G * glx::kFlagStride
+                                     : ic.devCredit;
         break;
       }
       case glx::REDUCE:
@@ -1439,6 +1439,7 @@ void HipPlanExecutor::buildDevSteps() {
   }
   if (fs.empty()) fs.push_back(nullptr);
   if (ds.empty()) ds.push_back(glx::DevStep{});  // never walked (nsteps = 0)
+  hostSteps_ = ds;
   GLX_HIP_CHECK(hipMalloc((void**)&devSteps_, ds.size() * sizeof(glx::DevStep)));
   GLX_HIP_CHECK(hipMemcpy(devSteps_, ds.data(), ds.size() * sizeof(glx::DevStep),
                           hipMemcpyHostToDevice));
@@ -1463,9 +1464,35 @@ void HipPlanExecutor::checkDevice() {
               " step " + std::to_string(step) + " of run " + std::to_string(devRuns_ - 1);
     }
     const volatile uint64_t* d = reinterpret_cast<const volatile uint64_t*>(ddStatus_);
+    // The flag words as the host reads them now (the kernel has finished):
+    // ours, and the peer's through our IPC mapping of its memory.  A receiver
+    // whose flag still holds the old value while its sender reads the new
+    // one through its mapping would mean the two views are not one memory.
+    std::string flags;
+    const size_t w = (size_t)d[3];
+    auto readFlag = [&](const uint64_t* row) -> std::string {
+      uint64_t v = 0;
+      if (row == nullptr || w >= (size_t)pk_.G) return "?";
+      if (hipMemcpy(&v, row + w * glx::kFlagStride, sizeof(v), hipMemcpyDeviceToHost) !=
+          hipSuccess) {
+        (void)hipGetLastError();
+        return "?";
+      }
+      return std::to_string(v);
+    };
+    if (engine_ == kEngineDevSteps && step >= 0 && (size_t)step < hostSteps_.size()) {
+      const glx::DevStep& ds = hostSteps_[(size_t)step];
+      if (ds.kind == glx::SEND) {
+        flags = "; now: our credit flag " + readFlag(ds.credit) +
+                ", the receiver's delivery flag through our mapping " + readFlag(ds.flag);
+      } else if (ds.kind == glx::RECV) {
+        flags = "; now: our delivery flag " + readFlag(ds.flag);
+      }
+    }
     GLX_THROW_TIMEOUT("Timed out waiting for data from rank ", peer, " (rank ", contextRank_,
                       ", device-driven allreduce", where, ": workgroup ", d[3], " saw ", d[1],
-                      ", awaited ", d[2], ", timeout ", effectiveTimeout().count(), " ms)");
+                      ", awaited ", d[2], ", timeout ", effectiveTimeout().count(), " ms",
+                      flags, ")");
   }
 }
 
@@ -1540,7 +1567,8 @@ void HipPlanExecutor::runDevice(char* ptr0) {
       const auto& pb = ddPeer_.at(j);
       p.push[j] = pb[(size_t)par] + (size_t)contextRank_ * ddSlot_;
       p.land[j] = ddBlocks_[(size_t)par] + (size_t)j * ddSlot_;
-      p.flagOut[j] = reinterpret_cast<uint64_t*>(pb[2]) + (size_t)contextRank_ * (size_t)p.G;
+      p.flagOut[j] = reinterpret_cast<uint64_t*>(pb[2]) +
+                     (size_t)contextRank_ * (size_t)p.G * glx::kFlagStride;
     }
     GLX_TRACE("r%d one-shot epoch %lu (G=%d slice=%zu)", contextRank_, (unsigned long)e, p.G,
               p.slice);
@@ -1580,8 +1608,8 @@ void HipPlanExecutor::runDevice(char* ptr0) {
       p.agPush[j] = vbase(pb[2 + (size_t)par] + mine, contextRank_);       // my result
       p.agLand[j] = vbase(ddBlocks_[2 + (size_t)par] + theirs, j);         // j's result
       uint64_t* pf = reinterpret_cast<uint64_t*>(pb[4]);
-      p.flagAOut[j] = pf + (size_t)contextRank_ * G;
-      p.flagBOut[j] = pf + (size_t)P * G + (size_t)contextRank_ * G;
+      p.flagAOut[j] = pf + (size_t)contextRank_ * G * glx::kFlagStride;
+      p.flagBOut[j] = pf + ((size_t)P * G + (size_t)contextRank_ * G) * glx::kFlagStride;
     }
     GLX_TRACE("r%d two-shot epoch %lu (G=%d slice=%zu)", contextRank_, (unsigned long)e, p.G,
               p.slice);

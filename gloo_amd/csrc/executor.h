@@ -123,9 +123,7 @@ class HipPlanExecutor : public Algorithm {
     int64_t start = 0;  // first element (in plan region coordinates)
     int64_t elems = 0;
     char* ptr = nullptr;
-    int64_t id = 0;           // the context's shared-block id (allocShared)
-    hipIpcMemHandle_t ipc{};  // exported at allocation (allocShared)
-    int32_t ipcStatus = 0;    // 1 exported, else -(hipError_t)
+    SharedRef ref;  // the context's shared block (allocShared), as peers map it
   };
   static constexpr size_t kMaxBlockBytes = size_t(256) << 20;
   struct InflightSend {
@@ -219,14 +217,11 @@ class HipPlanExecutor : public Algorithm {
   //             [4] flags: A [P][G], then B [P][G]
   int engine_ = kEngineSteps;
   std::vector<char*> ddBlocks_;
-  std::vector<int64_t> ddIds_;            // ddBlocks_' shared-block ids
-  std::vector<hipIpcMemHandle_t> ddIpc_;  // ddBlocks_' exported handles
-  std::vector<int32_t> ddIpcStatus_;
+  std::vector<SharedRef> ddRefs_;  // ddBlocks_' shared blocks, as peers map them
   // Device memory peers will map, from the context's pool of exported blocks
   // (flags 0: hipMalloc, else hipExtMallocWithFlags); back to the pool in
   // release().
-  char* allocShared(size_t bytes, unsigned flags, int64_t* id, hipIpcMemHandle_t* h,
-                    int32_t* status);
+  char* allocShared(size_t bytes, unsigned flags, SharedRef* ref);
   std::map<int, std::vector<char*>> ddPeer_;  // peers' blocks (IPC-mapped)
   size_t ddSlot_ = 0;                         // bytes per landing slot
   glx::OneShotParams os_{};                   // fixed parts of the kernels' parameters
@@ -237,12 +232,14 @@ class HipPlanExecutor : public Algorithm {
   glx::PlanParams prm_;
   glx::SyncTable sync_;
   glx::DevStep* devSteps_ = nullptr;
+  std::vector<glx::DevStep> hostSteps_;  // host copy (timeout diagnostics)
   glx::DevSegment* devSegs_ = nullptr;
   const char** devFoldSrc_ = nullptr;
   uint64_t devRuns_ = 0;
   uint64_t ddEpoch_ = 0;
   int* ddStatus_ = nullptr;  // pinned host word the kernels flag timeouts in
   int* ddStatusDev_ = nullptr;
+  int* ddClaim_ = nullptr;  // device word: the first timed-out workgroup claims the report
   hipEvent_t ddDone_ = nullptr;
   bool ddLaunched_ = false;
   int clockKhz_ = 100000;  // s_memrealtime rate

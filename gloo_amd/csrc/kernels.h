@@ -42,13 +42,18 @@ int copy_blocks();
 // regions and flags are uncached device memory (peers' via IPC).
 constexpr int kOsMaxRanks = 8;
 constexpr int kOsMaxSlices = 512;  // workgroups (= slices) per launch
+// Flags are 8-byte words, each alone in its 128-byte L2 line: flag f of a
+// row starts at row + f * kFlagStride (no line holds flags of two writers).
+constexpr int kFlagStride = 16;
+constexpr size_t kFlagBytes = kFlagStride * sizeof(uint64_t);
 struct OneShotParams {
   char* buf;                        // this rank's buffer: input and result
   char* push[kOsMaxRanks];          // this rank's landing region in peer j (j != rank)
   const char* land[kOsMaxRanks];    // rank k's landing region here (k != rank)
-  uint64_t* flagOut[kOsMaxRanks];   // peer j's flag row for this rank ([G] words)
-  const uint64_t* flagIn;           // this rank's flags: [P][G] words
+  uint64_t* flagOut[kOsMaxRanks];   // peer j's flag row for this rank ([G] flags)
+  const uint64_t* flagIn;           // this rank's flags: [P][G] flags
   int* status;                      // host-visible: 1 + rank that never arrived
+  int* claim;                       // device word: the first timed-out workgroup reports
   uint64_t epoch;                   // >= 1, +1 per call, equal on all ranks
   uint64_t timeoutTicks;            // s_memrealtime ticks
   size_t count;                     // elements
@@ -70,11 +75,12 @@ struct TwoShotParams {
   const char* rsLand[kOsMaxRanks];  // this rank's RS slot holding rank k's copy of range rank
   char* agPush[kOsMaxRanks];        // peer j's AG slot for this rank's finished range
   const char* agLand[kOsMaxRanks];  // this rank's AG slot holding owner j's finished range
-  uint64_t* flagAOut[kOsMaxRanks];  // owner j's A-flag row for this rank ([G] words)
+  uint64_t* flagAOut[kOsMaxRanks];  // owner j's A-flag row for this rank ([G] flags)
   const uint64_t* flagAIn;          // [P][G]: rank k's copy of my range slice landed
   uint64_t* flagBOut[kOsMaxRanks];  // peer j's B-flag row for this rank as owner
   const uint64_t* flagBIn;          // [P][G]: owner j's finished slice landed
   int* status;
+  int* claim;
   uint64_t epoch, timeoutTicks;
   size_t rangeOff[kOsMaxRanks], rangeLen[kOsMaxRanks];  // by owner
   uint8_t chain[kOsMaxRanks];       // this rank's fold order
@@ -120,6 +126,7 @@ struct PlanKernelParams {
   uint64_t run;                // runs completed before this one
   uint64_t timeoutTicks;
   int* status;
+  int* claim;
 };
 hipError_t launch_plan_kernel(int op, int dtype, const PlanKernelParams& p, hipStream_t s);
 

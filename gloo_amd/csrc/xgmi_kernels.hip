@@ -208,50 +208,91 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
   }
 }
 
+// Flag words are written by other agents (peers over xGMI, other processes
+// on this GPU, workgroups on other XCDs) and polled by their owner.  Writes
+// are atomic exchanges and polls atomic compare-exchanges, at system scope:
+// both execute at the memory side, so no L2 -- the writer's, the reader's or
+// that of another XCD -- ever holds a copy of a flag line that could be read
+// stale or written back over a newer value.  Each flag has a 128-byte line
+// of its own (kFlagStride words): one writer per line.
+__device__ __forceinline__ void put_flag(uint64_t* word, uint64_t v) {
+  (void)__hip_atomic_exchange(word, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// A compare-exchange that never matches (flags never reach ~0): a real
+// memory-side read (an idempotent add or or would be turned into a load).
+__device__ __forceinline__ uint64_t get_flag(const uint64_t* word) {
+  uint64_t v = ~uint64_t(0);
+  __hip_atomic_compare_exchange_strong(const_cast<uint64_t*>(word), &v, ~uint64_t(0),
+                                       __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+  return v;
+}
+
+__device__ __forceinline__ uint64_t* flag_at(uint64_t* row, int w) {
+  return row + (size_t)w * kFlagStride;
+}
+
+__device__ __forceinline__ const uint64_t* flag_at(const uint64_t* row, int w) {
+  return row + (size_t)w * kFlagStride;
+}
+
 // Every wave's stores complete and visible system-wide, then (by lanes
 // 0..P-1, lane r excluded, where want(lane)) flag words set to epoch.
 template <typename Want>
 __device__ __forceinline__ void release_flags(uint64_t* const* rows, int P, int rank, int w,
                                               uint64_t epoch, Want want) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  // the compiler may drop the wait after the write-back when it can prove no
+  // store is outstanding (MI355X_MICROARCH.md, compiler hazard): keep it
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
   const int t = (int)threadIdx.x;
-  if (t < P && t != rank && want(t)) {
-    __hip_atomic_store(rows[t] + w, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  if (t < P && t != rank && want(t)) put_flag(flag_at(rows[t], w), epoch);
 }
 
 // Every wave's stores complete and visible system-wide, then lane 0 stores
 // `value` into `word` (a flag in a peer's memory).
 __device__ __forceinline__ void signal_flag(uint64_t* word, uint64_t value) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(word, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x == 0) put_flag(word, value);
+}
+
+// The first workgroup of the launch whose wait times out reports it: status
+// = 1 + peer (+ 256 * (1 + step) when the plan kernel says where), then as
+// 64-bit words 1..3 the value seen, the value awaited and the workgroup.
+// `claim` (device memory, zero until a timeout) keeps the report of one
+// workgroup whole.
+__device__ __forceinline__ void report_timeout(int* status, int* claim, int code,
+                                               uint64_t seen, uint64_t awaited) {
+  int expected = 0;
+  if (!__hip_atomic_compare_exchange_strong(claim, &expected, 1, __ATOMIC_RELAXED,
+                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+    return;
   }
+  uint64_t* detail = reinterpret_cast<uint64_t*>(status);
+  __hip_atomic_store(detail + 1, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(detail + 2, awaited, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(detail + 3, (uint64_t)blockIdx.x, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Lane 0 waits until word >= epoch (bounded); the whole workgroup learns
-// the outcome.  Returns false after a timeout (status already set).
+// the outcome.  Returns false after a timeout (reported).
 __device__ __forceinline__ bool wait_flag(const uint64_t* word, uint64_t epoch, int peer,
                                           uint64_t start, uint64_t timeoutTicks, int* status,
-                                          int* s_ok, bool acquire = true, int where = 0) {
+                                          int* claim, int* s_ok, bool acquire = true,
+                                          int where = 0) {
   if (threadIdx.x == 0) {
     int ok = 1;
-    while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+    uint64_t v;
+    while ((v = get_flag(word)) < epoch) {
       if (__builtin_amdgcn_s_memrealtime() - start > timeoutTicks) {
         ok = 0;
-        // 1 + peer, plus 256 * (1 + step) when the plan kernel says where;
-        // the words after it: the value seen, the value awaited, the workgroup
-        uint64_t* detail = reinterpret_cast<uint64_t*>(status);
-        __hip_atomic_store(detail + 1,
-                           __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(detail + 2, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(detail + 3, (uint64_t)blockIdx.x, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(status, 1 + peer + 256 * where, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+        report_timeout(status, claim, 1 + peer + 256 * where, v, epoch);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -293,8 +334,8 @@ __global__ __launch_bounds__(kBlock, 2) void oneshot_kernel(OneShotParams p) {
   const uint64_t start = __builtin_amdgcn_s_memrealtime();
   for (int k = 0; k < p.P; k++) {
     if (k == p.rank) continue;
-    if (!wait_flag(p.flagIn + (size_t)k * p.G + w, p.epoch, k, start, p.timeoutTicks,
-                   p.status, &s_ok)) {
+    if (!wait_flag(flag_at(p.flagIn, k * p.G + w), p.epoch, k, start, p.timeoutTicks,
+                   p.status, p.claim, &s_ok)) {
       return;
     }
   }
@@ -359,8 +400,8 @@ __global__ __launch_bounds__(kBlock, 2) void twoshot_kernel(TwoShotParams p) {
   if (span(p.rank, a, b)) {
     for (int k = 0; k < p.P; k++) {
       if (k == p.rank) continue;
-      if (!wait_flag(p.flagAIn + (size_t)k * p.G + w, p.epoch, k, start, p.timeoutTicks,
-                     p.status, &s_ok)) {
+      if (!wait_flag(flag_at(p.flagAIn, k * p.G + w), p.epoch, k, start, p.timeoutTicks,
+                     p.status, p.claim, &s_ok)) {
         return;
       }
     }
@@ -388,8 +429,8 @@ __global__ __launch_bounds__(kBlock, 2) void twoshot_kernel(TwoShotParams p) {
     int j = p.rank - d;
     if (j < 0) j += p.P;
     if (!span(j, a, b)) continue;
-    if (!wait_flag(p.flagBIn + (size_t)j * p.G + w, p.epoch, j, start, p.timeoutTicks,
-                   p.status, &s_ok)) {
+    if (!wait_flag(flag_at(p.flagBIn, j * p.G + w), p.epoch, j, start, p.timeoutTicks,
+                   p.status, p.claim, &s_ok)) {
       return;
     }
     if (d == 1) stamp(4);
@@ -421,9 +462,9 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
     const uint64_t seq = p.run * st.perRun + st.seq;
     switch (st.kind) {
       case 0: {  // SEND, once the receiver has consumed message seq-1 of this slice
-        if (seq > 1 && !wait_flag(st.credit + w, seq - 1, st.peer,
+        if (seq > 1 && !wait_flag(flag_at(st.credit, w), seq - 1, st.peer,
                                   __builtin_amdgcn_s_memrealtime(), p.timeoutTicks, p.status,
-                                  &s_ok, /*acquire=*/false, 1 + i)) {
+                                  p.claim, &s_ok, /*acquire=*/false, 1 + i)) {
           return;
         }
         for (int g = st.seg0; g < st.seg1; g++) {
@@ -432,12 +473,12 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
             copy_span<S>(reinterpret_cast<S*>(st.dst), buf, a, b, aligned);
           }
         }
-        signal_flag(st.flag + w, seq);
+        signal_flag(flag_at(st.flag, w), seq);
         break;
       }
       case 1:  // RECV
-        if (!wait_flag(st.flag + w, seq, st.peer, __builtin_amdgcn_s_memrealtime(),
-                       p.timeoutTicks, p.status, &s_ok, true, 1 + i)) {
+        if (!wait_flag(flag_at(st.flag, w), seq, st.peer, __builtin_amdgcn_s_memrealtime(),
+                       p.timeoutTicks, p.status, p.claim, &s_ok, true, 1 + i)) {
           return;
         }
         break;
@@ -472,9 +513,7 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
       }
       case 4:  // RELEASE: every wave is done reading the region
         __syncthreads();
-        if (threadIdx.x == 0) {
-          __hip_atomic_store(st.flag + w, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        if (threadIdx.x == 0) put_flag(flag_at(st.flag, w), seq);
         break;
       default:
         break;
@@ -574,6 +613,7 @@ int device_engine_resident_blocks(int kernel, int op, int dtype) {
 }
 
 hipError_t launch_oneshot(int op, int dtype, const OneShotParams& p, hipStream_t s) {
+  if (p.status == nullptr || p.claim == nullptr) return hipErrorInvalidValue;
   if (p.P < 2 || p.P > kOsMaxRanks || p.G < 1 || p.G > kOsMaxSlices || p.njobs < 0 ||
       p.njobs > kOsMaxRanks || p.count == 0 || p.slice == 0 ||
       (size_t)p.G * p.slice < p.count || (size_t)(p.G - 1) * p.slice >= p.count) {
@@ -595,7 +635,7 @@ hipError_t launch_oneshot(int op, int dtype, const OneShotParams& p, hipStream_t
 
 hipError_t launch_plan_kernel(int op, int dtype, const PlanKernelParams& p, hipStream_t s) {
   if (p.G < 1 || p.G > kOsMaxSlices || p.nsteps < 0 || p.steps == nullptr ||
-      p.segs == nullptr || p.foldSrc == nullptr) {
+      p.segs == nullptr || p.foldSrc == nullptr || p.status == nullptr || p.claim == nullptr) {
     return hipErrorInvalidValue;
   }
   switch (dtype) {
@@ -618,7 +658,7 @@ hipError_t launch_twoshot(int op, int dtype, const TwoShotParams& p, hipStream_t
     maxLen = p.rangeLen[c] > maxLen ? p.rangeLen[c] : maxLen;
   }
   if (p.P < 2 || p.P > kOsMaxRanks || p.G < 1 || p.G > kOsMaxSlices || p.slice == 0 ||
-      (size_t)p.G * p.slice < maxLen) {
+      (size_t)p.G * p.slice < maxLen || p.status == nullptr || p.claim == nullptr) {
     return hipErrorInvalidValue;  // the slices must cover every range
   }
   switch (dtype) {

@@ -269,6 +269,59 @@ def make_allreduce_fn():
     print("allreduce_fn: %d cases" % len(index))
 
 
+# ---- BASELINE.json configs at full size (digests, not arrays) -------------
+# cfg3: ring_chunked fp32, 8 ranks, the 1K..16M element sweep;
+# cfg4: halving_doubling fp32, 8 ranks, 256 MiB per rank;
+# cfg5: ring_chunked fp16, 8 ranks, 1 GiB per rank (bf16: the oracle's
+#       restatement -- the reference has no bfloat16, parity unpinned).
+# Inputs are O.fill(dtype, N, seed=SEED, rank=r); the tests
+# regenerate them on each rank and compare SHA-256 digests.
+SCALE_CASES = [(O.RING_CHUNKED, 8, 1 << k, O.FLOAT32) for k in range(10, 25, 2)]
+SCALE_CASES += [(O.HALVING_DOUBLING, 8, 1 << 26, O.FLOAT32),
+                (O.RING_CHUNKED, 8, 1 << 28, O.FLOAT16),
+                (O.RING_CHUNKED, 8, 1 << 28, O.BFLOAT16)]
+
+
+def scale_case_name(c):
+    algo, P, N, dtype = c
+    return "%s_P%d_N%d_%s_sum" % ("ring" if algo == O.RING_CHUNKED else "hd", P, N,
+                                  O.DTYPE_NAMES[dtype])
+
+
+def make_scale():
+    path = os.path.join(HERE, "scale_golden.json")
+    cases = []
+    for c in SCALE_CASES:
+        algo, P, N, dtype = c
+        ins = [[O.fill(dtype, N, 0, seed=SEED, rank=r)] for r in range(P)]
+        pinned = dtype != O.BFLOAT16
+        res = O.allreduce(algo, O.SUM, dtype, ins, use_ref=pinned)
+        first = res[0][0]
+        for r in range(P):
+            assert np.array_equal(res[r][0].view(np.uint8), first.view(np.uint8)), \
+                "ranks disagree in %s" % scale_case_name(c)
+        idx = np.linspace(0, N - 1, 65).astype(np.int64)
+        cases.append({
+            "name": scale_case_name(c), "algo": algo, "P": P, "N": N, "dtype": dtype,
+            "op": O.SUM, "seed": SEED,
+            "source": "reference" if pinned else "oracle restatement (parity unpinned)",
+            "input_sha256": [sha([ins[r][0]]) for r in range(P)],
+            "output_sha256": sha([first]),
+            "sample_idx": idx.tolist(),
+            "sample": [int(v) for v in first.view(np.uint32 if first.itemsize == 4
+                                                  else np.uint16)[idx]],
+        })
+        print(cases[-1]["name"], cases[-1]["output_sha256"][:16], flush=True)
+        del ins, res, first
+    with open(path, "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py (make_scale)",
+                   "source": "oracle/_ref/libgloo_ref.so (the reference compiled from "
+                             "/root/reference by oracle/Makefile), P thread-ranks over "
+                             "TCP loopback; bfloat16 from oracle/liboracle.so",
+                   "sample_bits": "raw element bits at sample_idx",
+                   "cases": cases}, f, indent=1)
+
+
 if __name__ == "__main__":
     if not O.ref_available():
         sys.exit("oracle/_ref/libgloo_ref.so missing: make -C oracle ref")
@@ -281,4 +334,6 @@ if __name__ == "__main__":
         make_allreduce()
     if "allreduce_fn" in which:
         make_allreduce_fn()
+    if "scale" in which:  # not in the default set: minutes and ~20 GiB of RAM
+        make_scale()
     print("done")

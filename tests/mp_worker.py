@@ -15,6 +15,8 @@ algo: ring_chunked | halving_doubling | ring_chunked_mesh (class algorithms)
       devtimeout (rank 0 runs both device engines while the other ranks never
       call run(): its kernels must give up after the timeout and run() must
       raise IoException)
+      scale:cfg34 | scale:cfg5 (BASELINE.json configs at full size, 8 ranks:
+      every engine's output SHA-256 against tests/golden/scale_golden.json)
 
 Checks its result against the oracle and prints OK."""
 import os
@@ -43,6 +45,8 @@ def main():
         return run_devsteps(store_dir, rank, size)
     if algo == "churn":
         return run_churn(store_dir, rank, size)
+    if algo.startswith("scale:"):
+        return run_scale(store_dir, rank, size, algo[len("scale:"):])
     if algo.startswith("fn_"):
         return run_fn(store_dir, rank, size, algo, N)
     code = O.HALVING_DOUBLING if algo == "halving_doubling" else O.RING_CHUNKED
@@ -433,6 +437,93 @@ def run_device(store_dir, rank, size, mode):
     store.set("done/%d" % rank, b"1")
     for r in range(size):
         store.get("done/%d" % r, timeout_ms=60000)
+    ctx.close()
+    if bad:
+        print("MISMATCH rank", rank, bad[:10])
+        sys.exit(1)
+    print("OK")
+
+
+def run_scale(store_dir, rank, size, group):
+    """BASELINE.json configs at their full size against the reference's own
+    output digests (tests/golden/scale_golden.json, made by make_golden.py
+    scale): cfg3 ring_chunked fp32 1K..16M elements, cfg4 halving_doubling
+    256 MiB, cfg5 ring_chunked fp16 (and bf16, oracle-pinned only) 1 GiB, on
+    every engine the product has for the schedule.  Inputs are regenerated
+    here with the generator's seed; their digests are checked too."""
+    import hashlib
+    import json
+    import time
+
+    import numpy as np
+    import torch
+
+    import gloo_amd
+    from oracle import oracle as O
+    from test_reduce_gpu import from_dev, to_dev
+
+    with open(os.path.join(HERE, "golden", "scale_golden.json")) as f:
+        cases = json.load(f)["cases"]
+    if group == "cfg34":
+        cases = [c for c in cases if c["dtype"] == O.FLOAT32]
+    else:
+        cases = [c for c in cases if c["dtype"] != O.FLOAT32]
+    assert cases and all(c["P"] == size for c in cases), "scale cases are for P=%d" % size
+
+    def sha(a):
+        h = hashlib.sha256()
+        h.update(np.ascontiguousarray(a).view(np.uint8).tobytes())
+        return h.hexdigest()
+
+    store = gloo_amd.rendezvous.FileStore(store_dir)
+    ctx = gloo_amd.rendezvous.Context(rank, size, 0)
+    ctx.setTimeout(120)
+    ctx.connectFullMesh(store)
+    bad = []
+    for c in cases:
+        N, dt = c["N"], c["dtype"]
+        x = O.fill(dt, N, 0, seed=c["seed"], rank=rank)
+        if sha(x) != c["input_sha256"][rank]:
+            bad.append(("input", c["name"]))
+            continue
+        ring = c["algo"] == O.RING_CHUNKED
+        engines = [("device", "ring"), ("host", "ring"), ("device", "mesh")] if ring else \
+            [("device", "hd"), ("host", "hd")]
+        for eng, sched in engines:
+            buf = to_dev(x, dt)
+            del_src = None
+            gloo_amd.set_steps_engine(eng)
+            try:
+                if sched == "hd":
+                    alg = gloo_amd.AllreduceHalvingDoubling(ctx, [buf], dtype=dt)
+                else:
+                    alg = gloo_amd.AllreduceRingChunked(ctx, [buf], schedule=sched, dtype=dt)
+            finally:
+                gloo_amd.set_steps_engine("auto")
+            t0 = time.perf_counter()
+            for it in range(2):
+                if it:
+                    buf.copy_(to_dev(x, dt))
+                torch.cuda.synchronize()
+                alg.run()
+            ms = (time.perf_counter() - t0) * 1e3 / 2
+            got = from_dev(buf, dt)
+            ok = sha(got) == c["output_sha256"]
+            if not ok:
+                idx = np.array(c["sample_idx"])
+                bits = np.ascontiguousarray(got).view(np.uint32 if got.itemsize == 4
+                                                      else np.uint16)[idx]
+                nbad = int((bits != np.array(c["sample"], dtype=bits.dtype)).sum())
+                bad.append((c["name"], sched, alg.engine(), "sample mismatches", nbad))
+            print("SCALE rank %d %s %s engine %s %.1f ms/run %s" % (
+                rank, c["name"], sched, alg.engine(), ms, "ok" if ok else "MISMATCH"),
+                flush=True)
+            alg.close()
+            del buf, del_src
+            torch.cuda.empty_cache()
+    store.set("done/%d" % rank, b"1")
+    for r in range(size):
+        store.get("done/%d" % r, timeout_ms=120000)
     ctx.close()
     if bad:
         print("MISMATCH rank", rank, bad[:10])

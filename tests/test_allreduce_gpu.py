@@ -257,8 +257,9 @@ def test_multiprocess_ipc(algo):
             assert "OK" in outs[r]
 
 
-@pytest.mark.parametrize("mode", ["oneshot", "twoshot", "devsteps"])
-@pytest.mark.parametrize("P", [2, 3, 4])
+@pytest.mark.parametrize("P,mode", [(P, m) for P in (2, 3, 4)
+                                    for m in ("oneshot", "twoshot", "devsteps")] +
+                         [(8, "devsteps")])
 def test_device_engine_multiprocess(P, mode):
     """The replicated (one-shot) and mesh (two-shot) schedules, and the ring,
     halving-doubling and bcube step programs (plan kernel), as one
@@ -275,7 +276,7 @@ def test_device_engine_multiprocess(P, mode):
         outs = []
         for p in procs:
             try:
-                o, _ = p.communicate(timeout=240)
+                o, _ = p.communicate(timeout=420 if P > 4 else 240)
             except subprocess.TimeoutExpired:
                 for q in procs:
                     q.kill()
@@ -302,7 +303,7 @@ def test_algorithm_churn_multiprocess(P):
         outs = []
         for p in procs:
             try:
-                o, _ = p.communicate(timeout=240)
+                o, _ = p.communicate(timeout=420 if P > 4 else 240)
             except subprocess.TimeoutExpired:
                 for q in procs:
                     q.kill()

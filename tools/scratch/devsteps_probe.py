@@ -3,12 +3,12 @@ many ranks: runs the worker's dtype cases, reports per run how many elements
 differ from the oracle and where, optionally with a store barrier before
 every close (CLOSE_BARRIER=1).  One process per rank:
 
-    python tools/mp_launch.py --nproc 8 -- tools/devsteps_probe.py DIR
+    python tools/mp_launch.py --nproc 8 -- tools/scratch/devsteps_probe.py DIR
 """
 import os
 import sys
 
-HERE = os.path.dirname(os.path.abspath(__file__))
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(os.path.dirname(HERE), "tests"))
 
