@@ -76,48 +76,111 @@ def load_traffic(workload):
         return None
 
 
-def cpu_baseline(nbytes, seconds, dtype="f32"):
-    """gloo::sum<T> on the host cores (single thread, like the reference):
-    the reference itself (oracle/_ref, compiled from the reference sources in
-    the build container) when present, else the oracle's restatement."""
+def host_threads():
+    """Host threads for the CPU baseline: the cores this process may run on,
+    at most 16 (a one-GPU box's CPU share; nproc there counts the whole
+    machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def cpu_baseline(nbytes, seconds, dtype="f32", ring_ranks=8):
+    """The reference's CPU path on the host cores, in three legs, each a
+    bounded sample of about seconds/3:
+      * gloo::sum<T> c = a + b over the whole buffer split across T host
+        threads (the headline `value`, cores = T);
+      * the same on one thread (the reference's own single-threaded loop);
+      * AllreduceRingChunked<T> over `ring_ranks` thread-ranks on TCP
+        loopback (the reference's CPU allreduce of this buffer, as its own
+        tests run it: gloo/test/base_test.h:91-166).
+    The reference itself (oracle/_ref, compiled from /root/reference in the
+    build container) when present; else the oracle's port of gloo/math.h
+    on one thread only."""
+    import ctypes
     import numpy as np
     from oracle import oracle as O
     code = {"f32": O.FLOAT32, "f16": O.FLOAT16, "bf16": O.BFLOAT16}[dtype]
     es = 4 if dtype == "f32" else 2
     n = nbytes // es
+    leg = seconds / 3.0
     a = O.fill(code, n, 0, seed=1234, rank=0)
     b = O.fill(code, n, 0, seed=1234, rank=1)
-    c = np.empty_like(a)
+    c = np.zeros_like(a)
     # bf16 has no reference type: the oracle restatement is the only CPU path
-    kind = "reference" if (O.ref_available() and dtype != "bf16") else "port"
-    if kind == "reference":
-        lib = O._load_ref()
-
-        def step():
-            lib.ref_reduce(O.SUM, code, O._ptr(c), O._ptr(a), O._ptr(b), n)
-    elif dtype == "f32":
-        def step():
-            O.sum_f32(c, a, b)
-    else:
+    if not (O.ref_available() and dtype != "bf16"):
         lib = O._load_oracle()
 
         def step():
-            lib.oracle_reduce(O.SUM, code, O._ptr(c), O._ptr(a), O._ptr(b), n)
-    step()  # page in
-    reps, t0 = 0, time.perf_counter()
-    while True:
+            if dtype == "f32":
+                O.sum_f32(c, a, b)
+            else:
+                lib.oracle_reduce(O.SUM, code, O._ptr(c), O._ptr(a), O._ptr(b), n)
         step()
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or reps >= 2000:
-            break
-    t = el / reps
-    src = ("oracle/_ref: the reference's gloo/math.h" if kind == "reference"
-           else "oracle port of gloo/math.h")
-    return {"value": round(nbytes / t / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": kind,
-            "sample": "gloo::sum<%s> c=a+b over %d MiB, %d reps in %.1f s, 1 thread (%s)"
-                      % (DTYPES[dtype][0], nbytes >> 20, reps, el, src),
-            "ms_per_step": round(t * 1e3, 3), "nproc": os.cpu_count()}
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            step()
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds or reps >= 2000:
+                break
+        t = el / reps
+        return {"value": round(nbytes / t / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+                "sample": "oracle port of gloo/math.h sum<%s> c=a+b over %d MiB, %d reps in "
+                          "%.1f s, 1 thread" % (DTYPES[dtype][0], nbytes >> 20, reps, el),
+                "ms_per_step": round(t * 1e3, 3), "nproc": os.cpu_count()}
+    lib = O._load_ref()
+
+    def timed_sum(threads):
+        secs = ctypes.c_double(0.0)
+        # one untimed pass pages the buffers in, one timed pass sizes the sample
+        for it in (1, 1):
+            rc = lib.ref_reduce_mt(O.SUM, code, O._ptr(c), O._ptr(a), O._ptr(b), n, threads, it,
+                                   ctypes.byref(secs))
+            assert rc == 0, "ref_reduce_mt rc=%d" % rc
+        iters = max(1, min(2000, int(leg / max(secs.value, 1e-6))))
+        rc = lib.ref_reduce_mt(O.SUM, code, O._ptr(c), O._ptr(a), O._ptr(b), n, threads, iters,
+                               ctypes.byref(secs))
+        assert rc == 0
+        return secs.value / iters, iters, secs.value
+
+    T = host_threads()
+    tN, itN, elN = timed_sum(T)
+    t1, it1, el1 = timed_sum(1)
+    res = {"value": round(nbytes / tN / 1e9, 3), "unit": "GB/s", "cores": T,
+           "kind": "reference",
+           "sample": "gloo::sum<%s> c=a+b over %d MiB split across %d host threads, %d reps in "
+                     "%.1f s (oracle/_ref: the reference's gloo/math.h)"
+                     % (DTYPES[dtype][0], nbytes >> 20, T, itN, elN),
+           "ms_per_step": round(tN * 1e3, 3), "nproc": os.cpu_count(),
+           "single_thread": {"value": round(nbytes / t1 / 1e9, 3), "unit": "GB/s", "cores": 1,
+                             "ms_per_step": round(t1 * 1e3, 3),
+                             "sample": "%d reps in %.1f s" % (it1, el1)}}
+    del c
+    if ring_ranks > 1:
+        # the reference's own allreduce of this buffer size on the host:
+        # ring_ranks thread-ranks over TCP loopback, rank 0's wall time
+        try:
+            ins = [[O.fill(code, n, 0, seed=1234, rank=r)] for r in range(ring_ranks)]
+            O.allreduce(O.RING_CHUNKED, O.SUM, code, ins, use_ref=True, warmup=0, iters=1)
+            t_one = O.allreduce.last_seconds
+            iters = max(1, min(50, int(leg / max(t_one, 1e-6))))
+            O.allreduce(O.RING_CHUNKED, O.SUM, code, ins, use_ref=True, warmup=0, iters=iters)
+            t = O.allreduce.last_seconds / iters
+            res["ring_chunked"] = {
+                "value": round(ring_ranks * nbytes / t / 1e9, 3), "unit": "GB/s",
+                "cores": ring_ranks, "ranks": ring_ranks, "ms_per_step": round(t * 1e3, 2),
+                "algbw_GBps": round(nbytes / t / 1e9, 3),
+                "sample": "AllreduceRingChunked<%s> of %d MiB per rank, %d thread-ranks on "
+                          "TCP loopback (+ one epoll thread each), %d timed runs after 1 "
+                          "(oracle/_ref); value = ranks x bytes / time, as bench.py's N>1 "
+                          "value" % (DTYPES[dtype][0], nbytes >> 20, ring_ranks, iters)}
+            del ins
+        except Exception as e:  # noqa: BLE001 - reported, the other legs stand
+            res["ring_chunked"] = {"error": "%s: %s" % (type(e).__name__, str(e)[:200])}
+    return res
 
 
 DTYPES = {"f32": ("float32", 4), "f16": ("float16", 2), "bf16": ("bfloat16", 2)}
@@ -235,34 +298,34 @@ def bench_single(args):
     return res
 
 
-def reduce_kernel_roofline(torch, gloo_amd, dev, chunk_bytes, dtype="f32", reps=50):
-    """Live HBM roofline of the reduce kernel at the ring's chunk size and the
-    run's dtype, timed with HIP events on the stream it is launched on."""
-    name, es = DTYPES[dtype]
-    n = chunk_bytes // es
-    a = torch.rand(n, device=dev).to(getattr(torch, name))
-    b = torch.rand(n, device=dev).to(getattr(torch, name))
-    s = torch.cuda.current_stream(dev)
-    for _ in range(5):
-        gloo_amd.math.reduce(gloo_amd.ReductionType.SUM, a, a, b, stream=s)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(s)
-    for _ in range(reps):
-        gloo_amd.math.reduce(gloo_amd.ReductionType.SUM, a, a, b, stream=s)
-    e1.record(s)
-    torch.cuda.synchronize()
-    t = e0.elapsed_time(e1) / reps / 1e3
-    ach = 3 * chunk_bytes / t / 1e9
-    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
-            "kernel": "reduce in place, %d MiB %s chunk" % (chunk_bytes >> 20, dtype),
-            "algorithmic_bytes_per_launch": 3 * chunk_bytes}
+def plan_hbm_bytes(gloo_amd, algo, rank, world, count, es):
+    """Algorithmic HBM bytes one rank's GPU moves per run of the schedule
+    (from its compiled step program): a SEND reads its bytes here and writes
+    them into the receiver's HBM (counted here, the schedules being
+    symmetric), a REDUCE reads 2 and writes 1, a COPY reads 1 and writes 1,
+    a FOLD of k sources reads k and writes 1 -- per element.  Ring at P=8:
+    sends 2 x 1.75 S + reduces 3 x 0.875 S + copies 2 x 0.875 S = 7.875 S;
+    mesh 6.375 S; halving-doubling 7.875 S."""
+    steps, _, folds = gloo_amd.plan(plan_name(algo), rank, world, count, with_folds=True)
+    total = 0
+    for st in steps:
+        kind, ln = st[0], st[4]
+        if kind == 0:
+            total += 2 * ln
+        elif kind == 2:
+            total += 3 * ln
+        elif kind == 3:
+            total += 2 * ln
+        elif kind == 5:
+            total += (len(folds.get(st[5], [])) + 1) * ln
+    return total * es
 
 
 RING_SCHEDULES = {"ring_chunked": "ring", "ring_chunked_mesh": "mesh",
                   "ring_chunked_mesh_steps": "mesh", "ring_chunked_repl": "replicated",
                   "ring_chunked_auto": "auto"}
 ENGINES = {}  # bench name -> engine the product chose (steps/oneshot/twoshot/devsteps)
+TRANSPORT = {}  # bench name -> the algorithm's transport_stats() after its timed runs
 
 
 def plan_name(algo):
@@ -334,6 +397,7 @@ def time_schedule(torch, dist, gloo_amd, ctx, buf, algo, steps, warmup):
     el = torch.tensor([t1 - t0], dtype=torch.float64)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     sent = alg.bytes_sent()
+    TRANSPORT[algo] = alg.transport_stats()
     alg.close()
     log("%s: %.3f ms/step" % (algo, el.item() / steps * 1e3))
     return el.item() / steps, sent
@@ -616,11 +680,12 @@ def bench_multi(args):
             sweep, failed["sweep"] = None, err or "failed on another rank"
     res = None
     if rank == 0:
-        chunk = max(256 * es, -(-S // (2 * world)))
         algbw = S / t / 1e9
         busbw = algbw * 2 * (world - 1) / world
         link_max = busiest_link_bytes(gloo_amd, chosen, rank, world, n, es)
         link_ach = link_max / t / 1e9
+        hbm = plan_hbm_bytes(gloo_amd, chosen, rank, world, n, es)
+        hbm_ach = hbm / t / 1e9
         res = {
             "metric": "allreduce GB/s (device-resident, fp32) at 1/2/4/8 MI355X; % HBM|xGMI roofline",
             "value": round(world * S / t / 1e9, 3), "unit": "GB/s", "n_gpus": world,
@@ -648,15 +713,21 @@ def bench_multi(args):
                        "baseline_config": "configs[3]" if args.algo == "halving_doubling"
                        else "configs[2]"},
             "algbw_GBps": round(algbw, 3), "busbw_GBps": round(busbw, 3),
-            "roofline": reduce_kernel_roofline(torch, gloo_amd, dev, chunk, args.dtype),
-            "link_roofline": {"bound": "xgmi_link", "achieved": round(link_ach, 2),
-                              "peak": XGMI_LINK_GBPS, "unit": "GB/s",
-                              "frac": round(link_ach / XGMI_LINK_GBPS, 4),
-                              "busiest_link_bytes_per_step": link_max,
-                              "bytes_sent_per_step": link_bytes,
-                              "note": "busiest outgoing link's bytes per step / step time "
-                                      "(ring: everything on rank->rank+1; mesh: 1/(P-1) "
-                                      "per peer link)"},
+            # the collective's own bound: its busiest xGMI link (the ring puts
+            # all 1.75 S on rank -> rank+1), with the step's HBM bytes beside it
+            "roofline": {"bound": "xgmi_link", "achieved": round(link_ach, 2),
+                         "peak": XGMI_LINK_GBPS, "unit": "GB/s",
+                         "frac": round(link_ach / XGMI_LINK_GBPS, 4), "traffic": None,
+                         "busiest_link_bytes_per_step": link_max,
+                         "bytes_sent_per_step": link_bytes,
+                         "note": "busiest outgoing link's bytes per step / ms_per_step, "
+                                 "peak = one xGMI link per direction (task figure)",
+                         "hbm": {"achieved": round(hbm_ach, 1), "peak": HBM_PEAK_GBPS,
+                                 "unit": "GB/s", "frac": round(hbm_ach / HBM_PEAK_GBPS, 4),
+                                 "algorithmic_bytes_per_step": hbm,
+                                 "note": "one rank's HBM bytes per step from the step "
+                                         "program (bench.plan_hbm_bytes) / ms_per_step"}},
+            "transport_stats": {a: TRANSPORT.get(a) for a in runs},
             "alt_schedules": alts,
             "device_engines": device_engines,
             "sweep": sweep,

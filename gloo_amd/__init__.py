@@ -23,6 +23,7 @@ from .algorithms import (  # noqa: F401
     plan_sync,
 )
 from .collectives import AllreduceOptions, allreduce  # noqa: F401
+from .events import Event  # noqa: F401
 from . import errors  # noqa: F401
 from .errors import EnforceNotMet, Exception, HipError, IoException  # noqa: F401,A004
 

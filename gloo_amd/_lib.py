@@ -66,6 +66,14 @@ SIGNATURES = [
     ("glx_algorithm_bytes_sent", _i64, [_vp]),
     ("glx_algorithm_engine", _i, [_vp]),
     ("glx_algorithm_destroy", None, [_vp]),
+    ("glx_algorithm_transport_stats", _i, [_vp, ctypes.POINTER(_i64), _i]),
+    ("glx_algorithm_record", _i, [_vp, _vp]),
+    ("glx_context_ipc_stats", _i, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
+    ("glx_event_create", _i, [ctypes.POINTER(_vp)]),
+    ("glx_event_destroy", _i, [_vp]),
+    ("glx_event_record", _i, [_vp, _vp]),
+    ("glx_event_query", _i, [_vp]),
+    ("glx_event_wait", _i, [_vp, _vp]),
     ("glx_device_layout", _i64, [_i, _i, _i, _i64, _i, _i64, ctypes.POINTER(_i64), _i64]),
     ("glx_plan_sync", _i64, [_i, _i, _i, _i64, _i, _i64, _i64, _i, ctypes.POINTER(_i64),
                              _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
@@ -97,8 +105,8 @@ STORE_SET_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_char_p,
 STORE_GET_FN = ctypes.CFUNCTYPE(ctypes.c_int64, ctypes.c_void_p, ctypes.c_char_p,
                                 ctypes.c_void_p, ctypes.c_size_t)
 
-# status codes (glx_status)
-OK, ERR_INVALID, ERR_HIP, ERR_TIMEOUT, ERR_IO, ERR_ENFORCE, ERR_INTERNAL = range(7)
+# status codes (glx_status), and GLX_NOT_READY of glx_event_query
+OK, ERR_INVALID, ERR_HIP, ERR_TIMEOUT, ERR_IO, ERR_ENFORCE, ERR_INTERNAL, NOT_READY = range(8)
 
 
 def last_error():

@@ -178,6 +178,23 @@ class Algorithm:
         return {0: "steps", 1: "oneshot", 2: "twoshot",
                 3: "devsteps"}[lib.glx_algorithm_engine(self._h)]
 
+    def transport_stats(self):
+        """How this algorithm's messages moved since it was created:
+        peer_copies (hipMemcpyPeerAsync over xGMI), device_copies
+        (hipMemcpyAsync: same-device peers, or after hipMemcpyPeerAsync
+        refused a mapping), kernel_copies (copy kernel into the peer's
+        memory), device_kernels (device-driven engine launches), bytes."""
+        out = (ctypes.c_int64 * 5)()
+        if lib.glx_algorithm_transport_stats(self._h, out, 5) != 5:
+            check(_lib.ERR_INVALID, "transport_stats")
+        return dict(zip(("peer_copies", "device_copies", "kernel_copies", "device_kernels",
+                         "bytes"), list(out)))
+
+    def record(self, event):
+        """Record `event` (gloo_amd.Event) at the end of the last run()'s
+        work (on streams[0] when the algorithm has streams)."""
+        check(lib.glx_algorithm_record(self._h, event.handle), "record")
+
     def close(self):
         h = getattr(self, "_h", None)
         if h:

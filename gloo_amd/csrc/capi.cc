@@ -391,6 +391,73 @@ int glx_algorithm_engine(glx_algorithm* alg) {
   return alg->a->engine();
 }
 
+int glx_algorithm_transport_stats(glx_algorithm* alg, int64_t* out, int cap) {
+  if (alg == nullptr || out == nullptr || cap < 5) {
+    fail(GLX_ERR_INVALID, "glx_algorithm_transport_stats: null algorithm/output or cap < 5");
+    return -1;
+  }
+  const auto& t = alg->a->transportStats();
+  out[0] = t.peerCopies;
+  out[1] = t.deviceCopies;
+  out[2] = t.kernelCopies;
+  out[3] = t.deviceKernels;
+  out[4] = t.bytes;
+  return 5;
+}
+
+int glx_algorithm_record(glx_algorithm* alg, glx_event_t ev) {
+  return guarded([&]() -> int {
+    GLX_ENFORCE(alg != nullptr && ev != nullptr, "null algorithm/event");
+    alg->a->recordDone((hipEvent_t)ev);
+    return GLX_OK;
+  });
+}
+
+int glx_context_ipc_stats(glx_context* ctx, int64_t* imports, int64_t* base_fixups) {
+  if (ctx == nullptr) return fail(GLX_ERR_INVALID, "null context");
+  if (imports) *imports = ctx->c->ipcImports();
+  if (base_fixups) *base_fixups = ctx->c->ipcBaseFixups();
+  return GLX_OK;
+}
+
+int glx_event_create(glx_event_t* ev) {
+  if (ev == nullptr) return fail(GLX_ERR_INVALID, "glx_event_create: null output");
+  hipEvent_t e = nullptr;
+  const int rc = hipStatus(hipEventCreateWithFlags(&e, hipEventDisableTiming),
+                           "hipEventCreateWithFlags");
+  *ev = rc == GLX_OK ? (glx_event_t)e : nullptr;
+  return rc;
+}
+
+int glx_event_destroy(glx_event_t ev) {
+  if (ev == nullptr) return GLX_OK;
+  return hipStatus(hipEventDestroy((hipEvent_t)ev), "hipEventDestroy");
+}
+
+int glx_event_record(glx_event_t ev, glx_stream_t stream) {
+  if (ev == nullptr) return fail(GLX_ERR_INVALID, "glx_event_record: null event");
+  return hipStatus(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream), "hipEventRecord");
+}
+
+int glx_event_query(glx_event_t ev) {
+  if (ev == nullptr) return fail(GLX_ERR_INVALID, "glx_event_query: null event");
+  const hipError_t e = hipEventQuery((hipEvent_t)ev);
+  if (e == hipErrorNotReady) {
+    (void)hipGetLastError();
+    return GLX_NOT_READY;
+  }
+  return hipStatus(e, "hipEventQuery");
+}
+
+int glx_event_wait(glx_event_t ev, glx_stream_t stream) {
+  if (ev == nullptr) return fail(GLX_ERR_INVALID, "glx_event_wait: null event");
+  if (stream == nullptr) {
+    return hipStatus(hipEventSynchronize((hipEvent_t)ev), "hipEventSynchronize");
+  }
+  return hipStatus(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)ev, 0),
+                   "hipStreamWaitEvent");
+}
+
 void glx_algorithm_destroy(glx_algorithm* alg) {
   guarded([&]() -> int {
     delete alg;

@@ -303,6 +303,7 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
   events_.resize(plan_.steps.size() * (size_t)split_, nullptr);
   for (auto& e : events_) GLX_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   GLX_HIP_CHECK(hipEventCreateWithFlags(&computeMark_, hipEventDisableTiming));
+  GLX_HIP_CHECK(hipEventCreateWithFlags(&lastDone_, hipEventDisableTiming));
   if (contextSize_ > 1 && count_ > 0) publish();
 }
 
@@ -357,6 +358,9 @@ void HipPlanExecutor::release() noexcept {
   if (device_ < 0) return;  // nothing was acquired
   hipSetDevice(device_);
   drainCredits();
+  // the last call's work may sit on a caller's stream (runFn with a stream):
+  // it reads our scratch until it completes
+  if (lastDone_ != nullptr && lastStream_ != nullptr) hipEventSynchronize(lastDone_);
   if (compute_ != nullptr) hipStreamSynchronize(compute_);
   for (auto& c : copies_) hipStreamSynchronize(c.s);
   for (hipStream_t st : {h2d_, d2h_}) {
@@ -379,6 +383,7 @@ void HipPlanExecutor::release() noexcept {
     if (e != nullptr) hipEventDestroy(e);
   }
   if (computeMark_) hipEventDestroy(computeMark_);
+  if (lastDone_) hipEventDestroy(lastDone_);
   for (auto& b : blocks_) {
     if (b.ref.id > 0) context_->releaseShared(b.ref.id);
   }
@@ -735,6 +740,7 @@ void HipPlanExecutor::run() {
   for (size_t i = 1; i < ptrs_.size(); i++) {
     GLX_HIP_CHECK(hipMemcpyAsync(ptrs_[i], ptr0, bytes, hipMemcpyDeviceToDevice, compute_));
   }
+  noteDone(compute_);
   GLX_TRACE("r%d sync", contextRank_);
   if (!userStream_) {
     GLX_HIP_CHECK(spinSync(compute_));
@@ -813,6 +819,7 @@ void HipPlanExecutor::runFn(const FnCall& call) {
     GLX_HIP_CHECK(hipMemcpyAsync(call.out[i], out0, (size_t)count_ * esize_,
                                  hipMemcpyDeviceToDevice, compute_));
   }
+  noteDone(compute_);
   if (call.stream == nullptr) {
     GLX_HIP_CHECK(spinSync(compute_));
     checkDevice();
@@ -864,6 +871,7 @@ void HipPlanExecutor::runFnHost(const FnCall& call) {
   for (void* p : call.out) {
     GLX_HIP_CHECK(hipMemcpyAsync(p, out0, bytes, hipMemcpyDeviceToHost, compute_));
   }
+  noteDone(compute_);
   GLX_HIP_CHECK(hipStreamSynchronize(compute_));
   checkDevice();
 }
@@ -955,7 +963,18 @@ void HipPlanExecutor::runHost() {
   GLX_HIP_CHECK(hipStreamSynchronize(d2h_));
   GLX_HIP_CHECK(hipStreamSynchronize(compute_));
   GLX_HIP_CHECK(hipStreamSynchronize(h2d_));
+  noteDone(d2h_);
   checkDevice();
+}
+
+void HipPlanExecutor::noteDone(hipStream_t s) {
+  GLX_HIP_CHECK(hipEventRecord(lastDone_, s));
+  lastStream_ = s;
+}
+
+void HipPlanExecutor::recordDone(hipEvent_t ev) {
+  GLX_HIP_CHECK(hipSetDevice(device_));
+  GLX_HIP_CHECK(hipEventRecord(ev, lastStream_ != nullptr ? lastStream_ : compute_));
 }
 
 void HipPlanExecutor::exchange(char* ptr0) {
@@ -1009,17 +1028,30 @@ void HipPlanExecutor::exchange(char* ptr0) {
             if (copyEngine_ == kCopyKernel) {
               ce = glx::launch_copy(dst + at, src + at, len, cs.s);
               GLX_HIP_CHECK(ce);
+              transport_.kernelCopies++;
             } else if (peerCopyOk_ && oc.peerDevice >= 0 && oc.peerDevice != device_) {
               ce = hipMemcpyPeerAsync(dst + at, oc.peerDevice, src + at, device_, len, cs.s);
-              if (ce != hipSuccess) {
+              if (ce == hipSuccess) {
+                transport_.peerCopies++;
+              } else {
                 (void)hipGetLastError();
-                peerCopyOk_ = false;  // e.g. an IPC mapping the peer API rejects
+                // e.g. an IPC mapping the peer API rejects: the copy still
+                // crosses xGMI (the destination is the peer's memory), now as
+                // a plain device copy; say so once and count every one
+                peerCopyOk_ = false;
+                std::fprintf(stderr,
+                             "[gloo_amd] rank %d: hipMemcpyPeerAsync to device %d refused "
+                             "(%s: %s); peer copies of this algorithm use hipMemcpyAsync\n",
+                             contextRank_, oc.peerDevice, hipGetErrorName(ce),
+                             hipGetErrorString(ce));
               }
             }
             if (ce != hipSuccess) {
               GLX_HIP_CHECK(hipMemcpyAsync(dst + at, src + at, len, hipMemcpyDeviceToDevice,
                                            cs.s));
+              transport_.deviceCopies++;
             }
+            transport_.bytes += (int64_t)len;
             GLX_TRACE("r%d   copy part %d issued (%zu bytes)", contextRank_, j, len);
             hipEvent_t ev = events_[i * (size_t)split_ + (size_t)j];
             GLX_HIP_CHECK(hipEventRecord(ev, cs.s));
@@ -1573,6 +1605,7 @@ void HipPlanExecutor::runDevice(char* ptr0) {
     GLX_TRACE("r%d one-shot epoch %lu (G=%d slice=%zu)", contextRank_, (unsigned long)e, p.G,
               p.slice);
     GLX_HIP_CHECK(glx::launch_oneshot(op_, dtype_, p, compute_));
+    transport_.deviceKernels++;
   } else if (engine_ == kEngineDevSteps) {
     if (devSteps_ == nullptr) buildDevSteps();
     glx::PlanKernelParams p = pk_;
@@ -1582,6 +1615,7 @@ void HipPlanExecutor::runDevice(char* ptr0) {
     GLX_TRACE("r%d plan kernel run %lu (G=%d, %d steps)", contextRank_, (unsigned long)p.run,
               p.G, p.nsteps);
     GLX_HIP_CHECK(glx::launch_plan_kernel(op_, dtype_, p, compute_));
+    transport_.deviceKernels++;
   } else {
     glx::TwoShotParams p = ts_;
     p.buf = ptr0;
@@ -1614,6 +1648,7 @@ void HipPlanExecutor::runDevice(char* ptr0) {
     GLX_TRACE("r%d two-shot epoch %lu (G=%d slice=%zu)", contextRank_, (unsigned long)e, p.G,
               p.slice);
     GLX_HIP_CHECK(glx::launch_twoshot(op_, dtype_, p, compute_));
+    transport_.deviceKernels++;
     if (devTrace()) traceTwoShot(p);
   }
   GLX_HIP_CHECK(hipEventRecord(ddDone_, compute_));

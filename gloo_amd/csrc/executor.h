@@ -67,6 +67,23 @@ class HipPlanExecutor : public Algorithm {
 
   int64_t bytesSentPerRun() const { return plan_.bytes_sent * (int64_t)esize_; }
 
+  // How this algorithm's messages actually moved, counted since
+  // construction (SENDs of the host-issued steps engine, by mechanism, and
+  // launches of a device-driven engine, whose kernels store into the peers'
+  // memory themselves).
+  struct TransportStats {
+    int64_t peerCopies = 0;     // hipMemcpyPeerAsync (DMA engines over xGMI)
+    int64_t deviceCopies = 0;   // hipMemcpyAsync: same-device peers, or after
+                                // hipMemcpyPeerAsync refused an IPC mapping
+    int64_t kernelCopies = 0;   // copy kernel storing into the peer's memory
+    int64_t deviceKernels = 0;  // one-shot / two-shot / plan kernel launches
+    int64_t bytes = 0;          // bytes of the copies above
+  };
+  const TransportStats& transportStats() const { return transport_; }
+  // Record `ev` after this algorithm's last enqueued work: the compute
+  // stream of the last run (the caller's stream when one was given).
+  void recordDone(hipEvent_t ev);
+
   // Copies of one SEND are split over this many streams per destination
   // (several DMA engines feeding one link).  Read at construction.
   static void setCopySplit(int k);
@@ -175,6 +192,7 @@ class HipPlanExecutor : public Algorithm {
   int split_ = 1;
   int copyEngine_ = kCopyDma;
   bool peerCopyOk_ = true;  // hipMemcpyPeerAsync accepted for IPC-mapped peers
+  TransportStats transport_;
   bool ownCompute_ = false;
   std::vector<ScratchBlock> blocks_;                  // ours
   std::map<int, std::vector<ScratchBlock>> peerBlocks_;  // by destination rank
@@ -205,6 +223,11 @@ class HipPlanExecutor : public Algorithm {
   std::vector<int> stepChan_;        // channel index per step
   std::vector<hipEvent_t> events_;   // split_ per step
   hipEvent_t computeMark_ = nullptr;
+  // end of the last call's work and the stream it ran on (the caller's, for
+  // runFn with a stream): release() waits for it, recordDone() orders after it
+  hipEvent_t lastDone_ = nullptr;
+  hipStream_t lastStream_ = nullptr;
+  void noteDone(hipStream_t s);
   bool resolved_ = false;
   std::vector<Pending> pending_;
   std::vector<InflightSend> inflight_;

@@ -148,6 +148,14 @@ class Context:
     def nextSlot(self, numToSkip=1):  # noqa: N802,N803
         return lib.glx_context_next_slot(self._h, int(numToSkip))
 
+    def ipc_stats(self):
+        """IPC imports made and canary-checked, and how many the runtime
+        mapped at the base of the exporter's allocation (corrected)."""
+        import ctypes
+        a, b = ctypes.c_int64(0), ctypes.c_int64(0)
+        check(lib.glx_context_ipc_stats(self._h, ctypes.byref(a), ctypes.byref(b)), "ipc_stats")
+        return {"imports": a.value, "base_fixups": b.value}
+
     def close(self):
         h = getattr(self, "_h", None)
         if h:

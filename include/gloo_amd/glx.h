@@ -295,7 +295,45 @@ int64_t glx_algorithm_bytes_sent(glx_algorithm* alg);
  * the schedule's step program (the plan kernel). */
 #define GLX_ENGINE_DEVSTEPS 3
 int glx_algorithm_engine(glx_algorithm* alg);
+/* How this algorithm's messages actually moved since it was created, as 5
+ * int64 written to out (cap >= 5): {peer_copies (hipMemcpyPeerAsync, the DMA
+ * engines over xGMI), device_copies (hipMemcpyAsync: peers on the same device,
+ * or a peer whose IPC mapping hipMemcpyPeerAsync refused -- logged once),
+ * kernel_copies (copy kernel storing into the peer's memory),
+ * device_kernels (launches of a device-driven engine, whose kernels store into
+ * the peers' memory themselves), bytes (of the copies)}.  The peer-copy analog
+ * of the reference's transport byte counters and of its intra-process peer
+ * copies (gloo/cuda_collectives_native.h:205-276).  Returns 5 or -1. */
+int glx_algorithm_transport_stats(glx_algorithm* alg, int64_t* out, int cap);
 void glx_algorithm_destroy(glx_algorithm* alg);
+
+/* IPC imports this context has made and checked (every imported shared
+ * block's canary word is verified before use), and how many of them the
+ * runtime mapped at the base of the exporter's allocation rather than at the
+ * exported pointer (corrected with the published offset).  Returns GLX_OK. */
+int glx_context_ipc_stats(glx_context* ctx, int64_t* imports, int64_t* base_fixups);
+
+/* ---- events (gloo::CudaStream's record / wait, gloo/cuda.h:40-120) -------
+ * A caller that gives an algorithm streams gets its outputs valid once
+ * streams[0] reaches the end of run(); these order other streams (or the
+ * host) after that point without synchronising the device. */
+typedef void* glx_event_t; /* a hipEvent_t */
+/* hipEventCreateWithFlags(hipEventDisableTiming). */
+int glx_event_create(glx_event_t* ev);
+int glx_event_destroy(glx_event_t ev);
+/* Record on `stream` (NULL = the legacy default stream). */
+int glx_event_record(glx_event_t ev, glx_stream_t stream);
+/* GLX_OK when everything recorded before it has completed, GLX_NOT_READY
+ * while it is pending, else an error code. */
+#define GLX_NOT_READY 7
+int glx_event_query(glx_event_t ev);
+/* Make `stream` wait for the event on the device (hipStreamWaitEvent); with
+ * stream NULL the calling thread blocks until it completes. */
+int glx_event_wait(glx_event_t ev, glx_stream_t stream);
+/* Record `ev` where run() left the algorithm's work: the end of its last
+ * call on its compute stream (streams[0] when given, else the internal
+ * stream, on which a run without streams has already completed). */
+int glx_algorithm_record(glx_algorithm* alg, glx_event_t ev);
 
 /* ---- schedule introspection (host logic; no GPU needed) ----------------- */
 /* The per-rank step program an algorithm executes.  Each step is 8 int64:

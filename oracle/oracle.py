@@ -85,6 +85,8 @@ def _load_ref():
                                          ctypes.POINTER(vp)]
         lib.ref_allreduce_fn.restype = i
         lib.ref_last_error.restype = ctypes.c_char_p
+        lib.ref_reduce_mt.argtypes = [i, i, vp, vp, vp, sz, i, i, ctypes.POINTER(ctypes.c_double)]
+        lib.ref_reduce_mt.restype = i
         lib.ref_f32_to_f16.argtypes = [vp, vp, sz]
         lib.ref_f16_to_f32.argtypes = [vp, vp, sz]
         _ref = lib

@@ -11,6 +11,8 @@
 //   * gloo::allreduce(AllreduceOptions)       (gloo/allreduce.cc:97-146, RING/BCUBE)
 // exactly the way the reference's tests do: P threads in one process, one
 // HashStore, tcp devices on loopback (gloo/test/base_test.h:91-166).
+#include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdint>
 #include <cstring>
@@ -163,9 +165,54 @@ int allreduceFnT(int algo, int op, int P, int nin, int nout, size_t count, size_
   return 0;
 }
 
+template <typename T>
+int reduceSlices(int op, char* c, const char* a, const char* b, size_t n, int threads,
+                 int iters, double* seconds) {
+  if (threads < 1 || iters < 1) return -1;
+  std::atomic<int> ready{0};
+  std::atomic<bool> go{false};
+  std::vector<std::thread> ts;
+  const size_t per = (n + (size_t)threads - 1) / (size_t)threads;
+  for (int t = 0; t < threads; t++) {
+    ts.emplace_back([&, t]() {
+      const size_t lo = std::min(n, (size_t)t * per), hi = std::min(n, lo + per);
+      ready.fetch_add(1);
+      while (!go.load()) std::this_thread::yield();
+      for (int i = 0; i < iters; i++) {
+        reduceT<T>(op, c + lo * sizeof(T), a + lo * sizeof(T), b + lo * sizeof(T), hi - lo);
+      }
+    });
+  }
+  while (ready.load() < threads) std::this_thread::yield();
+  const auto t0 = std::chrono::steady_clock::now();
+  go.store(true);
+  for (auto& th : ts) th.join();
+  const auto t1 = std::chrono::steady_clock::now();
+  if (seconds != nullptr) *seconds = std::chrono::duration<double>(t1 - t0).count();
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
+
+// The reference's gloo::sum/product/max/min<T> split over `threads` host
+// threads (contiguous slices), each running its slice `iters` times; wall
+// time of the whole in *seconds (the CPU baseline's N-thread leg).
+int ref_reduce_mt(int op, int dtype, void* c, const void* a, const void* b, size_t n,
+                  int threads, int iters, double* seconds) {
+  char* cc = static_cast<char*>(c);
+  const char* ca = static_cast<const char*>(a);
+  const char* cb = static_cast<const char*>(b);
+  switch (dtype) {
+    case R_FLOAT32: return reduceSlices<float>(op, cc, ca, cb, n, threads, iters, seconds);
+    case R_FLOAT16:
+      return reduceSlices<gloo::float16>(op, cc, ca, cb, n, threads, iters, seconds);
+    case R_INT32: return reduceSlices<int32_t>(op, cc, ca, cb, n, threads, iters, seconds);
+    case R_FLOAT64: return reduceSlices<double>(op, cc, ca, cb, n, threads, iters, seconds);
+  }
+  return -1;
+}
 
 const char* ref_last_error() { return g_err.c_str(); }
 
