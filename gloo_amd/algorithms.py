@@ -183,12 +183,14 @@ class Algorithm:
         peer_copies (hipMemcpyPeerAsync over xGMI), device_copies
         (hipMemcpyAsync: same-device peers, or after hipMemcpyPeerAsync
         refused a mapping), kernel_copies (copy kernel into the peer's
-        memory), device_kernels (device-driven engine launches), bytes."""
-        out = (ctypes.c_int64 * 5)()
-        if lib.glx_algorithm_transport_stats(self._h, out, 5) != 5:
+        memory), device_kernels (device-driven engine launches), bytes, and
+        host_folds (multi-pointer host buffers below kOnDeviceThreshold folded
+        on the host)."""
+        out = (ctypes.c_int64 * 6)()
+        if lib.glx_algorithm_transport_stats(self._h, out, 6) != 6:
             check(_lib.ERR_INVALID, "transport_stats")
         return dict(zip(("peer_copies", "device_copies", "kernel_copies", "device_kernels",
-                         "bytes"), list(out)))
+                         "bytes", "host_folds"), list(out)))
 
     def record(self, event):
         """Record `event` (gloo_amd.Event) at the end of the last run()'s

@@ -12,6 +12,7 @@
 #include "common.h"
 #include "context.h"
 #include "executor.h"
+#include "host_ops.h"
 #include "kernels.h"
 #include "plan.h"
 #include "store.h"
@@ -126,6 +127,17 @@ int glx_reduce_n(int op, int dtype, void* dst, const void* const* srcs, int k, s
   }
   return hipStatus(glx::launch_reduce_n(op, dtype, dst, srcs, k, n, (hipStream_t)stream),
                    "glx_reduce_n");
+}
+
+int glx_host_reduce_n(int op, int dtype, void* dst, const void* const* srcs, int k,
+                      size_t n) {
+  return guarded([&]() -> int {
+    GLX_ENFORCE(validOp(op) && validDtype(dtype), "glx_host_reduce_n: unknown op/dtype");
+    GLX_ENFORCE(k >= 1 && srcs != nullptr && (n == 0 || dst != nullptr),
+                "glx_host_reduce_n: need k >= 1 sources and a destination");
+    if (n > 0) glx::host_reduce_n(op, dtype, dst, srcs, k, n);
+    return GLX_OK;
+  });
 }
 
 int glx_peer_copy(void* dst, int dst_dev, const void* src, int src_dev, size_t bytes,
@@ -392,8 +404,8 @@ int glx_algorithm_engine(glx_algorithm* alg) {
 }
 
 int glx_algorithm_transport_stats(glx_algorithm* alg, int64_t* out, int cap) {
-  if (alg == nullptr || out == nullptr || cap < 5) {
-    fail(GLX_ERR_INVALID, "glx_algorithm_transport_stats: null algorithm/output or cap < 5");
+  if (alg == nullptr || out == nullptr || cap < 6) {
+    fail(GLX_ERR_INVALID, "glx_algorithm_transport_stats: null algorithm/output or cap < 6");
     return -1;
   }
   const auto& t = alg->a->transportStats();
@@ -402,7 +414,8 @@ int glx_algorithm_transport_stats(glx_algorithm* alg, int64_t* out, int cap) {
   out[2] = t.kernelCopies;
   out[3] = t.deviceKernels;
   out[4] = t.bytes;
-  return 5;
+  out[5] = t.hostFolds;
+  return 6;
 }
 
 int glx_algorithm_record(glx_algorithm* alg, glx_event_t ev) {

@@ -15,6 +15,7 @@
 #include <thread>
 
 #include "common.h"
+#include "host_ops.h"
 #include "kernels.h"
 
 namespace gloo {
@@ -377,6 +378,7 @@ void HipPlanExecutor::release() noexcept {
   }
   if (hostDone_) hipEventDestroy(hostDone_);
   for (char* d : devBufs_) hipFree(d);
+  if (hostStage_) hipHostFree(hostStage_);
   for (char* d : fnStage_) hipFree(d);
   for (void* p : registered_) hipHostUnregister(p);
   for (auto& e : events_) {
@@ -878,7 +880,16 @@ void HipPlanExecutor::runFnHost(const FnCall& call) {
 
 void HipPlanExecutor::setupHostMode() {
   const size_t bytes = (size_t)count_ * esize_;
-  for (void* p : ptrs_) {
+  // Several host pointers under kOnDeviceThreshold: fold them on the host
+  // into one pinned staging buffer and stage only that through the device
+  // (the reference's cudaHostReduce / cudaHostBroadcast below the threshold,
+  // gloo/cuda_allreduce_halving_doubling.cc:478-484)
+  hostFold_ = ptrs_.size() > 1 && bytes < glx::kOnDeviceThreshold;
+  if (hostFold_) {
+    GLX_HIP_CHECK(hipHostMalloc((void**)&hostStage_, std::max<size_t>(bytes, 16),
+                                hipHostMallocDefault));
+  }
+  for (void* p : hostSources()) {
     if (!isPinnedHost(p)) {
       // pin the caller's buffer for the algorithm's lifetime (the reference's
       // algorithms also bind their buffers at construction); if the runtime
@@ -921,12 +932,19 @@ void HipPlanExecutor::waitH2D(hipStream_t s, int& waited, int64_t off, int64_t l
   }
 }
 
+// The host buffers the device copies are staged from and back to: the
+// user's pointers, or the one pinned buffer they were folded into.
+std::vector<void*> HipPlanExecutor::hostSources() const {
+  if (hostFold_) return {hostStage_};
+  return ptrs_;
+}
+
 // Final values of `ranges` (in devBufs_[0]) to every user pointer, on d2h_
 // (the caller has made d2h_ wait for the writes).
 void HipPlanExecutor::copyBack(const std::vector<glx::Range>& ranges) {
   for (const glx::Range& r : ranges) {
     const size_t at = (size_t)r.off * esize_, n = (size_t)r.len * esize_;
-    for (void* p : ptrs_) {
+    for (void* p : hostSources()) {
       GLX_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(p) + at, devBufs_[0] + at, n,
                                    hipMemcpyDeviceToHost, d2h_));
     }
@@ -935,18 +953,29 @@ void HipPlanExecutor::copyBack(const std::vector<glx::Range>& ranges) {
 
 void HipPlanExecutor::runHost() {
   if (contextSize_ == 1 && ptrs_.size() == 1) return;  // the result is the input
+  const size_t bytes = (size_t)count_ * esize_;
+  if (hostFold_) {  // local reduce on the host (below kOnDeviceThreshold)
+    std::vector<const void*> srcs(ptrs_.begin(), ptrs_.end());
+    glx::host_reduce_n(op_, dtype_, hostStage_, srcs.data(), (int)srcs.size(), (size_t)count_);
+    transport_.hostFolds++;
+    if (contextSize_ == 1) {
+      for (void* p : ptrs_) std::memcpy(p, hostStage_, bytes);
+      return;
+    }
+  }
+  const std::vector<void*> hsrc = hostSources();
   computeH2dWaited_ = -1;
   for (auto& c : copies_) c.h2dWaited = -1;
   for (size_t j = 0; j < stage_.h2d.size(); j++) {
     const glx::Range& r = stage_.h2d[j];
     const size_t at = (size_t)r.off * esize_, n = (size_t)r.len * esize_;
-    for (size_t k = 0; k < ptrs_.size(); k++) {
-      GLX_HIP_CHECK(hipMemcpyAsync(devBufs_[k] + at, static_cast<const char*>(ptrs_[k]) + at, n,
+    for (size_t k = 0; k < hsrc.size(); k++) {
+      GLX_HIP_CHECK(hipMemcpyAsync(devBufs_[k] + at, static_cast<const char*>(hsrc[k]) + at, n,
                                    hipMemcpyHostToDevice, h2d_));
     }
     GLX_HIP_CHECK(hipEventRecord(h2dEvents_[j], h2d_));
   }
-  if (ptrs_.size() > 1) {  // local fold needs every buffer whole
+  if (hsrc.size() > 1) {  // local fold needs every buffer whole
     waitH2D(compute_, computeH2dWaited_, 0, count_);
     std::vector<const void*> srcs(devBufs_.begin(), devBufs_.end());
     GLX_HIP_CHECK(glx::launch_reduce_n(op_, dtype_, devBufs_[0], srcs.data(), (int)srcs.size(),
@@ -955,7 +984,7 @@ void HipPlanExecutor::runHost() {
   if (contextSize_ > 1) exchange(devBufs_[0]);
   // ranges no step wrote: their value is the local fold (a no-op for one
   // pointer, whose host copy already holds it)
-  if (ptrs_.size() > 1 && !stage_.d2hRest.empty()) {
+  if (hsrc.size() > 1 && !stage_.d2hRest.empty()) {
     GLX_HIP_CHECK(hipEventRecord(hostDone_, compute_));
     GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, hostDone_, 0));
     copyBack(stage_.d2hRest);
@@ -965,6 +994,9 @@ void HipPlanExecutor::runHost() {
   GLX_HIP_CHECK(hipStreamSynchronize(h2d_));
   noteDone(d2h_);
   checkDevice();
+  if (hostFold_) {  // local broadcast on the host
+    for (void* p : ptrs_) std::memcpy(p, hostStage_, bytes);
+  }
 }
 
 void HipPlanExecutor::noteDone(hipStream_t s) {

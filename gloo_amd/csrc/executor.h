@@ -78,6 +78,7 @@ class HipPlanExecutor : public Algorithm {
     int64_t kernelCopies = 0;   // copy kernel storing into the peer's memory
     int64_t deviceKernels = 0;  // one-shot / two-shot / plan kernel launches
     int64_t bytes = 0;          // bytes of the copies above
+    int64_t hostFolds = 0;      // local reduces done on the host (kOnDeviceThreshold)
   };
   const TransportStats& transportStats() const { return transport_; }
   // Record `ev` after this algorithm's last enqueued work: the compute
@@ -204,7 +205,10 @@ class HipPlanExecutor : public Algorithm {
   // h2d_ and every step waits only for the pieces of its own range; each
   // range is copied back on d2h_ right after its final write.
   bool hostMode_ = false;
-  std::vector<char*> devBufs_;     // device copy of each user pointer
+  std::vector<char*> devBufs_;     // device copy of each user pointer (or of hostStage_)
+  bool hostFold_ = false;          // several pointers < kOnDeviceThreshold: fold on the host
+  char* hostStage_ = nullptr;      // pinned: the host fold's result, staged and returned
+  std::vector<void*> hostSources() const;
   std::vector<void*> registered_;  // host ranges pinned by us
   hipStream_t h2d_ = nullptr, d2h_ = nullptr;
   glx::StagePlan stage_;

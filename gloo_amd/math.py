@@ -60,3 +60,15 @@ def max(c, a, b, **kw):  # noqa: A001
 
 def min(c, a, b, **kw):  # noqa: A001
     return reduce(ReductionType.MIN, c, a, b, **kw)
+
+
+def host_reduce_n(op, dtype, dst, srcs):
+    """dst = left fold of op over srcs on HOST memory (numpy arrays of the
+    dtype's storage type; dst may be srcs[0]): the local reduce the
+    algorithms do on the host for multi-pointer host buffers below
+    kOnDeviceThreshold (gloo/algorithm.cc:16).  Same bits as the kernels."""
+    n = builtins.min([dst.size] + [s.size for s in srcs])
+    arr = (ctypes.c_void_p * len(srcs))(*[s.ctypes.data for s in srcs])
+    check(lib.glx_host_reduce_n(int(op), int(dtype), dst.ctypes.data, arr, len(srcs), int(n)),
+          "host_reduce_n")
+    return dst

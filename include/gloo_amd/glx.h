@@ -88,6 +88,15 @@ int glx_reduce(int op, int dtype, void* dst, const void* a, const void* b,
 int glx_reduce_n(int op, int dtype, void* dst, const void* const* srcs, int k,
                  size_t n, glx_stream_t stream);
 
+/* The same left fold on HOST memory (host pointers; dst may be srcs[0]),
+ * 1 <= k.  The analog of the reference's cudaHostReduce, which its GPU
+ * algorithms use below kOnDeviceThreshold = 256 KiB (gloo/algorithm.cc:16,
+ * gloo/cuda_allreduce_halving_doubling.cc:478-484); the algorithms here use
+ * it for multi-pointer host buffers under that size.  Same bits as
+ * glx_reduce_n. */
+int glx_host_reduce_n(int op, int dtype, void* dst, const void* const* srcs, int k,
+                      size_t n);
+
 /* Device->device copy of `bytes` from (src on srcDev) to (dst on dstDev) over
  * xGMI with hipMemcpyPeerAsync.  Replaces the D2D copy of CudaStream::copyAsync
  * (gloo/cuda.cu:91-149) and the transport's Buffer::send for device buffers
@@ -295,15 +304,17 @@ int64_t glx_algorithm_bytes_sent(glx_algorithm* alg);
  * the schedule's step program (the plan kernel). */
 #define GLX_ENGINE_DEVSTEPS 3
 int glx_algorithm_engine(glx_algorithm* alg);
-/* How this algorithm's messages actually moved since it was created, as 5
- * int64 written to out (cap >= 5): {peer_copies (hipMemcpyPeerAsync, the DMA
+/* How this algorithm's messages actually moved since it was created, as 6
+ * int64 written to out (cap >= 6): {peer_copies (hipMemcpyPeerAsync, the DMA
  * engines over xGMI), device_copies (hipMemcpyAsync: peers on the same device,
  * or a peer whose IPC mapping hipMemcpyPeerAsync refused -- logged once),
  * kernel_copies (copy kernel storing into the peer's memory),
  * device_kernels (launches of a device-driven engine, whose kernels store into
- * the peers' memory themselves), bytes (of the copies)}.  The peer-copy analog
+ * the peers' memory themselves), bytes (of the copies), host_folds (local
+ * multi-pointer reduces done on the host: host buffers below
+ * kOnDeviceThreshold = 256 KiB, gloo/algorithm.cc:16)}.  The peer-copy analog
  * of the reference's transport byte counters and of its intra-process peer
- * copies (gloo/cuda_collectives_native.h:205-276).  Returns 5 or -1. */
+ * copies (gloo/cuda_collectives_native.h:205-276).  Returns 6 or -1. */
 int glx_algorithm_transport_stats(glx_algorithm* alg, int64_t* out, int cap);
 void glx_algorithm_destroy(glx_algorithm* alg);
 

@@ -1,0 +1,221 @@
+// binding_test.cc -- TEST INFRASTRUCTURE: integration/gloo/hip_allreduce.h
+// (the header a gloo maintainer adds) compiled against the REFERENCE's own
+// headers (/root/reference) and linked with the reference's objects
+// (oracle/_ref/obj: its Context, rendezvous stores, tcp transport,
+// AllreduceRingChunked) plus libgloo_amd.so.  Built by `make -C oracle
+// binding` into oracle/_ref/binding_test.
+//
+//   binding_test cpu   no GPU: type / reduction-type mapping, CUSTOM refused
+//                      with gloo::EnforceNotMet, the store bridge both ways
+//   binding_test gpu   P thread-ranks on one GPU bootstrapped exactly like
+//                      the reference's tests (HashStore + tcp loopback +
+//                      rendezvous::Context::connectFullMesh, gloo/test/
+//                      base_test.h:91-166); HipAllreduceRingChunked<float>,
+//                      HipAllreduceHalvingDoubling<float16|int32> on device
+//                      buffers, compared bit for bit with the reference's
+//                      own CPU AllreduceRingChunked / HalvingDoubling run on
+//                      host copies of the same inputs in the same process.
+#include <hip/hip_runtime_api.h>
+
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "gloo/allreduce_halving_doubling.h"
+#include "gloo/allreduce_ring_chunked.h"
+#include "gloo/hip_allreduce.h"
+#include "gloo/rendezvous/context.h"
+#include "gloo/rendezvous/hash_store.h"
+#include "gloo/transport/tcp/device.h"
+
+namespace {
+
+int failures = 0;
+
+#define EXPECT(cond, ...)                                 \
+  do {                                                    \
+    if (!(cond)) {                                        \
+      std::fprintf(stderr, "FAIL %s:%d: %s ", __FILE__, __LINE__, #cond); \
+      std::fprintf(stderr, __VA_ARGS__);                  \
+      std::fprintf(stderr, "\n");                         \
+      failures++;                                         \
+    }                                                     \
+  } while (0)
+
+uint64_t mix(uint64_t x) {
+  x += 0x9e3779b97f4a7c15ull;
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+  return x ^ (x >> 31);
+}
+
+template <typename T> T value(int r, size_t i);
+template <> float value<float>(int r, size_t i) {
+  return (float)((int64_t)(mix(((uint64_t)r << 40) ^ i) >> 40) - (1 << 23)) / (float)(1 << 23);
+}
+template <> int32_t value<int32_t>(int r, size_t i) {
+  return (int32_t)(mix(((uint64_t)r << 40) ^ i) >> 44) - (1 << 19);
+}
+template <> gloo::float16 value<gloo::float16>(int r, size_t i) {
+  return gloo::cpu_float2half_rn(value<float>(r, i));
+}
+
+int cpuMode() {
+  using namespace gloo;
+  EXPECT(hip::GlxType<float>::value == GLX_FLOAT32, "float");
+  EXPECT(hip::GlxType<float16>::value == GLX_FLOAT16, "float16");
+  EXPECT(hip::GlxType<int32_t>::value == GLX_INT32, "int32");
+  EXPECT(hip::glxOp(ReductionFunction<float>::sum) == GLX_SUM, "sum");
+  EXPECT(hip::glxOp(ReductionFunction<float>::product) == GLX_PRODUCT, "product");
+  EXPECT(hip::glxOp(ReductionFunction<float>::max) == GLX_MAX, "max");
+  EXPECT(hip::glxOp(ReductionFunction<float>::min) == GLX_MIN, "min");
+  ReductionFunction<float> custom(CUSTOM, [](float*, const float*, size_t) {});
+  bool refused = false;
+  try {
+    hip::glxOp(&custom);
+  } catch (const EnforceNotMet&) {
+    refused = true;
+  }
+  EXPECT(refused, "CUSTOM must be refused with gloo::EnforceNotMet");
+  // glx_* errors surface as gloo's exceptions
+  bool io = false, enforce = false;
+  try {
+    hip::check(GLX_ERR_TIMEOUT, "probe");
+  } catch (const IoException&) {
+    io = true;
+  }
+  try {
+    hip::check(GLX_ERR_INVALID, "probe");
+  } catch (const EnforceNotMet&) {
+    enforce = true;
+  }
+  EXPECT(io && enforce, "error mapping");
+  // the store bridge, both ways, with a prefix
+  rendezvous::HashStore hs;
+  hip::StoreBridge bridge(hs, "pfx/");
+  const char msg[] = "endpoint";
+  EXPECT(glx_store_set(bridge.handle(), "a", msg, sizeof(msg)) == GLX_OK, "%s", glx_last_error());
+  const auto got = hs.get("pfx/a");
+  EXPECT(got.size() == sizeof(msg) && std::memcmp(got.data(), msg, sizeof(msg)) == 0, "set");
+  hs.set("pfx/b", std::vector<char>(70000, 'x'));
+  std::vector<char> buf(70000);
+  size_t len = 0;
+  EXPECT(glx_store_get(bridge.handle(), "b", buf.data(), buf.size(), &len, 1000) == GLX_OK,
+         "%s", glx_last_error());
+  EXPECT(len == 70000 && buf[69999] == 'x', "get");
+  EXPECT(glx_store_get(bridge.handle(), "missing", buf.data(), buf.size(), &len, 30) ==
+             GLX_ERR_TIMEOUT,
+         "a missing key must time out");
+  std::printf("binding_test cpu: %s\n", failures ? "FAILED" : "OK");
+  return failures ? 1 : 0;
+}
+
+// P thread-ranks as in gloo/test/base_test.h:91-166
+void spawn(int P, const std::function<void(std::shared_ptr<gloo::Context>,
+                                           gloo::rendezvous::Store&, int)>& fn) {
+  auto store = std::make_shared<gloo::rendezvous::HashStore>();
+  std::vector<std::thread> ts;
+  std::vector<std::string> errs(P);
+  for (int r = 0; r < P; r++) {
+    ts.emplace_back([&, r] {
+      try {
+        gloo::transport::tcp::attr attr("127.0.0.1");
+        auto dev = gloo::transport::tcp::CreateDevice(attr);
+        auto ctx = std::make_shared<gloo::rendezvous::Context>(r, P);
+        ctx->setTimeout(std::chrono::seconds(60));
+        ctx->connectFullMesh(*store, dev);
+        fn(ctx, *store, r);
+      } catch (const std::exception& e) {
+        errs[r] = e.what();
+      }
+    });
+  }
+  for (auto& t : ts) t.join();
+  for (int r = 0; r < P; r++) EXPECT(errs[r].empty(), "rank %d: %s", r, errs[r].c_str());
+}
+
+template <typename T, template <typename> class Hip, template <typename> class Ref>
+void compare(const char* name, int P, int count, int nptrs, const gloo::ReductionFunction<T>* fn) {
+  // inputs, and the reference's own CPU algorithm on host copies of them
+  std::vector<std::vector<std::vector<T>>> in(P), ref(P), got(P);
+  for (int r = 0; r < P; r++) {
+    for (int k = 0; k < nptrs; k++) {
+      std::vector<T> v((size_t)count);
+      for (int i = 0; i < count; i++) v[(size_t)i] = value<T>(r * nptrs + k, (size_t)i);
+      in[r].push_back(v);
+    }
+    ref[r] = in[r];
+    got[r] = in[r];
+  }
+  spawn(P, [&](std::shared_ptr<gloo::Context> ctx, gloo::rendezvous::Store&, int r) {
+    std::vector<T*> ptrs;
+    for (auto& v : ref[r]) ptrs.push_back(v.data());
+    Ref<T> alg(ctx, ptrs, count, fn);
+    alg.run();
+  });
+  spawn(P, [&](std::shared_ptr<gloo::Context> ctx, gloo::rendezvous::Store& store, int r) {
+    std::vector<T*> dev;
+    for (int k = 0; k < nptrs; k++) {
+      T* d = nullptr;
+      if (hipMalloc((void**)&d, sizeof(T) * (size_t)std::max(count, 1)) != hipSuccess) {
+        throw std::runtime_error("hipMalloc");
+      }
+      hipMemcpy(d, in[r][(size_t)k].data(), sizeof(T) * (size_t)count, hipMemcpyHostToDevice);
+      dev.push_back(d);
+    }
+    {
+      Hip<T> alg(ctx, store, dev, count, {}, fn);
+      for (int it = 0; it < 2; it++) {  // repeated runs on one instance
+        for (int k = 0; k < nptrs && it > 0; k++) {
+          hipMemcpy(dev[(size_t)k], in[r][(size_t)k].data(), sizeof(T) * (size_t)count,
+                    hipMemcpyHostToDevice);
+        }
+        alg.run();
+      }
+    }
+    for (int k = 0; k < nptrs; k++) {
+      hipMemcpy(got[r][(size_t)k].data(), dev[(size_t)k], sizeof(T) * (size_t)count,
+                hipMemcpyDeviceToHost);
+      hipFree(dev[(size_t)k]);
+    }
+  });
+  size_t bad = 0;
+  for (int r = 0; r < P; r++) {
+    for (int k = 0; k < nptrs; k++) {
+      bad += std::memcmp(got[r][(size_t)k].data(), ref[r][(size_t)k].data(),
+                         sizeof(T) * (size_t)count) != 0;
+    }
+  }
+  EXPECT(bad == 0, "%s: %zu buffers differ from the reference", name, bad);
+  std::printf("%s P=%d count=%d ptrs=%d: %s\n", name, P, count, nptrs, bad ? "MISMATCH" : "ok");
+}
+
+int gpuMode() {
+  using namespace gloo;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n < 1) {
+    std::printf("binding_test gpu: no GPU\n");
+    return 2;
+  }
+  compare<float, HipAllreduceRingChunked, AllreduceRingChunked>(
+      "ring_chunked<float> sum", 2, 100003, 1, ReductionFunction<float>::sum);
+  compare<float, HipAllreduceRingChunked, AllreduceRingChunked>(
+      "ring_chunked<float> max", 3, 4099, 2, ReductionFunction<float>::max);
+  compare<float16, HipAllreduceHalvingDoubling, AllreduceHalvingDoubling>(
+      "halving_doubling<float16> sum", 4, 65539, 1, ReductionFunction<float16>::sum);
+  compare<int32_t, HipAllreduceHalvingDoubling, AllreduceHalvingDoubling>(
+      "halving_doubling<int32> product", 3, 1000, 1, ReductionFunction<int32_t>::product);
+  std::printf("binding_test gpu: %s\n", failures ? "FAILED" : "OK");
+  return failures ? 1 : 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const std::string mode = argc > 1 ? argv[1] : "cpu";
+  return mode == "gpu" ? gpuMode() : cpuMode();
+}

@@ -439,3 +439,87 @@ def test_auto_schedule_is_ring_chunked(P, N):
     ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=23)
     out = gpu_allreduce(AUTO, O.SUM, O.FLOAT32, ins, runs=2)
     check_all(out, O.allreduce(O.RING_CHUNKED, O.SUM, O.FLOAT32, ins), O.FLOAT32, O.SUM)
+
+
+@pytest.mark.parametrize("algo", [O.RING_CHUNKED, O.HALVING_DOUBLING],
+                         ids=["ring_chunked", "halving_doubling"])
+def test_events_order_a_consumer_stream(algo):
+    """gloo::CudaStream's record/wait (gloo/cuda.h:40-120) through the C ABI:
+    the algorithm runs on a user stream; alg.record(ev) marks the end of its
+    work; a second stream waits for the event on the device and copies the
+    result out, with no host synchronisation in between."""
+    import gloo_amd
+    P, N = 3, 1 << 20
+    ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=23)
+    exp = O.allreduce(algo, O.SUM, O.FLOAT32, ins)
+    store = gloo_amd.rendezvous.HashStore()
+    bufs = [to_dev(ins[r][0], O.FLOAT32) for r in range(P)]
+    outs = [torch.zeros(N, device="cuda") for _ in range(P)]
+    torch.cuda.synchronize()
+    cls = gloo_amd.AllreduceRingChunked if algo == O.RING_CHUNKED \
+        else gloo_amd.AllreduceHalvingDoubling
+
+    def rank_fn(r):
+        ctx = gloo_amd.rendezvous.Context(r, P, 0)
+        ctx.setTimeout(60)
+        ctx.connectFullMesh(store)
+        work, consumer = torch.cuda.Stream(), torch.cuda.Stream()
+        kw = {"schedule": "ring"} if algo == O.RING_CHUNKED else {}
+        alg = cls(ctx, [bufs[r]], streams=[work], **kw)
+        ev = gloo_amd.Event()
+        alg.run()
+        alg.record(ev)
+        ev.wait(consumer)                 # device-side wait, host not blocked
+        with torch.cuda.stream(consumer):
+            outs[r].copy_(bufs[r])
+        ev2 = gloo_amd.Event()
+        ev2.record(consumer)
+        ev2.wait()                        # host waits for the consumer's copy
+        assert ev.query() and ev2.query()
+        alg.close()
+        return True
+
+    run_ranks(P, rank_fn, timeout=90)
+    for r in range(P):
+        assert_same(from_dev(outs[r], O.FLOAT32), exp[r][0], O.FLOAT32, O.SUM)
+
+
+def test_transport_stats_name_the_mechanism():
+    """transport_stats() says how messages moved: thread-ranks sharing one
+    device copy with hipMemcpyAsync (device_copies), the copy kernel counts
+    as kernel_copies, and the bytes match bytes_sent() per run."""
+    import gloo_amd
+    P, N = 2, 1 << 18
+    ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=24)
+    store = gloo_amd.rendezvous.HashStore()
+    bufs = [to_dev(ins[r][0], O.FLOAT32) for r in range(P)]
+    torch.cuda.synchronize()
+    stats = {}
+
+    def rank_fn(r, engine):
+        ctx = gloo_amd.rendezvous.Context(r, P, 0)
+        ctx.setTimeout(60)
+        ctx.connectFullMesh(store)
+        alg = gloo_amd.AllreduceRingChunked(ctx, [bufs[r]], schedule="ring")
+        for _ in range(3):
+            alg.run()
+        stats[(r, engine)] = (alg.transport_stats(), alg.bytes_sent(), alg.engine())
+        alg.close()
+        return True
+
+    # the copy engine is read at construction (process-wide setting)
+    for engine in ("dma", "kernel"):
+        store = gloo_amd.rendezvous.HashStore()
+        gloo_amd.set_copy_engine(engine, 64)
+        try:
+            run_ranks(P, lambda r: rank_fn(r, engine), timeout=90)
+        finally:
+            gloo_amd.set_copy_engine("dma")
+    for r in range(P):
+        st, sent, eng = stats[(r, "dma")]
+        assert eng == "steps"
+        assert st["peer_copies"] == 0 and st["device_copies"] > 0 and st["kernel_copies"] == 0
+        assert st["bytes"] == 3 * sent
+        st, sent, eng = stats[(r, "kernel")]
+        assert st["kernel_copies"] > 0 and st["device_copies"] == 0
+        assert st["bytes"] == 3 * sent

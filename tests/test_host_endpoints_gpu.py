@@ -28,7 +28,7 @@ def make(gloo_amd, algo, ctx, bufs, op):
         ctx, bufs, fn=fn, schedule="mesh" if algo == "ring_chunked_mesh" else "ring")
 
 
-def host_allreduce(algo, op, dtype, inputs, runs=1, pinned=False):
+def host_allreduce(algo, op, dtype, inputs, runs=1, pinned=False, stats=None):
     import gloo_amd
     P = len(inputs)
     store = gloo_amd.rendezvous.HashStore()
@@ -53,6 +53,8 @@ def host_allreduce(algo, op, dtype, inputs, runs=1, pinned=False):
                     else:
                         b[...] = x
             alg.run()
+        if stats is not None:
+            stats[r] = alg.transport_stats()
         alg.close()
         return True
 
@@ -100,3 +102,27 @@ def test_mixed_host_and_device_buffers_are_rejected():
     with pytest.raises(gloo_amd.EnforceNotMet):
         gloo_amd.AllreduceRingChunked(ctx, [np.zeros(64, np.float32),
                                             torch.zeros(64, device="cuda")])
+
+
+@pytest.mark.parametrize("algo", ["ring_chunked", "halving_doubling"])
+@pytest.mark.parametrize("dtype,op", [(O.FLOAT32, O.SUM), (O.FLOAT16, O.SUM),
+                                      (O.FLOAT16, O.MAX), (O.INT8, O.PRODUCT),
+                                      (O.BFLOAT16, O.SUM), (O.UINT64, O.MIN)], ids=str)
+@pytest.mark.parametrize("nptrs", [2, 3])
+def test_on_device_threshold(algo, dtype, op, nptrs):
+    """kOnDeviceThreshold (gloo/algorithm.cc:16): host buffers of several
+    pointers below 256 KiB are folded on the host and staged as one buffer
+    (the reference's cudaHostReduce/cudaHostBroadcast,
+    gloo/cuda_allreduce_halving_doubling.cc:478-484); at and above it the
+    fold runs on the device.  Same bits either way."""
+    es = {O.FLOAT32: 4, O.FLOAT16: 2, O.BFLOAT16: 2, O.INT8: 1, O.UINT64: 8}[dtype]
+    P = 2
+    for nbytes, host in ((64 << 10, True), ((256 << 10) - 16, True), (256 << 10, False),
+                         ((256 << 10) + 4096, False)):
+        N = nbytes // es
+        ins = case_inputs(P, N, dtype, nptrs, 0, seed=9)
+        stats = {}
+        out = host_allreduce(algo, op, dtype, ins, runs=2, stats=stats)
+        check(out, O.allreduce(ALGOS[algo], op, dtype, ins))
+        for r in range(P):
+            assert (stats[r]["host_folds"] == 2) == host, (nbytes, stats[r])
