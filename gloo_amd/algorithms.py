@@ -83,9 +83,11 @@ def _as_ptrs(bufs, dtype, allow_host=True):
             if not b.flags["C_CONTIGUOUS"] or not b.flags["WRITEABLE"]:
                 raise ValueError("host buffers must be contiguous and writeable")
             code = NUMPY_CODES.get(b.dtype.name)
-            if code is None:
+            if dtype is not None and lib.glx_dtype_size(dtype) == b.itemsize:
+                pass  # an explicit dtype reinterprets same-size elements (float16 as uint16 bits)
+            elif code is None:
                 raise TypeError("unsupported dtype %s" % b.dtype)
-            if dtype is None:
+            elif dtype is None:
                 dtype = code
             elif dtype != code:
                 raise TypeError("all buffers must share one dtype")

@@ -151,6 +151,13 @@ class Context {
   SharedBlock acquireShared(size_t bytes, unsigned flags);
   void releaseShared(int64_t id);
   char* importShared(int rank, const SharedRef& ref);
+  // Blocks this context returned to the runtime (over the pool's cap), by
+  // id: published in every algorithm record so that peers close their
+  // mappings of them (the physical memory is freed only when every importer
+  // has closed its handle).
+  std::vector<int64_t> retiredShared();
+  // Close our imports of rank r's blocks `ids` (those it has retired).
+  void dropImported(int r, const std::vector<int64_t>& ids);
   // Imports whose mapping the runtime returned at the base of the exporter's
   // allocation instead of at the exported pointer (the canary was found at
   // baseOff further on), and imports checked in all.
@@ -182,6 +189,7 @@ class Context {
   };
   std::map<std::pair<int, int64_t>, Imported> imported_;
   int64_t ipcBaseFixups_ = 0, ipcImports_ = 0;
+  std::vector<int64_t> retired_;
 };
 
 }  // namespace gloo

@@ -453,8 +453,38 @@ void HipPlanExecutor::publish() {
   putPod<int32_t>(b, engine_);
   putPod<int32_t>(b, (int32_t)ddBlocks_.size());
   for (size_t k = 0; k < ddBlocks_.size(); k++) putRef(b, ddRefs_[k]);
+  const std::vector<int64_t> retired = context_->retiredShared();
+  putPod<int32_t>(b, (int32_t)retired.size());
+  for (int64_t id : retired) putPod<int64_t>(b, id);
   context_->store().set(
       "glx/alg/" + std::to_string(slot_) + "/" + std::to_string(contextRank_), b);
+}
+
+// The retired shared-block ids at the end of an algorithm record (publish).
+std::vector<int64_t> HipPlanExecutor::retiredIn(const std::vector<char>& rec) const {
+  // walk the record's fixed parts to its tail
+  size_t at = 0;
+  getPod<uint32_t>(rec, at);
+  getPod<int64_t>(rec, at);
+  getPod<int32_t>(rec, at);
+  getPod<int64_t>(rec, at);
+  getPod<int32_t>(rec, at);
+  getPod<int32_t>(rec, at);
+  const int32_t nblocks = getPod<int32_t>(rec, at);
+  for (int32_t k = 0; k < nblocks; k++) {
+    getPod<int64_t>(rec, at);
+    getPod<int64_t>(rec, at);
+    getRef(rec, at);
+  }
+  const int32_t nchan = getPod<int32_t>(rec, at);
+  at += (size_t)nchan * 4 * sizeof(int32_t);
+  getPod<int32_t>(rec, at);  // engine
+  const int32_t nb = getPod<int32_t>(rec, at);
+  for (int32_t k = 0; k < nb; k++) getRef(rec, at);
+  const int32_t n = getPod<int32_t>(rec, at);
+  std::vector<int64_t> ids;
+  for (int32_t i = 0; i < n; i++) ids.push_back(getPod<int64_t>(rec, at));
+  return ids;
 }
 
 void HipPlanExecutor::resolvePeers() {
@@ -483,6 +513,9 @@ void HipPlanExecutor::resolvePeers() {
                 rcount, ", dtype ", rdtype, ", op ", rop, ") differs from rank ", contextRank_,
                 "'s (algorithm ", algo_, ", count ", count_, ", dtype ", dtype_, ", op ", op_,
                 "): the ranks created their algorithms in different orders");
+    // the peer's retired blocks sit at the end of its record: close our
+    // mappings of them before mapping anything new
+    if (!pe.sameProcess) context_->dropImported(r, retiredIn(b));
     const int32_t nblocks = getPod<int32_t>(b, at);
     bool needScratch = false;
     for (auto& oc : out_) needScratch = needScratch || oc.peer == r;

@@ -151,6 +151,7 @@ class HipPlanExecutor : public Algorithm {
 
   void publish();
   void resolvePeers();
+  std::vector<int64_t> retiredIn(const std::vector<char>& rec) const;
   int outIndex(int peer, int tag);
   int inIndex(int peer, int tag);
   void pollPending();

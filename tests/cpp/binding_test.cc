@@ -15,7 +15,10 @@
 //                      buffers, compared bit for bit with the reference's
 //                      own CPU AllreduceRingChunked / HalvingDoubling run on
 //                      host copies of the same inputs in the same process.
+#include <execinfo.h>
 #include <hip/hip_runtime_api.h>
+#include <signal.h>
+#include <unistd.h>
 
 #include <cstdio>
 #include <cstring>
@@ -151,12 +154,14 @@ void compare(const char* name, int P, int count, int nptrs, const gloo::Reductio
     ref[r] = in[r];
     got[r] = in[r];
   }
+  std::printf("%s: reference CPU run\n", name);
   spawn(P, [&](std::shared_ptr<gloo::Context> ctx, gloo::rendezvous::Store&, int r) {
     std::vector<T*> ptrs;
     for (auto& v : ref[r]) ptrs.push_back(v.data());
     Ref<T> alg(ctx, ptrs, count, fn);
     alg.run();
   });
+  std::printf("%s: HIP run\n", name);
   spawn(P, [&](std::shared_ptr<gloo::Context> ctx, gloo::rendezvous::Store& store, int r) {
     std::vector<T*> dev;
     for (int k = 0; k < nptrs; k++) {
@@ -215,7 +220,18 @@ int gpuMode() {
 
 }  // namespace
 
+void onFault(int sig) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  dprintf(2, "binding_test: signal %d, backtrace:\n", sig);
+  backtrace_symbols_fd(frames, n, 2);
+  _exit(128 + sig);
+}
+
 int main(int argc, char** argv) {
+  setvbuf(stdout, nullptr, _IONBF, 0);
+  signal(SIGSEGV, onFault);
+  signal(SIGABRT, onFault);
   const std::string mode = argc > 1 ? argv[1] : "cpu";
   return mode == "gpu" ? gpuMode() : cpuMode();
 }

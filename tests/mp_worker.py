@@ -210,6 +210,7 @@ def run_churn(store_dir, rank, size):
                 bad.append((it, sched, eng, n, alg.engine(), r))
         alg.close()
         fds.append(nfd())
+    print("IPC rank %d %s" % (rank, ctx.ipc_stats()), flush=True)
     ctx.close()
     print("fds", fds[:3], "...", fds[-3:])
     if bad:
@@ -328,6 +329,7 @@ def run_devsteps(store_dir, rank, size):
     store.set("done/%d" % rank, b"1")
     for r in range(size):
         store.get("done/%d" % r, timeout_ms=60000)
+    print("IPC rank %d %s" % (rank, ctx.ipc_stats()), flush=True)
     ctx.close()
     if bad:
         print("MISMATCH rank", rank, bad[:10])
@@ -437,6 +439,7 @@ def run_device(store_dir, rank, size, mode):
     store.set("done/%d" % rank, b"1")
     for r in range(size):
         store.get("done/%d" % r, timeout_ms=60000)
+    print("IPC rank %d %s" % (rank, ctx.ipc_stats()), flush=True)
     ctx.close()
     if bad:
         print("MISMATCH rank", rank, bad[:10])
@@ -524,6 +527,7 @@ def run_scale(store_dir, rank, size, group):
     store.set("done/%d" % rank, b"1")
     for r in range(size):
         store.get("done/%d" % r, timeout_ms=120000)
+    print("IPC rank %d %s" % (rank, ctx.ipc_stats()), flush=True)
     ctx.close()
     if bad:
         print("MISMATCH rank", rank, bad[:10])

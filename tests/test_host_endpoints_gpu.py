@@ -18,14 +18,15 @@ ALGOS = {"ring_chunked": O.RING_CHUNKED, "halving_doubling": O.HALVING_DOUBLING,
          "ring_chunked_mesh": O.RING_CHUNKED}
 
 
-def make(gloo_amd, algo, ctx, bufs, op):
+def make(gloo_amd, algo, ctx, bufs, op, dtype=None):
     fn = {O.SUM: gloo_amd.ReductionFunction.sum, O.MAX: gloo_amd.ReductionFunction.max,
           O.MIN: gloo_amd.ReductionFunction.min,
           O.PRODUCT: gloo_amd.ReductionFunction.product}[op]
     if algo == "halving_doubling":
-        return gloo_amd.AllreduceHalvingDoubling(ctx, bufs, fn=fn)
+        return gloo_amd.AllreduceHalvingDoubling(ctx, bufs, fn=fn, dtype=dtype)
     return gloo_amd.AllreduceRingChunked(
-        ctx, bufs, fn=fn, schedule="mesh" if algo == "ring_chunked_mesh" else "ring")
+        ctx, bufs, fn=fn, schedule="mesh" if algo == "ring_chunked_mesh" else "ring",
+        dtype=dtype)
 
 
 def host_allreduce(algo, op, dtype, inputs, runs=1, pinned=False, stats=None):
@@ -44,7 +45,8 @@ def host_allreduce(algo, op, dtype, inputs, runs=1, pinned=False, stats=None):
         ctx = gloo_amd.rendezvous.Context(r, P, 0)
         ctx.setTimeout(60)
         ctx.connectFullMesh(store)
-        alg = make(gloo_amd, algo, ctx, bufs[r], op)
+        alg = make(gloo_amd, algo, ctx, bufs[r], op,
+                   dtype if dtype in (O.FLOAT16, O.BFLOAT16) and not pinned else None)
         for k in range(runs):
             if k > 0:  # the host buffers are the algorithm's: refill in place
                 for b, x in zip(bufs[r], inputs[r]):
