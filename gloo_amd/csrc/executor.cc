@@ -1465,6 +1465,18 @@ void HipPlanExecutor::setupDevSteps() {
   for (size_t k = 0; k < out_.size(); k++) out_[k].creditWord = (uint32_t)(in_.size() + k);
   const size_t rows = std::max<size_t>(1, in_.size() + out_.size());
   ddAlloc(rows * G * glx::kFlagBytes);
+  static const int pollLoad = [] {
+    const char* e = std::getenv("GLOO_AMD_FLAG_POLL");
+    return (e != nullptr && std::strcmp(e, "load") == 0) ? 1 : 0;
+  }();
+  pk_.pollLoad = pollLoad;
+  pk_.trace = nullptr;
+  if (devTrace()) {
+    const size_t n = G * (2 * plan_.steps.size() + 1);
+    GLX_HIP_CHECK(hipHostMalloc((void**)&trace_, n * sizeof(uint64_t), hipHostMallocDefault));
+    std::memset(trace_, 0, n * sizeof(uint64_t));
+    pk_.trace = trace_;
+  }
 }
 
 // After resolvePeers: the step table with every address the kernel needs.
@@ -1639,6 +1651,50 @@ void HipPlanExecutor::traceTwoShot(const glx::TwoShotParams& launched) {
                mx[1], mean[2], mx[2], mean[3], mx[3], mean[4], mx[4], mean[5], mx[5]);
 }
 
+// Diagnostics (GLOO_AMD_DEVTRACE=1): wait for the plan kernel just launched
+// and print, per step, the mean over workgroups of the time spent waiting
+// (credit for a SEND, delivery for a RECV) and working, plus totals.
+void HipPlanExecutor::traceDevSteps(const glx::PlanKernelParams& launched) {
+  GLX_HIP_CHECK(hipStreamSynchronize(compute_));
+  const int G = launched.G, n = launched.nsteps;
+  const size_t row = 2 * (size_t)n + 1;
+  const double us = 1e3 / (double)clockKhz_;
+  static const char* kinds[] = {"SEND", "RECV", "REDUCE", "COPY", "RELEASE", "FOLD"};
+  uint64_t t0 = ~uint64_t(0), t1 = 0;
+  double waitTot[6] = {0}, workTot[6] = {0};
+  std::string lines;
+  for (int i = 0; i < n; i++) {
+    double wsum = 0, ksum = 0, kmax = 0;
+    for (int w = 0; w < G; w++) {
+      const uint64_t* t = trace_ + (size_t)w * row;
+      if (i == 0) t0 = std::min(t0, t[0]);
+      if (i == n - 1) t1 = std::max(t1, t[2 * (size_t)n]);
+      const uint64_t after = t[2 * i + 1] != 0 ? t[2 * i + 1] : t[2 * i];
+      const double wt = (double)(after - t[2 * i]) * us;
+      const double kt = (double)(t[2 * i + 2] - after) * us;
+      wsum += wt / G;
+      ksum += kt / G;
+      kmax = std::max(kmax, kt);
+    }
+    const int k = plan_.steps[(size_t)i].kind;
+    waitTot[k] += wsum;
+    workTot[k] += ksum;
+    char b[160];
+    std::snprintf(b, sizeof(b), "  step %2d %-7s len %9ld  wait %8.1f  work %8.1f (max %8.1f) us\n",
+                  i, kinds[k], (long)plan_.steps[(size_t)i].len, wsum, ksum, kmax);
+    lines += b;
+  }
+  std::fprintf(stderr, "[devtrace r%d plan kernel G=%d, %d steps, run %lu] span %.1f us\n%s",
+               contextRank_, G, n, (unsigned long)launched.run, (double)(t1 - t0) * us,
+               lines.c_str());
+  for (int k = 0; k < 6; k++) {
+    if (waitTot[k] + workTot[k] > 0) {
+      std::fprintf(stderr, "[devtrace r%d]   %-7s wait %9.1f us  work %9.1f us (sums of means)\n",
+                   contextRank_, kinds[k], waitTot[k], workTot[k]);
+    }
+  }
+}
+
 void HipPlanExecutor::runDevice(char* ptr0) {
   if (!resolved_) resolvePeers();
   checkDevice();  // an earlier asynchronous call that timed out
@@ -1679,8 +1735,12 @@ void HipPlanExecutor::runDevice(char* ptr0) {
     p.timeoutTicks = ticks;
     GLX_TRACE("r%d plan kernel run %lu (G=%d, %d steps)", contextRank_, (unsigned long)p.run,
               p.G, p.nsteps);
+    if (p.trace != nullptr) {
+      std::memset(trace_, 0, (size_t)p.G * (2 * (size_t)p.nsteps + 1) * sizeof(uint64_t));
+    }
     GLX_HIP_CHECK(glx::launch_plan_kernel(op_, dtype_, p, compute_));
     transport_.deviceKernels++;
+    if (p.trace != nullptr) traceDevSteps(p);
   } else {
     glx::TwoShotParams p = ts_;
     p.buf = ptr0;

@@ -274,6 +274,7 @@ class HipPlanExecutor : public Algorithm {
   uint64_t* trace_ = nullptr;  // GLOO_AMD_DEVTRACE=1: two-shot phase stamps (pinned host)
   static bool devTrace();
   void traceTwoShot(const glx::TwoShotParams& launched);
+  void traceDevSteps(const glx::PlanKernelParams& launched);
   static int engineFor(const Context& ctx, int algo, int64_t count, int esize);
   char* ddAlloc(size_t bytes);
   void setupDevice();

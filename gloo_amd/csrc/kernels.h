@@ -127,6 +127,11 @@ struct PlanKernelParams {
   uint64_t timeoutTicks;
   int* status;
   int* claim;
+  int pollLoad;                // 1: poll flags with atomic loads (GLOO_AMD_FLAG_POLL=load)
+  // diagnostics (GLOO_AMD_DEVTRACE=1): [G][2 * nsteps + 1] s_memrealtime
+  // stamps per workgroup: step i started (2i), its wait was satisfied
+  // (2i + 1; RECV / SEND only), the kernel ended (2 nsteps)
+  uint64_t* trace;
 };
 hipError_t launch_plan_kernel(int op, int dtype, const PlanKernelParams& p, hipStream_t s);
 

@@ -282,14 +282,22 @@ __device__ __forceinline__ void report_timeout(int* status, int* claim, int code
 
 // Lane 0 waits until word >= epoch (bounded); the whole workgroup learns
 // the outcome.  Returns false after a timeout (reported).
+// pollLoad: poll with a system-scope atomic LOAD (global/flat ... sc0 sc1)
+// instead of the memory-side compare-exchange (kPollLoad in the params;
+// GLOO_AMD_FLAG_POLL=load) -- an experiment knob, see DESIGN.md 5b.
+__device__ __forceinline__ uint64_t poll_flag(const uint64_t* word, bool pollLoad) {
+  if (pollLoad) return __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return get_flag(word);
+}
+
 __device__ __forceinline__ bool wait_flag(const uint64_t* word, uint64_t epoch, int peer,
                                           uint64_t start, uint64_t timeoutTicks, int* status,
                                           int* claim, int* s_ok, bool acquire = true,
-                                          int where = 0) {
+                                          int where = 0, bool pollLoad = false) {
   if (threadIdx.x == 0) {
     int ok = 1;
     uint64_t v;
-    while ((v = get_flag(word)) < epoch) {
+    while ((v = poll_flag(word, pollLoad)) < epoch) {
       if (__builtin_amdgcn_s_memrealtime() - start > timeoutTicks) {
         ok = 0;
         report_timeout(status, claim, 1 + peer + 256 * where, v, epoch);
@@ -457,16 +465,25 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
   const int w = blockIdx.x;
   S* buf = reinterpret_cast<S*>(p.buf);
   const bool aligned = ((uintptr_t)p.buf % 16) == 0;
+  const bool pollLoad = p.pollLoad != 0;
+  // diagnostics (GLOO_AMD_DEVTRACE=1): per workgroup and step, when the step
+  // started and when its wait (if any) was satisfied
+  uint64_t* tr = p.trace != nullptr ? p.trace + (size_t)w * (2 * (size_t)p.nsteps + 1) : nullptr;
+  auto stamp = [&](int k) {
+    if (tr != nullptr && threadIdx.x == 0) tr[k] = __builtin_amdgcn_s_memrealtime();
+  };
   for (int i = 0; i < p.nsteps; i++) {
     const DevStep st = p.steps[i];
     const uint64_t seq = p.run * st.perRun + st.seq;
+    stamp(2 * i);
     switch (st.kind) {
       case 0: {  // SEND, once the receiver has consumed message seq-1 of this slice
         if (seq > 1 && !wait_flag(flag_at(st.credit, w), seq - 1, st.peer,
                                   __builtin_amdgcn_s_memrealtime(), p.timeoutTicks, p.status,
-                                  p.claim, &s_ok, /*acquire=*/false, 1 + i)) {
+                                  p.claim, &s_ok, /*acquire=*/false, 1 + i, pollLoad)) {
           return;
         }
+        stamp(2 * i + 1);
         for (int g = st.seg0; g < st.seg1; g++) {
           size_t a, b;
           if (seg_part(p.segs[g], w, a, b)) {
@@ -478,9 +495,10 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
       }
       case 1:  // RECV
         if (!wait_flag(flag_at(st.flag, w), seq, st.peer, __builtin_amdgcn_s_memrealtime(),
-                       p.timeoutTicks, p.status, p.claim, &s_ok, true, 1 + i)) {
+                       p.timeoutTicks, p.status, p.claim, &s_ok, true, 1 + i, pollLoad)) {
           return;
         }
+        stamp(2 * i + 1);
         break;
       case 2:    // REDUCE: buf = op(buf, region), in place
       case 3:    // COPY:   buf = region
@@ -519,6 +537,7 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
         break;
     }
   }
+  stamp(2 * p.nsteps);
 }
 
 // ---- launch -------------------------------------------------------------------

@@ -27,6 +27,13 @@
 extern "C" {
 #endif
 
+/* libgloo_amd.so exports exactly these entry points: everything else in it
+ * is built with hidden visibility, so it links beside the reference's own
+ * libgloo (whose C++ symbols share the namespace `gloo`) without clashing. */
+#if defined(__GNUC__)
+#pragma GCC visibility push(default)
+#endif
+
 /* ---- codes ------------------------------------------------------------ */
 enum glx_dtype {
   GLX_INT8 = 0,
@@ -396,6 +403,10 @@ int64_t glx_plan_fold_ex(int algo, int rank, int size, int64_t count, int esize,
 int64_t glx_plan_stage(int algo, int rank, int size, int64_t count, int esize,
                        int64_t max_piece, int64_t* h2d, int64_t h2d_cap, int64_t* d2h,
                        int64_t d2h_cap, int64_t* n_d2h);
+
+#if defined(__GNUC__)
+#pragma GCC visibility pop
+#endif
 
 #ifdef __cplusplus
 }  /* extern "C" */

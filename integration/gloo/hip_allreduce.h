@@ -135,16 +135,22 @@ class XgmiContext {
                                          rendezvous::Store& store, int device) {
     static std::mutex m;
     static std::map<const Context*, std::weak_ptr<XgmiContext>> all;
-    std::lock_guard<std::mutex> g(m);
-    auto it = all.find(ctx.get());
-    if (it != all.end()) {
-      if (auto live = it->second.lock()) return live;
+    {
+      std::lock_guard<std::mutex> g(m);
+      auto it = all.find(ctx.get());
+      if (it != all.end()) {
+        if (auto live = it->second.lock()) return live;
+      }
     }
-    // the slot is the same on every rank: gloo contexts hand them out in
-    // algorithm-creation order (gloo/context.cc:49-54)
+    // Connect without the registry lock: connecting waits for the peers,
+    // which may be threads of this process making their own contexts (a gloo
+    // context is used by one thread at a time, so nobody races for this key).
+    // The slot is the same on every rank: gloo contexts hand them out in
+    // algorithm-creation order (gloo/context.cc:49-54).
     const int slot = ctx->nextSlot();
     std::shared_ptr<XgmiContext> x(
         new XgmiContext(ctx, store, device, "gloo_amd/" + std::to_string(slot) + "/"));
+    std::lock_guard<std::mutex> g(m);
     all[ctx.get()] = x;
     return x;
   }

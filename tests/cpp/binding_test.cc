@@ -67,6 +67,14 @@ template <> gloo::float16 value<gloo::float16>(int r, size_t i) {
   return gloo::cpu_float2half_rn(value<float>(r, i));
 }
 
+void spawn(int P, const std::function<void(std::shared_ptr<gloo::Context>,
+                                           gloo::rendezvous::Store&, int)>& fn);
+
+void spawnCpu2(const std::function<void(std::shared_ptr<gloo::Context>,
+                                        gloo::rendezvous::Store&, int)>& fn) {
+  spawn(2, fn);
+}
+
 int cpuMode() {
   using namespace gloo;
   EXPECT(hip::GlxType<float>::value == GLX_FLOAT32, "float");
@@ -113,6 +121,31 @@ int cpuMode() {
   EXPECT(glx_store_get(bridge.handle(), "missing", buf.data(), buf.size(), &len, 30) ==
              GLX_ERR_TIMEOUT,
          "a missing key must time out");
+  // two thread-ranks' gloo contexts get their xGMI contexts through the
+  // shared registry at once (it must not serialise their connects)
+  spawnCpu2([&](std::shared_ptr<gloo::Context> ctx, gloo::rendezvous::Store& st, int) {
+    auto x = hip::XgmiContext::of(ctx, st, -1);
+    EXPECT(x && x->get() != nullptr, "registry");
+    EXPECT(hip::XgmiContext::of(ctx, st, -1) == x, "one xGMI context per gloo context");
+  });
+  // two ranks' xGMI contexts connect through the bridge over one gloo store
+  // (the endpoint exchange needs no GPU)
+  {
+    rendezvous::HashStore shared;
+    std::vector<std::thread> ts;
+    int rcs[2] = {-1, -1};
+    for (int r = 0; r < 2; r++) {
+      ts.emplace_back([&, r] {
+        hip::StoreBridge b(shared, "cx/");
+        glx_context* c = glx_context_create(r, 2, -1);
+        rcs[r] = c ? glx_context_connect_full_mesh(c, b.handle()) : -2;
+        glx_context_destroy(c);
+      });
+    }
+    for (auto& t : ts) t.join();
+    EXPECT(rcs[0] == GLX_OK && rcs[1] == GLX_OK, "connect through the bridge: %d %d (%s)",
+           rcs[0], rcs[1], glx_last_error());
+  }
   std::printf("binding_test cpu: %s\n", failures ? "FAILED" : "OK");
   return failures ? 1 : 0;
 }

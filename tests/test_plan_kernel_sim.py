@@ -226,3 +226,33 @@ def test_plan_kernel_protocol_other_element_sizes(es, name, P, N, G):
     exp = expected(name, P, O.SUM, ins, 2)
     for r in range(P):
         assert same_bits(got[r], exp[r][0]), "rank %d" % r
+
+
+@pytest.mark.parametrize("name", ["ring_chunked", "halving_doubling", "fn_ring", "fn_bcube"])
+@pytest.mark.parametrize("P", [2, 3, 4, 5, 7, 8, 16])
+@pytest.mark.parametrize("N", [1, 4099, 1 << 20, 1 << 26])
+def test_sequence_numbers_agree_across_the_run_boundary(name, P, N):
+    """The plan kernel numbers message k of run j on a channel
+    j * perRun + seq (xgmi_kernels.hip): the sender's SENDs and the
+    receiver's RECVs/RELEASEs of every channel must number alike and have
+    the same perRun on both ends, or a run boundary would desynchronise them
+    (one of round 1's suspects for the P=8 stall, verdict item 1)."""
+    syncs = [gloo_amd.plan_sync(name, r, P, N, 4) for r in range(P)]
+    progs = [gloo_amd.plan(name, r, P, N)[0] for r in range(P)]
+    sent, recvd, released = {}, {}, {}
+    for r in range(P):
+        for st, sy in zip(progs[r], syncs[r]["steps"]):
+            kind, peer, tag = st[0], st[1], st[2]
+            if kind == SEND:
+                sent.setdefault((r, peer, tag), []).append((sy[3], sy[4]))
+            elif kind == RECV:
+                recvd.setdefault((peer, r, tag), []).append((sy[3], sy[4]))
+            elif kind == RELEASE:
+                released.setdefault((peer, r, tag), []).append((sy[3], sy[4]))
+    assert set(sent) == set(recvd) == set(released)
+    for ch in sent:
+        s, rv, rl = sent[ch], recvd[ch], released[ch]
+        per = len(s)
+        assert [q for q, _ in s] == list(range(1, per + 1)), ch
+        assert s == rv == rl, ch
+        assert all(p == per for _, p in s), ch
