@@ -556,6 +556,7 @@ int64_t glx_plan_sync(int algo, int rank, int size, int64_t count, int esize,
     if (info) {
       info[0] = t.slice;
       info[1] = t.safe ? 1 : 0;
+      info[2] = t.slots;
     }
     if (nbounds) *nbounds = (int64_t)t.bounds.size();
     for (int64_t i = 0; i < (int64_t)t.bounds.size() && i < bounds_cap && bounds != nullptr;
@@ -564,12 +565,15 @@ int64_t glx_plan_sync(int algo, int rank, int size, int64_t count, int esize,
     }
     for (int64_t i = 0; i < n && i < cap && steps != nullptr; i++) {
       const glx::StepSync& y = t.steps[(size_t)i];
-      int64_t* o = steps + 5 * i;
+      int64_t* o = steps + 8 * i;
       o[0] = y.chan;
       o[1] = y.seg0;
       o[2] = y.seg1;
       o[3] = (int64_t)y.seq;
       o[4] = (int64_t)y.perRun;
+      o[5] = y.fuse;
+      o[6] = (int64_t)y.rseq;
+      o[7] = (int64_t)y.rperRun;
     }
     return GLX_OK;
   });

@@ -244,12 +244,20 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
         1, std::min(maxSlices(2), ((size_t)maxSeg + minSlice - 1) / minSlice));
     sync_ = glx::syncTable(algo, contextRank_, contextSize_, count_, pp, (int)G);
     pk_.G = (int)G;
+    // GLOO_AMD_FUSE=0: one landing slot per channel and no reduce-and-forward
+    // (the round-1 protocol; every rank must agree, which resolvePeers checks)
+    static const bool fuse = [] {
+      const char* e = std::getenv("GLOO_AMD_FUSE");
+      return !(e != nullptr && e[0] == '0');
+    }();
+    slots_ = fuse ? sync_.slots : 1;
     if (!sync_.safe) engine_ = kEngineSteps;
   }
   if (engine_ == kEngineOneShot || engine_ == kEngineTwoShot) {
     setupDevice();
   } else {
-    allocScratch(engine_ == kEngineDevSteps);  // the plan kernel's peers store into it
+    // the plan kernel's peers store into it: uncached, `slots_` copies
+    allocScratch(engine_ == kEngineDevSteps, engine_ == kEngineDevSteps ? slots_ : 1);
   }
 
   // Channels named by the plan; allocate our counter words.
@@ -451,6 +459,7 @@ void HipPlanExecutor::publish() {
     putPod<int32_t>(b, (int32_t)oc.creditWord);
   }
   putPod<int32_t>(b, engine_);
+  putPod<int32_t>(b, (int32_t)slots_);
   putPod<int32_t>(b, (int32_t)ddBlocks_.size());
   for (size_t k = 0; k < ddBlocks_.size(); k++) putRef(b, ddRefs_[k]);
   const std::vector<int64_t> retired = context_->retiredShared();
@@ -479,6 +488,7 @@ std::vector<int64_t> HipPlanExecutor::retiredIn(const std::vector<char>& rec) co
   const int32_t nchan = getPod<int32_t>(rec, at);
   at += (size_t)nchan * 4 * sizeof(int32_t);
   getPod<int32_t>(rec, at);  // engine
+  getPod<int32_t>(rec, at);  // slots
   const int32_t nb = getPod<int32_t>(rec, at);
   for (int32_t k = 0; k < nb; k++) getRef(rec, at);
   const int32_t n = getPod<int32_t>(rec, at);
@@ -561,6 +571,10 @@ void HipPlanExecutor::resolvePeers() {
     const int32_t peerEngine = getPod<int32_t>(b, at);
     GLX_ENFORCE(peerEngine == engine_, "rank ", r, " runs engine ", peerEngine, ", rank ",
                 contextRank_, " engine ", engine_, " (schedules disagree)");
+    const int32_t peerSlots = getPod<int32_t>(b, at);
+    GLX_ENFORCE(engine_ != kEngineDevSteps || peerSlots == slots_, "rank ", r, " keeps ",
+                peerSlots, " landing slot(s) per channel, rank ", contextRank_, " ", slots_,
+                " (GLOO_AMD_FUSE must be the same on every rank)");
     const int32_t nb = getPod<int32_t>(b, at);
     std::vector<char*> blocks;
     for (int32_t k = 0; k < nb; k++) {
@@ -631,7 +645,21 @@ char* HipPlanExecutor::allocShared(size_t bytes, unsigned flags, SharedRef* ref)
   return b.ptr;
 }
 
-void HipPlanExecutor::allocScratch(bool uncached) {
+// Bytes from one landing slot of a scratch block to the next.
+size_t HipPlanExecutor::slotBytes(const ScratchBlock& b) const {
+  return ((size_t)b.elems * esize_ + 64 + 255) & ~(size_t)255;
+}
+
+const HipPlanExecutor::ScratchBlock& HipPlanExecutor::blockOf(
+    const std::vector<ScratchBlock>& blocks, int64_t boff) const {
+  for (const auto& b : blocks) {
+    if (b.start <= boff && boff < b.start + b.elems) return b;
+  }
+  GLX_ENFORCE(false, "no receive block holds region ", boff);
+  return blocks.front();
+}
+
+void HipPlanExecutor::allocScratch(bool uncached, int slots) {
   if (plan_.scratch_elems <= 0) return;
   // region starts = where messages land
   std::vector<int64_t> starts;
@@ -656,7 +684,7 @@ void HipPlanExecutor::allocScratch(bool uncached) {
   }
   if (cur.elems > 0) blocks_.push_back(cur);
   for (auto& b : blocks_) {
-    const size_t bytes = (size_t)b.elems * esize_ + 64;
+    const size_t bytes = slots > 1 ? (size_t)slots * slotBytes(b) : (size_t)b.elems * esize_ + 64;
     b.ptr = allocShared(bytes, uncached ? hipDeviceMallocUncached : 0u, &b.ref);
     GLX_HIP_CHECK(hipMemset(b.ptr, 0, bytes));
   }
@@ -1500,14 +1528,19 @@ void HipPlanExecutor::buildDevSteps() {
     d.seg1 = y.seg1;
     d.seq = y.seq;
     d.perRun = y.perRun;
+    d.rseq = y.rseq;
+    d.rperRun = y.rperRun;
+    const bool fused = slots_ == 2 && y.fuse >= 0;
     switch (s.kind) {
       case glx::SEND: {
         GLX_ENFORCE(y.chan == stepChan_[i], "plan kernel: channel numbering disagrees");
         const OutChan& oc = out_[(size_t)y.chan];
         d.dst = s.len > 0 ? vbase(landing(peerBlocks_[oc.peer], s.dst_off, s.off), s.off)
                           : nullptr;
+        d.dstSlot = s.len > 0 ? (int64_t)slotBytes(blockOf(peerBlocks_[oc.peer], s.dst_off)) : 0;
         d.flag = oc.devDelivery;
         d.credit = rows + (size_t)oc.creditWord * G * glx::kFlagStride;
+        if (fused) d.kind = glx::kStepNop;  // done inside step y.fuse
         break;
       }
       case glx::RECV:
@@ -1519,9 +1552,24 @@ void HipPlanExecutor::buildDevSteps() {
         break;
       }
       case glx::REDUCE:
-      case glx::COPY:
+      case glx::COPY: {
         d.src = vbase(landing(blocks_, s.boff, s.off), s.off);
+        d.srcSlot = (int64_t)slotBytes(blockOf(blocks_, s.boff));
+        if (fused) {  // and the SEND of the result: its peer, slot, flags, numbers
+          const glx::Step& t = plan_.steps[(size_t)y.fuse];
+          const glx::StepSync& ty = sync_.steps[(size_t)y.fuse];
+          const OutChan& oc = out_[(size_t)ty.chan];
+          d.kind = s.kind == glx::REDUCE ? glx::kStepReduceSend : glx::kStepCopySend;
+          d.peer = (int32_t)t.peer;
+          d.seq = ty.seq;
+          d.perRun = ty.perRun;
+          d.dst = vbase(landing(peerBlocks_[oc.peer], t.dst_off, t.off), t.off);
+          d.dstSlot = (int64_t)slotBytes(blockOf(peerBlocks_[oc.peer], t.dst_off));
+          d.flag = oc.devDelivery;
+          d.credit = rows + (size_t)oc.creditWord * G * glx::kFlagStride;
+        }
         break;
+      }
       case glx::FOLD: {
         const auto& f = plan_.folds[(size_t)s.boff];
         GLX_ENFORCE(f.size() <= (size_t)glx::kOsMaxRanks, "plan kernel: fold of ", f.size(),
@@ -1558,6 +1606,7 @@ void HipPlanExecutor::buildDevSteps() {
   pk_.steps = devSteps_;
   pk_.foldSrc = devFoldSrc_;
   pk_.nsteps = (int)plan_.steps.size();
+  pk_.slots = slots_;
 }
 
 void HipPlanExecutor::checkDevice() {

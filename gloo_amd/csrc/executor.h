@@ -164,7 +164,12 @@ class HipPlanExecutor : public Algorithm {
     return timeout_.count() > 0 ? timeout_ : context_->getTimeout();
   }  // the plan's steps on ptr0 (contextSize_ > 1)
   void localReduce(const std::vector<void*>& in, const std::vector<void*>& out);
-  void allocScratch(bool uncached = false);
+  // Receive scratch blocks; `slots` copies of each (the plan kernel's
+  // landing slots, plan.h SyncTable::slots), slotBytes() apart.
+  void allocScratch(bool uncached = false, int slots = 1);
+  size_t slotBytes(const ScratchBlock& b) const;
+  const ScratchBlock& blockOf(const std::vector<ScratchBlock>& blocks, int64_t boff) const;
+  int slots_ = 1;  // plan kernel: landing slots per channel
   void waitWar(int64_t off, int64_t len);
   // The constructor's work; on a throw the constructor releases whatever it
   // had acquired (the destructor never runs for a half-built object).

@@ -103,19 +103,28 @@ hipError_t launch_twoshot(int op, int dtype, const TwoShotParams& p, hipStream_t
 struct DevSegment {
   int64_t off, len, slice;  // slice: elements per workgroup, whole 16-byte vectors
 };
+// Step kinds of the plan kernel: glx::StepKind (0 SEND, 1 RECV, 2 REDUCE,
+// 3 COPY, 4 RELEASE, 5 FOLD) plus the reduce-and-forward forms (plan.h
+// StepSync::fuse): REDUCE or COPY and the SEND of the same range in one
+// pass, and the SEND they absorbed, which is then skipped.
+constexpr int32_t kStepReduceSend = 6, kStepCopySend = 7, kStepNop = 8;
 struct DevStep {
-  int32_t kind;            // glx::StepKind
+  int32_t kind;            // glx::StepKind or kStep* above
   int32_t peer;            // reported on timeout
   int32_t seg0, seg1;      // the step's element range = segments [seg0, seg1)
   int32_t nsrc;            // FOLD: number of sources, first at foldSrc[srcIndex]
   int32_t left;            // FOLD: 1 = left fold (plan.h kFoldLeft), 0 = the ring's chain
   int64_t srcIndex;
-  const char* src;         // REDUCE / COPY: landing region as a virtual buffer
-  char* dst;               // SEND: the peer's landing region as a virtual buffer
+  const char* src;         // REDUCE / COPY: landing region (slot 0) as a virtual buffer
+  char* dst;               // SEND: the peer's landing region (slot 0) as a virtual buffer
   uint64_t* flag;          // SEND: peer's delivery row; RECV: my delivery row;
                            // RELEASE: peer's credit row
   const uint64_t* credit;  // SEND: my credit row
-  uint64_t seq, perRun;    // message number within a run (1-based), messages per run
+  uint64_t seq, perRun;    // SEND/RECV/RELEASE: message number within a run (1-based),
+                           // messages per run
+  uint64_t rseq, rperRun;  // REDUCE / COPY: the same for the message they read
+  int64_t srcSlot;         // REDUCE / COPY: bytes from one landing slot to the next
+  int64_t dstSlot;         // SEND: the same in the peer's region
 };
 struct PlanKernelParams {
   char* buf;
@@ -123,6 +132,7 @@ struct PlanKernelParams {
   const DevSegment* segs;      // device memory
   const char* const* foldSrc;  // device memory; nullptr = buf
   int nsteps, G;
+  int slots;                   // landing slots per channel (1 or 2, plan.h SyncTable)
   uint64_t run;                // runs completed before this one
   uint64_t timeoutTicks;
   int* status;

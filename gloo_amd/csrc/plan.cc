@@ -901,6 +901,51 @@ SyncTable syncTable(int algo, int rank, int size, int64_t count, const PlanParam
     if (s.kind == SEND) y.perRun = sent[(size_t)y.chan];
     if (s.kind == RECV || s.kind == RELEASE) y.perRun = recvd[(size_t)y.chan];
   }
+  // the message a REDUCE / COPY reads: the latest RECV into its region
+  {
+    std::map<int64_t, size_t> lastRecv;  // region -> step
+    for (size_t i = 0; i < mine.steps.size(); i++) {
+      const Step& s = mine.steps[i];
+      if (s.kind == RECV) lastRecv[s.boff] = i;
+      if ((s.kind == REDUCE || s.kind == COPY) && s.len > 0) {
+        auto it = lastRecv.find(s.boff);
+        if (it == lastRecv.end()) fail("sync table: a step reads a region nothing was received into");
+        t.steps[i].rseq = t.steps[it->second].seq;
+        t.steps[i].rperRun = t.steps[it->second].perRun;
+      }
+    }
+  }
+  // two landing slots per channel when no program folds and every landing
+  // region is fed by one channel (a region shared by channels would need
+  // their slots kept in step)
+  t.slots = 2;
+  for (const Plan& p : all) {
+    std::map<int64_t, std::pair<int64_t, int64_t>> feeder;  // region -> (peer, channel)
+    for (const Step& s : p.steps) {
+      if (s.kind == FOLD) t.slots = 1;
+      if (s.kind != RECV) continue;
+      auto it = feeder.find(s.boff);
+      const std::pair<int64_t, int64_t> ch{s.peer, s.channel};
+      if (it == feeder.end()) {
+        feeder[s.boff] = ch;
+      } else if (it->second != ch) {
+        t.slots = 1;
+      }
+    }
+  }
+  // reduce-and-forward: a REDUCE / COPY followed (past RELEASEs only) by the
+  // SEND of exactly its range (only with two slots: see plan.h)
+  for (size_t i = 0; i < mine.steps.size() && t.slots == 2; i++) {
+    const Step& s = mine.steps[i];
+    if ((s.kind != REDUCE && s.kind != COPY) || s.len <= 0) continue;
+    size_t j = i + 1;
+    while (j < mine.steps.size() && mine.steps[j].kind == RELEASE) j++;
+    if (j < mine.steps.size() && mine.steps[j].kind == SEND && mine.steps[j].off == s.off &&
+        mine.steps[j].len == s.len && t.steps[j].fuse < 0) {
+      t.steps[i].fuse = (int32_t)j;
+      t.steps[j].fuse = (int32_t)i;
+    }
+  }
   return t;
 }
 

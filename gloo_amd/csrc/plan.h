@@ -163,15 +163,41 @@ DeviceLayout twoShotLayout(const Plan& plan, int rank, int size, int64_t count, 
 // byte they both cover to the same workgroup (a workgroup may run several
 // messages ahead of another).  Checked over every region of every rank;
 // when it fails the executor keeps the host-issued steps.
+//
+// fuse: a REDUCE or COPY whose result the program sends on next (the SEND of
+// the same range follows it with only RELEASEs in between -- the ring's
+// "reduce, notify, forward", gloo/allreduce_ring_chunked.h:141-157) names
+// that SEND; the plan kernel does both in one pass (the result goes to the
+// buffer and into the receiver's landing region together, so the link is
+// busy while the chunk is reduced) and waits for the SEND's credit before
+// the pass.  Moving that wait earlier cannot deadlock: the credit is for the
+// previous message on the channel, whose release depends only on older
+// messages.  The SEND itself then names the step it was fused into.
+//
+// slots: landing slots per channel.  The kernel keeps 2 when it can (no FOLD
+// in any rank's program, every landing region fed by one channel): message
+// n of a channel lands in slot (n-1) % 2, so a SEND waits for the release of
+// message n-2 instead of n-1.  That is what makes the fused wait above
+// deadlock-free: with one slot, rank r's fused pass would wait for rank
+// r+1's release of message k, which r+1 gives only after its own fused pass
+// waits for r+2's release of k ... around the ring; with two, each wait is
+// for an older message, down to the first two, which need none.  Fusion is
+// therefore used only with 2 slots.
+//
+// rseq/rperRun: for a REDUCE or COPY, the message number of the RECV whose
+// landing region it reads (its slot).
 struct StepSync {
   int32_t chan = -1;
   int32_t seg0 = 0, seg1 = 0;
   uint64_t seq = 0, perRun = 0;
+  int32_t fuse = -1;  // REDUCE/COPY: the SEND fused into it; SEND: the step it is in
+  uint64_t rseq = 0, rperRun = 0;
 };
 struct SyncTable {
   std::vector<int64_t> bounds;
   int64_t slice = 0;
   bool safe = true;
+  int slots = 1;
   std::vector<std::pair<int, int>> outChans, inChans;  // (peer, tag)
   std::vector<StepSync> steps;
 };

@@ -472,22 +472,47 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
   auto stamp = [&](int k) {
     if (tr != nullptr && threadIdx.x == 0) tr[k] = __builtin_amdgcn_s_memrealtime();
   };
+  // message m of a channel lands in slot (m - 1) % slots
+  auto slotOf = [&](uint64_t m) -> uint64_t { return p.slots == 2 ? ((m - 1) & 1) : 0; };
   for (int i = 0; i < p.nsteps; i++) {
     const DevStep st = p.steps[i];
     const uint64_t seq = p.run * st.perRun + st.seq;
     stamp(2 * i);
     switch (st.kind) {
-      case 0: {  // SEND, once the receiver has consumed message seq-1 of this slice
-        if (seq > 1 && !wait_flag(flag_at(st.credit, w), seq - 1, st.peer,
-                                  __builtin_amdgcn_s_memrealtime(), p.timeoutTicks, p.status,
-                                  p.claim, &s_ok, /*acquire=*/false, 1 + i, pollLoad)) {
+      case 0:                  // SEND, once the receiver has consumed message seq-slots
+      case kStepReduceSend:    // REDUCE + SEND of its result in one pass
+      case kStepCopySend: {    // COPY + SEND of its result in one pass
+        if (seq > (uint64_t)p.slots &&
+            !wait_flag(flag_at(st.credit, w), seq - p.slots, st.peer,
+                       __builtin_amdgcn_s_memrealtime(), p.timeoutTicks, p.status, p.claim,
+                       &s_ok, /*acquire=*/false, 1 + i, pollLoad)) {
           return;
         }
         stamp(2 * i + 1);
-        for (int g = st.seg0; g < st.seg1; g++) {
-          size_t a, b;
-          if (seg_part(p.segs[g], w, a, b)) {
-            copy_span<S>(reinterpret_cast<S*>(st.dst), buf, a, b, aligned);
+        char* dst = st.dst + slotOf(seq) * (uint64_t)st.dstSlot;
+        if (st.kind == 0) {
+          for (int g = st.seg0; g < st.seg1; g++) {
+            size_t a, b;
+            if (seg_part(p.segs[g], w, a, b)) {
+              copy_span<S>(reinterpret_cast<S*>(dst), buf, a, b, aligned);
+            }
+          }
+        } else {
+          const S* src = reinterpret_cast<const S*>(
+              st.src + slotOf(p.run * st.rperRun + st.rseq) * (uint64_t)st.srcSlot);
+          char* outs[2] = {reinterpret_cast<char*>(buf), dst};
+          const S* srcs[kOsMaxRanks];
+#pragma unroll
+          for (int k = 0; k < kOsMaxRanks; k++) srcs[k] = buf;
+          srcs[1] = src;
+          for (int g = st.seg0; g < st.seg1; g++) {
+            size_t a, b;
+            if (!seg_part(p.segs[g], w, a, b)) continue;
+            if (st.kind == kStepCopySend) {
+              scatter_span<S>(outs, 2, src, a, b, aligned);
+            } else {
+              fold_span<T, OP, true>(buf, srcs, 2, outs + 1, 1, a, b, aligned);
+            }
           }
         }
         signal_flag(flag_at(st.flag, w), seq);
@@ -514,7 +539,8 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
             if (q != nullptr) srcs[k] = reinterpret_cast<const S*>(q);
           }
         } else {
-          srcs[1] = reinterpret_cast<const S*>(st.src);
+          srcs[1] = reinterpret_cast<const S*>(
+              st.src + slotOf(p.run * st.rperRun + st.rseq) * (uint64_t)st.srcSlot);
         }
         for (int g = st.seg0; g < st.seg1; g++) {
           size_t a, b;
@@ -533,7 +559,7 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
         __syncthreads();
         if (threadIdx.x == 0) put_flag(flag_at(st.flag, w), seq);
         break;
-      default:
+      default:  // kStepNop: a SEND done inside the step it was fused into
         break;
     }
   }
@@ -654,7 +680,8 @@ hipError_t launch_oneshot(int op, int dtype, const OneShotParams& p, hipStream_t
 
 hipError_t launch_plan_kernel(int op, int dtype, const PlanKernelParams& p, hipStream_t s) {
   if (p.G < 1 || p.G > kOsMaxSlices || p.nsteps < 0 || p.steps == nullptr ||
-      p.segs == nullptr || p.foldSrc == nullptr || p.status == nullptr || p.claim == nullptr) {
+      p.segs == nullptr || p.foldSrc == nullptr || p.status == nullptr || p.claim == nullptr ||
+      (p.slots != 1 && p.slots != 2)) {
     return hipErrorInvalidValue;
   }
   switch (dtype) {

@@ -27,7 +27,7 @@ class Clobber(Exception):
     pass
 
 
-def simulate(name, P, N, G, op, ins, runs=2, es=4):
+def simulate(name, P, N, G, op, ins, runs=2, es=4, fuse=True):
     """es: the element size the programs and bookkeeping are compiled for
     (chunk phases and the 16-byte landing rule depend on it); the values
     themselves are simulated as float32."""
@@ -35,7 +35,9 @@ def simulate(name, P, N, G, op, ins, runs=2, es=4):
     progs = [gloo_amd.plan(name, r, P, N, with_folds=True, esize=es) for r in range(P)]
     syncs = [gloo_amd.plan_sync(name, r, P, N, G, esize=es) for r in range(P)]
     bounds, sl = syncs[0]["bounds"], syncs[0]["slice"]
-    assert all(s["bounds"] == bounds and s["slice"] == sl for s in syncs)
+    K = syncs[0]["slots"] if fuse else 1  # landing slots per channel
+    assert all(s["bounds"] == bounds and s["slice"] == sl and s["slots"] == syncs[0]["slots"]
+               for s in syncs)
     assert bounds[0] == 0 and bounds[-1] == N and bounds == sorted(set(bounds))
     assert sl % V == 0 and G * sl >= max(b - a for a, b in zip(bounds, bounds[1:]))
 
@@ -62,9 +64,10 @@ def simulate(name, P, N, G, op, ins, runs=2, es=4):
     bufs = [np.array(ins[r][0], copy=True) for r in range(P)]
     # landing regions in element units; element x of a message for
     # ptr0[a...] at region + (a mod V) + (x - a), as the 16-byte landing rule
+    # (with K slots, message n of a channel lands in slot (n-1) % K)
     size = [progs[r][1] + N + 64 for r in range(P)]
-    scratch = [np.zeros(size[r], dtype=np.float32) for r in range(P)]
-    pending = [np.zeros(size[r], dtype=bool) for r in range(P)]  # written, not yet read
+    scratch = [[np.zeros(size[r], dtype=np.float32) for _ in range(K)] for r in range(P)]
+    pending = [[np.zeros(size[r], dtype=bool) for _ in range(K)] for r in range(P)]
     delivery = [[[0] * G for _ in in_ch[r]] for r in range(P)]
     credit = [[[0] * G for _ in out_ch[r]] for r in range(P)]
     pc = [[0] * G for _ in range(P)]
@@ -73,10 +76,10 @@ def simulate(name, P, N, G, op, ins, runs=2, es=4):
     def pos(base, a, x):
         return base + a % V + (x - a)
 
-    def read(r, base, a, lo, hi):
+    def read(r, base, a, lo, hi, slot=0):
         i, j = pos(base, a, lo), pos(base, a, hi)
-        pending[r][i:j] = False
-        return np.array(scratch[r][i:j])
+        pending[r][slot][i:j] = False
+        return np.array(scratch[r][slot][i:j])
 
     def step(r, w):
         """Advance (r, w) by one step; False if it is blocked or finished."""
@@ -92,27 +95,51 @@ def simulate(name, P, N, G, op, ins, runs=2, es=4):
             return False
         i = pc[r][w]
         kind, peer, tag, off, ln, boff, dst_off, flags = steps[i]
-        chan, s0, s1, seq, per = syncs[r]["steps"][i]
+        chan, s0, s1, seq, per, fz, rseq, rper = syncs[r]["steps"][i]
         s = run[r][w] * per + seq
-        if kind == SEND:
-            if credit[r][chan][w] < s - 1:
+        rslot = (run[r][w] * rper + rseq - 1) % K if kind in (REDUCE, COPY) else 0
+
+        def send(j):
+            """SEND step j's stores and delivery (its credit already held)."""
+            _, peer_, tag_, off_, _, _, dst_off_, _ = steps[j]
+            _, s0_, s1_, seq_, per_ = syncs[r]["steps"][j][:5]
+            m = run[r][w] * per_ + seq_
+            slot = (m - 1) % K
+            for a, b in parts(s0_, s1_, w):
+                p0, p1 = pos(dst_off_, off_, a), pos(dst_off_, off_, b)
+                if pending[peer_][slot][p0:p1].any():
+                    raise Clobber("rank %d wg %d overwrote unread data of rank %d" % (r, w, peer_))
+                scratch[peer_][slot][p0:p1] = bufs[r][a:b]
+                pending[peer_][slot][p0:p1] = True
+            delivery[peer_][in_ch[peer_][(r, tag_)]][w] = m
+
+        def credit_ok(j):
+            chan_, _, _, seq_, per_ = syncs[r]["steps"][j][:5]
+            return credit[r][chan_][w] >= run[r][w] * per_ + seq_ - K
+
+        fused = fuse and fz >= 0
+        if kind == SEND and fused:
+            pass  # done inside the REDUCE/COPY it was fused into
+        elif kind == SEND:
+            if not credit_ok(i):
                 return False
-            for a, b in parts(s0, s1, w):
-                p0, p1 = pos(dst_off, off, a), pos(dst_off, off, b)
-                if pending[peer][p0:p1].any():
-                    raise Clobber("rank %d wg %d overwrote unread data of rank %d" % (r, w, peer))
-                scratch[peer][p0:p1] = bufs[r][a:b]
-                pending[peer][p0:p1] = True
-            delivery[peer][in_ch[peer][(r, tag)]][w] = s
+            send(i)
+        elif kind in (REDUCE, COPY) and fused and not credit_ok(fz):
+            return False  # the fused pass waits for the SEND's credit first
         elif kind == RECV:
             if delivery[r][chan][w] < s:
                 return False
-        elif kind == REDUCE:
+        if kind == REDUCE:
             for a, b in parts(s0, s1, w):
-                bufs[r][a:b] = O.reduce(op, O.FLOAT32, bufs[r][a:b], read(r, boff, off, a, b))
+                bufs[r][a:b] = O.reduce(op, O.FLOAT32, bufs[r][a:b],
+                                        read(r, boff, off, a, b, rslot))
+            if fused:
+                send(fz)
         elif kind == COPY:
             for a, b in parts(s0, s1, w):
-                bufs[r][a:b] = read(r, boff, off, a, b)
+                bufs[r][a:b] = read(r, boff, off, a, b, rslot)
+            if fused:
+                send(fz)
         elif kind == FOLD:
             for a, b in parts(s0, s1, w):
                 vals = []
@@ -165,11 +192,15 @@ NAMES = ["ring_chunked", "halving_doubling", "fn_ring", "fn_bcube", "ring_chunke
 @pytest.mark.parametrize("P", [2, 3, 5, 8])
 @pytest.mark.parametrize("N", [1, 1024, 999, 4099])
 @pytest.mark.parametrize("G", [1, 4])
-def test_plan_kernel_protocol_matches_oracle(name, P, N, G):
+@pytest.mark.parametrize("fuse", [True, False], ids=["fused", "unfused"])
+def test_plan_kernel_protocol_matches_oracle(name, P, N, G, fuse):
+    """fused: REDUCE/COPY + the SEND of the same range in one pass, the
+    SEND's credit awaited first (the kernel's default); unfused: the step
+    program as written (GLOO_AMD_FUSE=0)."""
     if not all(gloo_amd.plan_sync(name, r, P, N, G)["safe"] for r in range(P)):
         pytest.skip("the executor keeps host-issued steps for this program")
     ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=91)
-    got = simulate(name, P, N, G, O.SUM, ins)
+    got = simulate(name, P, N, G, O.SUM, ins, fuse=fuse)
     exp = expected(name, P, O.SUM, ins, 2)
     for r in range(P):
         assert same_bits(got[r], exp[r][0]), "rank %d" % r
@@ -207,8 +238,10 @@ def test_unsafe_program_is_detected_and_would_clobber():
     P, N, G = 2, 10003, 4
     assert not all(gloo_amd.plan_sync("ring_chunked", r, P, N, G)["safe"] for r in range(P))
     ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=93)
+    # one landing slot per channel (the unfused protocol): with two the
+    # interleaving that clobbers here needs more drift than this schedule has
     with pytest.raises(Clobber):
-        simulate("ring_chunked", P, N, G, O.SUM, ins)
+        simulate("ring_chunked", P, N, G, O.SUM, ins, fuse=False)
 
 
 @pytest.mark.parametrize("es", [2, 8])
@@ -256,3 +289,22 @@ def test_sequence_numbers_agree_across_the_run_boundary(name, P, N):
         assert [q for q, _ in s] == list(range(1, per + 1)), ch
         assert s == rv == rl, ch
         assert all(p == per for _, p in s), ch
+
+
+@pytest.mark.parametrize("name,P,N", [("ring_chunked", 8, 1 << 26), ("ring_chunked", 2, 1024),
+                                      ("fn_ring", 4, 1 << 20)])
+def test_ring_forwards_every_reduced_and_copied_chunk(name, P, N):
+    """The ring's reduce-and-forward: every SEND after the prelude is fused
+    into the REDUCE (reduce-scatter) or COPY (allgather) of its chunk, so the
+    link is fed while the chunk is reduced; at P=8, 256 MiB: 26 of 28."""
+    steps = gloo_amd.plan(name, 0, P, N)[0]
+    sy = gloo_amd.plan_sync(name, 0, P, N, 4)["steps"]
+    sends = [i for i, st in enumerate(steps) if st[0] == SEND and st[4] > 0]
+    fused = [i for i in sends if sy[i][5] >= 0]
+    for i in fused:
+        j = sy[i][5]
+        assert steps[j][0] in (REDUCE, COPY) and sy[j][5] == i
+        assert (steps[j][3], steps[j][4]) == (steps[i][3], steps[i][4])
+        assert all(steps[k][0] == RELEASE for k in range(j + 1, i))
+    if name == "ring_chunked":
+        assert len(sends) == 4 * P - 4 and len(fused) == 4 * P - 6  # all but the prelude
