@@ -64,6 +64,9 @@ SIGNATURES = [
     ("glx_allreduce_create", _vp,
      [_vp, _i, ctypes.POINTER(_vp), _i, _i, _i, _i, ctypes.POINTER(_vp), _i]),
     ("glx_algorithm_run", _i, [_vp]),
+    ("glx_algorithm_run_fed", _i, [_vp]),
+    ("glx_algorithm_feed", _i, [_vp, _i64, _i64]),
+    ("glx_algorithm_done_ranges", _i64, [_vp, ctypes.POINTER(_i64), _i64]),
     ("glx_algorithm_bytes_sent", _i64, [_vp]),
     ("glx_algorithm_engine", _i, [_vp]),
     ("glx_algorithm_destroy", None, [_vp]),

@@ -167,6 +167,29 @@ class Algorithm:
     def run(self):
         check(lib.glx_algorithm_run(self._h), type(self).__name__ + ".run")
 
+    def run_fed(self):
+        """run() on a host buffer that is still being filled (by a transport
+        thread calling feed()): each H2D piece goes as soon as it is fed,
+        each step waits only for its own range (gloo/transport/tcp/pair.cc:
+        385-451 receives into the buffer; here the schedule starts on the
+        first bytes).  Blocks until the result is back in host memory."""
+        check(lib.glx_algorithm_run_fed(self._h), type(self).__name__ + ".run_fed")
+
+    def feed(self, off, n):
+        """Elements [off, off+n) of the host buffer hold their data now (any
+        thread; before run_fed() they count for the next run)."""
+        check(lib.glx_algorithm_feed(self._h, int(off), int(n)), "feed")
+
+    def done_ranges(self):
+        """[(off, n)] element ranges whose results are already in host memory,
+        in completion order."""
+        k = lib.glx_algorithm_done_ranges(self._h, None, 0)
+        if k < 0:
+            check(_lib.ERR_INVALID, "done_ranges")
+        buf = (ctypes.c_int64 * max(2 * k, 1))()
+        k = lib.glx_algorithm_done_ranges(self._h, buf, k)
+        return [(buf[2 * i], buf[2 * i + 1]) for i in range(k)]
+
     def bytes_sent(self):
         """Bytes this rank moves over peer links per run()."""
         return lib.glx_algorithm_bytes_sent(self._h)

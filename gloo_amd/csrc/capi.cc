@@ -394,6 +394,37 @@ int glx_algorithm_run(glx_algorithm* alg) {
   });
 }
 
+int glx_algorithm_run_fed(glx_algorithm* alg) {
+  return guarded([&]() -> int {
+    GLX_ENFORCE(alg != nullptr, "null algorithm");
+    alg->a->runFed();
+    return GLX_OK;
+  });
+}
+
+int glx_algorithm_feed(glx_algorithm* alg, int64_t off, int64_t len) {
+  return guarded([&]() -> int {
+    GLX_ENFORCE(alg != nullptr, "null algorithm");
+    alg->a->feed(off, len);
+    return GLX_OK;
+  });
+}
+
+int64_t glx_algorithm_done_ranges(glx_algorithm* alg, int64_t* out, int64_t cap) {
+  int64_t n = -1;
+  guarded([&]() -> int {
+    GLX_ENFORCE(alg != nullptr, "null algorithm");
+    const std::vector<glx::Range> r = alg->a->doneRanges();
+    n = (int64_t)r.size();
+    for (int64_t i = 0; i < n && i < cap && out != nullptr; i++) {
+      out[2 * i] = r[(size_t)i].off;
+      out[2 * i + 1] = r[(size_t)i].len;
+    }
+    return GLX_OK;
+  });
+  return n;
+}
+
 int64_t glx_algorithm_bytes_sent(glx_algorithm* alg) {
   return alg ? alg->a->bytesSentPerRun() : -1;
 }

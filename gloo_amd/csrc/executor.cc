@@ -385,6 +385,9 @@ void HipPlanExecutor::release() noexcept {
     if (e != nullptr) hipEventDestroy(e);
   }
   if (hostDone_) hipEventDestroy(hostDone_);
+  for (auto& e : doneEvents_) {
+    if (e != nullptr) hipEventDestroy(e);
+  }
   for (char* d : devBufs_) hipFree(d);
   if (hostStage_) hipHostFree(hostStage_);
   for (char* d : fnStage_) hipFree(d);
@@ -982,6 +985,30 @@ void HipPlanExecutor::setupHostMode() {
 // Make `s` wait for the H2D pieces overlapping [off, off+len).  h2d_ is one
 // in-order stream, so waiting for the latest such piece covers the others.
 void HipPlanExecutor::waitH2D(hipStream_t s, int& waited, int64_t off, int64_t len) {
+  if (fedRun_) {
+    // pieces are issued as they are fed, in any order: wait (bounded) until
+    // every piece of the range has been issued, then for each one's copy
+    std::vector<size_t> need;
+    for (size_t j = 0; j < stage_.h2d.size(); j++) {
+      const glx::Range& r = stage_.h2d[j];
+      if (r.off < off + len && off < r.off + r.len) need.push_back(j);
+    }
+    std::unique_lock<std::mutex> lk(feedMutex_);
+    const auto deadline = std::chrono::steady_clock::now() + effectiveTimeout();
+    for (size_t j : need) {
+      while (!pieceIssued_[j]) {
+        if (feedCv_.wait_until(lk, deadline) == std::cv_status::timeout && !pieceIssued_[j]) {
+          broken_ = true;
+          GLX_THROW_TIMEOUT("Timed out waiting for host data: elements [", stage_.h2d[j].off,
+                            ", ", stage_.h2d[j].off + stage_.h2d[j].len,
+                            ") were never fed (rank ", contextRank_, ", timeout ",
+                            effectiveTimeout().count(), " ms)");
+        }
+      }
+      GLX_HIP_CHECK(hipStreamWaitEvent(s, h2dEvents_[j], 0));
+    }
+    return;
+  }
   int last = -1;
   for (size_t j = 0; j < stage_.h2d.size(); j++) {
     const glx::Range& r = stage_.h2d[j];
@@ -1010,6 +1037,124 @@ void HipPlanExecutor::copyBack(const std::vector<glx::Range>& ranges) {
                                    hipMemcpyDeviceToHost, d2h_));
     }
   }
+  if (ranges.empty() || hostFold_) return;  // host-folded results return at the end
+  // completion marker for doneRanges()
+  std::lock_guard<std::mutex> g(doneMutex_);
+  if (doneUsed_ == doneEvents_.size()) {
+    hipEvent_t e = nullptr;
+    GLX_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    doneEvents_.push_back(e);
+  }
+  hipEvent_t e = doneEvents_[doneUsed_++];
+  GLX_HIP_CHECK(hipEventRecord(e, d2h_));
+  doneQueue_.push_back(DoneBatch{e, ranges});
+}
+
+std::vector<glx::Range> HipPlanExecutor::doneRanges() {
+  std::lock_guard<std::mutex> g(doneMutex_);
+  std::vector<glx::Range> out;
+  for (const auto& b : doneQueue_) {
+    const hipError_t e = hipEventQuery(b.ev);
+    if (e == hipErrorNotReady) {
+      (void)hipGetLastError();
+      continue;
+    }
+    GLX_HIP_CHECK(e);
+    out.insert(out.end(), b.ranges.begin(), b.ranges.end());
+  }
+  return out;
+}
+
+// Issue piece j's H2D copy (the caller holds feedMutex_ or runs alone).
+void HipPlanExecutor::issuePiece(size_t j) {
+  const glx::Range& r = stage_.h2d[j];
+  const size_t at = (size_t)r.off * esize_, n = (size_t)r.len * esize_;
+  const std::vector<void*> hsrc = hostSources();
+  for (size_t k = 0; k < hsrc.size(); k++) {
+    GLX_HIP_CHECK(hipMemcpyAsync(devBufs_[k] + at, static_cast<const char*>(hsrc[k]) + at, n,
+                                 hipMemcpyHostToDevice, h2d_));
+  }
+  GLX_HIP_CHECK(hipEventRecord(h2dEvents_[j], h2d_));
+  pieceIssued_[j] = 1;
+}
+
+// Issue every piece the feeds now cover (feedMutex_ held, a fed run active).
+void HipPlanExecutor::issueFedPiecesLocked() {
+  for (size_t j = 0; j < stage_.h2d.size(); j++) {
+    if (pieceIssued_[j]) continue;
+    const glx::Range& r = stage_.h2d[j];
+    bool covered = false;
+    for (const glx::Range& f : fed_) {
+      if (f.off <= r.off && r.off + r.len <= f.off + f.len) covered = true;
+    }
+    if (covered) issuePiece(j);
+  }
+  feedCv_.notify_all();
+}
+
+void HipPlanExecutor::feed(int64_t off, int64_t len) {
+  GLX_ENFORCE(hostMode_, "feed() needs an algorithm on host-memory buffers");
+  GLX_ENFORCE(off >= 0 && len >= 0 && off + len <= count_, "feed range [", off, ", ",
+              off + len, ") outside the buffer of ", count_, " elements");
+  if (len == 0) return;
+  GLX_HIP_CHECK(hipSetDevice(device_));  // this may be the transport's thread
+  std::lock_guard<std::mutex> g(feedMutex_);
+  // merge into the fed set
+  int64_t lo = off, hi = off + len;
+  std::vector<glx::Range> merged;
+  for (const glx::Range& f : fed_) {
+    if (f.off + f.len < lo || f.off > hi) {
+      merged.push_back(f);
+    } else {
+      lo = std::min(lo, f.off);
+      hi = std::max(hi, f.off + f.len);
+    }
+  }
+  merged.push_back({lo, hi - lo});
+  fed_.swap(merged);
+  if (fedRun_) issueFedPiecesLocked();
+}
+
+void HipPlanExecutor::runFed() {
+  GLX_ENFORCE(hostMode_, "runFed() needs an algorithm on host-memory buffers");
+  GLX_ENFORCE(ptrs_.size() == 1, "runFed() takes one host buffer (the transport's)");
+  GLX_HIP_CHECK(hipSetDevice(device_));
+  {
+    std::lock_guard<std::mutex> g(doneMutex_);
+    doneQueue_.clear();
+    doneUsed_ = 0;
+  }
+  {
+    std::lock_guard<std::mutex> g(feedMutex_);
+    fedRun_ = true;
+    pieceIssued_.assign(stage_.h2d.size(), 0);
+    issueFedPiecesLocked();  // what arrived before the run
+  }
+  struct End {
+    HipPlanExecutor* e;
+    ~End() {
+      std::lock_guard<std::mutex> g(e->feedMutex_);
+      e->fedRun_ = false;
+      e->fed_.clear();
+    }
+  } end{this};
+  if (contextSize_ == 1) {
+    // nothing to exchange: the result is the input once it has all arrived
+    waitH2D(compute_, computeH2dWaited_, 0, count_);
+    GLX_HIP_CHECK(hipStreamSynchronize(h2d_));
+    copyBack({});
+    std::lock_guard<std::mutex> g(doneMutex_);
+    if (doneEvents_.empty()) {
+      hipEvent_t e = nullptr;
+      GLX_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      doneEvents_.push_back(e);
+    }
+    GLX_HIP_CHECK(hipEventRecord(doneEvents_[0], h2d_));
+    doneQueue_.push_back(DoneBatch{doneEvents_[0], {glx::Range{0, count_}}});
+    doneUsed_ = 1;
+    return;
+  }
+  runHost();
 }
 
 void HipPlanExecutor::runHost() {
@@ -1027,14 +1172,14 @@ void HipPlanExecutor::runHost() {
   const std::vector<void*> hsrc = hostSources();
   computeH2dWaited_ = -1;
   for (auto& c : copies_) c.h2dWaited = -1;
-  for (size_t j = 0; j < stage_.h2d.size(); j++) {
-    const glx::Range& r = stage_.h2d[j];
-    const size_t at = (size_t)r.off * esize_, n = (size_t)r.len * esize_;
-    for (size_t k = 0; k < hsrc.size(); k++) {
-      GLX_HIP_CHECK(hipMemcpyAsync(devBufs_[k] + at, static_cast<const char*>(hsrc[k]) + at, n,
-                                   hipMemcpyHostToDevice, h2d_));
+  if (!fedRun_) {
+    {
+      std::lock_guard<std::mutex> g(doneMutex_);
+      doneQueue_.clear();
+      doneUsed_ = 0;
     }
-    GLX_HIP_CHECK(hipEventRecord(h2dEvents_[j], h2d_));
+    pieceIssued_.assign(stage_.h2d.size(), 0);
+    for (size_t j = 0; j < stage_.h2d.size(); j++) issuePiece(j);
   }
   if (hsrc.size() > 1) {  // local fold needs every buffer whole
     waitH2D(compute_, computeH2dWaited_, 0, count_);

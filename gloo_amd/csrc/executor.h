@@ -17,6 +17,8 @@
 #include <hip/hip_runtime_api.h>
 
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -52,6 +54,20 @@ class HipPlanExecutor : public Algorithm {
   // Class-style run (gloo/allreduce_ring_chunked.h:83-212): fold ptrs into
   // ptrs[0], run the schedule on it, copy it to the other pointers.
   void run() override;
+
+  // Host-memory endpoint fed from a transport (the reference
+  // receives socket bytes into a registered host buffer,
+  // gloo/transport/tcp/pair.cc:385-451): runFed() is run() on a host buffer
+  // whose bytes are NOT all there yet -- each H2D piece is issued when
+  // feed() has covered it, and every step waits only for the pieces of its
+  // own range, so the schedule starts on the first bytes to arrive.  feed()
+  // may be called from another thread, before or during runFed() (feeds
+  // count for the next runFed).  doneRanges() lists the element ranges whose
+  // final values are back in host memory (in completion order; the ring
+  // returns chunk after chunk), for a caller streaming results out.
+  void runFed();
+  void feed(int64_t off, int64_t len);
+  std::vector<glx::Range> doneRanges();
 
   // Function-style run (gloo/allreduce.cc:97-146) on buffers given per call:
   // inputs reduced into out[0] (genLocalReduceFunction, :44-82), the schedule
@@ -226,6 +242,23 @@ class HipPlanExecutor : public Algorithm {
   void waitH2D(hipStream_t s, int& waited, int64_t off, int64_t len);
   void copyBack(const std::vector<glx::Range>& ranges);
   void runHost();
+  // fed runs (runFed / feed): feeds of the current run, merged; which H2D
+  // pieces have been issued; completed copy-backs (event, ranges)
+  std::mutex feedMutex_;
+  std::condition_variable feedCv_;
+  bool fedRun_ = false;
+  std::vector<glx::Range> fed_;
+  std::vector<uint8_t> pieceIssued_;
+  void issueFedPiecesLocked();
+  void issuePiece(size_t j);
+  std::mutex doneMutex_;
+  struct DoneBatch {
+    hipEvent_t ev;
+    std::vector<glx::Range> ranges;
+  };
+  std::vector<DoneBatch> doneQueue_;
+  std::vector<hipEvent_t> doneEvents_;  // pool
+  size_t doneUsed_ = 0;
   std::vector<char*> fnStage_;  // device staging of function-style host buffers
   void runFnHost(const FnCall& call);
   std::vector<OutChan> out_;

@@ -295,6 +295,29 @@ int glx_allreduce(glx_context* ctx, int algorithm, int dtype, int op,
 
 /* Algorithm::run() (gloo/algorithm.h:26). */
 int glx_algorithm_run(glx_algorithm* alg);
+
+/* Host-memory endpoint fed from a transport.  The reference receives socket
+ * bytes into a registered host buffer (gloo/transport/tcp/pair.cc:385-451)
+ * and reduces once a message is whole; here the algorithm (created on ONE
+ * host buffer) is run while that buffer is still filling:
+ *   glx_algorithm_run_fed  -- run() whose H2D copies wait for feeds: each
+ *                             8 MiB piece is copied as soon as feeds cover
+ *                             it, every step waits only for the pieces of
+ *                             its own range.  Blocks until the result is
+ *                             back in host memory; GLX_ERR_TIMEOUT if some
+ *                             piece is never fed within the timeout.
+ *   glx_algorithm_feed     -- elements [off, off+len) of the buffer hold
+ *                             their data now.  Any thread, before (counts
+ *                             for the next run) or during run_fed.
+ *   glx_algorithm_done_ranges -- element ranges {off, len} whose results are
+ *                             in host memory already, in completion order
+ *                             (the ring returns chunk after chunk), for a
+ *                             caller that streams results back out; writes at
+ *                             most cap pairs, returns their number or -1.
+ */
+int glx_algorithm_run_fed(glx_algorithm* alg);
+int glx_algorithm_feed(glx_algorithm* alg, int64_t off, int64_t len);
+int64_t glx_algorithm_done_ranges(glx_algorithm* alg, int64_t* out, int64_t cap);
 /* Number of bytes moved over the peer links by this rank in one run(). */
 int64_t glx_algorithm_bytes_sent(glx_algorithm* alg);
 /* How run() executes: GLX_ENGINE_STEPS = the schedule's steps issued by the

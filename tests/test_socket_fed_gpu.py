@@ -1,0 +1,150 @@
+"""Host-memory endpoints fed from a socket: the reference's
+path starts in host memory that a transport fills (gloo/transport/tcp/
+pair.cc:385-451 receives into the registered buffer) and returns results the
+same way.  Here each rank's host buffer is filled from a real TCP loopback
+socket by a receiver thread that calls alg.feed() as bytes arrive, while the
+rank runs alg.run_fed(): every 8 MiB piece is copied to the device as soon as
+it is complete and each schedule step waits only for its own pieces.  The
+result must be the reference's bits (oracle), done_ranges() must cover the
+buffer, and a piece that never arrives must end in IoException."""
+import socket
+import threading
+
+import numpy as np
+import pytest
+
+from helpers import case_inputs, run_ranks, same_bits
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+PIECE = 1 << 20  # socket send size (bytes)
+
+
+def socket_feeder(alg, buf, data, order="in_order"):
+    """A loopback TCP connection: a sender thread writes `data`'s bytes (in
+    `order`), the returned receiver thread recv_into()s them into `buf` and
+    feeds the elements each recv completes."""
+    es = buf.itemsize
+    srv = socket.create_server(("127.0.0.1", 0))
+    port = srv.getsockname()[1]
+    raw = memoryview(np.ascontiguousarray(data).view(np.uint8))
+    dst = memoryview(buf.view(np.uint8))
+    nbytes = raw.nbytes
+    pieces = [(o, min(PIECE, nbytes - o)) for o in range(0, nbytes, PIECE)]
+    if order == "reversed":
+        pieces = pieces[::-1]
+
+    def send():
+        with socket.create_connection(("127.0.0.1", port)) as c:
+            for o, n in pieces:
+                c.sendall(o.to_bytes(8, "little") + n.to_bytes(8, "little"))
+                c.sendall(raw[o:o + n])
+
+    def recv():
+        conn, _ = srv.accept()
+        with conn:
+            for _ in range(len(pieces)):
+                hdr = bytearray(16)
+                got = 0
+                while got < 16:
+                    got += conn.recv_into(memoryview(hdr)[got:], 16 - got)
+                o = int.from_bytes(hdr[:8], "little")
+                n = int.from_bytes(hdr[8:], "little")
+                got = 0
+                while got < n:
+                    k = conn.recv_into(dst[o + got:o + n], n - got)
+                    assert k > 0
+                    got += k
+                    # feed the whole elements of this piece received so far
+                lo, hi = o // es, (o + n) // es
+                alg.feed(lo, hi - lo)
+        srv.close()
+
+    ts = [threading.Thread(target=send, daemon=True), threading.Thread(target=recv, daemon=True)]
+    for t in ts:
+        t.start()
+    return ts
+
+
+def fed_allreduce(algo, P, N, dtype=O.FLOAT32, order="in_order", runs=1):
+    import gloo_amd
+    ins = case_inputs(P, N, dtype, 1, 0, seed=41)
+    store = gloo_amd.rendezvous.HashStore()
+    bufs = [np.zeros(N, dtype=O.NP_DTYPE[dtype]) for _ in range(P)]
+    done = [None] * P
+
+    def rank_fn(r):
+        ctx = gloo_amd.rendezvous.Context(r, P, 0)
+        ctx.setTimeout(60)
+        ctx.connectFullMesh(store)
+        dt = dtype if dtype in (O.FLOAT16, O.BFLOAT16) else None
+        if algo == "halving_doubling":
+            alg = gloo_amd.AllreduceHalvingDoubling(ctx, [bufs[r]], dtype=dt)
+        else:
+            alg = gloo_amd.AllreduceRingChunked(ctx, [bufs[r]], schedule="ring", dtype=dt)
+        for _ in range(runs):
+            ts = socket_feeder(alg, bufs[r], ins[r][0], order)
+            alg.run_fed()
+            for t in ts:
+                t.join(60)
+        done[r] = alg.done_ranges()
+        alg.close()
+        return True
+
+    run_ranks(P, rank_fn, timeout=120)
+    return bufs, done, ins
+
+
+def covered(ranges, N):
+    m = np.zeros(N, dtype=bool)
+    for o, n in ranges:
+        m[o:o + n] = True
+    return bool(m.all())
+
+
+@pytest.mark.parametrize("algo", ["ring_chunked", "halving_doubling"])
+@pytest.mark.parametrize("P,N", [(1, 100003), (2, 3 << 20), (3, (5 << 20) + 7), (4, 1 << 22)])
+def test_socket_fed_allreduce_vs_oracle(algo, P, N):
+    bufs, done, ins = fed_allreduce(algo, P, N)
+    code = O.HALVING_DOUBLING if algo == "halving_doubling" else O.RING_CHUNKED
+    exp = O.allreduce(code, O.SUM, O.FLOAT32, ins)
+    for r in range(P):
+        assert same_bits(bufs[r], exp[r][0]), "rank %d" % r
+        assert covered(done[r], N)
+
+
+def test_socket_fed_out_of_order_and_repeated():
+    """Pieces arriving back to front (a transport delivering out of order)
+    and two fed runs on one instance."""
+    P, N = 2, (3 << 20) + 5
+    bufs, done, ins = fed_allreduce("ring_chunked", P, N, order="reversed", runs=2)
+    exp = O.allreduce(O.RING_CHUNKED, O.SUM, O.FLOAT32, ins)
+    for r in range(P):
+        assert same_bits(bufs[r], exp[r][0])
+        assert covered(done[r], N)
+
+
+def test_socket_fed_float16():
+    P, N = 2, (2 << 20) + 3
+    bufs, done, ins = fed_allreduce("ring_chunked", P, N, dtype=O.FLOAT16)
+    exp = O.allreduce(O.RING_CHUNKED, O.SUM, O.FLOAT16, ins)
+    for r in range(P):
+        assert same_bits(bufs[r], exp[r][0])
+
+
+def test_unfed_piece_times_out():
+    """A piece that never arrives: run_fed() raises IoException ("Timed out
+    waiting for host data") after the context timeout instead of hanging."""
+    import gloo_amd
+    N = 3 << 20
+    ctx = gloo_amd.rendezvous.Context(0, 1, 0)
+    ctx.setTimeout(2)
+    buf = np.zeros(N, dtype=np.float32)
+    alg = gloo_amd.AllreduceRingChunked(ctx, [buf])
+    alg.feed(0, N // 2)  # the second half never comes
+    with pytest.raises(gloo_amd.IoException, match="host data"):
+        alg.run_fed()
+    alg.close()
