@@ -204,6 +204,7 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
   }
   GLX_ENFORCE(!hostMode_ || !userStream_, "streams cannot be used with host-memory buffers");
   if (hostMode_) setupHostMode();
+  staged_ = hostMode_;
   if (!hostMode_ && !perCallBuffers && count_ > 0) {
     // pointers on other GPUs of this rank (the reference's multi-device
     // ranks, gloo/cuda_allreduce_ring_chunked.cc): the fold kernel reads them
@@ -897,8 +898,82 @@ void HipPlanExecutor::runFn(const FnCall& call) {
 // they are not pinned; they are copied into device staging buffers owned by
 // this executor, the device path runs there, and the result is copied back
 // to every output.  Blocking, like the reference.
+// Staging of host memory for the function-style op (created at its first
+// overlapped host call): the class algorithms' machinery (setupHostMode)
+// with one device buffer and per-call host sources / destinations.
+void HipPlanExecutor::setupCallStaging() {
+  if (!devBufs_.empty()) return;
+  const size_t bytes = (size_t)count_ * esize_;
+  char* d = nullptr;
+  GLX_HIP_CHECK(hipMalloc((void**)&d, bytes));
+  devBufs_.push_back(d);
+  GLX_HIP_CHECK(hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking));
+  GLX_HIP_CHECK(hipStreamCreateWithFlags(&d2h_, hipStreamNonBlocking));
+  stage_ = glx::stagePlan(plan_, count_, std::max<int64_t>(1, kStagePieceBytes / (int64_t)esize_));
+  h2dEvents_.resize(stage_.h2d.size(), nullptr);
+  for (auto& e : h2dEvents_) GLX_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  d2hEvents_.assign(plan_.steps.size(), nullptr);
+  for (size_t i = 0; i < plan_.steps.size(); i++) {
+    if (!stage_.d2h[i].empty()) {
+      GLX_HIP_CHECK(hipEventCreateWithFlags(&d2hEvents_[i], hipEventDisableTiming));
+    }
+  }
+  GLX_HIP_CHECK(hipEventCreateWithFlags(&hostDone_, hipEventDisableTiming));
+}
+
+// gloo::allreduce(opts) on ONE host input (or in place on the output) and
+// ONE host output: staged like the class algorithms -- H2D pieces in the
+// order the schedule first touches them, every step waiting only for its
+// own, each range copied back to the output right after its final write --
+// instead of copying everything in, running, and copying everything out.
+void HipPlanExecutor::runFnHostStaged(const FnCall& call) {
+  setupCallStaging();
+  void* src = call.in.empty() ? call.out[0] : call.in[0];
+  callSrc_ = {src};
+  callDst_ = {call.out[0]};
+  staged_ = true;
+  timeout_ = call.timeout;
+  struct Restore {
+    HipPlanExecutor* e;
+    ~Restore() {
+      e->callSrc_.clear();
+      e->callDst_.clear();
+      e->staged_ = e->hostMode_;
+      e->timeout_ = std::chrono::milliseconds(0);
+    }
+  } restore{this};
+  computeH2dWaited_ = -1;
+  for (auto& c : copies_) c.h2dWaited = -1;
+  {
+    std::lock_guard<std::mutex> g(doneMutex_);
+    doneQueue_.clear();
+    doneUsed_ = 0;
+  }
+  pieceIssued_.assign(stage_.h2d.size(), 0);
+  for (size_t j = 0; j < stage_.h2d.size(); j++) issuePiece(j);
+  if (contextSize_ > 1) exchange(devBufs_[0]);
+  // ranges no step wrote hold the input: the output needs them too when it
+  // is another buffer (one input: genLocalReduceFunction copies,
+  // gloo/allreduce.cc:50-56)
+  if (src != call.out[0]) {
+    waitH2D(compute_, computeH2dWaited_, 0, count_);
+    GLX_HIP_CHECK(hipEventRecord(hostDone_, compute_));
+    GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, hostDone_, 0));
+    copyBack(contextSize_ > 1 ? stage_.d2hRest : std::vector<glx::Range>{{0, count_}});
+  }
+  GLX_HIP_CHECK(hipStreamSynchronize(d2h_));
+  GLX_HIP_CHECK(hipStreamSynchronize(compute_));
+  GLX_HIP_CHECK(hipStreamSynchronize(h2d_));
+  noteDone(d2h_);
+  checkDevice();
+}
+
 void HipPlanExecutor::runFnHost(const FnCall& call) {
   GLX_ENFORCE(call.stream == nullptr, "a stream cannot be used with host-memory buffers");
+  if (call.in.size() <= 1 && call.out.size() == 1) {
+    runFnHostStaged(call);
+    return;
+  }
   const size_t bytes = (size_t)count_ * esize_;
   // device staging: out[0], and the inputs (or, with no inputs, the outputs,
   // which are then folded into out[0])
@@ -1023,8 +1098,14 @@ void HipPlanExecutor::waitH2D(hipStream_t s, int& waited, int64_t off, int64_t l
 // The host buffers the device copies are staged from and back to: the
 // user's pointers, or the one pinned buffer they were folded into.
 std::vector<void*> HipPlanExecutor::hostSources() const {
+  if (!callSrc_.empty()) return callSrc_;
   if (hostFold_) return {hostStage_};
   return ptrs_;
+}
+
+std::vector<void*> HipPlanExecutor::hostDests() const {
+  if (!callDst_.empty()) return callDst_;
+  return hostSources();
 }
 
 // Final values of `ranges` (in devBufs_[0]) to every user pointer, on d2h_
@@ -1032,7 +1113,7 @@ std::vector<void*> HipPlanExecutor::hostSources() const {
 void HipPlanExecutor::copyBack(const std::vector<glx::Range>& ranges) {
   for (const glx::Range& r : ranges) {
     const size_t at = (size_t)r.off * esize_, n = (size_t)r.len * esize_;
-    for (void* p : hostSources()) {
+    for (void* p : hostDests()) {
       GLX_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(p) + at, devBufs_[0] + at, n,
                                    hipMemcpyDeviceToHost, d2h_));
     }
@@ -1261,7 +1342,7 @@ void HipPlanExecutor::exchange(char* ptr0) {
               GLX_HIP_CHECK(hipStreamWaitEvent(cs.s, computeMark_, 0));
               cs.waitedMark = markEpoch_;
             }
-            if (hostMode_) waitH2D(cs.s, cs.h2dWaited, s.off, s.len);
+            if (staged_) waitH2D(cs.s, cs.h2dWaited, s.off, s.len);
             hipError_t ce = hipErrorUnknown;
             if (copyEngine_ == kCopyKernel) {
               ce = glx::launch_copy(dst + at, src + at, len, cs.s);
@@ -1310,12 +1391,12 @@ void HipPlanExecutor::exchange(char* ptr0) {
       }
       case glx::REDUCE: {
         waitWar(s.off, s.len);
-        if (hostMode_) waitH2D(compute_, computeH2dWaited_, s.off, s.len);
+        if (staged_) waitH2D(compute_, computeH2dWaited_, s.off, s.len);
         char* dst = ptr0 + (size_t)s.off * esize_;
         const char* src = landing(blocks_, s.boff, s.off);
         GLX_HIP_CHECK(glx::launch_reduce(op_, dtype_, dst, dst, src, (size_t)s.len, compute_));
         computeSinceMark = true;
-        if (hostMode_ && !stage_.d2h[i].empty()) {  // final values: copy back now
+        if (staged_ && !stage_.d2h[i].empty()) {  // final values: copy back now
           GLX_HIP_CHECK(hipEventRecord(d2hEvents_[i], compute_));
           GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, d2hEvents_[i], 0));
           copyBack(stage_.d2h[i]);
@@ -1335,7 +1416,7 @@ void HipPlanExecutor::exchange(char* ptr0) {
         for (size_t q = i; q <= last; q++) {
           const glx::Step& f = steps[q];
           waitWar(f.off, f.len);
-          if (hostMode_) waitH2D(compute_, computeH2dWaited_, f.off, f.len);
+          if (staged_) waitH2D(compute_, computeH2dWaited_, f.off, f.len);
           char* dst = ptr0 + (size_t)f.off * esize_;
           glx::FoldSpec spec;
           spec.dst = dst;
@@ -1361,7 +1442,7 @@ void HipPlanExecutor::exchange(char* ptr0) {
         }
         computeSinceMark = true;
         for (size_t q = i; q <= last; q++) {
-          if (hostMode_ && !stage_.d2h[q].empty()) {  // final values: copy back now
+          if (staged_ && !stage_.d2h[q].empty()) {  // final values: copy back now
             GLX_HIP_CHECK(hipEventRecord(d2hEvents_[q], compute_));
             GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, d2hEvents_[q], 0));
             copyBack(stage_.d2h[q]);
@@ -1372,13 +1453,13 @@ void HipPlanExecutor::exchange(char* ptr0) {
       }
       case glx::COPY: {
         waitWar(s.off, s.len);
-        if (hostMode_) waitH2D(compute_, computeH2dWaited_, s.off, s.len);
+        if (staged_) waitH2D(compute_, computeH2dWaited_, s.off, s.len);
         char* dst = ptr0 + (size_t)s.off * esize_;
         const char* src = landing(blocks_, s.boff, s.off);
         GLX_HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)s.len * esize_,
                                      hipMemcpyDeviceToDevice, compute_));
         computeSinceMark = true;
-        if (hostMode_ && !stage_.d2h[i].empty()) {  // final values: copy back now
+        if (staged_ && !stage_.d2h[i].empty()) {  // final values: copy back now
           GLX_HIP_CHECK(hipEventRecord(d2hEvents_[i], compute_));
           GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, d2hEvents_[i], 0));
           copyBack(stage_.d2h[i]);
@@ -1898,7 +1979,7 @@ void HipPlanExecutor::runDevice(char* ptr0) {
   const uint64_t ticks = (uint64_t)effectiveTimeout().count() * (uint64_t)clockKhz_;
   // epochs stay ordered even when calls come on different streams
   if (ddLaunched_) GLX_HIP_CHECK(hipStreamWaitEvent(compute_, ddDone_, 0));
-  if (hostMode_) waitH2D(compute_, computeH2dWaited_, 0, count_);
+  if (staged_) waitH2D(compute_, computeH2dWaited_, 0, count_);
   if (engine_ == kEngineOneShot) {
     glx::OneShotParams p = os_;
     p.buf = ptr0;
@@ -1972,7 +2053,7 @@ void HipPlanExecutor::runDevice(char* ptr0) {
   }
   GLX_HIP_CHECK(hipEventRecord(ddDone_, compute_));
   ddLaunched_ = true;
-  if (hostMode_) {
+  if (staged_) {
     GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, ddDone_, 0));
     copyBack({glx::Range{0, count_}});
   }

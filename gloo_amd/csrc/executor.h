@@ -230,7 +230,15 @@ class HipPlanExecutor : public Algorithm {
   std::vector<char*> devBufs_;     // device copy of each user pointer (or of hostStage_)
   bool hostFold_ = false;          // several pointers < kOnDeviceThreshold: fold on the host
   char* hostStage_ = nullptr;      // pinned: the host fold's result, staged and returned
-  std::vector<void*> hostSources() const;
+  std::vector<void*> hostSources() const;  // H2D sources of the staged buffer
+  std::vector<void*> hostDests() const;    // where its final values go back to
+  // staged_: the current run stages host memory (class host mode, or a
+  // function-style call on host buffers); callSrc_/callDst_: that call's
+  // host buffers
+  bool staged_ = false;
+  std::vector<void*> callSrc_, callDst_;
+  void setupCallStaging();
+  void runFnHostStaged(const FnCall& call);
   std::vector<void*> registered_;  // host ranges pinned by us
   hipStream_t h2d_ = nullptr, d2h_ = nullptr;
   glx::StagePlan stage_;

@@ -287,3 +287,22 @@ def test_allreduce_fn_host_buffers_vs_reference_golden(rec):
     for r in range(rec["P"]):
         for i in range(rec["nout"]):
             check_against_golden(rec, DATA, got[r][i])
+
+
+@pytest.mark.parametrize("algo", [1, 2], ids=["ring", "bcube"])
+@pytest.mark.parametrize("inplace", [True, False], ids=["in_place", "out_of_place"])
+def test_allreduce_fn_host_staged_large(algo, inplace):
+    """One host input (or in place) and one host output above the staging
+    piece size: the overlapped path (H2D pieces in first-use order, each
+    range copied back after its final write) -- same bits as the oracle."""
+    P, N = 3, (5 << 20) + 3
+    data = case_inputs(P, N, O.FLOAT32, 1, 0, seed=51)
+    if inplace:
+        ins, outs = [[] for _ in range(P)], data
+    else:
+        ins, outs = data, [[np.zeros(N, np.float32)] for _ in range(P)]
+    got = host_allreduce_fn(algo, O.SUM, O.FLOAT32, ins, outs, runs=2)
+    code = O.FN_BCUBE if algo == 2 else O.FN_RING
+    exp = O.allreduce_fn(code, O.SUM, O.FLOAT32, [[] for _ in range(P)], data)
+    for r in range(P):
+        assert np.array_equal(got[r][0].view(np.uint32), exp[r][0].view(np.uint32)), r
