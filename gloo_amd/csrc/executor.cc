@@ -243,6 +243,12 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
     }
     const size_t G = std::max<size_t>(
         1, std::min(maxSlices(2), ((size_t)maxSeg + minSlice - 1) / minSlice));
+    // programs without FOLD steps run the 2-source variant (81 instead of 145
+    // VGPRs).  The grid stays sized by the 8-source variant's residency: with
+    // 8 ranks sharing one GPU, 160 instead of 96 workgroups per rank made the
+    // 256 MiB ring 30 % slower (stores through the IPC mappings contend;
+    // profiles/r2k_*); one rank per GPU gets 512 either way.
+    pk_.maxSrc = probe.anyFold ? glx::kOsMaxRanks : 2;
     sync_ = glx::syncTable(algo, contextRank_, contextSize_, count_, pp, (int)G);
     pk_.G = (int)G;
     // GLOO_AMD_FUSE=0: one landing slot per channel and no reduce-and-forward

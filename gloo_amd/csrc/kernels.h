@@ -133,6 +133,7 @@ struct PlanKernelParams {
   const char* const* foldSrc;  // device memory; nullptr = buf
   int nsteps, G;
   int slots;                   // landing slots per channel (1 or 2, plan.h SyncTable)
+  int maxSrc;                  // most sources of a FOLD step (2 when there is none)
   uint64_t run;                // runs completed before this one
   uint64_t timeoutTicks;
   int* status;
@@ -146,7 +147,8 @@ struct PlanKernelParams {
 hipError_t launch_plan_kernel(int op, int dtype, const PlanKernelParams& p, hipStream_t s);
 
 // Workgroups of a device-engine kernel (kernel 0 = one-shot, 1 = two-shot,
-// 2 = plan kernel) for (op, dtype) that fit on the current device at once
+// 2 = plan kernel, 3 = plan kernel for programs without FOLD steps) for
+// (op, dtype) that fit on the current device at once
 // (occupancy x CUs).  A grid of peers waiting on each other must be
 // resident as a whole.
 int device_engine_resident_blocks(int kernel, int op, int dtype);

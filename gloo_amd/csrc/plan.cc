@@ -922,7 +922,10 @@ SyncTable syncTable(int algo, int rank, int size, int64_t count, const PlanParam
   for (const Plan& p : all) {
     std::map<int64_t, std::pair<int64_t, int64_t>> feeder;  // region -> (peer, channel)
     for (const Step& s : p.steps) {
-      if (s.kind == FOLD) t.slots = 1;
+      if (s.kind == FOLD) {
+        t.slots = 1;
+        t.anyFold = true;
+      }
       if (s.kind != RECV) continue;
       auto it = feeder.find(s.boff);
       const std::pair<int64_t, int64_t> ch{s.peer, s.channel};

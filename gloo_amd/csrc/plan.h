@@ -198,6 +198,7 @@ struct SyncTable {
   int64_t slice = 0;
   bool safe = true;
   int slots = 1;
+  bool anyFold = false;  // some rank's program has a FOLD step
   std::vector<std::pair<int, int>> outChans, inChans;  // (peer, tag)
   std::vector<StepSync> steps;
 };

@@ -94,7 +94,7 @@ __device__ __forceinline__ void copy_span(S* dst, const S* src, size_t a, size_t
 }
 
 // Copy [a, b) of src to every dsts[d] for d < n (one load, n stores).
-template <typename S>
+template <typename S, int MAXD = kOsMaxRanks - 1>
 __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* src, size_t a,
                                              size_t b, bool aligned) {
   const Span sp = split_span<16 / sizeof(S)>(a, b, aligned);
@@ -103,7 +103,7 @@ __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* 
     const size_t i = sp.edge(t);
     const S x = src[i];
 #pragma unroll
-    for (int d = 0; d < kOsMaxRanks - 1; d++) {
+    for (int d = 0; d < MAXD; d++) {
       if (d < n) reinterpret_cast<S*>(dsts[d])[i] = x;
     }
   }
@@ -112,7 +112,7 @@ __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* 
   for (; i + kBlock < vb; i += 2 * kBlock) {
     const v4u x0 = vs[i], x1 = vs[i + kBlock];
 #pragma unroll
-    for (int d = 0; d < kOsMaxRanks - 1; d++) {
+    for (int d = 0; d < MAXD; d++) {
       if (d < n) {
         reinterpret_cast<v4u*>(dsts[d])[i] = x0;
         reinterpret_cast<v4u*>(dsts[d])[i + kBlock] = x1;
@@ -122,7 +122,7 @@ __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* 
   for (; i < vb; i += kBlock) {
     const v4u x = vs[i];
 #pragma unroll
-    for (int d = 0; d < kOsMaxRanks - 1; d++) {
+    for (int d = 0; d < MAXD; d++) {
       if (d < n) reinterpret_cast<v4u*>(dsts[d])[i] = x;
     }
   }
@@ -132,7 +132,7 @@ __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* 
 // (the ring's chain: the newer rank's value is the in-place destination)
 // or, LEFT, acc = op(acc, s_k) (a left fold, out = op(out, peer)).
 // The result also goes to every outs[d], d < nout.
-template <typename T, int OP, bool LEFT = false>
+template <typename T, int OP, bool LEFT = false, int MAXK = kOsMaxRanks>
 __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
                                           const typename Elem<T, OP>::S* const* srcs, int P,
                                           char* const* outs, int nout, size_t a, size_t b,
@@ -143,19 +143,19 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
   const size_t va = sp.va, vb = sp.vb;
   for (size_t t = threadIdx.x; t < sp.nedge(); t += kBlock) {
     const size_t i = sp.edge(t);
-    S y[kOsMaxRanks];
+    S y[MAXK];
 #pragma unroll
-    for (int k = 0; k < kOsMaxRanks; k++) {
+    for (int k = 0; k < MAXK; k++) {
       if (k < P) y[k] = srcs[k][i];
     }
     S acc = y[0];
 #pragma unroll
-    for (int k = 1; k < kOsMaxRanks; k++) {
+    for (int k = 1; k < MAXK; k++) {
       if (k < P) acc = LEFT ? E::apply(acc, y[k]) : E::apply(y[k], acc);
     }
     dst[i] = acc;
 #pragma unroll
-    for (int d = 0; d < kOsMaxRanks - 1; d++) {
+    for (int d = 0; d < MAXK - 1; d++) {
       if (d < nout) reinterpret_cast<S*>(outs[d])[i] = acc;
     }
   }
@@ -163,9 +163,9 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
   // 1-byte types: 16 lanes of byte ops per vector already fill the registers)
   size_t v = va + threadIdx.x;
   for (; sizeof(S) > 1 && v + kBlock < vb; v += 2 * kBlock) {
-    v4u y[kOsMaxRanks], z[kOsMaxRanks];
+    v4u y[MAXK], z[MAXK];
 #pragma unroll
-    for (int k = 0; k < kOsMaxRanks; k++) {
+    for (int k = 0; k < MAXK; k++) {
       if (k < P) {
         y[k] = reinterpret_cast<const v4u*>(srcs[k])[v];
         z[k] = reinterpret_cast<const v4u*>(srcs[k])[v + kBlock];
@@ -173,7 +173,7 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
     }
     v4u acc = y[0], acc2 = z[0];
 #pragma unroll
-    for (int k = 1; k < kOsMaxRanks; k++) {
+    for (int k = 1; k < MAXK; k++) {
       if (k < P) {
         acc = LEFT ? vec_apply<T, OP>(acc, y[k]) : vec_apply<T, OP>(y[k], acc);
         acc2 = LEFT ? vec_apply<T, OP>(acc2, z[k]) : vec_apply<T, OP>(z[k], acc2);
@@ -182,7 +182,7 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
     reinterpret_cast<v4u*>(dst)[v] = acc;
     reinterpret_cast<v4u*>(dst)[v + kBlock] = acc2;
 #pragma unroll
-    for (int d = 0; d < kOsMaxRanks - 1; d++) {
+    for (int d = 0; d < MAXK - 1; d++) {
       if (d < nout) {
         reinterpret_cast<v4u*>(outs[d])[v] = acc;
         reinterpret_cast<v4u*>(outs[d])[v + kBlock] = acc2;
@@ -190,19 +190,19 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
     }
   }
   for (; v < vb; v += kBlock) {
-    v4u y[kOsMaxRanks];
+    v4u y[MAXK];
 #pragma unroll
-    for (int k = 0; k < kOsMaxRanks; k++) {
+    for (int k = 0; k < MAXK; k++) {
       if (k < P) y[k] = reinterpret_cast<const v4u*>(srcs[k])[v];
     }
     v4u acc = y[0];
 #pragma unroll
-    for (int k = 1; k < kOsMaxRanks; k++) {
+    for (int k = 1; k < MAXK; k++) {
       if (k < P) acc = LEFT ? vec_apply<T, OP>(acc, y[k]) : vec_apply<T, OP>(y[k], acc);
     }
     reinterpret_cast<v4u*>(dst)[v] = acc;
 #pragma unroll
-    for (int d = 0; d < kOsMaxRanks - 1; d++) {
+    for (int d = 0; d < MAXK - 1; d++) {
       if (d < nout) reinterpret_cast<v4u*>(outs[d])[v] = acc;
     }
   }
@@ -458,7 +458,11 @@ __device__ __forceinline__ bool seg_part(const DevSegment& sg, int w, size_t& a,
   return a < b;
 }
 
-template <typename T, int OP>
+// MAXSRC: the most sources a FOLD step of the program has (8), or 2 for the
+// programs without FOLD steps (ring, halving-doubling, function-style ring):
+// the 8-way fold's registers would cut the resident workgroups per CU from
+// the 2-source variant's count (kernel-resource-usage) to 3.
+template <typename T, int OP, int MAXSRC>
 __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
   using S = typename Elem<T, OP>::S;
   __shared__ int s_ok;
@@ -501,17 +505,14 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
           const S* src = reinterpret_cast<const S*>(
               st.src + slotOf(p.run * st.rperRun + st.rseq) * (uint64_t)st.srcSlot);
           char* outs[2] = {reinterpret_cast<char*>(buf), dst};
-          const S* srcs[kOsMaxRanks];
-#pragma unroll
-          for (int k = 0; k < kOsMaxRanks; k++) srcs[k] = buf;
-          srcs[1] = src;
+          const S* srcs[2] = {buf, src};
           for (int g = st.seg0; g < st.seg1; g++) {
             size_t a, b;
             if (!seg_part(p.segs[g], w, a, b)) continue;
             if (st.kind == kStepCopySend) {
-              scatter_span<S>(outs, 2, src, a, b, aligned);
+              scatter_span<S, 2>(outs, 2, src, a, b, aligned);
             } else {
-              fold_span<T, OP, true>(buf, srcs, 2, outs + 1, 1, a, b, aligned);
+              fold_span<T, OP, true, 2>(buf, srcs, 2, outs + 1, 1, a, b, aligned);
             }
           }
         }
@@ -528,13 +529,13 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
       case 2:    // REDUCE: buf = op(buf, region), in place
       case 3:    // COPY:   buf = region
       case 5: {  // FOLD
-        const S* srcs[kOsMaxRanks];
+        const S* srcs[MAXSRC];
 #pragma unroll
-        for (int k = 0; k < kOsMaxRanks; k++) srcs[k] = buf;
+        for (int k = 0; k < MAXSRC; k++) srcs[k] = buf;
         int n = 2;
         if (st.kind == 5) {
           n = st.nsrc;
-          for (int k = 0; k < n && k < kOsMaxRanks; k++) {
+          for (int k = 0; k < n && k < MAXSRC; k++) {
             const char* q = p.foldSrc[st.srcIndex + k];
             if (q != nullptr) srcs[k] = reinterpret_cast<const S*>(q);
           }
@@ -548,9 +549,9 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
           if (st.kind == 3) {
             copy_span<S>(buf, srcs[1], a, b, aligned);
           } else if (st.kind == 2 || st.left) {
-            fold_span<T, OP, true>(buf, srcs, n, nullptr, 0, a, b, aligned);
+            fold_span<T, OP, true, MAXSRC>(buf, srcs, n, nullptr, 0, a, b, aligned);
           } else {
-            fold_span<T, OP, false>(buf, srcs, n, nullptr, 0, a, b, aligned);
+            fold_span<T, OP, false, MAXSRC>(buf, srcs, n, nullptr, 0, a, b, aligned);
           }
         }
         break;
@@ -602,7 +603,8 @@ template <typename T, int OP>
 const void* engine_kernel(int kernel) {
   if (kernel == 0) return (const void*)oneshot_kernel<T, OP>;
   if (kernel == 1) return (const void*)twoshot_kernel<T, OP>;
-  return (const void*)plan_kernel<T, OP>;
+  if (kernel == 3) return (const void*)plan_kernel<T, OP, 2>;
+  return (const void*)plan_kernel<T, OP, kOsMaxRanks>;
 }
 
 template <typename T>
@@ -625,19 +627,30 @@ int resident_typed(int kernel, int op) {
   return perCu * cus;
 }
 
-template <typename T>
-hipError_t launch_pk_op(int op, const PlanKernelParams& p, hipStream_t s) {
+template <typename T, int MAXSRC>
+hipError_t launch_pk_src(int op, const PlanKernelParams& p, hipStream_t s) {
   const dim3 grid((unsigned)p.G), block(kBlock);
   switch (op) {
-    case GLX_SUM: hipLaunchKernelGGL((plan_kernel<T, GLX_SUM>), grid, block, 0, s, p); break;
-    case GLX_PRODUCT:
-      hipLaunchKernelGGL((plan_kernel<T, GLX_PRODUCT>), grid, block, 0, s, p);
+    case GLX_SUM:
+      hipLaunchKernelGGL((plan_kernel<T, GLX_SUM, MAXSRC>), grid, block, 0, s, p);
       break;
-    case GLX_MAX: hipLaunchKernelGGL((plan_kernel<T, GLX_MAX>), grid, block, 0, s, p); break;
-    case GLX_MIN: hipLaunchKernelGGL((plan_kernel<T, GLX_MIN>), grid, block, 0, s, p); break;
+    case GLX_PRODUCT:
+      hipLaunchKernelGGL((plan_kernel<T, GLX_PRODUCT, MAXSRC>), grid, block, 0, s, p);
+      break;
+    case GLX_MAX:
+      hipLaunchKernelGGL((plan_kernel<T, GLX_MAX, MAXSRC>), grid, block, 0, s, p);
+      break;
+    case GLX_MIN:
+      hipLaunchKernelGGL((plan_kernel<T, GLX_MIN, MAXSRC>), grid, block, 0, s, p);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_pk_op(int op, const PlanKernelParams& p, hipStream_t s) {
+  return p.maxSrc <= 2 ? launch_pk_src<T, 2>(op, p, s) : launch_pk_src<T, kOsMaxRanks>(op, p, s);
 }
 
 }  // namespace
@@ -681,7 +694,7 @@ hipError_t launch_oneshot(int op, int dtype, const OneShotParams& p, hipStream_t
 hipError_t launch_plan_kernel(int op, int dtype, const PlanKernelParams& p, hipStream_t s) {
   if (p.G < 1 || p.G > kOsMaxSlices || p.nsteps < 0 || p.steps == nullptr ||
       p.segs == nullptr || p.foldSrc == nullptr || p.status == nullptr || p.claim == nullptr ||
-      (p.slots != 1 && p.slots != 2)) {
+      (p.slots != 1 && p.slots != 2) || p.maxSrc < 2 || p.maxSrc > kOsMaxRanks) {
     return hipErrorInvalidValue;
   }
   switch (dtype) {
