@@ -19,10 +19,12 @@
 
 #include <chrono>
 #include <cstdint>
+#include <algorithm>
 #include <memory>
 #include <stdexcept>
 #include <string>
 #include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "glx.h"
@@ -197,6 +199,34 @@ class Algorithm {  // gloo::Algorithm
   virtual void run() = 0;
 };
 
+// A HIP event (gloo::CudaStream's record / wait, gloo/cuda.h:40-120).
+class Event {
+ public:
+  Event() { check(glx_event_create(&e_), "Event"); }
+  ~Event() { glx_event_destroy(e_); }
+  Event(const Event&) = delete;
+  Event& operator=(const Event&) = delete;
+  void record(glx_stream_t stream) { check(glx_event_record(e_, stream), "Event::record"); }
+  // true once everything recorded before it has completed
+  bool query() {
+    const int rc = glx_event_query(e_);
+    if (rc == GLX_NOT_READY) return false;
+    check(rc, "Event::query");
+    return true;
+  }
+  // stream waits on the device; nullptr: the calling thread blocks
+  void wait(glx_stream_t stream = nullptr) { check(glx_event_wait(e_, stream), "Event::wait"); }
+  glx_event_t handle() const { return e_; }
+
+ private:
+  glx_event_t e_ = nullptr;
+};
+
+// How an algorithm's messages moved (glx_algorithm_transport_stats).
+struct TransportStats {
+  int64_t peerCopies, deviceCopies, kernelCopies, deviceKernels, bytes, hostFolds;
+};
+
 namespace detail {
 template <typename T>
 class DeviceAllreduce : public Algorithm {
@@ -220,6 +250,26 @@ class DeviceAllreduce : public Algorithm {
   int64_t bytesSentPerRun() const { return glx_algorithm_bytes_sent(a_); }
   // GLX_ENGINE_STEPS / _ONESHOT / _TWOSHOT / _DEVSTEPS (glx.h)
   int engine() const { return glx_algorithm_engine(a_); }
+  // Host buffer fed from a transport: runFed() runs while feed() (any
+  // thread) reports which elements have arrived; doneRanges() lists the
+  // {off, len} ranges already back in host memory.
+  void runFed() { check(glx_algorithm_run_fed(a_), "runFed"); }
+  void feed(int64_t off, int64_t len) { check(glx_algorithm_feed(a_, off, len), "feed"); }
+  std::vector<std::pair<int64_t, int64_t>> doneRanges() const {
+    const int64_t n = glx_algorithm_done_ranges(a_, nullptr, 0);
+    std::vector<int64_t> v((size_t)std::max<int64_t>(2 * n, 2));
+    const int64_t k = glx_algorithm_done_ranges(a_, v.data(), n);
+    std::vector<std::pair<int64_t, int64_t>> out;
+    for (int64_t i = 0; i < k && i < n; i++) out.emplace_back(v[2 * i], v[2 * i + 1]);
+    return out;
+  }
+  // record `ev` at the end of the last run's work (streams[0] with streams)
+  void record(Event& ev) { check(glx_algorithm_record(a_, ev.handle()), "record"); }
+  TransportStats transportStats() const {
+    int64_t o[6] = {0};
+    glx_algorithm_transport_stats(a_, o, 6);
+    return TransportStats{o[0], o[1], o[2], o[3], o[4], o[5]};
+  }
 
  private:
   std::shared_ptr<Context> ctx_;

@@ -277,9 +277,49 @@ void allreduceNewTimeout() {
   hipFree(dev);
 }
 
+// Streams + events: run() on a user stream, record the end of its work,
+// make a second stream wait for it on the device and copy the result out
+// (value = rank pattern -> every element P(P-1)/2), plus transport stats.
+void streamsAndEvents(int P, int N) {
+  spawn(P, [&](std::shared_ptr<gloo_amd::Context> ctx) {
+    hipStream_t work = nullptr, consumer = nullptr;
+    hipCheck(hipStreamCreate(&work), "hipStreamCreate");
+    hipCheck(hipStreamCreate(&consumer), "hipStreamCreate");
+    std::vector<float> host((size_t)N, (float)ctx->rank);
+    float *dev = nullptr, *out = nullptr;
+    hipCheck(hipMalloc((void**)&dev, sizeof(float) * N), "hipMalloc");
+    hipCheck(hipMalloc((void**)&out, sizeof(float) * N), "hipMalloc");
+    hipCheck(hipMemcpy(dev, host.data(), sizeof(float) * N, hipMemcpyHostToDevice), "H2D");
+    {
+      gloo_amd::HipAllreduceRingChunked<float> alg(ctx, {dev}, N, {work});
+      gloo_amd::Event ev;
+      alg.run();
+      alg.record(ev);
+      ev.wait(consumer);
+      hipCheck(hipMemcpyAsync(out, dev, sizeof(float) * N, hipMemcpyDeviceToDevice, consumer),
+               "D2D");
+      hipCheck(hipStreamSynchronize(consumer), "sync");
+      EXPECT(ev.query(), "event not complete after the consumer finished");
+      const gloo_amd::TransportStats t = alg.transportStats();
+      EXPECT(P == 1 || t.deviceCopies + t.peerCopies + t.kernelCopies + t.deviceKernels > 0,
+             "no transport recorded");
+    }
+    hipCheck(hipMemcpy(host.data(), out, sizeof(float) * N, hipMemcpyDeviceToHost), "D2H");
+    const float want = (float)(P * (P - 1) / 2);
+    size_t bad = 0;
+    for (float v : host) bad += v != want;
+    EXPECT(bad == 0, "streams/events P=%d N=%d: %zu elements != %g", P, N, bad, want);
+    hipFree(dev);
+    hipFree(out);
+    hipStreamDestroy(work);
+    hipStreamDestroy(consumer);
+  });
+}
+
 }  // namespace
 
 int main() {
+  for (int P : {1, 2, 4}) streamsAndEvents(P, 100003);
   for (int P = 1; P <= 8; P++) {
     for (int N : {0, 4, 100, 1000, 10000}) {
       singlePointer<gloo_amd::HipAllreduceRingChunked>("ring_chunked", P, N);
