@@ -410,7 +410,18 @@ void Context::connectFullMesh(std::shared_ptr<rendezvous::Store> store) {
         (void)hipGetLastError();  // clear "already enabled"
         hipSetDevice(cur);
       }
+      int atomics = 0;
+      if (hipDeviceGetP2PAttribute(&atomics, hipDevP2PAttrNativeAtomicSupported, device_,
+                                   p.localDevice) != hipSuccess ||
+          atomics == 0) {
+        (void)hipGetLastError();
+        flagStores_ = true;
+      }
     }
+  }
+  if (const char* e = std::getenv("GLOO_AMD_FLAG_WRITE")) {
+    if (std::strcmp(e, "store") == 0) flagStores_ = true;
+    if (std::strcmp(e, "atomic") == 0) flagStores_ = false;
   }
   // Everyone has mapped everyone: the names can go (mappings stay valid and
   // nothing is left behind in /dev/shm if a rank dies later).

@@ -132,6 +132,11 @@ class Context {
   bool ranksShareDevice() const;
   // Largest number of ranks on one GPU (by PCI bus id; equal on every rank).
   int maxRanksPerDevice() const;
+  // True when device kernels of this rank write peers' flag words with plain
+  // system-scope stores instead of atomic exchanges: some peer sits on
+  // another GPU whose link (hipDevP2PAttrNativeAtomicSupported) does not
+  // carry atomics, or GLOO_AMD_FLAG_WRITE=store.
+  bool flagStores() const { return flagStores_; }
 
   // Throws IoException if a peer process has exited.
   void checkPeersAlive();
@@ -175,6 +180,7 @@ class Context {
   int device_;
   int slot_ = 0;
   bool connected_ = false;
+  bool flagStores_ = false;
   std::chrono::milliseconds timeout_{30000};  // gloo/context.cc:18
   std::shared_ptr<rendezvous::Store> store_;
   ControlBlock local_;

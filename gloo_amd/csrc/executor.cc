@@ -1629,6 +1629,10 @@ void HipPlanExecutor::setupDevice() {
   os_.claim = ddClaim_;
   ts_.claim = ddClaim_;
   pk_.claim = ddClaim_;
+  const int fs = context_->flagStores() ? 1 : 0;
+  os_.flagStore = fs;
+  ts_.flagStore = fs;
+  pk_.flagStore = fs;
   GLX_HIP_CHECK(hipEventCreateWithFlags(&ddDone_, hipEventDisableTiming));
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) == hipSuccess &&

@@ -214,9 +214,16 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
 // both execute at the memory side, so no L2 -- the writer's, the reader's or
 // that of another XCD -- ever holds a copy of a flag line that could be read
 // stale or written back over a newer value.  Each flag has a 128-byte line
-// of its own (kFlagStride words): one writer per line.
-__device__ __forceinline__ void put_flag(uint64_t* word, uint64_t v) {
-  (void)__hip_atomic_exchange(word, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+// of its own (kFlagStride words): one writer per line.  Where the link to a
+// peer's GPU carries no atomics (Context::flagStores) the write is a
+// system-scope store instead: it goes through to the uncached flag block all
+// the same, and the owner's polls stay memory-side.
+__device__ __forceinline__ void put_flag(uint64_t* word, uint64_t v, bool store = false) {
+  if (store) {
+    __hip_atomic_store(word, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  } else {
+    (void)__hip_atomic_exchange(word, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // A compare-exchange that never matches (flags never reach ~0): a real
@@ -241,23 +248,23 @@ __device__ __forceinline__ const uint64_t* flag_at(const uint64_t* row, int w) {
 // 0..P-1, lane r excluded, where want(lane)) flag words set to epoch.
 template <typename Want>
 __device__ __forceinline__ void release_flags(uint64_t* const* rows, int P, int rank, int w,
-                                              uint64_t epoch, Want want) {
+                                              uint64_t epoch, bool store, Want want) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   // the compiler may drop the wait after the write-back when it can prove no
   // store is outstanding (MI355X_MICROARCH.md, compiler hazard): keep it
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
   const int t = (int)threadIdx.x;
-  if (t < P && t != rank && want(t)) put_flag(flag_at(rows[t], w), epoch);
+  if (t < P && t != rank && want(t)) put_flag(flag_at(rows[t], w), epoch, store);
 }
 
 // Every wave's stores complete and visible system-wide, then lane 0 stores
 // `value` into `word` (a flag in a peer's memory).
-__device__ __forceinline__ void signal_flag(uint64_t* word, uint64_t value) {
+__device__ __forceinline__ void signal_flag(uint64_t* word, uint64_t value, bool store) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) put_flag(word, value);
+  if (threadIdx.x == 0) put_flag(word, value, store);
 }
 
 // The first workgroup of the launch whose wait times out reports it: status
@@ -336,7 +343,7 @@ __global__ __launch_bounds__(kBlock, 2) void oneshot_kernel(OneShotParams p) {
     to[d - 1] = d < p.P ? p.push[j] : nullptr;
   }
   scatter_span<S>(to, p.P - 1, buf, e0, e1, aligned);
-  release_flags(p.flagOut, p.P, p.rank, w, p.epoch, [](int) { return true; });
+  release_flags(p.flagOut, p.P, p.rank, w, p.epoch, p.flagStore != 0, [](int) { return true; });
 
   // 2. wait
   const uint64_t start = __builtin_amdgcn_s_memrealtime();
@@ -395,7 +402,7 @@ __global__ __launch_bounds__(kBlock, 2) void twoshot_kernel(TwoShotParams p) {
     size_t a, b;
     if (span(j, a, b)) copy_span<S>(reinterpret_cast<S*>(p.rsPush[j]), buf, a, b, aligned);
   }
-  release_flags(p.flagAOut, p.P, p.rank, w, p.epoch, [&](int j) {
+  release_flags(p.flagAOut, p.P, p.rank, w, p.epoch, p.flagStore != 0, [&](int j) {
     size_t a, b;
     return span(j, a, b);
   });
@@ -428,7 +435,8 @@ __global__ __launch_bounds__(kBlock, 2) void twoshot_kernel(TwoShotParams p) {
       outs[d - 1] = d < p.P ? p.agPush[j] : nullptr;
     }
     fold_span<T, OP>(buf, src, p.P, outs, p.P - 1, a, b, aligned);
-    release_flags(p.flagBOut, p.P, p.rank, w, p.epoch, [](int) { return true; });
+    release_flags(p.flagBOut, p.P, p.rank, w, p.epoch, p.flagStore != 0,
+                  [](int) { return true; });
   }
   stamp(3);
 
@@ -516,7 +524,7 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
             }
           }
         }
-        signal_flag(flag_at(st.flag, w), seq);
+        signal_flag(flag_at(st.flag, w), seq, p.flagStore != 0);
         break;
       }
       case 1:  // RECV
@@ -558,7 +566,7 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
       }
       case 4:  // RELEASE: every wave is done reading the region
         __syncthreads();
-        if (threadIdx.x == 0) put_flag(flag_at(st.flag, w), seq);
+        if (threadIdx.x == 0) put_flag(flag_at(st.flag, w), seq, p.flagStore != 0);
         break;
       default:  // kStepNop: a SEND done inside the step it was fused into
         break;

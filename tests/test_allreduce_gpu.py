@@ -288,6 +288,37 @@ def test_device_engine_multiprocess(P, mode):
             assert "OK" in outs[r]
 
 
+@pytest.mark.parametrize("mode,knob", [("devsteps", "GLOO_AMD_FLAG_WRITE=store"),
+                                       ("twoshot", "GLOO_AMD_FLAG_WRITE=store"),
+                                       ("oneshot", "GLOO_AMD_FLAG_WRITE=store"),
+                                       ("devsteps", "GLOO_AMD_FUSE=0")])
+def test_device_engine_variants(mode, knob):
+    """The device engines' other forms, same checks as above at P=3: flag
+    words written with system-scope stores (what ranks use when the link to a
+    peer's GPU carries no atomics, Context::flagStores), and the plan kernel
+    without reduce-and-forward fusion (one landing slot per channel)."""
+    k, v = knob.split("=")
+    P = 3
+    with tempfile.TemporaryDirectory() as d:
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        env[k] = v
+        procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), mode],
+                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                 for r in range(P)]
+        outs = []
+        for p in procs:
+            try:
+                o, _ = p.communicate(timeout=240)
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+            outs.append(o.decode(errors="replace"))
+        for r, p in enumerate(procs):
+            assert p.returncode == 0, "rank %d failed:\n%s" % (r, outs[r])
+            assert "OK" in outs[r]
+
+
 @pytest.mark.parametrize("P", [2, 4])
 def test_algorithm_churn_multiprocess(P):
     """36 algorithms created, run twice and destroyed back to back per rank
