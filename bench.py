@@ -330,8 +330,9 @@ TRANSPORT = {}  # bench name -> the algorithm's transport_stats() after its time
 
 def plan_name(algo):
     """Schedule name of a bench candidate for gloo_amd.plan()."""
-    if algo.endswith("_host"):
-        algo = algo[:-len("_host")]
+    for suffix in ("_host", "_queued"):
+        if algo.endswith(suffix):
+            algo = algo[:-len(suffix)]
     return {"ring_chunked_mesh_steps": "ring_chunked_mesh",
             "ring_chunked_repl": "ring_chunked_repl"}.get(algo, algo)
 
@@ -341,10 +342,13 @@ def make_alg(gloo_amd, ctx, buf, algo):
     halving_doubling run their step programs in the plan kernel (devsteps) at
     every size up to 4 ranks, ring_chunked_mesh on the two-shot kernel, ring_chunked_repl on
     the one-shot kernel.  *_host and ring_chunked_mesh_steps are the same
-    schedules with host-issued steps (calibrated peer-copy transport)."""
+    schedules with host-issued steps (calibrated peer-copy transport), *_queued
+    the same steps enqueued at once with stream-ordered waits on peers."""
     engine = None
     if algo.endswith("_host"):
         engine, algo = "host", algo[:-len("_host")]
+    elif algo.endswith("_queued"):
+        engine, algo = "queued", algo[:-len("_queued")]
     elif algo in ("ring_chunked", "halving_doubling"):
         engine = "device"  # the plan kernel (the step program in one kernel per rank)
     if engine is not None:
@@ -352,8 +356,8 @@ def make_alg(gloo_amd, ctx, buf, algo):
     try:
         if algo == "halving_doubling":
             return gloo_amd.AllreduceHalvingDoubling(ctx, [buf])
-        if algo == "ring_chunked_mesh_steps":
-            gloo_amd.set_mesh_engine("steps")
+        if algo == "ring_chunked_mesh_steps" or (algo == "ring_chunked_mesh" and engine):
+            gloo_amd.set_mesh_engine("steps" if engine != "queued" else "queued")
             try:
                 return gloo_amd.AllreduceRingChunked(ctx, [buf], schedule="mesh")
             finally:
@@ -440,8 +444,9 @@ SWEEP_ELEMS = [1 << 10, 1 << 12, 1 << 14, 1 << 16, 1 << 18, 1 << 20, 1 << 22, 1 
 
 
 def probe_device_engines(torch, dist, gloo_amd, ctx, dev, dtype):
-    """Before timing them, check the device-driven engines (one-shot and
-    two-shot kernels) on this machine: short timeout, results bit-identical to
+    """Before timing them, check the device-driven engines (one-shot,
+    two-shot and plan kernels, and the queued steps engine's stream-ordered
+    waits) on this machine: short timeout, results bit-identical to
     the host-issued steps engine over three refilled runs.  If any rank fails,
     every rank turns them off for the rest of the run (the host-issued
     schedules remain) and the JSON says why."""
@@ -449,7 +454,8 @@ def probe_device_engines(torch, dist, gloo_amd, ctx, dev, dtype):
     ctx.setTimeout(15)
     try:
         for algo, n in (("ring_chunked_repl", 65536 + 3), ("ring_chunked_mesh", (1 << 20) + 5),
-                        ("ring_chunked", 1 << 20), ("halving_doubling", 1 << 20)):
+                        ("ring_chunked", 1 << 20), ("halving_doubling", 1 << 20),
+                        ("ring_chunked_queued", (1 << 20) + 3)):
             x = synthetic(torch, n, dtype, dev, 99 + int(os.environ.get("RANK", "0")))
             ref = x.clone()
             torch.cuda.synchronize()  # run() does not order itself after torch's stream
@@ -552,7 +558,8 @@ def bench_multi(args):
     def tuned(algo):
         calib = {}
         probe = make_alg(gloo_amd, ctx, buf, algo)
-        device_engine = probe.engine() != "steps"  # no peer-copy transport to tune
+        # no peer-copy transport to tune for the kernels that store themselves
+        device_engine = probe.engine() not in ("steps", "queued")
         probe.close()
         if args.copy_split == "auto" and not device_engine:
             for tr in TRANSPORTS:
@@ -577,7 +584,8 @@ def bench_multi(args):
         result = buf.clone()
         return {"t": t, "sent": sent,
                 "transport": ("device-driven kernel stores (%s)" % ENGINES[algo]
-                              if device_engine else tname(best)), "tr": best,
+                              if device_engine else tname(best) +
+                              (" (queued)" if ENGINES[algo] == "queued" else "")), "tr": best,
                 "calib_ms": {tname(k): round(v * 1e3, 3) for k, v in calib.items()},
                 "result": result}
 
@@ -585,10 +593,10 @@ def bench_multi(args):
         return int(t.view(torch.int16 if es == 2 else torch.int32).to(torch.int64).sum().item())
 
     if args.algo == "ring_chunked" and args.schedule == "auto":
-        candidates = ["ring_chunked", "ring_chunked_host", "ring_chunked_mesh",
-                      "ring_chunked_mesh_steps"]
+        candidates = ["ring_chunked", "ring_chunked_host", "ring_chunked_queued",
+                      "ring_chunked_mesh", "ring_chunked_mesh_steps", "ring_chunked_mesh_queued"]
     elif args.algo == "ring_chunked" and args.schedule == "mesh":
-        candidates = ["ring_chunked_mesh", "ring_chunked_mesh_steps"]
+        candidates = ["ring_chunked_mesh", "ring_chunked_mesh_steps", "ring_chunked_mesh_queued"]
     else:
         candidates = [args.algo]
     # A candidate that fails on any rank (a timeout, a HIP error) is dropped
@@ -642,7 +650,7 @@ def bench_multi(args):
                    "busiest_link_GBps": round(lm / runs[a]["t"] / 1e9, 2)}
     if not args.no_alt:
         for other in ("ring_chunked", "ring_chunked_mesh", "halving_doubling",
-                      "halving_doubling_host"):
+                      "halving_doubling_host", "halving_doubling_queued"):
             if other in runs:
                 continue
             buf.copy_(src)
@@ -664,7 +672,7 @@ def bench_multi(args):
     if args.staged:
         # host buffers: the fastest host-issued schedule (its H2D / D2H
         # overlap the steps); the device engines stage the whole buffer first
-        host_cands = [a for a in candidates if ENGINES.get(a) == "steps"] or [chosen]
+        host_cands = [a for a in candidates if ENGINES.get(a) in ("steps", "queued")] or [chosen]
         staged_algo = min(host_cands, key=lambda a: runs[a]["t"])
         staged, err = attempt("host-staged", lambda: host_endpoint_rate(
             torch, dist, gloo_amd, ctx, src, dev_result, staged_algo, reps=min(steps, 5)))
@@ -695,17 +703,15 @@ def bench_multi(args):
             "config": {"workload": "allreduce_%s_%s_%dMiB_per_rank" % (
                            args.algo, {"f32": "fp32"}.get(args.dtype, args.dtype), args.size_mib),
                        "algorithm": args.algo,
-                       "schedule": {"ring_chunked": "ring", "ring_chunked_host": "ring",
-                                    "ring_chunked_mesh": "mesh",
-                                    "ring_chunked_mesh_steps": "mesh",
-                                    "halving_doubling": "halving_doubling",
-                                    "halving_doubling_host": "halving_doubling"}[chosen],
+                       "schedule": {"ring_chunked": "ring", "ring_chunked_mesh": "mesh",
+                                    "halving_doubling": "halving_doubling"}[plan_name(chosen)],
                        "engine": ENGINES.get(chosen),
                        "schedule_note": "ring_chunked's chunking and reduction order; ring = "
                                         "the reference's data movement, mesh = all links "
                                         "(bit-identical, checked); engine: devsteps = the "
                                         "step program in one kernel, twoshot = the mesh in "
-                                        "one kernel, steps = host-issued",
+                                        "one kernel, steps = host-issued, queued = host-issued "
+                                        "at once with stream-ordered waits on peers",
                        "bytes_per_rank": S, "elements": n,
                        "parallelism": "dp%d" % world,
                        "transport": "xGMI peer copies: " + runs[chosen]["transport"],

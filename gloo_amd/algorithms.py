@@ -197,11 +197,12 @@ class Algorithm:
     def engine(self):
         """"steps" (host-issued schedule steps), "oneshot" (the replicated
         schedule as one device-driven kernel per rank), "twoshot" (the mesh
-        schedule as one device-driven kernel per rank) or "devsteps" (any
+        schedule as one device-driven kernel per rank), "devsteps" (any
         other schedule's step program walked by one device-driven kernel per
-        rank)."""
-        return {0: "steps", 1: "oneshot", 2: "twoshot",
-                3: "devsteps"}[lib.glx_algorithm_engine(self._h)]
+        rank) or "queued" (the host-issued steps enqueued at once, waits on
+        peers stream-ordered on device flags)."""
+        return {0: "steps", 1: "oneshot", 2: "twoshot", 3: "devsteps",
+                4: "queued"}[lib.glx_algorithm_engine(self._h)]
 
     def transport_stats(self):
         """How this algorithm's messages moved since it was created:

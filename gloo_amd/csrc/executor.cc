@@ -263,15 +263,31 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
   if (engine_ == kEngineOneShot || engine_ == kEngineTwoShot) {
     setupDevice();
   } else {
-    // the plan kernel's peers store into it: uncached, `slots_` copies
-    allocScratch(engine_ == kEngineDevSteps, engine_ == kEngineDevSteps ? slots_ : 1);
+    // Receive regions are written by a peer's copies (DMA or the peer's
+    // compute units over xGMI) behind this GPU's L2 and then read by our
+    // kernels with no cache maintenance of ours in between, and a region is
+    // reused every run: uncached, so no stale line of the last message can
+    // be read (the device engines' rule, and RCCL's for its receive buffers).
+    // The plan kernel keeps `slots_` copies.  Measured free for the host-issued
+    // engine (8 ranks on one GPU, 256 MiB: ring 9.19 vs 9.89 ms, mesh 3.74 vs
+    // 3.89 ms; profiles/r2q_*); GLOO_AMD_STEPS_SCRATCH=cached restores
+    // hipMalloc'd regions for it.
+    static const bool stepsUncached = [] {
+      const char* e = std::getenv("GLOO_AMD_STEPS_SCRATCH");
+      return !(e != nullptr && std::strcmp(e, "cached") == 0);
+    }();
+    allocScratch(engine_ == kEngineDevSteps || engine_ == kEngineQueued || stepsUncached,
+                 engine_ == kEngineDevSteps ? slots_ : 1);
   }
 
   // Channels named by the plan; allocate our counter words.
   auto& ctl = ctx->localControl();
   stepChan_.assign(plan_.steps.size(), -1);
   const bool hostSteps = engine_ == kEngineSteps;
-  for (size_t i = 0; i < plan_.steps.size() && (hostSteps || engine_ == kEngineDevSteps); i++) {
+  const bool copyStreams = hostSteps || engine_ == kEngineQueued;
+  for (size_t i = 0; i < plan_.steps.size() &&
+                     (copyStreams || engine_ == kEngineDevSteps);
+       i++) {
     const auto& s = plan_.steps[i];
     if (s.kind == glx::SEND) {
       int idx = outIndex((int)s.peer, (int)s.channel);
@@ -279,15 +295,16 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
         OutChan oc;
         oc.peer = (int)s.peer;
         oc.tag = (int)s.channel;
-        // plan kernel: no control-block words or copy streams (flag rows
-        // are assigned in setupDevSteps)
+        // plan kernel: no control-block words or copy streams; queued: copy
+        // streams, no words (flag rows are assigned in setupDevSteps /
+        // setupQueued)
         oc.creditWord = hostSteps ? ctl.allocWord() : 0;
         oc.credit = hostSteps ? ctl.word(oc.creditWord) : nullptr;
         // one copy stream per destination peer: copies to different peers
         // run concurrently on different xGMI links
-        oc.stream = hostSteps ? -1 : 0;
+        oc.stream = copyStreams ? -1 : 0;
         for (const auto& o : out_) {
-          if (hostSteps && o.peer == oc.peer) oc.stream = o.stream;
+          if (copyStreams && o.peer == oc.peer) oc.stream = o.stream;
         }
         if (oc.stream < 0) {
           oc.stream = (int)copies_.size();
@@ -315,7 +332,7 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
       stepChan_[i] = idx;
     }
   }
-  if (engine_ == kEngineDevSteps) setupDevice();
+  if (engine_ == kEngineDevSteps || engine_ == kEngineQueued) setupDevice();
   events_.resize(plan_.steps.size() * (size_t)split_, nullptr);
   for (auto& e : events_) GLX_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   GLX_HIP_CHECK(hipEventCreateWithFlags(&computeMark_, hipEventDisableTiming));
@@ -362,6 +379,21 @@ void HipPlanExecutor::drainCredits() noexcept {
           for (size_t w = 0; w < G && done; w++) done = row[w * glx::kFlagStride] >= want[c];
           if (done || std::chrono::steady_clock::now() >= deadline) break;
           context_->checkPeersAlive();  // throws if a peer exited: stop waiting
+          pause();
+        }
+      }
+    }
+    if (engine_ == kEngineQueued && !ddBlocks_.empty()) {
+      for (const auto& oc : out_) {
+        for (;;) {
+          uint64_t v = 0;
+          if (hipMemcpy(&v, flagRow(oc.creditWord), sizeof(v), hipMemcpyDeviceToHost) !=
+              hipSuccess) {
+            (void)hipGetLastError();
+            break;
+          }
+          if (v >= oc.sent || std::chrono::steady_clock::now() >= deadline) break;
+          context_->checkPeersAlive();
           pause();
         }
       }
@@ -596,7 +628,7 @@ void HipPlanExecutor::resolvePeers() {
       }
     }
     if (engine_ != kEngineSteps) ddPeer_[r] = blocks;
-    if (engine_ == kEngineDevSteps) {  // the peer's flag rows for our channels
+    if (engine_ == kEngineDevSteps || engine_ == kEngineQueued) {  // the peer's flag rows
       GLX_ENFORCE(!blocks.empty(), "rank ", r, " published no flag rows");
       uint64_t* rows = reinterpret_cast<uint64_t*>(blocks[0]);
       const size_t G = (size_t)pk_.G;
@@ -612,7 +644,7 @@ void HipPlanExecutor::resolvePeers() {
       }
     }
   }
-  const bool dev = engine_ == kEngineDevSteps;
+  const bool dev = engine_ == kEngineDevSteps || engine_ == kEngineQueued;
   for (auto& oc : out_) {
     GLX_ENFORCE(dev ? oc.devDelivery != nullptr : oc.delivery != nullptr, "rank ", oc.peer,
                 " has no receive channel ", oc.tag, " from rank ", contextRank_,
@@ -1303,6 +1335,10 @@ void HipPlanExecutor::recordDone(hipEvent_t ev) {
 }
 
 void HipPlanExecutor::exchange(char* ptr0) {
+  if (engine_ == kEngineQueued) {
+    exchangeQueued(ptr0);
+    return;
+  }
   if (engine_ != kEngineSteps) {
     runDevice(ptr0);
     return;
@@ -1508,8 +1544,9 @@ namespace {
 
 int initialMeshEngine() {
   const char* e = std::getenv("GLOO_AMD_MESH_ENGINE");
-  return (e != nullptr && std::strcmp(e, "steps") == 0) ? HipPlanExecutor::kEngineSteps
-                                                        : HipPlanExecutor::kEngineTwoShot;
+  if (e != nullptr && std::strcmp(e, "steps") == 0) return HipPlanExecutor::kEngineSteps;
+  if (e != nullptr && std::strcmp(e, "queued") == 0) return HipPlanExecutor::kEngineQueued;
+  return HipPlanExecutor::kEngineTwoShot;
 }
 
 std::atomic<int> g_mesh_engine{initialMeshEngine()};
@@ -1521,6 +1558,7 @@ int initialStepsEngine() {
   const char* e = std::getenv("GLOO_AMD_STEPS_ENGINE");
   if (e != nullptr && std::strcmp(e, "host") == 0) return HipPlanExecutor::kEngineSteps;
   if (e != nullptr && std::strcmp(e, "device") == 0) return HipPlanExecutor::kEngineDevSteps;
+  if (e != nullptr && std::strcmp(e, "queued") == 0) return HipPlanExecutor::kEngineQueued;
   return -1;
 }
 
@@ -1534,13 +1572,17 @@ std::atomic<int> g_steps_engine{initialStepsEngine()};
 }  // namespace
 
 void HipPlanExecutor::setMeshEngine(int engine) {
-  g_mesh_engine.store(engine == kEngineSteps ? kEngineSteps : kEngineTwoShot);
+  g_mesh_engine.store(engine == kEngineSteps || engine == kEngineQueued ? engine
+                                                                       : kEngineTwoShot);
 }
 
 int HipPlanExecutor::meshEngine() { return g_mesh_engine.load(); }
 
 void HipPlanExecutor::setStepsEngine(int engine) {
-  g_steps_engine.store(engine < 0 ? -1 : (engine == kEngineSteps ? kEngineSteps : kEngineDevSteps));
+  g_steps_engine.store(engine < 0 ? -1
+                                  : (engine == kEngineSteps || engine == kEngineQueued
+                                         ? engine
+                                         : kEngineDevSteps));
 }
 
 int HipPlanExecutor::stepsEngine() { return g_steps_engine.load(); }
@@ -1612,6 +1654,8 @@ void HipPlanExecutor::setupDevice() {
     setupOneShot();
   } else if (engine_ == kEngineTwoShot) {
     setupTwoShot();
+  } else if (engine_ == kEngineQueued) {
+    setupQueued();
   } else {
     setupDevSteps();
   }
@@ -2067,6 +2111,227 @@ void HipPlanExecutor::runDevice(char* ptr0) {
     GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, ddDone_, 0));
     copyBack({glx::Range{0, count_}});
   }
+}
+
+// ---------------------------------------------------------------------------
+// Queued steps engine
+// ---------------------------------------------------------------------------
+
+// Flag rows (one flag per 128-B line, the plan kernel's layout with G = 1):
+// [in_.size()] delivery flags, [out_.size()] credit flags, then one local copy
+// counter per out-channel (never published).
+void HipPlanExecutor::setupQueued() {
+  pk_.G = 1;
+  for (size_t k = 0; k < in_.size(); k++) in_[k].deliveryWord = (uint32_t)k;
+  for (size_t k = 0; k < out_.size(); k++) out_[k].creditWord = (uint32_t)(in_.size() + k);
+  const size_t rows = std::max<size_t>(1, in_.size() + 2 * out_.size());
+  ddAlloc(rows * glx::kFlagBytes);
+  for (size_t k = 0; k < out_.size(); k++) {
+    out_[k].devCounter = flagRow((uint32_t)(in_.size() + out_.size() + k));
+  }
+}
+
+uint64_t* HipPlanExecutor::flagRow(uint32_t row) const {
+  return reinterpret_cast<uint64_t*>(ddBlocks_.at(0)) + (size_t)row * glx::kFlagStride;
+}
+
+// The host engine's loop (exchange) with its two blocking waits and its
+// completion polling replaced by launches: a SEND's credit wait is a
+// flag_wait on its copy stream(s), the delivery that ends it a flag_put after
+// its copies (or the copy kernel's own last workgroup); a RECV is a flag_wait
+// on the compute stream, a RELEASE a flag_put after the reduce that read the
+// region.  The streams carry the program order the host loop used to
+// enforce, so the same deadlock-freedom holds: each wait blocks only work
+// issued after it in that order, and every signal is issued before any later
+// wait of its stream.  Message numbers are cumulative over runs (out_.sent,
+// in_.received / consumed), so no device state needs resetting.
+void HipPlanExecutor::exchangeQueued(char* ptr0) {
+  if (!resolved_) resolvePeers();
+  checkDevice();  // an earlier asynchronous call that timed out
+  devRuns_++;
+  const uint64_t ticks = (uint64_t)effectiveTimeout().count() * (uint64_t)clockKhz_;
+  const int store = context_->flagStores() ? 1 : 0;
+  auto code = [&](size_t step, int peer) { return 1 + peer + 256 * (1 + (int)step); };
+  bool computeSinceMark = true;  // the caller's writes to ptr0 count as compute
+  for (auto& c : copies_) c.last = nullptr;
+  const auto& steps = plan_.steps;
+  for (size_t i = 0; i < steps.size(); i++) {
+    const glx::Step& s = steps[i];
+    switch (s.kind) {
+      case glx::SEND: {
+        OutChan& oc = out_[stepChan_[i]];
+        const uint64_t n = ++oc.sent;
+        const size_t nbytes = (size_t)s.len * esize_;
+        CopyStream& c0 = copies_[oc.stream];
+        // message n may land once the receiver has consumed message n-1
+        auto creditWait = [&](hipStream_t st) {
+          if (n > 1) {
+            GLX_HIP_CHECK(glx::launch_flag_wait(flagRow(oc.creditWord), n - 1, ticks,
+                                                ddStatusDev_, ddClaim_, code(i, oc.peer), st));
+          }
+        };
+        if (nbytes == 0) {
+          creditWait(c0.s);
+          GLX_HIP_CHECK(glx::launch_flag_put(oc.devDelivery, n, store, c0.s));
+          break;
+        }
+        if (computeSinceMark) {
+          GLX_HIP_CHECK(hipEventRecord(computeMark_, compute_));
+          markEpoch_++;
+          computeSinceMark = false;
+        }
+        char* dst = landing(peerBlocks_[oc.peer], s.dst_off, s.off);
+        const char* src = ptr0 + (size_t)s.off * esize_;
+        auto prepare = [&](CopyStream& cs) {
+          creditWait(cs.s);
+          if (cs.waitedMark != markEpoch_) {
+            GLX_HIP_CHECK(hipStreamWaitEvent(cs.s, computeMark_, 0));
+            cs.waitedMark = markEpoch_;
+          }
+          if (staged_) waitH2D(cs.s, cs.h2dWaited, s.off, s.len);
+        };
+        hipEvent_t done = events_[i * (size_t)split_];
+        if (copyEngine_ == kCopyKernel) {
+          prepare(c0);
+          const int blocks = std::max(1, glx::copy_blocks());
+          oc.counterTarget += (uint64_t)blocks;
+          GLX_HIP_CHECK(glx::launch_copy_signal(dst, src, nbytes, blocks, oc.devCounter,
+                                                oc.counterTarget, oc.devDelivery, n, store,
+                                                c0.s));
+          transport_.kernelCopies++;
+        } else {
+          int parts = split_;
+          while (parts > 1 && nbytes / (size_t)parts < kMinSplitBytes) parts--;
+          const size_t per = ((nbytes / (size_t)parts) + 255) & ~(size_t)255;
+          for (int j = 0; j < parts; j++) {
+            const size_t at = (size_t)j * per;
+            if (at >= nbytes) break;
+            const size_t len = std::min(per, nbytes - at);
+            CopyStream& cs = copies_[oc.stream + j];
+            prepare(cs);
+            hipError_t ce = hipErrorUnknown;
+            if (peerCopyOk_ && oc.peerDevice >= 0 && oc.peerDevice != device_) {
+              ce = hipMemcpyPeerAsync(dst + at, oc.peerDevice, src + at, device_, len, cs.s);
+              if (ce == hipSuccess) {
+                transport_.peerCopies++;
+              } else {
+                (void)hipGetLastError();
+                peerCopyOk_ = false;
+                std::fprintf(stderr,
+                             "[gloo_amd] rank %d: hipMemcpyPeerAsync to device %d refused "
+                             "(%s: %s); peer copies of this algorithm use hipMemcpyAsync\n",
+                             contextRank_, oc.peerDevice, hipGetErrorName(ce),
+                             hipGetErrorString(ce));
+              }
+            }
+            if (ce != hipSuccess) {
+              GLX_HIP_CHECK(hipMemcpyAsync(dst + at, src + at, len, hipMemcpyDeviceToDevice,
+                                           cs.s));
+              transport_.deviceCopies++;
+            }
+            if (j > 0) {  // part j done -> the delivery on part 0's stream waits for it
+              hipEvent_t ev = events_[i * (size_t)split_ + (size_t)j];
+              GLX_HIP_CHECK(hipEventRecord(ev, cs.s));
+              GLX_HIP_CHECK(hipStreamWaitEvent(c0.s, ev, 0));
+              cs.last = ev;
+            }
+          }
+          GLX_HIP_CHECK(glx::launch_flag_put(oc.devDelivery, n, store, c0.s));
+        }
+        transport_.bytes += (int64_t)nbytes;
+        GLX_HIP_CHECK(hipEventRecord(done, c0.s));
+        c0.last = done;
+        inflight_.push_back({s.off, s.len, done});
+        break;
+      }
+      case glx::RECV: {
+        InChan& ic = in_[stepChan_[i]];
+        const uint64_t n = ++ic.received;
+        GLX_HIP_CHECK(glx::launch_flag_wait(flagRow(ic.deliveryWord), n, ticks, ddStatusDev_,
+                                            ddClaim_, code(i, ic.peer), compute_));
+        break;
+      }
+      case glx::REDUCE:
+      case glx::COPY: {
+        waitWar(s.off, s.len);
+        if (staged_) waitH2D(compute_, computeH2dWaited_, s.off, s.len);
+        char* dst = ptr0 + (size_t)s.off * esize_;
+        const char* src = landing(blocks_, s.boff, s.off);
+        if (s.kind == glx::REDUCE) {
+          GLX_HIP_CHECK(
+              glx::launch_reduce(op_, dtype_, dst, dst, src, (size_t)s.len, compute_));
+        } else {
+          GLX_HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)s.len * esize_,
+                                       hipMemcpyDeviceToDevice, compute_));
+        }
+        computeSinceMark = true;
+        if (staged_ && !stage_.d2h[i].empty()) {  // final values: copy back now
+          GLX_HIP_CHECK(hipEventRecord(d2hEvents_[i], compute_));
+          GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, d2hEvents_[i], 0));
+          copyBack(stage_.d2h[i]);
+        }
+        break;
+      }
+      case glx::FOLD: {
+        size_t last = i;
+        while (last + 1 < steps.size() && steps[last + 1].kind == glx::FOLD &&
+               steps[last + 1].flags == s.flags) {
+          last++;
+        }
+        const bool rev = (s.flags & glx::kFoldLeft) == 0;
+        const bool whole = (s.flags & glx::kFoldWhole) != 0;
+        std::vector<glx::FoldSpec> specs;
+        for (size_t q = i; q <= last; q++) {
+          const glx::Step& f = steps[q];
+          waitWar(f.off, f.len);
+          if (staged_) waitH2D(compute_, computeH2dWaited_, f.off, f.len);
+          glx::FoldSpec spec;
+          spec.dst = ptr0 + (size_t)f.off * esize_;
+          spec.n = (size_t)f.len;
+          for (int64_t r : plan_.folds[(size_t)f.boff]) {
+            if (r < 0) {
+              spec.srcs.push_back(spec.dst);
+            } else if (whole) {
+              spec.srcs.push_back(landing(blocks_, r, 0) + (size_t)f.off * esize_);
+            } else {
+              spec.srcs.push_back(landing(blocks_, r, f.off));
+            }
+          }
+          spec.k = (int)spec.srcs.size();
+          specs.push_back(std::move(spec));
+        }
+        if (specs.size() == 1) {
+          const glx::FoldSpec& f = specs[0];
+          GLX_HIP_CHECK(glx::launch_reduce_n(op_, dtype_, f.dst, f.srcs.data(), f.k, f.n,
+                                             compute_, rev));
+        } else {
+          GLX_HIP_CHECK(glx::launch_reduce_n_batch(op_, dtype_, specs, compute_, rev));
+        }
+        computeSinceMark = true;
+        for (size_t q = i; q <= last; q++) {
+          if (staged_ && !stage_.d2h[q].empty()) {
+            GLX_HIP_CHECK(hipEventRecord(d2hEvents_[q], compute_));
+            GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, d2hEvents_[q], 0));
+            copyBack(stage_.d2h[q]);
+          }
+        }
+        i = last;
+        break;
+      }
+      case glx::RELEASE: {
+        InChan& ic = in_[stepChan_[i]];
+        GLX_HIP_CHECK(glx::launch_flag_put(ic.devCredit, ++ic.consumed, store, compute_));
+        break;
+      }
+      default:
+        GLX_ENFORCE(false, "bad plan step kind ", s.kind);
+    }
+  }
+  // the caller's stream must not run ahead of copies still reading ptr0
+  for (auto& c : copies_) {
+    if (c.last != nullptr) GLX_HIP_CHECK(hipStreamWaitEvent(compute_, c.last, 0));
+  }
+  inflight_.clear();
 }
 
 }  // namespace gloo

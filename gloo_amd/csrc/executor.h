@@ -126,7 +126,9 @@ class HipPlanExecutor : public Algorithm {
     int peerDevice = -1;
     int stream = 0;
     int peerRow = -1;                 // plan kernel: the receiver's delivery row
-    uint64_t* devDelivery = nullptr;  // plan kernel: that row (peer memory)     // index into copies_ (one copy stream per destination peer)
+    uint64_t* devDelivery = nullptr;  // plan kernel / queued: that row (peer memory)
+    uint64_t* devCounter = nullptr;   // queued: local count of copy-kernel workgroups done
+    uint64_t counterTarget = 0;       // queued: its value once the last copy launch is done
   };
   struct CopyStream {
     hipStream_t s = nullptr;
@@ -141,7 +143,7 @@ class HipPlanExecutor : public Algorithm {
     std::atomic<uint64_t>* credit = nullptr;  // in peer's block
     uint64_t received = 0, consumed = 0;
     int peerRow = -1;               // plan kernel: the sender's credit row
-    uint64_t* devCredit = nullptr;  // plan kernel: that row (peer memory)
+    uint64_t* devCredit = nullptr;  // plan kernel / queued: that row (peer memory)
   };
   static constexpr int kMaxSplit = 8;
   struct Pending {  // fire `value` into `word` once all `ev` (maybe none) complete
@@ -331,10 +333,17 @@ class HipPlanExecutor : public Algorithm {
   void buildDevSteps();
   void runDevice(char* ptr0);
   void checkDevice();
+  // Queued steps engine: the host-issued engine's step loop with every wait
+  // on a peer and every counter write as a stream-ordered launch on device
+  // flag rows (one flag each: deliveries, credits, then one local copy
+  // counter per out-channel), so the loop never blocks.
+  void setupQueued();
+  void exchangeQueued(char* ptr0);
+  uint64_t* flagRow(uint32_t row) const;
 
  public:
   static constexpr int kEngineSteps = 0, kEngineOneShot = 1, kEngineTwoShot = 2,
-                       kEngineDevSteps = 3;
+                       kEngineDevSteps = 3, kEngineQueued = 4;
   // Whether device-driven engines can run on this context: GLOO_AMD_ONESHOT
   // (0 = never, 1 = always), by default when no two ranks are threads sharing
   // one device (their kernels might not be co-resident).  P <= 8.
@@ -343,15 +352,15 @@ class HipPlanExecutor : public Algorithm {
   // (caller guarantees co-residency), -1 = automatic (the default).
   static void setDeviceEngines(int mode);
   // Engine of the mesh schedule when available: kEngineTwoShot (default,
-  // env GLOO_AMD_MESH_ENGINE=steps overrides) or kEngineSteps.  Read at
-  // construction.
+  // env GLOO_AMD_MESH_ENGINE=steps|queued overrides), kEngineSteps or
+  // kEngineQueued.  Read at construction.
   static void setMeshEngine(int engine);
   static int meshEngine();
   // Engine of the ring, halving-doubling, bcube and function-style ring
   // schedules when available: -1 = by size (default: the plan kernel up to
   // 32 MiB per rank, env GLOO_AMD_DEVSTEPS_MAX_BYTES; host-issued steps
-  // above), kEngineDevSteps or kEngineSteps (env GLOO_AMD_STEPS_ENGINE=
-  // device|host).
+  // above), kEngineDevSteps, kEngineSteps or kEngineQueued (env
+  // GLOO_AMD_STEPS_ENGINE=device|host|queued).
   static void setStepsEngine(int engine);
   static int stepsEngine();
 };

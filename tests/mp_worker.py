@@ -12,6 +12,8 @@ algo: ring_chunked | halving_doubling | ring_chunked_mesh (class algorithms)
       through the plan kernel: dtypes x ops x sizes, device and host buffers,
       repeated runs; prints per-op latencies of the plan kernel vs the
       host-issued steps)
+      queued | queued_kernel (the same through the queued steps engine, with
+      DMA or copy-kernel sends, plus the mesh schedule on it)
       devtimeout (rank 0 runs both device engines while the other ranks never
       call run(): its kernels must give up after the timeout and run() must
       raise IoException)
@@ -43,6 +45,10 @@ def main():
         return run_device_timeout(store_dir, rank, size)
     if algo == "devsteps":
         return run_devsteps(store_dir, rank, size)
+    if algo in ("queued", "queued_kernel"):
+        if algo == "queued_kernel":
+            gloo_amd.set_copy_engine("kernel", 128)
+        return run_devsteps(store_dir, rank, size, eng="queued")
     if algo == "churn":
         return run_churn(store_dir, rank, size)
     if algo.startswith("scale:"):
@@ -222,7 +228,7 @@ def run_churn(store_dir, rank, size):
     print("OK")
 
 
-def run_devsteps(store_dir, rank, size):
+def run_devsteps(store_dir, rank, size, eng="device"):
     import time
 
     import numpy as np
@@ -243,24 +249,32 @@ def run_devsteps(store_dir, rank, size):
         return np.array_equal(np.ascontiguousarray(got).view(np.uint8),
                               np.ascontiguousarray(exp).view(np.uint8))
 
+    label = "devsteps" if eng == "device" else eng
+    MESH = 100  # the mesh schedule (ring_chunked semantics)
+
     def make(kind, buf, op=O.SUM, dt=None):
         fn = gloo_amd.ReductionFunction(op)
         if kind == O.HALVING_DOUBLING:
             return gloo_amd.AllreduceHalvingDoubling(ctx, [buf], fn=fn, dtype=dt)
-        return gloo_amd.AllreduceRingChunked(ctx, [buf], fn=fn, schedule="ring", dtype=dt)
+        return gloo_amd.AllreduceRingChunked(ctx, [buf], fn=fn, dtype=dt,
+                                             schedule="mesh" if kind == MESH else "ring")
 
     cases = []
-    for kind in (O.RING_CHUNKED, O.HALVING_DOUBLING):
+    kinds = (O.RING_CHUNKED, O.HALVING_DOUBLING) + ((MESH,) if eng == "queued" else ())
+    for kind in kinds:
         for n in (1, 3, 255, 256, 1000, 4099, 65539, 1 << 20, (1 << 22) + 5):
             cases.append((kind, n, O.FLOAT32, O.SUM))
         for dt in (O.FLOAT16, O.BFLOAT16, O.INT32, O.FLOAT64, O.INT8, O.UINT64):
             for op in (O.SUM, O.PRODUCT, O.MAX, O.MIN):
                 cases.append((kind, 4099, dt, op))
-    gloo_amd.set_steps_engine("device")
+    gloo_amd.set_steps_engine(eng)
+    if eng == "queued":
+        gloo_amd.set_mesh_engine("queued")
     engines = set()
     for seed, (kind, n, dt, op) in enumerate(cases):
         ins = case_inputs(size, n, dt, 1, 0, seed=200 + seed)
-        exp = O.allreduce(kind, op, dt, ins)[rank][0]
+        # the mesh schedule computes ring_chunked's result (same chunks and chains)
+        exp = O.allreduce(O.RING_CHUNKED if kind == MESH else kind, op, dt, ins)[rank][0]
         buf = to_dev(ins[rank][0], dt)
         alg = make(kind, buf, op, dt)
         # the plan kernel, or host-issued steps where a landing region would
@@ -268,7 +282,7 @@ def run_devsteps(store_dir, rank, size):
         engines.add(alg.engine())
         print("case %d kind %d n %d dtype %d op %d engine %s" % (seed, kind, n, dt, op,
                                                                  alg.engine()), flush=True)
-        if alg.engine() not in ("devsteps", "steps"):
+        if alg.engine() not in (label, "steps"):
             bad.append(("engine", kind, n, alg.engine()))
         for it in range(3):
             buf.copy_(to_dev(ins[rank][0], dt))
@@ -277,8 +291,8 @@ def run_devsteps(store_dir, rank, size):
             if not same(from_dev(buf, dt), exp):
                 bad.append(("class", kind, n, dt, op, it))
         alg.close()
-    if "devsteps" not in engines:
-        bad.append(("engine", "the plan kernel never ran"))
+    if label not in engines:
+        bad.append(("engine", label, "never ran"))
     n = 65536  # host buffers: staged H2D, kernel, D2H
     ins = case_inputs(size, n, O.FLOAT32, 1, 0, seed=8)
     for kind in (O.RING_CHUNKED, O.HALVING_DOUBLING):
@@ -310,8 +324,8 @@ def run_devsteps(store_dir, rank, size):
     # latency: the plan kernel vs the host-issued steps (same bits)
     for kind, label in ((O.RING_CHUNKED, "ring"), (O.HALVING_DOUBLING, "hd")):
         for n in (1024, 65536, 1 << 20, 3 << 22):
-            for eng in ("device", "host"):
-                gloo_amd.set_steps_engine(eng)
+            for e in (eng, "host"):
+                gloo_amd.set_steps_engine(e)
                 buf = torch.zeros(n, device="cuda")
                 torch.cuda.synchronize()
                 alg = make(kind, buf)
@@ -326,6 +340,7 @@ def run_devsteps(store_dir, rank, size):
                       % (rank, size, label, n, alg.engine(), us), flush=True)
                 alg.close()
     gloo_amd.set_steps_engine("auto")
+    gloo_amd.set_mesh_engine("device")
     store.set("done/%d" % rank, b"1")
     for r in range(size):
         store.get("done/%d" % r, timeout_ms=60000)
