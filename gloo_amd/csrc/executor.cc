@@ -263,20 +263,20 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
   if (engine_ == kEngineOneShot || engine_ == kEngineTwoShot) {
     setupDevice();
   } else {
-    // Receive regions are written by a peer's copies (DMA or the peer's
-    // compute units over xGMI) behind this GPU's L2 and then read by our
-    // kernels with no cache maintenance of ours in between, and a region is
-    // reused every run: uncached, so no stale line of the last message can
-    // be read (the device engines' rule, and RCCL's for its receive buffers).
-    // The plan kernel keeps `slots_` copies.  Measured free for the host-issued
-    // engine (8 ranks on one GPU, 256 MiB: ring 9.19 vs 9.89 ms, mesh 3.74 vs
-    // 3.89 ms; profiles/r2q_*); GLOO_AMD_STEPS_SCRATCH=cached restores
-    // hipMalloc'd regions for it.
+    // The plan kernel reads its landing slots inside the launch, right after
+    // an in-kernel flag wait: nothing between a peer's stores and our loads
+    // drops stale L2 lines, so its slots are uncached (`slots_` copies).  The
+    // host-issued and queued engines read a region in a NEW dispatch after
+    // the wait, and they move bytes with hipMemcpyPeerAsync / hipMemcpyAsync
+    // by default: DMA copies into uncached memory were measured unsafe on
+    // this runtime (history-dependent wrong results), so their
+    // regions are plain hipMalloc memory.  GLOO_AMD_STEPS_SCRATCH=uncached
+    // makes them uncached too (safe with copy-kernel sends only).
     static const bool stepsUncached = [] {
       const char* e = std::getenv("GLOO_AMD_STEPS_SCRATCH");
-      return !(e != nullptr && std::strcmp(e, "cached") == 0);
+      return e != nullptr && std::strcmp(e, "uncached") == 0;
     }();
-    allocScratch(engine_ == kEngineDevSteps || engine_ == kEngineQueued || stepsUncached,
+    allocScratch(engine_ == kEngineDevSteps || stepsUncached,
                  engine_ == kEngineDevSteps ? slots_ : 1);
   }
 

@@ -108,14 +108,17 @@ __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* 
     }
   }
   const v4u* vs = reinterpret_cast<const v4u*>(src);
+  constexpr int U = MAXD <= 2 ? 4 : 2;  // vectors in flight per lane
   size_t i = va + threadIdx.x;
-  for (; i + kBlock < vb; i += 2 * kBlock) {
-    const v4u x0 = vs[i], x1 = vs[i + kBlock];
+  for (; i + (U - 1) * kBlock < vb; i += U * kBlock) {
+    v4u x[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) x[u] = vs[i + u * kBlock];
 #pragma unroll
     for (int d = 0; d < MAXD; d++) {
       if (d < n) {
-        reinterpret_cast<v4u*>(dsts[d])[i] = x0;
-        reinterpret_cast<v4u*>(dsts[d])[i + kBlock] = x1;
+#pragma unroll
+        for (int u = 0; u < U; u++) reinterpret_cast<v4u*>(dsts[d])[i + u * kBlock] = x[u];
       }
     }
   }
@@ -159,33 +162,39 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
       if (d < nout) reinterpret_cast<S*>(outs[d])[i] = acc;
     }
   }
-  // two vectors per lane, all 2P loads in flight before the chains (not for
-  // 1-byte types: 16 lanes of byte ops per vector already fill the registers)
+  // U vectors per lane, all U*P loads in flight before the chains: 4 for
+  // the 2-source folds (the ring's reduce-and-forward), 2 for wider ones
+  // (registers); none for 1-byte types (16 lanes of byte ops per vector
+  // already fill the registers)
+  constexpr int U = MAXK <= 2 ? 4 : 2;
   size_t v = va + threadIdx.x;
-  for (; sizeof(S) > 1 && v + kBlock < vb; v += 2 * kBlock) {
-    v4u y[MAXK], z[MAXK];
+  for (; sizeof(S) > 1 && v + (U - 1) * kBlock < vb; v += U * kBlock) {
+    v4u y[U][MAXK];
 #pragma unroll
-    for (int k = 0; k < MAXK; k++) {
-      if (k < P) {
-        y[k] = reinterpret_cast<const v4u*>(srcs[k])[v];
-        z[k] = reinterpret_cast<const v4u*>(srcs[k])[v + kBlock];
+    for (int u = 0; u < U; u++) {
+#pragma unroll
+      for (int k = 0; k < MAXK; k++) {
+        if (k < P) y[u][k] = reinterpret_cast<const v4u*>(srcs[k])[v + u * kBlock];
       }
     }
-    v4u acc = y[0], acc2 = z[0];
+    v4u acc[U];
 #pragma unroll
-    for (int k = 1; k < MAXK; k++) {
-      if (k < P) {
-        acc = LEFT ? vec_apply<T, OP>(acc, y[k]) : vec_apply<T, OP>(y[k], acc);
-        acc2 = LEFT ? vec_apply<T, OP>(acc2, z[k]) : vec_apply<T, OP>(z[k], acc2);
+    for (int u = 0; u < U; u++) {
+      acc[u] = y[u][0];
+#pragma unroll
+      for (int k = 1; k < MAXK; k++) {
+        if (k < P) {
+          acc[u] = LEFT ? vec_apply<T, OP>(acc[u], y[u][k]) : vec_apply<T, OP>(y[u][k], acc[u]);
+        }
       }
     }
-    reinterpret_cast<v4u*>(dst)[v] = acc;
-    reinterpret_cast<v4u*>(dst)[v + kBlock] = acc2;
+#pragma unroll
+    for (int u = 0; u < U; u++) reinterpret_cast<v4u*>(dst)[v + u * kBlock] = acc[u];
 #pragma unroll
     for (int d = 0; d < MAXK - 1; d++) {
       if (d < nout) {
-        reinterpret_cast<v4u*>(outs[d])[v] = acc;
-        reinterpret_cast<v4u*>(outs[d])[v + kBlock] = acc2;
+#pragma unroll
+        for (int u = 0; u < U; u++) reinterpret_cast<v4u*>(outs[d])[v + u * kBlock] = acc[u];
       }
     }
   }
