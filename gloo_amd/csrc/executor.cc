@@ -263,21 +263,25 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
   if (engine_ == kEngineOneShot || engine_ == kEngineTwoShot) {
     setupDevice();
   } else {
-    // The plan kernel reads its landing slots inside the launch, right after
-    // an in-kernel flag wait: nothing between a peer's stores and our loads
-    // drops stale L2 lines, so its slots are uncached (`slots_` copies).  The
-    // host-issued and queued engines read a region in a NEW dispatch after
-    // the wait, and they move bytes with hipMemcpyPeerAsync / hipMemcpyAsync
-    // by default: DMA copies into uncached memory were measured unsafe on
-    // this runtime (history-dependent wrong results), so their
-    // regions are plain hipMalloc memory.  GLOO_AMD_STEPS_SCRATCH=uncached
-    // makes them uncached too (safe with copy-kernel sends only).
-    static const bool stepsUncached = [] {
+    // Peers' stores into a receive region bypass this GPU's L2, so a region
+    // that compute units of a peer write (the plan kernel, copy-kernel sends)
+    // is uncached: no stale line of the previous message can be read (the
+    // plan kernel reads its slots inside the launch, `slots_` copies).  DMA
+    // sends (hipMemcpyPeerAsync / hipMemcpyAsync) keep hipMalloc'd regions:
+    // DMA copies into uncached memory were measured unsafe on this runtime
+    // (history-dependent wrong results), and the runtime's
+    // copies are ordered with our kernels by its own rules.  Every rank must
+    // use the same copy engine (the algorithm record carries it).
+    // GLOO_AMD_STEPS_SCRATCH=cached|uncached overrides (diagnostics).
+    static const int stepsScratch = [] {
       const char* e = std::getenv("GLOO_AMD_STEPS_SCRATCH");
-      return e != nullptr && std::strcmp(e, "uncached") == 0;
+      if (e != nullptr && std::strcmp(e, "uncached") == 0) return 1;
+      if (e != nullptr && std::strcmp(e, "cached") == 0) return 0;
+      return -1;
     }();
-    allocScratch(engine_ == kEngineDevSteps || stepsUncached,
-                 engine_ == kEngineDevSteps ? slots_ : 1);
+    const bool uncached = engine_ == kEngineDevSteps ||
+                          (stepsScratch < 0 ? copyEngine_ == kCopyKernel : stepsScratch == 1);
+    allocScratch(uncached, engine_ == kEngineDevSteps ? slots_ : 1);
   }
 
   // Channels named by the plan; allocate our counter words.
@@ -502,6 +506,7 @@ void HipPlanExecutor::publish() {
   }
   putPod<int32_t>(b, engine_);
   putPod<int32_t>(b, (int32_t)slots_);
+  putPod<int32_t>(b, (int32_t)copyEngine_);
   putPod<int32_t>(b, (int32_t)ddBlocks_.size());
   for (size_t k = 0; k < ddBlocks_.size(); k++) putRef(b, ddRefs_[k]);
   const std::vector<int64_t> retired = context_->retiredShared();
@@ -531,6 +536,7 @@ std::vector<int64_t> HipPlanExecutor::retiredIn(const std::vector<char>& rec) co
   at += (size_t)nchan * 4 * sizeof(int32_t);
   getPod<int32_t>(rec, at);  // engine
   getPod<int32_t>(rec, at);  // slots
+  getPod<int32_t>(rec, at);  // copy engine
   const int32_t nb = getPod<int32_t>(rec, at);
   for (int32_t k = 0; k < nb; k++) getRef(rec, at);
   const int32_t n = getPod<int32_t>(rec, at);
@@ -617,6 +623,12 @@ void HipPlanExecutor::resolvePeers() {
     GLX_ENFORCE(engine_ != kEngineDevSteps || peerSlots == slots_, "rank ", r, " keeps ",
                 peerSlots, " landing slot(s) per channel, rank ", contextRank_, " ", slots_,
                 " (GLOO_AMD_FUSE must be the same on every rank)");
+    const int32_t peerCopy = getPod<int32_t>(b, at);
+    GLX_ENFORCE(!(engine_ == kEngineSteps || engine_ == kEngineQueued) ||
+                    peerCopy == copyEngine_,
+                "rank ", r, " sends with copy engine ", peerCopy, ", rank ", contextRank_,
+                " with ", copyEngine_, " (set_copy_engine must be the same on every rank: "
+                "it decides what memory the receive regions are)");
     const int32_t nb = getPod<int32_t>(b, at);
     std::vector<char*> blocks;
     for (int32_t k = 0; k < nb; k++) {
