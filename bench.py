@@ -41,8 +41,13 @@ def parse():
                    help="N>1, ring_chunked: data movement (bit-identical results); 'auto' "
                         "times both and reports the faster as value, the other beside it")
     p.add_argument("--copy-split", default="auto",
-                   help="N>1: peer-copy transport: 'auto' (short calibration over DMA with "
-                        "1/2/4 streams per copy and the xGMI copy kernel) or a DMA split 1/2/4")
+                   help="N>1: peer-copy transport: 'auto' (short calibration over the xGMI "
+                        "copy kernel at 32/64/128/256 workgroups, plus DMA with --dma) or a "
+                        "fixed DMA split 1/2/4")
+    p.add_argument("--dma", action="store_true",
+                   help="N>1: also calibrate hipMemcpyPeerAsync (1/2/4 streams per copy): "
+                        "opt-in, its cached receive regions rely on the runtime for "
+                        "coherence (DESIGN.md 5c)")
     p.add_argument("--no-alt", action="store_true",
                    help="N>1: do not also time the other schedules")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -326,6 +331,7 @@ RING_SCHEDULES = {"ring_chunked": "ring", "ring_chunked_mesh": "mesh",
                   "ring_chunked_auto": "auto"}
 ENGINES = {}  # bench name -> engine the product chose (steps/oneshot/twoshot/devsteps)
 TRANSPORT = {}  # bench name -> the algorithm's transport_stats() after its timed runs
+CHECKS = {}  # bench name -> result_check() of its post-timing run
 
 
 def plan_name(algo):
@@ -440,6 +446,28 @@ def host_endpoint_rate(torch, dist, gloo_amd, ctx, src, dev_result, algo, reps):
                     "overlapped with the schedule, per-range D2H after final writes"}
 
 
+def result_check(torch, dist, src, result):
+    """Independent check of an allreduce result against the inputs (no
+    oracle run at this size): with a fixed pseudo-random weight vector w,
+    sum_i w_i * result_i must equal sum over ranks of sum_i w_i * src_i
+    (each rank's term in float64, summed over ranks).  Tolerance: the
+    element type's rounding of the allreduce (fp32 1e-6, 16-bit 4e-3) times
+    sum_i |w_i * result_i|.  A chunk of stale or missing data moves the sum by
+    ~sqrt(chunk) while the tolerance grows ~chunk/1e6: it cannot pass.
+    Returns (ok, relative error)."""
+    n = src.numel()
+    g = torch.Generator(device=src.device).manual_seed(4242)
+    w = torch.rand(n, device=src.device, generator=g, dtype=torch.float32) * 2 - 1
+    mine = torch.tensor([float((w.double() * src.double()).sum().item())], dtype=torch.float64)
+    dist.all_reduce(mine)
+    rw = w.double() * result.double()
+    got = float(rw.sum().item())
+    scale = float(rw.abs().sum().item()) or 1.0
+    tol = (1e-6 if result.element_size() >= 4 else 4e-3) * scale
+    err = abs(got - float(mine.item()))
+    return err <= tol, err / scale
+
+
 SWEEP_ELEMS = [1 << 10, 1 << 12, 1 << 14, 1 << 16, 1 << 18, 1 << 20, 1 << 22, 1 << 24]
 
 
@@ -544,8 +572,10 @@ def bench_multi(args):
     # Transport calibration: peer copies by the DMA engines split over 1/2/4
     # streams, or by the xGMI copy kernel (32/128 workgroups); a few runs
     # each, max over ranks (every rank sees the same times and picks alike).
-    TRANSPORTS = [("dma", 1, 0), ("dma", 2, 0), ("dma", 4, 0), ("kernel", 1, 32),
-                  ("kernel", 1, 128)]
+    TRANSPORTS = [("kernel", 1, 32), ("kernel", 1, 64), ("kernel", 1, 128),
+                  ("kernel", 1, 256)]
+    if args.dma:
+        TRANSPORTS += [("dma", 1, 0), ("dma", 2, 0), ("dma", 4, 0)]
 
     def set_transport(tr):
         eng, k, blocks = tr
@@ -567,8 +597,10 @@ def bench_multi(args):
                 buf.copy_(src)
                 calib[tr], _ = time_schedule(torch, dist, gloo_amd, ctx, buf, algo, 3, 1)
             best = min(calib, key=lambda k: calib[k])
+        elif args.copy_split == "auto":
+            best = ("kernel", 1, 64)
         else:
-            best = ("dma", 1 if args.copy_split == "auto" else int(args.copy_split), 0)
+            best = ("dma", int(args.copy_split), 0)
         set_transport(best)
         buf.copy_(src)
         torch.cuda.synchronize()
@@ -617,10 +649,16 @@ def bench_multi(args):
     runs, failed = {}, {}
     for a in candidates:
         r, err = attempt(a, lambda: tuned(a))
-        if agreed(err is None):
+        if not agreed(err is None):
+            failed[a] = err or "failed on another rank"
+            continue
+        # every rank is here: the collective check of the result
+        ok, rel = result_check(torch, dist, src, r["result"])
+        CHECKS[a] = {"ok": ok, "rel_err": rel}
+        if agreed(ok):
             runs[a] = r
         else:
-            failed[a] = err or "failed on another rank"
+            failed[a] = "result check failed (weighted sum off by %.3g of its scale)" % rel
     if not runs:
         raise RuntimeError("every candidate failed: %s" % failed)
     candidates = [a for a in candidates if a in runs]
@@ -734,6 +772,7 @@ def bench_multi(args):
                                  "note": "one rank's HBM bytes per step from the step "
                                          "program (bench.plan_hbm_bytes) / ms_per_step"}},
             "transport_stats": {a: TRANSPORT.get(a) for a in runs},
+            "result_checks": CHECKS,
             "alt_schedules": alts,
             "device_engines": device_engines,
             "sweep": sweep,

@@ -73,9 +73,15 @@ int initialSplit() {
 
 std::atomic<int> g_copy_split{initialSplit()};
 
+// Default: the copy kernel (stores from the sending GPU's compute units into
+// the receiver's uncached region).  DMA (hipMemcpyPeerAsync) is opt-in,
+// GLOO_AMD_COPY_ENGINE=dma: its regions must be cached memory, read by a
+// kernel whose only ordering after the copy is our host handshake, and that
+// combination gave an intermittent wrong result in the GPU suite (DESIGN.md
+// 5c); the copy kernel + uncached regions never did.
 int initialEngine() {
   const char* e = std::getenv("GLOO_AMD_COPY_ENGINE");
-  return (e != nullptr && std::strcmp(e, "kernel") == 0) ? 1 : 0;
+  return (e != nullptr && std::strcmp(e, "dma") == 0) ? 0 : 1;
 }
 
 std::atomic<int> g_copy_engine{initialEngine()};
