@@ -46,8 +46,8 @@ def parse():
                         "fixed DMA split 1/2/4")
     p.add_argument("--dma", action="store_true",
                    help="N>1: also calibrate hipMemcpyPeerAsync (1/2/4 streams per copy): "
-                        "opt-in, its cached receive regions rely on the runtime for "
-                        "coherence (DESIGN.md 5c)")
+                        "opt-in, it gave one intermittent wrong result in the GPU suite "
+                        "(DESIGN.md 5c)")
     p.add_argument("--no-alt", action="store_true",
                    help="N>1: do not also time the other schedules")
     p.add_argument("--no-cpu-baseline", action="store_true")

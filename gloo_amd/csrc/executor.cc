@@ -74,11 +74,9 @@ int initialSplit() {
 std::atomic<int> g_copy_split{initialSplit()};
 
 // Default: the copy kernel (stores from the sending GPU's compute units into
-// the receiver's uncached region).  DMA (hipMemcpyPeerAsync) is opt-in,
-// GLOO_AMD_COPY_ENGINE=dma: its regions must be cached memory, read by a
-// kernel whose only ordering after the copy is our host handshake, and that
-// combination gave an intermittent wrong result in the GPU suite (DESIGN.md
-// 5c); the copy kernel + uncached regions never did.
+// the receiver's region over xGMI).  DMA (hipMemcpyPeerAsync) is opt-in,
+// GLOO_AMD_COPY_ENGINE=dma: it gave an intermittent wrong result in the GPU
+// suite, the copy kernel never did.
 int initialEngine() {
   const char* e = std::getenv("GLOO_AMD_COPY_ENGINE");
   return (e != nullptr && std::strcmp(e, "dma") == 0) ? 0 : 1;
@@ -269,24 +267,20 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
   if (engine_ == kEngineOneShot || engine_ == kEngineTwoShot) {
     setupDevice();
   } else {
-    // Peers' stores into a receive region bypass this GPU's L2, so a region
-    // that compute units of a peer write (the plan kernel, copy-kernel sends)
-    // is uncached: no stale line of the previous message can be read (the
-    // plan kernel reads its slots inside the launch, `slots_` copies).  DMA
-    // sends (hipMemcpyPeerAsync / hipMemcpyAsync) keep hipMalloc'd regions:
-    // DMA copies into uncached memory were measured unsafe on this runtime
-    // (history-dependent wrong results), and the runtime's
-    // copies are ordered with our kernels by its own rules.  Every rank must
-    // use the same copy engine (the algorithm record carries it).
-    // GLOO_AMD_STEPS_SCRATCH=cached|uncached overrides (diagnostics).
+    // The plan kernel reads its landing slots inside the launch, right after
+    // an in-kernel flag wait: no dispatch boundary (whose acquire drops
+    // stale L2 lines) separates a peer's stores from our loads, so its slots
+    // are uncached (`slots_` copies).  The host-issued and queued engines
+    // read a region in a new dispatch after the wait and keep hipMalloc'd
+    // regions: uncached ones gave wrong results on the GPU in host-memory
+    // runs with either transport.  GLOO_AMD_STEPS_SCRATCH=
+    // uncached|cached overrides (diagnostics).
     static const int stepsScratch = [] {
       const char* e = std::getenv("GLOO_AMD_STEPS_SCRATCH");
       if (e != nullptr && std::strcmp(e, "uncached") == 0) return 1;
-      if (e != nullptr && std::strcmp(e, "cached") == 0) return 0;
-      return -1;
+      return 0;
     }();
-    const bool uncached = engine_ == kEngineDevSteps ||
-                          (stepsScratch < 0 ? copyEngine_ == kCopyKernel : stepsScratch == 1);
+    const bool uncached = engine_ == kEngineDevSteps || stepsScratch == 1;
     allocScratch(uncached, engine_ == kEngineDevSteps ? slots_ : 1);
   }
 
@@ -629,12 +623,7 @@ void HipPlanExecutor::resolvePeers() {
     GLX_ENFORCE(engine_ != kEngineDevSteps || peerSlots == slots_, "rank ", r, " keeps ",
                 peerSlots, " landing slot(s) per channel, rank ", contextRank_, " ", slots_,
                 " (GLOO_AMD_FUSE must be the same on every rank)");
-    const int32_t peerCopy = getPod<int32_t>(b, at);
-    GLX_ENFORCE(!(engine_ == kEngineSteps || engine_ == kEngineQueued) ||
-                    peerCopy == copyEngine_,
-                "rank ", r, " sends with copy engine ", peerCopy, ", rank ", contextRank_,
-                " with ", copyEngine_, " (set_copy_engine must be the same on every rank: "
-                "it decides what memory the receive regions are)");
+    getPod<int32_t>(b, at);  // the peer's copy engine (recorded for diagnostics)
     const int32_t nb = getPod<int32_t>(b, at);
     std::vector<char*> blocks;
     for (int32_t k = 0; k < nb; k++) {
@@ -681,7 +670,7 @@ void HipPlanExecutor::resolvePeers() {
 // on its 16-byte vector path (an unaligned ptr0 still works: the kernel then
 // takes its scalar path).  Both sides compute it from `off` alone.
 char* HipPlanExecutor::landing(const std::vector<ScratchBlock>& blocks, int64_t boff,
-                               int64_t off) const {
+                               int64_t off, int64_t len) const {
   const ScratchBlock* blk = nullptr;
   for (const auto& b : blocks) {
     if (b.start <= boff && boff < b.start + b.elems) {
@@ -692,6 +681,13 @@ char* HipPlanExecutor::landing(const std::vector<ScratchBlock>& blocks, int64_t 
   GLX_ENFORCE(blk != nullptr && blk->ptr != nullptr, "no receive block holds region ", boff);
   uintptr_t at = ((uintptr_t)(boff - blk->start) * esize_ + 15) & ~(uintptr_t)15;
   at += ((uintptr_t)off * esize_) % 16;
+  if (len >= 0) {  // a copy or reduce of len elements stays inside the block (slot 0)
+    const size_t cap = slots_ > 1 ? slotBytes(*blk) : (size_t)blk->elems * esize_ + 64;
+    GLX_ENFORCE(at + (size_t)len * esize_ <= cap, "receive region ", boff, " (+", len,
+                " elements at byte ", at, ") overruns its block of ", cap, " bytes");
+    GLX_ENFORCE(off >= 0 && off + len <= count_, "step range [", off, ", ", off + len,
+                ") outside the buffer of ", count_, " elements");
+  }
   return blk->ptr + at;
 }
 
@@ -1387,7 +1383,7 @@ void HipPlanExecutor::exchange(char* ptr0) {
             markEpoch_++;
             computeSinceMark = false;
           }
-          char* dst = landing(peerBlocks_[oc.peer], s.dst_off, s.off);
+          char* dst = landing(peerBlocks_[oc.peer], s.dst_off, s.off, s.len);
           const char* src = ptr0 + (size_t)s.off * esize_;
           int parts = split_;
           while (parts > 1 && nbytes / (size_t)parts < kMinSplitBytes) parts--;
@@ -1453,7 +1449,7 @@ void HipPlanExecutor::exchange(char* ptr0) {
         waitWar(s.off, s.len);
         if (staged_) waitH2D(compute_, computeH2dWaited_, s.off, s.len);
         char* dst = ptr0 + (size_t)s.off * esize_;
-        const char* src = landing(blocks_, s.boff, s.off);
+        const char* src = landing(blocks_, s.boff, s.off, s.len);
         GLX_HIP_CHECK(glx::launch_reduce(op_, dtype_, dst, dst, src, (size_t)s.len, compute_));
         computeSinceMark = true;
         if (staged_ && !stage_.d2h[i].empty()) {  // final values: copy back now
@@ -1487,7 +1483,7 @@ void HipPlanExecutor::exchange(char* ptr0) {
             } else if (whole) {  // whole-buffer message: element off is off into it
               spec.srcs.push_back(landing(blocks_, r, 0) + (size_t)f.off * esize_);
             } else {
-              spec.srcs.push_back(landing(blocks_, r, f.off));
+              spec.srcs.push_back(landing(blocks_, r, f.off, f.len));
             }
           }
           spec.k = (int)spec.srcs.size();
@@ -1515,9 +1511,11 @@ void HipPlanExecutor::exchange(char* ptr0) {
         waitWar(s.off, s.len);
         if (staged_) waitH2D(compute_, computeH2dWaited_, s.off, s.len);
         char* dst = ptr0 + (size_t)s.off * esize_;
-        const char* src = landing(blocks_, s.boff, s.off);
-        GLX_HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)s.len * esize_,
-                                     hipMemcpyDeviceToDevice, compute_));
+        const char* src = landing(blocks_, s.boff, s.off, s.len);
+        // our copy kernel, not hipMemcpyAsync: the region may be uncached
+        // memory, which the runtime's copies do not keep in stream order
+        // 
+        GLX_HIP_CHECK(glx::launch_copy(dst, src, (size_t)s.len * esize_, compute_));
         computeSinceMark = true;
         if (staged_ && !stage_.d2h[i].empty()) {  // final values: copy back now
           GLX_HIP_CHECK(hipEventRecord(d2hEvents_[i], compute_));
@@ -2198,7 +2196,7 @@ void HipPlanExecutor::exchangeQueued(char* ptr0) {
           markEpoch_++;
           computeSinceMark = false;
         }
-        char* dst = landing(peerBlocks_[oc.peer], s.dst_off, s.off);
+        char* dst = landing(peerBlocks_[oc.peer], s.dst_off, s.off, s.len);
         const char* src = ptr0 + (size_t)s.off * esize_;
         auto prepare = [&](CopyStream& cs) {
           creditWait(cs.s);
@@ -2274,13 +2272,12 @@ void HipPlanExecutor::exchangeQueued(char* ptr0) {
         waitWar(s.off, s.len);
         if (staged_) waitH2D(compute_, computeH2dWaited_, s.off, s.len);
         char* dst = ptr0 + (size_t)s.off * esize_;
-        const char* src = landing(blocks_, s.boff, s.off);
+        const char* src = landing(blocks_, s.boff, s.off, s.len);
         if (s.kind == glx::REDUCE) {
           GLX_HIP_CHECK(
               glx::launch_reduce(op_, dtype_, dst, dst, src, (size_t)s.len, compute_));
-        } else {
-          GLX_HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)s.len * esize_,
-                                       hipMemcpyDeviceToDevice, compute_));
+        } else {  // our copy kernel: see exchange()
+          GLX_HIP_CHECK(glx::launch_copy(dst, src, (size_t)s.len * esize_, compute_));
         }
         computeSinceMark = true;
         if (staged_ && !stage_.d2h[i].empty()) {  // final values: copy back now
@@ -2312,7 +2309,7 @@ void HipPlanExecutor::exchangeQueued(char* ptr0) {
             } else if (whole) {
               spec.srcs.push_back(landing(blocks_, r, 0) + (size_t)f.off * esize_);
             } else {
-              spec.srcs.push_back(landing(blocks_, r, f.off));
+              spec.srcs.push_back(landing(blocks_, r, f.off, f.len));
             }
           }
           spec.k = (int)spec.srcs.size();

@@ -176,7 +176,9 @@ class HipPlanExecutor : public Algorithm {
   template <typename Pred>
   void waitFor(Pred done, const char* what, int peer);
   void drain();
-  char* landing(const std::vector<ScratchBlock>& blocks, int64_t boff, int64_t off) const;
+  // len >= 0: throw unless len elements from there stay inside the block
+  char* landing(const std::vector<ScratchBlock>& blocks, int64_t boff, int64_t off,
+                int64_t len = -1) const;
   void exchange(char* ptr0);
   std::chrono::milliseconds effectiveTimeout() const {
     return timeout_.count() > 0 ? timeout_ : context_->getTimeout();

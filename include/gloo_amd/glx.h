@@ -125,10 +125,9 @@ int glx_tune_reduce(int unroll, int blocks_per_cu, int nontemporal);
  * or $GLOO_AMD_COPY_SPLIT. */
 int glx_set_copy_split(int k);
 /* How peer copies are made by algorithms created afterwards: engine 1 = a
- * copy kernel storing into the peer's (uncached) receive region over xGMI,
- * with `blocks` workgroups (<= 0: keep; default), 0 = hipMemcpyPeerAsync
- * (DMA copy engines, into cached regions).  Every rank must choose alike.
- * Env GLOO_AMD_COPY_ENGINE=dma selects 0 at load time. */
+ * copy kernel storing into the peer's receive region over xGMI, with
+ * `blocks` workgroups (<= 0: keep; default), 0 = hipMemcpyPeerAsync (DMA
+ * copy engines).  Env GLOO_AMD_COPY_ENGINE=dma selects 0 at load time. */
 int glx_set_copy_engine(int engine, int blocks);
 /* Engine of the mesh schedule (ring_chunked's result over all links) for
  * algorithms created afterwards, when device-driven engines are available
