@@ -700,11 +700,14 @@ def bench_multi(args):
                 continue
             ta, sent_a = got
             lm = busiest_link_bytes(gloo_amd, other, rank, world, n, es)
+            eng = ENGINES.get(other)
             alts[other] = {"value": round(world * S / ta / 1e9, 3),
                            "ms_per_step": round(ta * 1e3, 4),
                            "algbw_GBps": round(S / ta / 1e9, 3),
-                           "bytes_sent_per_step": sent_a,
-                           "transport": runs[chosen]["transport"],
+                           "bytes_sent_per_step": sent_a, "engine": eng,
+                           "transport": ("device-driven kernel stores (%s)" % eng
+                                         if eng not in ("steps", "queued")
+                                         else tname(runs[chosen]["tr"])),
                            "busiest_link_GBps": round(lm / ta / 1e9, 2)}
     staged = None
     if args.staged:
