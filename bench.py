@@ -449,23 +449,28 @@ def host_endpoint_rate(torch, dist, gloo_amd, ctx, src, dev_result, algo, reps):
 def result_check(torch, dist, src, result):
     """Independent check of an allreduce result against the inputs (no
     oracle run at this size): with a fixed pseudo-random weight vector w,
-    sum_i w_i * result_i must equal sum over ranks of sum_i w_i * src_i
-    (each rank's term in float64, summed over ranks).  Tolerance: the
-    element type's rounding of the allreduce (fp32 1e-6, 16-bit 4e-3) times
-    sum_i |w_i * result_i|.  A chunk of stale or missing data moves the sum by
-    ~sqrt(chunk) while the tolerance grows ~chunk/1e6: it cannot pass.
-    Returns (ok, relative error)."""
+    sum_i w_i * result_i must equal the sum over ranks of sum_i w_i * src_i
+    (each rank's term in float64).  The result's own rounding (about P
+    roundings of unit u per element, independent signs) moves the weighted
+    sum by sigma ~ sqrt(P) * u * sqrt(sum_i (w_i * result_i)^2); the check
+    allows 6 sigma.  A stale or missing chunk of c elements moves it by
+    ~sqrt(sum over the chunk of (w_i * result_i)^2), i.e. sqrt(c/n) /
+    (6 sqrt(P) u) tolerances: far outside for any chunk a schedule moves.
+    Returns (ok, error / tolerance)."""
     n = src.numel()
+    P = dist.get_world_size()
     g = torch.Generator(device=src.device).manual_seed(4242)
     w = torch.rand(n, device=src.device, generator=g, dtype=torch.float32) * 2 - 1
     mine = torch.tensor([float((w.double() * src.double()).sum().item())], dtype=torch.float64)
     dist.all_reduce(mine)
     rw = w.double() * result.double()
     got = float(rw.sum().item())
-    scale = float(rw.abs().sum().item()) or 1.0
-    tol = (1e-6 if result.element_size() >= 4 else 4e-3) * scale
+    u = {torch.float32: 2.0 ** -24, torch.float64: 2.0 ** -53, torch.float16: 2.0 ** -11,
+         torch.bfloat16: 2.0 ** -8}.get(result.dtype, 2.0 ** -24)
+    sigma = (P ** 0.5) * u * float((rw * rw).sum().item()) ** 0.5
+    tol = 6 * sigma + 1e-12 * float(rw.abs().sum().item())
     err = abs(got - float(mine.item()))
-    return err <= tol, err / scale
+    return err <= tol, err / tol if tol > 0 else float(err > 0)
 
 
 SWEEP_ELEMS = [1 << 10, 1 << 12, 1 << 14, 1 << 16, 1 << 18, 1 << 20, 1 << 22, 1 << 24]
@@ -654,11 +659,11 @@ def bench_multi(args):
             continue
         # every rank is here: the collective check of the result
         ok, rel = result_check(torch, dist, src, r["result"])
-        CHECKS[a] = {"ok": ok, "rel_err": rel}
+        CHECKS[a] = {"ok": ok, "err_over_tol": round(rel, 4)}
         if agreed(ok):
             runs[a] = r
         else:
-            failed[a] = "result check failed (weighted sum off by %.3g of its scale)" % rel
+            failed[a] = "result check failed (weighted sum off by %.3g tolerances)" % rel
     if not runs:
         raise RuntimeError("every candidate failed: %s" % failed)
     candidates = [a for a in candidates if a in runs]
