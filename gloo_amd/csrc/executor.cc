@@ -424,6 +424,9 @@ void HipPlanExecutor::release() noexcept {
   for (auto& e : h2dEvents_) {
     if (e != nullptr) hipEventDestroy(e);
   }
+  for (auto& e : pieceDone_) {
+    if (e != nullptr) hipEventDestroy(e);
+  }
   for (auto& e : d2hEvents_) {
     if (e != nullptr) hipEventDestroy(e);
   }
@@ -964,6 +967,10 @@ void HipPlanExecutor::setupCallStaging() {
   stage_ = glx::stagePlan(plan_, count_, std::max<int64_t>(1, kStagePieceBytes / (int64_t)esize_));
   h2dEvents_.resize(stage_.h2d.size(), nullptr);
   for (auto& e : h2dEvents_) GLX_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (contextSize_ == 1 && ptrs_.size() > 1) {  // runHost's per-piece fold
+    pieceDone_.resize(stage_.h2d.size(), nullptr);
+    for (auto& e : pieceDone_) GLX_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
   d2hEvents_.assign(plan_.steps.size(), nullptr);
   for (size_t i = 0; i < plan_.steps.size(); i++) {
     if (!stage_.d2h[i].empty()) {
@@ -1100,6 +1107,10 @@ void HipPlanExecutor::setupHostMode() {
   stage_ = glx::stagePlan(plan_, count_, std::max<int64_t>(1, kStagePieceBytes / (int64_t)esize_));
   h2dEvents_.resize(stage_.h2d.size(), nullptr);
   for (auto& e : h2dEvents_) GLX_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (contextSize_ == 1 && ptrs_.size() > 1) {  // runHost's per-piece fold
+    pieceDone_.resize(stage_.h2d.size(), nullptr);
+    for (auto& e : pieceDone_) GLX_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
   d2hEvents_.assign(plan_.steps.size(), nullptr);
   for (size_t i = 0; i < plan_.steps.size(); i++) {
     if (!stage_.d2h[i].empty()) {
@@ -1313,6 +1324,30 @@ void HipPlanExecutor::runHost() {
     }
     pieceIssued_.assign(stage_.h2d.size(), 0);
     for (size_t j = 0; j < stage_.h2d.size(); j++) issuePiece(j);
+  }
+  if (contextSize_ == 1 && hsrc.size() > 1 && !fedRun_) {
+    // One rank, several host pointers: the allreduce is the local fold and
+    // broadcast.  Pipelined per H2D piece: the fold of piece j runs once its
+    // copies have landed, and its result goes back to every host pointer
+    // while later pieces are still coming in (H2D and D2H overlap on the
+    // full-duplex link).
+    for (size_t j = 0; j < stage_.h2d.size(); j++) {
+      const glx::Range& r = stage_.h2d[j];
+      GLX_HIP_CHECK(hipStreamWaitEvent(compute_, h2dEvents_[j], 0));
+      std::vector<const void*> srcs;
+      for (char* d : devBufs_) srcs.push_back(d + (size_t)r.off * esize_);
+      GLX_HIP_CHECK(glx::launch_reduce_n(op_, dtype_, devBufs_[0] + (size_t)r.off * esize_,
+                                         srcs.data(), (int)srcs.size(), (size_t)r.len,
+                                         compute_));
+      GLX_HIP_CHECK(hipEventRecord(pieceDone_[j], compute_));
+      GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, pieceDone_[j], 0));
+      copyBack({r});
+    }
+    GLX_HIP_CHECK(hipStreamSynchronize(d2h_));
+    GLX_HIP_CHECK(hipStreamSynchronize(compute_));
+    GLX_HIP_CHECK(hipStreamSynchronize(h2d_));
+    noteDone(d2h_);
+    return;
   }
   if (hsrc.size() > 1) {  // local fold needs every buffer whole
     waitH2D(compute_, computeH2dWaited_, 0, count_);

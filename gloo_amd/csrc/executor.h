@@ -247,6 +247,7 @@ class HipPlanExecutor : public Algorithm {
   hipStream_t h2d_ = nullptr, d2h_ = nullptr;
   glx::StagePlan stage_;
   std::vector<hipEvent_t> h2dEvents_;  // one per stage_.h2d piece
+  std::vector<hipEvent_t> pieceDone_;  // one rank, several pointers: piece j folded
   std::vector<hipEvent_t> d2hEvents_;  // one per step (recorded where d2h is non-empty)
   hipEvent_t hostDone_ = nullptr;
   int computeH2dWaited_ = -1;

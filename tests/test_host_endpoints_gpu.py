@@ -92,6 +92,19 @@ def test_pinned_multi_pointer_host_buffers(algo, dtype, op):
     check(out, O.allreduce(ALGOS[algo], op, dtype, ins))
 
 
+@pytest.mark.parametrize("pinned", [True, False], ids=["pinned", "pageable"])
+@pytest.mark.parametrize("dtype,op,nptrs", [(O.FLOAT32, O.SUM, 2), (O.FLOAT16, O.SUM, 3),
+                                            (O.INT32, O.MAX, 2)], ids=str)
+def test_single_rank_multi_pointer_host_pipelined(pinned, dtype, op, nptrs):
+    """One rank, several host pointers above kOnDeviceThreshold: the fold
+    runs per 8 MiB staging piece (H2D, fold, D2H to every pointer,
+    overlapped); several pieces and a ragged last one, two runs."""
+    N = (5 << 20) + 4099
+    ins = case_inputs(1, N, dtype, nptrs, 0, seed=61)
+    out = host_allreduce("ring_chunked", op, dtype, ins, runs=2, pinned=pinned)
+    check(out, O.allreduce(O.RING_CHUNKED, op, dtype, ins))
+
+
 def test_single_rank_multi_pointer_host():
     ins = case_inputs(1, 5000, O.FLOAT32, 3, 0, seed=6)
     out = host_allreduce("ring_chunked", O.SUM, O.FLOAT32, ins)
