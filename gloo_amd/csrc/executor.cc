@@ -2224,6 +2224,9 @@ void HipPlanExecutor::exchangeQueued(char* ptr0) {
         if (nbytes == 0) {
           creditWait(c0.s);
           GLX_HIP_CHECK(glx::launch_flag_put(oc.devDelivery, n, store, c0.s));
+          // the run ends only after this delivery too
+          GLX_HIP_CHECK(hipEventRecord(events_[i * (size_t)split_], c0.s));
+          c0.last = events_[i * (size_t)split_];
           break;
         }
         if (computeSinceMark) {
