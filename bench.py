@@ -41,13 +41,9 @@ def parse():
                    help="N>1, ring_chunked: data movement (bit-identical results); 'auto' "
                         "times both and reports the faster as value, the other beside it")
     p.add_argument("--copy-split", default="auto",
-                   help="N>1: peer-copy transport: 'auto' (short calibration over the xGMI "
-                        "copy kernel at 32/64/128/256 workgroups, plus DMA with --dma) or a "
-                        "fixed DMA split 1/2/4")
-    p.add_argument("--dma", action="store_true",
-                   help="N>1: also calibrate hipMemcpyPeerAsync (1/2/4 streams per copy): "
-                        "opt-in, it gave one intermittent wrong result in the GPU suite "
-                        "(DESIGN.md 5c)")
+                   help="N>1: peer-copy transport: 'auto' (short calibration over "
+                        "hipMemcpyPeerAsync with 1/2/4 streams per copy and the xGMI copy "
+                        "kernel at 32/64/128/256 workgroups) or a fixed DMA split 1/2/4")
     p.add_argument("--no-alt", action="store_true",
                    help="N>1: do not also time the other schedules")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -611,10 +607,8 @@ def bench_multi(args):
     # Transport calibration: peer copies by the DMA engines split over 1/2/4
     # streams, or by the xGMI copy kernel (32/128 workgroups); a few runs
     # each, max over ranks (every rank sees the same times and picks alike).
-    TRANSPORTS = [("kernel", 1, 32), ("kernel", 1, 64), ("kernel", 1, 128),
-                  ("kernel", 1, 256)]
-    if args.dma:
-        TRANSPORTS += [("dma", 1, 0), ("dma", 2, 0), ("dma", 4, 0)]
+    TRANSPORTS = [("dma", 1, 0), ("dma", 2, 0), ("dma", 4, 0), ("kernel", 1, 32),
+                  ("kernel", 1, 64), ("kernel", 1, 128), ("kernel", 1, 256)]
 
     def set_transport(tr):
         eng, k, blocks = tr
@@ -636,10 +630,8 @@ def bench_multi(args):
                 buf.copy_(src)
                 calib[tr], _ = time_schedule(torch, dist, gloo_amd, ctx, buf, algo, 3, 1)
             best = min(calib, key=lambda k: calib[k])
-        elif args.copy_split == "auto":
-            best = ("kernel", 1, 64)
         else:
-            best = ("dma", int(args.copy_split), 0)
+            best = ("dma", 1 if args.copy_split == "auto" else int(args.copy_split), 0)
         set_transport(best)
         buf.copy_(src)
         torch.cuda.synchronize()

@@ -38,9 +38,9 @@ def set_copy_split(k):
 
 
 def set_copy_engine(engine, blocks=0):
-    """Peer copies of algorithms created afterwards: "kernel" (default: a copy
-    kernel storing over xGMI into the peer's receive region, `blocks`
-    workgroups) or "dma" (hipMemcpyPeerAsync; opt-in)."""
+    """Peer copies of algorithms created afterwards: "dma" (hipMemcpyPeerAsync,
+    default) or "kernel" (a copy kernel storing over xGMI into the peer's
+    receive region, `blocks` workgroups)."""
     code = {"dma": 0, "kernel": 1}[engine]
     errors.check(_lib.lib.glx_set_copy_engine(code, int(blocks)), "set_copy_engine")
 

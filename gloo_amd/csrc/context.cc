@@ -143,28 +143,96 @@ Context::Context(int rank_, int size_, int device) : rank(rank_), size(size_), d
   peers_.resize(size_);
 }
 
+namespace {
+
+// The canary word's line, after a block's usable bytes.
+constexpr size_t kCanaryBytes = 128;
+
+// Uncached / fine-grained blocks are never handed back to the runtime while
+// the process lives: memory freed with hipFree after such an allocation was
+// seen coming back from later plain hipMalloc calls with broken semantics
+// (host-memory runs of the GPU suite gave wrong results in later, unrelated
+// tests of the same process -- even one-rank runs that allocate no
+// uncached memory at all -- and more of them the more uncached memory had
+// been freed).  Freed ones wait here, per device and kind,
+// for the next context to take them.
+struct KindCache {
+  std::mutex mu;
+  struct Entry {
+    int device;
+    unsigned flags;
+    size_t bytes;
+    char* ptr;
+  };
+  std::vector<Entry> free;
+};
+
+KindCache& kindCache() {
+  static KindCache* c = new KindCache();  // outlives every Context (never destroyed)
+  return *c;
+}
+
+char* takeCached(int device, unsigned flags, size_t bytes, size_t* got) {
+  KindCache& c = kindCache();
+  std::lock_guard<std::mutex> g(c.mu);
+  const size_t most = std::max(2 * bytes, bytes + (size_t(4) << 20));
+  size_t best = c.free.size();
+  for (size_t i = 0; i < c.free.size(); i++) {
+    const auto& e = c.free[i];
+    if (e.device == device && e.flags == flags && e.bytes >= bytes && e.bytes <= most &&
+        (best == c.free.size() || e.bytes < c.free[best].bytes)) {
+      best = i;
+    }
+  }
+  if (best == c.free.size()) return nullptr;
+  char* p = c.free[best].ptr;
+  *got = c.free[best].bytes;
+  c.free.erase(c.free.begin() + (long)best);
+  return p;
+}
+
+// Give a block of `flags` kind back: plain blocks to the runtime, the others
+// to the cache above.
+void freeBlock(int device, char* p, size_t bytes, unsigned flags) {
+  if (p == nullptr) return;
+  if (flags == 0) {
+    hipFree(p);
+    return;
+  }
+  KindCache& c = kindCache();
+  std::lock_guard<std::mutex> g(c.mu);
+  c.free.push_back(KindCache::Entry{device, flags, bytes, p});
+}
+
+// `bytes` in, the block's real size out (a cached block may be larger).
+char* allocBlock(int device, size_t* bytes, unsigned flags) {
+  char* d = nullptr;
+  if (flags != 0) {
+    size_t got = 0;
+    d = takeCached(device, flags, *bytes, &got);
+    if (d != nullptr) {
+      *bytes = got;
+      return d;
+    }
+    GLX_HIP_CHECK(hipExtMallocWithFlags((void**)&d, *bytes, flags));
+  } else {
+    GLX_HIP_CHECK(hipMalloc((void**)&d, *bytes));
+  }
+  return d;
+}
+}  // namespace
+
 Context::~Context() {
   if (shared_.empty() && imported_.empty()) return;
   if (device_ >= 0) hipSetDevice(device_);
   for (auto& kv : imported_) hipIpcCloseMemHandle(kv.second.opened);
-  for (auto& b : shared_) hipFree(b.ptr);
+  for (auto& b : shared_) freeBlock(device_, b.ptr, b.bytes + kCanaryBytes, b.flags);
 }
 
 namespace {
-char* allocBlock(size_t bytes, unsigned flags) {
-  char* d = nullptr;
-  if (flags != 0) {
-    GLX_HIP_CHECK(hipExtMallocWithFlags((void**)&d, bytes, flags));
-  } else {
-    GLX_HIP_CHECK(hipMalloc((void**)&d, bytes));
-  }
-  return d;
-}
 
 // Free pooled bytes kept beyond this are returned to the runtime.
 constexpr size_t kMaxFreeSharedBytes = size_t(8) << 30;
-// The canary word's line, after a block's usable bytes.
-constexpr size_t kCanaryBytes = 128;
 
 // Allocation granule of a shared block (GLOO_AMD_SHARED_GRANULE, bytes;
 // default one 4 KiB page).  Round 1 rounded every block up to 2 MiB after a
@@ -217,9 +285,11 @@ SharedBlock Context::acquireShared(size_t bytes, unsigned flags) {
     return *best;
   }
   SharedBlock nb;
+  size_t got = alloc;
+  nb.ptr = allocBlock(device_, &got, flags);  // a recycled block may be larger
+  bytes = got - kCanaryBytes;
   nb.bytes = bytes;
   nb.flags = flags;
-  nb.ptr = allocBlock(alloc, flags);
   nb.ref.ptr = (uint64_t)(uintptr_t)nb.ptr;
   nb.ref.id = nextSharedId_++;
   if (size > 1) {
@@ -227,8 +297,8 @@ SharedBlock Context::acquireShared(size_t bytes, unsigned flags) {
     const hipError_t e = hipIpcGetMemHandle(&nb.ref.ipc, nb.ptr);
     if (e != hipSuccess) {
       (void)hipGetLastError();
-      hipFree(nb.ptr);
-      GLX_ENFORCE(false, "rank ", rank, ": hipIpcGetMemHandle of a ", alloc,
+      freeBlock(device_, nb.ptr, got, flags);
+      GLX_ENFORCE(false, "rank ", rank, ": hipIpcGetMemHandle of a ", got,
                   "-byte shared block refused: ", hipGetErrorName(e), " (", hipGetErrorString(e),
                   ")");
     }
@@ -267,7 +337,7 @@ void Context::releaseShared(int64_t id) {
     }
     if (big == shared_.end()) break;
     freeBytes -= big->bytes;
-    hipFree(big->ptr);
+    freeBlock(device_, big->ptr, big->bytes + kCanaryBytes, big->flags);
     retired_.push_back(big->ref.id);
     shared_.erase(big);
   }

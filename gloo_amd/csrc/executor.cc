@@ -73,13 +73,12 @@ int initialSplit() {
 
 std::atomic<int> g_copy_split{initialSplit()};
 
-// Default: the copy kernel (stores from the sending GPU's compute units into
-// the receiver's region over xGMI).  DMA (hipMemcpyPeerAsync) is opt-in,
-// GLOO_AMD_COPY_ENGINE=dma: it gave an intermittent wrong result in the GPU
-// suite, the copy kernel never did.
+// Default: hipMemcpyPeerAsync (the DMA engines); GLOO_AMD_COPY_ENGINE=kernel
+// selects the copy kernel (the sending GPU's compute units store into the
+// receiver's region over xGMI).
 int initialEngine() {
   const char* e = std::getenv("GLOO_AMD_COPY_ENGINE");
-  return (e != nullptr && std::strcmp(e, "dma") == 0) ? 0 : 1;
+  return (e != nullptr && std::strcmp(e, "kernel") == 0) ? 1 : 0;
 }
 
 std::atomic<int> g_copy_engine{initialEngine()};
@@ -267,20 +266,18 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
   if (engine_ == kEngineOneShot || engine_ == kEngineTwoShot) {
     setupDevice();
   } else {
-    // The plan kernel reads its landing slots inside the launch, right after
-    // an in-kernel flag wait: no dispatch boundary (whose acquire drops
-    // stale L2 lines) separates a peer's stores from our loads, so its slots
-    // are uncached (`slots_` copies).  The host-issued and queued engines
-    // read a region in a new dispatch after the wait and keep hipMalloc'd
-    // regions: uncached ones gave wrong results on the GPU in host-memory
-    // runs with either transport.  GLOO_AMD_STEPS_SCRATCH=
-    // uncached|cached overrides (diagnostics).
-    static const int stepsScratch = [] {
+    // Receive regions are uncached for every engine: peers' stores (their
+    // kernels' or DMA) land behind this GPU's L2, and a region is reused
+    // every run, so no stale line of an earlier message may be cached.  (The
+    // plan kernel reads its `slots_` landing slots inside the launch right
+    // after an in-kernel flag wait, where nothing else could drop such a
+    // line.)  GLOO_AMD_STEPS_SCRATCH=cached gives the host-issued and queued
+    // engines hipMalloc'd regions instead (diagnostics).
+    static const bool stepsCached = [] {
       const char* e = std::getenv("GLOO_AMD_STEPS_SCRATCH");
-      if (e != nullptr && std::strcmp(e, "uncached") == 0) return 1;
-      return 0;
+      return e != nullptr && std::strcmp(e, "cached") == 0;
     }();
-    const bool uncached = engine_ == kEngineDevSteps || stepsScratch == 1;
+    const bool uncached = engine_ == kEngineDevSteps || !stepsCached;
     allocScratch(uncached, engine_ == kEngineDevSteps ? slots_ : 1);
   }
 

@@ -124,10 +124,10 @@ int glx_tune_reduce(int unroll, int blocks_per_cu, int nontemporal);
  * destination (k DMA engines feeding one link; parts >= 1 MiB).  Default 1,
  * or $GLOO_AMD_COPY_SPLIT. */
 int glx_set_copy_split(int k);
-/* How peer copies are made by algorithms created afterwards: engine 1 = a
- * copy kernel storing into the peer's receive region over xGMI, with
- * `blocks` workgroups (<= 0: keep; default), 0 = hipMemcpyPeerAsync (DMA
- * copy engines).  Env GLOO_AMD_COPY_ENGINE=dma selects 0 at load time. */
+/* How peer copies are made by algorithms created afterwards: engine 0 =
+ * hipMemcpyPeerAsync (DMA copy engines, default), 1 = a copy kernel storing
+ * into the peer's memory over xGMI, with `blocks` workgroups (<= 0: keep).
+ * Env GLOO_AMD_COPY_ENGINE=kernel selects 1 at load time. */
 int glx_set_copy_engine(int engine, int blocks);
 /* Engine of the mesh schedule (ring_chunked's result over all links) for
  * algorithms created afterwards, when device-driven engines are available

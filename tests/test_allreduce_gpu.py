@@ -387,7 +387,7 @@ def test_split_peer_copies(algo, split):
         out = gpu_allreduce(algo, O.SUM, O.FLOAT32, ins, runs=2)
     finally:
         gloo_amd.set_copy_split(1)
-        gloo_amd.set_copy_engine("kernel", 64)
+        gloo_amd.set_copy_engine("dma", 64)
     ref_algo = O.HALVING_DOUBLING if algo == O.HALVING_DOUBLING else O.RING_CHUNKED
     check_all(out, O.allreduce(ref_algo, O.SUM, O.FLOAT32, ins), O.FLOAT32, O.SUM)
 
@@ -408,7 +408,7 @@ def test_kernel_copy_engine(algo, split):
         out16 = gpu_allreduce(algo, O.SUM, O.FLOAT16,
                               case_inputs(3, 1001, O.FLOAT16, 1, 0, seed=2))
     finally:
-        gloo_amd.set_copy_engine("kernel", blocks=64)
+        gloo_amd.set_copy_engine("dma", blocks=64)
         gloo_amd.set_copy_split(1)
     ref_algo = O.HALVING_DOUBLING if algo == O.HALVING_DOUBLING else O.RING_CHUNKED
     check_all(out, O.allreduce(ref_algo, O.SUM, O.FLOAT32, ins), O.FLOAT32, O.SUM)
@@ -549,7 +549,7 @@ def test_transport_stats_name_the_mechanism():
         try:
             run_ranks(P, lambda r: rank_fn(r, engine), timeout=90)
         finally:
-            gloo_amd.set_copy_engine("kernel", 64)
+            gloo_amd.set_copy_engine("dma", 64)
     for r in range(P):
         st, sent, eng = stats[(r, "dma")]
         assert eng == "steps"
