@@ -105,6 +105,23 @@ def test_single_rank_multi_pointer_host_pipelined(pinned, dtype, op, nptrs):
     check(out, O.allreduce(O.RING_CHUNKED, op, dtype, ins))
 
 
+def test_freed_uncached_blocks_do_not_poison_later_allocations():
+    """memory freed with hipFree after an uncached allocation
+    came back broken from later plain hipMalloc calls (wrong results in
+    later host-memory runs of the same process).  Contexts here create and
+    destroy uncached receive regions, and every later run -- including a
+    one-rank run whose staging buffers are plain hipMalloc memory -- must
+    still be exact; the executor keeps freed uncached blocks in a
+    process-wide cache instead of handing them back."""
+    for rep in range(3):
+        ins = case_inputs(3, 300007, O.FLOAT64, 2, 0, seed=70 + rep)
+        out = host_allreduce("ring_chunked", O.PRODUCT, O.FLOAT64, ins, runs=2, pinned=True)
+        check(out, O.allreduce(O.RING_CHUNKED, O.PRODUCT, O.FLOAT64, ins))
+        ins1 = case_inputs(1, (5 << 20) + 4099, O.FLOAT32, 2, 0, seed=80 + rep)
+        out1 = host_allreduce("ring_chunked", O.SUM, O.FLOAT32, ins1, runs=2, pinned=True)
+        check(out1, O.allreduce(O.RING_CHUNKED, O.SUM, O.FLOAT32, ins1))
+
+
 def test_single_rank_multi_pointer_host():
     ins = case_inputs(1, 5000, O.FLOAT32, 3, 0, seed=6)
     out = host_allreduce("ring_chunked", O.SUM, O.FLOAT32, ins)
