@@ -195,7 +195,13 @@ char* takeCached(int device, unsigned flags, size_t bytes, size_t* got) {
 // to the cache above.
 void freeBlock(int device, char* p, size_t bytes, unsigned flags) {
   if (p == nullptr) return;
-  if (flags == 0) {
+  // GLOO_AMD_UC_CACHE=0 frees them like plain blocks (to reproduce the
+  // hazard; never in production)
+  static const bool cache = [] {
+    const char* e = std::getenv("GLOO_AMD_UC_CACHE");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  if (flags == 0 || !cache) {
     hipFree(p);
     return;
   }
