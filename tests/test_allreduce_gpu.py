@@ -104,6 +104,43 @@ def test_allreduce_vs_reference_golden(rec):
             check_against_golden(rec, DATA, out[r][i])
 
 
+# The reference test suite's own grid (gloo/test/allreduce_test.cc:251-269):
+# AllreduceRingChunked at P = 1..15 x N in {0, 4, 100, 1000, 10000} and
+# AllreduceHalvingDoubling at P in {1..9, 13, 16, 24, 32} x N in {0, 1, 64,
+# 1000}, SinglePointer (:143-169): rank r contributes value r, every element
+# must equal P(P-1)/2 exactly.  Thread-ranks on one GPU, like the reference's
+# ranks-as-threads tests (gloo/test/base_test.h:91-166).
+REF_GRID = ([(O.RING_CHUNKED, P, N) for P in range(1, 16) for N in (0, 4, 100, 1000, 10000)] +
+            [(O.HALVING_DOUBLING, P, N) for P in (1, 2, 3, 4, 5, 6, 7, 8, 9, 13, 16, 24, 32)
+             for N in (0, 1, 64, 1000)])
+
+
+@pytest.mark.parametrize("algo,P,N", REF_GRID,
+                         ids=["%s-P%d-N%d" % ("ring_chunked" if a == O.RING_CHUNKED
+                                              else "halving_doubling", P, N)
+                              for a, P, N in REF_GRID])
+def test_reference_test_grid_single_pointer(algo, P, N):
+    ins = [[np.full(N, r, dtype=np.float32)] for r in range(P)]
+    out = gpu_allreduce(algo, O.SUM, O.FLOAT32, ins, runs=2)
+    for r in range(P):
+        assert np.all(out[r][0] == P * (P - 1) // 2), "rank %d" % r
+
+
+# Beyond 8 ranks with seeded inputs, so the reduction ORDER is checked too
+# (value = rank sums exactly in any order): bit-exact against the oracle.
+@pytest.mark.parametrize("algo,P", [(O.RING_CHUNKED, 11), (O.RING_CHUNKED, 15),
+                                    (O.HALVING_DOUBLING, 13), (O.HALVING_DOUBLING, 16),
+                                    (O.HALVING_DOUBLING, 24), (O.HALVING_DOUBLING, 32)],
+                         ids=["ring_chunked-P11", "ring_chunked-P15", "halving_doubling-P13",
+                              "halving_doubling-P16", "halving_doubling-P24",
+                              "halving_doubling-P32"])
+@pytest.mark.parametrize("N", [1000, 10007])
+def test_many_ranks_vs_oracle(algo, P, N):
+    ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=31)
+    out = gpu_allreduce(algo, O.SUM, O.FLOAT32, ins)
+    check_all(out, O.allreduce(algo, O.SUM, O.FLOAT32, ins), O.FLOAT32, O.SUM)
+
+
 @pytest.mark.parametrize("algo", [O.RING_CHUNKED, O.HALVING_DOUBLING],
                          ids=["ring_chunked", "halving_doubling"])
 @pytest.mark.parametrize("dtype", [O.INT8, O.INT32, O.INT64, O.UINT64, O.FLOAT64,
