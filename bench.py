@@ -443,6 +443,66 @@ def time_schedule(torch, dist, gloo_amd, ctx, buf, algo, steps, warmup):
     return el.item() / steps, sent
 
 
+def link_ceiling(torch, dist, gloo_amd, dev, rank, world, nbytes=64 << 20, reps=5):
+    """Measured xGMI ceilings, the roofline's second denominator (SURVEY 8d:
+    'also record a measured single-link hipMemcpyPeerAsync ceiling and report
+    the fraction of both').  Every rank exports a receive buffer (torch CUDA
+    IPC) and, with every rank sending at once:
+      ring -- writes `nbytes` to rank+1 (the ring's link use; HD's per step);
+      mesh -- writes nbytes/(P-1) to every peer (the mesh's: all links busy);
+    by hipMemcpyPeerAsync (dma, one stream per destination) and by the kernel
+    transport's copy kernel (kernel, 256 workgroups over the destinations).
+    Per-link GB/s = bytes on the busiest link / max-over-ranks time."""
+    recv = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    send = torch.empty(nbytes, dtype=torch.uint8, device=dev).fill_(rank & 0xFF)
+    torch.cuda.synchronize()
+    handles = [None] * world
+    dist.all_gather_object(handles, recv.untyped_storage()._share_cuda_())
+    peers = {}
+    try:
+        for k in range(world):
+            if k != rank:
+                peers[k] = torch.UntypedStorage._new_shared_cuda(*handles[k])
+        streams = [torch.cuda.Stream(dev) for _ in range(world - 1)]
+        piece = (nbytes // max(1, world - 1)) & ~4095
+        out = {"bytes_per_rep": nbytes, "reps": reps}
+        for pattern in ("ring", "mesh"):
+            if pattern == "mesh" and world <= 2:
+                continue  # one peer: the mesh is the ring
+            for eng in ("dma", "kernel"):
+                if pattern == "ring":
+                    jobs = [((rank + 1) % world, 0, nbytes, streams[0])]
+                else:  # sender k lands in slot (k - j - 1) mod P of receiver j
+                    jobs = [(j, ((rank - j - 1) % world) * piece, piece, streams[i])
+                            for i, j in enumerate(k for k in range(world) if k != rank)]
+                blocks = max(32, 256 // len(jobs))
+
+                def issue():
+                    for j, off, ln, st in jobs:
+                        dptr = peers[j].data_ptr() + off
+                        if eng == "dma":
+                            gloo_amd.peer_copy(dptr, handles[j][0], send.data_ptr(),
+                                               dev.index, ln, st)
+                        else:
+                            gloo_amd.kernel_copy(dptr, send.data_ptr(), ln, blocks, st)
+                issue()  # warm: maps, peer access, first-touch
+                torch.cuda.synchronize()
+                dist.barrier()
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    issue()
+                torch.cuda.synchronize()
+                el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+                dist.all_reduce(el, op=dist.ReduceOp.MAX)
+                link_bytes = jobs[0][2]
+                out["%s_%s_GBps" % (pattern, eng)] = round(link_bytes * reps / el.item() / 1e9, 2)
+        return out
+    finally:
+        torch.cuda.synchronize()
+        peers.clear()
+        dist.barrier()  # nobody frees its buffer while a peer still maps it
+
+
 def host_endpoint_rate(torch, dist, gloo_amd, ctx, src, dev_result, algo, reps):
     """The path as the reference runs it: buffers in host memory.  The
     algorithm is built on a host buffer (pinned; the product pins pageable
@@ -604,6 +664,13 @@ def bench_multi(args):
     ctx.connectFullMesh(store)
     log("connected (world %d, device %d)" % (world, local))
     device_engines = probe_device_engines(torch, dist, gloo_amd, ctx, dev, args.dtype)
+    links, err = None, None
+    try:
+        links = link_ceiling(torch, dist, gloo_amd, dev, rank, world)
+        log("link ceilings: %s" % links)
+    except Exception as e:  # noqa: BLE001 - reported in the JSON line
+        err = "%s: %s" % (type(e).__name__, str(e)[:300])
+        log("link probe failed: %s" % err)
     # Transport calibration: peer copies by the DMA engines split over 1/2/4
     # streams, or by the xGMI copy kernel (32/128 workgroups); a few runs
     # each, max over ranks (every rank sees the same times and picks alike).
@@ -766,6 +833,17 @@ def bench_multi(args):
         link_ach = link_max / t / 1e9
         hbm = plan_hbm_bytes(gloo_amd, chosen, rank, world, n, es)
         hbm_ach = hbm / t / 1e9
+        measured = None
+        if links is not None:
+            pat = "mesh" if plan_name(chosen) == "ring_chunked_mesh" and world > 2 else "ring"
+            best = max(links.get("%s_dma_GBps" % pat, 0), links.get("%s_kernel_GBps" % pat, 0))
+            measured = dict(links, pattern=pat, best_GBps=best,
+                            frac=round(link_ach / best, 4) if best > 0 else None,
+                            note="fraction of the measured per-link ceiling for the chosen "
+                                 "schedule's pattern (ring: every rank -> rank+1 at once; "
+                                 "mesh: every rank -> every peer at once)")
+        elif err is not None:
+            measured = {"failed": err}
         res = {
             "metric": "allreduce GB/s (device-resident, fp32) at 1/2/4/8 MI355X; % HBM|xGMI roofline",
             "value": round(world * S / t / 1e9, 3), "unit": "GB/s", "n_gpus": world,
@@ -800,6 +878,7 @@ def bench_multi(args):
                          "bytes_sent_per_step": link_bytes,
                          "note": "busiest outgoing link's bytes per step / ms_per_step, "
                                  "peak = one xGMI link per direction (task figure)",
+                         "link_measured": measured,
                          "hbm": {"achieved": round(hbm_ach, 1), "peak": HBM_PEAK_GBPS,
                                  "unit": "GB/s", "frac": round(hbm_ach / HBM_PEAK_GBPS, 4),
                                  "algorithmic_bytes_per_step": hbm,

@@ -75,6 +75,24 @@ def set_device_engines(mode):
     errors.check(_lib.lib.glx_set_device_engines(code), "set_device_engines")
 
 
+def peer_copy(dst_ptr, dst_dev, src_ptr, src_dev, nbytes, stream):
+    """nbytes from src (on src_dev) to dst (on dst_dev; may be a peer's
+    IPC-mapped memory) by hipMemcpyPeerAsync (the DMA engines), on `stream`
+    (torch.cuda.Stream or raw hipStream_t).  Raw pointers: the link probe of
+    bench.py and callers holding foreign buffers."""
+    from .algorithms import _stream_ptr
+    errors.check(_lib.lib.glx_peer_copy(int(dst_ptr), int(dst_dev), int(src_ptr), int(src_dev),
+                                        int(nbytes), _stream_ptr(stream)), "peer_copy")
+
+
+def kernel_copy(dst_ptr, src_ptr, nbytes, blocks, stream):
+    """The same copy by the kernel transport's copy kernel: `blocks`
+    workgroups of this GPU storing 16-byte vectors into dst."""
+    from .algorithms import _stream_ptr
+    errors.check(_lib.lib.glx_copy(int(dst_ptr), int(src_ptr), int(nbytes), int(blocks),
+                                   _stream_ptr(stream)), "kernel_copy")
+
+
 def device_count():
     import ctypes
     n = ctypes.c_int(0)

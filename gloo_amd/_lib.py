@@ -37,6 +37,7 @@ SIGNATURES = [
     ("glx_reduce_n", _i, [_i, _i, _vp, ctypes.POINTER(_vp), _i, _sz, _vp]),
     ("glx_peer_copy", _i, [_vp, _i, _vp, _i, _sz, _vp]),
     ("glx_host_reduce_n", _i, [_i, _i, _vp, ctypes.POINTER(_vp), _i, _sz]),
+    ("glx_copy", _i, [_vp, _vp, _sz, _i, _vp]),
     ("glx_enable_peer", _i, [_i, _i]),
     ("glx_tune_reduce", _i, [_i, _i, _i]),
     ("glx_set_copy_split", _i, [_i]),

@@ -148,6 +148,13 @@ int glx_peer_copy(void* dst, int dst_dev, const void* src, int src_dev, size_t b
                    "hipMemcpyPeerAsync");
 }
 
+int glx_copy(void* dst, const void* src, size_t bytes, int blocks, glx_stream_t stream) {
+  if (bytes == 0) return GLX_OK;
+  if (dst == nullptr || src == nullptr) return fail(GLX_ERR_INVALID, "glx_copy: null");
+  return hipStatus(glx::launch_copy_blocks(dst, src, bytes, blocks, (hipStream_t)stream),
+                   "glx_copy");
+}
+
 int glx_enable_peer(int a, int b) {
   if (a == b) return GLX_OK;
   int cur = 0;

@@ -32,6 +32,9 @@ hipError_t launch_reduce_n_batch(int op, int dtype, const std::vector<FoldSpec>&
 // Byte copy dst <- src as a kernel on stream s (dst may be a peer GPU's
 // IPC-mapped memory: the stores then travel over xGMI).  Never synchronises.
 hipError_t launch_copy(void* dst, const void* src, size_t bytes, hipStream_t s);
+// The same with an explicit grid (<= 0: the configured copy_blocks()).
+hipError_t launch_copy_blocks(void* dst, const void* src, size_t bytes, int grid,
+                              hipStream_t s);
 // Grid (workgroups) of the copy kernel.
 void set_copy_blocks(int blocks);
 int copy_blocks();

@@ -474,9 +474,14 @@ hipError_t launch_n_op(int op, void* dst, const void* const* srcs, int k,
 }  // namespace
 
 hipError_t launch_copy(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  return launch_copy_blocks(dst, src, bytes, 0, s);
+}
+
+hipError_t launch_copy_blocks(void* dst, const void* src, size_t bytes, int grid,
+                              hipStream_t s) {
   if (bytes == 0) return hipSuccess;
   const uintptr_t pd = (uintptr_t)dst, ps = (uintptr_t)src;
-  const unsigned blocks = (unsigned)std::max(1, g_copy_blocks);
+  const unsigned blocks = (unsigned)std::max(1, grid > 0 ? grid : g_copy_blocks);
   if (pd % 16 != ps % 16) {
     hipLaunchKernelGGL(copy_bytes_kernel, dim3(blocks), dim3(kBlock), 0, s, (char*)dst,
                        (const char*)src, bytes);

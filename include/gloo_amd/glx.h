@@ -111,6 +111,14 @@ int glx_host_reduce_n(int op, int dtype, void* dst, const void* const* srcs, int
 int glx_peer_copy(void* dst, int dst_dev, const void* src, int src_dev,
                   size_t bytes, glx_stream_t stream);
 
+/* The same copy made by the copy kernel the kernel transport uses
+ * (glx_set_copy_engine(1, blocks)): 16-byte vector stores from this GPU's
+ * compute units straight into `dst`, which may be a peer GPU's memory mapped
+ * into this process (IPC) -- the CU-driven counterpart of glx_peer_copy, for
+ * measuring what stores over one xGMI link reach.  `blocks` workgroups
+ * (<= 0: the transport's current setting). */
+int glx_copy(void* dst, const void* src, size_t bytes, int blocks, glx_stream_t stream);
+
 /* hipDeviceEnablePeerAccess both ways between devices a and b (idempotent).
  * Analog of cudaDeviceEnablePeerAccess in gloo/cuda_collectives_native.h:216-276. */
 int glx_enable_peer(int dev_a, int dev_b);
