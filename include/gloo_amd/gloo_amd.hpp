@@ -193,10 +193,24 @@ class Context {
 
 using Context = rendezvous::Context;
 
-class Algorithm {  // gloo::Algorithm
+// gloo::Algorithm (gloo/algorithm.h:19-38): the algorithm keeps its context
+// and the caller's rank/size.  There are no transport pairs (peers are
+// reached through their IPC-mapped memory), so the ring helpers
+// getLeftPair()/getRightPair() become the ranks they would connect to.
+class Algorithm {
  public:
+  explicit Algorithm(const std::shared_ptr<Context>& context)
+      : context_(context), contextRank_(context->rank), contextSize_(context->size) {}
   virtual ~Algorithm() = default;
   virtual void run() = 0;
+
+ protected:
+  std::shared_ptr<Context> context_;
+  const int contextRank_;
+  const int contextSize_;
+
+  int getLeftRank() const { return (contextSize_ + contextRank_ - 1) % contextSize_; }
+  int getRightRank() const { return (contextRank_ + 1) % contextSize_; }
 };
 
 // A HIP event (gloo::CudaStream's record / wait, gloo/cuda.h:40-120).
@@ -236,7 +250,7 @@ class DeviceAllreduce : public Algorithm {
   DeviceAllreduce(Create create, const std::shared_ptr<Context>& ctx,
                   const std::vector<T*>& ptrs, int count,
                   const std::vector<glx_stream_t>& streams, const ReductionFunction<T>* fn)
-      : ctx_(ctx) {
+      : Algorithm(ctx) {
     std::vector<void*> p(ptrs.begin(), ptrs.end());
     a_ = checkHandle(create(ctx->handle(), p.data(), (int)p.size(), count, DType<T>::value,
                             fn->type(), streams.empty() ? nullptr : streams.data(),
@@ -272,7 +286,6 @@ class DeviceAllreduce : public Algorithm {
   }
 
  private:
-  std::shared_ptr<Context> ctx_;
   glx_algorithm* a_ = nullptr;
 };
 }  // namespace detail

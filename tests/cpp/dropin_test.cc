@@ -157,6 +157,56 @@ void multipleAlgorithms() {
   });
 }
 
+// A caller's own algorithm on the Algorithm base, the way reference users
+// compose gloo algorithms (gloo/algorithm.h:19-38: context_, contextRank_,
+// contextSize_, the ring neighbours): an average = allreduce + local scale.
+class AverageRingChunked : public gloo_amd::Algorithm {
+ public:
+  AverageRingChunked(const std::shared_ptr<gloo_amd::Context>& ctx, float* ptr, int count)
+      : gloo_amd::Algorithm(ctx), ptr_(ptr), count_(count), sum_(ctx, {ptr}, count) {}
+  void run() override {
+    sum_.run();
+    std::vector<float> host(count_);
+    hipCheck(hipMemcpy(host.data(), ptr_, count_ * sizeof(float), hipMemcpyDeviceToHost), "d2h");
+    for (auto& x : host) x /= (float)contextSize_;
+    hipCheck(hipMemcpy(ptr_, host.data(), count_ * sizeof(float), hipMemcpyHostToDevice), "h2d");
+  }
+  int rank() const { return contextRank_; }
+  int left() const { return getLeftRank(); }
+  int right() const { return getRightRank(); }
+  const gloo_amd::Context& context() const { return *context_; }
+
+ private:
+  float* ptr_;
+  int count_;
+  gloo_amd::HipAllreduceRingChunked<float> sum_;
+};
+
+void customAlgorithm() {
+  const int P = 3, N = 777;
+  spawn(P, [&](std::shared_ptr<gloo_amd::Context> ctx) {
+    float* dev = nullptr;
+    hipCheck(hipMalloc(&dev, N * sizeof(float)), "hipMalloc");
+    std::vector<float> host(N, (float)(2 * ctx->rank));
+    hipCheck(hipMemcpy(dev, host.data(), N * sizeof(float), hipMemcpyHostToDevice), "h2d");
+    {
+      AverageRingChunked alg(ctx, dev, N);
+      EXPECT(alg.rank() == ctx->rank && alg.context().size == P, "contextRank_/contextSize_");
+      EXPECT(alg.left() == (ctx->rank + P - 1) % P && alg.right() == (ctx->rank + 1) % P,
+             "ring neighbours of rank %d: %d %d", ctx->rank, alg.left(), alg.right());
+      alg.run();
+    }
+    hipCheck(hipMemcpy(host.data(), dev, N * sizeof(float), hipMemcpyDeviceToHost), "d2h");
+    hipFree(dev);
+    for (int i = 0; i < N; i++) {
+      if (host[i] != (float)(P - 1)) {
+        EXPECT(false, "CustomAlgorithm rank %d element %d = %f", ctx->rank, i, host[i]);
+        break;
+      }
+    }
+  });
+}
+
 void timeoutThrowsIoException() {
   // a lone rank of a 2-rank context: its peer never runs the collective
   gloo_amd::rendezvous::HashStore store;
@@ -343,6 +393,7 @@ int main() {
     }
   }
   multipleAlgorithms();
+  customAlgorithm();
   timeoutThrowsIoException();
   using Opts = gloo_amd::AllreduceOptions;
   for (auto algo : {Opts::RING, Opts::BCUBE, Opts::RING_MESH}) {
