@@ -190,7 +190,19 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
 
   userStream_ = !streams.empty();
   if (userStream_) {
+    GLX_ENFORCE(perCallBuffers || streams.size() == 1 || streams.size() == ptrs.size(),
+                "streams: pass one per pointer (", ptrs.size(), "), or one; got ",
+                streams.size());
     compute_ = streams[0];
+    for (size_t i = 1; i < streams.size(); i++) {
+      if (streams[i] == compute_) continue;
+      sideStreams_.push_back(streams[i]);
+      sideIn_.push_back(nullptr);
+      GLX_HIP_CHECK(hipEventCreateWithFlags(&sideIn_.back(), hipEventDisableTiming));
+    }
+    if (!sideStreams_.empty()) {
+      GLX_HIP_CHECK(hipEventCreateWithFlags(&sideOut_, hipEventDisableTiming));
+    }
   } else {
     GLX_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
     ownCompute_ = true;
@@ -440,6 +452,12 @@ void HipPlanExecutor::release() noexcept {
   }
   if (computeMark_) hipEventDestroy(computeMark_);
   if (lastDone_) hipEventDestroy(lastDone_);
+  for (auto& e : sideIn_) {
+    if (e != nullptr) hipEventDestroy(e);
+  }
+  sideIn_.clear();
+  if (sideOut_) hipEventDestroy(sideOut_);
+  sideOut_ = nullptr;
   for (auto& b : blocks_) {
     if (b.ref.id > 0) context_->releaseShared(b.ref.id);
   }
@@ -847,6 +865,11 @@ void HipPlanExecutor::run() {
   }
   char* ptr0 = static_cast<char*>(ptrs_[0]);
   const size_t bytes = (size_t)count_ * esize_;
+  // the caller's pending work on every pointer's stream comes first
+  for (size_t i = 0; i < sideStreams_.size(); i++) {
+    GLX_HIP_CHECK(hipEventRecord(sideIn_[i], sideStreams_[i]));
+    GLX_HIP_CHECK(hipStreamWaitEvent(compute_, sideIn_[i], 0));
+  }
 
   // Local multi-pointer reduce into ptrs_[0] (left fold, :89-91).
   if (ptrs_.size() > 1) {
@@ -858,6 +881,10 @@ void HipPlanExecutor::run() {
   // Local broadcast of ptrs_[0] (:209-211).
   for (size_t i = 1; i < ptrs_.size(); i++) {
     GLX_HIP_CHECK(hipMemcpyAsync(ptrs_[i], ptr0, bytes, hipMemcpyDeviceToDevice, compute_));
+  }
+  if (sideOut_ != nullptr) {  // results valid on every pointer's stream
+    GLX_HIP_CHECK(hipEventRecord(sideOut_, compute_));
+    for (hipStream_t st : sideStreams_) GLX_HIP_CHECK(hipStreamWaitEvent(st, sideOut_, 0));
   }
   noteDone(compute_);
   GLX_TRACE("r%d sync", contextRank_);

@@ -214,6 +214,12 @@ class HipPlanExecutor : public Algorithm {
   int slot_ = 0;
   bool userStream_ = false;
   hipStream_t compute_ = nullptr;
+  // the caller's streams of ptrs[1..] (CudaAllreduceRingChunked's one stream
+  // per pointer, gloo/cuda_allreduce_ring_chunked.cc:53-66): run() orders
+  // itself after their pending work and their later work after its results
+  std::vector<hipStream_t> sideStreams_;
+  std::vector<hipEvent_t> sideIn_;
+  hipEvent_t sideOut_ = nullptr;
   std::vector<CopyStream> copies_;
   uint64_t markEpoch_ = 0;
   int split_ = 1;

@@ -126,6 +126,23 @@ def test_reference_test_grid_single_pointer(algo, P, N):
         assert np.all(out[r][0] == P * (P - 1) // 2), "rank %d" % r
 
 
+# The CUDA algorithms' test grid (gloo/test/cuda_allreduce_test.cc:148-170,
+# 281-309: the same ranks, N without 0) with CudaFixture's values, the stride
+# pattern (gloo/test/base_test.h:184-192) checked for exact equality
+# (checkAllreduceResult, :216-236).
+@pytest.mark.parametrize("algo,P,N", [g for g in REF_GRID if g[2] > 0],
+                         ids=["%s-P%d-N%d" % ("ring_chunked" if a == O.RING_CHUNKED
+                                              else "halving_doubling", P, N)
+                              for a, P, N in REF_GRID if N > 0])
+def test_cuda_test_grid_stride_pattern(algo, P, N):
+    ins = case_inputs(P, N, O.FLOAT32, 1, 1)
+    out = gpu_allreduce(algo, O.SUM, O.FLOAT32, ins)
+    j = np.arange(N, dtype=np.float64)
+    exp = (j * P * P + P * (P - 1) / 2).astype(np.float32)
+    for r in range(P):
+        assert np.array_equal(out[r][0], exp), "rank %d" % r
+
+
 # Beyond 8 ranks with seeded inputs, so the reduction ORDER is checked too
 # (value = rank sums exactly in any order): bit-exact against the oracle.
 @pytest.mark.parametrize("algo,P", [(O.RING_CHUNKED, 11), (O.RING_CHUNKED, 15),
@@ -173,6 +190,71 @@ def test_user_streams(algo):
     ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=21)
     out = gpu_allreduce(algo, O.SUM, O.FLOAT32, ins, runs=2, streams=True)
     check_all(out, O.allreduce(algo, O.SUM, O.FLOAT32, ins), O.FLOAT32, O.SUM)
+
+
+@pytest.mark.parametrize("algo", [O.RING_CHUNKED, O.HALVING_DOUBLING, MESH],
+                         ids=["ring_chunked", "halving_doubling", "mesh"])
+@pytest.mark.parametrize("P,nptrs", [(1, 2), (2, 2), (3, 3), (4, 2)])
+def test_multi_pointer_async_streams(algo, P, nptrs):
+    """gloo/test/cuda_allreduce_test.cc:196-220 (MultiPointerAsync): one stream
+    per pointer; each pointer's values are written on ITS stream behind a
+    delay kernel (cudaSleep, gloo/test/cuda_base_test.h:60-74), nothing
+    synchronises before run(), and the results are read after synchronising
+    the streams (:216-218).  run() must order itself after every pointer's
+    pending work and every stream's later work after the results.  The
+    fixture's stride pattern (gloo/test/base_test.h:184-235) sums exactly."""
+    import gloo_amd
+    N = 3001
+    store = gloo_amd.rendezvous.HashStore()
+    stride = P * nptrs
+    j = np.arange(N, dtype=np.float64)
+    expected = (j * stride * stride + stride * (stride - 1) / 2).astype(np.float32)
+    cls = {O.RING_CHUNKED: lambda *a, **k: gloo_amd.AllreduceRingChunked(*a, schedule="ring", **k),
+           O.HALVING_DOUBLING: gloo_amd.AllreduceHalvingDoubling,
+           MESH: lambda *a, **k: gloo_amd.AllreduceRingChunked(*a, schedule="mesh", **k)}[algo]
+
+    def rank_fn(r):
+        ctx = gloo_amd.rendezvous.Context(r, P, 0)
+        ctx.setTimeout(60)
+        ctx.connectFullMesh(store)
+        ss = [torch.cuda.Stream() for _ in range(nptrs)]
+        bufs = [torch.zeros(N, device="cuda") for _ in range(nptrs)]
+        host = [torch.from_numpy((j * stride + r * nptrs + i).astype(np.float32)).pin_memory()
+                for i in range(nptrs)]
+        torch.cuda.synchronize()
+        alg = cls(ctx, [b.data_ptr() for b in bufs], N, gloo_amd.ReductionFunction.sum,
+                  streams=ss, dtype=O.FLOAT32)
+        for _ in range(2):
+            for i in range(nptrs):
+                with torch.cuda.stream(ss[i]):
+                    bufs[i].zero_()
+                    torch.cuda._sleep(200000)  # the fixture's cudaSleep
+                    bufs[i].copy_(host[i], non_blocking=True)
+            alg.run()
+            for st in ss:
+                st.synchronize()
+            for i in range(nptrs):
+                got = bufs[i].cpu().numpy()
+                assert np.array_equal(got, expected), "rank %d ptr %d" % (r, i)
+        alg.close()
+        return True
+
+    run_ranks(P, rank_fn, timeout=90)
+
+
+def test_streams_must_match_pointers():
+    """CudaAllreduceRingChunked enforces one stream per pointer
+    (gloo/cuda_allreduce_ring_chunked.cc:55-58); one stream is also taken."""
+    import gloo_amd
+    store = gloo_amd.rendezvous.HashStore()
+    ctx = gloo_amd.rendezvous.Context(0, 1, 0)
+    ctx.connectFullMesh(store)
+    bufs = [torch.zeros(100, device="cuda") for _ in range(3)]
+    ss = [torch.cuda.Stream() for _ in range(2)]
+    with pytest.raises(gloo_amd.EnforceNotMet, match="one per pointer"):
+        gloo_amd.AllreduceRingChunked(ctx, [b.data_ptr() for b in bufs], 100,
+                                      gloo_amd.ReductionFunction.sum, streams=ss,
+                                      dtype=O.FLOAT32)
 
 
 def test_back_to_back_without_refill_is_iterated_allreduce():
