@@ -43,6 +43,8 @@ def main():
         return run_device(store_dir, rank, size, algo)
     if algo == "devtimeout":
         return run_device_timeout(store_dir, rank, size)
+    if algo.startswith("killpeer:"):
+        return run_killpeer(store_dir, rank, size, *algo.split(":")[1:])
     if algo == "devsteps":
         return run_devsteps(store_dir, rank, size)
     if algo in ("queued", "queued_kernel"):
@@ -161,6 +163,73 @@ def run_device_timeout(store_dir, rank, size):
             store.get("timeout_done/%s" % sched, timeout_ms=120000)
         torch.cuda.synchronize()  # the kernels that gave up have exited
         alg.close()
+    ctx.close()
+    if not ok:
+        print("MISMATCH rank", rank)
+        sys.exit(1)
+    print("OK")
+
+
+def run_killpeer(store_dir, rank, size, engine, when):
+    """TransportMultiProcTest.IoErrors (gloo/test/transport_test.cc:53-110):
+    rank 0 is SIGKILLed; the survivors' next run() must raise IoException
+    within 2x the timeout.  engine: host (host-issued ring steps), device
+    (the ring's plan kernel), twoshot (the mesh kernel).  when: idle (rank 0
+    dies while the others are already waiting in run()) or mid (rank 0 dies
+    while its own run() is in flight)."""
+    import os
+    import signal
+    import threading
+    import time
+
+    import torch
+
+    import gloo_amd
+
+    T = 3.0
+    store = gloo_amd.rendezvous.FileStore(store_dir)
+    ctx = gloo_amd.rendezvous.Context(rank, size, 0)
+    ctx.setTimeout(T)
+    ctx.connectFullMesh(store)
+    n = 3 << 20  # 16-byte aligned ring chunks at P = 2, 3, 4 (plan-kernel eligible)
+    buf = torch.ones(n, device="cuda")
+    if engine == "twoshot":
+        alg = gloo_amd.AllreduceRingChunked(ctx, [buf], schedule="mesh")
+    else:
+        gloo_amd.set_steps_engine(engine)
+        alg = gloo_amd.AllreduceRingChunked(ctx, [buf], schedule="ring")
+        gloo_amd.set_steps_engine("auto")
+    want = {"host": "steps", "device": "devsteps", "twoshot": "twoshot"}[engine]
+    ok = alg.engine() == want
+    if not ok:
+        print("engine %s, expected %s" % (alg.engine(), want))
+    for _ in range(3):
+        buf.fill_(1.0)
+        torch.cuda.synchronize()
+        alg.run()
+        ok = ok and bool(torch.all(buf == size).item())
+    store.set("warm/%d" % rank, b"1")
+    for r in range(size):
+        store.get("warm/%d" % r, timeout_ms=60000)
+    if rank == 0:
+        if when == "mid":
+            threading.Timer(0.05, lambda: os.kill(os.getpid(), signal.SIGKILL)).start()
+            while True:
+                alg.run()
+        time.sleep(0.5)
+        os.kill(os.getpid(), signal.SIGKILL)
+    t0 = time.time()
+    try:
+        for _ in range(1000):  # 'mid': the peer may finish a few runs first
+            alg.run()
+        print("NO ERROR after the peer died")
+        ok = False
+    except gloo_amd.IoException as e:
+        dt = time.time() - t0
+        print("IoException after %.2f s: %s" % (dt, str(e)[:200]))
+        ok = ok and dt < 2 * T + 1.0
+    torch.cuda.synchronize()  # kernels that gave up have exited
+    alg.close()
     ctx.close()
     if not ok:
         print("MISMATCH rank", rank)

@@ -409,6 +409,38 @@ def test_device_engine_multiprocess(P, mode):
             assert "OK" in outs[r]
 
 
+@pytest.mark.parametrize("P,engine,when", [(2, "host", "idle"), (3, "host", "mid"),
+                                           (3, "device", "idle"), (3, "device", "mid"),
+                                           (3, "twoshot", "idle"), (3, "twoshot", "mid")])
+def test_peer_killed_raises_io_exception(P, engine, when):
+    """Fault injection as TransportMultiProcTest.IoErrors
+    (gloo/test/transport_test.cc:53-110, P in {2,3,4}): rank 0 is SIGKILLed
+    while idle or in the middle of its own run(); every survivor's run()
+    raises IoException within 2x the 3 s timeout (host engine: 'Connection
+    closed by peer' from the liveness check; device engines: the kernels'
+    bounded waits, 'Timed out'), and survivors then close cleanly."""
+    with tempfile.TemporaryDirectory() as d:
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P),
+                                   "killpeer:%s:%s" % (engine, when)],
+                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                 for r in range(P)]
+        outs = []
+        for p in procs:
+            try:
+                o, _ = p.communicate(timeout=120)
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+            outs.append(o.decode(errors="replace"))
+        assert procs[0].returncode == -9, outs[0]
+        for r in range(1, P):
+            print(outs[r])
+            assert procs[r].returncode == 0, "rank %d failed:\n%s" % (r, outs[r])
+            assert "OK" in outs[r]
+
+
 @pytest.mark.parametrize("mode,knob", [("devsteps", "GLOO_AMD_FLAG_WRITE=store"),
                                        ("twoshot", "GLOO_AMD_FLAG_WRITE=store"),
                                        ("oneshot", "GLOO_AMD_FLAG_WRITE=store"),
