@@ -13,6 +13,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <atomic>
+#include <cstdio>
 #include <cstring>
 #include <chrono>
 #include <cstdlib>
@@ -530,13 +531,37 @@ int Context::maxRanksPerDevice() const {
   return most;
 }
 
-void Context::checkPeersAlive() {
+namespace {
+// A killed process stays a zombie until its parent reaps it; kill(pid, 0)
+// still succeeds then, /proc/<pid>/stat says 'Z' (or 'X').
+bool processGone(pid_t pid) {
+  if (::kill(pid, 0) != 0) return errno == ESRCH;
+  char path[64];
+  std::snprintf(path, sizeof(path), "/proc/%d/stat", (int)pid);
+  FILE* f = std::fopen(path, "r");
+  if (f == nullptr) return false;
+  char buf[512];
+  const size_t n = std::fread(buf, 1, sizeof(buf) - 1, f);
+  std::fclose(f);
+  buf[n] = 0;
+  const char* rp = std::strrchr(buf, ')');  // comm may hold spaces and ')'
+  return rp != nullptr && rp[1] == ' ' && (rp[2] == 'Z' || rp[2] == 'X');
+}
+}  // namespace
+
+int Context::deadPeer() const {
   for (const auto& p : peers_) {
     if (p.rank == rank || p.sameProcess || p.pid <= 0) continue;
-    if (::kill(p.pid, 0) != 0 && errno == ESRCH) {
-      GLX_THROW_IO("Connection closed by peer: rank ", p.rank, " (pid ", p.pid,
-                   ") exited");
-    }
+    if (processGone(p.pid)) return p.rank;
+  }
+  return -1;
+}
+
+void Context::checkPeersAlive() {
+  const int r = deadPeer();
+  if (r >= 0) {
+    GLX_THROW_IO("Connection closed by peer: rank ", r, " (pid ", peers_[(size_t)r].pid,
+                 ") exited");
   }
 }
 

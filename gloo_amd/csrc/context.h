@@ -140,6 +140,8 @@ class Context {
 
   // Throws IoException if a peer process has exited.
   void checkPeersAlive();
+  // rank of a peer process that has exited, or -1
+  int deadPeer() const;
 
   // Shared device blocks, pooled per context: an algorithm takes a block
   // (allocated and IPC-exported once, or a free one of a fitting size) and

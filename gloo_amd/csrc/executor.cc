@@ -889,7 +889,7 @@ void HipPlanExecutor::run() {
   noteDone(compute_);
   GLX_TRACE("r%d sync", contextRank_);
   if (!userStream_) {
-    GLX_HIP_CHECK(spinSync(compute_));
+    waitDevice(compute_);
     checkDevice();
   }
   GLX_TRACE("r%d done", contextRank_);
@@ -967,7 +967,7 @@ void HipPlanExecutor::runFn(const FnCall& call) {
   }
   noteDone(compute_);
   if (call.stream == nullptr) {
-    GLX_HIP_CHECK(spinSync(compute_));
+    waitDevice(compute_);
     checkDevice();
   }
 }
@@ -1044,8 +1044,8 @@ void HipPlanExecutor::runFnHostStaged(const FnCall& call) {
     GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, hostDone_, 0));
     copyBack(contextSize_ > 1 ? stage_.d2hRest : std::vector<glx::Range>{{0, count_}});
   }
+  waitDevice(compute_);
   GLX_HIP_CHECK(hipStreamSynchronize(d2h_));
-  GLX_HIP_CHECK(hipStreamSynchronize(compute_));
   GLX_HIP_CHECK(hipStreamSynchronize(h2d_));
   noteDone(d2h_);
   checkDevice();
@@ -1096,7 +1096,7 @@ void HipPlanExecutor::runFnHost(const FnCall& call) {
     GLX_HIP_CHECK(hipMemcpyAsync(p, out0, bytes, hipMemcpyDeviceToHost, compute_));
   }
   noteDone(compute_);
-  GLX_HIP_CHECK(hipStreamSynchronize(compute_));
+  waitDevice(compute_);
   checkDevice();
 }
 
@@ -1367,8 +1367,8 @@ void HipPlanExecutor::runHost() {
       GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, pieceDone_[j], 0));
       copyBack({r});
     }
+    waitDevice(compute_);
     GLX_HIP_CHECK(hipStreamSynchronize(d2h_));
-    GLX_HIP_CHECK(hipStreamSynchronize(compute_));
     GLX_HIP_CHECK(hipStreamSynchronize(h2d_));
     noteDone(d2h_);
     return;
@@ -1387,8 +1387,8 @@ void HipPlanExecutor::runHost() {
     GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, hostDone_, 0));
     copyBack(stage_.d2hRest);
   }
+  waitDevice(compute_);
   GLX_HIP_CHECK(hipStreamSynchronize(d2h_));
-  GLX_HIP_CHECK(hipStreamSynchronize(compute_));
   GLX_HIP_CHECK(hipStreamSynchronize(h2d_));
   noteDone(d2h_);
   checkDevice();
@@ -1962,6 +1962,41 @@ void HipPlanExecutor::buildDevSteps() {
   pk_.foldSrc = devFoldSrc_;
   pk_.nsteps = (int)plan_.steps.size();
   pk_.slots = slots_;
+}
+
+void HipPlanExecutor::waitDevice(hipStream_t s) {
+  if (engine_ == kEngineSteps || ddStatus_ == nullptr || contextSize_ == 1) {
+    GLX_HIP_CHECK(spinSync(s));
+    return;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  auto lastAlive = t0;
+  for (uint64_t spin = 1;; spin++) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e != hipErrorNotReady) {
+      GLX_HIP_CHECK(e);
+      return;
+    }
+    if ((spin & 63) == 0) {
+      const auto now = std::chrono::steady_clock::now();
+      if (now - lastAlive > std::chrono::milliseconds(100)) {
+        lastAlive = now;
+        const int dead = context_->deadPeer();
+        if (dead >= 0) {
+          // every kernel wait polls this word and gives up; the launch drains
+          *reinterpret_cast<volatile int*>(ddStatus_) = 1 + dead;
+          (void)hipStreamSynchronize(s);
+          broken_ = true;
+          context_->checkPeersAlive();  // throws IoException naming the rank
+        }
+      }
+    }
+    if (spin > 4096) {
+      sched_yield();
+    } else {
+      _mm_pause();
+    }
+  }
 }
 
 void HipPlanExecutor::checkDevice() {

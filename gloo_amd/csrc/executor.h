@@ -342,6 +342,10 @@ class HipPlanExecutor : public Algorithm {
   void buildDevSteps();
   void runDevice(char* ptr0);
   void checkDevice();
+  // Wait for stream s after a device-engine launch.  While waiting, watch
+  // the peers' processes: if one exits, stop every kernel wait at once
+  // (status word) and throw IoException instead of running into the timeout.
+  void waitDevice(hipStream_t s);
   // Queued steps engine: the host-issued engine's step loop with every wait
   // on a peer and every counter write as a stream-ordered launch on device
   // flag rows (one flag each: deliveries, credits, then one local copy

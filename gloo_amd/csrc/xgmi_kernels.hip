@@ -313,10 +313,16 @@ __device__ __forceinline__ bool wait_flag(const uint64_t* word, uint64_t epoch, 
   if (threadIdx.x == 0) {
     int ok = 1;
     uint64_t v;
-    while ((v = poll_flag(word, pollLoad)) < epoch) {
+    for (uint32_t spin = 1; (v = poll_flag(word, pollLoad)) < epoch; spin++) {
       if (__builtin_amdgcn_s_memrealtime() - start > timeoutTicks) {
         ok = 0;
         report_timeout(status, claim, 1 + peer + 256 * where, v, epoch);
+        break;
+      }
+      // the status word is host memory: nonzero once another wait gave up or
+      // the host saw a peer process exit (it then stops every wait at once)
+      if ((spin & 127) == 0 && *reinterpret_cast<const volatile int*>(status) != 0) {
+        ok = 0;
         break;
       }
       __builtin_amdgcn_s_sleep(2);
