@@ -416,6 +416,9 @@ def busiest_link_bytes(gloo_amd, algo, rank, world, count, es):
     return max(per_peer.values()) if per_peer else 0
 
 
+P50 = {}  # algo -> p50 seconds per run (max over ranks) of its last timing
+
+
 def time_schedule(torch, dist, gloo_amd, ctx, buf, algo, steps, warmup):
     """warmup untimed runs, then `steps` timed runs between barriers +
     device syncs; returns (max-over-ranks seconds per step, link bytes/run)."""
@@ -429,13 +432,21 @@ def time_schedule(torch, dist, gloo_amd, ctx, buf, algo, steps, warmup):
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    marks = []
     for _ in range(steps):
-        alg.run()
+        alg.run()  # returns with the results complete (no caller stream)
+        marks.append(time.perf_counter())
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     dist.barrier()
     el = torch.tensor([t1 - t0], dtype=torch.float64)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    # the reference benchmark's p50 (gloo/benchmark/runner.cc:470-510): this
+    # rank's median run, max over ranks
+    per = sorted(b - a for a, b in zip([t0] + marks[:-1], marks))
+    med = torch.tensor([per[len(per) // 2] if per else 0.0], dtype=torch.float64)
+    dist.all_reduce(med, op=dist.ReduceOp.MAX)
+    P50[algo] = med.item()
     sent = alg.bytes_sent()
     TRANSPORT[algo] = alg.transport_stats()
     alg.close()
@@ -703,6 +714,7 @@ def bench_multi(args):
         buf.copy_(src)
         torch.cuda.synchronize()
         t, sent = time_schedule(torch, dist, gloo_amd, ctx, buf, algo, steps, args.warmup)
+        p50 = P50[algo]  # the sweep re-times the same names at other sizes later
         # correctness after the timing: one run on fresh inputs; every rank
         # must hold the same bits (the reduction order is rank-independent)
         buf.copy_(src)
@@ -712,7 +724,7 @@ def bench_multi(args):
         torch.cuda.synchronize()
         alg.close()
         result = buf.clone()
-        return {"t": t, "sent": sent,
+        return {"t": t, "sent": sent, "p50": p50,
                 "transport": ("device-driven kernel stores (%s)" % ENGINES[algo]
                               if device_engine else tname(best) +
                               (" (queued)" if ENGINES[algo] == "queued" else "")), "tr": best,
@@ -780,6 +792,7 @@ def bench_multi(args):
         lm = busiest_link_bytes(gloo_amd, a, rank, world, n, es)
         alts[a] = {"value": round(world * S / runs[a]["t"] / 1e9, 3),
                    "ms_per_step": round(runs[a]["t"] * 1e3, 4),
+                   "p50_ms_per_step": round(runs[a]["p50"] * 1e3, 4),
                    "algbw_GBps": round(S / runs[a]["t"] / 1e9, 3),
                    "bytes_sent_per_step": runs[a]["sent"], "transport": runs[a]["transport"],
                    "engine": ENGINES.get(a),
@@ -797,10 +810,12 @@ def bench_multi(args):
                 failed[other] = err or "failed on another rank"
                 continue
             ta, sent_a = got
+            p50_a = P50[other]
             lm = busiest_link_bytes(gloo_amd, other, rank, world, n, es)
             eng = ENGINES.get(other)
             alts[other] = {"value": round(world * S / ta / 1e9, 3),
                            "ms_per_step": round(ta * 1e3, 4),
+                           "p50_ms_per_step": round(p50_a * 1e3, 4),
                            "algbw_GBps": round(S / ta / 1e9, 3),
                            "bytes_sent_per_step": sent_a, "engine": eng,
                            "transport": ("device-driven kernel stores (%s)" % eng
@@ -869,6 +884,8 @@ def bench_multi(args):
                        "baseline_config": "configs[3]" if args.algo == "halving_doubling"
                        else "configs[2]"},
             "algbw_GBps": round(algbw, 3), "busbw_GBps": round(busbw, 3),
+            "algbw_GiBps": round(S / t / 2 ** 30, 3),
+            "p50_ms_per_step": round(runs[chosen]["p50"] * 1e3, 4),
             # the collective's own bound: its busiest xGMI link (the ring puts
             # all 1.75 S on rank -> rank+1), with the step's HBM bytes beside it
             "roofline": {"bound": "xgmi_link", "achieved": round(link_ach, 2),
