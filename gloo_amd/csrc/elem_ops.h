@@ -32,6 +32,35 @@ __device__ __forceinline__ void st16(v4u* p, v4u v) {
   }
 }
 
+// Write-through store (`sc1`): the line leaves this XCD's L2 with the store
+// instead of staying dirty there until an eviction writes it back.  For a
+// stream written once this is the fastest store (tools/scratch/store_policy.hip).
+// A vector-memory store like any other: later s_waitcnt vmcnt covers it.
+__device__ __forceinline__ void st16_wt(v4u* p, v4u v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+
+// Cache policy of a streaming kernel's loads and stores.
+enum StreamPolicy : int {
+  kPolPlain = 0,    // plain loads, plain stores
+  kPolNt = 1,       // nontemporal loads and stores
+  kPolNtWt = 2,     // nontemporal loads, write-through stores
+  kPolNtPlain = 3,  // nontemporal loads, plain stores
+};
+
+template <int POL>
+__device__ __forceinline__ v4u ld16p(const v4u* p) {
+  return ld16<POL != kPolPlain>(p);
+}
+template <int POL>
+__device__ __forceinline__ void st16p(v4u* p, v4u v) {
+  if (POL == kPolNtWt) {
+    st16_wt(p, v);
+  } else {
+    st16<POL == kPolNt>(p, v);
+  }
+}
+
 // ---- scalar element ops on storage types ---------------------------------
 
 __device__ __forceinline__ float h2f(uint16_t h) {

@@ -41,7 +41,7 @@ namespace {
 // dst may alias a or b: every lane reads its vectors before writing them.
 // LOADC: dst is not a, and its prior value matters (float16 assignment
 // semantics) -- read it as a third stream.
-template <typename T, int OP, int UNROLL, bool LOADC, bool NT>
+template <typename T, int OP, int UNROLL, bool LOADC, int POL>
 __global__ __launch_bounds__(kBlock) void reduce_kernel(
     typename Elem<T, OP>::S* dst, const typename Elem<T, OP>::S* a,
     const typename Elem<T, OP>::S* b, size_t head, size_t nvec, size_t tail) {
@@ -67,8 +67,8 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(
     for (int u = 0; u < UNROLL; u++) {
       size_t i = base + (size_t)u * kBlock;
       if (i < nvec) {
-        x[u] = ld16<NT>(va + i);
-        y[u] = ld16<NT>(vb + i);
+        x[u] = ld16p<POL>(va + i);
+        y[u] = ld16p<POL>(vb + i);
         if (LOADC) z[u] = vd[i];
       }
     }
@@ -76,7 +76,7 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(
     for (int u = 0; u < UNROLL; u++) {
       size_t i = base + (size_t)u * kBlock;
       if (i < nvec) {
-        st16<NT>(vd + i, LOADC ? vec_apply3<T, OP>(z[u], x[u], y[u]) : vec_apply<T, OP>(x[u], y[u]));
+        st16p<POL>(vd + i, LOADC ? vec_apply3<T, OP>(z[u], x[u], y[u]) : vec_apply<T, OP>(x[u], y[u]));
       }
     }
   }
@@ -259,7 +259,21 @@ int g_copy_blocks = 64;  // grid of the copy kernel (workgroups)
 int g_unroll = 4;         // tuned on MI355X: tools/tune_reduce.py, profiles/r1_tune_reduce_nt.log
 int g_blocks_per_cu = 64; // grid cap = CUs * this (256 MiB fp32: one vector pass per lane)
 int g_num_cus = 0;
-bool g_nontemporal = true;  // nt loads/stores: 123 us vs 137 us at 256 MiB
+// Cache policy of the reduce kernel's streams (StreamPolicy, or kPolAuto).
+// Measured on MI355X with uniform random fp32 (tools/tune_policy.py,
+// profiles/r4j_*, r4k_*): nontemporal loads always win; for the stores,
+// write-through (sc1) is fastest while the written stream fits the 256 MB
+// Infinity Cache (64 MiB: 28.0 vs 31.5 us; 256 MiB: 110.5 vs 123.7 us), and
+// nontemporal stores are fastest beyond it (320 MiB: 161.9 vs 163.7 us;
+// 1 GiB: 527 vs 543 us).
+constexpr int kPolAuto = 4;
+int g_policy = kPolAuto;
+size_t g_wt_max_bytes = size_t(256) << 20;  // per stream, write-through up to here
+
+int policy_for(size_t stream_bytes) {
+  if (g_policy != kPolAuto) return g_policy;
+  return stream_bytes <= g_wt_max_bytes ? kPolNtWt : kPolNt;
+}
 
 int num_cus() {
   if (g_num_cus == 0) {
@@ -292,18 +306,28 @@ hipError_t launch_vec(void* dst, const void* a, const void* b, size_t head,
   size_t blocks = grid_for(nvec, UNROLL);
   size_t edge_blocks = (std::max(head, tail) + kBlock - 1) / kBlock;
   if (blocks < edge_blocks) blocks = edge_blocks;
+  const dim3 grid((unsigned)blocks), block(kBlock);
   if (std::is_same<T, f16_t>::value && dst != a) {
-    hipLaunchKernelGGL((reduce_kernel<T, OP, UNROLL, true, false>), dim3((unsigned)blocks),
-                       dim3(kBlock), 0, s, (S*)dst, (const S*)a, (const S*)b, head,
-                       nvec, tail);
-  } else if (g_nontemporal) {
-    hipLaunchKernelGGL((reduce_kernel<T, OP, UNROLL, false, true>), dim3((unsigned)blocks),
-                       dim3(kBlock), 0, s, (S*)dst, (const S*)a, (const S*)b, head,
-                       nvec, tail);
-  } else {
-    hipLaunchKernelGGL((reduce_kernel<T, OP, UNROLL, false, false>), dim3((unsigned)blocks),
-                       dim3(kBlock), 0, s, (S*)dst, (const S*)a, (const S*)b, head,
-                       nvec, tail);
+    hipLaunchKernelGGL((reduce_kernel<T, OP, UNROLL, true, kPolPlain>), grid, block, 0, s,
+                       (S*)dst, (const S*)a, (const S*)b, head, nvec, tail);
+    return hipGetLastError();
+  }
+  switch (policy_for(nvec * 16)) {
+    case kPolPlain:
+      hipLaunchKernelGGL((reduce_kernel<T, OP, UNROLL, false, kPolPlain>), grid, block, 0, s,
+                         (S*)dst, (const S*)a, (const S*)b, head, nvec, tail);
+      break;
+    case kPolNtWt:
+      hipLaunchKernelGGL((reduce_kernel<T, OP, UNROLL, false, kPolNtWt>), grid, block, 0, s,
+                         (S*)dst, (const S*)a, (const S*)b, head, nvec, tail);
+      break;
+    case kPolNtPlain:
+      hipLaunchKernelGGL((reduce_kernel<T, OP, UNROLL, false, kPolNtPlain>), grid, block, 0, s,
+                         (S*)dst, (const S*)a, (const S*)b, head, nvec, tail);
+      break;
+    default:
+      hipLaunchKernelGGL((reduce_kernel<T, OP, UNROLL, false, kPolNt>), grid, block, 0, s,
+                         (S*)dst, (const S*)a, (const S*)b, head, nvec, tail);
   }
   return hipGetLastError();
 }
@@ -564,7 +588,7 @@ hipError_t launch_reduce_n(int op, int dtype, void* dst, const void* const* srcs
 void set_reduce_tuning(int unroll, int blocks_per_cu, int nontemporal) {
   if (unroll == 1 || unroll == 2 || unroll == 4 || unroll == 8) g_unroll = unroll;
   if (blocks_per_cu > 0) g_blocks_per_cu = blocks_per_cu;
-  if (nontemporal >= 0) g_nontemporal = nontemporal != 0;
+  if (nontemporal >= 0 && nontemporal <= kPolAuto) g_policy = nontemporal;
 }
 
 }  // namespace glx

@@ -125,7 +125,11 @@ int glx_enable_peer(int dev_a, int dev_b);
 
 /* Tuning hook of the reduce kernel: lanes' unroll depth (1, 2, 4 or 8 16-byte
  * vectors in flight per lane), grid cap in workgroups per CU (0 = keep) and
- * nontemporal streaming loads/stores (0 off, 1 on, -1 keep). */
+ * the cache policy of its streams (`nontemporal`; -1 keep): 0 plain loads and
+ * stores, 1 nontemporal loads and stores, 2 nontemporal loads and
+ * write-through (sc1) stores, 3 nontemporal loads and plain stores, 4 auto
+ * (default: 2 while one stream is at most 256 MiB -- the Infinity Cache's
+ * size -- and 1 above). */
 int glx_tune_reduce(int unroll, int blocks_per_cu, int nontemporal);
 
 /* Split every peer copy of algorithms created afterwards over k streams per
