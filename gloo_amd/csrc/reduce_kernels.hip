@@ -23,6 +23,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 #include <vector>
 
@@ -110,7 +111,7 @@ __device__ __forceinline__ typename Elem<T, OP>::S fold_step(typename Elem<T, OP
   return REV ? Elem<T, OP>::apply(y, acc) : Elem<T, OP>::apply(acc, y);
 }
 
-template <typename T, int OP, int UNROLL, bool REV>
+template <typename T, int OP, int UNROLL, bool REV, bool WT>
 __global__ __launch_bounds__(kBlock) void reduce_n_kernel(
     typename Elem<T, OP>::S* dst, SrcPtrs srcs, int k, size_t head, size_t nvec,
     size_t tail) {
@@ -153,7 +154,13 @@ __global__ __launch_bounds__(kBlock) void reduce_n_kernel(
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) {
       size_t i = base + (size_t)u * kBlock;
-      if (i < nvec) st16<true>(vd + i, acc[u]);
+      if (i < nvec) {
+        if (WT) {
+          st16_wt(vd + i, acc[u]);
+        } else {
+          st16<true>(vd + i, acc[u]);
+        }
+      }
     }
   }
 }
@@ -216,9 +223,10 @@ __global__ __launch_bounds__(kBlock) void reduce_n_scalar_kernel(
 // the sending GPU store 16-byte vectors straight into the peer's receive
 // region through its IPC-mapped address, so the copy runs over xGMI at the
 // rate of the compute units' remote stores rather than one copy engine's.
-// Nontemporal loads (the source is read once); plain stores (they leave the
-// GPU).  The first lanes move the unaligned head and tail bytes.
-template <int UNROLL>
+// Nontemporal loads (the source is read once); write-through or plain
+// stores by the stream policy (policy_for).  The first lanes move the
+// unaligned head and tail bytes.
+template <int UNROLL, bool WT>
 __global__ __launch_bounds__(kBlock) void copy_kernel(char* __restrict__ dst,
                                                       const char* __restrict__ src,
                                                       size_t head, size_t nvec, size_t tail) {
@@ -240,7 +248,13 @@ __global__ __launch_bounds__(kBlock) void copy_kernel(char* __restrict__ dst,
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) {
       size_t i = base + (size_t)u * kBlock;
-      if (i < nvec) st16<false>(vd + i, x[u]);
+      if (i < nvec) {
+        if (WT) {
+          st16_wt(vd + i, x[u]);
+        } else {
+          st16<false>(vd + i, x[u]);
+        }
+      }
     }
   }
 }
@@ -273,6 +287,21 @@ size_t g_wt_max_bytes = size_t(256) << 20;  // per stream, write-through up to h
 int policy_for(size_t stream_bytes) {
   if (g_policy != kPolAuto) return g_policy;
   return stream_bytes <= g_wt_max_bytes ? kPolNtWt : kPolNt;
+}
+
+// Write-through stores for the fold (reduce_n) and copy kernels: -1 by
+// policy_for, 0 never (fold: nontemporal, copy: plain stores), 1 always.
+// GLOO_AMD_FOLD_WT / GLOO_AMD_COPY_WT (measurement knobs).
+int env_wt(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e == nullptr ? dflt : std::atoi(e);
+}
+const int g_fold_wt = env_wt("GLOO_AMD_FOLD_WT", -1);
+const int g_copy_wt = env_wt("GLOO_AMD_COPY_WT", -1);
+
+bool use_wt(int knob, size_t stream_bytes) {
+  if (knob >= 0) return knob != 0;
+  return policy_for(stream_bytes) == kPolNtWt;
 }
 
 int num_cus() {
@@ -393,8 +422,13 @@ hipError_t launch_n_pass(void* dst, const void* const* srcs, int k, size_t n,
   size_t blocks = grid_for(nvec, 4);
   size_t edge_blocks = (std::max(head, tail) + kBlock - 1) / kBlock;
   if (blocks < edge_blocks) blocks = edge_blocks;
-  hipLaunchKernelGGL((reduce_n_kernel<T, OP, 4, REV>), dim3((unsigned)blocks),
-                     dim3(kBlock), 0, s, (S*)dst, sp, k, head, nvec, tail);
+  if (use_wt(g_fold_wt, nvec * 16)) {
+    hipLaunchKernelGGL((reduce_n_kernel<T, OP, 4, REV, true>), dim3((unsigned)blocks),
+                       dim3(kBlock), 0, s, (S*)dst, sp, k, head, nvec, tail);
+  } else {
+    hipLaunchKernelGGL((reduce_n_kernel<T, OP, 4, REV, false>), dim3((unsigned)blocks),
+                       dim3(kBlock), 0, s, (S*)dst, sp, k, head, nvec, tail);
+  }
   return hipGetLastError();
 }
 
@@ -515,8 +549,13 @@ hipError_t launch_copy_blocks(void* dst, const void* src, size_t bytes, int grid
   if (head > bytes) head = bytes;
   const size_t nvec = (bytes - head) / 16;
   const size_t tail = bytes - head - nvec * 16;
-  hipLaunchKernelGGL((copy_kernel<4>), dim3(blocks), dim3(kBlock), 0, s, (char*)dst,
-                     (const char*)src, head, nvec, tail);
+  if (use_wt(g_copy_wt, nvec * 16)) {
+    hipLaunchKernelGGL((copy_kernel<4, true>), dim3(blocks), dim3(kBlock), 0, s, (char*)dst,
+                       (const char*)src, head, nvec, tail);
+  } else {
+    hipLaunchKernelGGL((copy_kernel<4, false>), dim3(blocks), dim3(kBlock), 0, s, (char*)dst,
+                       (const char*)src, head, nvec, tail);
+  }
   return hipGetLastError();
 }
 
