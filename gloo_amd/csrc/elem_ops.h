@@ -32,13 +32,26 @@ __device__ __forceinline__ void st16(v4u* p, v4u v) {
   }
 }
 
-// Write-through store (`sc1`): the line leaves this XCD's L2 with the store
-// instead of staying dirty there until an eviction writes it back.  For a
-// stream written once this is the fastest store (tools/scratch/store_policy.hip).
-// A vector-memory store like any other: later s_waitcnt vmcnt covers it.
-__device__ __forceinline__ void st16_wt(v4u* p, v4u v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
+// Write-through stores (`sc1`): the line leaves this XCD's L2 with the store
+// instead of staying dirty there until an eviction writes it back; for a
+// stream written once that fits the Infinity Cache this is the fastest store
+// (tools/scratch/store_policy.hip, tools/tune_policy.py).  HIP has no global
+// store builtin with that cache policy, so the stream is written through a
+// buffer resource over its base (a compiler builtin, not inline asm: the
+// compiler then tracks the store for waitcnts and register hazards).
+// Offsets are 32-bit: a stream must stay below 2 GiB (kWtMaxStream).
+constexpr size_t kWtMaxStream = (size_t(1) << 31) - 16;
+struct WtStream {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ explicit WtStream(void* base)
+      // raw buffer, no stride, every byte below 2 GiB in range; dword3 of
+      // the descriptor as every gfx9-family part takes it
+      : r(__builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000)) {}
+  // 16-byte vector i of the stream; cache policy 16 = sc1 (gfx940 family)
+  __device__ __forceinline__ void put(size_t i, v4u v) const {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (unsigned)(i * 16), 0, 16);
+  }
+};
 
 // Cache policy of a streaming kernel's loads and stores.
 enum StreamPolicy : int {
@@ -52,14 +65,7 @@ template <int POL>
 __device__ __forceinline__ v4u ld16p(const v4u* p) {
   return ld16<POL != kPolPlain>(p);
 }
-template <int POL>
-__device__ __forceinline__ void st16p(v4u* p, v4u v) {
-  if (POL == kPolNtWt) {
-    st16_wt(p, v);
-  } else {
-    st16<POL == kPolNt>(p, v);
-  }
-}
+
 
 // ---- scalar element ops on storage types ---------------------------------
 

@@ -60,6 +60,7 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(
   v4u* vd = reinterpret_cast<v4u*>(dst + head);
   const v4u* va = reinterpret_cast<const v4u*>(a + head);
   const v4u* vb = reinterpret_cast<const v4u*>(b + head);
+  const WtStream wt(vd);
   const size_t step = (size_t)gridDim.x * kBlock * UNROLL;
   for (size_t base = (size_t)blockIdx.x * kBlock * UNROLL + threadIdx.x;
        base < nvec; base += step) {
@@ -77,7 +78,12 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(
     for (int u = 0; u < UNROLL; u++) {
       size_t i = base + (size_t)u * kBlock;
       if (i < nvec) {
-        st16p<POL>(vd + i, LOADC ? vec_apply3<T, OP>(z[u], x[u], y[u]) : vec_apply<T, OP>(x[u], y[u]));
+        const v4u r = LOADC ? vec_apply3<T, OP>(z[u], x[u], y[u]) : vec_apply<T, OP>(x[u], y[u]);
+        if (POL == kPolNtWt) {
+          wt.put(i, r);
+        } else {
+          st16<POL == kPolNt>(vd + i, r);
+        }
       }
     }
   }
@@ -129,6 +135,7 @@ __global__ __launch_bounds__(kBlock) void reduce_n_kernel(
     dst[i] = acc;
   }
   v4u* vd = reinterpret_cast<v4u*>(dst + head);
+  const WtStream wt(vd);
   const size_t step = (size_t)gridDim.x * kBlock * UNROLL;
   for (size_t base = (size_t)blockIdx.x * kBlock * UNROLL + threadIdx.x;
        base < nvec; base += step) {
@@ -156,7 +163,7 @@ __global__ __launch_bounds__(kBlock) void reduce_n_kernel(
       size_t i = base + (size_t)u * kBlock;
       if (i < nvec) {
         if (WT) {
-          st16_wt(vd + i, acc[u]);
+          wt.put(i, acc[u]);
         } else {
           st16<true>(vd + i, acc[u]);
         }
@@ -236,6 +243,7 @@ __global__ __launch_bounds__(kBlock) void copy_kernel(char* __restrict__ dst,
   if (gtid < tail) dst[tail_at + gtid] = src[tail_at + gtid];
   const v4u* vs = reinterpret_cast<const v4u*>(src + head);
   v4u* vd = reinterpret_cast<v4u*>(dst + head);
+  const WtStream wt(vd);
   const size_t stride = (size_t)gridDim.x * kBlock * UNROLL;
   for (size_t base = (size_t)blockIdx.x * kBlock * UNROLL + threadIdx.x; base < nvec;
        base += stride) {
@@ -250,7 +258,7 @@ __global__ __launch_bounds__(kBlock) void copy_kernel(char* __restrict__ dst,
       size_t i = base + (size_t)u * kBlock;
       if (i < nvec) {
         if (WT) {
-          st16_wt(vd + i, x[u]);
+          wt.put(i, x[u]);
         } else {
           st16<false>(vd + i, x[u]);
         }
@@ -285,7 +293,10 @@ int g_policy = kPolAuto;
 size_t g_wt_max_bytes = size_t(256) << 20;  // per stream, write-through up to here
 
 int policy_for(size_t stream_bytes) {
-  if (g_policy != kPolAuto) return g_policy;
+  if (g_policy != kPolAuto) {
+    // write-through streams are addressed by 32-bit buffer offsets
+    return g_policy == kPolNtWt && stream_bytes > kWtMaxStream ? kPolNt : g_policy;
+  }
   return stream_bytes <= g_wt_max_bytes ? kPolNtWt : kPolNt;
 }
 
@@ -300,6 +311,7 @@ const int g_fold_wt = env_wt("GLOO_AMD_FOLD_WT", -1);
 const int g_copy_wt = env_wt("GLOO_AMD_COPY_WT", -1);
 
 bool use_wt(int knob, size_t stream_bytes) {
+  if (stream_bytes > kWtMaxStream) return false;
   if (knob >= 0) return knob != 0;
   return policy_for(stream_bytes) == kPolNtWt;
 }
