@@ -495,19 +495,39 @@ def link_ceiling(torch, dist, gloo_amd, dev, rank, world, nbytes=64 << 20, reps=
     by hipMemcpyPeerAsync (dma, one stream per destination) and by the kernel
     transport's copy kernel (kernel, 256 workgroups over the destinations).
     Per-link GB/s = bytes on the busiest link / max-over-ranks time."""
+    def agreed(ok):  # every rank takes the same branch after a local failure
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        return bool(flag.item())
+
+    def attempt(fn):
+        try:
+            return fn(), None
+        except Exception as e:  # noqa: BLE001 - reported, and agreed on below
+            return None, "%s: %s" % (type(e).__name__, str(e)[:200])
+
     recv = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     send = torch.empty(nbytes, dtype=torch.uint8, device=dev).fill_(rank & 0xFF)
     torch.cuda.synchronize()
+    share, err = attempt(lambda: recv.untyped_storage()._share_cuda_())
     handles = [None] * world
-    dist.all_gather_object(handles, recv.untyped_storage()._share_cuda_())
+    dist.all_gather_object(handles, share)
     peers = {}
-    try:
+
+    def open_peers():
         for k in range(world):
             if k != rank:
                 peers[k] = torch.UntypedStorage._new_shared_cuda(*handles[k])
+    if err is None and all(h is not None for h in handles):
+        _, err = attempt(open_peers)
+    else:
+        err = err or "a peer could not export its buffer"
+    out = {"bytes_per_rep": nbytes, "reps": reps}
+    try:
+        if not agreed(err is None):
+            raise RuntimeError(err or "failed on another rank")
         streams = [torch.cuda.Stream(dev) for _ in range(world - 1)]
         piece = (nbytes // max(1, world - 1)) & ~4095
-        out = {"bytes_per_rep": nbytes, "reps": reps}
         for pattern in ("ring", "mesh"):
             if pattern == "mesh" and world <= 2:
                 continue  # one peer: the mesh is the ring
@@ -519,7 +539,7 @@ def link_ceiling(torch, dist, gloo_amd, dev, rank, world, nbytes=64 << 20, reps=
                             for i, j in enumerate(k for k in range(world) if k != rank)]
                 blocks = max(32, 256 // len(jobs))
 
-                def issue():
+                def issue(jobs=jobs, eng=eng, blocks=blocks):
                     for j, off, ln, st in jobs:
                         dptr = peers[j].data_ptr() + off
                         if eng == "dma":
@@ -527,22 +547,36 @@ def link_ceiling(torch, dist, gloo_amd, dev, rank, world, nbytes=64 << 20, reps=
                                                dev.index, ln, st)
                         else:
                             gloo_amd.kernel_copy(dptr, send.data_ptr(), ln, blocks, st)
-                issue()  # warm: maps, peer access, first-touch
-                torch.cuda.synchronize()
+
+                def warm(issue=issue):
+                    issue()
+                    torch.cuda.synchronize()
+
+                _, err = attempt(warm)  # maps, peer access, first-touch
+                if not agreed(err is None):
+                    out["%s_%s" % (pattern, eng)] = err or "failed on another rank"
+                    continue
                 dist.barrier()
                 t0 = time.perf_counter()
-                for _ in range(reps):
-                    issue()
-                torch.cuda.synchronize()
+
+                def timed(issue=issue):
+                    for _ in range(reps):
+                        issue()
+                    torch.cuda.synchronize()
+                _, err = attempt(timed)
                 el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
                 dist.all_reduce(el, op=dist.ReduceOp.MAX)
-                link_bytes = jobs[0][2]
-                out["%s_%s_GBps" % (pattern, eng)] = round(link_bytes * reps / el.item() / 1e9, 2)
+                if not agreed(err is None):
+                    out["%s_%s" % (pattern, eng)] = err or "failed on another rank"
+                    continue
+                out["%s_%s_GBps" % (pattern, eng)] = round(jobs[0][2] * reps / el.item() / 1e9, 2)
         return out
     finally:
-        torch.cuda.synchronize()
-        peers.clear()
-        dist.barrier()  # nobody frees its buffer while a peer still maps it
+        try:
+            torch.cuda.synchronize()
+        finally:
+            peers.clear()
+            dist.barrier()  # nobody frees its buffer while a peer still maps it
 
 
 def host_endpoint_rate(torch, dist, gloo_amd, ctx, src, dev_result, algo, reps):
