@@ -58,8 +58,9 @@ def set_mesh_engine(engine):
 def set_steps_engine(engine):
     """Engine of ring / halving-doubling / bcube / function-style ring
     algorithms created afterwards when the ranks are on distinct devices or
-    processes: "auto" (default: the plan kernel up to 32 MiB per rank,
-    host-issued steps above), "device" (the plan kernel, one device-driven
+    processes: "auto" (default: the plan kernel; at every size with one rank
+    per GPU, up to 32 MiB per rank when ranks share a GPU, host-issued steps
+    above), "device" (the plan kernel, one device-driven
     launch per rank), "host" (host-issued steps) or "queued" (host-issued
     steps enqueued at once, their waits on peers stream-ordered on device
     flags: no host round trip per hop).  Same results either way."""

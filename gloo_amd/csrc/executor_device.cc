@@ -113,7 +113,14 @@ int HipPlanExecutor::engineFor(const Context& ctx, int algo, int64_t count, int 
       algo == glx::ALGO_FN_RING || algo == glx::ALGO_FN_BCUBE) {
     const int e = stepsEngine();
     if (e >= 0) return e;
-    // auto: the plan kernel for small and medium buffers
+    // auto: the plan kernel, at every size when every rank has a GPU of its
+    // own (it takes the host's round trip out of each of the ring's 4P-4
+    // dependent hops); with ranks sharing a GPU (rehearsals)
+    // only up to devStepsMaxBytes(), where it was measured faster there.
+    // Every rank sees every endpoint, so all choose alike.
+    if (ctx.maxRanksPerDevice() == 1 && std::getenv("GLOO_AMD_DEVSTEPS_MAX_BYTES") == nullptr) {
+      return kEngineDevSteps;
+    }
     return count * esize <= devStepsMaxBytes() ? kEngineDevSteps : kEngineSteps;
   }
   return kEngineSteps;

@@ -155,8 +155,9 @@ int glx_set_mesh_engine(int engine);
 int glx_set_device_engines(int mode);
 /* Engine of the ring, halving-doubling, bcube and function-style ring
  * schedules for algorithms created afterwards, when device-driven engines
- * are available: -1 = by size (default: the plan kernel up to 32 MiB per
- * rank, env GLOO_AMD_DEVSTEPS_MAX_BYTES, host-issued steps above),
+ * are available: -1 = automatic (default: the plan kernel -- at every size
+ * with one rank per GPU, up to 32 MiB per rank when ranks share a GPU or
+ * env GLOO_AMD_DEVSTEPS_MAX_BYTES is set, host-issued steps above),
  * GLX_ENGINE_DEVSTEPS (the plan kernel), GLX_ENGINE_STEPS (host-issued
  * steps) or GLX_ENGINE_QUEUED (host-issued steps, stream-ordered waits).
  * Env GLOO_AMD_STEPS_ENGINE=device|host|queued. */
