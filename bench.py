@@ -407,7 +407,7 @@ def plan_name(algo):
 def make_alg(gloo_amd, ctx, buf, algo):
     """With the ranks on distinct devices/processes: ring_chunked and
     halving_doubling run their step programs in the plan kernel (devsteps) at
-    every size up to 4 ranks, ring_chunked_mesh on the two-shot kernel, ring_chunked_repl on
+    every size and P, ring_chunked_mesh on the two-shot kernel, ring_chunked_repl on
     the one-shot kernel.  *_host and ring_chunked_mesh_steps are the same
     schedules with host-issued steps (calibrated peer-copy transport), *_queued
     the same steps enqueued at once with stream-ordered waits on peers."""
