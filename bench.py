@@ -397,7 +397,7 @@ CHECKS = {}  # bench name -> result_check() of its post-timing run
 
 def plan_name(algo):
     """Schedule name of a bench candidate for gloo_amd.plan()."""
-    for suffix in ("_host", "_queued"):
+    for suffix in ("_host", "_queued", "_fast"):
         if algo.endswith(suffix):
             algo = algo[:-len(suffix)]
     return {"ring_chunked_mesh_steps": "ring_chunked_mesh",
@@ -410,7 +410,15 @@ def make_alg(gloo_amd, ctx, buf, algo):
     every size and P, ring_chunked_mesh on the two-shot kernel, ring_chunked_repl on
     the one-shot kernel.  *_host and ring_chunked_mesh_steps are the same
     schedules with host-issued steps (calibrated peer-copy transport), *_queued
-    the same steps enqueued at once with stream-ordered waits on peers."""
+    the same steps enqueued at once with stream-ordered waits on peers;
+    *_fast the plan kernel with nontemporal loads and write-through stores
+    (set_engine_streams)."""
+    if algo.endswith("_fast"):
+        gloo_amd.set_engine_streams("fast")
+        try:
+            return make_alg(gloo_amd, ctx, buf, algo[:-len("_fast")])
+        finally:
+            gloo_amd.set_engine_streams("plain")
     engine = None
     if algo.endswith("_host"):
         engine, algo = "host", algo[:-len("_host")]
@@ -800,8 +808,9 @@ def bench_multi(args):
         return int(t.view(torch.int16 if es == 2 else torch.int32).to(torch.int64).sum().item())
 
     if args.algo == "ring_chunked" and args.schedule == "auto":
-        candidates = ["ring_chunked", "ring_chunked_host", "ring_chunked_queued",
-                      "ring_chunked_mesh", "ring_chunked_mesh_steps", "ring_chunked_mesh_queued"]
+        candidates = ["ring_chunked", "ring_chunked_fast", "ring_chunked_host",
+                      "ring_chunked_queued", "ring_chunked_mesh", "ring_chunked_mesh_steps",
+                      "ring_chunked_mesh_queued"]
     elif args.algo == "ring_chunked" and args.schedule == "mesh":
         candidates = ["ring_chunked_mesh", "ring_chunked_mesh_steps", "ring_chunked_mesh_queued"]
     else:
@@ -941,7 +950,9 @@ def bench_multi(args):
                                         "(bit-identical, checked); engine: devsteps = the "
                                         "step program in one kernel, twoshot = the mesh in "
                                         "one kernel, steps = host-issued, queued = host-issued "
-                                        "at once with stream-ordered waits on peers",
+                                        "at once with stream-ordered waits on peers; *_fast = "
+                                        "the plan kernel with nontemporal loads and "
+                                        "write-through stores",
                        "bytes_per_rank": S, "elements": n,
                        "parallelism": "dp%d" % world,
                        "transport": "xGMI peer copies: " + runs[chosen]["transport"],

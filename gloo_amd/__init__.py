@@ -68,6 +68,14 @@ def set_steps_engine(engine):
     errors.check(_lib.lib.glx_set_steps_engine(code), "set_steps_engine")
 
 
+def set_engine_streams(policy):
+    """Loads and stores of the device-driven kernels for algorithms created
+    afterwards: "plain" (default) or "fast" (nontemporal loads, write-through
+    stores).  Same results either way."""
+    code = {"plain": 0, "fast": 1}[policy]
+    errors.check(_lib.lib.glx_set_engine_streams(code), "set_engine_streams")
+
+
 def set_device_engines(mode):
     """Device-driven engines (one-shot / two-shot kernels) for algorithms
     created afterwards: "auto" (default: when no two ranks are threads sharing

@@ -96,6 +96,7 @@ SIGNATURES = [
     ("glx_set_mesh_engine", _i, [_i]),
     ("glx_set_device_engines", _i, [_i]),
     ("glx_set_steps_engine", _i, [_i]),
+    ("glx_set_engine_streams", _i, [_i]),
     ("glx_allreduce", _i, [_vp, _i, _i, _i, ctypes.POINTER(_vp), _i, ctypes.POINTER(_vp), _i,
                            ctypes.c_size_t, ctypes.c_uint32, ctypes.c_size_t, _i64, _vp]),
 ]

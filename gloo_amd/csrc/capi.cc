@@ -201,6 +201,12 @@ int glx_set_mesh_engine(int engine) {
   return GLX_OK;
 }
 
+int glx_set_engine_streams(int fast) {
+  if (fast != 0 && fast != 1) return fail(GLX_ERR_INVALID, "engine streams must be 0 or 1");
+  gloo::HipPlanExecutor::setEngineStreams(fast);
+  return GLX_OK;
+}
+
 int glx_set_steps_engine(int engine) {
   if (engine != GLX_ENGINE_STEPS && engine != GLX_ENGINE_DEVSTEPS &&
       engine != GLX_ENGINE_QUEUED && engine != -1) {

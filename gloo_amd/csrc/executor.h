@@ -376,6 +376,11 @@ class HipPlanExecutor : public Algorithm {
   // GLOO_AMD_STEPS_ENGINE=device|host|queued).
   static void setStepsEngine(int engine);
   static int stepsEngine();
+  // Streams of the device-driven kernels for algorithms created afterwards:
+  // 0 plain loads and stores (default), 1 nontemporal loads and write-through
+  // stores (glx_set_engine_streams).
+  static void setEngineStreams(int fast);
+  static int engineStreams();
 };
 
 }  // namespace gloo

@@ -76,6 +76,17 @@ void HipPlanExecutor::setStepsEngine(int engine) {
 int HipPlanExecutor::stepsEngine() { return g_steps_engine.load(); }
 
 namespace {
+std::atomic<int> g_engine_streams{[] {
+  const char* e = std::getenv("GLOO_AMD_ENGINE_STREAMS");  // "fast" or "plain"
+  return e != nullptr && std::strcmp(e, "fast") == 0 ? 1 : 0;
+}()};
+}  // namespace
+
+void HipPlanExecutor::setEngineStreams(int fast) { g_engine_streams.store(fast != 0 ? 1 : 0); }
+
+int HipPlanExecutor::engineStreams() { return g_engine_streams.load(); }
+
+namespace {
 
 int initialDeviceEngines() {
   const char* e = std::getenv("GLOO_AMD_ONESHOT");
@@ -172,6 +183,11 @@ void HipPlanExecutor::setupDevice() {
   os_.flagStore = fs;
   ts_.flagStore = fs;
   pk_.flagStore = fs;
+  // the kernels' streams (setEngineStreams)
+  const int fast = engineStreams();
+  os_.fast = fast;
+  ts_.fast = fast;
+  pk_.fast = fast;
   GLX_HIP_CHECK(hipEventCreateWithFlags(&ddDone_, hipEventDisableTiming));
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) == hipSuccess &&

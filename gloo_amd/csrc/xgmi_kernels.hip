@@ -69,8 +69,29 @@ __device__ __forceinline__ Span split_span(size_t a, size_t b, bool aligned) {
   return s;
 }
 
+// Vector loads of the engines' streams: FAST = nontemporal (measurement
+// knob GLOO_AMD_XGMI_FAST, default off).  Stores: FAST = write-through
+// through a buffer resource over the destination (WtStream, compiler-tracked).
+template <bool FAST>
+__device__ __forceinline__ v4u ldv(const v4u* p) {
+  return ld16<FAST>(p);
+}
+template <bool FAST>
+struct VecOut {
+  v4u* base;
+  WtStream wt;
+  __device__ __forceinline__ explicit VecOut(void* b) : base(reinterpret_cast<v4u*>(b)), wt(b) {}
+  __device__ __forceinline__ void put(size_t i, v4u v) const {
+    if (FAST) {
+      wt.put(i, v);
+    } else {
+      base[i] = v;
+    }
+  }
+};
+
 // Copy [a, b) of src to dst (virtual-buffer pointers with equal phases).
-template <typename S>
+template <typename S, bool FAST>
 __device__ __forceinline__ void copy_span(S* dst, const S* src, size_t a, size_t b,
                                           bool aligned) {
   const Span sp = split_span<16 / sizeof(S)>(a, b, aligned);
@@ -80,21 +101,21 @@ __device__ __forceinline__ void copy_span(S* dst, const S* src, size_t a, size_t
     dst[i] = src[i];
   }
   const v4u* vs = reinterpret_cast<const v4u*>(src);
-  v4u* vd = reinterpret_cast<v4u*>(dst);
+  const VecOut<FAST> vd(dst);
   constexpr int U = 8;  // vectors in flight per lane
   size_t i = va + threadIdx.x;
   for (; i + (U - 1) * kBlock < vb; i += U * kBlock) {
     v4u x[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) x[u] = vs[i + u * kBlock];
+    for (int u = 0; u < U; u++) x[u] = ldv<FAST>(vs + i + u * kBlock);
 #pragma unroll
-    for (int u = 0; u < U; u++) vd[i + u * kBlock] = x[u];
+    for (int u = 0; u < U; u++) vd.put(i + u * kBlock, x[u]);
   }
-  for (; i < vb; i += kBlock) vd[i] = vs[i];
+  for (; i < vb; i += kBlock) vd.put(i, ldv<FAST>(vs + i));
 }
 
 // Copy [a, b) of src to every dsts[d] for d < n (one load, n stores).
-template <typename S, int MAXD = kOsMaxRanks - 1>
+template <typename S, bool FAST, int MAXD = kOsMaxRanks - 1>
 __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* src, size_t a,
                                              size_t b, bool aligned) {
   const Span sp = split_span<16 / sizeof(S)>(a, b, aligned);
@@ -113,20 +134,21 @@ __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* 
   for (; i + (U - 1) * kBlock < vb; i += U * kBlock) {
     v4u x[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) x[u] = vs[i + u * kBlock];
+    for (int u = 0; u < U; u++) x[u] = ldv<FAST>(vs + i + u * kBlock);
 #pragma unroll
     for (int d = 0; d < MAXD; d++) {
       if (d < n) {
+        const VecOut<FAST> o(dsts[d]);
 #pragma unroll
-        for (int u = 0; u < U; u++) reinterpret_cast<v4u*>(dsts[d])[i + u * kBlock] = x[u];
+        for (int u = 0; u < U; u++) o.put(i + u * kBlock, x[u]);
       }
     }
   }
   for (; i < vb; i += kBlock) {
-    const v4u x = vs[i];
+    const v4u x = ldv<FAST>(vs + i);
 #pragma unroll
     for (int d = 0; d < MAXD; d++) {
-      if (d < n) reinterpret_cast<v4u*>(dsts[d])[i] = x;
+      if (d < n) VecOut<FAST>(dsts[d]).put(i, x);
     }
   }
 }
@@ -135,7 +157,7 @@ __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* 
 // (the ring's chain: the newer rank's value is the in-place destination)
 // or, LEFT, acc = op(acc, s_k) (a left fold, out = op(out, peer)).
 // The result also goes to every outs[d], d < nout.
-template <typename T, int OP, bool LEFT = false, int MAXK = kOsMaxRanks>
+template <typename T, int OP, bool FAST, bool LEFT = false, int MAXK = kOsMaxRanks>
 __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
                                           const typename Elem<T, OP>::S* const* srcs, int P,
                                           char* const* outs, int nout, size_t a, size_t b,
@@ -174,7 +196,7 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
     for (int u = 0; u < U; u++) {
 #pragma unroll
       for (int k = 0; k < MAXK; k++) {
-        if (k < P) y[u][k] = reinterpret_cast<const v4u*>(srcs[k])[v + u * kBlock];
+        if (k < P) y[u][k] = ldv<FAST>(reinterpret_cast<const v4u*>(srcs[k]) + v + u * kBlock);
       }
     }
     v4u acc[U];
@@ -188,13 +210,15 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
         }
       }
     }
+    const VecOut<FAST> od(dst);
 #pragma unroll
-    for (int u = 0; u < U; u++) reinterpret_cast<v4u*>(dst)[v + u * kBlock] = acc[u];
+    for (int u = 0; u < U; u++) od.put(v + u * kBlock, acc[u]);
 #pragma unroll
     for (int d = 0; d < MAXK - 1; d++) {
       if (d < nout) {
+        const VecOut<FAST> o(outs[d]);
 #pragma unroll
-        for (int u = 0; u < U; u++) reinterpret_cast<v4u*>(outs[d])[v + u * kBlock] = acc[u];
+        for (int u = 0; u < U; u++) o.put(v + u * kBlock, acc[u]);
       }
     }
   }
@@ -202,17 +226,17 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
     v4u y[MAXK];
 #pragma unroll
     for (int k = 0; k < MAXK; k++) {
-      if (k < P) y[k] = reinterpret_cast<const v4u*>(srcs[k])[v];
+      if (k < P) y[k] = ldv<FAST>(reinterpret_cast<const v4u*>(srcs[k]) + v);
     }
     v4u acc = y[0];
 #pragma unroll
     for (int k = 1; k < MAXK; k++) {
       if (k < P) acc = LEFT ? vec_apply<T, OP>(acc, y[k]) : vec_apply<T, OP>(y[k], acc);
     }
-    reinterpret_cast<v4u*>(dst)[v] = acc;
+    VecOut<FAST>(dst).put(v, acc);
 #pragma unroll
     for (int d = 0; d < MAXK - 1; d++) {
-      if (d < nout) reinterpret_cast<v4u*>(outs[d])[v] = acc;
+      if (d < nout) VecOut<FAST>(outs[d]).put(v, acc);
     }
   }
 }
@@ -337,10 +361,8 @@ __device__ __forceinline__ bool wait_flag(const uint64_t* word, uint64_t epoch, 
 
 // ---- one-shot ---------------------------------------------------------------
 
-template <typename T, int OP>
-// >= 2 waves per SIMD: every rank's grid (<= kOsMaxSlices workgroups) stays
-// resident even when a few ranks share one GPU
-__global__ __launch_bounds__(kBlock, 2) void oneshot_kernel(OneShotParams p) {
+template <typename T, int OP, bool FAST>
+__device__ __forceinline__ void oneshot_body(const OneShotParams& p) {
   using S = typename Elem<T, OP>::S;
   __shared__ int s_ok;
   const int w = blockIdx.x;
@@ -357,7 +379,7 @@ __global__ __launch_bounds__(kBlock, 2) void oneshot_kernel(OneShotParams p) {
     if (j >= p.P) j -= p.P;
     to[d - 1] = d < p.P ? p.push[j] : nullptr;
   }
-  scatter_span<S>(to, p.P - 1, buf, e0, e1, aligned);
+  scatter_span<S, FAST>(to, p.P - 1, buf, e0, e1, aligned);
   release_flags(p.flagOut, p.P, p.rank, w, p.epoch, p.flagStore != 0, [](int) { return true; });
 
   // 2. wait
@@ -381,14 +403,25 @@ __global__ __launch_bounds__(kBlock, 2) void oneshot_kernel(OneShotParams p) {
       const int r = p.chain[q][i];
       src[i] = i < p.P ? (r == p.rank ? buf : reinterpret_cast<const S*>(p.land[r])) : nullptr;
     }
-    fold_span<T, OP>(buf, src, p.P, nullptr, 0, a, b, aligned);
+    fold_span<T, OP, FAST>(buf, src, p.P, nullptr, 0, a, b, aligned);
+  }
+}
+
+// >= 2 waves per SIMD: every rank's grid (<= kOsMaxSlices workgroups) stays
+// resident even when a few ranks share one GPU
+template <typename T, int OP>
+__global__ __launch_bounds__(kBlock, 2) void oneshot_kernel(OneShotParams p) {
+  if (p.fast) {
+    oneshot_body<T, OP, true>(p);
+  } else {
+    oneshot_body<T, OP, false>(p);
   }
 }
 
 // ---- two-shot ---------------------------------------------------------------
 
-template <typename T, int OP>
-__global__ __launch_bounds__(kBlock, 2) void twoshot_kernel(TwoShotParams p) {
+template <typename T, int OP, bool FAST>
+__device__ __forceinline__ void twoshot_body(const TwoShotParams& p) {
   using S = typename Elem<T, OP>::S;
   __shared__ int s_ok;
   const int w = blockIdx.x;
@@ -415,7 +448,7 @@ __global__ __launch_bounds__(kBlock, 2) void twoshot_kernel(TwoShotParams p) {
     int j = p.rank + 1 + (q + w) % (p.P - 1);
     if (j >= p.P) j -= p.P;
     size_t a, b;
-    if (span(j, a, b)) copy_span<S>(reinterpret_cast<S*>(p.rsPush[j]), buf, a, b, aligned);
+    if (span(j, a, b)) copy_span<S, FAST>(reinterpret_cast<S*>(p.rsPush[j]), buf, a, b, aligned);
   }
   release_flags(p.flagAOut, p.P, p.rank, w, p.epoch, p.flagStore != 0, [&](int j) {
     size_t a, b;
@@ -449,7 +482,7 @@ __global__ __launch_bounds__(kBlock, 2) void twoshot_kernel(TwoShotParams p) {
       if (j >= p.P) j -= p.P;
       outs[d - 1] = d < p.P ? p.agPush[j] : nullptr;
     }
-    fold_span<T, OP>(buf, src, p.P, outs, p.P - 1, a, b, aligned);
+    fold_span<T, OP, FAST>(buf, src, p.P, outs, p.P - 1, a, b, aligned);
     release_flags(p.flagBOut, p.P, p.rank, w, p.epoch, p.flagStore != 0,
                   [](int) { return true; });
   }
@@ -465,9 +498,18 @@ __global__ __launch_bounds__(kBlock, 2) void twoshot_kernel(TwoShotParams p) {
       return;
     }
     if (d == 1) stamp(4);
-    copy_span<S>(buf, reinterpret_cast<const S*>(p.agLand[j]), a, b, aligned);
+    copy_span<S, FAST>(buf, reinterpret_cast<const S*>(p.agLand[j]), a, b, aligned);
   }
   stamp(5);
+}
+
+template <typename T, int OP>
+__global__ __launch_bounds__(kBlock, 2) void twoshot_kernel(TwoShotParams p) {
+  if (p.fast) {
+    twoshot_body<T, OP, true>(p);
+  } else {
+    twoshot_body<T, OP, false>(p);
+  }
 }
 
 // ---- plan kernel --------------------------------------------------------------
@@ -485,8 +527,8 @@ __device__ __forceinline__ bool seg_part(const DevSegment& sg, int w, size_t& a,
 // programs without FOLD steps (ring, halving-doubling, function-style ring):
 // the 8-way fold's registers would cut the resident workgroups per CU from
 // the 2-source variant's count (kernel-resource-usage) to 3.
-template <typename T, int OP, int MAXSRC>
-__global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
+template <typename T, int OP, int MAXSRC, bool FAST>
+__device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
   using S = typename Elem<T, OP>::S;
   __shared__ int s_ok;
   const int w = blockIdx.x;
@@ -521,7 +563,7 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
           for (int g = st.seg0; g < st.seg1; g++) {
             size_t a, b;
             if (seg_part(p.segs[g], w, a, b)) {
-              copy_span<S>(reinterpret_cast<S*>(dst), buf, a, b, aligned);
+              copy_span<S, FAST>(reinterpret_cast<S*>(dst), buf, a, b, aligned);
             }
           }
         } else {
@@ -533,9 +575,9 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
             size_t a, b;
             if (!seg_part(p.segs[g], w, a, b)) continue;
             if (st.kind == kStepCopySend) {
-              scatter_span<S, 2>(outs, 2, src, a, b, aligned);
+              scatter_span<S, FAST, 2>(outs, 2, src, a, b, aligned);
             } else {
-              fold_span<T, OP, true, 2>(buf, srcs, 2, outs + 1, 1, a, b, aligned);
+              fold_span<T, OP, FAST, true, 2>(buf, srcs, 2, outs + 1, 1, a, b, aligned);
             }
           }
         }
@@ -570,11 +612,11 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
           size_t a, b;
           if (!seg_part(p.segs[g], w, a, b)) continue;
           if (st.kind == 3) {
-            copy_span<S>(buf, srcs[1], a, b, aligned);
+            copy_span<S, FAST>(buf, srcs[1], a, b, aligned);
           } else if (st.kind == 2 || st.left) {
-            fold_span<T, OP, true, MAXSRC>(buf, srcs, n, nullptr, 0, a, b, aligned);
+            fold_span<T, OP, FAST, true, MAXSRC>(buf, srcs, n, nullptr, 0, a, b, aligned);
           } else {
-            fold_span<T, OP, false, MAXSRC>(buf, srcs, n, nullptr, 0, a, b, aligned);
+            fold_span<T, OP, FAST, false, MAXSRC>(buf, srcs, n, nullptr, 0, a, b, aligned);
           }
         }
         break;
@@ -588,6 +630,15 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
     }
   }
   stamp(2 * p.nsteps);
+}
+
+template <typename T, int OP, int MAXSRC>
+__global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
+  if (p.fast) {
+    plan_body<T, OP, MAXSRC, true>(p);
+  } else {
+    plan_body<T, OP, MAXSRC, false>(p);
+  }
 }
 
 // ---- queued steps engine ------------------------------------------------------
