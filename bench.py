@@ -411,9 +411,9 @@ def make_alg(gloo_amd, ctx, buf, algo):
     the one-shot kernel.  *_host and ring_chunked_mesh_steps are the same
     schedules with host-issued steps (calibrated peer-copy transport), *_queued
     the same steps enqueued at once with stream-ordered waits on peers;
-    *_fast the plan kernel with nontemporal loads and write-through stores
-    (set_engine_streams)."""
-    if algo.endswith("_fast"):
+    *_fast the plan kernel with the opt-in nontemporal loads and
+    write-through stores (set_engine_streams)."""
+    if algo.endswith("_fast"):  # the plan kernel with the opt-in fast streams
         gloo_amd.set_engine_streams("fast")
         try:
             return make_alg(gloo_amd, ctx, buf, algo[:-len("_fast")])
@@ -952,7 +952,7 @@ def bench_multi(args):
                                         "one kernel, steps = host-issued, queued = host-issued "
                                         "at once with stream-ordered waits on peers; *_fast = "
                                         "the plan kernel with nontemporal loads and "
-                                        "write-through stores",
+                                        "write-through stores (opt-in)",
                        "bytes_per_rank": S, "elements": n,
                        "parallelism": "dp%d" % world,
                        "transport": "xGMI peer copies: " + runs[chosen]["transport"],

@@ -70,9 +70,9 @@ def set_steps_engine(engine):
 
 def set_engine_streams(policy):
     """Loads and stores of the device-driven kernels for algorithms created
-    afterwards: "plain" (default) or "fast" (nontemporal loads, write-through
-    stores).  Same results either way."""
-    code = {"plain": 0, "fast": 1}[policy]
+    afterwards: "plain" (default; "auto" is the same) or "fast" (nontemporal
+    loads, write-through stores; opt-in)."""
+    code = {"plain": 0, "fast": 1, "auto": -1}[policy]
     errors.check(_lib.lib.glx_set_engine_streams(code), "set_engine_streams")
 
 

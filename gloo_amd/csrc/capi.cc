@@ -202,7 +202,9 @@ int glx_set_mesh_engine(int engine) {
 }
 
 int glx_set_engine_streams(int fast) {
-  if (fast != 0 && fast != 1) return fail(GLX_ERR_INVALID, "engine streams must be 0 or 1");
+  if (fast != 0 && fast != 1 && fast != -1) {
+    return fail(GLX_ERR_INVALID, "engine streams must be -1, 0 or 1");
+  }
   gloo::HipPlanExecutor::setEngineStreams(fast);
   return GLX_OK;
 }

@@ -163,11 +163,13 @@ int glx_set_device_engines(int mode);
  * Env GLOO_AMD_STEPS_ENGINE=device|host|queued. */
 int glx_set_steps_engine(int engine);
 /* Cache policy of the device-driven kernels' own loads and stores (one-shot,
- * two-shot, plan kernel) for algorithms created afterwards: 0 plain (default),
- * 1 nontemporal loads and write-through (sc1) stores -- the reduce kernel's
- * policy.  Same results either way; on one shared GPU it made the ring's plan
- * kernel ~6 % faster and halving-doubling / two-shot ~7 % slower,
- * so bench.py times the ring both ways.  Env GLOO_AMD_ENGINE_STREAMS=fast. */
+ * two-shot, plan kernel) for algorithms created afterwards: 0 plain (default;
+ * -1 is the same), 1 nontemporal loads and write-through (sc1) stores -- the
+ * reduce kernel's policy.  An opt-in: on one shared GPU it made the ring's
+ * plan kernel 6-9 % faster and halving-doubling / two-shot ~7 % slower, and
+ * one two-shot test run with it failed; bench.py times the
+ * ring with it as a separate, result-checked candidate.  Env
+ * GLOO_AMD_ENGINE_STREAMS=fast. */
 int glx_set_engine_streams(int fast);
 
 /* Number of visible HIP devices (0 when no GPU). */
