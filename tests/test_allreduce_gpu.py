@@ -475,9 +475,11 @@ def test_device_engine_variants(mode, knob):
                     q.kill()
                 raise
             outs.append(o.decode(errors="replace"))
+        # every rank's output: the first rank to fail is often not rank 0
+        every = "\n".join("---- rank %d (rc %s) ----\n%s" % (r, p.returncode, outs[r])
+                          for r, p in enumerate(procs))
         for r, p in enumerate(procs):
-            assert p.returncode == 0, "rank %d failed:\n%s" % (r, outs[r])
-            assert "OK" in outs[r]
+            assert p.returncode == 0 and "OK" in outs[r], "rank %d failed:\n%s" % (r, every)
 
 
 @pytest.mark.parametrize("P", [2, 4])
