@@ -47,6 +47,9 @@ def parse():
     p.add_argument("--no-alt", action="store_true",
                    help="N>1: do not also time the other schedules")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--link-probe", action="store_true",
+                   help="N>1: also measure per-link copy ceilings (torch CUDA IPC; opt-in: "
+                        "opening peers' buffers hung once with 1 GiB buffers, DESIGN.md 6)")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bounded CPU baseline sample (seconds of CPU work)")
     p.add_argument("--dtype", default="f32", choices=["f32", "f16", "bf16"],
@@ -748,13 +751,16 @@ def bench_multi(args):
     ctx.connectFullMesh(store)
     log("connected (world %d, device %d)" % (world, local))
     device_engines = probe_device_engines(torch, dist, gloo_amd, ctx, dev, args.dtype)
-    links, err = None, None
-    try:
-        links = link_ceiling(torch, dist, gloo_amd, dev, rank, world)
-        log("link ceilings: %s" % links)
-    except Exception as e:  # noqa: BLE001 - reported in the JSON line
-        err = "%s: %s" % (type(e).__name__, str(e)[:300])
-        log("link probe failed: %s" % err)
+    links, err = None, "not run (bench.py --link-probe)"
+    if args.link_probe:
+        err = None
+        log("link probe: start")
+        try:
+            links = link_ceiling(torch, dist, gloo_amd, dev, rank, world)
+            log("link ceilings: %s" % links)
+        except Exception as e:  # noqa: BLE001 - reported in the JSON line
+            err = "%s: %s" % (type(e).__name__, str(e)[:300])
+            log("link probe failed: %s" % err)
     # Transport calibration: peer copies by the DMA engines split over 1/2/4
     # streams, or by the xGMI copy kernel (32/128 workgroups); a few runs
     # each, max over ranks (every rank sees the same times and picks alike).
@@ -771,6 +777,7 @@ def bench_multi(args):
 
     def tuned(algo):
         calib = {}
+        log("%s: creating" % algo)
         probe = make_alg(gloo_amd, ctx, buf, algo)
         # no peer-copy transport to tune for the kernels that store themselves
         device_engine = probe.engine() not in ("steps", "queued")
@@ -932,7 +939,7 @@ def bench_multi(args):
                                  "schedule's pattern (ring: every rank -> rank+1 at once; "
                                  "mesh: every rank -> every peer at once)")
         elif err is not None:
-            measured = {"failed": err}
+            measured = {"note": err}
         res = {
             "metric": "allreduce GB/s (device-resident, fp32) at 1/2/4/8 MI355X; % HBM|xGMI roofline",
             "value": round(world * S / t / 1e9, 3), "unit": "GB/s", "n_gpus": world,
