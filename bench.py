@@ -751,16 +751,16 @@ def bench_multi(args):
     ctx.connectFullMesh(store)
     log("connected (world %d, device %d)" % (world, local))
     device_engines = probe_device_engines(torch, dist, gloo_amd, ctx, dev, args.dtype)
-    links, err = None, "not run (bench.py --link-probe)"
+    links, link_err = None, "not run (bench.py --link-probe)"
     if args.link_probe:
-        err = None
+        link_err = None
         log("link probe: start")
         try:
             links = link_ceiling(torch, dist, gloo_amd, dev, rank, world)
             log("link ceilings: %s" % links)
         except Exception as e:  # noqa: BLE001 - reported in the JSON line
-            err = "%s: %s" % (type(e).__name__, str(e)[:300])
-            log("link probe failed: %s" % err)
+            link_err = "%s: %s" % (type(e).__name__, str(e)[:300])
+            log("link probe failed: %s" % link_err)
     # Transport calibration: peer copies by the DMA engines split over 1/2/4
     # streams, or by the xGMI copy kernel (32/128 workgroups); a few runs
     # each, max over ranks (every rank sees the same times and picks alike).
@@ -938,8 +938,8 @@ def bench_multi(args):
                             note="fraction of the measured per-link ceiling for the chosen "
                                  "schedule's pattern (ring: every rank -> rank+1 at once; "
                                  "mesh: every rank -> every peer at once)")
-        elif err is not None:
-            measured = {"note": err}
+        elif link_err is not None:
+            measured = {"note": link_err}
         res = {
             "metric": "allreduce GB/s (device-resident, fp32) at 1/2/4/8 MI355X; % HBM|xGMI roofline",
             "value": round(world * S / t / 1e9, 3), "unit": "GB/s", "n_gpus": world,
