@@ -41,6 +41,14 @@ __device__ __forceinline__ void st16(v4u* p, v4u v) {
 // compiler then tracks the store for waitcnts and register hazards).
 // Offsets are 32-bit: a stream must stay below 2 GiB (kWtMaxStream).
 constexpr size_t kWtMaxStream = (size_t(1) << 31) - 16;
+// p as the compiler can prove wave-uniform (callers pass one value to every
+// lane), so a buffer resource over it stays in SGPRs.
+__device__ __forceinline__ void* uniform_ptr(void* p) {
+  const uint64_t u = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+}
 struct WtStream {
   __amdgpu_buffer_rsrc_t r;
   __device__ __forceinline__ explicit WtStream(void* base)

@@ -188,14 +188,10 @@ void HipPlanExecutor::setupDevice() {
   os_.flagStore = fs;
   ts_.flagStore = fs;
   pk_.flagStore = fs;
-  // the kernels' streams (setEngineStreams)
-  // the kernels' streams: plain unless set_engine_streams("fast") -- an
-  // opt-in measured faster for the ring's plan kernel on the rehearsal but
-  // seen failing once in the two-shot kernel
-  const int fast = engineStreams() > 0 ? 1 : 0;
-  os_.fast = fast;
-  ts_.fast = fast;
-  pk_.fast = fast;
+  // The plan kernel's streams (setEngineStreams): plain unless
+  // set_engine_streams("fast").  The one-shot and two-shot kernels are
+  // always plain.
+  pk_.fast = engineStreams() > 0 ? 1 : 0;
   GLX_HIP_CHECK(hipEventCreateWithFlags(&ddDone_, hipEventDisableTiming));
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) == hipSuccess &&

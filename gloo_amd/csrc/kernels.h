@@ -58,7 +58,6 @@ struct OneShotParams {
   int* status;                      // host-visible: 1 + rank that never arrived
   int* claim;                       // device word: the first timed-out workgroup reports
   int flagStore;                    // 1: write peers' flags with stores (Context::flagStores)
-  int fast;                         // 1: nontemporal loads, write-through stores
   uint64_t epoch;                   // >= 1, +1 per call, equal on all ranks
   uint64_t timeoutTicks;            // s_memrealtime ticks
   size_t count;                     // elements
@@ -87,7 +86,6 @@ struct TwoShotParams {
   int* status;
   int* claim;
   int flagStore;
-  int fast;                         // 1: nontemporal loads, write-through stores
   uint64_t epoch, timeoutTicks;
   size_t rangeOff[kOsMaxRanks], rangeLen[kOsMaxRanks];  // by owner
   uint8_t chain[kOsMaxRanks];       // this rank's fold order
@@ -147,7 +145,8 @@ struct PlanKernelParams {
   int* claim;
   int pollLoad;                // 1: poll flags with atomic loads (GLOO_AMD_FLAG_POLL=load)
   int flagStore;               // 1: write peers' flags with stores (Context::flagStores)
-  int fast;                    // 1: nontemporal loads, write-through stores
+  int fast;                    // 1: nontemporal loads, write-through stores (plan kernel only;
+                               // every span's stores stay below kWtMaxStream by construction)
   // diagnostics (GLOO_AMD_DEVTRACE=1): [G][2 * nsteps + 1] s_memrealtime
   // stamps per workgroup: step i started (2i), its wait was satisfied
   // (2i + 1; RECV / SEND only), the kernel ended (2 nsteps)

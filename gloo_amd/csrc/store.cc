@@ -132,10 +132,12 @@ void CallbackStore::set(const std::string& key, const std::vector<char>& data) {
 bool CallbackStore::tryGet(const std::string& key, std::vector<char>* out) {
   std::vector<char> buf(256);
   int64_t n = get_(user_, key.c_str(), buf.data(), buf.size());
+  if (n == -2) GLX_THROW_IO("CallbackStore: key '", key, "' will never be set");
   if (n < 0) return false;
   if ((size_t)n > buf.size()) {
     buf.resize((size_t)n);
     n = get_(user_, key.c_str(), buf.data(), buf.size());
+    if (n == -2) GLX_THROW_IO("CallbackStore: key '", key, "' will never be set");
     if (n < 0) return false;
   }
   buf.resize((size_t)n);

@@ -69,21 +69,30 @@ __device__ __forceinline__ Span split_span(size_t a, size_t b, bool aligned) {
   return s;
 }
 
-// Vector loads of the engines' streams: FAST = nontemporal (measurement
-// knob GLOO_AMD_XGMI_FAST, default off).  Stores: FAST = write-through
-// through a buffer resource over the destination (WtStream, compiler-tracked).
+// Vector loads of the plan kernel's streams: FAST = nontemporal.  Stores:
+// FAST = write-through through a buffer resource (WtStream, compiler-tracked).
+// The one-shot and two-shot kernels always run plain.
 template <bool FAST>
 __device__ __forceinline__ v4u ldv(const v4u* p) {
   return ld16<FAST>(p);
 }
+// Stores of vectors [va, vb) of one workgroup's span.  The write-through
+// resource is built at the span's first vector, not at the (virtual) buffer
+// base: its 32-bit offsets then stay below the span's size whatever the
+// buffer's, and the base is made wave-uniform (readfirstlane) so the resource
+// lives in SGPRs instead of a per-store waterfall loop.
 template <bool FAST>
 struct VecOut {
   v4u* base;
+  size_t origin;
   WtStream wt;
-  __device__ __forceinline__ explicit VecOut(void* b) : base(reinterpret_cast<v4u*>(b)), wt(b) {}
+  __device__ __forceinline__ VecOut(void* b, size_t va)
+      : base(reinterpret_cast<v4u*>(b)),
+        origin(va),
+        wt(FAST ? uniform_ptr(reinterpret_cast<v4u*>(b) + va) : b) {}
   __device__ __forceinline__ void put(size_t i, v4u v) const {
     if (FAST) {
-      wt.put(i, v);
+      wt.put(i - origin, v);
     } else {
       base[i] = v;
     }
@@ -101,7 +110,7 @@ __device__ __forceinline__ void copy_span(S* dst, const S* src, size_t a, size_t
     dst[i] = src[i];
   }
   const v4u* vs = reinterpret_cast<const v4u*>(src);
-  const VecOut<FAST> vd(dst);
+  const VecOut<FAST> vd(dst, va);
   constexpr int U = 8;  // vectors in flight per lane
   size_t i = va + threadIdx.x;
   for (; i + (U - 1) * kBlock < vb; i += U * kBlock) {
@@ -138,7 +147,7 @@ __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* 
 #pragma unroll
     for (int d = 0; d < MAXD; d++) {
       if (d < n) {
-        const VecOut<FAST> o(dsts[d]);
+        const VecOut<FAST> o(dsts[d], va);
 #pragma unroll
         for (int u = 0; u < U; u++) o.put(i + u * kBlock, x[u]);
       }
@@ -148,7 +157,7 @@ __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* 
     const v4u x = ldv<FAST>(vs + i);
 #pragma unroll
     for (int d = 0; d < MAXD; d++) {
-      if (d < n) VecOut<FAST>(dsts[d]).put(i, x);
+      if (d < n) VecOut<FAST>(dsts[d], va).put(i, x);
     }
   }
 }
@@ -210,13 +219,13 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
         }
       }
     }
-    const VecOut<FAST> od(dst);
+    const VecOut<FAST> od(dst, va);
 #pragma unroll
     for (int u = 0; u < U; u++) od.put(v + u * kBlock, acc[u]);
 #pragma unroll
     for (int d = 0; d < MAXK - 1; d++) {
       if (d < nout) {
-        const VecOut<FAST> o(outs[d]);
+        const VecOut<FAST> o(outs[d], va);
 #pragma unroll
         for (int u = 0; u < U; u++) o.put(v + u * kBlock, acc[u]);
       }
@@ -233,10 +242,10 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
     for (int k = 1; k < MAXK; k++) {
       if (k < P) acc = LEFT ? vec_apply<T, OP>(acc, y[k]) : vec_apply<T, OP>(y[k], acc);
     }
-    VecOut<FAST>(dst).put(v, acc);
+    VecOut<FAST>(dst, va).put(v, acc);
 #pragma unroll
     for (int d = 0; d < MAXK - 1; d++) {
-      if (d < nout) VecOut<FAST>(outs[d]).put(v, acc);
+      if (d < nout) VecOut<FAST>(outs[d], va).put(v, acc);
     }
   }
 }
@@ -411,11 +420,7 @@ __device__ __forceinline__ void oneshot_body(const OneShotParams& p) {
 // resident even when a few ranks share one GPU
 template <typename T, int OP>
 __global__ __launch_bounds__(kBlock, 2) void oneshot_kernel(OneShotParams p) {
-  if (p.fast) {
-    oneshot_body<T, OP, true>(p);
-  } else {
-    oneshot_body<T, OP, false>(p);
-  }
+  oneshot_body<T, OP, false>(p);
 }
 
 // ---- two-shot ---------------------------------------------------------------
@@ -505,11 +510,7 @@ __device__ __forceinline__ void twoshot_body(const TwoShotParams& p) {
 
 template <typename T, int OP>
 __global__ __launch_bounds__(kBlock, 2) void twoshot_kernel(TwoShotParams p) {
-  if (p.fast) {
-    twoshot_body<T, OP, true>(p);
-  } else {
-    twoshot_body<T, OP, false>(p);
-  }
+  twoshot_body<T, OP, false>(p);
 }
 
 // ---- plan kernel --------------------------------------------------------------

@@ -186,8 +186,11 @@ glx_store* glx_file_store_create(const char* path);
 /* Key prefixing wrapper: gloo/rendezvous/prefix_store.h. */
 glx_store* glx_prefix_store_create(const char* prefix, glx_store* base);
 /* Store implemented by the caller (e.g. a torch.distributed TCPStore from
- * Python).  set: store value.  get: copy the value of an EXISTING key into
- * buf (cap bytes), return its full length or -1 if the key is absent. */
+ * Python, or gloo's own context in integration/gloo/hip_allreduce.h).  set:
+ * store value.  get: copy the value of an EXISTING key into buf (cap bytes),
+ * return its full length, -1 if the key is absent (the caller polls again
+ * until its timeout), or -2 if it is absent and never will be (the wait fails
+ * at once with GLX_ERR_IO). */
 typedef int (*glx_store_set_fn)(void* user, const char* key, const void* data,
                                 size_t len);
 typedef int64_t (*glx_store_get_fn)(void* user, const char* key, void* buf,

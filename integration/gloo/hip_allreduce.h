@@ -15,12 +15,22 @@
 // MIN; the reference's accelerated paths do the same, gloo/algorithm.h:40-48:
 // a CUSTOM function cannot run on the device and is refused).
 //
-// The one addition to the CUDA constructors is the rendezvous::Store the
-// gloo context was connected with: the xGMI transport publishes its device
-// endpoints (IPC handles of receive regions, flag rows) through it.  It must
-// outlive the algorithms' first run().  The first algorithm created on a gloo
-// context sets up one xGMI context for it (all ranks create algorithms in the
-// same order, as gloo requires); later ones share it.
+// The constructors are the CUDA ones, argument for argument (plus the
+// optional ReductionFunction of the CPU algorithms).  The xGMI transport
+// exchanges its device endpoints (IPC handles of receive regions, flag rows)
+// over the gloo context's own pairs with gloo::allgather (ContextStore
+// below), so nothing beyond the connected context is needed.  An overload
+// taking the rendezvous::Store the context was connected with is kept: it
+// publishes the endpoints there instead (no collective at first run).  The
+// first algorithm created on a gloo context sets up one xGMI context for it
+// (all ranks create algorithms in the same order, as gloo requires); later
+// ones share it.
+//
+// gloo::hip::allreduce(opts[, stream]) is gloo::allreduce(const
+// AllreduceOptions&) (gloo/allreduce.h:193) for device buffers: the same
+// options object (inputs, outputs, algorithm, tag, segment size, timeout);
+// the reduce function must be one of the gloo/math.h templates (&gloo::sum<T>
+// ...), which also names the element type.
 //
 // Failures map onto gloo's own exceptions: timeouts and lost peers throw
 // gloo::IoException (GLOO_THROW_IO_EXCEPTION, gloo/common/error.h:50),
@@ -34,6 +44,7 @@
 #include <chrono>
 #include <cstdint>
 #include <cstring>
+#include <exception>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -41,6 +52,9 @@
 #include <vector>
 
 #include "gloo/algorithm.h"
+#include "gloo/allgather.h"
+#include "gloo/allreduce.h"
+#include "gloo/math.h"
 #include "gloo/common/error.h"
 #include "gloo/common/logging.h"
 #include "gloo/context.h"
@@ -128,11 +142,134 @@ class StoreBridge {
   glx_store* handle_ = nullptr;
 };
 
+// The xGMI layer's rendezvous keys carried by the gloo context itself.
+// Every key is set by the rank that owns it and read by its peers, and every
+// rank sets and reads them at the same points of its program -- connecting,
+// then each algorithm's record at its creation, read at its first run -- in
+// the same order on every rank (gloo's own rule for creating algorithms).  A
+// read that misses is therefore answered by ONE collective exchange: every
+// rank contributes the keys it set since the previous exchange, gathered with
+// gloo::allgather (gloo/allgather.h:71) over the context's pairs.  A key still
+// missing after an exchange will never arrive (the ranks' programs differ):
+// the read fails at once (-2) instead of waiting out the timeout.
+class ContextStore {
+ public:
+  // the allgather tag of the exchanges: any value user collectives on this
+  // context do not run under concurrently (they run on the same thread)
+  static constexpr uint32_t kTag = 0x676c7800u;  // "glx"
+
+  explicit ContextStore(std::shared_ptr<Context> ctx) : ctx_(std::move(ctx)) {
+    handle_ = glx_callback_store_create(&ContextStore::set, &ContextStore::get, this);
+    GLOO_ENFORCE(handle_ != nullptr, "glx_callback_store_create failed");
+  }
+  ~ContextStore() { glx_store_destroy(handle_); }
+  ContextStore(const ContextStore&) = delete;
+  ContextStore& operator=(const ContextStore&) = delete;
+  glx_store* handle() const { return handle_; }
+  int exchanges() const { return exchanges_; }
+  const std::string& lastError() const { return error_; }
+
+ private:
+  static int set(void* user, const char* key, const void* data, size_t len) {
+    auto* self = static_cast<ContextStore*>(user);
+    const char* d = static_cast<const char*>(data);
+    self->known_[key] = std::vector<char>(d, d + len);
+    self->pending_.push_back(key);
+    return 0;
+  }
+
+  static int64_t get(void* user, const char* key, void* buf, size_t cap) {
+    auto* self = static_cast<ContextStore*>(user);
+    auto it = self->known_.find(key);
+    if (it == self->known_.end()) {
+      try {
+        self->exchange();
+      } catch (const std::exception& e) {
+        self->error_ = e.what();
+        return -2;
+      }
+      it = self->known_.find(key);
+      if (it == self->known_.end()) {
+        self->error_ = std::string("no rank published '") + key + "'";
+        return -2;
+      }
+    }
+    std::memcpy(buf, it->second.data(), std::min(cap, it->second.size()));
+    return (int64_t)it->second.size();
+  }
+
+  template <typename U>
+  static void put(std::vector<char>& b, const U& v) {
+    const char* p = reinterpret_cast<const char*>(&v);
+    b.insert(b.end(), p, p + sizeof(U));
+  }
+
+  // keys set since the last exchange: [u32 key length, key, u64 value
+  // length, value]...; two allgathers: every rank's byte count, then the
+  // records padded to the longest
+  void exchange() {
+    std::vector<char> mine;
+    for (const auto& k : pending_) {
+      const std::vector<char>& v = known_[k];
+      put<uint32_t>(mine, (uint32_t)k.size());
+      mine.insert(mine.end(), k.begin(), k.end());
+      put<uint64_t>(mine, (uint64_t)v.size());
+      mine.insert(mine.end(), v.begin(), v.end());
+    }
+    const int P = ctx_->size;
+    int64_t len = (int64_t)mine.size();
+    std::vector<int64_t> lens((size_t)P, 0);
+    {
+      AllgatherOptions o(ctx_);
+      o.setInput(&len, 1);
+      o.setOutput(lens.data(), (size_t)P);
+      o.setTag(kTag);
+      allgather(o);
+    }
+    const size_t mx = (size_t)*std::max_element(lens.begin(), lens.end());
+    std::vector<char> all(mx * (size_t)P);
+    if (mx > 0) {
+      mine.resize(mx);
+      AllgatherOptions o(ctx_);
+      o.setInput(mine.data(), mx);
+      o.setOutput(all.data(), mx * (size_t)P);
+      o.setTag(kTag);
+      allgather(o);
+    }
+    for (int r = 0; r < P; r++) {
+      const char* p = all.data() + (size_t)r * mx;
+      const char* end = p + lens[(size_t)r];
+      while (p < end) {
+        uint32_t kl;
+        std::memcpy(&kl, p, sizeof(kl));
+        p += sizeof(kl);
+        std::string k(p, kl);
+        p += kl;
+        uint64_t vl;
+        std::memcpy(&vl, p, sizeof(vl));
+        p += sizeof(vl);
+        known_[k] = std::vector<char>(p, p + vl);
+        p += vl;
+      }
+    }
+    pending_.clear();
+    exchanges_++;
+  }
+
+  std::shared_ptr<Context> ctx_;
+  glx_store* handle_ = nullptr;
+  std::map<std::string, std::vector<char>> known_;
+  std::vector<std::string> pending_;
+  int exchanges_ = 0;
+  std::string error_;
+};
+
 // One xGMI context per gloo context, shared by the algorithms made on it.
 class XgmiContext {
  public:
+  // store == nullptr: the endpoints travel over the gloo context (ContextStore)
   static std::shared_ptr<XgmiContext> of(const std::shared_ptr<Context>& ctx,
-                                         rendezvous::Store& store, int device) {
+                                         rendezvous::Store* store, int device) {
     static std::mutex m;
     static std::map<const Context*, std::weak_ptr<XgmiContext>> all;
     {
@@ -156,19 +293,28 @@ class XgmiContext {
   }
   ~XgmiContext() { glx_context_destroy(glx_); }
   glx_context* get() const { return glx_; }
+  // exchanges over the gloo context so far (0 with a rendezvous store)
+  int exchanges() const { return viaContext_ ? viaContext_->exchanges() : 0; }
 
  private:
-  XgmiContext(const std::shared_ptr<Context>& ctx, rendezvous::Store& store, int device,
-              const std::string& prefix)
-      : bridge_(store, prefix) {
+  XgmiContext(const std::shared_ptr<Context>& ctx, rendezvous::Store* store, int device,
+              const std::string& prefix) {
+    glx_store* st = nullptr;
+    if (store != nullptr) {
+      bridge_.reset(new StoreBridge(*store, prefix));
+      st = bridge_->handle();
+    } else {
+      viaContext_.reset(new ContextStore(ctx));
+      st = viaContext_->handle();
+    }
     glx_ = glx_context_create(ctx->rank, ctx->size, device);
     GLOO_ENFORCE(glx_ != nullptr, "glx_context_create: ", glx_last_error());
     check(glx_context_set_timeout(glx_, (int64_t)ctx->getTimeout().count()),
           "glx_context_set_timeout");
-    check(glx_context_connect_full_mesh(glx_, bridge_.handle()),
-          "glx_context_connect_full_mesh");
+    check(glx_context_connect_full_mesh(glx_, st), "glx_context_connect_full_mesh");
   }
-  StoreBridge bridge_;
+  std::unique_ptr<StoreBridge> bridge_;
+  std::unique_ptr<ContextStore> viaContext_;
   glx_context* glx_ = nullptr;
 };
 
@@ -191,9 +337,11 @@ class Allreduce : public Algorithm {
   ~Allreduce() override { glx_algorithm_destroy(alg_); }
   // bytes moved over the peer links per run (introspection)
   int64_t bytesSent() const { return glx_algorithm_bytes_sent(alg_); }
+  // endpoint exchanges over the gloo context so far (introspection)
+  int exchanges() const { return xgmi_->exchanges(); }
 
  protected:
-  Allreduce(int algo, const std::shared_ptr<Context>& context, rendezvous::Store& store,
+  Allreduce(int algo, const std::shared_ptr<Context>& context, rendezvous::Store* store,
             const std::vector<T*>& ptrs, int count, const std::vector<hipStream_t>& streams,
             const ReductionFunction<T>* fn)
       : Algorithm(context) {
@@ -212,26 +360,140 @@ class Allreduce : public Algorithm {
   glx_algorithm* alg_ = nullptr;
 };
 
+// AllreduceOptions keeps its settings in a protected member that only
+// gloo::allreduce may read (gloo/allreduce.h:187-190); a pointer to that
+// member, formed inside a derived class, reads it from any options object.
+struct OptionsAccess : AllreduceOptions {
+  static const detail::AllreduceOptionsImpl& of(const AllreduceOptions& o) {
+    return o.*(&OptionsAccess::impl_);
+  }
+};
+
+// The glx element type and op of a reduce function that is one of the
+// gloo/math.h templates (&gloo::sum<T>, &gloo::product<T>, &gloo::max<T>,
+// &gloo::min<T>); false for anything else (a host-only std::function).
+using MathFn = void (*)(void*, const void*, const void*, size_t);
+
+template <typename T>
+bool matchMath(MathFn f, int* dtype, int* op) {
+  const MathFn fns[4] = {&gloo::sum<T>, &gloo::product<T>, &gloo::max<T>, &gloo::min<T>};
+  const int ops[4] = {GLX_SUM, GLX_PRODUCT, GLX_MAX, GLX_MIN};
+  for (int i = 0; i < 4; i++) {
+    if (f == fns[i]) {
+      *dtype = GlxType<T>::value;
+      *op = ops[i];
+      return true;
+    }
+  }
+  return false;
+}
+
+inline bool mathFunction(const AllreduceOptions::Func& fn, int* dtype, int* op) {
+  const MathFn* f = fn.target<MathFn>();
+  if (f == nullptr || *f == nullptr) return false;
+  return matchMath<float>(*f, dtype, op) || matchMath<double>(*f, dtype, op) ||
+         matchMath<float16>(*f, dtype, op) || matchMath<int32_t>(*f, dtype, op) ||
+         matchMath<int64_t>(*f, dtype, op) || matchMath<uint64_t>(*f, dtype, op) ||
+         matchMath<int8_t>(*f, dtype, op) || matchMath<uint8_t>(*f, dtype, op);
+}
+
+inline size_t glxElementSize(int dtype) {
+  switch (dtype) {
+    case GLX_INT8:
+    case GLX_UINT8: return 1;
+    case GLX_FLOAT16: return 2;
+    case GLX_INT32:
+    case GLX_FLOAT32: return 4;
+    default: return 8;
+  }
+}
+
+// gloo::allreduce(const AllreduceOptions&) (gloo/allreduce.h:193,
+// gloo/allreduce.cc:97-146) on device buffers.  Same options, same checks
+// (gloo/allreduce.cc:113-119), same result bits; opts.setAlgorithm picks
+// the reference's schedule (RING, BCUBE; UNSPECIFIED = RING's result with
+// the data movement chosen by size).  stream == nullptr: the outputs are
+// complete on return; else the work is ordered on `stream`.
+inline void allreduce(const AllreduceOptions& opts, hipStream_t stream = nullptr) {
+  const detail::AllreduceOptionsImpl& o = OptionsAccess::of(opts);
+  GLOO_ENFORCE(o.context, "allreduce: no context");
+  GLOO_ENFORCE(!o.out.empty(), "allreduce: no output buffer");
+  GLOO_ENFORCE(o.elementSize > 0);
+  int dtype = -1, op = -1;
+  GLOO_ENFORCE(o.reduce && mathFunction(o.reduce, &dtype, &op),
+               "HIP allreduce: the reduce function must be one of gloo/math.h's "
+               "sum/product/max/min<T> (a host std::function cannot run on the device)");
+  GLOO_ENFORCE_EQ(glxElementSize(dtype), o.elementSize,
+                  "reduce function's element type differs from the buffers'");
+  const size_t bytes = o.elements * o.elementSize;
+  std::vector<void*> in, out;
+  for (const auto& b : o.in) {
+    GLOO_ENFORCE_EQ(b->size, bytes, "input buffers must all hold the element count");
+    in.push_back(b->ptr);
+  }
+  for (const auto& b : o.out) {
+    GLOO_ENFORCE_EQ(b->size, bytes, "output buffers must all hold the element count");
+    out.push_back(b->ptr);
+  }
+  int algorithm = GLX_ALLREDUCE_UNSPECIFIED;
+  switch (o.algorithm) {
+    case detail::AllreduceOptionsImpl::RING: algorithm = GLX_ALLREDUCE_RING; break;
+    case detail::AllreduceOptionsImpl::BCUBE: algorithm = GLX_ALLREDUCE_BCUBE; break;
+    default: break;
+  }
+  auto x = XgmiContext::of(o.context, nullptr, deviceOf(out[0]));
+  check(glx_allreduce(x->get(), algorithm, dtype, op, in.empty() ? nullptr : in.data(),
+                      (int)in.size(), out.data(), (int)out.size(), o.elements, o.tag,
+                      o.maxSegmentSize, (int64_t)o.timeout.count(), stream),
+        "allreduce");
+}
+
 }  // namespace hip
 
+// ~ CudaAllreduceRingChunked<T> (gloo/cuda_allreduce_ring_chunked.h:19-25)
 template <typename T>
 class HipAllreduceRingChunked : public hip::Allreduce<T> {
  public:
-  HipAllreduceRingChunked(const std::shared_ptr<Context>& context, rendezvous::Store& store,
-                          const std::vector<T*>& ptrs, int count,
+  HipAllreduceRingChunked(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs,
+                          const int count,
                           const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
                           const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
-      : hip::Allreduce<T>(GLX_ALGO_RING_CHUNKED, context, store, ptrs, count, streams, fn) {}
+      : hip::Allreduce<T>(GLX_ALGO_RING_CHUNKED, context, nullptr, ptrs, count, streams, fn) {}
+  // endpoints published through the store the context was connected with
+  HipAllreduceRingChunked(const std::shared_ptr<Context>& context, rendezvous::Store& store,
+                          const std::vector<T*>& ptrs, const int count,
+                          const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
+                          const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
+      : hip::Allreduce<T>(GLX_ALGO_RING_CHUNKED, context, &store, ptrs, count, streams, fn) {}
 };
 
+// ~ CudaAllreduceHalvingDoubling<T> (gloo/cuda_allreduce_halving_doubling.h:25-30)
 template <typename T>
 class HipAllreduceHalvingDoubling : public hip::Allreduce<T> {
  public:
-  HipAllreduceHalvingDoubling(const std::shared_ptr<Context>& context, rendezvous::Store& store,
-                              const std::vector<T*>& ptrs, int count,
+  HipAllreduceHalvingDoubling(const std::shared_ptr<Context>& context,
+                              const std::vector<T*>& ptrs, const int count,
                               const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
                               const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
-      : hip::Allreduce<T>(GLX_ALGO_HALVING_DOUBLING, context, store, ptrs, count, streams,
+      : hip::Allreduce<T>(GLX_ALGO_HALVING_DOUBLING, context, nullptr, ptrs, count, streams,
+                          fn) {}
+  // the CUDA constructor's last argument: whether to pipeline the local
+  // broadcast with the reduce (gloo/cuda_allreduce_halving_doubling.h:30).
+  // The result is the same either way; the device-driven schedule overlaps
+  // its steps regardless, so the flag is accepted and has nothing to change.
+  HipAllreduceHalvingDoubling(const std::shared_ptr<Context>& context,
+                              const std::vector<T*>& ptrs, const int count,
+                              const std::vector<hipStream_t>& streams,
+                              bool pipelineBroadcastAndReduce)
+      : hip::Allreduce<T>(GLX_ALGO_HALVING_DOUBLING, context, nullptr, ptrs, count, streams,
+                          ReductionFunction<T>::sum) {
+    (void)pipelineBroadcastAndReduce;
+  }
+  HipAllreduceHalvingDoubling(const std::shared_ptr<Context>& context, rendezvous::Store& store,
+                              const std::vector<T*>& ptrs, const int count,
+                              const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
+                              const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
+      : hip::Allreduce<T>(GLX_ALGO_HALVING_DOUBLING, context, &store, ptrs, count, streams,
                           fn) {}
 };
 

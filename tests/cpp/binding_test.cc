@@ -7,14 +7,20 @@
 //
 //   binding_test cpu   no GPU: type / reduction-type mapping, CUSTOM refused
 //                      with gloo::EnforceNotMet, the store bridge both ways
+//                      the endpoint exchange over the gloo context itself
+//                      (ContextStore: gloo::allgather on the tcp pairs)
 //   binding_test gpu   P thread-ranks on one GPU bootstrapped exactly like
 //                      the reference's tests (HashStore + tcp loopback +
 //                      rendezvous::Context::connectFullMesh, gloo/test/
 //                      base_test.h:91-166); HipAllreduceRingChunked<float>,
-//                      HipAllreduceHalvingDoubling<float16|int32> on device
-//                      buffers, compared bit for bit with the reference's
-//                      own CPU AllreduceRingChunked / HalvingDoubling run on
-//                      host copies of the same inputs in the same process.
+//                      HipAllreduceHalvingDoubling<float16|int32> built with
+//                      the CUDA constructors' exact arguments (ctx, ptrs,
+//                      count[, streams]) on device buffers, and
+//                      gloo::hip::allreduce(AllreduceOptions) on the same
+//                      options the reference's gloo::allreduce takes,
+//                      compared bit for bit with the reference's own CPU
+//                      algorithms run on host copies of the same inputs in
+//                      the same process.
 #include <execinfo.h>
 #include <hip/hip_runtime_api.h>
 #include <signal.h>
@@ -22,12 +28,15 @@
 
 #include <cstdio>
 #include <cstring>
+#include <chrono>
 #include <functional>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <thread>
 #include <vector>
 
+#include "gloo/allreduce.h"
 #include "gloo/allreduce_halving_doubling.h"
 #include "gloo/allreduce_ring_chunked.h"
 #include "gloo/hip_allreduce.h"
@@ -62,6 +71,9 @@ template <> float value<float>(int r, size_t i) {
 }
 template <> int32_t value<int32_t>(int r, size_t i) {
   return (int32_t)(mix(((uint64_t)r << 40) ^ i) >> 44) - (1 << 19);
+}
+template <> uint64_t value<uint64_t>(int r, size_t i) {
+  return mix(((uint64_t)r << 40) ^ i);
 }
 template <> gloo::float16 value<gloo::float16>(int r, size_t i) {
   return gloo::cpu_float2half_rn(value<float>(r, i));
@@ -124,9 +136,37 @@ int cpuMode() {
   // two thread-ranks' gloo contexts get their xGMI contexts through the
   // shared registry at once (it must not serialise their connects)
   spawnCpu2([&](std::shared_ptr<gloo::Context> ctx, gloo::rendezvous::Store& st, int) {
-    auto x = hip::XgmiContext::of(ctx, st, -1);
+    auto x = hip::XgmiContext::of(ctx, &st, -1);
     EXPECT(x && x->get() != nullptr, "registry");
-    EXPECT(hip::XgmiContext::of(ctx, st, -1) == x, "one xGMI context per gloo context");
+    EXPECT(hip::XgmiContext::of(ctx, &st, -1) == x, "one xGMI context per gloo context");
+    EXPECT(hip::XgmiContext::of(ctx, nullptr, -1) == x, "the store does not split the registry");
+  });
+  // the drop-in's endpoint exchange over the gloo context alone (no store):
+  // two thread-ranks connect their xGMI contexts through gloo::allgather
+  spawnCpu2([&](std::shared_ptr<gloo::Context> ctx, gloo::rendezvous::Store&, int) {
+    auto x = hip::XgmiContext::of(ctx, nullptr, -1);
+    EXPECT(x && x->get() != nullptr, "connect over the gloo context");
+    EXPECT(x->exchanges() == 2, "connect takes two exchanges (endpoints, mapped): %d",
+           x->exchanges());
+  });
+  // the exchange store on its own: keys set by each rank are read by the
+  // other after one collective exchange; a key nobody set fails at once
+  // (one more exchange), not after the timeout
+  spawnCpu2([&](std::shared_ptr<gloo::Context> ctx, gloo::rendezvous::Store&, int r) {
+    hip::ContextStore cs(ctx);
+    const std::string mine = "k/" + std::to_string(r), theirs = "k/" + std::to_string(1 - r);
+    std::vector<char> val(3000 + (size_t)r, (char)('a' + r));
+    EXPECT(glx_store_set(cs.handle(), mine.c_str(), val.data(), val.size()) == GLX_OK, "set");
+    std::vector<char> buf(4096);
+    size_t len = 0;
+    EXPECT(glx_store_get(cs.handle(), theirs.c_str(), buf.data(), buf.size(), &len, 10000) ==
+               GLX_OK, "get: %s", glx_last_error());
+    EXPECT(len == 3000 + (size_t)(1 - r) && buf[0] == (char)('a' + 1 - r), "value");
+    EXPECT(cs.exchanges() == 1, "one exchange: %d", cs.exchanges());
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = glx_store_get(cs.handle(), "never", buf.data(), buf.size(), &len, 20000);
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    EXPECT(rc == GLX_ERR_IO && s < 5.0, "a key nobody set: rc %d after %.1f s", rc, s);
   });
   // two ranks' xGMI contexts connect through the bridge over one gloo store
   // (the endpoint exchange needs no GPU)
@@ -175,7 +215,8 @@ void spawn(int P, const std::function<void(std::shared_ptr<gloo::Context>,
 }
 
 template <typename T, template <typename> class Hip, template <typename> class Ref>
-void compare(const char* name, int P, int count, int nptrs, const gloo::ReductionFunction<T>* fn) {
+void compare(const char* name, int P, int count, int nptrs, const gloo::ReductionFunction<T>* fn,
+             bool viaStore = false) {
   // inputs, and the reference's own CPU algorithm on host copies of them
   std::vector<std::vector<std::vector<T>>> in(P), ref(P), got(P);
   for (int r = 0; r < P; r++) {
@@ -206,7 +247,16 @@ void compare(const char* name, int P, int count, int nptrs, const gloo::Reductio
       dev.push_back(d);
     }
     {
-      Hip<T> alg(ctx, store, dev, count, {}, fn);
+      // the CUDA constructors' arguments; SUM needs no function at all
+      std::unique_ptr<Hip<T>> a;
+      if (viaStore) {
+        a.reset(new Hip<T>(ctx, store, dev, count, {}, fn));
+      } else if (fn == gloo::ReductionFunction<T>::sum) {
+        a.reset(new Hip<T>(ctx, dev, count));
+      } else {
+        a.reset(new Hip<T>(ctx, dev, count, {}, fn));
+      }
+      Hip<T>& alg = *a;
       for (int it = 0; it < 2; it++) {  // repeated runs on one instance
         for (int k = 0; k < nptrs && it > 0; k++) {
           hipMemcpy(dev[(size_t)k], in[r][(size_t)k].data(), sizeof(T) * (size_t)count,
@@ -229,7 +279,88 @@ void compare(const char* name, int P, int count, int nptrs, const gloo::Reductio
     }
   }
   EXPECT(bad == 0, "%s: %zu buffers differ from the reference", name, bad);
-  std::printf("%s P=%d count=%d ptrs=%d: %s\n", name, P, count, nptrs, bad ? "MISMATCH" : "ok");
+  std::printf("%s P=%d count=%d ptrs=%d%s: %s\n", name, P, count, nptrs,
+              viaStore ? " (store)" : "", bad ? "MISMATCH" : "ok");
+}
+
+// gloo::hip::allreduce(opts) against the reference's gloo::allreduce(opts):
+// the same options (inputs or in-place outputs, algorithm, segment size, tag)
+// built on each side, device buffers for the HIP call, host copies for the
+// reference's.
+template <typename T>
+void compareFn(const char* name, int P, int count, int nin, int nout,
+               gloo::AllreduceOptions::Algorithm algo, size_t maxSeg,
+               void (*fn)(void*, const void*, const void*, size_t)) {
+  std::vector<std::vector<std::vector<T>>> in(P), out0(P), ref(P), got(P);
+  for (int r = 0; r < P; r++) {
+    for (int k = 0; k < nin; k++) {
+      std::vector<T> v((size_t)count);
+      for (int i = 0; i < count; i++) v[(size_t)i] = value<T>(r * 8 + k, (size_t)i);
+      in[r].push_back(v);
+    }
+    for (int k = 0; k < nout; k++) {
+      std::vector<T> v((size_t)count);
+      for (int i = 0; i < count; i++) v[(size_t)i] = value<T>(r * 8 + 4 + k, (size_t)i);
+      out0[r].push_back(v);
+    }
+    ref[r] = out0[r];
+    got[r] = out0[r];
+  }
+  auto setup = [&](gloo::AllreduceOptions& o, std::vector<T*>& ins, std::vector<T*>& outs) {
+    o.setAlgorithm(algo);
+    if (!ins.empty()) o.setInputs(ins, (size_t)count);
+    o.setOutputs(outs, (size_t)count);
+    o.setReduceFunction(fn);
+    o.setTag(7);
+    if (maxSeg > 0) o.setMaxSegmentSize(maxSeg);
+  };
+  spawn(P, [&](std::shared_ptr<gloo::Context> ctx, gloo::rendezvous::Store&, int r) {
+    std::vector<std::vector<T>> hin = in[r];
+    std::vector<T*> ins, outs;
+    for (auto& v : hin) ins.push_back(v.data());
+    for (auto& v : ref[r]) outs.push_back(v.data());
+    gloo::AllreduceOptions o(ctx);
+    setup(o, ins, outs);
+    gloo::allreduce(o);
+  });
+  spawn(P, [&](std::shared_ptr<gloo::Context> ctx, gloo::rendezvous::Store&, int r) {
+    std::vector<T*> ins, outs;
+    auto upload = [&](const std::vector<T>& v) {
+      T* d = nullptr;
+      if (hipMalloc((void**)&d, sizeof(T) * (size_t)std::max(count, 1)) != hipSuccess) {
+        throw std::runtime_error("hipMalloc");
+      }
+      hipMemcpy(d, v.data(), sizeof(T) * (size_t)count, hipMemcpyHostToDevice);
+      return d;
+    };
+    for (auto& v : in[r]) ins.push_back(upload(v));
+    for (auto& v : out0[r]) outs.push_back(upload(v));
+    for (int it = 0; it < 2; it++) {  // the second call reuses the exchanged buffers
+      for (int k = 0; k < nout && it > 0; k++) {
+        hipMemcpy(outs[(size_t)k], out0[r][(size_t)k].data(), sizeof(T) * (size_t)count,
+                  hipMemcpyHostToDevice);
+      }
+      gloo::AllreduceOptions o(ctx);
+      setup(o, ins, outs);
+      gloo::hip::allreduce(o);
+    }
+    for (int k = 0; k < nout; k++) {
+      hipMemcpy(got[r][(size_t)k].data(), outs[(size_t)k], sizeof(T) * (size_t)count,
+                hipMemcpyDeviceToHost);
+    }
+    for (T* d : ins) hipFree(d);
+    for (T* d : outs) hipFree(d);
+  });
+  size_t bad = 0;
+  for (int r = 0; r < P; r++) {
+    for (int k = 0; k < nout; k++) {
+      bad += std::memcmp(got[r][(size_t)k].data(), ref[r][(size_t)k].data(),
+                         sizeof(T) * (size_t)count) != 0;
+    }
+  }
+  EXPECT(bad == 0, "%s: %zu buffers differ from the reference", name, bad);
+  std::printf("%s P=%d count=%d in=%d out=%d: %s\n", name, P, count, nin, nout,
+              bad ? "MISMATCH" : "ok");
 }
 
 int gpuMode() {
@@ -247,6 +378,19 @@ int gpuMode() {
       "halving_doubling<float16> sum", 4, 65539, 1, ReductionFunction<float16>::sum);
   compare<int32_t, HipAllreduceHalvingDoubling, AllreduceHalvingDoubling>(
       "halving_doubling<int32> product", 3, 1000, 1, ReductionFunction<int32_t>::product);
+  compare<float, HipAllreduceRingChunked, AllreduceRingChunked>(
+      "ring_chunked<float> sum", 2, 4099, 1, ReductionFunction<float>::sum, /*viaStore=*/true);
+  using MathFn = void (*)(void*, const void*, const void*, size_t);
+  compareFn<float>("allreduce(opts) RING float sum", 3, 100003, 0, 1,
+                   AllreduceOptions::Algorithm::RING, 0, (MathFn)&gloo::sum<float>);
+  compareFn<float>("allreduce(opts) RING float sum, 2 in, 2 out, 128 B segments", 4, 10000, 2, 2,
+                   AllreduceOptions::Algorithm::RING, 128, (MathFn)&gloo::sum<float>);
+  compareFn<float16>("allreduce(opts) BCUBE float16 max", 4, 65539, 1, 1,
+                     AllreduceOptions::Algorithm::BCUBE, 0, (MathFn)&gloo::max<float16>);
+  compareFn<uint64_t>("allreduce(opts) RING uint64 sum", 7, 1000, 0, 3,
+                      AllreduceOptions::Algorithm::RING, 128, (MathFn)&gloo::sum<uint64_t>);
+  compareFn<int32_t>("allreduce(opts) UNSPECIFIED int32 min", 2, 5000, 1, 1,
+                     AllreduceOptions::Algorithm::UNSPECIFIED, 0, (MathFn)&gloo::min<int32_t>);
   std::printf("binding_test gpu: %s\n", failures ? "FAILED" : "OK");
   return failures ? 1 : 0;
 }
