@@ -22,6 +22,7 @@ import os
 import sys
 import time
 
+T_START = time.time()
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -45,11 +46,18 @@ def parse():
                         "hipMemcpyPeerAsync with 1/2/4 streams per copy and the xGMI copy "
                         "kernel at 32/64/128/256 workgroups) or a fixed DMA split 1/2/4")
     p.add_argument("--no-alt", action="store_true",
-                   help="N>1: do not also time the other schedules")
+                   help="N>1: do not also time halving-doubling beside the candidates")
+    p.add_argument("--candidates", default="default",
+                   help="N>1: 'default' (ring on the plan kernel, mesh on the two-shot "
+                        "kernel, ring as host-issued steps), 'all' (+ the opt-in engines and "
+                        "stream policies) or a comma list of candidate names")
+    p.add_argument("--calibrate", default="default", choices=["default", "all"],
+                   help="N>1: host-issued steps' transports tried (default: DMA and the "
+                        "copy kernel at 128 workgroups; all: 7 variants)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--link-probe", action="store_true",
-                   help="N>1: also measure per-link copy ceilings (torch CUDA IPC; opt-in: "
-                        "opening peers' buffers hung once with 1 GiB buffers, DESIGN.md 6)")
+    p.add_argument("--link-probe", dest="link_probe", action="store_true", default=True,
+                   help="N>1: measure per-link copy ceilings (default; the product's IPC path)")
+    p.add_argument("--no-link-probe", dest="link_probe", action="store_false")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bounded CPU baseline sample (seconds of CPU work)")
     p.add_argument("--dtype", default="f32", choices=["f32", "f16", "bf16"],
@@ -78,6 +86,12 @@ def load_traffic(workload):
         return d.get(workload, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
+
+
+def metric_name(dtype):
+    """BASELINE.json's metric, with the element type actually run."""
+    return ("allreduce GB/s (device-resident, %s) at 1/2/4/8 MI355X; %% HBM|xGMI roofline"
+            % {"f32": "fp32"}.get(dtype, dtype))
 
 
 def host_threads():
@@ -336,7 +350,7 @@ def bench_single(args):
                                                args.size_mib)
     traffic = load_traffic(workload)
     res = {
-        "metric": "allreduce GB/s (device-resident, fp32) at 1/2/4/8 MI355X; % HBM|xGMI roofline",
+        "metric": metric_name(args.dtype),
         "value": round(S / t / 1e9, 3), "unit": "GB/s", "n_gpus": 1, "steps": steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
@@ -367,26 +381,36 @@ def bench_single(args):
     return res
 
 
-def plan_hbm_bytes(gloo_amd, algo, rank, world, count, es):
+def plan_hbm_bytes(gloo_amd, algo, rank, world, count, es, fused=False):
     """Algorithmic HBM bytes one rank's GPU moves per run of the schedule
     (from its compiled step program): a SEND reads its bytes here and writes
     them into the receiver's HBM (counted here, the schedules being
     symmetric), a REDUCE reads 2 and writes 1, a COPY reads 1 and writes 1,
     a FOLD of k sources reads k and writes 1 -- per element.  Ring at P=8:
     sends 2 x 1.75 S + reduces 3 x 0.875 S + copies 2 x 0.875 S = 7.875 S;
-    mesh 6.375 S; halving-doubling 7.875 S."""
+    mesh 6.375 S; halving-doubling 7.875 S.  fused: the plan
+    kernel's reduce-and-forward -- a SEND of exactly the range the REDUCE or
+    COPY before it (past RELEASEs only) just wrote reads nothing more, it only
+    writes the receiver's copy: the ring at P=8 then moves 6.125 S."""
     steps, _, folds = gloo_amd.plan(plan_name(algo), rank, world, count, with_folds=True)
     total = 0
+    last = None  # (off, len) of the last REDUCE / COPY, while only RELEASEs follow it
     for st in steps:
-        kind, ln = st[0], st[4]
+        kind, off, ln = st[0], st[3], st[4]
         if kind == 0:
-            total += 2 * ln
+            total += (1 if fused and last == (off, ln) else 2) * ln
+            last = None
         elif kind == 2:
             total += 3 * ln
+            last = (off, ln)
         elif kind == 3:
             total += 2 * ln
+            last = (off, ln)
         elif kind == 5:
             total += (len(folds.get(st[5], [])) + 1) * ln
+            last = None
+        elif kind != 4:
+            last = None
     return total * es
 
 
@@ -395,12 +419,13 @@ RING_SCHEDULES = {"ring_chunked": "ring", "ring_chunked_mesh": "mesh",
                   "ring_chunked_auto": "auto"}
 ENGINES = {}  # bench name -> engine the product chose (steps/oneshot/twoshot/devsteps)
 TRANSPORT = {}  # bench name -> the algorithm's transport_stats() after its timed runs
+FAST = {}  # bench name -> whether its plan kernel ran the fast streams
 CHECKS = {}  # bench name -> result_check() of its post-timing run
 
 
 def plan_name(algo):
     """Schedule name of a bench candidate for gloo_amd.plan()."""
-    for suffix in ("_host", "_queued", "_fast"):
+    for suffix in ("_host", "_queued", "_fast", "_plain"):
         if algo.endswith(suffix):
             algo = algo[:-len(suffix)]
     return {"ring_chunked_mesh_steps": "ring_chunked_mesh",
@@ -416,12 +441,13 @@ def make_alg(gloo_amd, ctx, buf, algo):
     the same steps enqueued at once with stream-ordered waits on peers;
     *_fast the plan kernel with the opt-in nontemporal loads and
     write-through stores (set_engine_streams)."""
-    if algo.endswith("_fast"):  # the plan kernel with the opt-in fast streams
-        gloo_amd.set_engine_streams("fast")
-        try:
-            return make_alg(gloo_amd, ctx, buf, algo[:-len("_fast")])
-        finally:
-            gloo_amd.set_engine_streams("plain")
+    for suffix, policy in (("_fast", "fast"), ("_plain", "plain")):
+        if algo.endswith(suffix):  # the plan kernel with a forced stream policy
+            gloo_amd.set_engine_streams(policy)
+            try:
+                return make_alg(gloo_amd, ctx, buf, algo[:-len(suffix)])
+            finally:
+                gloo_amd.set_engine_streams("auto")
     engine = None
     if algo.endswith("_host"):
         engine, algo = "host", algo[:-len("_host")]
@@ -466,6 +492,7 @@ def time_schedule(torch, dist, gloo_amd, ctx, buf, algo, steps, warmup):
     device syncs; returns (max-over-ranks seconds per step, link bytes/run)."""
     alg = make_alg(gloo_amd, ctx, buf, algo)
     ENGINES[algo] = alg.engine()
+    FAST[algo] = alg.fast_streams() if ENGINES[algo] == "devsteps" else None
     log("%s: created (engine %s), warmup %d" % (algo, ENGINES[algo], warmup))
     for _ in range(warmup):
         alg.run()
@@ -496,98 +523,72 @@ def time_schedule(torch, dist, gloo_amd, ctx, buf, algo, steps, warmup):
     return el.item() / steps, sent
 
 
-def link_ceiling(torch, dist, gloo_amd, dev, rank, world, nbytes=64 << 20, reps=5):
+def link_ceiling(torch, dist, gloo_amd, ctx, world, nbytes=64 << 20, reps=5):
     """Measured xGMI ceilings, the roofline's second denominator (SURVEY 8d:
     'also record a measured single-link hipMemcpyPeerAsync ceiling and report
-    the fraction of both').  Every rank exports a receive buffer (torch CUDA
-    IPC) and, with every rank sending at once:
-      ring -- writes `nbytes` to rank+1 (the ring's link use; HD's per step);
-      mesh -- writes nbytes/(P-1) to every peer (the mesh's: all links busy);
-    by hipMemcpyPeerAsync (dma, one stream per destination) and by the kernel
-    transport's copy kernel (kernel, 256 workgroups over the destinations).
-    Per-link GB/s = bytes on the busiest link / max-over-ranks time."""
-    def agreed(ok):  # every rank takes the same branch after a local failure
-        flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        return bool(flag.item())
-
-    def attempt(fn):
-        try:
-            return fn(), None
-        except Exception as e:  # noqa: BLE001 - reported, and agreed on below
-            return None, "%s: %s" % (type(e).__name__, str(e)[:200])
-
-    recv = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    send = torch.empty(nbytes, dtype=torch.uint8, device=dev).fill_(rank & 0xFF)
-    torch.cuda.synchronize()
-    share, err = attempt(lambda: recv.untyped_storage()._share_cuda_())
-    handles = [None] * world
-    dist.all_gather_object(handles, share)
-    peers = {}
-
-    def open_peers():
-        for k in range(world):
-            if k != rank:
-                peers[k] = torch.UntypedStorage._new_shared_cuda(*handles[k])
-    if err is None and all(h is not None for h in handles):
-        _, err = attempt(open_peers)
-    else:
-        err = err or "a peer could not export its buffer"
-    out = {"bytes_per_rep": nbytes, "reps": reps}
+    the fraction of both').  Through the product's own LinkProbe (glx.h
+    glx_link_probe_*): every rank's receive block is exported and imported by
+    the context's canary-checked IPC path, uncached like the engines' landing
+    regions.  With every rank sending at once:
+      ring -- `nbytes` to rank+1 (the ring's link use; HD's per step);
+      mesh -- nbytes/(P-1) to every peer (the mesh's: all links busy);
+    by hipMemcpyPeerAsync (dma, one stream per destination) and by the copy
+    kernel (kernel, 256 workgroups over the destinations).  Per-link GB/s =
+    bytes on the busiest link / max-over-ranks time.  (Round 2 mapped torch
+    CUDA IPC buffers here and hung in that import on an 8-rank rehearsal,
+    profiles/r5d_link_probe_hang.txt)"""
+    out = {"bytes_per_rep": nbytes, "reps": reps, "path": "glx_link_probe (product IPC, uncached)"}
+    probe = gloo_amd.rendezvous.LinkProbe(ctx, nbytes)
     try:
-        if not agreed(err is None):
-            raise RuntimeError(err or "failed on another rank")
-        streams = [torch.cuda.Stream(dev) for _ in range(world - 1)]
-        piece = (nbytes // max(1, world - 1)) & ~4095
-        for pattern in ("ring", "mesh"):
-            if pattern == "mesh" and world <= 2:
+        for pattern, pname in ((probe.RING, "ring"), (probe.MESH, "mesh")):
+            if pattern == probe.MESH and world <= 2:
                 continue  # one peer: the mesh is the ring
-            for eng in ("dma", "kernel"):
-                if pattern == "ring":
-                    jobs = [((rank + 1) % world, 0, nbytes, streams[0])]
-                else:  # sender k lands in slot (k - j - 1) mod P of receiver j
-                    jobs = [(j, ((rank - j - 1) % world) * piece, piece, streams[i])
-                            for i, j in enumerate(k for k in range(world) if k != rank)]
-                blocks = max(32, 256 // len(jobs))
-
-                def issue(jobs=jobs, eng=eng, blocks=blocks):
-                    for j, off, ln, st in jobs:
-                        dptr = peers[j].data_ptr() + off
-                        if eng == "dma":
-                            gloo_amd.peer_copy(dptr, handles[j][0], send.data_ptr(),
-                                               dev.index, ln, st)
-                        else:
-                            gloo_amd.kernel_copy(dptr, send.data_ptr(), ln, blocks, st)
-
-                def warm(issue=issue):
-                    issue()
-                    torch.cuda.synchronize()
-
-                _, err = attempt(warm)  # maps, peer access, first-touch
-                if not agreed(err is None):
-                    out["%s_%s" % (pattern, eng)] = err or "failed on another rank"
-                    continue
+            for engine, ename in ((probe.DMA, "dma"), (probe.KERNEL, "kernel")):
+                probe.run(pattern, engine, 256, 1)  # first touch, peer access
                 dist.barrier()
-                t0 = time.perf_counter()
-
-                def timed(issue=issue):
-                    for _ in range(reps):
-                        issue()
-                    torch.cuda.synchronize()
-                _, err = attempt(timed)
-                el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+                secs, link = probe.run(pattern, engine, 256, reps)
+                el = torch.tensor([secs], dtype=torch.float64)
                 dist.all_reduce(el, op=dist.ReduceOp.MAX)
-                if not agreed(err is None):
-                    out["%s_%s" % (pattern, eng)] = err or "failed on another rank"
-                    continue
-                out["%s_%s_GBps" % (pattern, eng)] = round(jobs[0][2] * reps / el.item() / 1e9, 2)
+                out["%s_%s_GBps" % (pname, ename)] = round(link * reps / el.item() / 1e9, 2)
         return out
     finally:
-        try:
-            torch.cuda.synchronize()
-        finally:
-            peers.clear()
-            dist.barrier()  # nobody frees its buffer while a peer still maps it
+        dist.barrier()  # nobody frees its block while a peer may still write it
+        probe.close()
+
+
+def transport_health(peer_infos, stats):
+    """The node run must not silently degrade.  peer_infos:
+    per rank, the context's peer_info() of every peer; stats: per rank,
+    {candidate: transport_stats()}.  When every rank sits on a GPU of its own,
+    an xGMI transport is expected: a hipMemcpyAsync fallback (device_copies:
+    hipMemcpyPeerAsync refused a mapping), a link without native atomics
+    (flag words then written with plain stores) or a peer GPU the runtime
+    says we cannot access are errors.  Returns (status dict, error or None)."""
+    distinct = all(not i["same_gpu"] for infos in peer_infos for i in infos)
+    problems = []
+    for r, infos in enumerate(peer_infos):
+        for i in infos:
+            if i["same_gpu"]:
+                continue
+            if i["can_access_peer"] is False:
+                problems.append("rank %d cannot access the GPU of a peer (device %d)"
+                                % (r, i["device"]))
+            if i["native_atomics"] is False:
+                problems.append("rank %d: link to device %d has no native atomics "
+                                "(flag words written with stores)" % (r, i["device"]))
+    for r, per in enumerate(stats):
+        for cand, st in sorted(per.items()):
+            if st and st.get("device_copies", 0) > 0 and distinct:
+                problems.append("rank %d, %s: %d hipMemcpyAsync fallbacks instead of peer "
+                                "copies" % (r, cand, st["device_copies"]))
+    status = {"ranks_on_distinct_gpus": distinct,
+              "native_atomics": [[i["native_atomics"] for i in infos] for infos in peer_infos],
+              "flag_stores": [any(i["flag_stores"] for i in infos) for infos in peer_infos],
+              "problems": problems}
+    err = None
+    if distinct and problems:
+        err = "degraded xGMI transport: " + "; ".join(problems[:8])
+    return status, err
 
 
 def host_endpoint_rate(torch, dist, gloo_amd, ctx, src, dev_result, algo, reps):
@@ -655,8 +656,7 @@ SWEEP_ELEMS = [1 << 10, 1 << 12, 1 << 14, 1 << 16, 1 << 18, 1 << 20, 1 << 22, 1 
 
 def probe_device_engines(torch, dist, gloo_amd, ctx, dev, dtype):
     """Before timing them, check the device-driven engines (one-shot,
-    two-shot and plan kernels, and the queued steps engine's stream-ordered
-    waits) on this machine: short timeout, results bit-identical to
+    two-shot and plan kernels) on this machine: short timeout, results bit-identical to
     the host-issued steps engine over three refilled runs.  If any rank fails,
     every rank turns them off for the rest of the run (the host-issued
     schedules remain) and the JSON says why."""
@@ -664,8 +664,7 @@ def probe_device_engines(torch, dist, gloo_amd, ctx, dev, dtype):
     ctx.setTimeout(15)
     try:
         for algo, n in (("ring_chunked_repl", 65536 + 3), ("ring_chunked_mesh", (1 << 20) + 5),
-                        ("ring_chunked", 1 << 20), ("halving_doubling", 1 << 20),
-                        ("ring_chunked_queued", (1 << 20) + 3)):
+                        ("ring_chunked", 1 << 20), ("halving_doubling", 1 << 20)):
             x = synthetic(torch, n, dtype, dev, 99 + int(os.environ.get("RANK", "0")))
             ref = x.clone()
             torch.cuda.synchronize()  # run() does not order itself after torch's stream
@@ -724,6 +723,65 @@ def element_sweep(torch, dist, gloo_amd, ctx, dev, schedules, dtype):
     return out
 
 
+DEFAULT_CANDIDATES = ["ring_chunked", "ring_chunked_mesh", "ring_chunked_host"]
+EXTRA_CANDIDATES = ["ring_chunked_fast", "ring_chunked_plain", "ring_chunked_queued",
+                    "ring_chunked_mesh_steps", "ring_chunked_mesh_queued"]
+DEFAULT_ALTS = ["halving_doubling"]
+EXTRA_ALTS = ["halving_doubling_host", "halving_doubling_queued"]
+# host-issued steps' peer-copy transports: (engine, DMA split, copy-kernel workgroups)
+TRANSPORTS_DEFAULT = [("dma", 1, 0), ("kernel", 1, 128)]
+TRANSPORTS_ALL = [("dma", 1, 0), ("dma", 2, 0), ("dma", 4, 0), ("kernel", 1, 32),
+                  ("kernel", 1, 64), ("kernel", 1, 128), ("kernel", 1, 256)]
+
+
+def candidate_lists(args):
+    """(candidates timed for `value`, schedules timed beside them).  The
+    default run keeps to four schedules -- the north star's ring on the plan
+    kernel, the mesh on the two-shot kernel, the ring as host-issued steps,
+    and halving-doubling on the plan kernel -- each one more chance for a
+    first run on new hardware to fail;
+    --candidates all adds the opt-in engines and stream policies."""
+    if args.algo == "ring_chunked" and args.schedule == "auto":
+        cands = list(DEFAULT_CANDIDATES)
+        alts = list(DEFAULT_ALTS)
+        if args.candidates == "all":
+            cands += EXTRA_CANDIDATES
+            alts += EXTRA_ALTS
+        elif args.candidates != "default":
+            cands = [c for c in args.candidates.split(",") if c]
+    elif args.algo == "ring_chunked" and args.schedule == "mesh":
+        cands, alts = ["ring_chunked_mesh", "ring_chunked_mesh_steps"], []
+    elif args.algo == "ring_chunked" and args.schedule == "ring":
+        cands, alts = ["ring_chunked", "ring_chunked_host"], []
+    else:
+        cands, alts = [args.algo], []
+    if args.no_alt:
+        alts = []
+    return cands, [a for a in alts if a not in cands]
+
+
+def north_star_block(S, world, t, p50, engine, hbm_bytes):
+    """allreduce_ring_chunked of S per rank across `world`
+    GPUs with the reference's own data movement (r -> r+1), whichever
+    schedule wins `value`.  Link bound: 2(P-1)/P * S on the one link per
+    direction (1.75 S at P = 8) at 153 GB/s; the target is >= 80 % of it
+    (t <= 3.84 ms for 256 MiB at P = 8)."""
+    link_bytes = 2 * (world - 1) * S // world
+    t_star = link_bytes / (XGMI_LINK_GBPS * 1e9)
+    return {"schedule": "ring_chunked (r -> r+1)", "engine": engine,
+            "ms_per_step": round(t * 1e3, 4), "p50_ms_per_step": round(p50 * 1e3, 4),
+            "algbw_GBps": round(S / t / 1e9, 3),
+            "link_bytes_per_step": link_bytes,
+            "link_GBps": round(link_bytes / t / 1e9, 2),
+            "link_frac": round(t_star / t, 4),
+            "link_bound_ms": round(t_star * 1e3, 4),
+            "target_ms": round(t_star / 0.8 * 1e3, 4),
+            "hbm_bytes_per_step": hbm_bytes,
+            "hbm_frac": round(hbm_bytes / t / 1e9 / HBM_PEAK_GBPS, 4),
+            "note": "link_frac = (2(P-1)/P * S / 153 GB/s) / ms_per_step; the north star "
+                    "is link_frac >= 0.8"}
+
+
 def bench_multi(args):
     import torch
     import torch.distributed as dist
@@ -750,22 +808,33 @@ def bench_multi(args):
     ctx.setTimeout(120)
     ctx.connectFullMesh(store)
     log("connected (world %d, device %d)" % (world, local))
+    peer_info = [ctx.peer_info(k) for k in range(world) if k != rank]
     device_engines = probe_device_engines(torch, dist, gloo_amd, ctx, dev, args.dtype)
-    links, link_err = None, "not run (bench.py --link-probe)"
-    if args.link_probe:
-        link_err = None
-        log("link probe: start")
+
+    # A failure on any rank (a timeout, a HIP error) is agreed on by all, so
+    # every rank takes the same branch; the JSON line names it.
+    def agreed(ok):
+        flag = torch.tensor([0 if ok else 1], dtype=torch.int32)
+        dist.all_reduce(flag)
+        return int(flag.item()) == 0
+
+    def attempt(what, fn):
         try:
-            links = link_ceiling(torch, dist, gloo_amd, dev, rank, world)
-            log("link ceilings: %s" % links)
+            return fn(), None
         except Exception as e:  # noqa: BLE001 - reported in the JSON line
-            link_err = "%s: %s" % (type(e).__name__, str(e)[:300])
-            log("link probe failed: %s" % link_err)
-    # Transport calibration: peer copies by the DMA engines split over 1/2/4
-    # streams, or by the xGMI copy kernel (32/128 workgroups); a few runs
-    # each, max over ranks (every rank sees the same times and picks alike).
-    TRANSPORTS = [("dma", 1, 0), ("dma", 2, 0), ("dma", 4, 0), ("kernel", 1, 32),
-                  ("kernel", 1, 64), ("kernel", 1, 128), ("kernel", 1, 256)]
+            err = "%s: %s" % (type(e).__name__, str(e)[:300])
+            log("%s failed: %s" % (what, err))
+            return None, err
+
+    failed = {}
+    links = None
+    if args.link_probe:
+        log("link probe: start")
+        links, err = attempt("link probe", lambda: link_ceiling(torch, dist, gloo_amd, ctx, world))
+        if not agreed(err is None):
+            links, failed["link_probe"] = None, err or "failed on another rank"
+        log("link ceilings: %s" % links)
+    transports = TRANSPORTS_ALL if args.calibrate == "all" else TRANSPORTS_DEFAULT
 
     def set_transport(tr):
         eng, k, blocks = tr
@@ -783,7 +852,7 @@ def bench_multi(args):
         device_engine = probe.engine() not in ("steps", "queued")
         probe.close()
         if args.copy_split == "auto" and not device_engine:
-            for tr in TRANSPORTS:
+            for tr in transports:
                 set_transport(tr)
                 buf.copy_(src)
                 calib[tr], _ = time_schedule(torch, dist, gloo_amd, ctx, buf, algo, 3, 1)
@@ -814,30 +883,8 @@ def bench_multi(args):
     def checksum(t):
         return int(t.view(torch.int16 if es == 2 else torch.int32).to(torch.int64).sum().item())
 
-    if args.algo == "ring_chunked" and args.schedule == "auto":
-        candidates = ["ring_chunked", "ring_chunked_fast", "ring_chunked_host",
-                      "ring_chunked_queued", "ring_chunked_mesh", "ring_chunked_mesh_steps",
-                      "ring_chunked_mesh_queued"]
-    elif args.algo == "ring_chunked" and args.schedule == "mesh":
-        candidates = ["ring_chunked_mesh", "ring_chunked_mesh_steps", "ring_chunked_mesh_queued"]
-    else:
-        candidates = [args.algo]
-    # A candidate that fails on any rank (a timeout, a HIP error) is dropped
-    # on every rank and named in the JSON line; the others still report.
-    def agreed(ok):
-        flag = torch.tensor([0 if ok else 1], dtype=torch.int32)
-        dist.all_reduce(flag)
-        return int(flag.item()) == 0
-
-    def attempt(what, fn):
-        try:
-            return fn(), None
-        except Exception as e:  # noqa: BLE001 - reported in the JSON line
-            err = "%s: %s" % (type(e).__name__, str(e)[:300])
-            log("%s failed: %s" % (what, err))
-            return None, err
-
-    runs, failed = {}, {}
+    candidates, alt_list = candidate_lists(args)
+    runs = {}
     for a in candidates:
         r, err = attempt(a, lambda: tuned(a))
         if not agreed(err is None):
@@ -878,31 +925,26 @@ def bench_multi(args):
                    "bytes_sent_per_step": runs[a]["sent"], "transport": runs[a]["transport"],
                    "engine": ENGINES.get(a),
                    "busiest_link_GBps": round(lm / runs[a]["t"] / 1e9, 2)}
-    if not args.no_alt:
-        for other in ("ring_chunked", "ring_chunked_mesh", "halving_doubling",
-                      "halving_doubling_host", "halving_doubling_queued"):
-            if other in runs:
-                continue
-            buf.copy_(src)
-            torch.cuda.synchronize()
-            got, err = attempt(other, lambda: time_schedule(torch, dist, gloo_amd, ctx, buf,
-                                                            other, steps, args.warmup))
-            if not agreed(err is None):
-                failed[other] = err or "failed on another rank"
-                continue
-            ta, sent_a = got
-            p50_a = P50[other]
-            lm = busiest_link_bytes(gloo_amd, other, rank, world, n, es)
-            eng = ENGINES.get(other)
-            alts[other] = {"value": round(world * S / ta / 1e9, 3),
-                           "ms_per_step": round(ta * 1e3, 4),
-                           "p50_ms_per_step": round(p50_a * 1e3, 4),
-                           "algbw_GBps": round(S / ta / 1e9, 3),
-                           "bytes_sent_per_step": sent_a, "engine": eng,
-                           "transport": ("device-driven kernel stores (%s)" % eng
-                                         if eng not in ("steps", "queued")
-                                         else tname(runs[chosen]["tr"])),
-                           "busiest_link_GBps": round(lm / ta / 1e9, 2)}
+    for other in alt_list:
+        buf.copy_(src)
+        torch.cuda.synchronize()
+        got, err = attempt(other, lambda: time_schedule(torch, dist, gloo_amd, ctx, buf,
+                                                        other, steps, args.warmup))
+        if not agreed(err is None):
+            failed[other] = err or "failed on another rank"
+            continue
+        ta, sent_a = got
+        lm = busiest_link_bytes(gloo_amd, other, rank, world, n, es)
+        eng = ENGINES.get(other)
+        alts[other] = {"value": round(world * S / ta / 1e9, 3),
+                       "ms_per_step": round(ta * 1e3, 4),
+                       "p50_ms_per_step": round(P50[other] * 1e3, 4),
+                       "algbw_GBps": round(S / ta / 1e9, 3),
+                       "bytes_sent_per_step": sent_a, "engine": eng,
+                       "transport": ("device-driven kernel stores (%s)" % eng
+                                     if eng not in ("steps", "queued")
+                                     else tname(runs[chosen]["tr"])),
+                       "busiest_link_GBps": round(lm / ta / 1e9, 2)}
     staged = None
     if args.staged:
         # host buffers: the fastest host-issued schedule (its H2D / D2H
@@ -917,17 +959,25 @@ def bench_multi(args):
             staged, failed["host_staged"] = None, err or "failed on another rank"
     sweep = None
     if args.sweep:
+        sweep_scheds = [a for a in ("ring_chunked", "ring_chunked_mesh") if a in runs]
         sweep, err = attempt("sweep", lambda: element_sweep(torch, dist, gloo_amd, ctx, dev,
-                                                            candidates, args.dtype))
+                                                            sweep_scheds, args.dtype))
         if not agreed(err is None):
             sweep, failed["sweep"] = None, err or "failed on another rank"
+    # transport health: every rank's peer view and transport counters
+    mine = {"peer_info": peer_info, "stats": {a: TRANSPORT.get(a) for a in runs}}
+    every = [None] * world
+    dist.all_gather_object(every, mine)
+    health, health_err = transport_health([e["peer_info"] for e in every],
+                                          [e["stats"] for e in every])
     res = None
     if rank == 0:
         algbw = S / t / 1e9
         busbw = algbw * 2 * (world - 1) / world
         link_max = busiest_link_bytes(gloo_amd, chosen, rank, world, n, es)
         link_ach = link_max / t / 1e9
-        hbm = plan_hbm_bytes(gloo_amd, chosen, rank, world, n, es)
+        fused = ENGINES.get(chosen) == "devsteps"
+        hbm = plan_hbm_bytes(gloo_amd, chosen, rank, world, n, es, fused=fused)
         hbm_ach = hbm / t / 1e9
         measured = None
         if links is not None:
@@ -938,10 +988,31 @@ def bench_multi(args):
                             note="fraction of the measured per-link ceiling for the chosen "
                                  "schedule's pattern (ring: every rank -> rank+1 at once; "
                                  "mesh: every rank -> every peer at once)")
-        elif link_err is not None:
-            measured = {"note": link_err}
+        elif "link_probe" in failed:
+            measured = {"error": failed["link_probe"]}
+        else:
+            measured = {"note": "not run (--no-link-probe)"}
+        ns = None
+        # the reference's own data movement (r -> r+1) on whichever engine ran
+        # it fastest: the plan kernel or host-issued steps
+        ring_runs = [a for a in runs if plan_name(a) == "ring_chunked"]
+        if ring_runs:
+            best_ring = min(ring_runs, key=lambda a: runs[a]["t"])
+            rr = runs[best_ring]
+            ns = north_star_block(S, world, rr["t"], rr["p50"], ENGINES.get(best_ring),
+                                  plan_hbm_bytes(gloo_amd, best_ring, rank, world, n, es,
+                                                 fused=ENGINES.get(best_ring) == "devsteps"))
+            ns["candidate"] = best_ring
+            ns["transport"] = rr["transport"]
+            if links is not None:
+                best = max(links.get("ring_dma_GBps", 0), links.get("ring_kernel_GBps", 0))
+                if best > 0:
+                    ns["measured_link_GBps"] = best
+                    ns["measured_link_frac"] = round(ns["link_GBps"] / best, 4)
+        else:
+            ns = {"error": failed.get("ring_chunked", "not timed")}
         res = {
-            "metric": "allreduce GB/s (device-resident, fp32) at 1/2/4/8 MI355X; % HBM|xGMI roofline",
+            "metric": metric_name(args.dtype),
             "value": round(world * S / t / 1e9, 3), "unit": "GB/s", "n_gpus": world,
             "steps": steps, "warmup": args.warmup, "ms_per_step": round(t * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -949,17 +1020,16 @@ def bench_multi(args):
             "config": {"workload": "allreduce_%s_%s_%dMiB_per_rank" % (
                            args.algo, {"f32": "fp32"}.get(args.dtype, args.dtype), args.size_mib),
                        "algorithm": args.algo,
+                       "candidate": chosen,
                        "schedule": {"ring_chunked": "ring", "ring_chunked_mesh": "mesh",
                                     "halving_doubling": "halving_doubling"}[plan_name(chosen)],
                        "engine": ENGINES.get(chosen),
+                       "fast_streams": FAST.get(chosen),
                        "schedule_note": "ring_chunked's chunking and reduction order; ring = "
                                         "the reference's data movement, mesh = all links "
                                         "(bit-identical, checked); engine: devsteps = the "
                                         "step program in one kernel, twoshot = the mesh in "
-                                        "one kernel, steps = host-issued, queued = host-issued "
-                                        "at once with stream-ordered waits on peers; *_fast = "
-                                        "the plan kernel with nontemporal loads and "
-                                        "write-through stores (opt-in)",
+                                        "one kernel, steps = host-issued",
                        "bytes_per_rank": S, "elements": n,
                        "parallelism": "dp%d" % world,
                        "transport": "xGMI peer copies: " + runs[chosen]["transport"],
@@ -969,6 +1039,7 @@ def bench_multi(args):
             "algbw_GBps": round(algbw, 3), "busbw_GBps": round(busbw, 3),
             "algbw_GiBps": round(S / t / 2 ** 30, 3),
             "p50_ms_per_step": round(runs[chosen]["p50"] * 1e3, 4),
+            "north_star": ns,
             # the collective's own bound: its busiest xGMI link (the ring puts
             # all 1.75 S on rank -> rank+1), with the step's HBM bytes beside it
             "roofline": {"bound": "xgmi_link", "achieved": round(link_ach, 2),
@@ -985,12 +1056,15 @@ def bench_multi(args):
                                  "note": "one rank's HBM bytes per step from the step "
                                          "program (bench.plan_hbm_bytes) / ms_per_step"}},
             "transport_stats": {a: TRANSPORT.get(a) for a in runs},
+            "transport_health": health,
             "result_checks": CHECKS,
             "alt_schedules": alts,
             "device_engines": device_engines,
             "sweep": sweep,
             "verified": verified,
         }
+        if health_err is not None:
+            res["error"] = health_err
         if staged is not None:
             res["host_staged"] = staged
         if failed:
@@ -1021,6 +1095,7 @@ def main():
                      "(one process per GPU)")
         res = bench_single(args)
     if res is not None:
+        res["bench_wall_s"] = round(time.time() - T_START, 2)
         print(json.dumps(res), flush=True)
 
 

@@ -69,9 +69,10 @@ def set_steps_engine(engine):
 
 
 def set_engine_streams(policy):
-    """Loads and stores of the device-driven kernels for algorithms created
-    afterwards: "plain" (default; "auto" is the same) or "fast" (nontemporal
-    loads, write-through stores; opt-in)."""
+    """Loads and stores of the plan kernel for algorithms created afterwards:
+    "auto" (default: "fast" for the ring's programs, "plain" for the others),
+    "plain", or "fast" (nontemporal loads, write-through stores; DESIGN.md
+    5b, 9).  The one-shot and two-shot kernels are always plain."""
     code = {"plain": 0, "fast": 1, "auto": -1}[policy]
     errors.check(_lib.lib.glx_set_engine_streams(code), "set_engine_streams")
 

@@ -70,10 +70,16 @@ SIGNATURES = [
     ("glx_algorithm_done_ranges", _i64, [_vp, ctypes.POINTER(_i64), _i64]),
     ("glx_algorithm_bytes_sent", _i64, [_vp]),
     ("glx_algorithm_engine", _i, [_vp]),
+    ("glx_algorithm_fast_streams", _i, [_vp]),
     ("glx_algorithm_destroy", None, [_vp]),
     ("glx_algorithm_transport_stats", _i, [_vp, ctypes.POINTER(_i64), _i]),
     ("glx_algorithm_record", _i, [_vp, _vp]),
     ("glx_context_ipc_stats", _i, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
+    ("glx_context_peer_info", _i, [_vp, _i, ctypes.POINTER(_i)]),
+    ("glx_link_probe_create", _vp, [_vp, _sz]),
+    ("glx_link_probe_run", _i, [_vp, _i, _i, _i, _i, ctypes.POINTER(ctypes.c_double),
+                                ctypes.POINTER(_sz)]),
+    ("glx_link_probe_destroy", None, [_vp]),
     ("glx_event_create", _i, [ctypes.POINTER(_vp)]),
     ("glx_event_destroy", _i, [_vp]),
     ("glx_event_record", _i, [_vp, _vp]),

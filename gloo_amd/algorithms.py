@@ -204,6 +204,11 @@ class Algorithm:
         return {0: "steps", 1: "oneshot", 2: "twoshot", 3: "devsteps",
                 4: "queued"}[lib.glx_algorithm_engine(self._h)]
 
+    def fast_streams(self):
+        """True when the plan kernel runs nontemporal loads and write-through
+        stores (set_engine_streams; automatic for the ring's programs)."""
+        return bool(lib.glx_algorithm_fast_streams(self._h))
+
     def transport_stats(self):
         """How this algorithm's messages moved since it was created:
         peer_copies (hipMemcpyPeerAsync over xGMI), device_copies

@@ -14,6 +14,7 @@
 #include "executor.h"
 #include "host_ops.h"
 #include "kernels.h"
+#include "linkprobe.h"
 #include "plan.h"
 #include "store.h"
 
@@ -25,6 +26,9 @@ struct glx_context {
 };
 struct glx_algorithm {
   std::unique_ptr<gloo::HipPlanExecutor> a;
+};
+struct glx_link_probe {
+  std::unique_ptr<gloo::LinkProbe> p;
 };
 
 namespace {
@@ -452,6 +456,10 @@ int glx_algorithm_engine(glx_algorithm* alg) {
   return alg->a->engine();
 }
 
+int glx_algorithm_fast_streams(glx_algorithm* alg) {
+  return alg != nullptr && alg->a->fastStreams() ? 1 : 0;
+}
+
 int glx_algorithm_transport_stats(glx_algorithm* alg, int64_t* out, int cap) {
   if (alg == nullptr || out == nullptr || cap < 6) {
     fail(GLX_ERR_INVALID, "glx_algorithm_transport_stats: null algorithm/output or cap < 6");
@@ -471,6 +479,52 @@ int glx_algorithm_record(glx_algorithm* alg, glx_event_t ev) {
   return guarded([&]() -> int {
     GLX_ENFORCE(alg != nullptr && ev != nullptr, "null algorithm/event");
     alg->a->recordDone((hipEvent_t)ev);
+    return GLX_OK;
+  });
+}
+
+int glx_context_peer_info(glx_context* ctx, int peer, int* info) {
+  return guarded([&]() -> int {
+    GLX_ENFORCE(ctx != nullptr && info != nullptr, "null argument");
+    GLX_ENFORCE(ctx->c->connected(), "context not connected");
+    GLX_ENFORCE(peer >= 0 && peer < ctx->c->size, "peer ", peer, " out of range");
+    const gloo::PeerEndpoint& p = ctx->c->peer(peer);
+    const gloo::PeerEndpoint& me = ctx->c->peer(ctx->c->rank);
+    info[0] = p.localDevice;
+    info[1] = (!p.busId.empty() && p.busId == me.busId) ||
+                      (p.busId.empty() && p.pid == me.pid && p.device == me.device)
+                  ? 1
+                  : 0;
+    info[2] = p.canAccessPeer;
+    info[3] = p.nativeAtomics;
+    info[4] = ctx->c->flagStores() ? 1 : 0;
+    return GLX_OK;
+  });
+}
+
+glx_link_probe* glx_link_probe_create(glx_context* ctx, size_t bytes) {
+  glx_link_probe* out = nullptr;
+  guarded([&]() -> int {
+    GLX_ENFORCE(ctx != nullptr, "null context");
+    out = new glx_link_probe{std::unique_ptr<gloo::LinkProbe>(new gloo::LinkProbe(ctx->c, bytes))};
+    return GLX_OK;
+  });
+  return out;
+}
+
+int glx_link_probe_run(glx_link_probe* probe, int pattern, int engine, int blocks, int reps,
+                       double* seconds, size_t* link_bytes) {
+  return guarded([&]() -> int {
+    GLX_ENFORCE(probe != nullptr && seconds != nullptr, "null argument");
+    *seconds = probe->p->run(pattern, engine, blocks, reps);
+    if (link_bytes != nullptr) *link_bytes = probe->p->busiestLinkBytes(pattern);
+    return GLX_OK;
+  });
+}
+
+void glx_link_probe_destroy(glx_link_probe* probe) {
+  guarded([&]() -> int {
+    delete probe;
     return GLX_OK;
   });
 }

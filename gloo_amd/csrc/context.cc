@@ -475,7 +475,12 @@ void Context::connectFullMesh(std::shared_ptr<rendezvous::Store> store) {
     p.ctl->open(p.shmName);
     if (p.localDevice >= 0 && p.localDevice != device_) {
       int can = 0;
-      if (hipDeviceCanAccessPeer(&can, device_, p.localDevice) == hipSuccess && can) {
+      if (hipDeviceCanAccessPeer(&can, device_, p.localDevice) != hipSuccess) {
+        (void)hipGetLastError();
+        can = 0;
+      }
+      p.canAccessPeer = can;
+      if (can) {
         int cur = 0;
         hipGetDevice(&cur);
         hipSetDevice(device_);
@@ -489,11 +494,12 @@ void Context::connectFullMesh(std::shared_ptr<rendezvous::Store> store) {
       }
       int atomics = 0;
       if (hipDeviceGetP2PAttribute(&atomics, hipDevP2PAttrNativeAtomicSupported, device_,
-                                   p.localDevice) != hipSuccess ||
-          atomics == 0) {
+                                   p.localDevice) != hipSuccess) {
         (void)hipGetLastError();
-        flagStores_ = true;
+        atomics = 0;
       }
+      p.nativeAtomics = atomics;
+      if (atomics == 0) flagStores_ = true;
     }
   }
   if (const char* e = std::getenv("GLOO_AMD_FLAG_WRITE")) {

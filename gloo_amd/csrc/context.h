@@ -76,6 +76,11 @@ struct PeerEndpoint {
   int localDevice = -1;  // the same GPU's ordinal in this process (-1: unknown)
   bool sameProcess = false;
   std::string busId;  // PCI bus id of the rank's GPU ("" if unknown)
+  // read at connect when the peer's GPU is another one of this process's
+  // devices (-1 otherwise): hipDeviceCanAccessPeer, and
+  // hipDevP2PAttrNativeAtomicSupported of the link (0 -> flag stores)
+  int canAccessPeer = -1;
+  int nativeAtomics = -1;
   std::string shmName;
   std::unique_ptr<ControlBlock> ctl;  // mapped peer control block
 };

@@ -115,6 +115,8 @@ class HipPlanExecutor : public Algorithm {
   // How run() executes: kEngineSteps (host-issued schedule steps),
   // kEngineOneShot / kEngineTwoShot (one device-driven kernel per rank).
   int engine() const { return engine_; }
+  // the plan kernel runs nontemporal loads and write-through stores
+  bool fastStreams() const { return engine_ == kEngineDevSteps && pk_.fast != 0; }
 
  private:
   struct OutChan {  // this rank -> peer

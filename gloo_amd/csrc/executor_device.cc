@@ -76,7 +76,8 @@ void HipPlanExecutor::setStepsEngine(int engine) {
 int HipPlanExecutor::stepsEngine() { return g_steps_engine.load(); }
 
 namespace {
-// 0 plain (default; -1 = auto = plain), 1 fast.  GLOO_AMD_ENGINE_STREAMS=fast|plain.
+// -1 auto (default: fast for the ring's programs), 0 plain, 1 fast.
+// GLOO_AMD_ENGINE_STREAMS=fast|plain|auto.
 std::atomic<int> g_engine_streams{[] {
   const char* e = std::getenv("GLOO_AMD_ENGINE_STREAMS");
   if (e != nullptr && std::strcmp(e, "fast") == 0) return 1;
@@ -188,10 +189,15 @@ void HipPlanExecutor::setupDevice() {
   os_.flagStore = fs;
   ts_.flagStore = fs;
   pk_.flagStore = fs;
-  // The plan kernel's streams (setEngineStreams): plain unless
-  // set_engine_streams("fast").  The one-shot and two-shot kernels are
-  // always plain.
-  pk_.fast = engineStreams() > 0 ? 1 : 0;
+  // The plan kernel's streams (setEngineStreams).  Automatic:
+  // nontemporal loads and write-through stores for the ring's programs,
+  // whose fused reduce-and-forward passes then leave no dirty line for each
+  // step's system-scope release to write back; plain for the
+  // others (halving-doubling measured slower with them).  The one-shot and
+  // two-shot kernels are always plain.
+  const int pol = engineStreams();
+  const bool ring = algo_ == glx::ALGO_RING_CHUNKED || algo_ == glx::ALGO_FN_RING;
+  pk_.fast = (pol > 0 || (pol < 0 && ring)) ? 1 : 0;
   GLX_HIP_CHECK(hipEventCreateWithFlags(&ddDone_, hipEventDisableTiming));
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) == hipSuccess &&
@@ -293,6 +299,11 @@ void HipPlanExecutor::setupDevSteps() {
     return (e != nullptr && std::strcmp(e, "load") == 0) ? 1 : 0;
   }();
   pk_.pollLoad = pollLoad;
+  static const int narrow = [] {
+    const char* e = std::getenv("GLOO_AMD_RELEASE");
+    return (e != nullptr && std::strcmp(e, "narrow") == 0) ? 1 : 0;
+  }();
+  pk_.narrowRelease = narrow;
   pk_.trace = nullptr;
   if (devTrace()) {
     const size_t n = G * (2 * plan_.steps.size() + 1);

@@ -144,6 +144,8 @@ struct PlanKernelParams {
   int* status;
   int* claim;
   int pollLoad;                // 1: poll flags with atomic loads (GLOO_AMD_FLAG_POLL=load)
+  int narrowRelease;           // 1: SEND flags after completing the stores only, no L2
+                               //    write-back (GLOO_AMD_RELEASE=narrow; experiment)
   int flagStore;               // 1: write peers' flags with stores (Context::flagStores)
   int fast;                    // 1: nontemporal loads, write-through stores (plan kernel only;
                                // every span's stores stay below kWtMaxStream by construction)

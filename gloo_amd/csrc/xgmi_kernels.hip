@@ -309,6 +309,20 @@ __device__ __forceinline__ void signal_flag(uint64_t* word, uint64_t value, bool
   if (threadIdx.x == 0) put_flag(word, value, store);
 }
 
+// The plan kernel's narrow form (PlanKernelParams::narrowRelease): the data a
+// peer reads after this flag was stored into ITS landing slot, uncached
+// memory (MTYPE UC) that no L2 holds, so completing the stores (vmcnt) is
+// enough; the system-scope release above also writes back every dirty line
+// of this XCD's L2 (buffer_wbl2), which only our own buffer's lines can be.
+// An experiment knob (GLOO_AMD_RELEASE=narrow): the one-GPU box cannot show
+// cross-GPU visibility, bench.py times it as a result-checked candidate.
+__device__ __forceinline__ void signal_flag_narrow(uint64_t* word, uint64_t value, bool store) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) put_flag(word, value, store);
+}
+
 // The first workgroup of the launch whose wait times out reports it: status
 // = 1 + peer (+ 256 * (1 + step) when the plan kernel says where), then as
 // 64-bit words 1..3 the value seen, the value awaited and the workgroup.
@@ -582,7 +596,11 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
             }
           }
         }
-        signal_flag(flag_at(st.flag, w), seq, p.flagStore != 0);
+        if (p.narrowRelease) {
+          signal_flag_narrow(flag_at(st.flag, w), seq, p.flagStore != 0);
+        } else {
+          signal_flag(flag_at(st.flag, w), seq, p.flagStore != 0);
+        }
         break;
       }
       case 1:  // RECV

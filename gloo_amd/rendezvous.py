@@ -156,10 +156,54 @@ class Context:
         check(lib.glx_context_ipc_stats(self._h, ctypes.byref(a), ctypes.byref(b)), "ipc_stats")
         return {"imports": a.value, "base_fixups": b.value}
 
+    def peer_info(self, peer):
+        """What this rank read at connect about `peer`'s GPU: its device
+        ordinal here, whether it is our own GPU, hipDeviceCanAccessPeer and
+        the link's hipDevP2PAttrNativeAtomicSupported (None: same GPU or not
+        asked), and whether our kernels write peers' flags with stores."""
+        import ctypes
+        v = (ctypes.c_int * 5)()
+        check(lib.glx_context_peer_info(self._h, int(peer), v), "peer_info")
+        opt = (lambda x: None if x < 0 else bool(x))
+        return {"device": v[0], "same_gpu": bool(v[1]), "can_access_peer": opt(v[2]),
+                "native_atomics": opt(v[3]), "flag_stores": bool(v[4])}
+
     def close(self):
         h = getattr(self, "_h", None)
         if h:
             lib.glx_context_destroy(h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+class LinkProbe:
+    """Measured link ceilings between the context's ranks (glx.h
+    glx_link_probe_*): a receive block per rank through the context's own
+    canary-checked IPC path.  Creating one is collective.  run() is per rank
+    and does not synchronise: barrier before it and take the max time over
+    ranks; barrier again before close()."""
+
+    RING, MESH = 0, 1
+    DMA, KERNEL = 0, 1
+
+    def __init__(self, ctx, nbytes):
+        self._ctx = ctx  # keep alive
+        self._h = check_handle(lib.glx_link_probe_create(ctx.handle, int(nbytes)), "LinkProbe")
+
+    def run(self, pattern, engine, blocks=256, reps=5):
+        """(seconds on this rank, bytes per round on its busiest link)."""
+        import ctypes
+        secs, lb = ctypes.c_double(0.0), ctypes.c_size_t(0)
+        check(lib.glx_link_probe_run(self._h, int(pattern), int(engine), int(blocks), int(reps),
+                                     ctypes.byref(secs), ctypes.byref(lb)), "LinkProbe.run")
+        return secs.value, lb.value
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib.glx_link_probe_destroy(h)
             self._h = None
 
     def __del__(self):

@@ -162,14 +162,13 @@ int glx_set_device_engines(int mode);
  * steps) or GLX_ENGINE_QUEUED (host-issued steps, stream-ordered waits).
  * Env GLOO_AMD_STEPS_ENGINE=device|host|queued. */
 int glx_set_steps_engine(int engine);
-/* Cache policy of the device-driven kernels' own loads and stores (one-shot,
- * two-shot, plan kernel) for algorithms created afterwards: 0 plain (default;
- * -1 is the same), 1 nontemporal loads and write-through (sc1) stores -- the
- * reduce kernel's policy.  An opt-in: on one shared GPU it made the ring's
- * plan kernel 6-9 % faster and halving-doubling / two-shot ~7 % slower, and
- * one two-shot test run with it failed; bench.py times the
- * ring with it as a separate, result-checked candidate.  Env
- * GLOO_AMD_ENGINE_STREAMS=fast. */
+/* Cache policy of the plan kernel's own loads and stores for algorithms
+ * created afterwards: -1 automatic (default: nontemporal loads and
+ * write-through (sc1) stores -- the reduce kernel's policy -- for the ring's
+ * programs, whose reduce-and-forward steps then leave nothing dirty for the
+ * per-step release; plain for the others), 0 plain, 1 nontemporal and
+ * write-through for every program.  The one-shot and two-shot kernels are
+ * always plain.  Env GLOO_AMD_ENGINE_STREAMS=fast|plain. */
 int glx_set_engine_streams(int fast);
 
 /* Number of visible HIP devices (0 when no GPU). */
@@ -368,6 +367,9 @@ int64_t glx_algorithm_bytes_sent(glx_algorithm* alg);
  * side streams, reductions the glx reduce kernel on the compute stream. */
 #define GLX_ENGINE_QUEUED 4
 int glx_algorithm_engine(glx_algorithm* alg);
+/* 1 when the algorithm's plan kernel runs nontemporal loads and write-through
+ * stores (glx_set_engine_streams), else 0. */
+int glx_algorithm_fast_streams(glx_algorithm* alg);
 /* How this algorithm's messages actually moved since it was created, as 6
  * int64 written to out (cap >= 6): {peer_copies (hipMemcpyPeerAsync, the DMA
  * engines over xGMI), device_copies (hipMemcpyAsync: peers on the same device,
@@ -387,6 +389,35 @@ void glx_algorithm_destroy(glx_algorithm* alg);
  * runtime mapped at the base of the exporter's allocation rather than at the
  * exported pointer (corrected with the published offset).  Returns GLX_OK. */
 int glx_context_ipc_stats(glx_context* ctx, int64_t* imports, int64_t* base_fixups);
+
+/* What this rank learnt about peer `peer`'s GPU at connect (the link the
+ * transport will use; the reference's analog is the PCI distance it reads,
+ * gloo/common/linux.cc:126).  info[5] =
+ *   {device ordinal of the peer's GPU in this process (-1 unknown),
+ *    1 if it is this rank's own GPU,
+ *    hipDeviceCanAccessPeer (-1: same GPU / not asked),
+ *    hipDevP2PAttrNativeAtomicSupported of the link (-1: same GPU / not asked),
+ *    1 if this rank's kernels write peers' flags with stores (some link lacks
+ *      atomics, or GLOO_AMD_FLAG_WRITE=store)}. */
+int glx_context_peer_info(glx_context* ctx, int peer, int* info);
+
+/* ---- measured link ceilings ----------------------------------
+ * A receive block of `bytes` per rank, exported and imported through the
+ * context's own canary-checked IPC path (the one every engine uses) and
+ * uncached like the engines' landing regions.  create is collective (every
+ * rank, same bytes, in the same order as its other creations).  run writes
+ * `reps` rounds, pattern 0 = ring (`bytes` to rank+1) or 1 = mesh
+ * (bytes/(P-1) to every peer), engine 0 = hipMemcpyPeerAsync (one stream per
+ * destination) or 1 = the copy kernel (`blocks` workgroups shared by the
+ * destinations), and returns this rank's seconds and the bytes one round
+ * puts on its busiest link.  run is NOT synchronising: callers barrier
+ * before it (so every rank sends at once) and take the max over ranks;
+ * destroy only after a barrier that follows every rank's last run. */
+typedef struct glx_link_probe glx_link_probe;
+glx_link_probe* glx_link_probe_create(glx_context* ctx, size_t bytes);
+int glx_link_probe_run(glx_link_probe* probe, int pattern, int engine, int blocks, int reps,
+                       double* seconds, size_t* link_bytes);
+void glx_link_probe_destroy(glx_link_probe* probe);
 
 /* ---- events (gloo::CudaStream's record / wait, gloo/cuda.h:40-120) -------
  * A caller that gives an algorithm streams gets its outputs valid once

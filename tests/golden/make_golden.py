@@ -277,9 +277,11 @@ def make_allreduce_fn():
 # Inputs are O.fill(dtype, N, seed=SEED, rank=r); the tests
 # regenerate them on each rank and compare SHA-256 digests.
 SCALE_CASES = [(O.RING_CHUNKED, 8, 1 << k, O.FLOAT32) for k in range(10, 25, 2)]
-SCALE_CASES += [(O.HALVING_DOUBLING, 8, 1 << 26, O.FLOAT32),
-                (O.RING_CHUNKED, 8, 1 << 28, O.FLOAT16),
-                (O.RING_CHUNKED, 8, 1 << 28, O.BFLOAT16)]
+# cfg5 is 1 GiB per rank: 2^29 16-bit elements (536,870,912;
+# the reference's `int count` holds it, gloo/allreduce_ring_chunked.h:239-240)
+CFG5_CASES = [(O.RING_CHUNKED, 8, 1 << 29, O.FLOAT16),
+              (O.RING_CHUNKED, 8, 1 << 29, O.BFLOAT16)]
+SCALE_CASES += [(O.HALVING_DOUBLING, 8, 1 << 26, O.FLOAT32)] + CFG5_CASES
 
 
 def scale_case_name(c):
@@ -288,10 +290,14 @@ def scale_case_name(c):
                                   O.DTYPE_NAMES[dtype])
 
 
-def make_scale():
+def make_scale(only=None):
+    """Every BASELINE-scale case, or (only = a list of cases) just those,
+    replacing the same-named or same-(algo, P, dtype) entries of the existing
+    file (cfg5 alone: `make_golden.py scale5`, ~40 GiB of RAM)."""
     path = os.path.join(HERE, "scale_golden.json")
     cases = []
-    for c in SCALE_CASES:
+    todo = SCALE_CASES if only is None else only
+    for c in todo:
         algo, P, N, dtype = c
         ins = [[O.fill(dtype, N, 0, seed=SEED, rank=r)] for r in range(P)]
         pinned = dtype != O.BFLOAT16
@@ -313,6 +319,11 @@ def make_scale():
         })
         print(cases[-1]["name"], cases[-1]["output_sha256"][:16], flush=True)
         del ins, res, first
+    if only is not None:
+        with open(path) as f:
+            old = json.load(f)["cases"]
+        keys = {(c["algo"], c["P"], c["dtype"]) for c in cases}
+        cases = [c for c in old if (c["algo"], c["P"], c["dtype"]) not in keys] + cases
     with open(path, "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py (make_scale)",
                    "source": "oracle/_ref/libgloo_ref.so (the reference compiled from "
@@ -334,6 +345,8 @@ if __name__ == "__main__":
         make_allreduce()
     if "allreduce_fn" in which:
         make_allreduce_fn()
-    if "scale" in which:  # not in the default set: minutes and ~20 GiB of RAM
+    if "scale" in which:  # not in the default set: minutes and ~40 GiB of RAM
         make_scale()
+    if "scale5" in which:  # cfg5 alone (1 GiB per rank, 8 ranks)
+        make_scale(CFG5_CASES)
     print("done")

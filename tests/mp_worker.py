@@ -19,6 +19,10 @@ algo: ring_chunked | halving_doubling | ring_chunked_mesh (class algorithms)
       raise IoException)
       scale:cfg34 | scale:cfg5 (BASELINE.json configs at full size, 8 ranks:
       every engine's output SHA-256 against tests/golden/scale_golden.json)
+      big:fast | big:plain (the ring on the plan kernel over MORE than 2 GiB per
+      rank, P = 2, the given stream policy: every 32-bit store offset the
+      write-through path could form is exceeded; exact at P = 2 since fp32
+      addition commutes: the result must equal x0 + x1 bit for bit)
 
 Checks its result against the oracle and prints OK."""
 import os
@@ -55,6 +59,8 @@ def main():
         return run_churn(store_dir, rank, size)
     if algo.startswith("scale:"):
         return run_scale(store_dir, rank, size, algo[len("scale:"):])
+    if algo.startswith("big:"):
+        return run_big(store_dir, rank, size, algo[len("big:"):])
     if algo.startswith("fn_"):
         return run_fn(store_dir, rank, size, algo, N)
     code = O.HALVING_DOUBLING if algo == "halving_doubling" else O.RING_CHUNKED
@@ -525,6 +531,57 @@ def run_device(store_dir, rank, size, mode):
     for r in range(size):
         store.get("done/%d" % r, timeout_ms=60000)
     print("IPC rank %d %s" % (rank, ctx.ipc_stats()), flush=True)
+    ctx.close()
+    if bad:
+        print("MISMATCH rank", rank, bad[:10])
+        sys.exit(1)
+    print("OK")
+
+
+def run_big(store_dir, rank, size, policy):
+    import torch
+
+    import gloo_amd
+    assert size == 2, "big: P = 2 (the result is x0 + x1 exactly)"
+    n = (1 << 29) + 4096 + 5  # fp32: 2 GiB + 16 KiB + 20 B per rank, odd tail
+    dev = torch.device("cuda", 0)
+
+    def inp(r):
+        g = torch.Generator(device=dev).manual_seed(777 + r)
+        return torch.rand(n, device=dev, generator=g) * 2 - 1
+    buf = inp(rank)
+    torch.cuda.synchronize()
+    store = gloo_amd.rendezvous.FileStore(store_dir)
+    ctx = gloo_amd.rendezvous.Context(rank, size, 0)
+    ctx.setTimeout(120)
+    ctx.connectFullMesh(store)
+    gloo_amd.set_steps_engine("device")
+    gloo_amd.set_engine_streams(policy)
+    try:
+        alg = gloo_amd.AllreduceRingChunked(ctx, [buf], schedule="ring")
+    finally:
+        gloo_amd.set_steps_engine("auto")
+        gloo_amd.set_engine_streams("auto")
+    print("big rank %d engine %s fast %s" % (rank, alg.engine(), alg.fast_streams()), flush=True)
+    bad = []
+    if alg.engine() != "devsteps" or alg.fast_streams() != (policy == "fast"):
+        bad.append(("engine", alg.engine(), alg.fast_streams()))
+    for it in range(2):
+        if it:
+            buf.copy_(inp(rank))
+            torch.cuda.synchronize()
+        alg.run()
+        exp = inp(0) + inp(1)
+        diff = int((buf.view(torch.int32) != exp.view(torch.int32)).sum().item())
+        if diff:
+            first = int((buf.view(torch.int32) != exp.view(torch.int32)).nonzero()[0].item())
+            bad.append(("run", it, diff, first))
+        del exp
+        torch.cuda.empty_cache()
+    alg.close()
+    store.set("done/%d" % rank, b"1")
+    for r in range(size):
+        store.get("done/%d" % r, timeout_ms=120000)
     ctx.close()
     if bad:
         print("MISMATCH rank", rank, bad[:10])

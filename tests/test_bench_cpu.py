@@ -93,3 +93,71 @@ def test_roofline_byte_counts_ring_p8():
     assert mesh == 2 * S // 8
     hbm = bench.plan_hbm_bytes(gloo_amd, "ring_chunked", 0, 8, n, es)
     assert hbm == 63 * S // 8  # 7.875 S: sends 2 x 1.75 S, reduces 3 x 0.875 S, copies 2 x 0.875 S
+
+
+def test_fused_hbm_bytes_ring_p8():
+    """The plan kernel's reduce-and-forward: 26 of the ring's 28 sends at P=8
+    re-use the pass that wrote their range, so they only write the receiver's
+    copy: 7.875 S - 26/16 S = 6.25 S per step."""
+    gloo_amd = pytest.importorskip("gloo_amd")
+    n, es = 1 << 20, 4
+    S = n * es
+    hbm = bench.plan_hbm_bytes(gloo_amd, "ring_chunked", 0, 8, n, es, fused=True)
+    assert hbm == 100 * S // 16
+
+
+def test_north_star_block_p8():
+    S = 256 << 20
+    ns = bench.north_star_block(S, 8, 3.5e-3, 3.4e-3, "devsteps", 100 * S // 16)
+    # 1.75 S on the one link at 153 GB/s = 3.07 ms; the 80 % target 3.84 ms
+    assert ns["link_bytes_per_step"] == 7 * S // 4
+    assert abs(ns["link_bound_ms"] - 3.0704) < 1e-3
+    assert abs(ns["target_ms"] - 3.838) < 1e-3
+    assert abs(ns["link_frac"] - 3.0704 / 3.5) < 1e-3
+
+
+def test_candidate_lists_default_is_small():
+    class A:
+        algo, schedule, candidates, no_alt = "ring_chunked", "auto", "default", False
+    c, alts = bench.candidate_lists(A)
+    assert c[0] == "ring_chunked" and len(c) + len(alts) <= 4
+    assert not any(x.endswith(("_fast", "_queued")) for x in c + alts)
+    A.candidates = "all"
+    c, alts = bench.candidate_lists(A)
+    assert "ring_chunked_fast" in c and "halving_doubling_queued" in alts
+
+
+def test_metric_name_follows_dtype():
+    assert bench.metric_name("f32") == (
+        "allreduce GB/s (device-resident, fp32) at 1/2/4/8 MI355X; % HBM|xGMI roofline")
+    assert "f16" in bench.metric_name("f16")
+
+
+def _info(same, atomics=True, access=True, stores=False):
+    return {"device": 1, "same_gpu": same, "can_access_peer": None if same else access,
+            "native_atomics": None if same else atomics, "flag_stores": stores}
+
+
+def test_transport_health_distinct_gpus():
+    ok = {"ring_chunked": {"peer_copies": 0, "device_copies": 0, "kernel_copies": 0,
+                           "device_kernels": 3, "bytes": 0, "host_folds": 0}}
+    infos = [[_info(False)], [_info(False)]]
+    st, err = bench.transport_health(infos, [ok, ok])
+    assert err is None and st["ranks_on_distinct_gpus"]
+    # a hipMemcpyAsync fallback on one rank is an error on the node
+    bad = {"ring_chunked_host": dict(ok["ring_chunked"], device_copies=28)}
+    st, err = bench.transport_health(infos, [ok, bad])
+    assert err is not None and "hipMemcpyAsync" in err and "rank 1" in err
+    # a link without native atomics (flag words written with stores)
+    infos2 = [[_info(False, atomics=False, stores=True)], [_info(False)]]
+    st, err = bench.transport_health(infos2, [ok, ok])
+    assert err is not None and "atomics" in err and st["flag_stores"] == [True, False]
+
+
+def test_transport_health_shared_gpu_rehearsal_is_not_an_error():
+    """Ranks sharing one GPU (the one-GPU rehearsal) copy with hipMemcpyAsync
+    by design; that is reported, not an error."""
+    st = {"ring_chunked_host": {"peer_copies": 0, "device_copies": 28, "kernel_copies": 0,
+                                "device_kernels": 0, "bytes": 1, "host_folds": 0}}
+    status, err = bench.transport_health([[_info(True)], [_info(True)]], [st, st])
+    assert err is None and not status["ranks_on_distinct_gpus"]
