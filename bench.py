@@ -420,12 +420,13 @@ RING_SCHEDULES = {"ring_chunked": "ring", "ring_chunked_mesh": "mesh",
 ENGINES = {}  # bench name -> engine the product chose (steps/oneshot/twoshot/devsteps)
 TRANSPORT = {}  # bench name -> the algorithm's transport_stats() after its timed runs
 FAST = {}  # bench name -> whether its plan kernel ran the fast streams
+SYNC = {}  # bench name -> its device engine's flag sync ("narrow" / "system" / None)
 CHECKS = {}  # bench name -> result_check() of its post-timing run
 
 
 def plan_name(algo):
     """Schedule name of a bench candidate for gloo_amd.plan()."""
-    for suffix in ("_host", "_queued", "_fast", "_plain"):
+    for suffix in ("_narrow", "_system", "_host", "_queued", "_fast", "_plain"):
         if algo.endswith(suffix):
             algo = algo[:-len(suffix)]
     return {"ring_chunked_mesh_steps": "ring_chunked_mesh",
@@ -441,6 +442,13 @@ def make_alg(gloo_amd, ctx, buf, algo):
     the same steps enqueued at once with stream-ordered waits on peers;
     *_fast the plan kernel with the opt-in nontemporal loads and
     write-through stores (set_engine_streams)."""
+    for suffix, policy in (("_narrow", "narrow"), ("_system", "system")):
+        if algo.endswith(suffix):  # the device engines with a forced flag sync
+            gloo_amd.set_device_sync(policy)
+            try:
+                return make_alg(gloo_amd, ctx, buf, algo[:-len(suffix)])
+            finally:
+                gloo_amd.set_device_sync("auto")
     for suffix, policy in (("_fast", "fast"), ("_plain", "plain")):
         if algo.endswith(suffix):  # the plan kernel with a forced stream policy
             gloo_amd.set_engine_streams(policy)
@@ -493,6 +501,7 @@ def time_schedule(torch, dist, gloo_amd, ctx, buf, algo, steps, warmup):
     alg = make_alg(gloo_amd, ctx, buf, algo)
     ENGINES[algo] = alg.engine()
     FAST[algo] = alg.fast_streams() if ENGINES[algo] == "devsteps" else None
+    SYNC[algo] = alg.sync_mode()
     log("%s: created (engine %s), warmup %d" % (algo, ENGINES[algo], warmup))
     for _ in range(warmup):
         alg.run()
@@ -923,7 +932,8 @@ def bench_multi(args):
                    "p50_ms_per_step": round(runs[a]["p50"] * 1e3, 4),
                    "algbw_GBps": round(S / runs[a]["t"] / 1e9, 3),
                    "bytes_sent_per_step": runs[a]["sent"], "transport": runs[a]["transport"],
-                   "engine": ENGINES.get(a),
+                   "engine": ENGINES.get(a), "fast_streams": FAST.get(a),
+                   "sync": SYNC.get(a),
                    "busiest_link_GBps": round(lm / runs[a]["t"] / 1e9, 2)}
     for other in alt_list:
         buf.copy_(src)
@@ -941,6 +951,7 @@ def bench_multi(args):
                        "p50_ms_per_step": round(P50[other] * 1e3, 4),
                        "algbw_GBps": round(S / ta / 1e9, 3),
                        "bytes_sent_per_step": sent_a, "engine": eng,
+                       "fast_streams": FAST.get(other), "sync": SYNC.get(other),
                        "transport": ("device-driven kernel stores (%s)" % eng
                                      if eng not in ("steps", "queued")
                                      else tname(runs[chosen]["tr"])),
@@ -1004,6 +1015,8 @@ def bench_multi(args):
                                                  fused=ENGINES.get(best_ring) == "devsteps"))
             ns["candidate"] = best_ring
             ns["transport"] = rr["transport"]
+            ns["fast_streams"] = FAST.get(best_ring)
+            ns["sync"] = SYNC.get(best_ring)
             if links is not None:
                 best = max(links.get("ring_dma_GBps", 0), links.get("ring_kernel_GBps", 0))
                 if best > 0:
@@ -1025,6 +1038,7 @@ def bench_multi(args):
                                     "halving_doubling": "halving_doubling"}[plan_name(chosen)],
                        "engine": ENGINES.get(chosen),
                        "fast_streams": FAST.get(chosen),
+                       "sync": SYNC.get(chosen),
                        "schedule_note": "ring_chunked's chunking and reduction order; ring = "
                                         "the reference's data movement, mesh = all links "
                                         "(bit-identical, checked); engine: devsteps = the "

@@ -77,6 +77,16 @@ def set_engine_streams(policy):
     errors.check(_lib.lib.glx_set_engine_streams(code), "set_engine_streams")
 
 
+def set_device_sync(mode):
+    """Release / acquire around the device engines' flags for algorithms
+    created afterwards: "auto" (default), "system" (L2 written back before
+    and invalidated after every flag) or "narrow" (stores completed before a
+    flag, the CU's L1 invalidated after a wait: enough because every flag
+    publishes data in the receiver's uncached landing slots)."""
+    code = {"auto": -1, "system": 0, "narrow": 1}[mode]
+    errors.check(_lib.lib.glx_set_device_sync(code), "set_device_sync")
+
+
 def set_device_engines(mode):
     """Device-driven engines (one-shot / two-shot kernels) for algorithms
     created afterwards: "auto" (default: when no two ranks are threads sharing

@@ -71,6 +71,8 @@ SIGNATURES = [
     ("glx_algorithm_bytes_sent", _i64, [_vp]),
     ("glx_algorithm_engine", _i, [_vp]),
     ("glx_algorithm_fast_streams", _i, [_vp]),
+    ("glx_algorithm_sync", _i, [_vp]),
+    ("glx_set_device_sync", _i, [_i]),
     ("glx_algorithm_destroy", None, [_vp]),
     ("glx_algorithm_transport_stats", _i, [_vp, ctypes.POINTER(_i64), _i]),
     ("glx_algorithm_record", _i, [_vp, _vp]),

@@ -209,6 +209,11 @@ class Algorithm:
         stores (set_engine_streams; automatic for the ring's programs)."""
         return bool(lib.glx_algorithm_fast_streams(self._h))
 
+    def sync_mode(self):
+        """Release / acquire of its device engine around flags: "narrow",
+        "system", or None for host-issued steps (set_device_sync)."""
+        return {1: "narrow", 0: "system", -1: None}[lib.glx_algorithm_sync(self._h)]
+
     def transport_stats(self):
         """How this algorithm's messages moved since it was created:
         peer_copies (hipMemcpyPeerAsync over xGMI), device_copies

@@ -456,6 +456,14 @@ int glx_algorithm_engine(glx_algorithm* alg) {
   return alg->a->engine();
 }
 
+int glx_set_device_sync(int mode) {
+  if (mode < -1 || mode > 1) return fail(GLX_ERR_INVALID, "glx_set_device_sync: -1, 0 or 1");
+  gloo::HipPlanExecutor::setDeviceSync(mode);
+  return GLX_OK;
+}
+
+int glx_algorithm_sync(glx_algorithm* alg) { return alg != nullptr ? alg->a->syncMode() : -1; }
+
 int glx_algorithm_fast_streams(glx_algorithm* alg) {
   return alg != nullptr && alg->a->fastStreams() ? 1 : 0;
 }

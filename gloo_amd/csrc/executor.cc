@@ -396,7 +396,8 @@ void HipPlanExecutor::release() noexcept {
     if (e != nullptr) hipEventDestroy(e);
   }
   for (char* d : devBufs_) hipFree(d);
-  if (hostStage_) hipHostFree(hostStage_);
+  givePinned(hostStage_, hostStageBytes_);
+  hostStage_ = nullptr;
   for (char* d : fnStage_) hipFree(d);
   for (void* p : registered_) hipHostUnregister(p);
   for (auto& e : events_) {

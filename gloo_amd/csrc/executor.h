@@ -199,6 +199,7 @@ class HipPlanExecutor : public Algorithm {
                  const std::vector<hipStream_t>& streams, const glx::PlanParams& prm,
                  bool perCallBuffers);
   void release() noexcept;
+  static void givePinned(char* p, size_t bytes);
   // Before our memory is freed: wait (bounded by the context timeout) until
   // every receiver has credited our last message.  Those credit stores are
   // the only writes a peer can still make into our memory (shm counters or,
@@ -242,6 +243,7 @@ class HipPlanExecutor : public Algorithm {
   std::vector<char*> devBufs_;     // device copy of each user pointer (or of hostStage_)
   bool hostFold_ = false;          // several pointers < kOnDeviceThreshold: fold on the host
   char* hostStage_ = nullptr;      // pinned: the host fold's result, staged and returned
+  size_t hostStageBytes_ = 0;      // its size (from and back to a process-wide cache)
   std::vector<void*> hostSources() const;  // H2D sources of the staged buffer
   std::vector<void*> hostDests() const;    // where its final values go back to
   // staged_: the current run stages host memory (class host mode, or a
@@ -382,6 +384,19 @@ class HipPlanExecutor : public Algorithm {
   // 0 plain loads and stores (default), 1 nontemporal loads and write-through
   // stores (glx_set_engine_streams).
   static void setEngineStreams(int fast);
+  // release / acquire around the device engines' flags: -1 auto, 0 system
+  // scope, 1 narrow (kernels.h); for algorithms created afterwards
+  static void setDeviceSync(int mode);
+  static int deviceSync();
+  static constexpr bool kAutoNarrow = false;
+  // 1 when the device engine runs the narrow release / acquire, 0 system
+  // scope, -1 host-issued steps
+  int syncMode() const {
+    return engine_ == kEngineSteps || engine_ == kEngineQueued
+               ? -1
+               : (engine_ == kEngineDevSteps ? pk_.narrow
+                                              : (engine_ == kEngineOneShot ? os_.narrow : ts_.narrow));
+  }
   static int engineStreams();
 };
 

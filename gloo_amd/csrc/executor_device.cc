@@ -86,6 +86,23 @@ std::atomic<int> g_engine_streams{[] {
 }()};
 }  // namespace
 
+namespace {
+// -1 auto, 0 system-scope release / acquire around the device engines' flags,
+// 1 narrow (kernels.h).  GLOO_AMD_SYNC=system|narrow.
+std::atomic<int> g_device_sync{[] {
+  const char* e = std::getenv("GLOO_AMD_SYNC");
+  if (e != nullptr && std::strcmp(e, "narrow") == 0) return 1;
+  if (e != nullptr && std::strcmp(e, "system") == 0) return 0;
+  return -1;
+}()};
+}  // namespace
+
+void HipPlanExecutor::setDeviceSync(int mode) {
+  g_device_sync.store(mode < 0 ? -1 : (mode != 0 ? 1 : 0));
+}
+
+int HipPlanExecutor::deviceSync() { return g_device_sync.load(); }
+
 void HipPlanExecutor::setEngineStreams(int fast) {
   g_engine_streams.store(fast < 0 ? -1 : (fast != 0 ? 1 : 0));
 }
@@ -198,6 +215,12 @@ void HipPlanExecutor::setupDevice() {
   const int pol = engineStreams();
   const bool ring = algo_ == glx::ALGO_RING_CHUNKED || algo_ == glx::ALGO_FN_RING;
   pk_.fast = (pol > 0 || (pol < 0 && ring)) ? 1 : 0;
+  // release / acquire around the flags (kernels.h): automatic = kAutoNarrow
+  const int sync = deviceSync();
+  const int narrow = sync < 0 ? (kAutoNarrow ? 1 : 0) : sync;
+  os_.narrow = narrow;
+  ts_.narrow = narrow;
+  pk_.narrow = narrow;
   GLX_HIP_CHECK(hipEventCreateWithFlags(&ddDone_, hipEventDisableTiming));
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) == hipSuccess &&
@@ -299,11 +322,7 @@ void HipPlanExecutor::setupDevSteps() {
     return (e != nullptr && std::strcmp(e, "load") == 0) ? 1 : 0;
   }();
   pk_.pollLoad = pollLoad;
-  static const int narrow = [] {
-    const char* e = std::getenv("GLOO_AMD_RELEASE");
-    return (e != nullptr && std::strcmp(e, "narrow") == 0) ? 1 : 0;
-  }();
-  pk_.narrowRelease = narrow;
+
   pk_.trace = nullptr;
   if (devTrace()) {
     const size_t n = G * (2 * plan_.steps.size() + 1);

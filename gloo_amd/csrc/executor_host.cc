@@ -7,6 +7,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <mutex>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -152,6 +153,51 @@ void HipPlanExecutor::runFnHost(const FnCall& call) {
   checkDevice();
 }
 
+namespace {
+// Pinned host staging blocks (hipHostMalloc) are not handed back to the
+// runtime while the process lives: they wait here for the next algorithm,
+// the policy context.cc applies to uncached device blocks after freed ones
+// were seen breaking later allocations of the same process.
+struct PinnedCache {
+  std::mutex mu;
+  std::vector<std::pair<size_t, char*>> free;
+};
+
+PinnedCache& pinnedCache() {
+  static PinnedCache* c = new PinnedCache();  // never destroyed
+  return *c;
+}
+
+char* takePinned(size_t* bytes) {
+  PinnedCache& c = pinnedCache();
+  {
+    std::lock_guard<std::mutex> g(c.mu);
+    const size_t most = std::max(2 * *bytes, *bytes + (size_t(4) << 20));
+    size_t best = c.free.size();
+    for (size_t i = 0; i < c.free.size(); i++) {
+      const size_t b = c.free[i].first;
+      if (b >= *bytes && b <= most && (best == c.free.size() || b < c.free[best].first)) best = i;
+    }
+    if (best != c.free.size()) {
+      char* p = c.free[best].second;
+      *bytes = c.free[best].first;
+      c.free.erase(c.free.begin() + (long)best);
+      return p;
+    }
+  }
+  char* p = nullptr;
+  GLX_HIP_CHECK(hipHostMalloc((void**)&p, *bytes, hipHostMallocDefault));
+  return p;
+}
+}  // namespace
+
+void HipPlanExecutor::givePinned(char* p, size_t bytes) {
+  if (p == nullptr) return;
+  PinnedCache& c = pinnedCache();
+  std::lock_guard<std::mutex> g(c.mu);
+  c.free.emplace_back(bytes, p);
+}
+
 void HipPlanExecutor::setupHostMode() {
   const size_t bytes = (size_t)count_ * esize_;
   // Several host pointers under kOnDeviceThreshold: fold them on the host
@@ -160,8 +206,8 @@ void HipPlanExecutor::setupHostMode() {
   // gloo/cuda_allreduce_halving_doubling.cc:478-484)
   hostFold_ = ptrs_.size() > 1 && bytes < glx::kOnDeviceThreshold;
   if (hostFold_) {
-    GLX_HIP_CHECK(hipHostMalloc((void**)&hostStage_, std::max<size_t>(bytes, 16),
-                                hipHostMallocDefault));
+    hostStageBytes_ = std::max<size_t>(bytes, 16);
+    hostStage_ = takePinned(&hostStageBytes_);
   }
   for (void* p : hostSources()) {
     if (!isPinnedHost(p)) {

@@ -48,6 +48,13 @@ constexpr int kOsMaxSlices = 512;  // workgroups (= slices) per launch
 // Flags are 8-byte words, each alone in its 128-byte L2 line: flag f of a
 // row starts at row + f * kFlagStride (no line holds flags of two writers).
 constexpr int kFlagStride = 16;
+// Release / acquire around the device engines' flags.  Everything a flag
+// publishes lives in the receiver's landing slots: uncached device memory
+// (MTYPE UC), never held by an L2.  System scope (narrow = 0) still writes
+// back every dirty line of the XCD's L2 before each flag (buffer_wbl2 sc0
+// sc1) and invalidates the L2 after each wait (buffer_inv sc0 sc1); narrow
+// (1) only completes the stores (s_waitcnt vmcnt(0)) before a flag and
+// invalidates the CU's L1 after a wait (agent scope).
 constexpr size_t kFlagBytes = kFlagStride * sizeof(uint64_t);
 struct OneShotParams {
   char* buf;                        // this rank's buffer: input and result
@@ -58,6 +65,7 @@ struct OneShotParams {
   int* status;                      // host-visible: 1 + rank that never arrived
   int* claim;                       // device word: the first timed-out workgroup reports
   int flagStore;                    // 1: write peers' flags with stores (Context::flagStores)
+  int narrow;                       // 1: narrow release / acquire around flags (below)
   uint64_t epoch;                   // >= 1, +1 per call, equal on all ranks
   uint64_t timeoutTicks;            // s_memrealtime ticks
   size_t count;                     // elements
@@ -86,6 +94,7 @@ struct TwoShotParams {
   int* status;
   int* claim;
   int flagStore;
+  int narrow;                       // 1: narrow release / acquire around flags (below)
   uint64_t epoch, timeoutTicks;
   size_t rangeOff[kOsMaxRanks], rangeLen[kOsMaxRanks];  // by owner
   uint8_t chain[kOsMaxRanks];       // this rank's fold order
@@ -144,8 +153,7 @@ struct PlanKernelParams {
   int* status;
   int* claim;
   int pollLoad;                // 1: poll flags with atomic loads (GLOO_AMD_FLAG_POLL=load)
-  int narrowRelease;           // 1: SEND flags after completing the stores only, no L2
-                               //    write-back (GLOO_AMD_RELEASE=narrow; experiment)
+  int narrow;                  // 1: narrow release / acquire around flags (below)
   int flagStore;               // 1: write peers' flags with stores (Context::flagStores)
   int fast;                    // 1: nontemporal loads, write-through stores (plan kernel only;
                                // every span's stores stay below kWtMaxStream by construction)

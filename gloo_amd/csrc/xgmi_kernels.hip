@@ -288,13 +288,39 @@ __device__ __forceinline__ const uint64_t* flag_at(const uint64_t* row, int w) {
 
 // Every wave's stores complete and visible system-wide, then (by lanes
 // 0..P-1, lane r excluded, where want(lane)) flag words set to epoch.
-template <typename Want>
-__device__ __forceinline__ void release_flags(uint64_t* const* rows, int P, int rank, int w,
-                                              uint64_t epoch, bool store, Want want) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+// Release before a flag.  system: every dirty line of this XCD's L2 written
+// back (buffer_wbl2 sc0 sc1) and the stores completed.  narrow: the stores
+// completed only -- enough when everything the flag publishes was stored into
+// the receiver's landing slot, uncached memory (MTYPE UC) that no L2 holds
+// (the device engines' protocol); the workgroup fence keeps
+// the compiler from moving the stores past the flag.
+__device__ __forceinline__ void release_stores(bool narrow) {
+  if (narrow) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  }
   // the compiler may drop the wait after the write-back when it can prove no
   // store is outstanding (MI355X_MICROARCH.md, compiler hazard): keep it
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+
+// Acquire after a flag.  system: this CU's L1 and this XCD's L2 invalidated
+// (buffer_inv sc0 sc1).  narrow: the L1 only (agent scope, buffer_inv sc1):
+// the landing slots are uncached, so no L2 line of them can be stale.
+__device__ __forceinline__ void acquire_loads(bool narrow) {
+  if (narrow) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+}
+
+template <typename Want>
+__device__ __forceinline__ void release_flags(uint64_t* const* rows, int P, int rank, int w,
+                                              uint64_t epoch, bool store, Want want,
+                                              bool narrow) {
+  release_stores(narrow);
   __syncthreads();
   const int t = (int)threadIdx.x;
   if (t < P && t != rank && want(t)) put_flag(flag_at(rows[t], w), epoch, store);
@@ -302,23 +328,9 @@ __device__ __forceinline__ void release_flags(uint64_t* const* rows, int P, int 
 
 // Every wave's stores complete and visible system-wide, then lane 0 stores
 // `value` into `word` (a flag in a peer's memory).
-__device__ __forceinline__ void signal_flag(uint64_t* word, uint64_t value, bool store) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) put_flag(word, value, store);
-}
-
-// The plan kernel's narrow form (PlanKernelParams::narrowRelease): the data a
-// peer reads after this flag was stored into ITS landing slot, uncached
-// memory (MTYPE UC) that no L2 holds, so completing the stores (vmcnt) is
-// enough; the system-scope release above also writes back every dirty line
-// of this XCD's L2 (buffer_wbl2), which only our own buffer's lines can be.
-// An experiment knob (GLOO_AMD_RELEASE=narrow): the one-GPU box cannot show
-// cross-GPU visibility, bench.py times it as a result-checked candidate.
-__device__ __forceinline__ void signal_flag_narrow(uint64_t* word, uint64_t value, bool store) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+__device__ __forceinline__ void signal_flag(uint64_t* word, uint64_t value, bool store,
+                                            bool narrow) {
+  release_stores(narrow);
   __syncthreads();
   if (threadIdx.x == 0) put_flag(word, value, store);
 }
@@ -355,7 +367,7 @@ __device__ __forceinline__ uint64_t poll_flag(const uint64_t* word, bool pollLoa
 
 __device__ __forceinline__ bool wait_flag(const uint64_t* word, uint64_t epoch, int peer,
                                           uint64_t start, uint64_t timeoutTicks, int* status,
-                                          int* claim, int* s_ok, bool acquire = true,
+                                          int* claim, int* s_ok, bool narrow, bool acquire = true,
                                           int where = 0, bool pollLoad = false) {
   if (threadIdx.x == 0) {
     int ok = 1;
@@ -375,7 +387,7 @@ __device__ __forceinline__ bool wait_flag(const uint64_t* word, uint64_t epoch, 
       __builtin_amdgcn_s_sleep(2);
     }
     // drop any stale copy of the landing lines before anyone reads them
-    if (acquire) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (acquire) acquire_loads(narrow);
     *s_ok = ok;
   }
   __syncthreads();
@@ -403,14 +415,15 @@ __device__ __forceinline__ void oneshot_body(const OneShotParams& p) {
     to[d - 1] = d < p.P ? p.push[j] : nullptr;
   }
   scatter_span<S, FAST>(to, p.P - 1, buf, e0, e1, aligned);
-  release_flags(p.flagOut, p.P, p.rank, w, p.epoch, p.flagStore != 0, [](int) { return true; });
+  release_flags(p.flagOut, p.P, p.rank, w, p.epoch, p.flagStore != 0, [](int) { return true; },
+                p.narrow != 0);
 
   // 2. wait
   const uint64_t start = __builtin_amdgcn_s_memrealtime();
   for (int k = 0; k < p.P; k++) {
     if (k == p.rank) continue;
     if (!wait_flag(flag_at(p.flagIn, k * p.G + w), p.epoch, k, start, p.timeoutTicks,
-                   p.status, p.claim, &s_ok)) {
+                   p.status, p.claim, &s_ok, p.narrow != 0)) {
       return;
     }
   }
@@ -472,7 +485,7 @@ __device__ __forceinline__ void twoshot_body(const TwoShotParams& p) {
   release_flags(p.flagAOut, p.P, p.rank, w, p.epoch, p.flagStore != 0, [&](int j) {
     size_t a, b;
     return span(j, a, b);
-  });
+  }, p.narrow != 0);
   stamp(1);
 
   // 2. fold my range's slice from every peer's copy; result to my buffer
@@ -483,7 +496,7 @@ __device__ __forceinline__ void twoshot_body(const TwoShotParams& p) {
     for (int k = 0; k < p.P; k++) {
       if (k == p.rank) continue;
       if (!wait_flag(flag_at(p.flagAIn, k * p.G + w), p.epoch, k, start, p.timeoutTicks,
-                     p.status, p.claim, &s_ok)) {
+                     p.status, p.claim, &s_ok, p.narrow != 0)) {
         return;
       }
     }
@@ -503,7 +516,7 @@ __device__ __forceinline__ void twoshot_body(const TwoShotParams& p) {
     }
     fold_span<T, OP, FAST>(buf, src, p.P, outs, p.P - 1, a, b, aligned);
     release_flags(p.flagBOut, p.P, p.rank, w, p.epoch, p.flagStore != 0,
-                  [](int) { return true; });
+                  [](int) { return true; }, p.narrow != 0);
   }
   stamp(3);
 
@@ -513,7 +526,7 @@ __device__ __forceinline__ void twoshot_body(const TwoShotParams& p) {
     if (j < 0) j += p.P;
     if (!span(j, a, b)) continue;
     if (!wait_flag(flag_at(p.flagBIn, j * p.G + w), p.epoch, j, start, p.timeoutTicks,
-                   p.status, p.claim, &s_ok)) {
+                   p.status, p.claim, &s_ok, p.narrow != 0)) {
       return;
     }
     if (d == 1) stamp(4);
@@ -550,6 +563,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
   S* buf = reinterpret_cast<S*>(p.buf);
   const bool aligned = ((uintptr_t)p.buf % 16) == 0;
   const bool pollLoad = p.pollLoad != 0;
+  const bool narrow = p.narrow != 0;
   // diagnostics (GLOO_AMD_DEVTRACE=1): per workgroup and step, when the step
   // started and when its wait (if any) was satisfied
   uint64_t* tr = p.trace != nullptr ? p.trace + (size_t)w * (2 * (size_t)p.nsteps + 1) : nullptr;
@@ -569,7 +583,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
         if (seq > (uint64_t)p.slots &&
             !wait_flag(flag_at(st.credit, w), seq - p.slots, st.peer,
                        __builtin_amdgcn_s_memrealtime(), p.timeoutTicks, p.status, p.claim,
-                       &s_ok, /*acquire=*/false, 1 + i, pollLoad)) {
+                       &s_ok, narrow, /*acquire=*/false, 1 + i, pollLoad)) {
           return;
         }
         stamp(2 * i + 1);
@@ -596,16 +610,12 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
             }
           }
         }
-        if (p.narrowRelease) {
-          signal_flag_narrow(flag_at(st.flag, w), seq, p.flagStore != 0);
-        } else {
-          signal_flag(flag_at(st.flag, w), seq, p.flagStore != 0);
-        }
+        signal_flag(flag_at(st.flag, w), seq, p.flagStore != 0, narrow);
         break;
       }
       case 1:  // RECV
         if (!wait_flag(flag_at(st.flag, w), seq, st.peer, __builtin_amdgcn_s_memrealtime(),
-                       p.timeoutTicks, p.status, p.claim, &s_ok, true, 1 + i, pollLoad)) {
+                       p.timeoutTicks, p.status, p.claim, &s_ok, narrow, true, 1 + i, pollLoad)) {
           return;
         }
         stamp(2 * i + 1);

@@ -171,6 +171,17 @@ int glx_set_steps_engine(int engine);
  * always plain.  Env GLOO_AMD_ENGINE_STREAMS=fast|plain. */
 int glx_set_engine_streams(int fast);
 
+/* Release / acquire around the device engines' flag words (one-shot,
+ * two-shot, plan kernel) for algorithms created afterwards.  Everything a
+ * flag publishes is stored into the receiver's landing slot, uncached device
+ * memory that no L2 holds.  0 = system scope: before every flag the XCD's
+ * whole L2 is written back (buffer_wbl2 sc0 sc1), after every wait it is
+ * invalidated (buffer_inv sc0 sc1); 1 = narrow: the stores are completed
+ * (s_waitcnt vmcnt(0)) before a flag and the CU's L1 invalidated after a wait
+ * (agent scope); -1 = automatic (default).  Env GLOO_AMD_SYNC=system|narrow.
+ * Every rank may choose independently (the protocol is the same). */
+int glx_set_device_sync(int mode);
+
 /* Number of visible HIP devices (0 when no GPU). */
 int glx_device_count(int* count);
 
@@ -370,6 +381,9 @@ int glx_algorithm_engine(glx_algorithm* alg);
 /* 1 when the algorithm's plan kernel runs nontemporal loads and write-through
  * stores (glx_set_engine_streams), else 0. */
 int glx_algorithm_fast_streams(glx_algorithm* alg);
+/* Release / acquire its device engine runs around flag words: 1 narrow, 0
+ * system scope, -1 host-issued steps (glx_set_device_sync). */
+int glx_algorithm_sync(glx_algorithm* alg);
 /* How this algorithm's messages actually moved since it was created, as 6
  * int64 written to out (cap >= 6): {peer_copies (hipMemcpyPeerAsync, the DMA
  * engines over xGMI), device_copies (hipMemcpyAsync: peers on the same device,
