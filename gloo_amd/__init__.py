@@ -70,16 +70,17 @@ def set_steps_engine(engine):
 
 def set_engine_streams(policy):
     """Loads and stores of the plan kernel for algorithms created afterwards:
-    "auto" (default: "fast" for the ring's programs, "plain" for the others),
-    "plain", or "fast" (nontemporal loads, write-through stores; DESIGN.md
-    5b, 9).  The one-shot and two-shot kernels are always plain."""
+    "auto" (default: "plain", except "fast" for the ring's programs under the
+    system-scope flag sync), "plain", or "fast" (nontemporal loads,
+    write-through stores).  The one-shot and two-shot kernels
+    are always plain."""
     code = {"plain": 0, "fast": 1, "auto": -1}[policy]
     errors.check(_lib.lib.glx_set_engine_streams(code), "set_engine_streams")
 
 
 def set_device_sync(mode):
     """Release / acquire around the device engines' flags for algorithms
-    created afterwards: "auto" (default), "system" (L2 written back before
+    created afterwards: "auto" (default: narrow), "system" (L2 written back before
     and invalidated after every flag) or "narrow" (stores completed before a
     flag, the CU's L1 invalidated after a wait: enough because every flag
     publishes data in the receiver's uncached landing slots)."""

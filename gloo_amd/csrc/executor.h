@@ -388,7 +388,7 @@ class HipPlanExecutor : public Algorithm {
   // scope, 1 narrow (kernels.h); for algorithms created afterwards
   static void setDeviceSync(int mode);
   static int deviceSync();
-  static constexpr bool kAutoNarrow = false;
+  static constexpr bool kAutoNarrow = true;
   // 1 when the device engine runs the narrow release / acquire, 0 system
   // scope, -1 host-issued steps
   int syncMode() const {

@@ -206,21 +206,22 @@ void HipPlanExecutor::setupDevice() {
   os_.flagStore = fs;
   ts_.flagStore = fs;
   pk_.flagStore = fs;
-  // The plan kernel's streams (setEngineStreams).  Automatic:
-  // nontemporal loads and write-through stores for the ring's programs,
-  // whose fused reduce-and-forward passes then leave no dirty line for each
-  // step's system-scope release to write back; plain for the
-  // others (halving-doubling measured slower with them).  The one-shot and
-  // two-shot kernels are always plain.
-  const int pol = engineStreams();
-  const bool ring = algo_ == glx::ALGO_RING_CHUNKED || algo_ == glx::ALGO_FN_RING;
-  pk_.fast = (pol > 0 || (pol < 0 && ring)) ? 1 : 0;
+  // The plan kernel's streams (setEngineStreams): nontemporal loads and
+  // write-through stores, or plain.  The one-shot and two-shot kernels are
+  // always plain.
   // release / acquire around the flags (kernels.h): automatic = kAutoNarrow
   const int sync = deviceSync();
   const int narrow = sync < 0 ? (kAutoNarrow ? 1 : 0) : sync;
   os_.narrow = narrow;
   ts_.narrow = narrow;
   pk_.narrow = narrow;
+  // the plan kernel's stream policy, automatic: write-through only where a
+  // system-scope release would otherwise write back the ring's freshly
+  // reduced lines; with the narrow release nothing is written back and plain
+  // stores measured faster
+  const int pol = engineStreams();
+  const bool ring = algo_ == glx::ALGO_RING_CHUNKED || algo_ == glx::ALGO_FN_RING;
+  pk_.fast = (pol > 0 || (pol < 0 && ring && !narrow)) ? 1 : 0;
   GLX_HIP_CHECK(hipEventCreateWithFlags(&ddDone_, hipEventDisableTiming));
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) == hipSuccess &&
@@ -234,11 +235,22 @@ void HipPlanExecutor::setupDevice() {
 // resident capacity shared by the ranks on the busiest GPU is smaller (ranks
 // spin on each other's workgroups, so every grid must be resident at once).
 // Same inputs on every rank -> same grid.
+//
+// When several ranks share a GPU (the one-GPU rehearsals and tests) their
+// grids together would fill exactly the occupancy the runtime reports, and
+// every workgroup of every grid must be resident at once: if the dispatcher
+// packs the CUs even slightly unevenly (waves of a workgroup sharing a SIMD,
+// another kernel briefly holding a slot) a workgroup waits for a slot that
+// only a spinning workgroup could free -- a deadlock that ends at the
+// timeout.  So shared GPUs keep a quarter of the reported capacity free.
 size_t HipPlanExecutor::maxSlices(int kernel) const {
   const int cap = glx::device_engine_resident_blocks(kernel, op_, dtype_);
-  const int share = context_->maxRanksPerDevice();
+  const int share = std::max(1, context_->maxRanksPerDevice());
   size_t g = glx::kOsMaxSlices;
-  if (cap > 0) g = std::min(g, (size_t)std::max(1, cap / std::max(1, share)));
+  if (cap > 0) {
+    const int usable = share > 1 ? cap * 3 / 4 : cap;
+    g = std::min(g, (size_t)std::max(1, usable / share));
+  }
   return g;
 }
 

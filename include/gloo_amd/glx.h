@@ -163,10 +163,10 @@ int glx_set_device_engines(int mode);
  * Env GLOO_AMD_STEPS_ENGINE=device|host|queued. */
 int glx_set_steps_engine(int engine);
 /* Cache policy of the plan kernel's own loads and stores for algorithms
- * created afterwards: -1 automatic (default: nontemporal loads and
- * write-through (sc1) stores -- the reduce kernel's policy -- for the ring's
- * programs, whose reduce-and-forward steps then leave nothing dirty for the
- * per-step release; plain for the others), 0 plain, 1 nontemporal and
+ * created afterwards: -1 automatic (default: plain, except nontemporal loads
+ * and write-through (sc1) stores -- the reduce kernel's policy -- for the
+ * ring's programs under the system-scope flag sync, whose per-step release
+ * then finds nothing dirty to write back), 0 plain, 1 nontemporal and
  * write-through for every program.  The one-shot and two-shot kernels are
  * always plain.  Env GLOO_AMD_ENGINE_STREAMS=fast|plain. */
 int glx_set_engine_streams(int fast);
@@ -178,7 +178,8 @@ int glx_set_engine_streams(int fast);
  * whole L2 is written back (buffer_wbl2 sc0 sc1), after every wait it is
  * invalidated (buffer_inv sc0 sc1); 1 = narrow: the stores are completed
  * (s_waitcnt vmcnt(0)) before a flag and the CU's L1 invalidated after a wait
- * (agent scope); -1 = automatic (default).  Env GLOO_AMD_SYNC=system|narrow.
+ * (agent scope); -1 = automatic (default: narrow).  Env
+ * GLOO_AMD_SYNC=system|narrow.
  * Every rank may choose independently (the protocol is the same). */
 int glx_set_device_sync(int mode);
 
