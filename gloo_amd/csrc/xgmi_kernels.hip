@@ -76,41 +76,85 @@ template <bool FAST>
 __device__ __forceinline__ v4u ldv(const v4u* p) {
   return ld16<FAST>(p);
 }
+
+// Store policies of a span's destination: plain, write-through at device
+// scope (sc1: the plan kernel's fast streams into this rank's buffer), or
+// write-through at system scope (sc0 sc1) -- every store into ANOTHER rank's
+// landing slot.  Those slots are uncached memory, so even a plain store
+// reaches it, but the narrow flag sync (kernels.h) relies on nothing of a
+// handed-off message waiting in this XCD's L2: the system write-through makes
+// that hold whatever memory type a peer's mapping gets.
+enum StorePol : int { kStPlain = 0, kStLocalWt = 1, kStRemote = 2 };
+
+template <int SP>
+struct WtCache {
+  static constexpr int aux = SP == kStRemote ? 17 : 16;  // sc0 sc1 | sc1 (gfx940 family)
+};
+
 // Stores of vectors [va, vb) of one workgroup's span.  The write-through
 // resource is built at the span's first vector, not at the (virtual) buffer
 // base: its 32-bit offsets then stay below the span's size whatever the
 // buffer's, and the base is made wave-uniform (readfirstlane) so the resource
 // lives in SGPRs instead of a per-store waterfall loop.
-template <bool FAST>
+template <int SP>
 struct VecOut {
   v4u* base;
   size_t origin;
-  WtStream wt;
+  __amdgpu_buffer_rsrc_t r;
   __device__ __forceinline__ VecOut(void* b, size_t va)
       : base(reinterpret_cast<v4u*>(b)),
         origin(va),
-        wt(FAST ? uniform_ptr(reinterpret_cast<v4u*>(b) + va) : b) {}
+        r(__builtin_amdgcn_make_buffer_rsrc(
+            SP != kStPlain ? uniform_ptr(reinterpret_cast<v4u*>(b) + va) : b, 0, 0x7fffffff,
+            0x00020000)) {}
   __device__ __forceinline__ void put(size_t i, v4u v) const {
-    if (FAST) {
-      wt.put(i - origin, v);
+    if (SP != kStPlain) {
+      __builtin_amdgcn_raw_buffer_store_b128(v, r, (unsigned)((i - origin) * 16), 0,
+                                             WtCache<SP>::aux);
     } else {
       base[i] = v;
     }
   }
 };
 
-// Copy [a, b) of src to dst (virtual-buffer pointers with equal phases).
-template <typename S, bool FAST>
+template <int N> struct BitsOf;
+template <> struct BitsOf<1> { using type = uint8_t; };
+template <> struct BitsOf<2> { using type = uint16_t; };
+template <> struct BitsOf<4> { using type = uint32_t; };
+template <> struct BitsOf<8> { using type = uint64_t; };
+
+// One element store with policy SP (the unaligned head / tail of a span):
+// write-through stores are relaxed atomic stores at the matching scope,
+// i.e. global_store_{byte,short,dword,dwordx2} sc1 / sc0 sc1.
+template <int SP, typename S>
+__device__ __forceinline__ void put1(S* p, S v) {
+  if (SP == kStPlain) {
+    *p = v;
+  } else {
+    using U = typename BitsOf<sizeof(S)>::type;
+    U u;
+    __builtin_memcpy(&u, &v, sizeof(S));
+    if (SP == kStRemote) {
+      __hip_atomic_store(reinterpret_cast<U*>(p), u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+      __hip_atomic_store(reinterpret_cast<U*>(p), u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Copy [a, b) of src to dst (virtual-buffer pointers with equal phases):
+// loads as FAST says, stores with policy SP.
+template <typename S, bool FAST, int SP>
 __device__ __forceinline__ void copy_span(S* dst, const S* src, size_t a, size_t b,
                                           bool aligned) {
   const Span sp = split_span<16 / sizeof(S)>(a, b, aligned);
   const size_t va = sp.va, vb = sp.vb;
   for (size_t t = threadIdx.x; t < sp.nedge(); t += kBlock) {
     const size_t i = sp.edge(t);
-    dst[i] = src[i];
+    put1<SP>(dst + i, src[i]);
   }
   const v4u* vs = reinterpret_cast<const v4u*>(src);
-  const VecOut<FAST> vd(dst, va);
+  const VecOut<SP> vd(dst, va);
   constexpr int U = 8;  // vectors in flight per lane
   size_t i = va + threadIdx.x;
   for (; i + (U - 1) * kBlock < vb; i += U * kBlock) {
@@ -123,8 +167,10 @@ __device__ __forceinline__ void copy_span(S* dst, const S* src, size_t a, size_t
   for (; i < vb; i += kBlock) vd.put(i, ldv<FAST>(vs + i));
 }
 
-// Copy [a, b) of src to every dsts[d] for d < n (one load, n stores).
-template <typename S, bool FAST, int MAXD = kOsMaxRanks - 1>
+// Copy [a, b) of src to every dsts[d] for d < n (one load, n stores):
+// dsts[0 .. FIRST_REMOTE-1] are this rank's (policy LSP), the rest other
+// ranks' landing slots (system write-through).
+template <typename S, bool FAST, int LSP, int FIRST_REMOTE, int MAXD = kOsMaxRanks - 1>
 __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* src, size_t a,
                                              size_t b, bool aligned) {
   const Span sp = split_span<16 / sizeof(S)>(a, b, aligned);
@@ -134,7 +180,13 @@ __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* 
     const S x = src[i];
 #pragma unroll
     for (int d = 0; d < MAXD; d++) {
-      if (d < n) reinterpret_cast<S*>(dsts[d])[i] = x;
+      if (d < n) {
+        if (d >= FIRST_REMOTE) {
+          put1<kStRemote>(reinterpret_cast<S*>(dsts[d]) + i, x);
+        } else {
+          put1<LSP>(reinterpret_cast<S*>(dsts[d]) + i, x);
+        }
+      }
     }
   }
   const v4u* vs = reinterpret_cast<const v4u*>(src);
@@ -147,9 +199,15 @@ __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* 
 #pragma unroll
     for (int d = 0; d < MAXD; d++) {
       if (d < n) {
-        const VecOut<FAST> o(dsts[d], va);
+        if (d >= FIRST_REMOTE) {
+          const VecOut<kStRemote> o(dsts[d], va);
 #pragma unroll
-        for (int u = 0; u < U; u++) o.put(i + u * kBlock, x[u]);
+          for (int u = 0; u < U; u++) o.put(i + u * kBlock, x[u]);
+        } else {
+          const VecOut<LSP> o(dsts[d], va);
+#pragma unroll
+          for (int u = 0; u < U; u++) o.put(i + u * kBlock, x[u]);
+        }
       }
     }
   }
@@ -157,7 +215,13 @@ __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* 
     const v4u x = ldv<FAST>(vs + i);
 #pragma unroll
     for (int d = 0; d < MAXD; d++) {
-      if (d < n) VecOut<FAST>(dsts[d], va).put(i, x);
+      if (d < n) {
+        if (d >= FIRST_REMOTE) {
+          VecOut<kStRemote>(dsts[d], va).put(i, x);
+        } else {
+          VecOut<LSP>(dsts[d], va).put(i, x);
+        }
+      }
     }
   }
 }
@@ -166,11 +230,14 @@ __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* 
 // (the ring's chain: the newer rank's value is the in-place destination)
 // or, LEFT, acc = op(acc, s_k) (a left fold, out = op(out, peer)).
 // The result also goes to every outs[d], d < nout.
+// dst is this rank's buffer (stores as FAST says); outs are other ranks'
+// landing slots (system write-through).
 template <typename T, int OP, bool FAST, bool LEFT = false, int MAXK = kOsMaxRanks>
 __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
                                           const typename Elem<T, OP>::S* const* srcs, int P,
                                           char* const* outs, int nout, size_t a, size_t b,
                                           bool aligned) {
+  constexpr int LSP = FAST ? kStLocalWt : kStPlain;
   using E = Elem<T, OP>;
   using S = typename E::S;
   const Span sp = split_span<16 / sizeof(S)>(a, b, aligned);
@@ -187,10 +254,10 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
     for (int k = 1; k < MAXK; k++) {
       if (k < P) acc = LEFT ? E::apply(acc, y[k]) : E::apply(y[k], acc);
     }
-    dst[i] = acc;
+    put1<LSP>(dst + i, acc);
 #pragma unroll
     for (int d = 0; d < MAXK - 1; d++) {
-      if (d < nout) reinterpret_cast<S*>(outs[d])[i] = acc;
+      if (d < nout) put1<kStRemote>(reinterpret_cast<S*>(outs[d]) + i, acc);
     }
   }
   // U vectors per lane, all U*P loads in flight before the chains: 4 for
@@ -219,13 +286,13 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
         }
       }
     }
-    const VecOut<FAST> od(dst, va);
+    const VecOut<LSP> od(dst, va);
 #pragma unroll
     for (int u = 0; u < U; u++) od.put(v + u * kBlock, acc[u]);
 #pragma unroll
     for (int d = 0; d < MAXK - 1; d++) {
       if (d < nout) {
-        const VecOut<FAST> o(outs[d], va);
+        const VecOut<kStRemote> o(outs[d], va);
 #pragma unroll
         for (int u = 0; u < U; u++) o.put(v + u * kBlock, acc[u]);
       }
@@ -242,10 +309,10 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
     for (int k = 1; k < MAXK; k++) {
       if (k < P) acc = LEFT ? vec_apply<T, OP>(acc, y[k]) : vec_apply<T, OP>(y[k], acc);
     }
-    VecOut<FAST>(dst, va).put(v, acc);
+    VecOut<LSP>(dst, va).put(v, acc);
 #pragma unroll
     for (int d = 0; d < MAXK - 1; d++) {
-      if (d < nout) VecOut<FAST>(outs[d], va).put(v, acc);
+      if (d < nout) VecOut<kStRemote>(outs[d], va).put(v, acc);
     }
   }
 }
@@ -414,7 +481,7 @@ __device__ __forceinline__ void oneshot_body(const OneShotParams& p) {
     if (j >= p.P) j -= p.P;
     to[d - 1] = d < p.P ? p.push[j] : nullptr;
   }
-  scatter_span<S, FAST>(to, p.P - 1, buf, e0, e1, aligned);
+  scatter_span<S, FAST, kStPlain, 0>(to, p.P - 1, buf, e0, e1, aligned);
   release_flags(p.flagOut, p.P, p.rank, w, p.epoch, p.flagStore != 0, [](int) { return true; },
                 p.narrow != 0);
 
@@ -480,7 +547,9 @@ __device__ __forceinline__ void twoshot_body(const TwoShotParams& p) {
     int j = p.rank + 1 + (q + w) % (p.P - 1);
     if (j >= p.P) j -= p.P;
     size_t a, b;
-    if (span(j, a, b)) copy_span<S, FAST>(reinterpret_cast<S*>(p.rsPush[j]), buf, a, b, aligned);
+    if (span(j, a, b)) {
+      copy_span<S, FAST, kStRemote>(reinterpret_cast<S*>(p.rsPush[j]), buf, a, b, aligned);
+    }
   }
   release_flags(p.flagAOut, p.P, p.rank, w, p.epoch, p.flagStore != 0, [&](int j) {
     size_t a, b;
@@ -530,7 +599,7 @@ __device__ __forceinline__ void twoshot_body(const TwoShotParams& p) {
       return;
     }
     if (d == 1) stamp(4);
-    copy_span<S, FAST>(buf, reinterpret_cast<const S*>(p.agLand[j]), a, b, aligned);
+    copy_span<S, FAST, kStPlain>(buf, reinterpret_cast<const S*>(p.agLand[j]), a, b, aligned);
   }
   stamp(5);
 }
@@ -592,7 +661,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
           for (int g = st.seg0; g < st.seg1; g++) {
             size_t a, b;
             if (seg_part(p.segs[g], w, a, b)) {
-              copy_span<S, FAST>(reinterpret_cast<S*>(dst), buf, a, b, aligned);
+              copy_span<S, FAST, kStRemote>(reinterpret_cast<S*>(dst), buf, a, b, aligned);
             }
           }
         } else {
@@ -604,7 +673,8 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
             size_t a, b;
             if (!seg_part(p.segs[g], w, a, b)) continue;
             if (st.kind == kStepCopySend) {
-              scatter_span<S, FAST, 2>(outs, 2, src, a, b, aligned);
+              scatter_span<S, FAST, FAST ? kStLocalWt : kStPlain, 1, 2>(outs, 2, src, a, b,
+                                                                        aligned);
             } else {
               fold_span<T, OP, FAST, true, 2>(buf, srcs, 2, outs + 1, 1, a, b, aligned);
             }
@@ -641,7 +711,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
           size_t a, b;
           if (!seg_part(p.segs[g], w, a, b)) continue;
           if (st.kind == 3) {
-            copy_span<S, FAST>(buf, srcs[1], a, b, aligned);
+            copy_span<S, FAST, FAST ? kStLocalWt : kStPlain>(buf, srcs[1], a, b, aligned);
           } else if (st.kind == 2 || st.left) {
             fold_span<T, OP, FAST, true, MAXSRC>(buf, srcs, n, nullptr, 0, a, b, aligned);
           } else {

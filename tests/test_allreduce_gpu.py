@@ -450,14 +450,18 @@ def test_peer_killed_raises_io_exception(P, engine, when):
                                        ("twoshot", "GLOO_AMD_FLAG_WRITE=store"),
                                        ("oneshot", "GLOO_AMD_FLAG_WRITE=store"),
                                        ("devsteps", "GLOO_AMD_FUSE=0"),
-                                       ("devsteps", "GLOO_AMD_ENGINE_STREAMS=fast")])
+                                       ("devsteps", "GLOO_AMD_ENGINE_STREAMS=fast"),
+                                       ("devsteps", "GLOO_AMD_SYNC=system"),
+                                       ("twoshot", "GLOO_AMD_SYNC=system"),
+                                       ("oneshot", "GLOO_AMD_SYNC=system")])
 def test_device_engine_variants(mode, knob):
     """The device engines' other forms, same checks as above at P=3: flag
     words written with system-scope stores (what ranks use when the link to a
-    peer's GPU carries no atomics, Context::flagStores), and the plan kernel
-    without reduce-and-forward fusion (one landing slot per channel), and the
-    plan kernel with the opt-in fast streams (nontemporal loads,
-    write-through stores)."""
+    peer's GPU carries no atomics, Context::flagStores), the plan kernel
+    without reduce-and-forward fusion (one landing slot per channel), the
+    plan kernel with nontemporal loads and write-through stores, and every
+    engine with the system-scope flag sync instead of the default narrow one
+    (DESIGN.md 4)."""
     k, v = knob.split("=")
     P = 3
     with tempfile.TemporaryDirectory() as d:
