@@ -421,12 +421,13 @@ ENGINES = {}  # bench name -> engine the product chose (steps/oneshot/twoshot/de
 TRANSPORT = {}  # bench name -> the algorithm's transport_stats() after its timed runs
 FAST = {}  # bench name -> whether its plan kernel ran the fast streams
 SYNC = {}  # bench name -> its device engine's flag sync ("narrow" / "system" / None)
+RUN_SYNC = ["auto"]  # the run's flag sync (probe_device_engines may fall back to "system")
 CHECKS = {}  # bench name -> result_check() of its post-timing run
 
 
 def plan_name(algo):
     """Schedule name of a bench candidate for gloo_amd.plan()."""
-    for suffix in ("_narrow", "_system", "_host", "_queued", "_fast", "_plain"):
+    for suffix in ("_narrow", "_system", "_host", "_fast", "_plain"):
         if algo.endswith(suffix):
             algo = algo[:-len(suffix)]
     return {"ring_chunked_mesh_steps": "ring_chunked_mesh",
@@ -438,17 +439,17 @@ def make_alg(gloo_amd, ctx, buf, algo):
     halving_doubling run their step programs in the plan kernel (devsteps) at
     every size and P, ring_chunked_mesh on the two-shot kernel, ring_chunked_repl on
     the one-shot kernel.  *_host and ring_chunked_mesh_steps are the same
-    schedules with host-issued steps (calibrated peer-copy transport), *_queued
-    the same steps enqueued at once with stream-ordered waits on peers;
-    *_fast the plan kernel with the opt-in nontemporal loads and
-    write-through stores (set_engine_streams)."""
+    schedules with host-issued steps (calibrated peer-copy transport);
+    *_fast / *_plain the plan kernel with a forced stream policy
+    (set_engine_streams), *_narrow / *_system the device engines with a
+    forced flag sync (set_device_sync; the run's default is RUN_SYNC)."""
     for suffix, policy in (("_narrow", "narrow"), ("_system", "system")):
         if algo.endswith(suffix):  # the device engines with a forced flag sync
             gloo_amd.set_device_sync(policy)
             try:
                 return make_alg(gloo_amd, ctx, buf, algo[:-len(suffix)])
             finally:
-                gloo_amd.set_device_sync("auto")
+                gloo_amd.set_device_sync(RUN_SYNC[0])
     for suffix, policy in (("_fast", "fast"), ("_plain", "plain")):
         if algo.endswith(suffix):  # the plan kernel with a forced stream policy
             gloo_amd.set_engine_streams(policy)
@@ -459,8 +460,6 @@ def make_alg(gloo_amd, ctx, buf, algo):
     engine = None
     if algo.endswith("_host"):
         engine, algo = "host", algo[:-len("_host")]
-    elif algo.endswith("_queued"):
-        engine, algo = "queued", algo[:-len("_queued")]
     elif algo in ("ring_chunked", "halving_doubling"):
         engine = "device"  # the plan kernel (the step program in one kernel per rank)
     if engine is not None:
@@ -469,7 +468,7 @@ def make_alg(gloo_amd, ctx, buf, algo):
         if algo == "halving_doubling":
             return gloo_amd.AllreduceHalvingDoubling(ctx, [buf])
         if algo == "ring_chunked_mesh_steps" or (algo == "ring_chunked_mesh" and engine):
-            gloo_amd.set_mesh_engine("steps" if engine != "queued" else "queued")
+            gloo_amd.set_mesh_engine("steps")
             try:
                 return gloo_amd.AllreduceRingChunked(ctx, [buf], schedule="mesh")
             finally:
@@ -663,50 +662,71 @@ def result_check(torch, dist, src, result):
 SWEEP_ELEMS = [1 << 10, 1 << 12, 1 << 14, 1 << 16, 1 << 18, 1 << 20, 1 << 22, 1 << 24]
 
 
-def probe_device_engines(torch, dist, gloo_amd, ctx, dev, dtype):
+def probe_device_engines(torch, dist, gloo_amd, connect, dev, dtype):
     """Before timing them, check the device-driven engines (one-shot,
-    two-shot and plan kernels) on this machine: short timeout, results bit-identical to
-    the host-issued steps engine over three refilled runs.  If any rank fails,
-    every rank turns them off for the rest of the run (the host-issued
-    schedules remain) and the JSON says why."""
-    ok, note = 1, "ok"
-    ctx.setTimeout(15)
-    try:
-        for algo, n in (("ring_chunked_repl", 65536 + 3), ("ring_chunked_mesh", (1 << 20) + 5),
-                        ("ring_chunked", 1 << 20), ("halving_doubling", 1 << 20)):
-            x = synthetic(torch, n, dtype, dev, 99 + int(os.environ.get("RANK", "0")))
-            ref = x.clone()
-            torch.cuda.synchronize()  # run() does not order itself after torch's stream
-            gloo_amd.set_device_engines("off")
-            try:
-                a = make_alg(gloo_amd, ctx, ref, algo)
-            finally:
-                gloo_amd.set_device_engines("auto")
-            a.run()
-            a.close()
-            y = x.clone()
-            a = make_alg(gloo_amd, ctx, y, algo)
-            eng = a.engine()
-            for _ in range(3):
-                y.copy_(x)
-                torch.cuda.synchronize()
+    two-shot and plan kernels) on this machine: short timeout, results
+    bit-identical to the host-issued steps engine over three refilled runs.
+    Each attempt runs on a context of its own (`connect(tag)`), so a failed
+    attempt cannot leave the ranks' algorithm slots out of step for the run.
+    The default narrow flag sync is tried first; if any rank fails, the
+    system-scope sync is tried, and if that passes it is kept
+    for the whole run; if both fail, every rank turns the device engines off
+    (the host-issued schedules remain).  The JSON line says which."""
+
+    def attempt(tag):
+        ok, note = 1, "ok"
+        ctx = connect(tag)
+        ctx.setTimeout(15)
+        try:
+            for algo, n in (("ring_chunked_repl", 65536 + 3),
+                            ("ring_chunked_mesh", (1 << 20) + 5),
+                            ("ring_chunked", 1 << 20), ("halving_doubling", 1 << 20)):
+                x = synthetic(torch, n, dtype, dev, 99 + int(os.environ.get("RANK", "0")))
+                ref = x.clone()
+                torch.cuda.synchronize()  # run() does not order itself after torch's stream
+                gloo_amd.set_device_engines("off")
+                try:
+                    a = make_alg(gloo_amd, ctx, ref, algo)
+                finally:
+                    gloo_amd.set_device_engines("auto")
                 a.run()
-                torch.cuda.synchronize()
-                if not torch.equal(y.view(torch.uint8), ref.view(torch.uint8)):
-                    ok, note = 0, "%s (%s) differs from the steps engine" % (algo, eng)
-            a.close()
-    except Exception as e:  # timeout (IoException) or HIP error on this rank
-        ok, note = 0, "%s: %s" % (type(e).__name__, str(e)[:200])
-    ctx.setTimeout(120)
-    flag = torch.tensor([ok], dtype=torch.int64)
-    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-    enabled = bool(flag.item())
-    if not enabled:
-        gloo_amd.set_device_engines("off")
-        if note == "ok":
+                a.close()
+                y = x.clone()
+                a = make_alg(gloo_amd, ctx, y, algo)
+                eng = a.engine()
+                for _ in range(3):
+                    y.copy_(x)
+                    torch.cuda.synchronize()
+                    a.run()
+                    torch.cuda.synchronize()
+                    if not torch.equal(y.view(torch.uint8), ref.view(torch.uint8)):
+                        ok, note = 0, "%s (%s) differs from the steps engine" % (algo, eng)
+                a.close()
+        except Exception as e:  # timeout (IoException) or HIP error on this rank
+            ok, note = 0, "%s: %s" % (type(e).__name__, str(e)[:200])
+        flag = torch.tensor([ok], dtype=torch.int64)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if ok and not flag.item():
             note = "failed on another rank"
-    log("device engines: %s (%s)" % ("enabled" if enabled else "DISABLED", note))
-    return {"enabled": enabled, "probe": note}
+        dist.barrier()
+        ctx.close()
+        return bool(flag.item()), note
+
+    enabled, note = attempt("narrow")
+    out = {"enabled": enabled, "sync": "narrow", "probe": note}
+    if not enabled:
+        log("device engines: narrow sync failed the probe (%s); trying the system sync" % note)
+        gloo_amd.set_device_sync("system")
+        RUN_SYNC[0] = "system"
+        enabled, note2 = attempt("system")
+        out = {"enabled": enabled, "sync": "system", "probe": note2,
+               "narrow_probe": note}
+        if not enabled:
+            gloo_amd.set_device_sync("auto")
+            RUN_SYNC[0] = "auto"
+            gloo_amd.set_device_engines("off")
+    log("device engines: %s (%s)" % ("enabled" if enabled else "DISABLED", out))
+    return out
 
 
 def element_sweep(torch, dist, gloo_amd, ctx, dev, schedules, dtype):
@@ -733,10 +753,10 @@ def element_sweep(torch, dist, gloo_amd, ctx, dev, schedules, dtype):
 
 
 DEFAULT_CANDIDATES = ["ring_chunked", "ring_chunked_mesh", "ring_chunked_host"]
-EXTRA_CANDIDATES = ["ring_chunked_fast", "ring_chunked_plain", "ring_chunked_queued",
-                    "ring_chunked_mesh_steps", "ring_chunked_mesh_queued"]
+EXTRA_CANDIDATES = ["ring_chunked_fast", "ring_chunked_system", "ring_chunked_mesh_system",
+                    "ring_chunked_mesh_steps"]
 DEFAULT_ALTS = ["halving_doubling"]
-EXTRA_ALTS = ["halving_doubling_host", "halving_doubling_queued"]
+EXTRA_ALTS = ["halving_doubling_host", "halving_doubling_system"]
 # host-issued steps' peer-copy transports: (engine, DMA split, copy-kernel workgroups)
 TRANSPORTS_DEFAULT = [("dma", 1, 0), ("kernel", 1, 128)]
 TRANSPORTS_ALL = [("dma", 1, 0), ("dma", 2, 0), ("dma", 4, 0), ("kernel", 1, 32),
@@ -818,7 +838,14 @@ def bench_multi(args):
     ctx.connectFullMesh(store)
     log("connected (world %d, device %d)" % (world, local))
     peer_info = [ctx.peer_info(k) for k in range(world) if k != rank]
-    device_engines = probe_device_engines(torch, dist, gloo_amd, ctx, dev, args.dtype)
+
+    def connect(tag):  # a context of its own for each probe attempt
+        c = gloo_amd.rendezvous.Context(rank, world, local)
+        c.connectFullMesh(gloo_amd.rendezvous.PrefixStore(
+            "gloo_amd_probe_" + tag,
+            gloo_amd.rendezvous.TorchStore(dist.distributed_c10d._get_default_store())))
+        return c
+    device_engines = probe_device_engines(torch, dist, gloo_amd, connect, dev, args.dtype)
 
     # A failure on any rank (a timeout, a HIP error) is agreed on by all, so
     # every rank takes the same branch; the JSON line names it.
@@ -858,7 +885,7 @@ def bench_multi(args):
         log("%s: creating" % algo)
         probe = make_alg(gloo_amd, ctx, buf, algo)
         # no peer-copy transport to tune for the kernels that store themselves
-        device_engine = probe.engine() not in ("steps", "queued")
+        device_engine = probe.engine() != "steps"
         probe.close()
         if args.copy_split == "auto" and not device_engine:
             for tr in transports:
@@ -885,7 +912,7 @@ def bench_multi(args):
         return {"t": t, "sent": sent, "p50": p50,
                 "transport": ("device-driven kernel stores (%s)" % ENGINES[algo]
                               if device_engine else tname(best) +
-                              (" (queued)" if ENGINES[algo] == "queued" else "")), "tr": best,
+                              ""), "tr": best,
                 "calib_ms": {tname(k): round(v * 1e3, 3) for k, v in calib.items()},
                 "result": result}
 
@@ -953,14 +980,14 @@ def bench_multi(args):
                        "bytes_sent_per_step": sent_a, "engine": eng,
                        "fast_streams": FAST.get(other), "sync": SYNC.get(other),
                        "transport": ("device-driven kernel stores (%s)" % eng
-                                     if eng not in ("steps", "queued")
+                                     if eng != "steps"
                                      else tname(runs[chosen]["tr"])),
                        "busiest_link_GBps": round(lm / ta / 1e9, 2)}
     staged = None
     if args.staged:
         # host buffers: the fastest host-issued schedule (its H2D / D2H
         # overlap the steps); the device engines stage the whole buffer first
-        host_cands = [a for a in candidates if ENGINES.get(a) in ("steps", "queued")] or [chosen]
+        host_cands = [a for a in candidates if ENGINES.get(a) == "steps"] or [chosen]
         staged_algo = min(host_cands, key=lambda a: runs[a]["t"])
         staged, err = attempt("host-staged", lambda: host_endpoint_rate(
             torch, dist, gloo_amd, ctx, src, dev_result, staged_algo, reps=min(steps, 5)))

@@ -48,10 +48,9 @@ def set_copy_engine(engine, blocks=0):
 def set_mesh_engine(engine):
     """Engine of mesh-schedule algorithms created afterwards when the ranks
     are on distinct devices or processes: "device" (the two-shot kernel, one
-    device-driven launch per rank; default), "steps" (host-issued copies
-    and fold kernels) or "queued" (the same steps enqueued at once, their
-    waits on peers stream-ordered on device flags).  Same results either way."""
-    code = {"steps": 0, "device": 2, "queued": 4}[engine]
+    device-driven launch per rank; default) or "steps" (host-issued copies
+    and fold kernels).  Same results either way."""
+    code = {"steps": 0, "device": 2}[engine]
     errors.check(_lib.lib.glx_set_mesh_engine(code), "set_mesh_engine")
 
 
@@ -61,10 +60,9 @@ def set_steps_engine(engine):
     processes: "auto" (default: the plan kernel; at every size with one rank
     per GPU, up to 32 MiB per rank when ranks share a GPU, host-issued steps
     above), "device" (the plan kernel, one device-driven
-    launch per rank), "host" (host-issued steps) or "queued" (host-issued
-    steps enqueued at once, their waits on peers stream-ordered on device
-    flags: no host round trip per hop).  Same results either way."""
-    code = {"host": 0, "device": 3, "auto": -1, "queued": 4}[engine]
+    launch per rank) or "host" (host-issued steps).  Same results either
+    way."""
+    code = {"host": 0, "device": 3, "auto": -1}[engine]
     errors.check(_lib.lib.glx_set_steps_engine(code), "set_steps_engine")
 
 

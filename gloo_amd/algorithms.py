@@ -199,10 +199,9 @@ class Algorithm:
         schedule as one device-driven kernel per rank), "twoshot" (the mesh
         schedule as one device-driven kernel per rank), "devsteps" (any
         other schedule's step program walked by one device-driven kernel per
-        rank) or "queued" (the host-issued steps enqueued at once, waits on
-        peers stream-ordered on device flags)."""
-        return {0: "steps", 1: "oneshot", 2: "twoshot", 3: "devsteps",
-                4: "queued"}[lib.glx_algorithm_engine(self._h)]
+        rank)."""
+        return {0: "steps", 1: "oneshot", 2: "twoshot",
+                3: "devsteps"}[lib.glx_algorithm_engine(self._h)]
 
     def fast_streams(self):
         """True when the plan kernel runs nontemporal loads and write-through

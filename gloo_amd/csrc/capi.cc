@@ -197,9 +197,8 @@ int glx_set_copy_engine(int engine, int blocks) {
 }
 
 int glx_set_mesh_engine(int engine) {
-  if (engine != GLX_ENGINE_STEPS && engine != GLX_ENGINE_TWOSHOT && engine != GLX_ENGINE_QUEUED) {
-    return fail(GLX_ERR_INVALID,
-                "mesh engine must be GLX_ENGINE_STEPS, GLX_ENGINE_TWOSHOT or GLX_ENGINE_QUEUED");
+  if (engine != GLX_ENGINE_STEPS && engine != GLX_ENGINE_TWOSHOT) {
+    return fail(GLX_ERR_INVALID, "mesh engine must be GLX_ENGINE_STEPS or GLX_ENGINE_TWOSHOT");
   }
   gloo::HipPlanExecutor::setMeshEngine(engine);
   return GLX_OK;
@@ -214,11 +213,9 @@ int glx_set_engine_streams(int fast) {
 }
 
 int glx_set_steps_engine(int engine) {
-  if (engine != GLX_ENGINE_STEPS && engine != GLX_ENGINE_DEVSTEPS &&
-      engine != GLX_ENGINE_QUEUED && engine != -1) {
+  if (engine != GLX_ENGINE_STEPS && engine != GLX_ENGINE_DEVSTEPS && engine != -1) {
     return fail(GLX_ERR_INVALID,
-                "steps engine must be GLX_ENGINE_STEPS, GLX_ENGINE_DEVSTEPS, GLX_ENGINE_QUEUED "
-                "or -1 (by size)");
+                "steps engine must be GLX_ENGINE_STEPS, GLX_ENGINE_DEVSTEPS or -1 (by size)");
   }
   gloo::HipPlanExecutor::setStepsEngine(engine);
   return GLX_OK;

@@ -1,7 +1,6 @@
 // executor.cc -- HipPlanExecutor: construction, rendezvous of scratch between
 // ranks, the host-issued steps engine and run()/runFn().  The host-memory
-// endpoints, device-driven engines and queued engine live in
-// executor_{host,device,queued}.cc.  See executor.h.
+// endpoints and device-driven engines live in executor_{host,device}.cc.  See executor.h.
 #include "executor.h"
 
 #include <immintrin.h>
@@ -235,8 +234,8 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
     // every run, so no stale line of an earlier message may be cached.  (The
     // plan kernel reads its `slots_` landing slots inside the launch right
     // after an in-kernel flag wait, where nothing else could drop such a
-    // line.)  GLOO_AMD_STEPS_SCRATCH=cached gives the host-issued and queued
-    // engines hipMalloc'd regions instead (diagnostics).
+    // line.)  GLOO_AMD_STEPS_SCRATCH=cached gives the host-issued engine
+    // hipMalloc'd regions instead (diagnostics).
     static const bool stepsCached = [] {
       const char* e = std::getenv("GLOO_AMD_STEPS_SCRATCH");
       return e != nullptr && std::strcmp(e, "cached") == 0;
@@ -249,7 +248,7 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
   auto& ctl = ctx->localControl();
   stepChan_.assign(plan_.steps.size(), -1);
   const bool hostSteps = engine_ == kEngineSteps;
-  const bool copyStreams = hostSteps || engine_ == kEngineQueued;
+  const bool copyStreams = hostSteps;
   for (size_t i = 0; i < plan_.steps.size() &&
                      (copyStreams || engine_ == kEngineDevSteps);
        i++) {
@@ -260,9 +259,8 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
         OutChan oc;
         oc.peer = (int)s.peer;
         oc.tag = (int)s.channel;
-        // plan kernel: no control-block words or copy streams; queued: copy
-        // streams, no words (flag rows are assigned in setupDevSteps /
-        // setupQueued)
+        // plan kernel: no control-block words or copy streams (its flag
+        // rows are assigned in setupDevSteps)
         oc.creditWord = hostSteps ? ctl.allocWord() : 0;
         oc.credit = hostSteps ? ctl.word(oc.creditWord) : nullptr;
         // one copy stream per destination peer: copies to different peers
@@ -297,7 +295,7 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
       stepChan_[i] = idx;
     }
   }
-  if (engine_ == kEngineDevSteps || engine_ == kEngineQueued) setupDevice();
+  if (engine_ == kEngineDevSteps) setupDevice();
   events_.resize(plan_.steps.size() * (size_t)split_, nullptr);
   for (auto& e : events_) GLX_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   GLX_HIP_CHECK(hipEventCreateWithFlags(&computeMark_, hipEventDisableTiming));
@@ -344,21 +342,6 @@ void HipPlanExecutor::drainCredits() noexcept {
           for (size_t w = 0; w < G && done; w++) done = row[w * glx::kFlagStride] >= want[c];
           if (done || std::chrono::steady_clock::now() >= deadline) break;
           context_->checkPeersAlive();  // throws if a peer exited: stop waiting
-          pause();
-        }
-      }
-    }
-    if (engine_ == kEngineQueued && !ddBlocks_.empty()) {
-      for (const auto& oc : out_) {
-        for (;;) {
-          uint64_t v = 0;
-          if (hipMemcpy(&v, flagRow(oc.creditWord), sizeof(v), hipMemcpyDeviceToHost) !=
-              hipSuccess) {
-            (void)hipGetLastError();
-            break;
-          }
-          if (v >= oc.sent || std::chrono::steady_clock::now() >= deadline) break;
-          context_->checkPeersAlive();
           pause();
         }
       }
@@ -606,7 +589,7 @@ void HipPlanExecutor::resolvePeers() {
       }
     }
     if (engine_ != kEngineSteps) ddPeer_[r] = blocks;
-    if (engine_ == kEngineDevSteps || engine_ == kEngineQueued) {  // the peer's flag rows
+    if (engine_ == kEngineDevSteps) {  // the peer's flag rows
       GLX_ENFORCE(!blocks.empty(), "rank ", r, " published no flag rows");
       uint64_t* rows = reinterpret_cast<uint64_t*>(blocks[0]);
       const size_t G = (size_t)pk_.G;
@@ -622,7 +605,7 @@ void HipPlanExecutor::resolvePeers() {
       }
     }
   }
-  const bool dev = engine_ == kEngineDevSteps || engine_ == kEngineQueued;
+  const bool dev = engine_ == kEngineDevSteps;
   for (auto& oc : out_) {
     GLX_ENFORCE(dev ? oc.devDelivery != nullptr : oc.delivery != nullptr, "rank ", oc.peer,
                 " has no receive channel ", oc.tag, " from rank ", contextRank_,
@@ -936,10 +919,6 @@ void HipPlanExecutor::recordDone(hipEvent_t ev) {
 }
 
 void HipPlanExecutor::exchange(char* ptr0) {
-  if (engine_ == kEngineQueued) {
-    exchangeQueued(ptr0);
-    return;
-  }
   if (engine_ != kEngineSteps) {
     runDevice(ptr0);
     return;

@@ -128,9 +128,7 @@ class HipPlanExecutor : public Algorithm {
     int peerDevice = -1;
     int stream = 0;
     int peerRow = -1;                 // plan kernel: the receiver's delivery row
-    uint64_t* devDelivery = nullptr;  // plan kernel / queued: that row (peer memory)
-    uint64_t* devCounter = nullptr;   // queued: local count of copy-kernel workgroups done
-    uint64_t counterTarget = 0;       // queued: its value once the last copy launch is done
+    uint64_t* devDelivery = nullptr;  // plan kernel: that row (peer memory)
   };
   struct CopyStream {
     hipStream_t s = nullptr;
@@ -145,7 +143,7 @@ class HipPlanExecutor : public Algorithm {
     std::atomic<uint64_t>* credit = nullptr;  // in peer's block
     uint64_t received = 0, consumed = 0;
     int peerRow = -1;               // plan kernel: the sender's credit row
-    uint64_t* devCredit = nullptr;  // plan kernel / queued: that row (peer memory)
+    uint64_t* devCredit = nullptr;  // plan kernel: that row (peer memory)
   };
   static constexpr int kMaxSplit = 8;
   struct Pending {  // fire `value` into `word` once all `ev` (maybe none) complete
@@ -350,17 +348,10 @@ class HipPlanExecutor : public Algorithm {
   // the peers' processes: if one exits, stop every kernel wait at once
   // (status word) and throw IoException instead of running into the timeout.
   void waitDevice(hipStream_t s);
-  // Queued steps engine: the host-issued engine's step loop with every wait
-  // on a peer and every counter write as a stream-ordered launch on device
-  // flag rows (one flag each: deliveries, credits, then one local copy
-  // counter per out-channel), so the loop never blocks.
-  void setupQueued();
-  void exchangeQueued(char* ptr0);
-  uint64_t* flagRow(uint32_t row) const;
 
  public:
   static constexpr int kEngineSteps = 0, kEngineOneShot = 1, kEngineTwoShot = 2,
-                       kEngineDevSteps = 3, kEngineQueued = 4;
+                       kEngineDevSteps = 3;
   // Whether device-driven engines can run on this context: GLOO_AMD_ONESHOT
   // (0 = never, 1 = always), by default when no two ranks are threads sharing
   // one device (their kernels might not be co-resident).  P <= 8.
@@ -369,15 +360,15 @@ class HipPlanExecutor : public Algorithm {
   // (caller guarantees co-residency), -1 = automatic (the default).
   static void setDeviceEngines(int mode);
   // Engine of the mesh schedule when available: kEngineTwoShot (default,
-  // env GLOO_AMD_MESH_ENGINE=steps|queued overrides), kEngineSteps or
-  // kEngineQueued.  Read at construction.
+  // env GLOO_AMD_MESH_ENGINE=steps overrides) or kEngineSteps.  Read at
+  // construction.
   static void setMeshEngine(int engine);
   static int meshEngine();
   // Engine of the ring, halving-doubling, bcube and function-style ring
   // schedules when available: -1 = by size (default: the plan kernel up to
   // 32 MiB per rank, env GLOO_AMD_DEVSTEPS_MAX_BYTES; host-issued steps
-  // above), kEngineDevSteps, kEngineSteps or kEngineQueued (env
-  // GLOO_AMD_STEPS_ENGINE=device|host|queued).
+  // above), kEngineDevSteps or kEngineSteps (env
+  // GLOO_AMD_STEPS_ENGINE=device|host).
   static void setStepsEngine(int engine);
   static int stepsEngine();
   // Streams of the device-driven kernels for algorithms created afterwards:
@@ -392,7 +383,7 @@ class HipPlanExecutor : public Algorithm {
   // 1 when the device engine runs the narrow release / acquire, 0 system
   // scope, -1 host-issued steps
   int syncMode() const {
-    return engine_ == kEngineSteps || engine_ == kEngineQueued
+    return engine_ == kEngineSteps
                ? -1
                : (engine_ == kEngineDevSteps ? pk_.narrow
                                               : (engine_ == kEngineOneShot ? os_.narrow : ts_.narrow));

@@ -33,7 +33,6 @@ namespace {
 int initialMeshEngine() {
   const char* e = std::getenv("GLOO_AMD_MESH_ENGINE");
   if (e != nullptr && std::strcmp(e, "steps") == 0) return HipPlanExecutor::kEngineSteps;
-  if (e != nullptr && std::strcmp(e, "queued") == 0) return HipPlanExecutor::kEngineQueued;
   return HipPlanExecutor::kEngineTwoShot;
 }
 
@@ -46,7 +45,6 @@ int initialStepsEngine() {
   const char* e = std::getenv("GLOO_AMD_STEPS_ENGINE");
   if (e != nullptr && std::strcmp(e, "host") == 0) return HipPlanExecutor::kEngineSteps;
   if (e != nullptr && std::strcmp(e, "device") == 0) return HipPlanExecutor::kEngineDevSteps;
-  if (e != nullptr && std::strcmp(e, "queued") == 0) return HipPlanExecutor::kEngineQueued;
   return -1;
 }
 
@@ -60,17 +58,13 @@ std::atomic<int> g_steps_engine{initialStepsEngine()};
 }  // namespace
 
 void HipPlanExecutor::setMeshEngine(int engine) {
-  g_mesh_engine.store(engine == kEngineSteps || engine == kEngineQueued ? engine
-                                                                       : kEngineTwoShot);
+  g_mesh_engine.store(engine == kEngineSteps ? engine : kEngineTwoShot);
 }
 
 int HipPlanExecutor::meshEngine() { return g_mesh_engine.load(); }
 
 void HipPlanExecutor::setStepsEngine(int engine) {
-  g_steps_engine.store(engine < 0 ? -1
-                                  : (engine == kEngineSteps || engine == kEngineQueued
-                                         ? engine
-                                         : kEngineDevSteps));
+  g_steps_engine.store(engine < 0 ? -1 : (engine == kEngineSteps ? engine : kEngineDevSteps));
 }
 
 int HipPlanExecutor::stepsEngine() { return g_steps_engine.load(); }
@@ -183,8 +177,6 @@ void HipPlanExecutor::setupDevice() {
     setupOneShot();
   } else if (engine_ == kEngineTwoShot) {
     setupTwoShot();
-  } else if (engine_ == kEngineQueued) {
-    setupQueued();
   } else {
     setupDevSteps();
   }

@@ -164,24 +164,6 @@ struct PlanKernelParams {
 };
 hipError_t launch_plan_kernel(int op, int dtype, const PlanKernelParams& p, hipStream_t s);
 
-// Queued steps engine (xgmi_kernels.hip): the host-issued engine's waits and
-// counter writes as stream-ordered launches on device flag words (one per
-// 128-B line, the plan kernel's protocol with one workgroup).
-//   flag_wait: one wave waits for *word >= target (bounded; reports `code`
-//              into status as the device engines do, and returns at once
-//              when an earlier wait has reported);
-//   flag_put:  *word = value once the stream's earlier work completed;
-//   copy_signal: copy `bytes` with `blocks` workgroups, then the launch's
-//              last workgroup (local *counter, cumulative, reaching target)
-//              writes *flag = value.
-// store: write peers' flags with system-scope stores (Context::flagStores).
-hipError_t launch_flag_wait(const uint64_t* word, uint64_t target, uint64_t timeoutTicks,
-                            int* status, int* claim, int code, hipStream_t s);
-hipError_t launch_flag_put(uint64_t* word, uint64_t value, int store, hipStream_t s);
-hipError_t launch_copy_signal(void* dst, const void* src, size_t bytes, int blocks,
-                              uint64_t* counter, uint64_t target, uint64_t* flag,
-                              uint64_t value, int store, hipStream_t s);
-
 // Workgroups of a device-engine kernel (kernel 0 = one-shot, 1 = two-shot,
 // 2 = plan kernel, 3 = plan kernel for programs without FOLD steps) for
 // (op, dtype) that fit on the current device at once

@@ -740,85 +740,6 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
   }
 }
 
-// ---- queued steps engine ------------------------------------------------------
-// The host engine's waits and counter bumps as stream-ordered launches: the
-// whole step program is enqueued up front and no step waits for the host.
-
-// Waits until *word >= target, then lets the stream go on.  Gives up (and
-// reports) after timeoutTicks; once any wait of the algorithm has reported,
-// later ones return at once, so a broken run ends after one timeout.
-__global__ __launch_bounds__(64) void flag_wait_kernel(const uint64_t* word, uint64_t target,
-                                                       uint64_t timeoutTicks, int* status,
-                                                       int* claim, int code) {
-  if (threadIdx.x != 0) return;
-  const volatile int* st = status;
-  if (*st != 0) return;
-  const uint64_t start = __builtin_amdgcn_s_memrealtime();
-  uint64_t v;
-  for (uint32_t spin = 1; (v = get_flag(word)) < target; spin++) {
-    if (__builtin_amdgcn_s_memrealtime() - start > timeoutTicks) {
-      report_timeout(status, claim, code, v, target);
-      return;
-    }
-    if ((spin & 1023) == 0 && *st != 0) return;
-    __builtin_amdgcn_s_sleep(2);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-}
-
-// *word = value, after everything earlier on the stream (a DMA copy into the
-// peer's landing region, or the reduce that read ours) has completed.
-__global__ __launch_bounds__(64) void flag_put_kernel(uint64_t* word, uint64_t value, int store) {
-  if (threadIdx.x != 0) return;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  put_flag(word, value, store != 0);
-}
-
-// A SEND by the compute units: copy bytes into the peer's landing region and
-// have the last workgroup to finish write the delivery flag.  Every
-// workgroup's stores are complete system-wide before it counts itself in
-// (counter: a local word, cumulative over launches; the launch's last
-// workgroup sees target), so the flag follows every byte.
-__global__ __launch_bounds__(kBlock) void copy_signal_kernel(char* __restrict__ dst,
-                                                             const char* __restrict__ src,
-                                                             size_t head, size_t nvec,
-                                                             size_t tail, uint64_t* counter,
-                                                             uint64_t target, uint64_t* flag,
-                                                             uint64_t value, int store) {
-  const size_t gtid = (size_t)blockIdx.x * kBlock + threadIdx.x;
-  const size_t threads = (size_t)gridDim.x * kBlock;
-  // unaligned bytes (all of them when the two phases differ): grid-stride
-  for (size_t i = gtid; i < head; i += threads) dst[i] = src[i];
-  const size_t tailAt = head + nvec * 16;
-  for (size_t i = gtid; i < tail; i += threads) dst[tailAt + i] = src[tailAt + i];
-  const v4u* vs = reinterpret_cast<const v4u*>(src + head);
-  v4u* vd = reinterpret_cast<v4u*>(dst + head);
-  constexpr int U = 4;
-  const size_t stride = (size_t)gridDim.x * kBlock * U;
-  for (size_t base = (size_t)blockIdx.x * kBlock * U + threadIdx.x; base < nvec;
-       base += stride) {
-    v4u x[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const size_t i = base + (size_t)u * kBlock;
-      if (i < nvec) x[u] = __builtin_nontemporal_load(vs + i);
-    }
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const size_t i = base + (size_t)u * kBlock;
-      if (i < nvec) vd[i] = x[u];
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint64_t before = __hip_atomic_fetch_add(counter, uint64_t(1), __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_SYSTEM);
-    if (before + 1 == target) put_flag(flag, value, store != 0);
-  }
-}
-
 // ---- launch -------------------------------------------------------------------
 
 template <typename T>
@@ -984,40 +905,6 @@ hipError_t launch_twoshot(int op, int dtype, const TwoShotParams& p, hipStream_t
     case GLX_BFLOAT16: return launch_ts_op<bf16_t>(op, p, s);
   }
   return hipErrorInvalidValue;
-}
-
-hipError_t launch_flag_wait(const uint64_t* word, uint64_t target, uint64_t timeoutTicks,
-                            int* status, int* claim, int code, hipStream_t s) {
-  if (word == nullptr || status == nullptr || claim == nullptr) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(flag_wait_kernel, dim3(1), dim3(64), 0, s, word, target, timeoutTicks,
-                     status, claim, code);
-  return hipGetLastError();
-}
-
-hipError_t launch_flag_put(uint64_t* word, uint64_t value, int store, hipStream_t s) {
-  if (word == nullptr) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(flag_put_kernel, dim3(1), dim3(64), 0, s, word, value, store);
-  return hipGetLastError();
-}
-
-hipError_t launch_copy_signal(void* dst, const void* src, size_t bytes, int blocks,
-                              uint64_t* counter, uint64_t target, uint64_t* flag,
-                              uint64_t value, int store, hipStream_t s) {
-  if (bytes == 0 || blocks < 1 || counter == nullptr || flag == nullptr) {
-    return hipErrorInvalidValue;
-  }
-  const uintptr_t pd = (uintptr_t)dst, ps = (uintptr_t)src;
-  size_t head = bytes, nvec = 0, tail = 0;  // phases differ: bytes only
-  if (pd % 16 == ps % 16) {
-    head = (16 - pd % 16) % 16;
-    if (head > bytes) head = bytes;
-    nvec = (bytes - head) / 16;
-    tail = bytes - head - nvec * 16;
-  }
-  hipLaunchKernelGGL(copy_signal_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s,
-                     static_cast<char*>(dst), static_cast<const char*>(src), head, nvec, tail,
-                     counter, target, flag, value, store);
-  return hipGetLastError();
 }
 
 }  // namespace glx

@@ -262,7 +262,7 @@ class DeviceAllreduce : public Algorithm {
   ~DeviceAllreduce() override { glx_algorithm_destroy(a_); }
   void run() override { check(glx_algorithm_run(a_), "run"); }
   int64_t bytesSentPerRun() const { return glx_algorithm_bytes_sent(a_); }
-  // GLX_ENGINE_STEPS / _ONESHOT / _TWOSHOT / _DEVSTEPS / _QUEUED (glx.h)
+  // GLX_ENGINE_STEPS / _ONESHOT / _TWOSHOT / _DEVSTEPS (glx.h)
   int engine() const { return glx_algorithm_engine(a_); }
   // Host buffer fed from a transport: runFed() runs while feed() (any
   // thread) reports which elements have arrived; doneRanges() lists the
@@ -304,9 +304,9 @@ enum class Schedule { RING, MESH, REPLICATED, AUTO };
 // Engine knobs for algorithms created afterwards (process-wide; every rank
 // must set them alike).  mode: -1 automatic, 0 never, 1 always.
 inline void setDeviceEngines(int mode) { check(glx_set_device_engines(mode), "setDeviceEngines"); }
-// GLX_ENGINE_TWOSHOT (default), GLX_ENGINE_STEPS or GLX_ENGINE_QUEUED for the MESH schedule.
+// GLX_ENGINE_TWOSHOT (default) or GLX_ENGINE_STEPS for the MESH schedule.
 inline void setMeshEngine(int engine) { check(glx_set_mesh_engine(engine), "setMeshEngine"); }
-// GLX_ENGINE_DEVSTEPS (default), GLX_ENGINE_STEPS or GLX_ENGINE_QUEUED for RING,
+// GLX_ENGINE_DEVSTEPS (default) or GLX_ENGINE_STEPS for RING,
 // halving-doubling, bcube and the function-style ring.
 inline void setStepsEngine(int engine) { check(glx_set_steps_engine(engine), "setStepsEngine"); }
 

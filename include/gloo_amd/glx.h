@@ -144,9 +144,8 @@ int glx_set_copy_engine(int engine, int blocks);
 /* Engine of the mesh schedule (ring_chunked's result over all links) for
  * algorithms created afterwards, when device-driven engines are available
  * (ranks on distinct devices or processes, P <= 8): GLX_ENGINE_TWOSHOT (one
- * device-driven kernel per rank, default), GLX_ENGINE_STEPS (host-issued
- * copies and fold kernels) or GLX_ENGINE_QUEUED (the same, stream-ordered).
- * Env GLOO_AMD_MESH_ENGINE=steps|queued at load time. */
+ * device-driven kernel per rank, default) or GLX_ENGINE_STEPS (host-issued
+ * copies and fold kernels).  Env GLOO_AMD_MESH_ENGINE=steps at load time. */
 int glx_set_mesh_engine(int engine);
 /* Device-driven engines for algorithms created afterwards: 0 = never (every
  * schedule runs as host-issued steps), 1 = always (the caller guarantees the
@@ -158,9 +157,8 @@ int glx_set_device_engines(int mode);
  * are available: -1 = automatic (default: the plan kernel -- at every size
  * with one rank per GPU, up to 32 MiB per rank when ranks share a GPU or
  * env GLOO_AMD_DEVSTEPS_MAX_BYTES is set, host-issued steps above),
- * GLX_ENGINE_DEVSTEPS (the plan kernel), GLX_ENGINE_STEPS (host-issued
- * steps) or GLX_ENGINE_QUEUED (host-issued steps, stream-ordered waits).
- * Env GLOO_AMD_STEPS_ENGINE=device|host|queued. */
+ * GLX_ENGINE_DEVSTEPS (the plan kernel) or GLX_ENGINE_STEPS (host-issued
+ * steps).  Env GLOO_AMD_STEPS_ENGINE=device|host. */
 int glx_set_steps_engine(int engine);
 /* Cache policy of the plan kernel's own loads and stores for algorithms
  * created afterwards: -1 automatic (default: plain, except nontemporal loads
@@ -371,13 +369,6 @@ int64_t glx_algorithm_bytes_sent(glx_algorithm* alg);
  * function-style ring) run as ONE device-driven kernel per rank that walks
  * the schedule's step program (the plan kernel). */
 #define GLX_ENGINE_DEVSTEPS 3
-/* GLX_ENGINE_QUEUED = the host-issued steps engine with the host out of the
- * loop: the whole step program is enqueued at once, and the waits on peers
- * (delivery, credit) and the counter writes that end them are stream-ordered
- * launches on device flag words, so no hop waits for a host round trip.
- * Copies are hipMemcpyPeerAsync (or the copy kernel, glx_set_copy_engine) on
- * side streams, reductions the glx reduce kernel on the compute stream. */
-#define GLX_ENGINE_QUEUED 4
 int glx_algorithm_engine(glx_algorithm* alg);
 /* 1 when the algorithm's plan kernel runs nontemporal loads and write-through
  * stores (glx_set_engine_streams), else 0. */

@@ -12,8 +12,6 @@ algo: ring_chunked | halving_doubling | ring_chunked_mesh (class algorithms)
       through the plan kernel: dtypes x ops x sizes, device and host buffers,
       repeated runs; prints per-op latencies of the plan kernel vs the
       host-issued steps)
-      queued | queued_kernel (the same through the queued steps engine, with
-      DMA or copy-kernel sends, plus the mesh schedule on it)
       devtimeout (rank 0 runs both device engines while the other ranks never
       call run(): its kernels must give up after the timeout and run() must
       raise IoException)
@@ -51,10 +49,6 @@ def main():
         return run_killpeer(store_dir, rank, size, *algo.split(":")[1:])
     if algo == "devsteps":
         return run_devsteps(store_dir, rank, size)
-    if algo in ("queued", "queued_kernel"):
-        if algo == "queued_kernel":
-            gloo_amd.set_copy_engine("kernel", 128)
-        return run_devsteps(store_dir, rank, size, eng="queued")
     if algo == "churn":
         return run_churn(store_dir, rank, size)
     if algo.startswith("scale:"):
@@ -336,7 +330,7 @@ def run_devsteps(store_dir, rank, size, eng="device"):
                                              schedule="mesh" if kind == MESH else "ring")
 
     cases = []
-    kinds = (O.RING_CHUNKED, O.HALVING_DOUBLING) + ((MESH,) if eng == "queued" else ())
+    kinds = (O.RING_CHUNKED, O.HALVING_DOUBLING)
     for kind in kinds:
         for n in (1, 3, 255, 256, 1000, 4099, 65539, 1 << 20, (1 << 22) + 5):
             cases.append((kind, n, O.FLOAT32, O.SUM))
@@ -344,8 +338,6 @@ def run_devsteps(store_dir, rank, size, eng="device"):
             for op in (O.SUM, O.PRODUCT, O.MAX, O.MIN):
                 cases.append((kind, 4099, dt, op))
     gloo_amd.set_steps_engine(eng)
-    if eng == "queued":
-        gloo_amd.set_mesh_engine("queued")
     engines = set()
     for seed, (kind, n, dt, op) in enumerate(cases):
         ins = case_inputs(size, n, dt, 1, 0, seed=200 + seed)

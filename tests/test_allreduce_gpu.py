@@ -377,14 +377,12 @@ def test_multiprocess_ipc(algo):
 
 
 @pytest.mark.parametrize("P,mode", [(P, m) for P in (2, 3, 4)
-                                    for m in ("oneshot", "twoshot", "devsteps", "queued")] +
-                         [(3, "queued_kernel"), (8, "devsteps"), (8, "queued")])
+                                    for m in ("oneshot", "twoshot", "devsteps")] +
+                         [(8, "devsteps")])
 def test_device_engine_multiprocess(P, mode):
     """The replicated (one-shot) and mesh (two-shot) schedules, and the ring,
     halving-doubling and bcube step programs (plan kernel), as one
-    device-driven kernel per rank (xgmi_kernels.hip), one process per rank;
-    and the same programs plus the mesh on the queued steps engine (DMA or
-    copy-kernel sends, stream-ordered flag waits):
+    device-driven kernel per rank (xgmi_kernels.hip), one process per rank:
     peers' kernels push into each other's IPC-mapped uncached regions and
     wait on flags.  Bit-exact with the reference ring's chains for every
     dtype/op, device and host buffers, class and function style, repeated

@@ -75,10 +75,10 @@ def test_result_check_world2(dtype, corrupt):
 
 def test_plan_names():
     assert bench.plan_name("ring_chunked_host") == "ring_chunked"
-    assert bench.plan_name("ring_chunked_queued") == "ring_chunked"
+    assert bench.plan_name("ring_chunked_plain_narrow") == "ring_chunked"
     assert bench.plan_name("ring_chunked_mesh_steps") == "ring_chunked_mesh"
-    assert bench.plan_name("ring_chunked_mesh_queued") == "ring_chunked_mesh"
-    assert bench.plan_name("halving_doubling_queued") == "halving_doubling"
+    assert bench.plan_name("ring_chunked_mesh_system") == "ring_chunked_mesh"
+    assert bench.plan_name("halving_doubling_host") == "halving_doubling"
 
 
 def test_roofline_byte_counts_ring_p8():
@@ -121,10 +121,11 @@ def test_candidate_lists_default_is_small():
         algo, schedule, candidates, no_alt = "ring_chunked", "auto", "default", False
     c, alts = bench.candidate_lists(A)
     assert c[0] == "ring_chunked" and len(c) + len(alts) <= 4
-    assert not any(x.endswith(("_fast", "_queued")) for x in c + alts)
+    assert not any(x.endswith(("_fast", "_system")) for x in c + alts)
     A.candidates = "all"
     c, alts = bench.candidate_lists(A)
-    assert "ring_chunked_fast" in c and "halving_doubling_queued" in alts
+    assert "ring_chunked_fast" in c and "ring_chunked_system" in c
+    assert "halving_doubling_host" in alts
 
 
 def test_metric_name_follows_dtype():
