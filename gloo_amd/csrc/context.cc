@@ -1,5 +1,6 @@
 // context.cc -- see context.h.
 #include "context.h"
+#include "executor_internal.h"
 
 #include <algorithm>
 
@@ -203,9 +204,11 @@ void freeBlock(int device, char* p, size_t bytes, unsigned flags) {
     return !(e != nullptr && e[0] == '0');
   }();
   if (flags == 0 || !cache) {
+    GLX_TRACE_MEM("hipFree block %p (%zu, flags %u)", (void*)p, bytes, flags);
     hipFree(p);
     return;
   }
+  GLX_TRACE_MEM("cache block %p (%zu, flags %u)", (void*)p, bytes, flags);
   KindCache& c = kindCache();
   std::lock_guard<std::mutex> g(c.mu);
   c.free.push_back(KindCache::Entry{device, flags, bytes, p});
@@ -225,6 +228,7 @@ char* allocBlock(int device, size_t* bytes, unsigned flags) {
   } else {
     GLX_HIP_CHECK(hipMalloc((void**)&d, *bytes));
   }
+  GLX_TRACE_MEM("alloc block %p (%zu, flags %u)", (void*)d, *bytes, flags);
   return d;
 }
 }  // namespace
@@ -299,7 +303,10 @@ SharedBlock Context::acquireShared(size_t bytes, unsigned flags) {
   nb.flags = flags;
   nb.ref.ptr = (uint64_t)(uintptr_t)nb.ptr;
   nb.ref.id = nextSharedId_++;
-  if (size > 1) {
+  // exported only when some peer is another process: thread-ranks of this
+  // process use the pointer itself, and an IPC export (a dmabuf the runtime
+  // keeps per allocation) is one more thing the block's memory carries
+  if (size > 1 && crossProcess_) {
     std::memset(&nb.ref.ipc, 0, sizeof(nb.ref.ipc));
     const hipError_t e = hipIpcGetMemHandle(&nb.ref.ipc, nb.ptr);
     if (e != hipSuccess) {
@@ -513,6 +520,8 @@ void Context::connectFullMesh(std::shared_ptr<rendezvous::Store> store) {
     if (r != rank) store_->get("glx/ep/" + std::to_string(r) + "/mapped", timeout_);
   }
   local_.unlink();
+  crossProcess_ = false;
+  for (const auto& p : peers_) crossProcess_ = crossProcess_ || !p.sameProcess;
   connected_ = true;
 }
 

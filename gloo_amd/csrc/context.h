@@ -188,6 +188,7 @@ class Context {
   int slot_ = 0;
   bool connected_ = false;
   bool flagStores_ = false;
+  bool crossProcess_ = true;  // some peer is another process (set at connect)
   std::chrono::milliseconds timeout_{30000};  // gloo/context.cc:18
   std::shared_ptr<rendezvous::Store> store_;
   ControlBlock local_;

@@ -378,11 +378,17 @@ void HipPlanExecutor::release() noexcept {
   for (auto& e : doneEvents_) {
     if (e != nullptr) hipEventDestroy(e);
   }
-  for (char* d : devBufs_) hipFree(d);
+  for (char* d : devBufs_) {
+    GLX_TRACE_MEM("r%d hipFree devBuf %p", contextRank_, (void*)d);
+    hipFree(d);
+  }
   givePinned(hostStage_, hostStageBytes_);
   hostStage_ = nullptr;
   for (char* d : fnStage_) hipFree(d);
-  for (void* p : registered_) hipHostUnregister(p);
+  for (void* p : registered_) {
+    const hipError_t ue = hipHostUnregister(p);
+    GLX_TRACE_MEM("r%d hipHostUnregister(%p) -> %d", contextRank_, p, (int)ue);
+  }
   for (auto& e : events_) {
     if (e != nullptr) hipEventDestroy(e);
   }

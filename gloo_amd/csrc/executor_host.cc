@@ -214,7 +214,9 @@ void HipPlanExecutor::setupHostMode() {
       // pin the caller's buffer for the algorithm's lifetime (the reference's
       // algorithms also bind their buffers at construction); if the runtime
       // refuses, pageable copies are still correct, only slower
-      if (hipHostRegister(p, bytes, hipHostRegisterPortable) == hipSuccess) {
+      const hipError_t re = hipHostRegister(p, bytes, hipHostRegisterPortable);
+      GLX_TRACE_MEM("r%d hipHostRegister(%p, %zu) -> %d", contextRank_, p, bytes, (int)re);
+      if (re == hipSuccess) {
         registered_.push_back(p);
       } else {
         (void)hipGetLastError();
@@ -222,6 +224,7 @@ void HipPlanExecutor::setupHostMode() {
     }
     char* d = nullptr;
     GLX_HIP_CHECK(hipMalloc((void**)&d, bytes));
+    GLX_TRACE_MEM("r%d hipMalloc devBuf %p (%zu)", contextRank_, (void*)d, bytes);
     devBufs_.push_back(d);
   }
   GLX_HIP_CHECK(hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking));

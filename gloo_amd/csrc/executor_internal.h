@@ -1,7 +1,7 @@
 // executor_internal.h -- helpers shared by the executor's translation units
 // (executor.cc: construction, rendezvous of scratch, the host-issued steps
 // engine; executor_host.cc: host-memory endpoints; executor_device.cc: the
-// device-driven engines; executor_queued.cc: the queued steps engine).
+// device-driven engines).
 #pragma once
 
 #include <immintrin.h>
@@ -34,6 +34,24 @@ inline bool traceOn() {
       std::fprintf(stderr, "[glx-trace] " __VA_ARGS__);  \
       std::fputc('\n', stderr);                          \
     }                                                    \
+  } while (0)
+
+// GLOO_AMD_TRACE_MEM=1: one stderr line per allocation, free, host
+// registration and unregistration the library makes (diagnostics).
+inline bool traceMemOn() {
+  static const bool on = [] {
+    const char* e = std::getenv("GLOO_AMD_TRACE_MEM");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+
+#define GLX_TRACE_MEM(...)                                   \
+  do {                                                       \
+    if (::gloo::exec::traceMemOn()) {                        \
+      std::fprintf(stderr, "[glx-mem] " __VA_ARGS__);        \
+      std::fputc('\n', stderr);                              \
+    }                                                        \
   } while (0)
 
 // Host memory (pageable or pinned) as opposed to device/managed memory.
