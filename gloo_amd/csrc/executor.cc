@@ -234,14 +234,8 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
     // every run, so no stale line of an earlier message may be cached.  (The
     // plan kernel reads its `slots_` landing slots inside the launch right
     // after an in-kernel flag wait, where nothing else could drop such a
-    // line.)  GLOO_AMD_STEPS_SCRATCH=cached gives the host-issued engine
-    // hipMalloc'd regions instead (diagnostics).
-    static const bool stepsCached = [] {
-      const char* e = std::getenv("GLOO_AMD_STEPS_SCRATCH");
-      return e != nullptr && std::strcmp(e, "cached") == 0;
-    }();
-    const bool uncached = engine_ == kEngineDevSteps || !stepsCached;
-    allocScratch(uncached, engine_ == kEngineDevSteps ? slots_ : 1);
+    // line.)
+    allocScratch(true, engine_ == kEngineDevSteps ? slots_ : 1);
   }
 
   // Channels named by the plan; allocate our counter words.

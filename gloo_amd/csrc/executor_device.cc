@@ -154,17 +154,11 @@ int HipPlanExecutor::engineFor(const Context& ctx, int algo, int64_t count, int 
   return kEngineSteps;
 }
 
-// Peers' stores land in our HBM behind our caches' back: uncached memory
-// (default), or fine-grained memory (GLOO_AMD_DD_MEM=finegrained: cached
-// non-coherently, the kernels' system-scope acquire drops stale lines).
+// Peers' stores land in our HBM behind our caches' back: uncached memory,
+// which no L2 holds -- the narrow flag sync relies on it (kernels.h).
 char* HipPlanExecutor::ddAlloc(size_t bytes) {
-  static const unsigned flags = [] {
-    const char* e = std::getenv("GLOO_AMD_DD_MEM");
-    return (e != nullptr && std::strcmp(e, "finegrained") == 0) ? hipDeviceMallocFinegrained
-                                                                 : hipDeviceMallocUncached;
-  }();
   SharedRef ref;
-  char* d = allocShared(bytes, flags, &ref);
+  char* d = allocShared(bytes, hipDeviceMallocUncached, &ref);
   ddRefs_.push_back(ref);
   GLX_TRACE("r%d ddAlloc %zu bytes at %p", contextRank_, bytes, (void*)d);
   ddBlocks_.push_back(d);
@@ -321,11 +315,6 @@ void HipPlanExecutor::setupDevSteps() {
   for (size_t k = 0; k < out_.size(); k++) out_[k].creditWord = (uint32_t)(in_.size() + k);
   const size_t rows = std::max<size_t>(1, in_.size() + out_.size());
   ddAlloc(rows * G * glx::kFlagBytes);
-  static const int pollLoad = [] {
-    const char* e = std::getenv("GLOO_AMD_FLAG_POLL");
-    return (e != nullptr && std::strcmp(e, "load") == 0) ? 1 : 0;
-  }();
-  pk_.pollLoad = pollLoad;
 
   pk_.trace = nullptr;
   if (devTrace()) {

@@ -152,7 +152,6 @@ struct PlanKernelParams {
   uint64_t timeoutTicks;
   int* status;
   int* claim;
-  int pollLoad;                // 1: poll flags with atomic loads (GLOO_AMD_FLAG_POLL=load)
   int narrow;                  // 1: narrow release / acquire around flags (below)
   int flagStore;               // 1: write peers' flags with stores (Context::flagStores)
   int fast;                    // 1: nontemporal loads, write-through stores (plan kernel only;

@@ -300,19 +300,10 @@ int policy_for(size_t stream_bytes) {
   return stream_bytes <= g_wt_max_bytes ? kPolNtWt : kPolNt;
 }
 
-// Write-through stores for the fold (reduce_n) and copy kernels: -1 by
-// policy_for, 0 never (fold: nontemporal, copy: plain stores), 1 always.
-// GLOO_AMD_FOLD_WT / GLOO_AMD_COPY_WT (measurement knobs).
-int env_wt(const char* name, int dflt) {
-  const char* e = std::getenv(name);
-  return e == nullptr ? dflt : std::atoi(e);
-}
-const int g_fold_wt = env_wt("GLOO_AMD_FOLD_WT", -1);
-const int g_copy_wt = env_wt("GLOO_AMD_COPY_WT", -1);
-
-bool use_wt(int knob, size_t stream_bytes) {
+// Write-through stores for the fold (reduce_n) and copy kernels: the
+// reduce kernel's policy (policy_for) for the stream's size.
+bool use_wt(size_t stream_bytes) {
   if (stream_bytes > kWtMaxStream) return false;
-  if (knob >= 0) return knob != 0;
   return policy_for(stream_bytes) == kPolNtWt;
 }
 
@@ -434,7 +425,7 @@ hipError_t launch_n_pass(void* dst, const void* const* srcs, int k, size_t n,
   size_t blocks = grid_for(nvec, 4);
   size_t edge_blocks = (std::max(head, tail) + kBlock - 1) / kBlock;
   if (blocks < edge_blocks) blocks = edge_blocks;
-  if (use_wt(g_fold_wt, nvec * 16)) {
+  if (use_wt(nvec * 16)) {
     hipLaunchKernelGGL((reduce_n_kernel<T, OP, 4, REV, true>), dim3((unsigned)blocks),
                        dim3(kBlock), 0, s, (S*)dst, sp, k, head, nvec, tail);
   } else {
@@ -561,7 +552,7 @@ hipError_t launch_copy_blocks(void* dst, const void* src, size_t bytes, int grid
   if (head > bytes) head = bytes;
   const size_t nvec = (bytes - head) / 16;
   const size_t tail = bytes - head - nvec * 16;
-  if (use_wt(g_copy_wt, nvec * 16)) {
+  if (use_wt(nvec * 16)) {
     hipLaunchKernelGGL((copy_kernel<4, true>), dim3(blocks), dim3(kBlock), 0, s, (char*)dst,
                        (const char*)src, head, nvec, tail);
   } else {

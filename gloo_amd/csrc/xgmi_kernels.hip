@@ -424,22 +424,15 @@ __device__ __forceinline__ void report_timeout(int* status, int* claim, int code
 
 // Lane 0 waits until word >= epoch (bounded); the whole workgroup learns
 // the outcome.  Returns false after a timeout (reported).
-// pollLoad: poll with a system-scope atomic LOAD (global/flat ... sc0 sc1)
-// instead of the memory-side compare-exchange (kPollLoad in the params;
-// GLOO_AMD_FLAG_POLL=load) -- an experiment knob, see DESIGN.md 5b.
-__device__ __forceinline__ uint64_t poll_flag(const uint64_t* word, bool pollLoad) {
-  if (pollLoad) return __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  return get_flag(word);
-}
 
 __device__ __forceinline__ bool wait_flag(const uint64_t* word, uint64_t epoch, int peer,
                                           uint64_t start, uint64_t timeoutTicks, int* status,
                                           int* claim, int* s_ok, bool narrow, bool acquire = true,
-                                          int where = 0, bool pollLoad = false) {
+                                          int where = 0) {
   if (threadIdx.x == 0) {
     int ok = 1;
     uint64_t v;
-    for (uint32_t spin = 1; (v = poll_flag(word, pollLoad)) < epoch; spin++) {
+    for (uint32_t spin = 1; (v = get_flag(word)) < epoch; spin++) {
       if (__builtin_amdgcn_s_memrealtime() - start > timeoutTicks) {
         ok = 0;
         report_timeout(status, claim, 1 + peer + 256 * where, v, epoch);
@@ -631,7 +624,6 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
   const int w = blockIdx.x;
   S* buf = reinterpret_cast<S*>(p.buf);
   const bool aligned = ((uintptr_t)p.buf % 16) == 0;
-  const bool pollLoad = p.pollLoad != 0;
   const bool narrow = p.narrow != 0;
   // diagnostics (GLOO_AMD_DEVTRACE=1): per workgroup and step, when the step
   // started and when its wait (if any) was satisfied
@@ -652,7 +644,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
         if (seq > (uint64_t)p.slots &&
             !wait_flag(flag_at(st.credit, w), seq - p.slots, st.peer,
                        __builtin_amdgcn_s_memrealtime(), p.timeoutTicks, p.status, p.claim,
-                       &s_ok, narrow, /*acquire=*/false, 1 + i, pollLoad)) {
+                       &s_ok, narrow, /*acquire=*/false, 1 + i)) {
           return;
         }
         stamp(2 * i + 1);
@@ -685,7 +677,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
       }
       case 1:  // RECV
         if (!wait_flag(flag_at(st.flag, w), seq, st.peer, __builtin_amdgcn_s_memrealtime(),
-                       p.timeoutTicks, p.status, p.claim, &s_ok, narrow, true, 1 + i, pollLoad)) {
+                       p.timeoutTicks, p.status, p.claim, &s_ok, narrow, true, 1 + i)) {
           return;
         }
         stamp(2 * i + 1);
