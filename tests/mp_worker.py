@@ -17,6 +17,8 @@ algo: ring_chunked | halving_doubling | ring_chunked_mesh (class algorithms)
       raise IoException)
       scale:cfg34 | scale:cfg5 (BASELINE.json configs at full size, 8 ranks:
       every engine's output SHA-256 against tests/golden/scale_golden.json)
+      linkprobe (the measured-link probe through the product's IPC path, and
+      every peer's connect-time view; then an allreduce on the same context)
       big:fast | big:plain (the ring on the plan kernel over MORE than 2 GiB per
       rank, P = 2, the given stream policy: every 32-bit store offset the
       write-through path could form is exceeded; exact at P = 2 since fp32
@@ -55,6 +57,8 @@ def main():
         return run_scale(store_dir, rank, size, algo[len("scale:"):])
     if algo.startswith("big:"):
         return run_big(store_dir, rank, size, algo[len("big:"):])
+    if algo == "linkprobe":
+        return run_linkprobe(store_dir, rank, size)
     if algo.startswith("fn_"):
         return run_fn(store_dir, rank, size, algo, N)
     code = O.HALVING_DOUBLING if algo == "halving_doubling" else O.RING_CHUNKED
@@ -579,6 +583,58 @@ def run_big(store_dir, rank, size, policy):
         print("MISMATCH rank", rank, bad[:10])
         sys.exit(1)
     print("OK")
+
+
+def run_linkprobe(store_dir, rank, size):
+    import torch
+
+    import gloo_amd
+    store = gloo_amd.rendezvous.FileStore(store_dir)
+    ctx = gloo_amd.rendezvous.Context(rank, size, 0)
+    ctx.setTimeout(60)
+    ctx.connectFullMesh(store)
+    bad = []
+    for k in range(size):
+        if k == rank:
+            continue
+        info = ctx.peer_info(k)
+        # one GPU: every peer is on this rank's own GPU, nothing asked of a link
+        if not (info["same_gpu"] and info["device"] == 0 and info["can_access_peer"] is None
+                and info["native_atomics"] is None):
+            bad.append(("peer_info", k, info))
+    nbytes = (8 << 20) + 4096
+    probe = gloo_amd.rendezvous.LinkProbe(ctx, nbytes)
+    piece = (nbytes // (size - 1)) & ~4095
+    for pattern, name in ((probe.RING, "ring"), (probe.MESH, "mesh")):
+        for engine in (probe.DMA, probe.KERNEL):
+            barrier(store, rank, size, "lp%s%d" % (name, engine))
+            secs, link = probe.run(pattern, engine, 128, 3)
+            want = nbytes if pattern == probe.RING else piece
+            if not (secs > 0 and link == want):
+                bad.append(("probe", name, engine, secs, link, want))
+            print("LINK rank %d %s engine %d %.1f GB/s" % (rank, name, engine,
+                                                         link * 3 / secs / 1e9), flush=True)
+    barrier(store, rank, size, "lpdone")
+    probe.close()
+    # the context goes on working after the probe: its blocks went back to the pool
+    buf = torch.full((1 << 20,), float(rank + 1), device="cuda")
+    alg = gloo_amd.AllreduceRingChunked(ctx, [buf])
+    alg.run()
+    if not bool((buf == size * (size + 1) / 2).all().item()):
+        bad.append(("allreduce after probe",))
+    alg.close()
+    barrier(store, rank, size, "end")
+    ctx.close()
+    if bad:
+        print("MISMATCH rank", rank, bad[:10])
+        sys.exit(1)
+    print("OK")
+
+
+def barrier(store, rank, size, tag):
+    store.set("bar/%s/%d" % (tag, rank), b"1")
+    for r in range(size):
+        store.get("bar/%s/%d" % (tag, r), timeout_ms=60000)
 
 
 def run_scale(store_dir, rank, size, group):

@@ -484,6 +484,34 @@ def test_device_engine_variants(mode, knob):
             assert p.returncode == 0 and "OK" in outs[r], "rank %d failed:\n%s" % (r, every)
 
 
+@pytest.mark.parametrize("P", [2, 3])
+def test_link_probe_multiprocess(P):
+    """The measured-link probe bench.py runs on the node (glx_link_probe):
+    every rank's receive block through the context's canary-checked IPC path,
+    ring and mesh patterns, DMA and copy-kernel writes, the busiest link's
+    byte count; each peer's connect-time view (glx_context_peer_info); and an
+    allreduce on the same context afterwards (the probe's blocks went back to
+    the pool)."""
+    with tempfile.TemporaryDirectory() as d:
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), "linkprobe"],
+                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                 for r in range(P)]
+        outs = []
+        for p in procs:
+            try:
+                o, _ = p.communicate(timeout=180)
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+            outs.append(o.decode(errors="replace"))
+        every = "\n".join("---- rank %d (rc %s) ----\n%s" % (r, p.returncode, outs[r])
+                          for r, p in enumerate(procs))
+        for r, p in enumerate(procs):
+            assert p.returncode == 0 and "OK" in outs[r], "rank %d failed:\n%s" % (r, every)
+
+
 @pytest.mark.parametrize("P", [2, 4])
 def test_algorithm_churn_multiprocess(P):
     """36 algorithms created, run twice and destroyed back to back per rank
