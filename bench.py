@@ -55,6 +55,8 @@ def parse():
                    help="N>1: host-issued steps' transports tried (default: DMA and the "
                         "copy kernel at 128 workgroups; all: 7 variants)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-multidev", action="store_true",
+                   help="N=1: skip the multi-device-pointer check run on boxes with >= 2 GPUs")
     p.add_argument("--link-probe", dest="link_probe", action="store_true", default=True,
                    help="N>1: measure per-link copy ceilings (default; the product's IPC path)")
     p.add_argument("--no-link-probe", dest="link_probe", action="store_false")
@@ -306,8 +308,31 @@ def cold_rate(torch, gloo_amd, n, dtype, dev, stream, steps, pairs=4):
             "us_per_launch": round(t * 1e6, 2), "pairs": pairs}
 
 
+def multidev_check(torch, timeout=240):
+    """SURVEY 8f #4 on hardware: one rank's pointers on several GPUs
+    (tools/multidev_check.py), run as a child process -- before this process
+    touches a GPU -- so that a failure there cannot take the headline
+    measurement down.  Only where >= 2 GPUs are visible (the driver's
+    multi-GPU node); None elsewhere."""
+    if torch.cuda.device_count() < 2:  # counting devices does not initialise them
+        return None
+    import subprocess
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools",
+                          "multidev_check.py")
+    try:
+        out = subprocess.run([sys.executable, script], capture_output=True, text=True,
+                             timeout=timeout)
+    except subprocess.TimeoutExpired:
+        return {"ok": False, "error": "timed out after %d s" % timeout}
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    if out.returncode != 0 or not lines:
+        return {"ok": False, "error": "exit %d: %s" % (out.returncode, out.stderr[-300:])}
+    return json.loads(lines[-1])
+
+
 def bench_single(args):
     import torch
+    multidev = None if args.no_multidev else multidev_check(torch)
     import gloo_amd
     S = args.size_mib << 20
     es = DTYPES[args.dtype][1]
@@ -378,6 +403,8 @@ def bench_single(args):
             reps=min(steps, 10))
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(S, args.cpu_seconds, args.dtype)
+    if multidev is not None:
+        res["multi_device_pointers"] = multidev
     return res
 
 
@@ -601,8 +628,8 @@ def transport_health(peer_infos, stats):
 
 def host_endpoint_rate(torch, dist, gloo_amd, ctx, src, dev_result, algo, reps):
     """The path as the reference runs it: buffers in host memory.  The
-    algorithm is built on a host buffer (pinned; the product pins pageable
-    buffers itself) and stages it: H2D in first-use order overlapped with the
+    algorithm is built on a host buffer (pinned; the product stages pageable
+    buffers through pinned mirrors of its own) and stages it: H2D in first-use order overlapped with the
     schedule, each range copied back after its final write.  Timed end to end
     (max over ranks); the result must equal the device-resident run's bits."""
     host = src.cpu()

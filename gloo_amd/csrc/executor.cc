@@ -379,10 +379,11 @@ void HipPlanExecutor::release() noexcept {
   givePinned(hostStage_, hostStageBytes_);
   hostStage_ = nullptr;
   for (char* d : fnStage_) hipFree(d);
-  for (void* p : registered_) {
-    const hipError_t ue = hipHostUnregister(p);
-    GLX_TRACE_MEM("r%d hipHostUnregister(%p) -> %d", contextRank_, p, (int)ue);
-  }
+  for (PinnedBlock& m : ptrMirror_) givePinned(m.p, m.bytes);
+  ptrMirror_.clear();
+  for (PinnedBlock& m : callMirror_) givePinned(m.p, m.bytes);
+  for (PinnedBlock& m : fnMirror_) givePinned(m.p, m.bytes);
+  fnMirror_.clear();
   for (auto& e : events_) {
     if (e != nullptr) hipEventDestroy(e);
   }

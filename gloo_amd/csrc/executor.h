@@ -233,17 +233,43 @@ class HipPlanExecutor : public Algorithm {
   std::chrono::milliseconds timeout_{0};  // per-call override (0: context's)
 
   // Host-memory endpoints (host mode): the user's pointers are
-  // host memory (pinned here with hipHostRegister when possible); the
-  // schedule runs on device copies.  H2D pieces go out in first-use order on
-  // h2d_ and every step waits only for the pieces of its own range; each
-  // range is copied back on d2h_ right after its final write.
+  // host memory; the schedule runs on device copies.  H2D pieces go out in
+  // first-use order on h2d_ and every step waits only for the pieces of its
+  // own range; each range is copied back on d2h_ right after its final write.
+  // Pinned user memory is copied directly.  Pageable user memory is never
+  // handed to the runtime (no hipHostRegister of the caller's pages, no
+  // pageable hipMemcpy): it is mirrored by a pinned workspace block, as the
+  // reference's CUDA algorithms stage host data through a pinned host
+  // workspace (gloo/cuda_workspace.h, CudaHostWorkspace); a piece is copied
+  // into the mirror on the host when it is issued, and a range comes back
+  // out of it once its D2H copy has completed (doneRanges / end of run).
   bool hostMode_ = false;
   std::vector<char*> devBufs_;     // device copy of each user pointer (or of hostStage_)
   bool hostFold_ = false;          // several pointers < kOnDeviceThreshold: fold on the host
   char* hostStage_ = nullptr;      // pinned: the host fold's result, staged and returned
   size_t hostStageBytes_ = 0;      // its size (from and back to a process-wide cache)
-  std::vector<void*> hostSources() const;  // H2D sources of the staged buffer
-  std::vector<void*> hostDests() const;    // where its final values go back to
+  // A host buffer as the copies see it: `user` (the caller's) and `dma`
+  // (what the DMA reads / writes: `user` itself when pinned, else its mirror)
+  struct HostSide {
+    char* user;
+    char* dma;
+  };
+  std::vector<HostSide> hostSources() const;  // H2D sources of the staged buffer
+  std::vector<HostSide> hostDests() const;    // where its final values go back to
+  struct PinnedBlock {
+    char* p = nullptr;
+    size_t bytes = 0;
+  };
+  std::vector<PinnedBlock> ptrMirror_;  // per ptrs_ entry (p == nullptr: pinned)
+  PinnedBlock callMirror_[2];           // a function-style call: source, destination
+  bool callMirrored_[2] = {false, false};  // the current call uses them
+  std::vector<PinnedBlock> fnMirror_;   // runFnHost's whole-buffer copies
+  // The pinned block `m` (taken from the process-wide cache on first use)
+  // when `user` is pageable, else `user`.
+  char* mirrorFor(void* user, PinnedBlock& m);
+  // Mirrored destinations: ranges [at, at+n) from the mirror to the user.
+  void copyOut(const std::vector<glx::Range>& ranges);
+  void flushMirrors();  // every completed batch's copy-out (end of a run)
   // staged_: the current run stages host memory (class host mode, or a
   // function-style call on host buffers); callSrc_/callDst_: that call's
   // host buffers
@@ -251,7 +277,6 @@ class HipPlanExecutor : public Algorithm {
   std::vector<void*> callSrc_, callDst_;
   void setupCallStaging();
   void runFnHostStaged(const FnCall& call);
-  std::vector<void*> registered_;  // host ranges pinned by us
   hipStream_t h2d_ = nullptr, d2h_ = nullptr;
   glx::StagePlan stage_;
   std::vector<hipEvent_t> h2dEvents_;  // one per stage_.h2d piece
@@ -276,6 +301,7 @@ class HipPlanExecutor : public Algorithm {
   struct DoneBatch {
     hipEvent_t ev;
     std::vector<glx::Range> ranges;
+    bool pendingOut;  // the ranges still sit in mirrors only
   };
   std::vector<DoneBatch> doneQueue_;
   std::vector<hipEvent_t> doneEvents_;  // pool

@@ -67,6 +67,11 @@ void HipPlanExecutor::runFnHostStaged(const FnCall& call) {
   void* src = call.in.empty() ? call.out[0] : call.in[0];
   callSrc_ = {src};
   callDst_ = {call.out[0]};
+  for (int i = 0; i < 2; i++) {  // pageable source / destination: through a mirror
+    void* u = i == 0 ? src : call.out[0];
+    callMirrored_[i] = !isPinnedHost(u);
+    if (callMirrored_[i] && callMirror_[i].p == nullptr) mirrorFor(nullptr, callMirror_[i]);
+  }
   staged_ = true;
   timeout_ = call.timeout;
   struct Restore {
@@ -102,6 +107,7 @@ void HipPlanExecutor::runFnHostStaged(const FnCall& call) {
   GLX_HIP_CHECK(hipStreamSynchronize(h2d_));
   noteDone(d2h_);
   checkDevice();
+  flushMirrors();
 }
 
 void HipPlanExecutor::runFnHost(const FnCall& call) {
@@ -125,9 +131,12 @@ void HipPlanExecutor::runFnHost(const FnCall& call) {
     HipPlanExecutor* e;
     ~Restore() { e->timeout_ = std::chrono::milliseconds(0); }
   } restore{this};
+  // pageable buffers through pinned mirrors: slots 0..srcs-1 the sources,
+  // then out[0]'s old value (float16), then the outputs
+  while (fnMirror_.size() < srcs.size() + 1 + call.out.size()) fnMirror_.emplace_back();
   for (size_t i = 0; i < srcs.size(); i++) {
-    GLX_HIP_CHECK(hipMemcpyAsync(fnStage_[1 + i], srcs[i], bytes, hipMemcpyHostToDevice,
-                                 compute_));
+    GLX_HIP_CHECK(hipMemcpyAsync(fnStage_[1 + i], mirrorFor(srcs[i], fnMirror_[i]), bytes,
+                                 hipMemcpyHostToDevice, compute_));
   }
   std::vector<void*> din, dout;
   char* out0;
@@ -140,17 +149,25 @@ void HipPlanExecutor::runFnHost(const FnCall& call) {
     out0 = fnStage_[0];
     if (dtype_ == GLX_FLOAT16 && din.size() >= 2) {
       // float16's assignment reads out[0]'s old value
-      GLX_HIP_CHECK(hipMemcpyAsync(out0, call.out[0], bytes, hipMemcpyHostToDevice, compute_));
+      GLX_HIP_CHECK(hipMemcpyAsync(out0, mirrorFor(call.out[0], fnMirror_[srcs.size()]), bytes,
+                                   hipMemcpyHostToDevice, compute_));
     }
   }
   localReduce(din, dout);
   if (contextSize_ > 1) exchange(out0);
-  for (void* p : call.out) {
-    GLX_HIP_CHECK(hipMemcpyAsync(p, out0, bytes, hipMemcpyDeviceToHost, compute_));
+  std::vector<char*> outDma(call.out.size());
+  for (size_t i = 0; i < call.out.size(); i++) {
+    PinnedBlock& m = fnMirror_[srcs.size() + 1 + i];
+    outDma[i] = isPinnedHost(call.out[i]) ? static_cast<char*>(call.out[i])
+                                          : (m.p ? m.p : mirrorFor(nullptr, m));
+    GLX_HIP_CHECK(hipMemcpyAsync(outDma[i], out0, bytes, hipMemcpyDeviceToHost, compute_));
   }
   noteDone(compute_);
   waitDevice(compute_);
   checkDevice();
+  for (size_t i = 0; i < call.out.size(); i++) {
+    if (outDma[i] != call.out[i]) std::memcpy(call.out[i], outDma[i], bytes);
+  }
 }
 
 namespace {
@@ -198,6 +215,21 @@ void HipPlanExecutor::givePinned(char* p, size_t bytes) {
   c.free.emplace_back(bytes, p);
 }
 
+// `user` when it is pinned (or null: a destination-only mirror is wanted);
+// else the pinned mirror block m, taken on first use, with `user`'s
+// bytes copied in when `user` is a source (the whole-buffer case).
+char* HipPlanExecutor::mirrorFor(void* user, PinnedBlock& m) {
+  if (user != nullptr && isPinnedHost(user)) return static_cast<char*>(user);
+  const size_t bytes = std::max<size_t>((size_t)count_ * esize_, 16);
+  if (m.p == nullptr) {
+    m.bytes = bytes;
+    m.p = takePinned(&m.bytes);
+    GLX_TRACE_MEM("r%d mirror %p (%zu) for %p", contextRank_, (void*)m.p, m.bytes, user);
+  }
+  if (user != nullptr) std::memcpy(m.p, user, (size_t)count_ * esize_);
+  return m.p;
+}
+
 void HipPlanExecutor::setupHostMode() {
   const size_t bytes = (size_t)count_ * esize_;
   // Several host pointers under kOnDeviceThreshold: fold them on the host
@@ -209,19 +241,19 @@ void HipPlanExecutor::setupHostMode() {
     hostStageBytes_ = std::max<size_t>(bytes, 16);
     hostStage_ = takePinned(&hostStageBytes_);
   }
-  for (void* p : hostSources()) {
-    if (!isPinnedHost(p)) {
-      // pin the caller's buffer for the algorithm's lifetime (the reference's
-      // algorithms also bind their buffers at construction); if the runtime
-      // refuses, pageable copies are still correct, only slower
-      const hipError_t re = hipHostRegister(p, bytes, hipHostRegisterPortable);
-      GLX_TRACE_MEM("r%d hipHostRegister(%p, %zu) -> %d", contextRank_, p, bytes, (int)re);
-      if (re == hipSuccess) {
-        registered_.push_back(p);
-      } else {
-        (void)hipGetLastError();
-      }
+  // pageable buffers get their pinned mirrors (a host fold's single source
+  // is the pinned hostStage_ itself)
+  ptrMirror_.assign(ptrs_.size(), PinnedBlock{});
+  if (!hostFold_) {
+    for (size_t k = 0; k < ptrs_.size(); k++) {
+      if (isPinnedHost(ptrs_[k])) continue;
+      ptrMirror_[k].bytes = std::max<size_t>(bytes, 16);
+      ptrMirror_[k].p = takePinned(&ptrMirror_[k].bytes);
+      GLX_TRACE_MEM("r%d mirror %p (%zu) for %p", contextRank_, (void*)ptrMirror_[k].p,
+                    ptrMirror_[k].bytes, ptrs_[k]);
     }
+  }
+  for (size_t k = 0; k < hostSources().size(); k++) {
     char* d = nullptr;
     GLX_HIP_CHECK(hipMalloc((void**)&d, bytes));
     GLX_TRACE_MEM("r%d hipMalloc devBuf %p (%zu)", contextRank_, (void*)d, bytes);
@@ -285,25 +317,58 @@ void HipPlanExecutor::waitH2D(hipStream_t s, int& waited, int64_t off, int64_t l
 
 // The host buffers the device copies are staged from and back to: the
 // user's pointers, or the one pinned buffer they were folded into.
-std::vector<void*> HipPlanExecutor::hostSources() const {
-  if (!callSrc_.empty()) return callSrc_;
-  if (hostFold_) return {hostStage_};
-  return ptrs_;
+std::vector<HipPlanExecutor::HostSide> HipPlanExecutor::hostSources() const {
+  if (!callSrc_.empty()) {
+    char* u = static_cast<char*>(callSrc_[0]);
+    return {HostSide{u, callMirrored_[0] ? callMirror_[0].p : u}};
+  }
+  if (hostFold_) return {HostSide{hostStage_, hostStage_}};
+  std::vector<HostSide> v;
+  for (size_t k = 0; k < ptrs_.size(); k++) {
+    char* u = static_cast<char*>(ptrs_[k]);
+    v.push_back(HostSide{u, ptrMirror_[k].p ? ptrMirror_[k].p : u});
+  }
+  return v;
 }
 
-std::vector<void*> HipPlanExecutor::hostDests() const {
-  if (!callDst_.empty()) return callDst_;
+std::vector<HipPlanExecutor::HostSide> HipPlanExecutor::hostDests() const {
+  if (!callDst_.empty()) {
+    char* u = static_cast<char*>(callDst_[0]);
+    return {HostSide{u, callMirrored_[1] ? callMirror_[1].p : u}};
+  }
   return hostSources();
+}
+
+void HipPlanExecutor::copyOut(const std::vector<glx::Range>& ranges) {
+  for (const HostSide& h : hostDests()) {
+    if (h.dma == h.user) continue;
+    for (const glx::Range& r : ranges) {
+      const size_t at = (size_t)r.off * esize_, n = (size_t)r.len * esize_;
+      std::memcpy(h.user + at, h.dma + at, n);
+    }
+  }
+}
+
+// After the run's streams are synchronised: every batch not yet copied out.
+void HipPlanExecutor::flushMirrors() {
+  std::lock_guard<std::mutex> g(doneMutex_);
+  for (DoneBatch& b : doneQueue_) {
+    if (!b.pendingOut) continue;
+    copyOut(b.ranges);
+    b.pendingOut = false;
+  }
 }
 
 // Final values of `ranges` (in devBufs_[0]) to every user pointer, on d2h_
 // (the caller has made d2h_ wait for the writes).
 void HipPlanExecutor::copyBack(const std::vector<glx::Range>& ranges) {
+  const std::vector<HostSide> dsts = hostDests();
+  bool mirrored = false;
+  for (const HostSide& h : dsts) mirrored = mirrored || h.dma != h.user;
   for (const glx::Range& r : ranges) {
     const size_t at = (size_t)r.off * esize_, n = (size_t)r.len * esize_;
-    for (void* p : hostDests()) {
-      GLX_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(p) + at, devBufs_[0] + at, n,
-                                   hipMemcpyDeviceToHost, d2h_));
+    for (const HostSide& h : dsts) {
+      GLX_HIP_CHECK(hipMemcpyAsync(h.dma + at, devBufs_[0] + at, n, hipMemcpyDeviceToHost, d2h_));
     }
   }
   if (ranges.empty() || hostFold_) return;  // host-folded results return at the end
@@ -316,19 +381,23 @@ void HipPlanExecutor::copyBack(const std::vector<glx::Range>& ranges) {
   }
   hipEvent_t e = doneEvents_[doneUsed_++];
   GLX_HIP_CHECK(hipEventRecord(e, d2h_));
-  doneQueue_.push_back(DoneBatch{e, ranges});
+  doneQueue_.push_back(DoneBatch{e, ranges, mirrored});
 }
 
 std::vector<glx::Range> HipPlanExecutor::doneRanges() {
   std::lock_guard<std::mutex> g(doneMutex_);
   std::vector<glx::Range> out;
-  for (const auto& b : doneQueue_) {
+  for (auto& b : doneQueue_) {
     const hipError_t e = hipEventQuery(b.ev);
     if (e == hipErrorNotReady) {
       (void)hipGetLastError();
       continue;
     }
     GLX_HIP_CHECK(e);
+    if (b.pendingOut) {  // landed in the mirror: out to the caller's buffer first
+      copyOut(b.ranges);
+      b.pendingOut = false;
+    }
     out.insert(out.end(), b.ranges.begin(), b.ranges.end());
   }
   return out;
@@ -338,10 +407,13 @@ std::vector<glx::Range> HipPlanExecutor::doneRanges() {
 void HipPlanExecutor::issuePiece(size_t j) {
   const glx::Range& r = stage_.h2d[j];
   const size_t at = (size_t)r.off * esize_, n = (size_t)r.len * esize_;
-  const std::vector<void*> hsrc = hostSources();
+  const std::vector<HostSide> hsrc = hostSources();
   for (size_t k = 0; k < hsrc.size(); k++) {
-    GLX_HIP_CHECK(hipMemcpyAsync(devBufs_[k] + at, static_cast<const char*>(hsrc[k]) + at, n,
-                                 hipMemcpyHostToDevice, h2d_));
+    // pageable: into the mirror on the host first (the copy below then
+    // reads pinned memory only)
+    if (hsrc[k].dma != hsrc[k].user) std::memcpy(hsrc[k].dma + at, hsrc[k].user + at, n);
+    GLX_HIP_CHECK(hipMemcpyAsync(devBufs_[k] + at, hsrc[k].dma + at, n, hipMemcpyHostToDevice,
+                                 h2d_));
   }
   GLX_HIP_CHECK(hipEventRecord(h2dEvents_[j], h2d_));
   pieceIssued_[j] = 1;
@@ -419,7 +491,8 @@ void HipPlanExecutor::runFed() {
       doneEvents_.push_back(e);
     }
     GLX_HIP_CHECK(hipEventRecord(doneEvents_[0], h2d_));
-    doneQueue_.push_back(DoneBatch{doneEvents_[0], {glx::Range{0, count_}}});
+    // in place: the caller's buffer already holds the result
+    doneQueue_.push_back(DoneBatch{doneEvents_[0], {glx::Range{0, count_}}, false});
     doneUsed_ = 1;
     return;
   }
@@ -438,7 +511,7 @@ void HipPlanExecutor::runHost() {
       return;
     }
   }
-  const std::vector<void*> hsrc = hostSources();
+  const size_t nsrc = hostSources().size();
   computeH2dWaited_ = -1;
   for (auto& c : copies_) c.h2dWaited = -1;
   if (!fedRun_) {
@@ -450,7 +523,7 @@ void HipPlanExecutor::runHost() {
     pieceIssued_.assign(stage_.h2d.size(), 0);
     for (size_t j = 0; j < stage_.h2d.size(); j++) issuePiece(j);
   }
-  if (contextSize_ == 1 && hsrc.size() > 1 && !fedRun_) {
+  if (contextSize_ == 1 && nsrc > 1 && !fedRun_) {
     // One rank, several host pointers: the allreduce is the local fold and
     // broadcast.  Pipelined per H2D piece: the fold of piece j runs once its
     // copies have landed, and its result goes back to every host pointer
@@ -472,9 +545,10 @@ void HipPlanExecutor::runHost() {
     GLX_HIP_CHECK(hipStreamSynchronize(d2h_));
     GLX_HIP_CHECK(hipStreamSynchronize(h2d_));
     noteDone(d2h_);
+    flushMirrors();
     return;
   }
-  if (hsrc.size() > 1) {  // local fold needs every buffer whole
+  if (nsrc > 1) {  // local fold needs every buffer whole
     waitH2D(compute_, computeH2dWaited_, 0, count_);
     std::vector<const void*> srcs(devBufs_.begin(), devBufs_.end());
     GLX_HIP_CHECK(glx::launch_reduce_n(op_, dtype_, devBufs_[0], srcs.data(), (int)srcs.size(),
@@ -483,7 +557,7 @@ void HipPlanExecutor::runHost() {
   if (contextSize_ > 1) exchange(devBufs_[0]);
   // ranges no step wrote: their value is the local fold (a no-op for one
   // pointer, whose host copy already holds it)
-  if (hsrc.size() > 1 && !stage_.d2hRest.empty()) {
+  if (nsrc > 1 && !stage_.d2hRest.empty()) {
     GLX_HIP_CHECK(hipEventRecord(hostDone_, compute_));
     GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, hostDone_, 0));
     copyBack(stage_.d2hRest);
@@ -493,6 +567,7 @@ void HipPlanExecutor::runHost() {
   GLX_HIP_CHECK(hipStreamSynchronize(h2d_));
   noteDone(d2h_);
   checkDevice();
+  flushMirrors();
   if (hostFold_) {  // local broadcast on the host
     for (void* p : ptrs_) std::memcpy(p, hostStage_, bytes);
   }

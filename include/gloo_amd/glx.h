@@ -285,11 +285,12 @@ glx_algorithm* glx_allreduce_create(glx_context* ctx, int algo, void* const* ptr
                                     const glx_stream_t* streams, int nstreams);
 
 /* Buffers may be device memory or host memory (pageable or pinned; all
- * pointers of one algorithm alike).  Host buffers are pinned with
- * hipHostRegister for the algorithm's lifetime when the runtime allows and
- * staged through device copies: H2D in the order the schedule first touches
- * each piece, every step waiting only for its own range, and each range
- * copied back as soon as its final value is written. */
+ * pointers of one algorithm alike).  Host buffers are staged through device
+ * copies: H2D in the order the schedule first touches each piece, every step
+ * waiting only for its own range, and each range copied back as soon as its
+ * final value is written.  Pinned buffers are copied
+ * directly; pageable ones through a pinned workspace mirror (the caller's
+ * pages are never registered with the runtime). */
 
 /* ---- function-style collective ---------------------------------------- */
 /* gloo::AllreduceOptions::Algorithm (gloo/allreduce.h:38-42), plus
