@@ -213,6 +213,69 @@ def synthetic(torch, n, dtype, dev, seed):
     return x.to(getattr(torch, DTYPES[dtype][0]))
 
 
+def _s64(c):
+    """An unsigned 64-bit constant as the int64 with the same bits."""
+    return c - (1 << 64) if c >= 1 << 63 else c
+
+
+def splitmix_fill(torch, n, dtype, dev, seed, rank, chunk=1 << 24):
+    """SURVEY 8d's synthetic inputs, generated on the device: element i of
+    rank r is x = ((h >> 40) - 2^23) / 2^23 with h = splitmix64(seed ^ r<<40 ^
+    i), in [-1, 1) on a 24-bit grid (fp16 / bf16: the fp32 value rounded to
+    nearest even).  The same values as the test oracle's generator, so the
+    allreduce's output can be checked against the reference's own digest
+    (tests/golden/bench_golden.json).  int64 arithmetic wraps like the
+    uint64 original; shifts are made logical by masking."""
+    def lsr(z, k):
+        return (z >> k) & ((1 << (64 - k)) - 1)
+    out = torch.empty(n, dtype=getattr(torch, DTYPES[dtype][0]), device=dev)
+    key = _s64(seed ^ (rank << 40))
+    for lo in range(0, n, chunk):
+        z = torch.arange(lo, min(n, lo + chunk), dtype=torch.int64, device=dev) ^ key
+        z = z + _s64(0x9e3779b97f4a7c15)
+        z = (z ^ lsr(z, 30)) * _s64(0xbf58476d1ce4e5b9)
+        z = (z ^ lsr(z, 27)) * _s64(0x94d049bb133111eb)
+        z = z ^ lsr(z, 31)
+        v = (lsr(z, 40) - 8388608).to(torch.float32) / 8388608.0
+        out[lo:lo + v.numel()] = v.to(out.dtype)
+    return out
+
+
+# golden fixture codes (oracle/oracle.py): dtypes and the two class algorithms
+GOLDEN_DTYPE = {"f32": 5, "f16": 7, "bf16": 8}
+GOLDEN_ALGO = {"ring_chunked": 0, "halving_doubling": 1}
+
+
+def reference_cases(world, n, dtype):
+    """The reference's own output digests for this run's workload, by plan
+    ("ring_chunked" / "halving_doubling"): tests/golden/bench_golden.json
+    (256 MiB fp32 at P = 2, 4, 8) and scale_golden.json (cfg3..cfg5; bf16
+    there is the oracle's restatement, marked unpinned).  Data fixtures, made
+    by tests/golden/make_golden.py from the reference compiled from source."""
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden")
+    found = {}
+    for name in ("scale_golden.json", "bench_golden.json"):
+        try:
+            with open(os.path.join(here, name)) as f:
+                cases = json.load(f)["cases"]
+        except (OSError, ValueError, KeyError):
+            continue
+        for c in cases:
+            if (c["P"] == world and c["N"] == n and c["dtype"] == GOLDEN_DTYPE[dtype]
+                    and c.get("seed") == SEED and c.get("op", 1) == 1):
+                for plan, code in GOLDEN_ALGO.items():
+                    if c["algo"] == code:
+                        found[plan] = c
+    return found
+
+
+def sha256_of(t):
+    import hashlib
+    h = hashlib.sha256()
+    h.update(t.contiguous().view(-1).view(__import__("torch").uint8).cpu().numpy().tobytes())
+    return h.hexdigest()
+
+
 def expected_sum(torch, a, b):
     """Independent torch restatement of c = a + b with the reference's
     semantics: IEEE add in fp32 rounded once to the element type; for float16
@@ -450,6 +513,8 @@ FAST = {}  # bench name -> whether its plan kernel ran the fast streams
 SYNC = {}  # bench name -> its device engine's flag sync ("narrow" / "system" / None)
 RUN_SYNC = ["auto"]  # the run's flag sync (probe_device_engines may fall back to "system")
 CHECKS = {}  # bench name -> result_check() of its post-timing run
+REFDIG = {}  # bench name -> its output's SHA-256 equals the reference's (bench_golden.json)
+SEED = 1234  # SURVEY 8d's synthetic-input seed
 
 
 def plan_name(algo):
@@ -459,6 +524,13 @@ def plan_name(algo):
             algo = algo[:-len(suffix)]
     return {"ring_chunked_mesh_steps": "ring_chunked_mesh",
             "ring_chunked_repl": "ring_chunked_repl"}.get(algo, algo)
+
+
+def golden_plan(algo):
+    """The reference algorithm whose output a candidate must equal bit for
+    bit: the ring's chunking and reduction order (mesh and replicated
+    schedules included) or halving-doubling's."""
+    return "halving_doubling" if plan_name(algo) == "halving_doubling" else "ring_chunked"
 
 
 def make_alg(gloo_amd, ctx, buf, algo):
@@ -838,6 +910,12 @@ def north_star_block(S, world, t, p50, engine, hbm_bytes):
                     "is link_frac >= 0.8"}
 
 
+def agreed_inputs(torch, dist, ok):
+    flag = torch.tensor([0 if ok else 1], dtype=torch.int32)
+    dist.all_reduce(flag)
+    return int(flag.item()) == 0
+
+
 def bench_multi(args):
     import torch
     import torch.distributed as dist
@@ -855,9 +933,18 @@ def bench_multi(args):
     es = DTYPES[args.dtype][1]
     n = S // es
     steps = args.steps or 20
-    src = synthetic(torch, n, args.dtype, dev, 1234 + rank)
+    # SURVEY 8d's synthetic inputs, the ones the reference's digests were
+    # made from (tests/golden/bench_golden.json)
+    src = splitmix_fill(torch, n, args.dtype, dev, SEED, rank)
     buf = src.clone()
     torch.cuda.synchronize()
+    golden = reference_cases(world, n, args.dtype)
+    gin = None
+    if golden:
+        mine = sha256_of(src)
+        gin = all(mine == c["input_sha256"][rank] for c in golden.values())
+        if not agreed_inputs(torch, dist, gin):
+            gin = False
     store = gloo_amd.rendezvous.PrefixStore(
         "gloo_amd_bench", gloo_amd.rendezvous.TorchStore(dist.distributed_c10d._get_default_store()))
     ctx = gloo_amd.rendezvous.Context(rank, world, local)
@@ -956,6 +1043,11 @@ def bench_multi(args):
         # every rank is here: the collective check of the result
         ok, rel = result_check(torch, dist, src, r["result"])
         CHECKS[a] = {"ok": ok, "err_over_tol": round(rel, 4)}
+        gc = golden.get(golden_plan(a))
+        if gc is not None and gin:
+            # every rank holds the same bits; rank 0's digest speaks for all
+            # (the cross-rank checksum below compares them)
+            REFDIG[a] = sha256_of(r["result"]) == gc["output_sha256"]
         if agreed(ok):
             runs[a] = r
         else:
@@ -1126,6 +1218,15 @@ def bench_multi(args):
             "transport_stats": {a: TRANSPORT.get(a) for a in runs},
             "transport_health": health,
             "result_checks": CHECKS,
+            "reference_digest": ({"cases": {k: v["name"] for k, v in golden.items()},
+                                  "inputs_match": gin,
+                                  "outputs_match": dict(REFDIG),
+                                  "note": "SHA-256 of each timed candidate's output (rank 0) "
+                                          "vs the reference's own output for the same inputs "
+                                          "(tests/golden/bench_golden.json, made from the "
+                                          "reference compiled from source)"}
+                                 if golden else {"note": "no reference digest for P=%d, "
+                                                         "N=%d, %s" % (world, n, args.dtype)}),
             "alt_schedules": alts,
             "device_engines": device_engines,
             "sweep": sweep,

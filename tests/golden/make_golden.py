@@ -333,6 +333,42 @@ def make_scale(only=None):
                    "cases": cases}, f, indent=1)
 
 
+# The N > 1 bench workloads (configs[2] / configs[3] at the driver's node
+# sizes: 256 MiB fp32 per rank at 2, 4 and 8 ranks), so bench.py can check
+# the output of every timed candidate against the reference's own digest.
+# The inputs are SURVEY 8d's synthetic values (oracle_fill kind 0, seed 1234,
+# rank r), which bench.py regenerates on the device.
+BENCH_CASES = [(a, P, 1 << 26, O.FLOAT32) for a in (O.RING_CHUNKED, O.HALVING_DOUBLING)
+               for P in (2, 4, 8)]
+
+
+def make_bench():
+    path = os.path.join(HERE, "bench_golden.json")
+    cases = []
+    for c in BENCH_CASES:
+        algo, P, N, dtype = c
+        ins = [[O.fill(dtype, N, 0, seed=SEED, rank=r)] for r in range(P)]
+        res = O.allreduce(algo, O.SUM, dtype, ins, use_ref=True)
+        first = res[0][0]
+        for r in range(P):
+            assert np.array_equal(res[r][0].view(np.uint8), first.view(np.uint8))
+        cases.append({"name": scale_case_name(c), "algo": algo, "P": P, "N": N,
+                      "dtype": dtype, "op": O.SUM, "seed": SEED, "source": "reference",
+                      "input_sha256": [sha([ins[r][0]]) for r in range(P)],
+                      "output_sha256": sha([first])})
+        print(cases[-1]["name"], cases[-1]["output_sha256"][:16], flush=True)
+        del ins, res, first
+    with open(path, "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py bench",
+                   "source": "oracle/_ref/libgloo_ref.so (the reference compiled from "
+                             "/root/reference by oracle/Makefile), P thread-ranks over "
+                             "TCP loopback",
+                   "inputs": "oracle_fill kind 0 (SURVEY 8d: splitmix64 of seed ^ rank<<40 ^ "
+                             "i, ((h>>40) - 2^23) / 2^23), seed 1234; bench.py regenerates "
+                             "them on the device and checks their digests too",
+                   "cases": cases}, f, indent=1)
+
+
 if __name__ == "__main__":
     if not O.ref_available():
         sys.exit("oracle/_ref/libgloo_ref.so missing: make -C oracle ref")
@@ -347,6 +383,8 @@ if __name__ == "__main__":
         make_allreduce_fn()
     if "scale" in which:  # not in the default set: minutes and ~40 GiB of RAM
         make_scale()
+    if "bench" in which:  # bench.py's N > 1 workloads (256 MiB fp32, P = 2, 4, 8)
+        make_bench()
     if "scale5" in which:  # cfg5 alone (1 GiB per rank, 8 ranks)
         make_scale(CFG5_CASES)
     print("done")

@@ -162,3 +162,40 @@ def test_transport_health_shared_gpu_rehearsal_is_not_an_error():
                                 "device_kernels": 0, "bytes": 1, "host_folds": 0}}
     status, err = bench.transport_health([[_info(True)], [_info(True)]], [st, st])
     assert err is None and not status["ranks_on_distinct_gpus"]
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f16", "bf16"])
+def test_splitmix_fill_matches_oracle_generator(dtype):
+    """bench.py regenerates SURVEY 8d's inputs in torch (int64 with masked
+    shifts); they must be the oracle generator's bits, or the reference
+    digests in tests/golden/bench_golden.json could never match."""
+    import numpy as np
+    from oracle import oracle as O
+    code = {"f32": O.FLOAT32, "f16": O.FLOAT16, "bf16": O.BFLOAT16}[dtype]
+    for rank in (0, 1, 5):
+        n = 70001
+        t = bench.splitmix_fill(torch, n, dtype, "cpu", bench.SEED, rank, chunk=20000)
+        got = t.view(torch.int16 if t.element_size() == 2 else torch.int32).numpy()
+        exp = O.fill(code, n, 0, seed=bench.SEED, rank=rank)
+        assert np.array_equal(got.view(np.uint8), exp.view(np.uint8))
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_reference_cases_for_the_bench_workload(world):
+    """The N > 1 default workload (256 MiB fp32 per rank) has the reference's
+    digests for both plans, and their recorded input digests are those of
+    the generator bench.py uses (checked on a prefix-independent basis: the
+    full 256 MiB input of rank 1)."""
+    n = (256 << 20) // 4
+    cases = bench.reference_cases(world, n, "f32")
+    assert set(cases) == {"ring_chunked", "halving_doubling"}
+    x = bench.splitmix_fill(torch, n, "f32", "cpu", bench.SEED, 1)
+    assert bench.sha256_of(x) == cases["ring_chunked"]["input_sha256"][1]
+    assert bench.golden_plan("ring_chunked_mesh") == "ring_chunked"
+    assert bench.golden_plan("halving_doubling_system") == "halving_doubling"
+    assert bench.reference_cases(3, n, "f32") == {}
+
+
+def test_reference_cases_cfg5():
+    cases = bench.reference_cases(8, 1 << 29, "f16")
+    assert set(cases) == {"ring_chunked"}
