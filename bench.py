@@ -371,7 +371,7 @@ def cold_rate(torch, gloo_amd, n, dtype, dev, stream, steps, pairs=4):
             "us_per_launch": round(t * 1e6, 2), "pairs": pairs}
 
 
-def multidev_check(torch, timeout=240):
+def multidev_check(torch, timeout=120):
     """SURVEY 8f #4 on hardware: one rank's pointers on several GPUs
     (tools/multidev_check.py), run as a child process -- before this process
     touches a GPU -- so that a failure there cannot take the headline
@@ -1090,6 +1090,20 @@ def bench_multi(args):
             failed[other] = err or "failed on another rank"
             continue
         ta, sent_a = got
+        gc = golden.get(golden_plan(other))
+        if gc is not None and gin:
+            # one run on fresh inputs: its output against the reference's digest
+            def digest_run():
+                buf.copy_(src)
+                torch.cuda.synchronize()
+                alg = make_alg(gloo_amd, ctx, buf, other)
+                alg.run()
+                torch.cuda.synchronize()
+                alg.close()
+                return sha256_of(buf) == gc["output_sha256"]
+            match, err = attempt(other + " digest", digest_run)
+            if agreed(err is None):
+                REFDIG[other] = match
         lm = busiest_link_bytes(gloo_amd, other, rank, world, n, es)
         eng = ENGINES.get(other)
         alts[other] = {"value": round(world * S / ta / 1e9, 3),

@@ -379,9 +379,17 @@ class HipPlanExecutor : public Algorithm {
   static constexpr int kEngineSteps = 0, kEngineOneShot = 1, kEngineTwoShot = 2,
                        kEngineDevSteps = 3;
   // Whether device-driven engines can run on this context: GLOO_AMD_ONESHOT
-  // (0 = never, 1 = always), by default when no two ranks are threads sharing
-  // one device (their kernels might not be co-resident).  P <= 8.
+  // (0 = never, 1 = always), by default when every rank has a GPU of its
+  // own, or ranks that share one are processes whose hardware queues fit
+  // kSharedQueueBudget (their kernels must all run at once).  P <= 8.
   static bool deviceEnginesAvailable(const Context& ctx);
+  // Processes sharing one GPU get the device engines by default only while
+  // ranks-on-the-GPU x (hwQueuesPerProcess() + 1) stays within this many
+  // hardware queues, leaving room for one more process's (measured on one
+  // MI355X with a busy parent process: 2x4, 3x4, 4x4, 5x2, 6x2, 8x1
+  // co-schedule; 8x2 and 8x4 time-slice: tools/scratch/queue_oversub.py).
+  static constexpr int kSharedQueueBudget = 20;
+  static int hwQueuesPerProcess();
   // Override for algorithms created afterwards: 0 = never, 1 = always
   // (caller guarantees co-residency), -1 = automatic (the default).
   static void setDeviceEngines(int mode);

@@ -120,11 +120,31 @@ void HipPlanExecutor::setDeviceEngines(int mode) {
   g_device_engines.store(mode < 0 ? -1 : (mode > 0 ? 1 : 0));
 }
 
+// Hardware queues one process opens (HIP's GPU_MAX_HW_QUEUES, default 4).
+int HipPlanExecutor::hwQueuesPerProcess() {
+  const char* e = std::getenv("GPU_MAX_HW_QUEUES");
+  const int n = e != nullptr ? std::atoi(e) : 0;
+  return n > 0 ? n : 4;
+}
+
 bool HipPlanExecutor::deviceEnginesAvailable(const Context& ctx) {
   if (ctx.size < 2 || ctx.size > glx::kOsMaxRanks) return false;
   const int mode = g_device_engines.load();
   if (mode >= 0) return mode == 1;
-  return !ctx.ranksShareDevice();
+  // The device engines' kernels wait on each other, so every rank's kernel
+  // must be running at once.  One rank per GPU: always.  Threads of one
+  // process sharing a GPU: never (their launches may serialise).  Processes
+  // sharing a GPU: only while all their hardware queues fit what the GPU's
+  // scheduler maps at once; beyond that it time-slices the queues and every
+  // dependent step waits for a rotation (8 processes x 4 queues on one
+  // MI355X: ~170 ms per 1-element allreduce, 8 x 2: ~60 ms, 8 x 1 and
+  // 4 x 4: < 1 ms; the suite's P=8 test timed out at 20 s: DESIGN.md 9,
+  // tools/scratch/queue_oversub.py, profiles/r7e_*, r7g_queue_sweep.txt).
+  if (ctx.maxRanksPerDevice() == 1) return true;
+  if (ctx.ranksShareDevice()) return false;
+  // each process: its hardware queues plus an allowance of one (the
+  // measurements need it; 8 x 2 time-slices although 4 x 4 does not)
+  return ctx.maxRanksPerDevice() * (hwQueuesPerProcess() + 1) <= kSharedQueueBudget;
 }
 
 // The inputs are the same on every rank, so every rank makes the same choice

@@ -177,3 +177,17 @@ def run_ranks(P, fn, timeout=120):
         if e is not None:
             raise e
     return results
+
+
+def rank_env(P):
+    """Environment of P rank processes sharing the box's one GPU.  Device
+    engines need every rank's kernel running at once; the GPU's scheduler
+    maps a bounded number of hardware queues and time-slices the rest, so
+    above 4 ranks each process keeps to one queue (the product's default
+    budget, HipPlanExecutor::kSharedQueueBudget: ranks x (queues + 1) <= 20;
+    8 ranks x 2 queues measured time-sliced, profiles/r7g_queue_sweep.txt)."""
+    import os
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    if P > 4:
+        env["GPU_MAX_HW_QUEUES"] = "1"
+    return env

@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 from helpers import (case_inputs, check_against_golden, fn_case_buffers,
-                     load_allreduce_fn_golden, run_ranks, same_bits)
+                     load_allreduce_fn_golden, rank_env, run_ranks, same_bits)
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -222,7 +222,7 @@ WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "mp_worker.py"
 def test_multiprocess_ipc(algo):
     P = 3
     with tempfile.TemporaryDirectory() as d:
-        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        env = rank_env(P)
         procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), algo],
                                   env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
                  for r in range(P)]

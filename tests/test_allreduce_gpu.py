@@ -13,7 +13,7 @@ import time
 import numpy as np
 import pytest
 
-from helpers import case_inputs, check_against_golden, load_allreduce_golden, run_ranks
+from helpers import case_inputs, check_against_golden, load_allreduce_golden, rank_env, run_ranks
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -358,7 +358,7 @@ def test_multiprocess_ipc(algo):
     receive regions shared with hipIpcGetMemHandle/hipIpcOpenMemHandle."""
     P = 3
     with tempfile.TemporaryDirectory() as d:
-        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        env = rank_env(P)
         procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), algo],
                                   env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
                  for r in range(P)]
@@ -388,7 +388,7 @@ def test_device_engine_multiprocess(P, mode):
     dtype/op, device and host buffers, class and function style, repeated
     runs, ranges left empty at small sizes (mp_worker.py)."""
     with tempfile.TemporaryDirectory() as d:
-        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        env = rank_env(P)
         procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), mode],
                                   env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
                  for r in range(P)]
@@ -401,10 +401,13 @@ def test_device_engine_multiprocess(P, mode):
                     q.kill()
                 raise
             outs.append(o.decode(errors="replace"))
+        # every rank's output on a failure: a rank's own timeout report says
+        # which step and flag it waited for, and only all of them together
+        # show where a cycle of waits closed
+        every = "\n".join("---- rank %d (rc %s) ----\n%s" % (r, p.returncode, outs[r])
+                          for r, p in enumerate(procs))
         for r, p in enumerate(procs):
-            print(outs[r])
-            assert p.returncode == 0, "rank %d failed:\n%s" % (r, outs[r])
-            assert "OK" in outs[r]
+            assert p.returncode == 0 and "OK" in outs[r], "rank %d failed:\n%s" % (r, every)
 
 
 @pytest.mark.parametrize("P,engine,when", [(2, "host", "idle"), (3, "host", "mid"),
@@ -420,7 +423,7 @@ def test_peer_killed_raises_io_exception(P, engine, when):
     latter stop their kernels' waits through the status word.  Survivors
     then close cleanly."""
     with tempfile.TemporaryDirectory() as d:
-        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        env = rank_env(P)
         procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P),
                                    "killpeer:%s:%s" % (engine, when)],
                                   env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
@@ -463,7 +466,7 @@ def test_device_engine_variants(mode, knob):
     k, v = knob.split("=")
     P = 3
     with tempfile.TemporaryDirectory() as d:
-        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        env = rank_env(P)
         env[k] = v
         procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), mode],
                                   env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
@@ -493,7 +496,7 @@ def test_link_probe_multiprocess(P):
     allreduce on the same context afterwards (the probe's blocks went back to
     the pool)."""
     with tempfile.TemporaryDirectory() as d:
-        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        env = rank_env(P)
         procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), "linkprobe"],
                                   env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
                  for r in range(P)]
@@ -520,7 +523,7 @@ def test_algorithm_churn_multiprocess(P):
     peers may still be finishing, so this checks the drain-before-reuse and
     pooling rules: bit-exact results, no fd growth."""
     with tempfile.TemporaryDirectory() as d:
-        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        env = rank_env(P)
         procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), "churn"],
                                   env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
                  for r in range(P)]
@@ -544,7 +547,7 @@ def test_device_engine_timeout_raises_io_exception():
     context timeout (every wave exits), and run() raises IoException."""
     P = 2
     with tempfile.TemporaryDirectory() as d:
-        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        env = rank_env(P)
         procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), "devtimeout"],
                                   env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
                  for r in range(P)]
