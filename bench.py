@@ -270,9 +270,11 @@ def reference_cases(world, n, dtype):
 
 
 def sha256_of(t):
+    """SHA-256 of a tensor's bytes (as the golden fixtures hash numpy arrays)."""
     import hashlib
+    import torch
     h = hashlib.sha256()
-    h.update(t.contiguous().view(-1).view(__import__("torch").uint8).cpu().numpy().tobytes())
+    h.update(t.contiguous().view(-1).view(torch.uint8).cpu().numpy().tobytes())
     return h.hexdigest()
 
 
@@ -910,7 +912,8 @@ def north_star_block(S, world, t, p50, engine, hbm_bytes):
                     "is link_frac >= 0.8"}
 
 
-def agreed_inputs(torch, dist, ok):
+def all_ok(torch, dist, ok):
+    """True on every rank iff `ok` is true on every rank."""
     flag = torch.tensor([0 if ok else 1], dtype=torch.int32)
     dist.all_reduce(flag)
     return int(flag.item()) == 0
@@ -943,7 +946,7 @@ def bench_multi(args):
     if golden:
         mine = sha256_of(src)
         gin = all(mine == c["input_sha256"][rank] for c in golden.values())
-        if not agreed_inputs(torch, dist, gin):
+        if not all_ok(torch, dist, gin):
             gin = False
     store = gloo_amd.rendezvous.PrefixStore(
         "gloo_amd_bench", gloo_amd.rendezvous.TorchStore(dist.distributed_c10d._get_default_store()))
@@ -964,9 +967,7 @@ def bench_multi(args):
     # A failure on any rank (a timeout, a HIP error) is agreed on by all, so
     # every rank takes the same branch; the JSON line names it.
     def agreed(ok):
-        flag = torch.tensor([0 if ok else 1], dtype=torch.int32)
-        dist.all_reduce(flag)
-        return int(flag.item()) == 0
+        return all_ok(torch, dist, ok)
 
     def attempt(what, fn):
         try:
