@@ -1,0 +1,85 @@
+"""GPU: randomized shapes (hypothesis, fixed seed, bounded example counts)
+against the oracle, bit for bit -- off the parametrized grids:
+
+* the reduce kernel (glx_reduce, gloo/math.h:15-73) with random lengths,
+  element offsets of a, b and c chosen independently (so the three streams
+  share a 16-byte phase, or do not and take the scalar path), in place or
+  into a third buffer;
+* the class allreduce on thread-ranks (host-issued steps: ranks sharing the
+  box's one GPU) with random rank counts, lengths, pointer counts, dtypes,
+  ops and schedules."""
+import numpy as np
+import pytest
+
+hyp = pytest.importorskip("hypothesis")
+from hypothesis import HealthCheck, given, seed, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+from helpers import case_inputs, same_bits  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from test_allreduce_gpu import MESH, gpu_allreduce  # noqa: E402
+from test_reduce_gpu import ALL_DTYPES, ALL_OPS, assert_same, from_dev, to_dev  # noqa: E402
+
+SETTINGS = dict(deadline=None, derandomize=True,
+                suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+
+
+@settings(max_examples=150, **SETTINGS)
+@seed(31)
+@given(dtype=st.sampled_from(ALL_DTYPES), op=st.sampled_from(ALL_OPS),
+       n=st.one_of(st.integers(1, 40), st.integers(41, 300000)),
+       offs=st.tuples(st.integers(0, 17), st.integers(0, 17), st.integers(0, 17)),
+       inplace=st.booleans())
+def test_reduce_kernel_random_offsets(dtype, op, n, offs, inplace):
+    import ctypes
+    import gloo_amd
+    from gloo_amd import _lib
+    es = np.dtype(O.NP_DTYPE[dtype]).itemsize
+    a = O.fill(dtype, n, 0, seed=n, rank=0)
+    b = O.fill(dtype, n, 0, seed=n, rank=1)
+    c0 = O.fill(dtype, n, 0, seed=n, rank=2)
+    oa, ob, oc = offs
+    if inplace:
+        oc = oa
+    pad = 32
+    bufs = {}
+    for key, x, o in (("a", a, oa), ("b", b, ob), ("c", c0, oc)):
+        bufs[key] = to_dev(np.concatenate([np.zeros(o, x.dtype), x, np.zeros(pad, x.dtype)]),
+                           dtype)
+    pa = bufs["a"].data_ptr() + oa * es
+    pb = bufs["b"].data_ptr() + ob * es
+    C = bufs["a"] if inplace else bufs["c"]
+    pc = C.data_ptr() + oc * es
+    rc = _lib.lib.glx_reduce(op, dtype, ctypes.c_void_p(pc), ctypes.c_void_p(pa),
+                             ctypes.c_void_p(pb), n,
+                             ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    gloo_amd.errors.check(rc, "glx_reduce")
+    torch.cuda.synchronize()
+    full = from_dev(C, dtype)
+    assert np.all(full[:oc] == 0) and np.all(full[oc + n:] == 0), "wrote outside [c, c+n)"
+    exp = O.reduce(op, dtype, a, b) if inplace else O.reduce(op, dtype, a, b, inplace=False, c=c0)
+    assert_same(full[oc:oc + n], exp, dtype, op)
+
+
+ALGOS = [O.RING_CHUNKED, O.HALVING_DOUBLING, MESH]
+
+
+@settings(max_examples=40, **SETTINGS)
+@seed(32)
+@given(algo=st.sampled_from(ALGOS), P=st.integers(1, 9),
+       N=st.one_of(st.integers(0, 64), st.integers(65, 200000)), nptrs=st.integers(1, 3),
+       dtype=st.sampled_from([O.FLOAT32, O.FLOAT16, O.BFLOAT16, O.INT32, O.FLOAT64]),
+       op=st.sampled_from(ALL_OPS))
+def test_allreduce_random_shapes(algo, P, N, nptrs, dtype, op):
+    ins = case_inputs(P, N, dtype, nptrs, 0, seed=P * 7 + N % 13)
+    out = gpu_allreduce(algo, op, dtype, ins, runs=2)
+    ref_algo = O.HALVING_DOUBLING if algo == O.HALVING_DOUBLING else O.RING_CHUNKED
+    exp = O.allreduce(ref_algo, op, dtype, ins)
+    for r in range(P):
+        for i in range(nptrs):
+            assert same_bits(out[r][i], exp[r][i]), (r, i)
