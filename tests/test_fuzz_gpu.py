@@ -29,7 +29,7 @@ SETTINGS = dict(deadline=None, derandomize=True,
                 suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
 
 
-@settings(max_examples=150, **SETTINGS)
+@settings(max_examples=600, **SETTINGS)
 @seed(31)
 @given(dtype=st.sampled_from(ALL_DTYPES), op=st.sampled_from(ALL_OPS),
        n=st.one_of(st.integers(1, 40), st.integers(41, 300000)),
@@ -69,7 +69,7 @@ def test_reduce_kernel_random_offsets(dtype, op, n, offs, inplace):
 ALGOS = [O.RING_CHUNKED, O.HALVING_DOUBLING, MESH]
 
 
-@settings(max_examples=40, **SETTINGS)
+@settings(max_examples=200, **SETTINGS)
 @seed(32)
 @given(algo=st.sampled_from(ALGOS), P=st.integers(1, 9),
        N=st.one_of(st.integers(0, 64), st.integers(65, 200000)), nptrs=st.integers(1, 3),
