@@ -1264,6 +1264,19 @@ def log(msg):
     sys.stderr.flush()
 
 
+def failure_line(args, world, exc):
+    """The N > 1 JSON line when no candidate could be measured."""
+    return {"metric": metric_name(args.dtype), "value": None, "unit": "GB/s",
+            "n_gpus": world, "steps": args.steps or 20, "warmup": args.warmup,
+            "ms_per_step": None, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
+            "config": {"workload": "allreduce_%s_%s_%dMiB_per_rank" % (
+                args.algo, {"f32": "fp32"}.get(args.dtype, args.dtype), args.size_mib),
+                "parallelism": "dp%d" % world},
+            "error": "%s: %s" % (type(exc).__name__, str(exc)[:600]),
+            "bench_wall_s": round(time.time() - T_START, 2)}
+
+
 def main():
     args = parse()
     import faulthandler
@@ -1272,7 +1285,14 @@ def main():
     faulthandler.dump_traceback_later(args.watchdog, exit=True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
-        res = bench_multi(args)
+        try:
+            res = bench_multi(args)
+        except Exception as e:  # noqa: BLE001 - the line says what failed
+            # a run that cannot measure anything still reports why, on the
+            # one line the driver reads, and fails
+            if int(os.environ.get("RANK", "0")) == 0:
+                print(json.dumps(failure_line(args, world, e)), flush=True)
+            raise
     else:
         if args.gpus > 1:
             sys.exit("bench.py --gpus N>1 must be launched with torch.distributed.run "

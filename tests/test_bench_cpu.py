@@ -199,3 +199,15 @@ def test_reference_cases_for_the_bench_workload(world):
 def test_reference_cases_cfg5():
     cases = bench.reference_cases(8, 1 << 29, "f16")
     assert set(cases) == {"ring_chunked"}
+
+
+def test_failure_line_is_one_json_line_with_the_error():
+    import argparse
+    import json
+    ns = argparse.Namespace(dtype="f32", steps=None, warmup=5, algo="ring_chunked", size_mib=256)
+    line = bench.failure_line(ns, 8, RuntimeError("every candidate failed: {...}"))
+    s = json.dumps(line)
+    assert "\n" not in s
+    d = json.loads(s)
+    assert d["value"] is None and d["n_gpus"] == 8 and "every candidate failed" in d["error"]
+    assert d["metric"] == bench.metric_name("f32")
