@@ -752,3 +752,20 @@ def test_transport_stats_name_the_mechanism():
         st, sent, eng = stats[(r, "kernel")]
         assert st["kernel_copies"] > 0 and st["device_copies"] == 0
         assert st["bytes"] == 3 * sent
+
+
+def test_multidev_check_script_on_one_device():
+    """tools/multidev_check.py -- what bench.py's N = 1 line runs on a box
+    with several GPUs -- in its self-test mode: the same
+    cases with every "device" being device 0, so the script's plumbing and
+    checks are exercised on the one-GPU boxes too."""
+    import json
+    import subprocess
+    import sys
+    script = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                          "tools", "multidev_check.py")
+    p = subprocess.run([sys.executable, script, "--same-device"], capture_output=True,
+                       text=True, timeout=240)
+    assert p.returncode == 0, p.stdout + p.stderr
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["ok"] is True and len(d["cases"]) == 6, d

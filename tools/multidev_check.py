@@ -21,6 +21,8 @@ import threading
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# self-test of this script on a one-GPU box: every "device" is device 0
+SAME_DEVICE = len(sys.argv) > 1 and sys.argv[1] == "--same-device"
 sys.path.insert(0, ROOT)
 
 
@@ -30,9 +32,10 @@ def run_case(torch, gloo_amd, algo, k, n, dtype, seed):
     ins = [[torch.randint(-1000, 1000, (n,), generator=g, dtype=torch.int64) for _ in range(k)]
            for _ in range(P)]
     expect = sum(x for row in ins for x in row)
-    bufs = [[ins[r][i].to(dtype).to("cuda:%d" % i) for i in range(k)] for r in range(P)]
+    dev = (lambda i: 0) if SAME_DEVICE else (lambda i: i)
+    bufs = [[ins[r][i].to(dtype).to("cuda:%d" % dev(i)) for i in range(k)] for r in range(P)]
     for d in range(k):
-        torch.cuda.synchronize(d)
+        torch.cuda.synchronize(dev(d))
     store = gloo_amd.rendezvous.HashStore()
     errors = [None] * P
 
@@ -47,7 +50,7 @@ def run_case(torch, gloo_amd, algo, k, n, dtype, seed):
             for _ in range(2):  # the second run reuses the algorithm's state
                 for i in range(k):
                     bufs[r][i].copy_(ins[r][i].to(dtype))
-                    torch.cuda.synchronize(i)
+                    torch.cuda.synchronize(dev(i))
                 alg.run()
             alg.close()
         except BaseException as e:  # noqa: BLE001 - reported
@@ -77,7 +80,9 @@ def run_case(torch, gloo_amd, algo, k, n, dtype, seed):
 def main():
     import torch
     ndev = torch.cuda.device_count()
-    if ndev < 2:
+    if SAME_DEVICE:
+        ndev = 3
+    elif ndev < 2:
         print(json.dumps({"devices": ndev, "ok": None, "skipped": "fewer than 2 GPUs"}))
         return 0
     import gloo_amd
