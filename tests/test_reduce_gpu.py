@@ -146,3 +146,33 @@ def test_reduce_n_left_fold():
         gloo_amd.math.reduce_n(gloo_amd.ReductionType.SUM, ts[0], ts)
         torch.cuda.synchronize()
         assert_same(from_dev(ts[0], dtype), exp, dtype, O.SUM)
+
+
+def test_bf16_against_torch_rounding():
+    """bfloat16 has no reference type (parity unpinned against gloo); as an
+    independent restatement of the same rule -- widen, op in fp32, round to
+    nearest even once -- torch's own fp32 -> bf16 conversion must give the
+    kernel's bits for sum and product, and torch.where the operand choice of
+    max / min (gloo/math.h:51,66 order), on 1M random values incl. specials."""
+    import gloo_amd
+    g = torch.Generator(device="cuda").manual_seed(17)
+    n = 1 << 20
+    a = (torch.randn(n, device="cuda", generator=g) * 64).to(torch.bfloat16)
+    b = (torch.randn(n, device="cuda", generator=g) * 64).to(torch.bfloat16)
+    special = torch.tensor([0.0, -0.0, float("inf"), -float("inf"), 1e-40, -3e38, 3e38],
+                           device="cuda").to(torch.bfloat16)
+    a[:special.numel()] = special
+    b[:special.numel()] = special.flip(0)
+    af, bf = a.float(), b.float()
+    exp = {gloo_amd.ReductionType.SUM: (af + bf).to(torch.bfloat16),
+           gloo_amd.ReductionType.PRODUCT: (af * bf).to(torch.bfloat16),
+           gloo_amd.ReductionType.MAX: torch.where(af < bf, b, a),
+           gloo_amd.ReductionType.MIN: torch.where(bf < af, b, a)}
+    for op, e in exp.items():
+        c = torch.empty_like(a)
+        gloo_amd.math.reduce(op, c, a, b)
+        torch.cuda.synchronize()
+        got, want = c.view(torch.int16), e.view(torch.int16)
+        nan = torch.isnan(e.float())
+        assert torch.equal(torch.isnan(c.float()), nan)
+        assert torch.equal(got[~nan], want[~nan]), op
