@@ -19,6 +19,8 @@ algo: ring_chunked | halving_doubling | ring_chunked_mesh (class algorithms)
       every engine's output SHA-256 against tests/golden/scale_golden.json)
       linkprobe (the measured-link probe through the product's IPC path, and
       every peer's connect-time view; then an allreduce on the same context)
+      engine_choice (which engine the automatic policy picks on the shared
+      GPU under this process's GPU_MAX_HW_QUEUES, and one exact run)
       big:fast | big:plain (the ring on the plan kernel over MORE than 2 GiB per
       rank, P = 2, the given stream policy: every 32-bit store offset the
       write-through path could form is exceeded; exact at P = 2 since fp32
@@ -59,6 +61,8 @@ def main():
         return run_big(store_dir, rank, size, algo[len("big:"):])
     if algo == "linkprobe":
         return run_linkprobe(store_dir, rank, size)
+    if algo == "engine_choice":
+        return run_engine_choice(store_dir, rank, size)
     if algo.startswith("fn_"):
         return run_fn(store_dir, rank, size, algo, N)
     code = O.HALVING_DOUBLING if algo == "halving_doubling" else O.RING_CHUNKED
@@ -627,6 +631,35 @@ def run_linkprobe(store_dir, rank, size):
     ctx.close()
     if bad:
         print("MISMATCH rank", rank, bad[:10])
+        sys.exit(1)
+    print("OK")
+
+
+def run_engine_choice(store_dir, rank, size):
+    """The engine the automatic policy gives the ring on a shared GPU under
+    this process's GPU_MAX_HW_QUEUES (HipPlanExecutor::deviceEnginesAvailable:
+    processes sharing a GPU get the device engines only within the
+    hardware-queue budget), and one exact run of it."""
+    import torch
+
+    import gloo_amd
+    store = gloo_amd.rendezvous.FileStore(store_dir)
+    ctx = gloo_amd.rendezvous.Context(rank, size, 0)
+    ctx.setTimeout(60)
+    ctx.connectFullMesh(store)
+    buf = torch.full((4099,), float(rank + 1), device="cuda")
+    alg = gloo_amd.AllreduceRingChunked(ctx, [buf], schedule="ring")
+    alg.run()
+    torch.cuda.synchronize()
+    ok = bool((buf == size * (size + 1) / 2).all().item())
+    print("ENGINE rank %d %s" % (rank, alg.engine()), flush=True)
+    alg.close()
+    store.set("done/%d" % rank, b"1")
+    for r in range(size):
+        store.get("done/%d" % r, timeout_ms=60000)
+    ctx.close()
+    if not ok:
+        print("MISMATCH rank", rank)
         sys.exit(1)
     print("OK")
 

@@ -769,3 +769,32 @@ def test_multidev_check_script_on_one_device():
     assert p.returncode == 0, p.stdout + p.stderr
     d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert d["ok"] is True and len(d["cases"]) == 6, d
+
+
+@pytest.mark.parametrize("P,queues,engine", [(8, "4", "steps"), (8, "1", "devsteps"),
+                                             (4, "4", "devsteps")])
+def test_device_engines_respect_the_shared_gpu_queue_budget(P, queues, engine):
+    """Processes sharing one GPU get the device engines only while ranks x
+    (GPU_MAX_HW_QUEUES + 1) <= 20 (beyond the GPU's 24 user
+    queues the scheduler time-slices them and every dependent step waits for
+    a rotation).  8 x 4 must fall back to host-issued steps; 8 x 1 and 4 x 4
+    keep the plan kernel; every rank agrees and the result is exact."""
+    with tempfile.TemporaryDirectory() as d:
+        env = dict(rank_env(P), GPU_MAX_HW_QUEUES=queues)
+        procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), "engine_choice"],
+                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                 for r in range(P)]
+        outs = []
+        for p in procs:
+            try:
+                o, _ = p.communicate(timeout=240)
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+            outs.append(o.decode(errors="replace"))
+        every = "\n".join("---- rank %d (rc %s) ----\n%s" % (r, p.returncode, outs[r])
+                          for r, p in enumerate(procs))
+        for r, p in enumerate(procs):
+            assert p.returncode == 0 and "OK" in outs[r], "rank %d failed:\n%s" % (r, every)
+            assert "ENGINE rank %d %s" % (r, engine) in outs[r], every
