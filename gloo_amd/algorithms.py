@@ -183,12 +183,15 @@ class Algorithm:
     def done_ranges(self):
         """[(off, n)] element ranges whose results are already in host memory,
         in completion order."""
-        k = lib.glx_algorithm_done_ranges(self._h, None, 0)
-        if k < 0:
-            check(_lib.ERR_INVALID, "done_ranges")
-        buf = (ctypes.c_int64 * max(2 * k, 1))()
-        k = lib.glx_algorithm_done_ranges(self._h, buf, k)
-        return [(buf[2 * i], buf[2 * i + 1]) for i in range(k)]
+        cap = 0
+        while True:  # ranges keep completing while a run is in flight
+            buf = (ctypes.c_int64 * max(2 * cap, 2))()
+            k = lib.glx_algorithm_done_ranges(self._h, buf, cap)
+            if k < 0:
+                check(_lib.ERR_INVALID, "done_ranges")
+            if k <= cap:
+                return [(buf[2 * i], buf[2 * i + 1]) for i in range(k)]
+            cap = 2 * k
 
     def bytes_sent(self):
         """Bytes this rank moves over peer links per run()."""

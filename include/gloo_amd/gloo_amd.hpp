@@ -270,12 +270,18 @@ class DeviceAllreduce : public Algorithm {
   void runFed() { check(glx_algorithm_run_fed(a_), "runFed"); }
   void feed(int64_t off, int64_t len) { check(glx_algorithm_feed(a_, off, len), "feed"); }
   std::vector<std::pair<int64_t, int64_t>> doneRanges() const {
-    const int64_t n = glx_algorithm_done_ranges(a_, nullptr, 0);
-    std::vector<int64_t> v((size_t)std::max<int64_t>(2 * n, 2));
-    const int64_t k = glx_algorithm_done_ranges(a_, v.data(), n);
-    std::vector<std::pair<int64_t, int64_t>> out;
-    for (int64_t i = 0; i < k && i < n; i++) out.emplace_back(v[2 * i], v[2 * i + 1]);
-    return out;
+    int64_t cap = 0;
+    for (;;) {  // ranges keep completing while a run is in flight
+      std::vector<int64_t> v((size_t)std::max<int64_t>(2 * cap, 2));
+      const int64_t k = glx_algorithm_done_ranges(a_, v.data(), cap);
+      check(k < 0 ? GLX_ERR_INVALID : GLX_OK, "doneRanges");
+      if (k <= cap) {
+        std::vector<std::pair<int64_t, int64_t>> out;
+        for (int64_t i = 0; i < k; i++) out.emplace_back(v[2 * i], v[2 * i + 1]);
+        return out;
+      }
+      cap = 2 * k;
+    }
   }
   // record `ev` at the end of the last run's work (streams[0] with streams)
   void record(Event& ev) { check(glx_algorithm_record(a_, ev.handle()), "record"); }

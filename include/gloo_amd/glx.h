@@ -350,7 +350,9 @@ int glx_algorithm_run(glx_algorithm* alg);
  *                             in host memory already, in completion order
  *                             (the ring returns chunk after chunk), for a
  *                             caller that streams results back out; writes at
- *                             most cap pairs, returns their number or -1.
+ *                             most cap pairs and returns how many ranges are
+ *                             done (more than cap when more completed; call
+ *                             again with a larger buffer), or -1.
  */
 int glx_algorithm_run_fed(glx_algorithm* alg);
 int glx_algorithm_feed(glx_algorithm* alg, int64_t off, int64_t len);
