@@ -69,7 +69,10 @@ def socket_feeder(alg, buf, data, order="in_order"):
     return ts
 
 
-def fed_allreduce(algo, P, N, dtype=O.FLOAT32, order="in_order", runs=1):
+def fed_allreduce(algo, P, N, dtype=O.FLOAT32, order="in_order", runs=1, poll=None):
+    """poll: per-rank lists that collect done_ranges() snapshots taken by a
+    second thread while the fed runs are in flight (a consumer streaming
+    finished ranges back out, what done_ranges() is for)."""
     import gloo_amd
     ins = case_inputs(P, N, dtype, 1, 0, seed=41)
     store = gloo_amd.rendezvous.HashStore()
@@ -85,11 +88,25 @@ def fed_allreduce(algo, P, N, dtype=O.FLOAT32, order="in_order", runs=1):
             alg = gloo_amd.AllreduceHalvingDoubling(ctx, [bufs[r]], dtype=dt)
         else:
             alg = gloo_amd.AllreduceRingChunked(ctx, [bufs[r]], schedule="ring", dtype=dt)
-        for _ in range(runs):
-            ts = socket_feeder(alg, bufs[r], ins[r][0], order)
-            alg.run_fed()
-            for t in ts:
-                t.join(60)
+        stop = threading.Event()
+
+        def poller():
+            while not stop.is_set():
+                poll[r].append(alg.done_ranges())
+
+        pt = threading.Thread(target=poller, daemon=True) if poll is not None else None
+        if pt is not None:
+            pt.start()
+        try:
+            for _ in range(runs):
+                ts = socket_feeder(alg, bufs[r], ins[r][0], order)
+                alg.run_fed()
+                for t in ts:
+                    t.join(60)
+        finally:
+            stop.set()
+            if pt is not None:
+                pt.join(60)
         done[r] = alg.done_ranges()
         alg.close()
         return True
@@ -148,3 +165,22 @@ def test_unfed_piece_times_out():
     with pytest.raises(gloo_amd.IoException, match="host data"):
         alg.run_fed()
     alg.close()
+
+
+@pytest.mark.parametrize("P", [1, 2, 3])
+def test_done_ranges_polled_while_runs_are_in_flight(P):
+    """A second thread polls done_ranges() without pause during the fed runs:
+    ranges complete between the wrapper's calls into the C ABI (round 3's
+    race), every snapshot must be well-formed ranges inside the
+    buffer, and the final result exact and fully covered."""
+    N = (3 << 20) + 11
+    poll = [[] for _ in range(P)]
+    bufs, done, ins = fed_allreduce("ring_chunked", P, N, runs=2, poll=poll)
+    exp = O.allreduce(O.RING_CHUNKED, O.SUM, O.FLOAT32, ins)
+    for r in range(P):
+        assert same_bits(bufs[r], exp[r][0])
+        assert covered(done[r], N)
+        assert poll[r], "the poller never ran"
+        for snap in poll[r]:
+            for o, n in snap:
+                assert 0 <= o and 0 < n and o + n <= N
