@@ -37,6 +37,15 @@ def set_copy_split(k):
     errors.check(_lib.lib.glx_set_copy_split(int(k)), "set_copy_split")
 
 
+def set_pinned_mirror_limit(nbytes):
+    """Host-memory endpoints of algorithms created afterwards: a pageable
+    buffer larger than `nbytes` (0: no limit, the default) -- or one the
+    runtime cannot pin a whole mirror for -- is staged through an 8 MiB
+    pinned bounce block piece by piece instead of a pinned mirror of its
+    size (glx.h glx_set_pinned_mirror_limit)."""
+    errors.check(_lib.lib.glx_set_pinned_mirror_limit(int(nbytes)), "set_pinned_mirror_limit")
+
+
 def set_copy_engine(engine, blocks=0):
     """Peer copies of algorithms created afterwards: "dma" (hipMemcpyPeerAsync,
     default) or "kernel" (a copy kernel storing over xGMI into the peer's
@@ -87,9 +96,13 @@ def set_device_sync(mode):
 
 
 def set_device_engines(mode):
-    """Device-driven engines (one-shot / two-shot kernels) for algorithms
-    created afterwards: "auto" (default: when no two ranks are threads sharing
-    a device), "off" (host-issued steps only) or "on"."""
+    """Device-driven engines (plan, one-shot and two-shot kernels) for
+    algorithms created afterwards: "auto", "off" (host-issued steps only) or
+    "on".  "auto" (default): always with one rank per GPU; never for threads
+    of one process sharing a GPU; for processes sharing a GPU only while
+    ranks-on-the-GPU x (queues + 1) <= 20, where queues is the largest
+    GPU_MAX_HW_QUEUES any rank's process published at connect (default 4) --
+    every rank decides from the same endpoints."""
     code = {"auto": -1, "off": 0, "on": 1}[mode]
     errors.check(_lib.lib.glx_set_device_engines(code), "set_device_engines")
 

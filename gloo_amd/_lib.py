@@ -41,6 +41,7 @@ SIGNATURES = [
     ("glx_enable_peer", _i, [_i, _i]),
     ("glx_tune_reduce", _i, [_i, _i, _i]),
     ("glx_set_copy_split", _i, [_i]),
+    ("glx_set_pinned_mirror_limit", _i, [_sz]),
     ("glx_device_count", _i, [ctypes.POINTER(_i)]),
     ("glx_hash_store_create", _vp, []),
     ("glx_file_store_create", _vp, [ctypes.c_char_p]),

@@ -12,6 +12,7 @@
 #include "common.h"
 #include "context.h"
 #include "executor.h"
+#include "executor_internal.h"
 #include "host_ops.h"
 #include "kernels.h"
 #include "linkprobe.h"
@@ -230,6 +231,11 @@ int glx_set_device_engines(int mode) {
 int glx_set_copy_split(int k) {
   if (k < 1 || k > 8) return fail(GLX_ERR_INVALID, "glx_set_copy_split: k must be in [1, 8]");
   gloo::HipPlanExecutor::setCopySplit(k);
+  return GLX_OK;
+}
+
+int glx_set_pinned_mirror_limit(size_t bytes) {
+  gloo::exec::setPinnedMirrorLimit(bytes);
   return GLX_OK;
 }
 

@@ -445,6 +445,7 @@ void Context::connectFullMesh(std::shared_ptr<rendezvous::Store> store) {
   putPod<int32_t>(rec, device_);
   putStr(rec, busId_);
   putStr(rec, shm);
+  putPod<int32_t>(rec, hwQueuesOfProcess());
   store_->set("glx/ep/" + std::to_string(rank), rec);
 
   for (int r = 0; r < size; r++) {
@@ -457,6 +458,7 @@ void Context::connectFullMesh(std::shared_ptr<rendezvous::Store> store) {
       p.sameProcess = true;
       p.busId = busId_;
       p.shmName = shm;
+      p.hwQueues = hwQueuesOfProcess();
       continue;
     }
     auto b = store_->get("glx/ep/" + std::to_string(r), timeout_);
@@ -469,6 +471,7 @@ void Context::connectFullMesh(std::shared_ptr<rendezvous::Store> store) {
     std::string bus = rd.str();
     p.busId = bus;
     p.shmName = rd.str();
+    p.hwQueues = rd.pod<int32_t>();
     p.sameProcess = (p.pid == pid);
     if (p.sameProcess) {
       p.localDevice = p.device;
@@ -532,6 +535,21 @@ bool Context::ranksShareDevice() const {
     }
   }
   return false;
+}
+
+// Hardware queues this process opens per device (HIP's GPU_MAX_HW_QUEUES,
+// default 4).  Published in the endpoint record, so every rank decides on
+// the device engines from the same (largest) value.
+int hwQueuesOfProcess() {
+  const char* e = std::getenv("GPU_MAX_HW_QUEUES");
+  const int n = e != nullptr ? std::atoi(e) : 0;
+  return n > 0 ? n : 4;
+}
+
+int Context::maxHwQueues() const {
+  int most = 1;
+  for (const auto& p : peers_) most = std::max(most, p.hwQueues);
+  return most;
 }
 
 int Context::maxRanksPerDevice() const {

@@ -82,8 +82,11 @@ struct PeerEndpoint {
   int canAccessPeer = -1;
   int nativeAtomics = -1;
   std::string shmName;
+  int hwQueues = 4;  // the rank's process's GPU_MAX_HW_QUEUES (default 4)
   std::unique_ptr<ControlBlock> ctl;  // mapped peer control block
 };
+
+int hwQueuesOfProcess();
 
 // What a peer needs to map one of our shared device blocks (published in
 // algorithm records).
@@ -137,6 +140,8 @@ class Context {
   bool ranksShareDevice() const;
   // Largest number of ranks on one GPU (by PCI bus id; equal on every rank).
   int maxRanksPerDevice() const;
+  // the largest GPU_MAX_HW_QUEUES of any rank's process (from the endpoints)
+  int maxHwQueues() const;
   // True when device kernels of this rank write peers' flag words with plain
   // system-scope stores instead of atomic exchanges: some peer sits on
   // another GPU whose link (hipDevP2PAttrNativeAtomicSupported) does not

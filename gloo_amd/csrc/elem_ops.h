@@ -8,6 +8,7 @@
 #include <stdint.h>
 
 #include "common.h"
+#include "kernels.h"
 
 namespace glx {
 namespace {
@@ -39,8 +40,8 @@ __device__ __forceinline__ void st16(v4u* p, v4u v) {
 // store builtin with that cache policy, so the stream is written through a
 // buffer resource over its base (a compiler builtin, not inline asm: the
 // compiler then tracks the store for waitcnts and register hazards).
-// Offsets are 32-bit: a stream must stay below 2 GiB (kWtMaxStream).
-constexpr size_t kWtMaxStream = (size_t(1) << 31) - 16;
+// Offsets are 32-bit: a stream must stay below 2 GiB (kWtMaxStream,
+// kernels.h; the executors enforce it for every workgroup span).
 // p as the compiler can prove wave-uniform (callers pass one value to every
 // lane), so a buffer resource over it stays in SGPRs.
 __device__ __forceinline__ void* uniform_ptr(void* p) {

@@ -248,18 +248,33 @@ class HipPlanExecutor : public Algorithm {
   bool hostFold_ = false;          // several pointers < kOnDeviceThreshold: fold on the host
   char* hostStage_ = nullptr;      // pinned: the host fold's result, staged and returned
   size_t hostStageBytes_ = 0;      // its size (from and back to a process-wide cache)
-  // A host buffer as the copies see it: `user` (the caller's) and `dma`
-  // (what the DMA reads / writes: `user` itself when pinned, else its mirror)
-  struct HostSide {
-    char* user;
-    char* dma;
-  };
-  std::vector<HostSide> hostSources() const;  // H2D sources of the staged buffer
-  std::vector<HostSide> hostDests() const;    // where its final values go back to
+  // A pinned block of the process-wide cache: a whole-buffer mirror, or --
+  // when no mirror of the buffer's size could be pinned (or it exceeds
+  // glx_set_pinned_mirror_limit) -- a bounce block of at most
+  // kBounceBytes that every copy goes through piece by piece, waiting for
+  // each piece (a failed pinned allocation must not fail the op)
   struct PinnedBlock {
     char* p = nullptr;
     size_t bytes = 0;
+    bool bounce = false;
   };
+  // A host buffer as the copies see it: `user` (the caller's) and `dma`
+  // (what the DMA reads / writes: `user` itself when pinned, else its
+  // mirror; null when the copies go through the bounce block `bounce`)
+  struct HostSide {
+    char* user;
+    char* dma;
+    PinnedBlock* bounce;
+  };
+  std::vector<HostSide> hostSources() const;  // H2D sources of the staged buffer
+  std::vector<HostSide> hostDests() const;    // where its final values go back to
+  static HostSide sideOf(char* u, const PinnedBlock* m);
+  // m's mirror for a pageable buffer of `bytes` (or its bounce block)
+  void takeMirror(PinnedBlock& m, size_t bytes);
+  // copies through a bounce block: H2D returns with the last piece in flight
+  // on `s`; D2H returns with every byte in `user`
+  void bounceIn(char* dev, const char* user, size_t n, PinnedBlock& b, hipStream_t s);
+  void bounceOut(char* user, const char* dev, size_t n, PinnedBlock& b, hipStream_t s);
   std::vector<PinnedBlock> ptrMirror_;  // per ptrs_ entry (p == nullptr: pinned)
   PinnedBlock callMirror_[2];           // a function-style call: source, destination
   bool callMirrored_[2] = {false, false};  // the current call uses them
@@ -390,6 +405,7 @@ class HipPlanExecutor : public Algorithm {
   // co-schedule; 8x2 and 8x4 time-slice: tools/scratch/queue_oversub.py).
   static constexpr int kSharedQueueBudget = 20;
   static int hwQueuesPerProcess();
+  void enforceSpan(size_t sliceElems) const;
   // Override for algorithms created afterwards: 0 = never, 1 = always
   // (caller guarantees co-residency), -1 = automatic (the default).
   static void setDeviceEngines(int mode);

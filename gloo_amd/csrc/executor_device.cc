@@ -121,11 +121,7 @@ void HipPlanExecutor::setDeviceEngines(int mode) {
 }
 
 // Hardware queues one process opens (HIP's GPU_MAX_HW_QUEUES, default 4).
-int HipPlanExecutor::hwQueuesPerProcess() {
-  const char* e = std::getenv("GPU_MAX_HW_QUEUES");
-  const int n = e != nullptr ? std::atoi(e) : 0;
-  return n > 0 ? n : 4;
-}
+int HipPlanExecutor::hwQueuesPerProcess() { return hwQueuesOfProcess(); }
 
 bool HipPlanExecutor::deviceEnginesAvailable(const Context& ctx) {
   if (ctx.size < 2 || ctx.size > glx::kOsMaxRanks) return false;
@@ -143,8 +139,10 @@ bool HipPlanExecutor::deviceEnginesAvailable(const Context& ctx) {
   if (ctx.maxRanksPerDevice() == 1) return true;
   if (ctx.ranksShareDevice()) return false;
   // each process: its hardware queues plus an allowance of one (the
-  // measurements need it; 8 x 2 time-slices although 4 x 4 does not)
-  return ctx.maxRanksPerDevice() * (hwQueuesPerProcess() + 1) <= kSharedQueueBudget;
+  // measurements need it; 8 x 2 time-slices although 4 x 4 does not).  The
+  // largest queue count any rank published, so ranks launched with
+  // different GPU_MAX_HW_QUEUES still choose alike.
+  return ctx.maxRanksPerDevice() * (ctx.maxHwQueues() + 1) <= kSharedQueueBudget;
 }
 
 // The inputs are the same on every rank, so every rank makes the same choice
@@ -260,6 +258,15 @@ size_t HipPlanExecutor::maxSlices(int kernel) const {
   return g;
 }
 
+// A workgroup's span of one segment: its stores into a peer's slot go through
+// a write-through buffer resource with 32-bit offsets (xgmi_kernels.hip
+// VecOut), so the span must stay below kWtMaxStream.  Spans are
+// slice elements; a slice over 2 GiB would need a buffer over 1 TiB per rank.
+void HipPlanExecutor::enforceSpan(size_t sliceElems) const {
+  GLX_ENFORCE(sliceElems * esize_ <= glx::kWtMaxStream, "device engine: a workgroup span of ",
+              sliceElems * esize_, " bytes exceeds the write-through stores' 2 GiB offsets");
+}
+
 void HipPlanExecutor::setupOneShot() {
   const int P = contextSize_;
   const glx::DeviceLayout d =
@@ -271,6 +278,7 @@ void HipPlanExecutor::setupOneShot() {
   p.slice = (size_t)d.slice;
   p.G = d.G;
   p.njobs = d.njobs;
+  enforceSpan((size_t)d.slice);
   for (int q = 0; q < d.njobs; q++) {
     p.jobOff[q] = (size_t)d.jobOff[q];
     p.jobLen[q] = (size_t)d.jobLen[q];
@@ -298,6 +306,7 @@ void HipPlanExecutor::setupTwoShot() {
   }
   p.slice = (size_t)d.slice;
   p.G = d.G;
+  enforceSpan((size_t)d.slice);
   if (devTrace()) {
     const size_t n = (size_t)std::max<int64_t>(1, maxSlices(1)) * glx::kTsTrace;
     GLX_HIP_CHECK(hipHostMalloc((void**)&trace_, n * sizeof(uint64_t), hipHostMallocDefault));
@@ -317,6 +326,7 @@ void HipPlanExecutor::setupTwoShot() {
 void HipPlanExecutor::setupDevSteps() {
   GLX_ENFORCE(sync_.outChans.size() == out_.size() && sync_.inChans.size() == in_.size(),
               "plan kernel: channel tables disagree");
+  enforceSpan((size_t)sync_.slice);
   const size_t G = (size_t)pk_.G;
   std::vector<glx::DevSegment> segs;
   for (size_t k = 0; k + 1 < sync_.bounds.size(); k++) {

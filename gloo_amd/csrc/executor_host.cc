@@ -70,7 +70,9 @@ void HipPlanExecutor::runFnHostStaged(const FnCall& call) {
   for (int i = 0; i < 2; i++) {  // pageable source / destination: through a mirror
     void* u = i == 0 ? src : call.out[0];
     callMirrored_[i] = !isPinnedHost(u);
-    if (callMirrored_[i] && callMirror_[i].p == nullptr) mirrorFor(nullptr, callMirror_[i]);
+    if (callMirrored_[i] && callMirror_[i].p == nullptr) {
+      takeMirror(callMirror_[i], std::max<size_t>((size_t)count_ * esize_, 16));
+    }
   }
   staged_ = true;
   timeout_ = call.timeout;
@@ -134,10 +136,17 @@ void HipPlanExecutor::runFnHost(const FnCall& call) {
   // pageable buffers through pinned mirrors: slots 0..srcs-1 the sources,
   // then out[0]'s old value (float16), then the outputs
   while (fnMirror_.size() < srcs.size() + 1 + call.out.size()) fnMirror_.emplace_back();
-  for (size_t i = 0; i < srcs.size(); i++) {
-    GLX_HIP_CHECK(hipMemcpyAsync(fnStage_[1 + i], mirrorFor(srcs[i], fnMirror_[i]), bytes,
-                                 hipMemcpyHostToDevice, compute_));
-  }
+  // a whole host buffer to the device: directly when pinned, else through its
+  // mirror (or bounce block)
+  auto stageIn = [&](char* dev, void* user, PinnedBlock& m) {
+    char* src = mirrorFor(user, m);
+    if (m.bounce && src == m.p) {
+      bounceIn(dev, static_cast<const char*>(user), bytes, m, compute_);
+    } else {
+      GLX_HIP_CHECK(hipMemcpyAsync(dev, src, bytes, hipMemcpyHostToDevice, compute_));
+    }
+  };
+  for (size_t i = 0; i < srcs.size(); i++) stageIn(fnStage_[1 + i], srcs[i], fnMirror_[i]);
   std::vector<void*> din, dout;
   char* out0;
   if (call.in.empty()) {  // the staged outputs are the data; out[0]'s copy gets the result
@@ -149,8 +158,7 @@ void HipPlanExecutor::runFnHost(const FnCall& call) {
     out0 = fnStage_[0];
     if (dtype_ == GLX_FLOAT16 && din.size() >= 2) {
       // float16's assignment reads out[0]'s old value
-      GLX_HIP_CHECK(hipMemcpyAsync(out0, mirrorFor(call.out[0], fnMirror_[srcs.size()]), bytes,
-                                   hipMemcpyHostToDevice, compute_));
+      stageIn(out0, call.out[0], fnMirror_[srcs.size()]);
     }
   }
   localReduce(din, dout);
@@ -159,14 +167,21 @@ void HipPlanExecutor::runFnHost(const FnCall& call) {
   for (size_t i = 0; i < call.out.size(); i++) {
     PinnedBlock& m = fnMirror_[srcs.size() + 1 + i];
     outDma[i] = isPinnedHost(call.out[i]) ? static_cast<char*>(call.out[i])
-                                          : (m.p ? m.p : mirrorFor(nullptr, m));
+                                          : mirrorFor(nullptr, m);
+    if (m.bounce && outDma[i] == m.p) continue;  // after the run, piece by piece
     GLX_HIP_CHECK(hipMemcpyAsync(outDma[i], out0, bytes, hipMemcpyDeviceToHost, compute_));
   }
   noteDone(compute_);
   waitDevice(compute_);
   checkDevice();
   for (size_t i = 0; i < call.out.size(); i++) {
-    if (outDma[i] != call.out[i]) std::memcpy(call.out[i], outDma[i], bytes);
+    PinnedBlock& m = fnMirror_[srcs.size() + 1 + i];
+    if (outDma[i] == call.out[i]) continue;
+    if (m.bounce) {
+      bounceOut(static_cast<char*>(call.out[i]), out0, bytes, m, compute_);
+    } else {
+      std::memcpy(call.out[i], outDma[i], bytes);
+    }
   }
 }
 
@@ -175,9 +190,14 @@ namespace {
 // runtime while the process lives: they wait here for the next algorithm,
 // the policy context.cc applies to uncached device blocks after freed ones
 // were seen breaking later allocations of the same process.
+// Cached blocks are our own hipHostMalloc allocations; none of them ever
+// shares a page with a caller's memory (the round-3 illegal address came from
+// registering callers' pages), so handing the ones beyond the
+// cap back to the runtime is safe.
 struct PinnedCache {
   std::mutex mu;
-  std::vector<std::pair<size_t, char*>> free;
+  std::vector<std::pair<size_t, char*>> free;  // oldest first
+  size_t total = 0;                            // bytes in `free`
 };
 
 PinnedCache& pinnedCache() {
@@ -185,7 +205,10 @@ PinnedCache& pinnedCache() {
   return *c;
 }
 
-char* takePinned(size_t* bytes) {
+// A cached block of at least *bytes (at most about twice that), else a new
+// one; null when the runtime cannot pin that much even after the cache gave
+// its blocks back.
+char* tryTakePinned(size_t* bytes) {
   PinnedCache& c = pinnedCache();
   {
     std::lock_guard<std::mutex> g(c.mu);
@@ -198,35 +221,94 @@ char* takePinned(size_t* bytes) {
     if (best != c.free.size()) {
       char* p = c.free[best].second;
       *bytes = c.free[best].first;
+      c.total -= *bytes;
       c.free.erase(c.free.begin() + (long)best);
       return p;
     }
   }
-  char* p = nullptr;
-  GLX_HIP_CHECK(hipHostMalloc((void**)&p, *bytes, hipHostMallocDefault));
+  for (int attempt = 0; attempt < 2; attempt++) {
+    char* p = nullptr;
+    if (hipHostMalloc((void**)&p, *bytes, hipHostMallocDefault) == hipSuccess) return p;
+    (void)hipGetLastError();
+    if (attempt == 0) {  // give the cached blocks back and try once more
+      std::lock_guard<std::mutex> g(c.mu);
+      for (auto& b : c.free) (void)hipHostFree(b.second);
+      c.free.clear();
+      c.total = 0;
+    }
+  }
+  return nullptr;
+}
+
+char* takePinned(size_t* bytes) {
+  char* p = tryTakePinned(bytes);
+  GLX_ENFORCE(p != nullptr, "cannot pin ", *bytes, " bytes of host memory");
   return p;
 }
+
+size_t g_mirrorLimit = 0;  // glx_set_pinned_mirror_limit
 }  // namespace
+
+namespace exec {
+size_t pinnedMirrorLimit() { return g_mirrorLimit; }
+void setPinnedMirrorLimit(size_t bytes) { g_mirrorLimit = bytes; }
+}  // namespace exec
 
 void HipPlanExecutor::givePinned(char* p, size_t bytes) {
   if (p == nullptr) return;
   PinnedCache& c = pinnedCache();
   std::lock_guard<std::mutex> g(c.mu);
   c.free.emplace_back(bytes, p);
+  c.total += bytes;
+  while (c.total > kPinnedCacheCap && !c.free.empty()) {
+    (void)hipHostFree(c.free.front().second);
+    c.total -= c.free.front().first;
+    c.free.erase(c.free.begin());
+  }
+}
+
+void HipPlanExecutor::takeMirror(PinnedBlock& m, size_t bytes) {
+  m.bounce = false;
+  m.bytes = bytes;
+  const size_t limit = pinnedMirrorLimit();
+  m.p = (limit == 0 || bytes <= limit) ? tryTakePinned(&m.bytes) : nullptr;
+  if (m.p == nullptr) {
+    m.bytes = std::min(bytes, kBounceBytes);
+    m.p = takePinned(&m.bytes);
+    m.bounce = true;
+  }
+  GLX_TRACE_MEM("r%d %s %p (%zu) for a pageable buffer of %zu", contextRank_,
+                m.bounce ? "bounce" : "mirror", (void*)m.p, m.bytes, bytes);
+}
+
+void HipPlanExecutor::bounceIn(char* dev, const char* user, size_t n, PinnedBlock& b,
+                               hipStream_t s) {
+  for (size_t at = 0; at < n; at += b.bytes) {
+    const size_t len = std::min(b.bytes, n - at);
+    GLX_HIP_CHECK(hipStreamSynchronize(s));  // the block's previous piece has been read
+    std::memcpy(b.p, user + at, len);
+    GLX_HIP_CHECK(hipMemcpyAsync(dev + at, b.p, len, hipMemcpyHostToDevice, s));
+  }
+}
+
+void HipPlanExecutor::bounceOut(char* user, const char* dev, size_t n, PinnedBlock& b,
+                                hipStream_t s) {
+  for (size_t at = 0; at < n; at += b.bytes) {
+    const size_t len = std::min(b.bytes, n - at);
+    GLX_HIP_CHECK(hipMemcpyAsync(b.p, dev + at, len, hipMemcpyDeviceToHost, s));
+    GLX_HIP_CHECK(hipStreamSynchronize(s));
+    std::memcpy(user + at, b.p, len);
+  }
 }
 
 // `user` when it is pinned (or null: a destination-only mirror is wanted);
-// else the pinned mirror block m, taken on first use, with `user`'s
-// bytes copied in when `user` is a source (the whole-buffer case).
+// else the pinned block m, taken on first use, with `user`'s bytes copied
+// in when `user` is a source and m is a whole mirror (a bounce block is
+// filled piece by piece by bounceIn).
 char* HipPlanExecutor::mirrorFor(void* user, PinnedBlock& m) {
   if (user != nullptr && isPinnedHost(user)) return static_cast<char*>(user);
-  const size_t bytes = std::max<size_t>((size_t)count_ * esize_, 16);
-  if (m.p == nullptr) {
-    m.bytes = bytes;
-    m.p = takePinned(&m.bytes);
-    GLX_TRACE_MEM("r%d mirror %p (%zu) for %p", contextRank_, (void*)m.p, m.bytes, user);
-  }
-  if (user != nullptr) std::memcpy(m.p, user, (size_t)count_ * esize_);
+  if (m.p == nullptr) takeMirror(m, std::max<size_t>((size_t)count_ * esize_, 16));
+  if (user != nullptr && !m.bounce) std::memcpy(m.p, user, (size_t)count_ * esize_);
   return m.p;
 }
 
@@ -247,10 +329,7 @@ void HipPlanExecutor::setupHostMode() {
   if (!hostFold_) {
     for (size_t k = 0; k < ptrs_.size(); k++) {
       if (isPinnedHost(ptrs_[k])) continue;
-      ptrMirror_[k].bytes = std::max<size_t>(bytes, 16);
-      ptrMirror_[k].p = takePinned(&ptrMirror_[k].bytes);
-      GLX_TRACE_MEM("r%d mirror %p (%zu) for %p", contextRank_, (void*)ptrMirror_[k].p,
-                    ptrMirror_[k].bytes, ptrs_[k]);
+      takeMirror(ptrMirror_[k], std::max<size_t>(bytes, 16));
     }
   }
   for (size_t k = 0; k < hostSources().size(); k++) {
@@ -317,16 +396,22 @@ void HipPlanExecutor::waitH2D(hipStream_t s, int& waited, int64_t off, int64_t l
 
 // The host buffers the device copies are staged from and back to: the
 // user's pointers, or the one pinned buffer they were folded into.
+// user buffer `u` as the copies see it, given its block (null: pinned)
+HipPlanExecutor::HostSide HipPlanExecutor::sideOf(char* u, const PinnedBlock* m) {
+  if (m == nullptr || m->p == nullptr) return {u, u, nullptr};
+  if (m->bounce) return {u, nullptr, const_cast<PinnedBlock*>(m)};
+  return {u, m->p, nullptr};
+}
+
 std::vector<HipPlanExecutor::HostSide> HipPlanExecutor::hostSources() const {
   if (!callSrc_.empty()) {
     char* u = static_cast<char*>(callSrc_[0]);
-    return {HostSide{u, callMirrored_[0] ? callMirror_[0].p : u}};
+    return {sideOf(u, callMirrored_[0] ? &callMirror_[0] : nullptr)};
   }
-  if (hostFold_) return {HostSide{hostStage_, hostStage_}};
+  if (hostFold_) return {HostSide{hostStage_, hostStage_, nullptr}};
   std::vector<HostSide> v;
   for (size_t k = 0; k < ptrs_.size(); k++) {
-    char* u = static_cast<char*>(ptrs_[k]);
-    v.push_back(HostSide{u, ptrMirror_[k].p ? ptrMirror_[k].p : u});
+    v.push_back(sideOf(static_cast<char*>(ptrs_[k]), &ptrMirror_[k]));
   }
   return v;
 }
@@ -334,14 +419,14 @@ std::vector<HipPlanExecutor::HostSide> HipPlanExecutor::hostSources() const {
 std::vector<HipPlanExecutor::HostSide> HipPlanExecutor::hostDests() const {
   if (!callDst_.empty()) {
     char* u = static_cast<char*>(callDst_[0]);
-    return {HostSide{u, callMirrored_[1] ? callMirror_[1].p : u}};
+    return {sideOf(u, callMirrored_[1] ? &callMirror_[1] : nullptr)};
   }
   return hostSources();
 }
 
 void HipPlanExecutor::copyOut(const std::vector<glx::Range>& ranges) {
   for (const HostSide& h : hostDests()) {
-    if (h.dma == h.user) continue;
+    if (h.dma == h.user || h.dma == nullptr) continue;  // pinned, or bounced already
     for (const glx::Range& r : ranges) {
       const size_t at = (size_t)r.off * esize_, n = (size_t)r.len * esize_;
       std::memcpy(h.user + at, h.dma + at, n);
@@ -364,10 +449,14 @@ void HipPlanExecutor::flushMirrors() {
 void HipPlanExecutor::copyBack(const std::vector<glx::Range>& ranges) {
   const std::vector<HostSide> dsts = hostDests();
   bool mirrored = false;
-  for (const HostSide& h : dsts) mirrored = mirrored || h.dma != h.user;
+  for (const HostSide& h : dsts) mirrored = mirrored || (h.dma != h.user && h.dma != nullptr);
   for (const glx::Range& r : ranges) {
     const size_t at = (size_t)r.off * esize_, n = (size_t)r.len * esize_;
     for (const HostSide& h : dsts) {
+      if (h.bounce != nullptr) {  // no mirror: through the bounce block, now
+        bounceOut(h.user + at, devBufs_[0] + at, n, *h.bounce, d2h_);
+        continue;
+      }
       GLX_HIP_CHECK(hipMemcpyAsync(h.dma + at, devBufs_[0] + at, n, hipMemcpyDeviceToHost, d2h_));
     }
   }
@@ -409,6 +498,10 @@ void HipPlanExecutor::issuePiece(size_t j) {
   const size_t at = (size_t)r.off * esize_, n = (size_t)r.len * esize_;
   const std::vector<HostSide> hsrc = hostSources();
   for (size_t k = 0; k < hsrc.size(); k++) {
+    if (hsrc[k].bounce != nullptr) {
+      bounceIn(devBufs_[k] + at, hsrc[k].user + at, n, *hsrc[k].bounce, h2d_);
+      continue;
+    }
     // pageable: into the mirror on the host first (the copy below then
     // reads pinned memory only)
     if (hsrc[k].dma != hsrc[k].user) std::memcpy(hsrc[k].dma + at, hsrc[k].user + at, n);

@@ -90,6 +90,15 @@ inline hipError_t spinSync(hipStream_t s) {
 // H2D pieces of host-mode staging: small enough that the schedule starts
 // early, large enough to run the PCIe link at full rate.
 constexpr int64_t kStagePieceBytes = int64_t(8) << 20;
+// bounce block of a pageable buffer that has no whole pinned mirror
+constexpr size_t kBounceBytes = size_t(8) << 20;
+// free pinned blocks the process-wide cache keeps for later algorithms; the
+// rest go back to the runtime (hipHostFree)
+constexpr size_t kPinnedCacheCap = size_t(1) << 30;
+// glx_set_pinned_mirror_limit: pageable buffers above it use a bounce block
+// (0: no limit)
+size_t pinnedMirrorLimit();
+void setPinnedMirrorLimit(size_t bytes);
 
 }  // namespace exec
 }  // namespace gloo

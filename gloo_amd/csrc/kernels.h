@@ -45,6 +45,10 @@ int copy_blocks();
 // regions and flags are uncached device memory (peers' via IPC).
 constexpr int kOsMaxRanks = 8;
 constexpr int kOsMaxSlices = 512;  // workgroups (= slices) per launch
+// Write-through stores address their stream through a buffer resource with
+// 32-bit offsets (elem_ops.h): one stream -- a reduce launch's destination,
+// or one workgroup's span of a device engine -- must stay below 2 GiB.
+constexpr size_t kWtMaxStream = (size_t(1) << 31) - 16;
 // Flags are 8-byte words, each alone in its 128-byte L2 line: flag f of a
 // row starts at row + f * kFlagStride (no line holds flags of two writers).
 constexpr int kFlagStride = 16;
@@ -155,7 +159,7 @@ struct PlanKernelParams {
   int narrow;                  // 1: narrow release / acquire around flags (below)
   int flagStore;               // 1: write peers' flags with stores (Context::flagStores)
   int fast;                    // 1: nontemporal loads, write-through stores (plan kernel only;
-                               // every span's stores stay below kWtMaxStream by construction)
+                               // every span's stores stay below kWtMaxStream: setupDevSteps)
   // diagnostics (GLOO_AMD_DEVTRACE=1): [G][2 * nsteps + 1] s_memrealtime
   // stamps per workgroup: step i started (2i), its wait was satisfied
   // (2i + 1; RECV / SEND only), the kernel ended (2 nsteps)

@@ -335,10 +335,26 @@ inline glx_algorithm* createAuto(glx_context* c, void* const* p, int n, int coun
 }
 }  // namespace detail
 
-// gloo::CudaAllreduceRingChunked<T> analog (gloo/cuda_allreduce_ring_chunked.h:22-26).
+// gloo::CudaHostWorkspace<T> / CudaDeviceWorkspace<T> analogs
+// (gloo/cuda_workspace.h:20-30), the algorithms' optional second template
+// argument.  Over xGMI the inter-rank scratch is always the receiver's device
+// memory, so both tags run the same schedule with the same result bits.
 template <typename T>
+struct HipHostWorkspace {
+  using Pointer = T*;
+  static constexpr const char* kName = "host";
+};
+template <typename T>
+struct HipDeviceWorkspace {
+  using Pointer = T*;
+  static constexpr const char* kName = "device";
+};
+
+// gloo::CudaAllreduceRingChunked<T, W> analog (gloo/cuda_allreduce_ring_chunked.h:19-26).
+template <typename T, typename W = HipHostWorkspace<T>>
 class HipAllreduceRingChunked : public detail::DeviceAllreduce<T> {
  public:
+  static const char* workspace() { return W::kName; }
   HipAllreduceRingChunked(const std::shared_ptr<Context>& ctx, const std::vector<T*>& ptrs,
                           int count, const std::vector<glx_stream_t>& streams = {},
                           const ReductionFunction<T>* fn = ReductionFunction<T>::sum,
@@ -350,16 +366,41 @@ class HipAllreduceRingChunked : public detail::DeviceAllreduce<T> {
                                    ctx, ptrs, count, streams, fn) {}
 };
 
-// gloo::CudaAllreduceHalvingDoubling<T> analog (gloo/cuda_allreduce_halving_doubling.h:25-30).
-template <typename T>
+// gloo::CudaAllreduceHalvingDoubling<T, W> analog (gloo/cuda_allreduce_halving_doubling.h:22-30).
+template <typename T, typename W = HipHostWorkspace<T>>
 class HipAllreduceHalvingDoubling : public detail::DeviceAllreduce<T> {
  public:
+  static const char* workspace() { return W::kName; }
   HipAllreduceHalvingDoubling(const std::shared_ptr<Context>& ctx,
                               const std::vector<T*>& ptrs, int count,
                               const std::vector<glx_stream_t>& streams = {},
                               const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
       : detail::DeviceAllreduce<T>(&glx_allreduce_halving_doubling_create, ctx, ptrs, count,
                                    streams, fn) {}
+  // the CUDA constructor's pipelineBroadcastAndReduce: recorded, same result
+  // (the device-driven schedule overlaps its steps either way)
+  HipAllreduceHalvingDoubling(const std::shared_ptr<Context>& ctx,
+                              const std::vector<T*>& ptrs, int count,
+                              const std::vector<glx_stream_t>& streams,
+                              bool pipelineBroadcastAndReduce)
+      : detail::DeviceAllreduce<T>(&glx_allreduce_halving_doubling_create, ctx, ptrs, count,
+                                   streams, ReductionFunction<T>::sum),
+        pipelined_(pipelineBroadcastAndReduce) {}
+  bool pipelined() const { return pipelined_; }
+
+ private:
+  bool pipelined_ = false;
+};
+
+// gloo::CudaAllreduceHalvingDoublingPipelined<T, W> analog
+// (gloo/cuda_allreduce_halving_doubling_pipelined.h:13-27).
+template <typename T, typename W = HipHostWorkspace<T>>
+class HipAllreduceHalvingDoublingPipelined : public HipAllreduceHalvingDoubling<T, W> {
+ public:
+  HipAllreduceHalvingDoublingPipelined(const std::shared_ptr<Context>& ctx,
+                                       const std::vector<T*>& ptrs, int count,
+                                       const std::vector<glx_stream_t>& streams = {})
+      : HipAllreduceHalvingDoubling<T, W>(ctx, ptrs, count, streams, true) {}
 };
 
 // gloo::sum<T>(c, a, b, n) on the device (gloo/math.h:15-28).

@@ -136,6 +136,12 @@ int glx_tune_reduce(int unroll, int blocks_per_cu, int nontemporal);
  * destination (k DMA engines feeding one link; parts >= 1 MiB).  Default 1,
  * or $GLOO_AMD_COPY_SPLIT. */
 int glx_set_copy_split(int k);
+/* Host-memory endpoints: a pageable buffer is staged through a pinned mirror
+ * of its size (the reference's CudaHostWorkspace, gloo/cuda_workspace.h:20);
+ * above `bytes` (0: no limit, the default), or when the runtime cannot pin a
+ * mirror that large, through an 8 MiB pinned bounce block instead, piece by
+ * piece (slower, same result).  For algorithms created afterwards. */
+int glx_set_pinned_mirror_limit(size_t bytes);
 /* How peer copies are made by algorithms created afterwards: engine 0 =
  * hipMemcpyPeerAsync (DMA copy engines, default), 1 = a copy kernel storing
  * into the peer's memory over xGMI, with `blocks` workgroups (<= 0: keep).

@@ -3,10 +3,24 @@
 // tree (next to gloo/cuda_allreduce_ring_chunked.h) and links
 // -lgloo_amd -lamdhip64; callers keep gloo's types, macros and exceptions.
 //
-//   HipAllreduceRingChunked<T>     ~ CudaAllreduceRingChunked<T>
-//                                    (gloo/cuda_allreduce_ring_chunked.h:22-26)
-//   HipAllreduceHalvingDoubling<T> ~ CudaAllreduceHalvingDoubling<T>
-//                                    (gloo/cuda_allreduce_halving_doubling.h:25-30)
+//   HipAllreduceRingChunked<T, W>     ~ CudaAllreduceRingChunked<T, W>
+//                                       (gloo/cuda_allreduce_ring_chunked.h:19-26)
+//   HipAllreduceHalvingDoubling<T, W> ~ CudaAllreduceHalvingDoubling<T, W>
+//                                       (gloo/cuda_allreduce_halving_doubling.h:22-30)
+//   HipAllreduceHalvingDoublingPipelined<T, W>
+//                                     ~ CudaAllreduceHalvingDoublingPipelined<T, W>
+//                                       (gloo/cuda_allreduce_halving_doubling_pipelined.h:13-27)
+//   HipHostWorkspace<T>, HipDeviceWorkspace<T>
+//                                     ~ CudaHostWorkspace<T>, CudaDeviceWorkspace<T>
+//                                       (gloo/cuda_workspace.h:20-30)
+//
+// W defaults to the host workspace as in the reference, so every CUDA call
+// site (gloo/test/cuda_allreduce_test.cc:85-144, gloo/benchmark/
+// cuda_main.cc:184-197) switches by renaming the type.  The workspace only
+// says where the CUDA algorithms keep their inter-rank scratch (host memory
+// for a TCP pair, device memory for a GPUDirect one); over xGMI the scratch is
+// always the receiver's device memory, so both tags run the same schedule
+// with the same result bits (workspace() reports the tag).
 //
 // Both take the reference's gloo::Context, the device pointers of this rank,
 // the element count, optional streams (outputs valid once streams[0] reaches
@@ -19,7 +33,9 @@
 // optional ReductionFunction of the CPU algorithms).  The xGMI transport
 // exchanges its device endpoints (IPC handles of receive regions, flag rows)
 // over the gloo context's own pairs with gloo::allgather (ContextStore
-// below), so nothing beyond the connected context is needed.  An overload
+// below), so nothing beyond the connected context is needed: at connect (the
+// first HIP algorithm created on a context) and at each algorithm's first
+// run(), every rank, whatever else it did in between.  An overload
 // taking the rendezvous::Store the context was connected with is kept: it
 // publishes the endpoints there instead (no collective at first run).  The
 // first algorithm created on a gloo context sets up one xGMI context for it
@@ -49,6 +65,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "gloo/algorithm.h"
@@ -143,15 +160,27 @@ class StoreBridge {
 };
 
 // The xGMI layer's rendezvous keys carried by the gloo context itself.
-// Every key is set by the rank that owns it and read by its peers, and every
-// rank sets and reads them at the same points of its program -- connecting,
-// then each algorithm's record at its creation, read at its first run -- in
-// the same order on every rank (gloo's own rule for creating algorithms).  A
-// read that misses is therefore answered by ONE collective exchange: every
-// rank contributes the keys it set since the previous exchange, gathered with
-// gloo::allgather (gloo/allgather.h:71) over the context's pairs.  A key still
-// missing after an exchange will never arrive (the ranks' programs differ):
-// the read fails at once (-2) instead of waiting out the timeout.
+// Every key is set by the rank that owns it and read by its peers.  An
+// exchange is ONE collective: every rank contributes the keys it set since
+// the previous one, gathered with gloo::allgather (gloo/allgather.h:71) over
+// the context's pairs.  Exchanges happen at program points every rank passes
+// in the same order, never because one rank happens to lack a key:
+//   * connect (the first HIP algorithm created on the context) and
+//     gloo::hip::allreduce calls: the rank sets its own keys and then reads
+//     its peers' ones, which no earlier exchange can have carried (a peer
+//     sets them in the same call) -- so every rank misses and exchanges;
+//   * each class algorithm's first run(): one exchange, unconditionally
+//     (sync()), after which the algorithm's records must all be here.  gloo
+//     constructors are local, so ranks may interleave creating and running
+//     algorithms differently (create A, create B, run A, run B on one rank;
+//     create A, run A, create B, run B on another); runs are collective and
+//     come in the same order everywhere, so the exchanges line up.  (Round 3
+//     exchanged on a missed read only; with that interleaving the second rank
+//     already held B's record from A's exchange, skipped the one the first
+//     rank started at B's run, and both waited out the timeout.)
+// A key still missing after its exchange will never arrive (the ranks'
+// programs differ): the read fails at once (-2) instead of waiting out the
+// timeout, and a strict read (inside a first run) never exchanges at all.
 class ContextStore {
  public:
   // the allgather tag of the exchanges: any value user collectives on this
@@ -169,6 +198,11 @@ class ContextStore {
   int exchanges() const { return exchanges_; }
   const std::string& lastError() const { return error_; }
 
+  // one collective exchange now, whatever this rank already knows
+  void sync() { exchange(); }
+  // strict: a missed read fails at once instead of exchanging
+  void setStrict(bool strict) { strict_ = strict; }
+
  private:
   static int set(void* user, const char* key, const void* data, size_t len) {
     auto* self = static_cast<ContextStore*>(user);
@@ -181,6 +215,12 @@ class ContextStore {
   static int64_t get(void* user, const char* key, void* buf, size_t cap) {
     auto* self = static_cast<ContextStore*>(user);
     auto it = self->known_.find(key);
+    if (it == self->known_.end() && self->strict_) {
+      self->error_ = std::string("no rank published '") + key +
+                     "' before this algorithm's first run (the ranks created their "
+                     "algorithms in different orders)";
+      return -2;
+    }
     if (it == self->known_.end()) {
       try {
         self->exchange();
@@ -261,6 +301,7 @@ class ContextStore {
   std::map<std::string, std::vector<char>> known_;
   std::vector<std::string> pending_;
   int exchanges_ = 0;
+  bool strict_ = false;
   std::string error_;
 };
 
@@ -295,6 +336,24 @@ class XgmiContext {
   glx_context* get() const { return glx_; }
   // exchanges over the gloo context so far (0 with a rendezvous store)
   int exchanges() const { return viaContext_ ? viaContext_->exchanges() : 0; }
+  // an algorithm's first run: one exchange on every rank, then `fn` with
+  // strict reads (nothing to do with a rendezvous store: its reads wait)
+  template <typename F>
+  void firstRun(F&& fn) {
+    if (!viaContext_) {
+      fn();
+      return;
+    }
+    viaContext_->sync();
+    viaContext_->setStrict(true);
+    try {
+      fn();
+    } catch (...) {
+      viaContext_->setStrict(false);
+      throw;
+    }
+    viaContext_->setStrict(false);
+  }
 
  private:
   XgmiContext(const std::shared_ptr<Context>& ctx, rendezvous::Store* store, int device,
@@ -333,7 +392,14 @@ inline int deviceOf(const void* p) {
 template <typename T>
 class Allreduce : public Algorithm {
  public:
-  void run() override { check(glx_algorithm_run(alg_), "run"); }
+  void run() override {
+    if (ran_) {
+      check(glx_algorithm_run(alg_), "run");
+      return;
+    }
+    xgmi_->firstRun([&] { check(glx_algorithm_run(alg_), "run"); });
+    ran_ = true;
+  }
   ~Allreduce() override { glx_algorithm_destroy(alg_); }
   // bytes moved over the peer links per run (introspection)
   int64_t bytesSent() const { return glx_algorithm_bytes_sent(alg_); }
@@ -358,6 +424,7 @@ class Allreduce : public Algorithm {
  private:
   std::shared_ptr<XgmiContext> xgmi_;
   glx_algorithm* alg_ = nullptr;
+  bool ran_ = false;
 };
 
 // AllreduceOptions keeps its settings in a protected member that only
@@ -450,10 +517,39 @@ inline void allreduce(const AllreduceOptions& opts, hipStream_t stream = nullptr
 
 }  // namespace hip
 
-// ~ CudaAllreduceRingChunked<T> (gloo/cuda_allreduce_ring_chunked.h:19-25)
+// ~ CudaHostWorkspace<T> / CudaDeviceWorkspace<T> (gloo/cuda_workspace.h:20-30):
+// the algorithms' second template argument.  Pointer is what the scratch of
+// that workspace would be; over xGMI both run the same device schedule.
 template <typename T>
-class HipAllreduceRingChunked : public hip::Allreduce<T> {
+class HipHostWorkspace {
  public:
+  using Pointer = T*;
+  static constexpr const char* kName = "host";
+};
+
+template <typename T>
+class HipDeviceWorkspace {
+ public:
+  using Pointer = T*;
+  static constexpr const char* kName = "device";
+};
+
+namespace hip {
+template <typename T, typename W>
+struct IsWorkspace {
+  static constexpr bool value = std::is_same<W, HipHostWorkspace<T>>::value ||
+                                std::is_same<W, HipDeviceWorkspace<T>>::value;
+};
+}  // namespace hip
+
+// ~ CudaAllreduceRingChunked<T, W> (gloo/cuda_allreduce_ring_chunked.h:19-26)
+template <typename T, typename W = HipHostWorkspace<T>>
+class HipAllreduceRingChunked : public hip::Allreduce<T> {
+  static_assert(hip::IsWorkspace<T, W>::value,
+                "W must be HipHostWorkspace<T> or HipDeviceWorkspace<T>");
+
+ public:
+  static const char* workspace() { return W::kName; }
   HipAllreduceRingChunked(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs,
                           const int count,
                           const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
@@ -467,10 +563,14 @@ class HipAllreduceRingChunked : public hip::Allreduce<T> {
       : hip::Allreduce<T>(GLX_ALGO_RING_CHUNKED, context, &store, ptrs, count, streams, fn) {}
 };
 
-// ~ CudaAllreduceHalvingDoubling<T> (gloo/cuda_allreduce_halving_doubling.h:25-30)
-template <typename T>
+// ~ CudaAllreduceHalvingDoubling<T, W> (gloo/cuda_allreduce_halving_doubling.h:22-30)
+template <typename T, typename W = HipHostWorkspace<T>>
 class HipAllreduceHalvingDoubling : public hip::Allreduce<T> {
+  static_assert(hip::IsWorkspace<T, W>::value,
+                "W must be HipHostWorkspace<T> or HipDeviceWorkspace<T>");
+
  public:
+  static const char* workspace() { return W::kName; }
   HipAllreduceHalvingDoubling(const std::shared_ptr<Context>& context,
                               const std::vector<T*>& ptrs, const int count,
                               const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
@@ -478,23 +578,42 @@ class HipAllreduceHalvingDoubling : public hip::Allreduce<T> {
       : hip::Allreduce<T>(GLX_ALGO_HALVING_DOUBLING, context, nullptr, ptrs, count, streams,
                           fn) {}
   // the CUDA constructor's last argument: whether to pipeline the local
-  // broadcast with the reduce (gloo/cuda_allreduce_halving_doubling.h:30).
-  // The result is the same either way; the device-driven schedule overlaps
-  // its steps regardless, so the flag is accepted and has nothing to change.
+  // broadcast with the reduce (gloo/cuda_allreduce_halving_doubling.h:30;
+  // gloo/cuda_allreduce_halving_doubling.cc:252-279,374-392: with several
+  // local pointers, fold only the first send's range before sending, the rest
+  // while the first receive is in flight, and broadcast each allgather step's
+  // block to the other pointers as soon as it lands).  The result is the
+  // same either way; the device-driven schedule overlaps its steps
+  // regardless, so the flag is recorded (pipelined()) and changes nothing.
   HipAllreduceHalvingDoubling(const std::shared_ptr<Context>& context,
                               const std::vector<T*>& ptrs, const int count,
                               const std::vector<hipStream_t>& streams,
                               bool pipelineBroadcastAndReduce)
       : hip::Allreduce<T>(GLX_ALGO_HALVING_DOUBLING, context, nullptr, ptrs, count, streams,
-                          ReductionFunction<T>::sum) {
-    (void)pipelineBroadcastAndReduce;
-  }
+                          ReductionFunction<T>::sum),
+        pipelined_(pipelineBroadcastAndReduce) {}
   HipAllreduceHalvingDoubling(const std::shared_ptr<Context>& context, rendezvous::Store& store,
                               const std::vector<T*>& ptrs, const int count,
                               const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
                               const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
       : hip::Allreduce<T>(GLX_ALGO_HALVING_DOUBLING, context, &store, ptrs, count, streams,
                           fn) {}
+  bool pipelined() const { return pipelined_; }
+
+ private:
+  bool pipelined_ = false;
+};
+
+// ~ CudaAllreduceHalvingDoublingPipelined<T, W>
+// (gloo/cuda_allreduce_halving_doubling_pipelined.h:13-27): halving-doubling
+// with pipelineBroadcastAndReduce = true, the same four arguments.
+template <typename T, typename W = HipHostWorkspace<T>>
+class HipAllreduceHalvingDoublingPipelined : public HipAllreduceHalvingDoubling<T, W> {
+ public:
+  HipAllreduceHalvingDoublingPipelined(
+      const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, const int count,
+      const std::vector<hipStream_t>& streams = std::vector<hipStream_t>())
+      : HipAllreduceHalvingDoubling<T, W>(context, ptrs, count, streams, true) {}
 };
 
 }  // namespace gloo

@@ -13,9 +13,12 @@
 //                      the reference's tests (HashStore + tcp loopback +
 //                      rendezvous::Context::connectFullMesh, gloo/test/
 //                      base_test.h:91-166); HipAllreduceRingChunked<float>,
-//                      HipAllreduceHalvingDoubling<float16|int32> built with
+//                      HipAllreduceHalvingDoubling<float16|int32>,
+//                      HipAllreduceHalvingDoublingPipelined<float|float16>
+//                      and the HipDeviceWorkspace instantiations built with
 //                      the CUDA constructors' exact arguments (ctx, ptrs,
-//                      count[, streams]) on device buffers, and
+//                      count[, streams]) on device buffers; algorithms
+//                      created and run in different interleavings per rank;
 //                      gloo::hip::allreduce(AllreduceOptions) on the same
 //                      options the reference's gloo::allreduce takes,
 //                      compared bit for bit with the reference's own CPU
@@ -34,6 +37,7 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "gloo/allreduce.h"
@@ -168,6 +172,57 @@ int cpuMode() {
     const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     EXPECT(rc == GLX_ERR_IO && s < 5.0, "a key nobody set: rc %d after %.1f s", rc, s);
   });
+  // exchange points that do not depend on what a rank already knows (ADVICE
+  // r3): rank 0 creates A and B before running A, rank 1 creates B only after
+  // running A.  Each first run is one exchange on every rank (sync()), its
+  // reads strict; exchanging on a missed read instead, rank 1 would hold B0
+  // from A's exchange, skip the one rank 0 starts at B's run, and both would
+  // wait out the timeout.
+  spawnCpu2([&](std::shared_ptr<gloo::Context> ctx, gloo::rendezvous::Store&, int r) {
+    hip::ContextStore cs(ctx);
+    std::vector<char> buf(64);
+    size_t len = 0;
+    auto set = [&](const std::string& k) {
+      EXPECT(glx_store_set(cs.handle(), k.c_str(), k.data(), k.size()) == GLX_OK, "set");
+    };
+    auto firstRun = [&](const std::string& k) {  // what XgmiContext::firstRun does
+      cs.sync();
+      cs.setStrict(true);
+      const int rc = glx_store_get(cs.handle(), k.c_str(), buf.data(), buf.size(), &len, 20000);
+      cs.setStrict(false);
+      EXPECT(rc == GLX_OK && len == k.size() && std::memcmp(buf.data(), k.data(), len) == 0,
+             "rank %d reads %s: rc %d (%s)", r, k.c_str(), rc, glx_last_error());
+    };
+    const std::string peer = std::to_string(1 - r), me = std::to_string(r);
+    if (r == 0) {
+      set("A/" + me);
+      set("B/" + me);
+      firstRun("A/" + peer);
+      firstRun("B/" + peer);
+    } else {
+      set("A/" + me);
+      firstRun("A/" + peer);
+      set("B/" + me);
+      firstRun("B/" + peer);
+    }
+    EXPECT(cs.exchanges() == 2, "rank %d: two exchanges, one per first run: %d", r,
+           cs.exchanges());
+    // a strict read of a key nobody set fails at once, without an exchange
+    cs.setStrict(true);
+    EXPECT(glx_store_get(cs.handle(), "never", buf.data(), buf.size(), &len, 20000) ==
+               GLX_ERR_IO && cs.exchanges() == 2,
+           "strict miss");
+    cs.setStrict(false);
+  });
+  // the CUDA type surface compiles with the type renamed
+  static_assert(std::is_same<HipAllreduceRingChunked<float>,
+                             HipAllreduceRingChunked<float, HipHostWorkspace<float>>>::value,
+                "the host workspace is the default, as in the reference");
+  static_assert(std::is_base_of<HipAllreduceHalvingDoubling<float16>,
+                                HipAllreduceHalvingDoublingPipelined<float16>>::value,
+                "Pipelined derives from HalvingDoubling, as in the reference");
+  EXPECT(std::string(HipAllreduceRingChunked<float, HipDeviceWorkspace<float>>::workspace()) ==
+             "device", "workspace tag");
   // two ranks' xGMI contexts connect through the bridge over one gloo store
   // (the endpoint exchange needs no GPU)
   {
@@ -214,9 +269,12 @@ void spawn(int P, const std::function<void(std::shared_ptr<gloo::Context>,
   for (int r = 0; r < P; r++) EXPECT(errs[r].empty(), "rank %d: %s", r, errs[r].c_str());
 }
 
+enum Ctor { kDefault, kStreams, kViaStore };
+
 template <typename T, template <typename> class Hip, template <typename> class Ref>
 void compare(const char* name, int P, int count, int nptrs, const gloo::ReductionFunction<T>* fn,
-             bool viaStore = false) {
+             Ctor how = kDefault) {
+  const bool viaStore = how == kViaStore;
   // inputs, and the reference's own CPU algorithm on host copies of them
   std::vector<std::vector<std::vector<T>>> in(P), ref(P), got(P);
   for (int r = 0; r < P; r++) {
@@ -246,15 +304,35 @@ void compare(const char* name, int P, int count, int nptrs, const gloo::Reductio
       hipMemcpy(d, in[r][(size_t)k].data(), sizeof(T) * (size_t)count, hipMemcpyHostToDevice);
       dev.push_back(d);
     }
+    std::vector<hipStream_t> streams;
+    if (how == kStreams) {  // one stream per pointer, as cuda_allreduce_test.cc passes them
+      for (int k = 0; k < nptrs; k++) {
+        hipStream_t st = nullptr;
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+          throw std::runtime_error("hipStreamCreate");
+        }
+        streams.push_back(st);
+      }
+    }
     {
       // the CUDA constructors' arguments; SUM needs no function at all
       std::unique_ptr<Hip<T>> a;
-      if (viaStore) {
-        a.reset(new Hip<T>(ctx, store, dev, count, {}, fn));
-      } else if (fn == gloo::ReductionFunction<T>::sum) {
+      // the Pipelined class has the CUDA one's four arguments only
+      constexpr bool withFn =
+          std::is_constructible<Hip<T>, std::shared_ptr<gloo::Context>, std::vector<T*>, int,
+                                std::vector<hipStream_t>, const gloo::ReductionFunction<T>*>::value;
+      if (how == kStreams) {
+        a.reset(new Hip<T>(ctx, dev, count, streams));  // gloo/test/cuda_allreduce_test.cc:85-144
+      } else if (fn == gloo::ReductionFunction<T>::sum && !viaStore) {
         a.reset(new Hip<T>(ctx, dev, count));
+      } else if constexpr (withFn) {
+        if (viaStore) {
+          a.reset(new Hip<T>(ctx, store, dev, count, {}, fn));
+        } else {
+          a.reset(new Hip<T>(ctx, dev, count, {}, fn));
+        }
       } else {
-        a.reset(new Hip<T>(ctx, dev, count, {}, fn));
+        throw std::runtime_error("this class takes no reduction function");
       }
       Hip<T>& alg = *a;
       for (int it = 0; it < 2; it++) {  // repeated runs on one instance
@@ -263,8 +341,12 @@ void compare(const char* name, int P, int count, int nptrs, const gloo::Reductio
                     hipMemcpyHostToDevice);
         }
         alg.run();
+        // with streams the outputs are valid once the streams reach the end
+        // of run() (docs/cuda.md:9-11)
+        for (hipStream_t st : streams) hipStreamSynchronize(st);
       }
     }
+    for (hipStream_t st : streams) hipStreamDestroy(st);
     for (int k = 0; k < nptrs; k++) {
       hipMemcpy(got[r][(size_t)k].data(), dev[(size_t)k], sizeof(T) * (size_t)count,
                 hipMemcpyDeviceToHost);
@@ -280,7 +362,8 @@ void compare(const char* name, int P, int count, int nptrs, const gloo::Reductio
   }
   EXPECT(bad == 0, "%s: %zu buffers differ from the reference", name, bad);
   std::printf("%s P=%d count=%d ptrs=%d%s: %s\n", name, P, count, nptrs,
-              viaStore ? " (store)" : "", bad ? "MISMATCH" : "ok");
+              viaStore ? " (store)" : how == kStreams ? " (streams)" : "",
+              bad ? "MISMATCH" : "ok");
 }
 
 // gloo::hip::allreduce(opts) against the reference's gloo::allreduce(opts):
@@ -363,6 +446,65 @@ void compareFn(const char* name, int P, int count, int nin, int nout,
               bad ? "MISMATCH" : "ok");
 }
 
+template <typename T>
+using RingDeviceWs = gloo::HipAllreduceRingChunked<T, gloo::HipDeviceWorkspace<T>>;
+template <typename T>
+using HdDeviceWs = gloo::HipAllreduceHalvingDoubling<T, gloo::HipDeviceWorkspace<T>>;
+
+// Algorithms created and run in different interleavings on different ranks
+// (legal: gloo constructors are local, runs are collective in one order).
+// Rank 0: create A, create B, run A, run B; the others: create A, run A,
+// create B, run B.  The endpoint exchanges over the gloo context must line up
+// (ADVICE r3); both results against the reference's CPU algorithms.
+void interleaved() {
+  using namespace gloo;
+  const int P = 3, count = 50001;
+  std::vector<std::vector<float>> in(P), refA(P), refB(P), gotA(P), gotB(P);
+  for (int r = 0; r < P; r++) {
+    in[r].resize((size_t)count);
+    for (int i = 0; i < count; i++) in[r][(size_t)i] = value<float>(r, (size_t)i);
+    refA[r] = refB[r] = gotA[r] = gotB[r] = in[r];
+  }
+  spawn(P, [&](std::shared_ptr<Context> ctx, rendezvous::Store&, int r) {
+    std::vector<float*> a{refA[r].data()}, b{refB[r].data()};
+    AllreduceRingChunked<float>(ctx, a, count).run();
+    AllreduceHalvingDoubling<float>(ctx, b, count).run();
+  });
+  spawn(P, [&](std::shared_ptr<Context> ctx, rendezvous::Store&, int r) {
+    float *da = nullptr, *db = nullptr;
+    if (hipMalloc((void**)&da, sizeof(float) * count) != hipSuccess ||
+        hipMalloc((void**)&db, sizeof(float) * count) != hipSuccess) {
+      throw std::runtime_error("hipMalloc");
+    }
+    hipMemcpy(da, in[r].data(), sizeof(float) * count, hipMemcpyHostToDevice);
+    hipMemcpy(db, in[r].data(), sizeof(float) * count, hipMemcpyHostToDevice);
+    std::vector<float*> pa{da}, pb{db};
+    std::unique_ptr<HipAllreduceRingChunked<float>> A(
+        new HipAllreduceRingChunked<float>(ctx, pa, count));
+    std::unique_ptr<HipAllreduceHalvingDoublingPipelined<float>> B;
+    if (r == 0) B.reset(new HipAllreduceHalvingDoublingPipelined<float>(ctx, pb, count));
+    A->run();
+    if (r != 0) B.reset(new HipAllreduceHalvingDoublingPipelined<float>(ctx, pb, count));
+    B->run();
+    EXPECT(A->exchanges() == 4, "rank %d: connect (2) + one per first run (2): %d", r,
+           A->exchanges());
+    hipMemcpy(gotA[r].data(), da, sizeof(float) * count, hipMemcpyDeviceToHost);
+    hipMemcpy(gotB[r].data(), db, sizeof(float) * count, hipMemcpyDeviceToHost);
+    A.reset();
+    B.reset();
+    hipFree(da);
+    hipFree(db);
+  });
+  size_t bad = 0;
+  for (int r = 0; r < P; r++) {
+    bad += gotA[r] != refA[r];
+    bad += gotB[r] != refB[r];
+  }
+  EXPECT(bad == 0, "interleaved creation: %zu buffers differ from the reference", bad);
+  std::printf("interleaved creation/run (rank 0: A, B, run A, run B) P=%d: %s\n", P,
+              bad ? "MISMATCH" : "ok");
+}
+
 int gpuMode() {
   using namespace gloo;
   int n = 0;
@@ -379,7 +521,27 @@ int gpuMode() {
   compare<int32_t, HipAllreduceHalvingDoubling, AllreduceHalvingDoubling>(
       "halving_doubling<int32> product", 3, 1000, 1, ReductionFunction<int32_t>::product);
   compare<float, HipAllreduceRingChunked, AllreduceRingChunked>(
-      "ring_chunked<float> sum", 2, 4099, 1, ReductionFunction<float>::sum, /*viaStore=*/true);
+      "ring_chunked<float> sum", 2, 4099, 1, ReductionFunction<float>::sum, kViaStore);
+  // the reference CUDA test's factories (gloo/test/cuda_allreduce_test.cc:
+  // 85-144) with the type renamed: <T> with (ctx, ptrs, count, streams), the
+  // pipelined halving-doubling, and the device-workspace instantiations
+  // (cuda_allreduce_ring_chunked.cc:361, cuda_allreduce_halving_doubling.cc:647)
+  compare<float, HipAllreduceRingChunked, AllreduceRingChunked>(
+      "ring_chunked<float> (ctx, ptrs, count, streams)", 3, 70001, 2,
+      ReductionFunction<float>::sum, kStreams);
+  compare<float16, HipAllreduceHalvingDoubling, AllreduceHalvingDoubling>(
+      "halving_doubling<float16> (ctx, ptrs, count, streams)", 3, 40961, 2,
+      ReductionFunction<float16>::sum, kStreams);
+  compare<float, HipAllreduceHalvingDoublingPipelined, AllreduceHalvingDoubling>(
+      "halving_doubling_pipelined<float>", 4, 100003, 2, ReductionFunction<float>::sum, kStreams);
+  compare<float16, HipAllreduceHalvingDoublingPipelined, AllreduceHalvingDoubling>(
+      "halving_doubling_pipelined<float16>", 5, 65539, 1, ReductionFunction<float16>::sum);
+  compare<float, RingDeviceWs, AllreduceRingChunked>(
+      "ring_chunked<float, HipDeviceWorkspace>", 2, 100003, 1, ReductionFunction<float>::sum,
+      kStreams);
+  compare<float, HdDeviceWs, AllreduceHalvingDoubling>(
+      "halving_doubling<float, HipDeviceWorkspace>", 3, 100003, 1, ReductionFunction<float>::sum);
+  interleaved();
   using MathFn = void (*)(void*, const void*, const void*, size_t);
   compareFn<float>("allreduce(opts) RING float sum", 3, 100003, 0, 1,
                    AllreduceOptions::Algorithm::RING, 0, (MathFn)&gloo::sum<float>);

@@ -378,6 +378,8 @@ int main() {
   for (int P : {1, 2, 3, 4, 5, 6, 7, 8, 9, 13}) {
     for (int N : {0, 1, 64, 1000}) {
       singlePointer<gloo_amd::HipAllreduceHalvingDoubling>("halving_doubling", P, N);
+      singlePointer<gloo_amd::HipAllreduceHalvingDoublingPipelined>("halving_doubling_pipelined",
+                                                                      P, N);
     }
   }
   for (int P = 1; P <= 8; P++) {

@@ -17,6 +17,8 @@ algo: ring_chunked | halving_doubling | ring_chunked_mesh (class algorithms)
       raise IoException)
       scale:cfg34 | scale:cfg5 (BASELINE.json configs at full size, 8 ranks:
       every engine's output SHA-256 against tests/golden/scale_golden.json)
+      scale:ns (the north-star size, 256 MiB fp32 per rank, ring and HD at
+      P = size: every engine against tests/golden/bench_golden.json)
       linkprobe (the measured-link probe through the product's IPC path, and
       every peer's connect-time view; then an allreduce on the same context)
       engine_choice (which engine the automatic policy picks on the shared
@@ -688,12 +690,19 @@ def run_scale(store_dir, rank, size, group):
     from oracle import oracle as O
     from test_reduce_gpu import from_dev, to_dev
 
-    with open(os.path.join(HERE, "golden", "scale_golden.json")) as f:
-        cases = json.load(f)["cases"]
-    if group == "cfg34":
-        cases = [c for c in cases if c["dtype"] == O.FLOAT32]
+    if group == "ns":
+        # the north-star size (2^26 fp32 = 256 MiB per rank) at this P, ring and
+        # halving-doubling: the digests bench.py's N > 1 line checks
+        # (tests/golden/bench_golden.json, make_golden.py bench)
+        with open(os.path.join(HERE, "golden", "bench_golden.json")) as f:
+            cases = [c for c in json.load(f)["cases"] if c["P"] == size]
     else:
-        cases = [c for c in cases if c["dtype"] != O.FLOAT32]
+        with open(os.path.join(HERE, "golden", "scale_golden.json")) as f:
+            cases = json.load(f)["cases"]
+        if group == "cfg34":
+            cases = [c for c in cases if c["dtype"] == O.FLOAT32]
+        else:
+            cases = [c for c in cases if c["dtype"] != O.FLOAT32]
     assert cases and all(c["P"] == size for c in cases), "scale cases are for P=%d" % size
 
     def sha(a):
@@ -735,7 +744,9 @@ def run_scale(store_dir, rank, size, group):
             ms = (time.perf_counter() - t0) * 1e3 / 2
             got = from_dev(buf, dt)
             ok = sha(got) == c["output_sha256"]
-            if not ok:
+            if not ok and "sample_idx" not in c:
+                bad.append((c["name"], sched, alg.engine(), "digest mismatch"))
+            elif not ok:
                 idx = np.array(c["sample_idx"])
                 bits = np.ascontiguousarray(got).view(np.uint32 if got.itemsize == 4
                                                       else np.uint16)[idx]

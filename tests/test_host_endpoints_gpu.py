@@ -164,3 +164,97 @@ def test_on_device_threshold(algo, dtype, op, nptrs):
         check(out, O.allreduce(ALGOS[algo], op, dtype, ins))
         for r in range(P):
             assert (stats[r]["host_folds"] == 2) == host, (nbytes, stats[r])
+
+
+@pytest.fixture
+def bounce_only():
+    """Every pageable buffer of algorithms created meanwhile goes through the
+    8 MiB bounce block instead of a pinned mirror of its size -- what the
+    product does when the runtime cannot pin a whole mirror."""
+    import gloo_amd
+    gloo_amd.set_pinned_mirror_limit(4096)
+    try:
+        yield
+    finally:
+        gloo_amd.set_pinned_mirror_limit(0)
+
+
+@pytest.mark.parametrize("algo", list(ALGOS))
+@pytest.mark.parametrize("P,N", [(1, 1000), (2, 100003), (3, (5 << 20) + 3)])
+def test_pageable_through_bounce_block(bounce_only, algo, P, N):
+    ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=71)
+    out = host_allreduce(algo, O.SUM, O.FLOAT32, ins, runs=2)
+    check(out, O.allreduce(ALGOS[algo], O.SUM, O.FLOAT32, ins))
+
+
+@pytest.mark.parametrize("dtype,op,nptrs", [(O.FLOAT32, O.SUM, 2), (O.FLOAT16, O.SUM, 3)],
+                         ids=str)
+def test_single_rank_multi_pointer_through_bounce_block(bounce_only, dtype, op, nptrs):
+    N = (5 << 20) + 4099
+    ins = case_inputs(1, N, dtype, nptrs, 0, seed=72)
+    out = host_allreduce("ring_chunked", op, dtype, ins, runs=2)
+    check(out, O.allreduce(O.RING_CHUNKED, op, dtype, ins))
+
+
+@pytest.mark.parametrize("nin,nout", [(0, 1), (1, 1), (2, 2)])
+def test_fn_host_buffers_through_bounce_block(bounce_only, nin, nout):
+    """gloo_amd.allreduce on pageable host buffers: the staged path (one
+    input or in place, one output) and the whole-buffer path (several)."""
+    from test_allreduce_fn_gpu import host_allreduce_fn
+    P, N = 3, (3 << 20) + 5
+    data = case_inputs(P, N, O.FLOAT32, max(nin, nout), 0, seed=73)
+    if nin == 0:
+        ins, outs = [[] for _ in range(P)], [row[:nout] for row in data]
+    else:
+        ins = [row[:nin] for row in data]
+        outs = [[np.zeros(N, np.float32) for _ in range(nout)] for _ in range(P)]
+    got = host_allreduce_fn(1, O.SUM, O.FLOAT32, ins, outs, runs=2)
+    exp = O.allreduce_fn(O.FN_RING, O.SUM, O.FLOAT32, ins, outs)
+    for r in range(P):
+        for i in range(nout):
+            assert np.array_equal(got[r][i].view(np.uint32), exp[r][i].view(np.uint32)), (r, i)
+
+
+def _hip_memory_type(ptr):
+    """hipPointerGetAttributes(ptr).type through the HIP runtime the library
+    uses: 1 = hipMemoryTypeHost (pinned or registered), anything else (or an
+    error) = memory the runtime does not know."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    attr = (ctypes.c_byte * 128)()
+    rc = hip.hipPointerGetAttributes(ctypes.byref(attr), ctypes.c_void_p(ptr))
+    if rc != 0:
+        hip.hipGetLastError()
+        return None
+    return ctypes.cast(attr, ctypes.POINTER(ctypes.c_int))[0]
+
+
+@pytest.mark.parametrize("limit", [0, 4096], ids=["mirror", "bounce"])
+def test_caller_pages_stay_unregistered(limit):
+    """while an algorithm lives on a pageable host buffer, and
+    after it ran, the caller's pages are unknown to the HIP runtime (no
+    hipHostRegister of caller memory: the round-3 illegal address)."""
+    import gloo_amd
+    P, N = 2, (1 << 20) + 7
+    ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=74)
+    bufs = [np.array(row[0], copy=True) for row in ins]
+    store = gloo_amd.rendezvous.HashStore()
+    kinds = {}
+    gloo_amd.set_pinned_mirror_limit(limit)
+    try:
+        def rank_fn(r):
+            ctx = gloo_amd.rendezvous.Context(r, P, 0)
+            ctx.setTimeout(60)
+            ctx.connectFullMesh(store)
+            alg = gloo_amd.AllreduceRingChunked(ctx, [bufs[r]], schedule="ring")
+            alg.run()
+            kinds[r] = (_hip_memory_type(bufs[r].ctypes.data),
+                        _hip_memory_type(bufs[r].ctypes.data + 4 * (N - 1)))
+            alg.close()
+            ctx.close()
+            return True
+        run_ranks(P, rank_fn, timeout=120)
+    finally:
+        gloo_amd.set_pinned_mirror_limit(0)
+    assert all(k != 1 for r in range(P) for k in kinds[r]), kinds
+    check([[b] for b in bufs], O.allreduce(O.RING_CHUNKED, O.SUM, O.FLOAT32, ins))

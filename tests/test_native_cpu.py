@@ -107,3 +107,34 @@ def test_algorithm_needs_connected_context():
     c = gloo_amd.rendezvous.Context(0, 2)
     with pytest.raises(gloo_amd.EnforceNotMet, match="connect"):
         gloo_amd.AllreduceRingChunked(c, [1 << 20], count=16, dtype=5)
+
+
+def test_library_never_registers_or_copies_caller_host_pages():
+    """DESIGN.md 9 (the round-3 illegal address): the library must not hand
+    a caller's host pages to the runtime.  It imports neither
+    hipHostRegister nor hipHostUnregister, and every host<->device copy of
+    the staging code reads or writes a pointer that is pinned: the caller's
+    own when already pinned (isPinnedHost), else a mirror or bounce block the
+    library took from hipHostMalloc."""
+    import shutil
+    import subprocess
+    nm = shutil.which("nm")
+    if nm is None:
+        pytest.skip("no nm")
+    out = subprocess.run([nm, "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    imported = {line.split()[-1].split("@")[0] for line in out.splitlines() if line.strip()}
+    assert "hipHostMalloc" in imported  # the mirrors' allocator (sanity: nm saw the imports)
+    assert not {"hipHostRegister", "hipHostUnregister"} & imported
+    # the staging copies: the host side is `.dma` (pinned by construction),
+    # a mirror / bounce block, or a pointer that passed isPinnedHost
+    src = open(os.path.join(ROOT, "gloo_amd", "csrc", "executor_host.cc")).read()
+    copies = re.findall(r"hipMemcpyAsync\(([^;]*?)\);", src, flags=re.S)
+    assert copies
+    for args in copies:
+        a = [x.strip() for x in args.split(",")]
+        kind = a[3]
+        host = a[1] if kind == "hipMemcpyHostToDevice" else a[0]
+        if kind not in ("hipMemcpyHostToDevice", "hipMemcpyDeviceToHost"):
+            continue
+        assert re.search(r"\.dma\b|\bb\.p\b|\bsrc\b|outDma\[i\]", host), (host, args)

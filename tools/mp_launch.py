@@ -4,7 +4,14 @@ each, MASTER_ADDR=127.0.0.1), optionally with rank 0 under rocprofv3 -- a
 stand-in for torchrun when one rank needs a profiler in front of it.  This
 launcher never touches the GPU; every rank is its own child process.
 
-    python tools/mp_launch.py --nproc 2 [--prof-dir D] -- bench.py --gpus 2 ...
+    python tools/mp_launch.py --nproc 2 [--prof-dir D] [--pmc COUNTER] -- bench.py --gpus 2 ...
+
+--pmc runs rank 0 under `rocprofv3 --pmc COUNTER` (one counter group per
+pass: FETCH_SIZE and WRITE_SIZE do not fit one pass on gfx950) instead of
+the kernel trace; tools/pmc_traffic.py reads the two passes' directories.
+On a box where the ranks share one GPU the TCC counters are device-wide, so
+a dispatch of rank 0 also counts what the other ranks' kernels moved in the
+same window (DESIGN.md 4 says how the per-rank figure is derived).
 """
 import argparse
 import os
@@ -18,6 +25,9 @@ def main():
     ap.add_argument("--port", type=int, default=29581)
     ap.add_argument("--prof-dir", default=None,
                     help="rank 0 runs under rocprofv3 --kernel-trace --stats, output here")
+    ap.add_argument("--pmc", default=None,
+                    help="with --prof-dir: rank 0 runs under rocprofv3 --pmc <this> instead")
+    ap.add_argument("--prof-name", default="rank0", help="rocprofv3 -o name")
     ap.add_argument("cmd", nargs=argparse.REMAINDER)
     a = ap.parse_args()
     cmd = a.cmd[1:] if a.cmd and a.cmd[0] == "--" else a.cmd
@@ -28,8 +38,9 @@ def main():
                    MASTER_PORT=str(a.port), HSA_ENABLE_IPC_MODE_LEGACY="0")
         argv = [sys.executable] + cmd
         if r == 0 and a.prof_dir:
-            argv = ["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv",
-                    "-d", a.prof_dir, "-o", "rank0", "--"] + argv
+            what = ["--pmc"] + a.pmc.split(",") if a.pmc else ["--kernel-trace", "--stats"]
+            argv = ["rocprofv3"] + what + ["--output-format", "csv",
+                                           "-d", a.prof_dir, "-o", a.prof_name, "--"] + argv
         procs.append(subprocess.Popen(argv, env=env))
     rc = 0
     for p in procs:
