@@ -31,7 +31,6 @@ class LinkProbe {
   size_t busiestLinkBytes(int pattern) const;
 
  private:
-  size_t piece() const;
   void issue(int pattern, int engine, int blocks);
 
   std::shared_ptr<Context> ctx_;

@@ -417,12 +417,13 @@ int glx_context_ipc_stats(glx_context* ctx, int64_t* imports, int64_t* base_fixu
 int glx_context_peer_info(glx_context* ctx, int peer, int* info);
 
 /* ---- measured link ceilings ----------------------------------
- * A receive block of `bytes` per rank, exported and imported through the
- * context's own canary-checked IPC path (the one every engine uses) and
- * uncached like the engines' landing regions.  create is collective (every
- * rank, same bytes, in the same order as its other creations).  run writes
- * `reps` rounds, pattern 0 = ring (`bytes` to rank+1) or 1 = mesh
- * (bytes/(P-1) to every peer), engine 0 = hipMemcpyPeerAsync (one stream per
+ * A receive block of (P-1) x `bytes` per rank, exported and imported
+ * through the context's own canary-checked IPC path (the one every engine
+ * uses) and uncached like the engines' landing regions.  create is
+ * collective (every rank, same bytes, in the same order as its other
+ * creations).  run writes `reps` rounds, pattern 0 = ring (`bytes` to
+ * rank+1) or 1 = mesh (`bytes` to every peer: the same volume on each of the
+ * P-1 links), engine 0 = hipMemcpyPeerAsync (one stream per
  * destination) or 1 = the copy kernel (`blocks` workgroups shared by the
  * destinations), and returns this rank's seconds and the bytes one round
  * puts on its busiest link.  run is NOT synchronising: callers barrier

@@ -116,6 +116,66 @@ def test_north_star_block_p8():
     assert abs(ns["link_frac"] - 3.0704 / 3.5) < 1e-3
 
 
+def _ring_run(t, engine, tr):
+    return {"t": t, "p50": t, "engine": engine, "hbm": 100 * (256 << 20) // 16,
+            "transport": "x", "tr": tr, "fast": False, "sync": "narrow"}
+
+
+def test_north_star_section_carries_both_rings():
+    """the plan kernel (CU stores) and the host-issued DMA ring
+    both appear, each with its own link fraction, measured-link fraction
+    against the probe of ITS transport, and reference-digest match; the top
+    level repeats the faster one."""
+    S = 256 << 20
+    links = {"ring_dma_GBps": 140.0, "ring_kernel_GBps": 120.0}
+    runs = {"ring_chunked": _ring_run(3.5e-3, "devsteps", ("dma", 1, 0)),
+            "ring_chunked_host": _ring_run(3.3e-3, "steps", ("dma", 1, 0))}
+    ns = bench.north_star_section(S, 8, runs, links,
+                                  {"ring_chunked": True, "ring_chunked_host": True}, {})
+    pk, host = ns["rings"]["ring_chunked"], ns["rings"]["ring_chunked_host"]
+    for b in (pk, host):
+        for k in ("ms_per_step", "link_frac", "measured_link_frac", "reference_digest_match"):
+            assert k in b, (k, b)
+    assert pk["measured_link"] == "ring_kernel_GBps" and host["measured_link"] == "ring_dma_GBps"
+    assert abs(pk["measured_link_frac"] - pk["link_GBps"] / 120.0) < 1e-3
+    assert ns["candidate"] == "ring_chunked_host"  # the faster one
+    # one of them failed: it still appears, with its error
+    ns = bench.north_star_section(S, 8, {"ring_chunked": runs["ring_chunked"]}, None, {},
+                                  {"ring_chunked_host": "IoException: boom"})
+    assert ns["rings"]["ring_chunked_host"] == {"error": "IoException: boom"}
+    assert ns["candidate"] == "ring_chunked" and "measured_link_frac" not in ns
+    ns = bench.north_star_section(S, 8, {}, None, {}, {})
+    assert "error" in ns and set(ns["rings"]) == set(bench.NS_RINGS)
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 5, 8])
+@pytest.mark.parametrize("mib", [4, 256, 1024])
+def test_link_probe_moves_at_least_the_candidates_per_link_volume(world, mib):
+    """the probe's ceiling for a pattern must come from at
+    least the per-link volume the candidates move in one run -- the mesh's
+    2S/P per link, a ring chunk S/2P per step -- and never from a
+    latency-bound size (>= 64 MiB), on every link the pattern uses."""
+    gloo_amd = pytest.importorskip("gloo_amd")
+    S = mib << 20
+    b = bench.probe_link_bytes(S, world)
+    n = S // 4
+    mesh = bench.busiest_link_bytes(gloo_amd, "ring_chunked_mesh_steps", 0, world, n, 4)
+    ring_chunk = S // (2 * world)
+    assert b >= mesh and b >= ring_chunk and b >= 64 << 20 and b % 4096 == 0
+    assert bench.PROBE_REPS >= 10 and bench.PROBE_BLOCKS >= 512
+
+
+def test_twoshot_hbm_bytes_p8():
+    assert bench.twoshot_hbm_bytes(256 << 20, 8) == int(5.5 * (256 << 20))
+
+
+def test_n_gt_1_traffic_record_is_keyed_by_candidate():
+    rec = bench.load_traffic("ring_chunked:f32:256MiB:P8", record=True)
+    assert rec and 0.98 < rec["hbm_bytes_per_launch"] / (6.25 * (256 << 20)) < 1.1
+    rec = bench.load_traffic("ring_chunked_mesh:f32:256MiB:P8", record=True)
+    assert rec and 0.98 < rec["hbm_bytes_per_launch"] / bench.twoshot_hbm_bytes(256 << 20, 8) < 1.1
+
+
 def test_candidate_lists_default_is_small():
     class A:
         algo, schedule, candidates, no_alt = "ring_chunked", "auto", "default", False
