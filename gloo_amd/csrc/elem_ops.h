@@ -36,7 +36,7 @@ __device__ __forceinline__ void st16(v4u* p, v4u v) {
 // Write-through stores (`sc1`): the line leaves this XCD's L2 with the store
 // instead of staying dirty there until an eviction writes it back; for a
 // stream written once that fits the Infinity Cache this is the fastest store
-// (tools/scratch/store_policy.hip, tools/tune_policy.py).  HIP has no global
+// (tools/tune_policy.py; profiles/r4j_*, r4k_*).  HIP has no global
 // store builtin with that cache policy, so the stream is written through a
 // buffer resource over its base (a compiler builtin, not inline asm: the
 // compiler then tracks the store for waitcnts and register hazards).

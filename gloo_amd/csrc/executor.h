@@ -402,7 +402,7 @@ class HipPlanExecutor : public Algorithm {
   // ranks-on-the-GPU x (hwQueuesPerProcess() + 1) stays within this many
   // hardware queues, leaving room for one more process's (measured on one
   // MI355X with a busy parent process: 2x4, 3x4, 4x4, 5x2, 6x2, 8x1
-  // co-schedule; 8x2 and 8x4 time-slice: tools/scratch/queue_oversub.py).
+  // co-schedule; 8x2 and 8x4 time-slice: profiles/r7g_queue_sweep.txt).
   static constexpr int kSharedQueueBudget = 20;
   static int hwQueuesPerProcess();
   void enforceSpan(size_t sliceElems) const;

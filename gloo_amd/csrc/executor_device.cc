@@ -135,7 +135,7 @@ bool HipPlanExecutor::deviceEnginesAvailable(const Context& ctx) {
   // dependent step waits for a rotation (8 processes x 4 queues on one
   // MI355X: ~170 ms per 1-element allreduce, 8 x 2: ~60 ms, 8 x 1 and
   // 4 x 4: < 1 ms; the suite's P=8 test timed out at 20 s: DESIGN.md 9,
-  // tools/scratch/queue_oversub.py, profiles/r7e_*, r7g_queue_sweep.txt).
+  // profiles/r7e_*, r7g_queue_sweep.txt).
   if (ctx.maxRanksPerDevice() == 1) return true;
   if (ctx.ranksShareDevice()) return false;
   // each process: its hardware queues plus an allowance of one (the
