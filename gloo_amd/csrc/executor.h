@@ -250,9 +250,10 @@ class HipPlanExecutor : public Algorithm {
   size_t hostStageBytes_ = 0;      // its size (from and back to a process-wide cache)
   // A pinned block of the process-wide cache: a whole-buffer mirror, or --
   // when no mirror of the buffer's size could be pinned (or it exceeds
-  // glx_set_pinned_mirror_limit) -- a bounce block of at most
-  // kBounceBytes that every copy goes through piece by piece, waiting for
-  // each piece (a failed pinned allocation must not fail the op)
+  // glx_set_pinned_mirror_limit) -- a bounce block of two halves of at
+  // most kBounceBytes (H2D pieces through the first, D2H ranges through the
+  // second) that every copy goes through piece by piece, waiting for each
+  // piece (a failed pinned allocation must not fail the op)
   struct PinnedBlock {
     char* p = nullptr;
     size_t bytes = 0;

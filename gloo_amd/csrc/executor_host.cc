@@ -273,7 +273,11 @@ void HipPlanExecutor::takeMirror(PinnedBlock& m, size_t bytes) {
   const size_t limit = pinnedMirrorLimit();
   m.p = (limit == 0 || bytes <= limit) ? tryTakePinned(&m.bytes) : nullptr;
   if (m.p == nullptr) {
-    m.bytes = std::min(bytes, kBounceBytes);
+    // two halves: H2D pieces read the first while D2H ranges land in the
+    // second (a class algorithm's buffer is both source and destination,
+    // and its last H2D piece may still be in flight when the first range
+    // comes back)
+    m.bytes = 2 * std::min(bytes, kBounceBytes);
     m.p = takePinned(&m.bytes);
     m.bounce = true;
   }
@@ -283,9 +287,10 @@ void HipPlanExecutor::takeMirror(PinnedBlock& m, size_t bytes) {
 
 void HipPlanExecutor::bounceIn(char* dev, const char* user, size_t n, PinnedBlock& b,
                                hipStream_t s) {
-  for (size_t at = 0; at < n; at += b.bytes) {
-    const size_t len = std::min(b.bytes, n - at);
-    GLX_HIP_CHECK(hipStreamSynchronize(s));  // the block's previous piece has been read
+  const size_t half = b.bytes / 2;  // the block's H2D half
+  for (size_t at = 0; at < n; at += half) {
+    const size_t len = std::min(half, n - at);
+    GLX_HIP_CHECK(hipStreamSynchronize(s));  // the half's previous piece has been read
     std::memcpy(b.p, user + at, len);
     GLX_HIP_CHECK(hipMemcpyAsync(dev + at, b.p, len, hipMemcpyHostToDevice, s));
   }
@@ -293,11 +298,13 @@ void HipPlanExecutor::bounceIn(char* dev, const char* user, size_t n, PinnedBloc
 
 void HipPlanExecutor::bounceOut(char* user, const char* dev, size_t n, PinnedBlock& b,
                                 hipStream_t s) {
-  for (size_t at = 0; at < n; at += b.bytes) {
-    const size_t len = std::min(b.bytes, n - at);
-    GLX_HIP_CHECK(hipMemcpyAsync(b.p, dev + at, len, hipMemcpyDeviceToHost, s));
+  const size_t half = b.bytes / 2;
+  char* out = b.p + half;  // the block's D2H half
+  for (size_t at = 0; at < n; at += half) {
+    const size_t len = std::min(half, n - at);
+    GLX_HIP_CHECK(hipMemcpyAsync(out, dev + at, len, hipMemcpyDeviceToHost, s));
     GLX_HIP_CHECK(hipStreamSynchronize(s));
-    std::memcpy(user + at, b.p, len);
+    std::memcpy(user + at, out, len);
   }
 }
 

@@ -127,7 +127,8 @@ def test_library_never_registers_or_copies_caller_host_pages():
     assert "hipHostMalloc" in imported  # the mirrors' allocator (sanity: nm saw the imports)
     assert not {"hipHostRegister", "hipHostUnregister"} & imported
     # the staging copies: the host side is `.dma` (pinned by construction),
-    # a mirror / bounce block, or a pointer that passed isPinnedHost
+    # a mirror / bounce block (b.p, its D2H half `out`), or a pointer that
+    # passed isPinnedHost (src, outDma)
     src = open(os.path.join(ROOT, "gloo_amd", "csrc", "executor_host.cc")).read()
     copies = re.findall(r"hipMemcpyAsync\(([^;]*?)\);", src, flags=re.S)
     assert copies
@@ -137,4 +138,4 @@ def test_library_never_registers_or_copies_caller_host_pages():
         host = a[1] if kind == "hipMemcpyHostToDevice" else a[0]
         if kind not in ("hipMemcpyHostToDevice", "hipMemcpyDeviceToHost"):
             continue
-        assert re.search(r"\.dma\b|\bb\.p\b|\bsrc\b|outDma\[i\]", host), (host, args)
+        assert re.search(r"\.dma\b|\bb\.p\b|\bsrc\b|\bout\b|outDma\[i\]", host), (host, args)

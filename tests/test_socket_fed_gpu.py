@@ -184,3 +184,23 @@ def test_done_ranges_polled_while_runs_are_in_flight(P):
         for snap in poll[r]:
             for o, n in snap:
                 assert 0 <= o and 0 < n and o + n <= N
+
+
+@pytest.mark.parametrize("algo", ["ring_chunked", "halving_doubling"])
+def test_socket_fed_through_bounce_block(algo):
+    """A fed run whose buffer has no whole pinned mirror (the bounce block of
+    executor_host.cc): H2D pieces are issued by the feeding thread while the
+    run's thread copies finished ranges back through the block's other half,
+    out-of-order pieces, two runs."""
+    import gloo_amd
+    gloo_amd.set_pinned_mirror_limit(4096)
+    try:
+        P, N = 3, (5 << 20) + 7
+        bufs, done, ins = fed_allreduce(algo, P, N, order="reversed", runs=2)
+    finally:
+        gloo_amd.set_pinned_mirror_limit(0)
+    code = O.HALVING_DOUBLING if algo == "halving_doubling" else O.RING_CHUNKED
+    exp = O.allreduce(code, O.SUM, O.FLOAT32, ins)
+    for r in range(P):
+        assert same_bits(bufs[r], exp[r][0]), "rank %d" % r
+        assert covered(done[r], N)
