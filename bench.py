@@ -74,6 +74,9 @@ def parse():
                    help="seconds before dumping stacks and exiting")
     p.add_argument("--kernel-only", action="store_true",
                    help="N=1: run only the timed kernel loop (for rocprofv3 --pmc)")
+    p.add_argument("--no-pmc", action="store_true",
+                   help="N=1: do not measure roofline.traffic with rocprofv3 --pmc child "
+                        "passes (the stored figure is reported instead)")
     return p.parse_args()
 
 
@@ -399,8 +402,54 @@ def multidev_check(torch, timeout=120):
     return json.loads(lines[-1])
 
 
+def live_pmc_traffic(args, timeout=90):
+    """HBM bytes per launch of the timed reduce kernel, measured in THIS run
+    (the figure used to come from a stored pass):
+    two child processes of this same command's kernel loop (--kernel-only)
+    under `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE` -- one counter
+    group per pass, as the guide prescribes for gfx950 -- started before this
+    process touches the GPU, each under its own kill timeout.  FETCH_SIZE is
+    doubled (gfx950 tallies a 128-B request as 64 B), both are KiB; the median
+    over the child's reduce launches.  None (the stored pass is used) where
+    rocprofv3 is missing or a pass fails."""
+    import shutil
+    import subprocess
+    import tempfile
+    if args.no_pmc or shutil.which("rocprofv3") is None:
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_traffic import per_launch
+    d = tempfile.mkdtemp(prefix="glx_pmc_")
+    child = [sys.executable, os.path.abspath(__file__), "--kernel-only", "--steps", "10",
+             "--warmup", "2", "--dtype", args.dtype, "--size-mib", str(args.size_mib),
+             "--no-multidev", "--no-cpu-baseline", "--no-staged", "--no-pmc"]
+    got = {}
+    try:
+        for counter, name in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+            cmd = ["timeout", "-s", "KILL", str(timeout), "rocprofv3", "--pmc", counter,
+                   "--output-format", "csv", "-d", d, "-o", name, "--"] + child
+            out = subprocess.run(cmd, capture_output=True, text=True)
+            if out.returncode != 0:
+                return {"error": "%s pass: exit %d: %s" % (counter, out.returncode,
+                                                           out.stderr[-200:])}
+            got[name] = per_launch(d, name, counter, "reduce_kernel")
+    except (OSError, SystemExit) as e:
+        return {"error": "%s: %s" % (type(e).__name__, str(e)[:200])}
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    fetch_kib, nf = got["fetch"]
+    write_kib, nw = got["write"]
+    return {"hbm_bytes_per_launch": int((2 * fetch_kib + write_kib) * 1024),
+            "fetch_bytes": int(2 * fetch_kib * 1024), "write_bytes": int(write_kib * 1024),
+            "dispatches": {"fetch": nf, "write": nw},
+            "source": "live: rocprofv3 --pmc FETCH_SIZE (x2) and WRITE_SIZE passes of this "
+                      "command's kernel loop, run as child processes of this run"}
+
+
 def bench_single(args):
     import torch
+    # counters first, in child processes, before this process touches a GPU
+    pmc = None if args.kernel_only else live_pmc_traffic(args)
     multidev = None if args.no_multidev else multidev_check(torch)
     import gloo_amd
     S = args.size_mib << 20
@@ -442,7 +491,14 @@ def bench_single(args):
     achieved = alg_bytes / t / 1e9
     workload = "local_reduce_sum_%s_%dMiB" % ({"f32": "fp32"}.get(args.dtype, args.dtype),
                                                args.size_mib)
-    traffic = load_traffic(workload)
+    if pmc and "hbm_bytes_per_launch" in pmc:
+        traffic = pmc["hbm_bytes_per_launch"]
+        traffic_src = dict(pmc, ratio=round(traffic / (3 * S), 5))
+    else:
+        traffic = load_traffic(workload)
+        traffic_src = {"source": "stored: profiles/pmc_traffic.json (the same command under "
+                                 "rocprofv3 --pmc, tools/pmc_traffic.py)",
+                       "live_error": (pmc or {}).get("error", "not run")}
     res = {
         "metric": metric_name(args.dtype),
         "value": round(S / t / 1e9, 3), "unit": "GB/s", "n_gpus": 1, "steps": steps,
@@ -454,6 +510,7 @@ def bench_single(args):
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": traffic,
+                     "traffic_pmc": traffic_src,
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "cold": cold,
                      "note": "back-to-back passes over the same 512 MiB of inputs, as the "

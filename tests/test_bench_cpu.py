@@ -271,3 +271,16 @@ def test_failure_line_is_one_json_line_with_the_error():
     d = json.loads(s)
     assert d["value"] is None and d["n_gpus"] == 8 and "every candidate failed" in d["error"]
     assert d["metric"] == bench.metric_name("f32")
+
+
+def test_live_pmc_traffic_off_and_failure_paths(monkeypatch):
+    """N = 1 roofline.traffic is measured in the run by rocprofv3 --pmc child
+    passes; --no-pmc (the children themselves) and a missing rocprofv3 fall
+    back to the stored pass."""
+    class A:
+        no_pmc, dtype, size_mib = True, "f32", 256
+    assert bench.live_pmc_traffic(A) is None
+    A.no_pmc = False
+    import shutil
+    monkeypatch.setattr(shutil, "which", lambda name: None)
+    assert bench.live_pmc_traffic(A) is None
