@@ -252,7 +252,7 @@ class AllreduceRingChunked(Algorithm):
     schedule="auto" (default) picks the data movement by size: replicated
     up to 16 MiB per rank at P=2, 2 MiB at P<=4, 1 MiB at P<=8 when the
     device-driven engines are available (256 KiB otherwise), mesh above;
-    env GLOO_AMD_RING_SCHEDULE forces one.
+    the other schedules force one.
     schedule="ring" moves chunks around the ring exactly as the
     reference does (one link per direction); schedule="mesh" computes the
     identical result (same chunks, same reduction chain and operand order)

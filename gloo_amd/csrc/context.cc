@@ -245,21 +245,13 @@ namespace {
 // Free pooled bytes kept beyond this are returned to the runtime.
 constexpr size_t kMaxFreeSharedBytes = size_t(8) << 30;
 
-// Allocation granule of a shared block (GLOO_AMD_SHARED_GRANULE, bytes;
-// default one 4 KiB page).  Round 1 rounded every block up to 2 MiB after a
+// Allocation granule of a shared block: one 4 KiB page.  Round 1 rounded every block up to 2 MiB after a
 // peer's mapping of a small block was seen pointing elsewhere; with every
 // import now checked against the exporter's canary (and corrected by the
 // published base offset if the runtime maps the allocation's base), 4 KiB
 // blocks passed 8-rank runs with ~120 checked imports per rank, no fixup and
 // no mismatch, so the granule is back to a page.
-size_t sharedGranule() {
-  static const size_t g = [] {
-    const char* e = std::getenv("GLOO_AMD_SHARED_GRANULE");
-    const long long v = e != nullptr ? std::atoll(e) : 0;
-    return v >= 4096 ? (size_t)v : (size_t)4096;
-  }();
-  return g;
-}
+size_t sharedGranule() { return 4096; }
 
 std::atomic<uint64_t> g_canary_counter{0};
 

@@ -67,23 +67,12 @@ SharedRef getRef(const std::vector<char>& b, size_t& at) {
 
 enum { DIR_IN = 0, DIR_OUT = 1 };
 
-int initialSplit() {
-  const char* e = std::getenv("GLOO_AMD_COPY_SPLIT");
-  int k = e ? std::atoi(e) : 1;
-  return k < 1 ? 1 : k;
-}
+std::atomic<int> g_copy_split{1};  // glx_set_copy_split
 
-std::atomic<int> g_copy_split{initialSplit()};
-
-// Default: hipMemcpyPeerAsync (the DMA engines); GLOO_AMD_COPY_ENGINE=kernel
+// Default: hipMemcpyPeerAsync (the DMA engines); glx_set_copy_engine(1, ...)
 // selects the copy kernel (the sending GPU's compute units store into the
 // receiver's region over xGMI).
-int initialEngine() {
-  const char* e = std::getenv("GLOO_AMD_COPY_ENGINE");
-  return (e != nullptr && std::strcmp(e, "kernel") == 0) ? 1 : 0;
-}
-
-std::atomic<int> g_copy_engine{initialEngine()};
+std::atomic<int> g_copy_engine{0};
 
 }  // namespace
 

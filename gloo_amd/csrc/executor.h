@@ -394,7 +394,7 @@ class HipPlanExecutor : public Algorithm {
  public:
   static constexpr int kEngineSteps = 0, kEngineOneShot = 1, kEngineTwoShot = 2,
                        kEngineDevSteps = 3;
-  // Whether device-driven engines can run on this context: GLOO_AMD_ONESHOT
+  // Whether device-driven engines can run on this context: setDeviceEngines
   // (0 = never, 1 = always), by default when every rank has a GPU of its
   // own, or ranks that share one are processes whose hardware queues fit
   // kSharedQueueBudget (their kernels must all run at once).  P <= 8.
@@ -410,16 +410,14 @@ class HipPlanExecutor : public Algorithm {
   // Override for algorithms created afterwards: 0 = never, 1 = always
   // (caller guarantees co-residency), -1 = automatic (the default).
   static void setDeviceEngines(int mode);
-  // Engine of the mesh schedule when available: kEngineTwoShot (default,
-  // env GLOO_AMD_MESH_ENGINE=steps overrides) or kEngineSteps.  Read at
-  // construction.
+  // Engine of the mesh schedule when available: kEngineTwoShot (default)
+  // or kEngineSteps.  Read at construction.
   static void setMeshEngine(int engine);
   static int meshEngine();
   // Engine of the ring, halving-doubling, bcube and function-style ring
-  // schedules when available: -1 = by size (default: the plan kernel up to
-  // 32 MiB per rank, env GLOO_AMD_DEVSTEPS_MAX_BYTES; host-issued steps
-  // above), kEngineDevSteps or kEngineSteps (env
-  // GLOO_AMD_STEPS_ENGINE=device|host).
+  // schedules when available: -1 = automatic (default: the plan kernel with
+  // one rank per GPU; ranks sharing a GPU: up to 32 MiB per rank, host-issued
+  // steps above), kEngineDevSteps or kEngineSteps.
   static void setStepsEngine(int engine);
   static int stepsEngine();
   // Streams of the device-driven kernels for algorithms created afterwards:

@@ -30,30 +30,17 @@ using namespace exec;  // NOLINT: the executor's own helpers
 
 namespace {
 
-int initialMeshEngine() {
-  const char* e = std::getenv("GLOO_AMD_MESH_ENGINE");
-  if (e != nullptr && std::strcmp(e, "steps") == 0) return HipPlanExecutor::kEngineSteps;
-  return HipPlanExecutor::kEngineTwoShot;
-}
+// Process-wide engine choices (glx_set_mesh_engine / glx_set_steps_engine;
+// no environment overrides: every rank's process must choose alike).
+std::atomic<int> g_mesh_engine{HipPlanExecutor::kEngineTwoShot};
 
-std::atomic<int> g_mesh_engine{initialMeshEngine()};
+// -1 = by size (the plan kernel up to kDevStepsMaxBytes per rank when ranks
+// share a GPU, where its per-step flag round trips beat host-issued steps;
+// host-issued steps with their wide copy and reduce launches above), else a
+// fixed engine.
+std::atomic<int> g_steps_engine{-1};
 
-// -1 = by size (the plan kernel up to kDevStepsMaxBytes per rank, where its
-// per-step flag round trips beat host-issued steps; host-issued steps with
-// their wide copy and reduce launches above), else a fixed engine.
-int initialStepsEngine() {
-  const char* e = std::getenv("GLOO_AMD_STEPS_ENGINE");
-  if (e != nullptr && std::strcmp(e, "host") == 0) return HipPlanExecutor::kEngineSteps;
-  if (e != nullptr && std::strcmp(e, "device") == 0) return HipPlanExecutor::kEngineDevSteps;
-  return -1;
-}
-
-int64_t devStepsMaxBytes() {
-  const char* e = std::getenv("GLOO_AMD_DEVSTEPS_MAX_BYTES");
-  return e != nullptr ? std::atoll(e) : (int64_t(32) << 20);
-}
-
-std::atomic<int> g_steps_engine{initialStepsEngine()};
+constexpr int64_t kDevStepsMaxBytes = int64_t(32) << 20;
 
 }  // namespace
 
@@ -105,14 +92,7 @@ int HipPlanExecutor::engineStreams() { return g_engine_streams.load(); }
 
 namespace {
 
-int initialDeviceEngines() {
-  const char* e = std::getenv("GLOO_AMD_ONESHOT");
-  if (e != nullptr && e[0] == '0') return 0;
-  if (e != nullptr && e[0] == '1') return 1;
-  return -1;
-}
-
-std::atomic<int> g_device_engines{initialDeviceEngines()};
+std::atomic<int> g_device_engines{-1};  // glx_set_device_engines
 
 }  // namespace
 
@@ -162,12 +142,10 @@ int HipPlanExecutor::engineFor(const Context& ctx, int algo, int64_t count, int 
     // auto: the plan kernel, at every size when every rank has a GPU of its
     // own (it takes the host's round trip out of each of the ring's 4P-4
     // dependent hops); with ranks sharing a GPU (rehearsals)
-    // only up to devStepsMaxBytes(), where it was measured faster there.
+    // only up to kDevStepsMaxBytes, where it was measured faster there.
     // Every rank sees every endpoint, so all choose alike.
-    if (ctx.maxRanksPerDevice() == 1 && std::getenv("GLOO_AMD_DEVSTEPS_MAX_BYTES") == nullptr) {
-      return kEngineDevSteps;
-    }
-    return count * esize <= devStepsMaxBytes() ? kEngineDevSteps : kEngineSteps;
+    if (ctx.maxRanksPerDevice() == 1) return kEngineDevSteps;
+    return count * esize <= kDevStepsMaxBytes ? kEngineDevSteps : kEngineSteps;
   }
   return kEngineSteps;
 }

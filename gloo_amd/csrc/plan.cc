@@ -707,12 +707,6 @@ int autoRingSchedule(int size, int64_t bytes, bool fn, bool deviceDriven) {
   const int ring = fn ? ALGO_FN_RING : ALGO_RING_CHUNKED;
   const int mesh = fn ? ALGO_FN_RING_MESH : ALGO_RING_CHUNKED_MESH;
   const int repl = fn ? ALGO_FN_RING_REPL : ALGO_RING_CHUNKED_REPL;
-  if (const char* e = std::getenv("GLOO_AMD_RING_SCHEDULE")) {
-    const std::string v(e);
-    if (v == "ring") return ring;
-    if (v == "mesh") return mesh;
-    if (v == "replicated") return repl;
-  }
   // host-mediated: the reference's kOnDeviceThreshold (algorithm.cc:16).
   // Device-driven: one-shot moves S per link in one round, two-shot 2S/P per
   // link in two; with a round costing L and links B, one-shot wins below
@@ -722,7 +716,6 @@ int autoRingSchedule(int size, int64_t bytes, bool fn, bool deviceDriven) {
     maxRepl = size <= 2 ? (int64_t(16) << 20) : size <= 4 ? (int64_t(2) << 20)
                                                           : (int64_t(1) << 20);
   }
-  if (const char* e = std::getenv("GLOO_AMD_REPLICATED_MAX_BYTES")) maxRepl = std::atoll(e);
   if (size <= 1) return ring;
   return bytes <= maxRepl ? repl : mesh;
 }

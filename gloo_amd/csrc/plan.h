@@ -120,9 +120,8 @@ Plan makePlan(int algo, int rank, int size, int64_t count,
 // mesh above.  fn: the function-style RING family instead of the class
 // ring_chunked one.  deviceDriven: the replicated schedule will run as the
 // one-shot kernel (no host round trips), which moves the threshold from
-// 256 KiB to 16 MiB (P = 2), 2 MiB (P <= 4) or 1 MiB (P <= 8).  Env
-// GLOO_AMD_RING_SCHEDULE=ring|mesh|replicated forces one;
-// GLOO_AMD_REPLICATED_MAX_BYTES sets the threshold.
+// 256 KiB to 16 MiB (P = 2), 2 MiB (P <= 4) or 1 MiB (P <= 8).  (An
+// explicit schedule -- "ring", "mesh", "replicated" -- forces one.)
 int autoRingSchedule(int size, int64_t bytes, bool fn, bool deviceDriven = false);
 
 // Geometry of the device-driven engines (xgmi_kernels.hip), read off a

@@ -134,7 +134,7 @@ int glx_tune_reduce(int unroll, int blocks_per_cu, int nontemporal);
 
 /* Split every peer copy of algorithms created afterwards over k streams per
  * destination (k DMA engines feeding one link; parts >= 1 MiB).  Default 1,
- * or $GLOO_AMD_COPY_SPLIT. */
+ * (every rank's process alike). */
 int glx_set_copy_split(int k);
 /* Host-memory endpoints: a pageable buffer is staged through a pinned mirror
  * of its size (the reference's CudaHostWorkspace, gloo/cuda_workspace.h:20);
@@ -145,26 +145,27 @@ int glx_set_pinned_mirror_limit(size_t bytes);
 /* How peer copies are made by algorithms created afterwards: engine 0 =
  * hipMemcpyPeerAsync (DMA copy engines, default), 1 = a copy kernel storing
  * into the peer's memory over xGMI, with `blocks` workgroups (<= 0: keep).
- * Env GLOO_AMD_COPY_ENGINE=kernel selects 1 at load time. */
+ * Default 0. */
 int glx_set_copy_engine(int engine, int blocks);
 /* Engine of the mesh schedule (ring_chunked's result over all links) for
  * algorithms created afterwards, when device-driven engines are available
  * (ranks on distinct devices or processes, P <= 8): GLX_ENGINE_TWOSHOT (one
  * device-driven kernel per rank, default) or GLX_ENGINE_STEPS (host-issued
- * copies and fold kernels).  Env GLOO_AMD_MESH_ENGINE=steps at load time. */
+ * copies and fold kernels). */
 int glx_set_mesh_engine(int engine);
 /* Device-driven engines for algorithms created afterwards: 0 = never (every
  * schedule runs as host-issued steps), 1 = always (the caller guarantees the
- * ranks' kernels can run concurrently), -1 = automatic (default: when no two
- * ranks are threads sharing one device).  Env GLOO_AMD_ONESHOT=0/1. */
+ * ranks' kernels can run concurrently), -1 = automatic (default: one rank
+ * per GPU always; processes sharing a GPU while ranks x (queues + 1) <= 20,
+ * queues = the largest GPU_MAX_HW_QUEUES any rank published; never threads
+ * sharing one device). */
 int glx_set_device_engines(int mode);
 /* Engine of the ring, halving-doubling, bcube and function-style ring
  * schedules for algorithms created afterwards, when device-driven engines
  * are available: -1 = automatic (default: the plan kernel -- at every size
- * with one rank per GPU, up to 32 MiB per rank when ranks share a GPU or
- * env GLOO_AMD_DEVSTEPS_MAX_BYTES is set, host-issued steps above),
- * GLX_ENGINE_DEVSTEPS (the plan kernel) or GLX_ENGINE_STEPS (host-issued
- * steps).  Env GLOO_AMD_STEPS_ENGINE=device|host. */
+ * with one rank per GPU, up to 32 MiB per rank when ranks share a GPU,
+ * host-issued steps above), GLX_ENGINE_DEVSTEPS (the plan kernel) or
+ * GLX_ENGINE_STEPS (host-issued steps). */
 int glx_set_steps_engine(int engine);
 /* Cache policy of the plan kernel's own loads and stores for algorithms
  * created afterwards: -1 automatic (default: plain, except nontemporal loads
@@ -282,8 +283,8 @@ enum glx_algo {
   GLX_ALGO_RING_CHUNKED_REPL = 6,
   GLX_ALGO_FN_RING_REPL = 7,
   /* AllreduceRingChunked's result, data movement chosen at creation:
-   * replicated up to 256 KiB per rank, mesh above (GLOO_AMD_RING_SCHEDULE /
-   * GLOO_AMD_REPLICATED_MAX_BYTES override) */
+   * replicated up to 256 KiB per rank (16 / 2 / 1 MiB at P = 2 / <= 4 / <= 8
+   * on the device-driven engines), mesh above */
   GLX_ALGO_RING_CHUNKED_AUTO = 8
 };
 glx_algorithm* glx_allreduce_create(glx_context* ctx, int algo, void* const* ptrs,
@@ -329,8 +330,8 @@ enum glx_allreduce_algorithm {
  * max_segment_size.  The first call with a given combination sets up and
  * exchanges receive buffers with the peers (once; later calls reuse them).
  * UNSPECIFIED computes RING's result with the data movement chosen per
- * size (replicated up to 256 KiB per rank, mesh above; GLOO_AMD_RING_SCHEDULE
- * forces ring|mesh|replicated). */
+ * size (replicated up to 256 KiB per rank -- 16 / 2 / 1 MiB at P = 2 /
+ * <= 4 / <= 8 on the device-driven engines -- mesh above). */
 int glx_allreduce(glx_context* ctx, int algorithm, int dtype, int op,
                   void* const* inputs, int num_inputs, void* const* outputs,
                   int num_outputs, size_t elements, uint32_t tag,
