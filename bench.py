@@ -947,6 +947,10 @@ DEFAULT_ALTS = ["halving_doubling"]
 EXTRA_ALTS = ["halving_doubling_host", "halving_doubling_system"]
 # host-issued steps' peer-copy transports: (engine, DMA split, copy-kernel workgroups)
 TRANSPORTS_DEFAULT = [("dma", 1, 0), ("kernel", 1, 128)]
+# the north star's own transport for the host-issued ring: hipMemcpyPeerAsync
+# on side streams, the copy split over 1, 2 or 4 DMA engines per link (CU
+# stores are the plan kernel's ring, the other half of north_star.rings)
+TRANSPORTS_DMA = [("dma", 1, 0), ("dma", 2, 0), ("dma", 4, 0)]
 TRANSPORTS_ALL = [("dma", 1, 0), ("dma", 2, 0), ("dma", 4, 0), ("kernel", 1, 32),
                   ("kernel", 1, 64), ("kernel", 1, 128), ("kernel", 1, 256)]
 
@@ -1140,7 +1144,8 @@ def bench_multi(args):
         device_engine = probe.engine() != "steps"
         probe.close()
         if args.copy_split == "auto" and not device_engine:
-            for tr in transports:
+            for tr in (TRANSPORTS_DMA if algo == "ring_chunked_host" and args.calibrate != "all"
+                       else transports):
                 set_transport(tr)
                 buf.copy_(src)
                 calib[tr], _ = time_schedule(torch, dist, gloo_amd, ctx, buf, algo, 3, 1)
