@@ -13,8 +13,10 @@ from . import _lib  # noqa: F401  (raises ImportError if the HIP build is missin
 from . import math, rendezvous  # noqa: F401
 from .algorithms import (  # noqa: F401
     AllreduceHalvingDoubling,
+    AllreduceRing,
     AllreduceRingChunked,
     HipAllreduceHalvingDoubling,
+    HipAllreduceRing,
     HipAllreduceRingChunked,
     ReductionFunction,
     ReductionType,

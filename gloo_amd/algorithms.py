@@ -124,7 +124,9 @@ ALGO_CODES = {"ring_chunked": 0, "halving_doubling": 1, "ring_chunked_mesh": 2,
               # one-round variants for small buffers
               "ring_chunked_repl": 6, "fn_ring_repl": 7,
               # creation-time choice among the ring_chunked schedules
-              "ring_chunked_auto": 8}
+              "ring_chunked_auto": 8,
+              # class AllreduceRing (whole buffers, each rank's own left fold)
+              "ring": 9}
 
 
 class Algorithm:
@@ -277,9 +279,20 @@ class AllreduceHalvingDoubling(Algorithm):
     _algo = ALGO_CODES["halving_doubling"]
 
 
+class AllreduceRing(Algorithm):
+    """gloo::AllreduceRing<T> (gloo/allreduce_ring.h:20): every rank ends
+    with its own left fold x[r] op x[r-1] op ... op x[r-P+1] of the ranks'
+    (locally reduced) buffers, as the reference's P-1 forwarding rounds
+    compute it -- so float results may differ between ranks, exactly as in
+    the reference.  The data moves in one round over every link (each rank
+    sends its buffer to every peer) instead of P-1 dependent ring rounds."""
+    _algo = ALGO_CODES["ring"]
+
+
 # The device classes under the names the reference's GPU path uses.
 HipAllreduceRingChunked = AllreduceRingChunked
 HipAllreduceHalvingDoubling = AllreduceHalvingDoubling
+HipAllreduceRing = AllreduceRing
 
 
 DEFAULT_MIN_PIECE_BYTES = 4 << 20

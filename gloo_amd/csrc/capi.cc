@@ -380,7 +380,8 @@ glx_algorithm* glx_allreduce_create(glx_context* ctx, int algo, void* const* ptr
                                  /*fn=*/false, gloo::HipPlanExecutor::deviceEnginesAvailable(*ctx->c));
   }
   if (algo != GLX_ALGO_RING_CHUNKED && algo != GLX_ALGO_HALVING_DOUBLING &&
-      algo != GLX_ALGO_RING_CHUNKED_MESH && algo != GLX_ALGO_RING_CHUNKED_REPL) {
+      algo != GLX_ALGO_RING_CHUNKED_MESH && algo != GLX_ALGO_RING_CHUNKED_REPL &&
+      algo != GLX_ALGO_RING) {
     fail(GLX_ERR_INVALID, "glx_allreduce_create: unknown algorithm");
     return nullptr;
   }

@@ -383,6 +383,33 @@ Plan replicatedPlan(int rank, int size, int64_t count, Range range, Chain chain)
   return p;
 }
 
+// AllreduceRing (gloo/allreduce_ring.h:81-110): round k hands rank r the
+// locally reduced buffer of rank r-1-k (forwarded by the ranks between), and
+// ptrs[0] = op(ptrs[0], inbox) (:94): a left fold over r, r-1, ..., r-P+1.
+Plan planRing(int rank, int size, int64_t count) {
+  if (count == 0 || size == 1) return Plan();
+  Plan p;
+  const int64_t region = count + kPadElems;
+  p.scratch_elems = (int64_t)size * region;  // one whole-buffer region per source rank
+  for (int d = 1; d < size; d++) {
+    const int j = (rank + d) % size;
+    p.steps.push_back({SEND, j, 2, 0, count, 0, (int64_t)rank * region, 0});
+    p.bytes_sent += count;
+  }
+  std::vector<int64_t> srcs = {-1};  // acc = ptrs[0] (the local fold)
+  for (int d = 1; d < size; d++) {
+    const int k = (rank - d + size) % size;
+    p.steps.push_back({RECV, k, 2, 0, count, (int64_t)k * region, 0, 0});
+    srcs.push_back((int64_t)k * region);
+  }
+  p.folds.push_back(srcs);
+  p.steps.push_back({FOLD, -1, (int64_t)srcs.size(), 0, count, 0, 0, kFoldLeft | kFoldWhole});
+  for (int d = 1; d < size; d++) {
+    p.steps.push_back({RELEASE, (rank - d + size) % size, 2, 0, 0, 0, 0, 0});
+  }
+  return p;
+}
+
 // ring_chunked (gloo/allreduce_ring_chunked.h:106-158) reduces chunk pair j
 // (chunks 2j, 2j+1) along ranks j, j+1, ..., j+P-1: rank j+k computes
 // op(x[j+k], partial) in place.  The broadcast pass (:163-200) becomes the
@@ -731,6 +758,7 @@ Plan makePlan(int algo, int rank, int size, int64_t count, const PlanParams& prm
     case ALGO_FN_BCUBE: return planFnBcube(rank, size, count);
     case ALGO_RING_CHUNKED_REPL: return planRingChunkedReplicated(rank, size, count);
     case ALGO_FN_RING_REPL: return planFnRingReplicated(rank, size, count, prm);
+    case ALGO_RING: return planRing(rank, size, count);
   }
   fail("unknown algorithm");
   return Plan();

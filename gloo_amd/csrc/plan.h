@@ -61,6 +61,7 @@ enum Algo {
   ALGO_FN_BCUBE = 5,           // gloo::allreduce(opts), Algorithm::BCUBE
   ALGO_RING_CHUNKED_REPL = 6,  // ring_chunked's result in one round (small buffers)
   ALGO_FN_RING_REPL = 7,       // RING's result in one round (small buffers)
+  ALGO_RING = 9,               // class AllreduceRing (whole buffers, per-rank order)
 };
 
 constexpr int64_t kFoldLeft = 1;  // FOLD flag, see above
@@ -111,6 +112,13 @@ Plan planFnRingReplicated(int rank, int size, int64_t count, const PlanParams& p
 
 // gloo/allreduce.cc:395-669 (bcube, n = 2)
 Plan planFnBcube(int rank, int size, int64_t count);
+// AllreduceRing (gloo/allreduce_ring.h:72-114): every rank ends with its own
+// left fold x[r] op x[r-1] op ... op x[r-P+1] of the locally reduced buffers
+// (ranks' float results may differ, as in the reference).  The reference
+// forwards whole buffers around the ring in P-1 dependent rounds; here every
+// rank sends its buffer to every peer in one round (P-1 links, S each) and
+// folds in the reference's order.
+Plan planRing(int rank, int size, int64_t count);
 
 Plan makePlan(int algo, int rank, int size, int64_t count,
               const PlanParams& prm = PlanParams());

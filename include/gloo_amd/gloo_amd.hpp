@@ -333,6 +333,10 @@ inline glx_algorithm* createAuto(glx_context* c, void* const* p, int n, int coun
                                  int op, const glx_stream_t* s, int ns) {
   return glx_allreduce_create(c, GLX_ALGO_RING_CHUNKED_AUTO, p, n, count, dt, op, s, ns);
 }
+inline glx_algorithm* createRingWhole(glx_context* c, void* const* p, int n, int count, int dt,
+                                      int op, const glx_stream_t* s, int ns) {
+  return glx_allreduce_create(c, GLX_ALGO_RING, p, n, count, dt, op, s, ns);
+}
 }  // namespace detail
 
 // gloo::CudaHostWorkspace<T> / CudaDeviceWorkspace<T> analogs
@@ -390,6 +394,20 @@ class HipAllreduceHalvingDoubling : public detail::DeviceAllreduce<T> {
 
  private:
   bool pipelined_ = false;
+};
+
+// gloo::CudaAllreduceRing<T, W> / AllreduceRing<T> analog
+// (gloo/cuda_allreduce_ring.h:17-24, gloo/allreduce_ring.h:20): each rank's
+// own left fold x[r] op x[r-1] op ... (float results may differ between
+// ranks, as in the reference).
+template <typename T, typename W = HipHostWorkspace<T>>
+class HipAllreduceRing : public detail::DeviceAllreduce<T> {
+ public:
+  static const char* workspace() { return W::kName; }
+  HipAllreduceRing(const std::shared_ptr<Context>& ctx, const std::vector<T*>& ptrs, int count,
+                   const std::vector<glx_stream_t>& streams = {},
+                   const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
+      : detail::DeviceAllreduce<T>(&detail::createRingWhole, ctx, ptrs, count, streams, fn) {}
 };
 
 // gloo::CudaAllreduceHalvingDoublingPipelined<T, W> analog

@@ -285,7 +285,12 @@ enum glx_algo {
   /* AllreduceRingChunked's result, data movement chosen at creation:
    * replicated up to 256 KiB per rank (16 / 2 / 1 MiB at P = 2 / <= 4 / <= 8
    * on the device-driven engines), mesh above */
-  GLX_ALGO_RING_CHUNKED_AUTO = 8
+  GLX_ALGO_RING_CHUNKED_AUTO = 8,
+  /* gloo::AllreduceRing<T> (gloo/allreduce_ring.h:20): each rank's left fold
+   * of the ranks' buffers starting from its own, r, r-1, ..., r-P+1 (float
+   * results may differ between ranks, as in the reference); whole buffers,
+   * one round over every link instead of P-1 forwarding rounds */
+  GLX_ALGO_RING = 9
 };
 glx_algorithm* glx_allreduce_create(glx_context* ctx, int algo, void* const* ptrs,
                                     int nptrs, int count, int dtype, int op,

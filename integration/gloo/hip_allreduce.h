@@ -7,6 +7,8 @@
 //                                       (gloo/cuda_allreduce_ring_chunked.h:19-26)
 //   HipAllreduceHalvingDoubling<T, W> ~ CudaAllreduceHalvingDoubling<T, W>
 //                                       (gloo/cuda_allreduce_halving_doubling.h:22-30)
+//   HipAllreduceRing<T, W>            ~ CudaAllreduceRing<T, W>
+//                                       (gloo/cuda_allreduce_ring.h:17-24)
 //   HipAllreduceHalvingDoublingPipelined<T, W>
 //                                     ~ CudaAllreduceHalvingDoublingPipelined<T, W>
 //                                       (gloo/cuda_allreduce_halving_doubling_pipelined.h:13-27)
@@ -602,6 +604,29 @@ class HipAllreduceHalvingDoubling : public hip::Allreduce<T> {
 
  private:
   bool pipelined_ = false;
+};
+
+// ~ CudaAllreduceRing<T, W> (gloo/cuda_allreduce_ring.h:17-24) and the CPU
+// AllreduceRing<T> (gloo/allreduce_ring.h:20): each rank's own left fold
+// x[r] op x[r-1] op ... op x[r-P+1] (float results may differ between ranks,
+// as in the reference); whole buffers, one round over every link.
+template <typename T, typename W = HipHostWorkspace<T>>
+class HipAllreduceRing : public hip::Allreduce<T> {
+  static_assert(hip::IsWorkspace<T, W>::value,
+                "W must be HipHostWorkspace<T> or HipDeviceWorkspace<T>");
+
+ public:
+  static const char* workspace() { return W::kName; }
+  HipAllreduceRing(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs,
+                   const int count,
+                   const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
+                   const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
+      : hip::Allreduce<T>(GLX_ALGO_RING, context, nullptr, ptrs, count, streams, fn) {}
+  HipAllreduceRing(const std::shared_ptr<Context>& context, rendezvous::Store& store,
+                   const std::vector<T*>& ptrs, const int count,
+                   const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
+                   const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
+      : hip::Allreduce<T>(GLX_ALGO_RING, context, &store, ptrs, count, streams, fn) {}
 };
 
 // ~ CudaAllreduceHalvingDoublingPipelined<T, W>

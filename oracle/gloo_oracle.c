@@ -481,6 +481,39 @@ static void local_broadcast(int P, int nptrs, int dtype, size_t count,
       memcpy(bufs[r * nptrs + i], bufs[r * nptrs], count * kSize[dtype]);
 }
 
+/* ---- allreduce_ring (gloo/allreduce_ring.h) ------------------------ */
+
+/* AllreduceRing<T>::run() (:72-114): local fold into ptrs[0] (:76-79); the
+ * outbox starts as that buffer (:82); in round k every rank sends its outbox
+ * right, receives its left neighbour's into the inbox, ptrs[0] =
+ * fn(ptrs[0], inbox) (:94), and forwards the inbox as its next outbox
+ * (:100-102) -- so round k delivers rank r-1-k's locally reduced buffer;
+ * finally ptrs[0] is copied to the other pointers (:113-115). */
+int oracle_allreduce_ring(int op, int dtype, int P, int nptrs, int count, void** bufs) {
+  unsigned char** orig;
+  int r, round, rc = 0;
+  const size_t bytes = (size_t)(count > 0 ? count : 0) * kSize[dtype >= 0 && dtype < OR_NDTYPES ? dtype : 0];
+  if (P < 1 || nptrs < 1 || count < 0 || dtype < 0 || dtype >= OR_NDTYPES) return -1;
+  if (count == 0) return 0; /* :72-74 */
+  local_reduce_and(P, nptrs, op, dtype, (size_t)count, bufs);
+  orig = (unsigned char**)calloc((size_t)P, sizeof(void*));
+  if (!orig) return -1;
+  for (r = 0; r < P; r++) {
+    orig[r] = (unsigned char*)malloc(bytes);
+    if (!orig[r]) { rc = -1; goto done; }
+    memcpy(orig[r], bufs[r * nptrs], bytes);
+  }
+  for (round = 0; round < P - 1; round++)
+    for (r = 0; r < P; r++)
+      oracle_reduce(op, dtype, bufs[r * nptrs], bufs[r * nptrs],
+                    orig[(r - 1 - round + 2 * P) % P], (size_t)count);
+  local_broadcast(P, nptrs, dtype, (size_t)count, bufs);
+done:
+  for (r = 0; r < P; r++) free(orig[r]);
+  free(orig);
+  return rc;
+}
+
 /* ---- allreduce_ring_chunked (gloo/allreduce_ring_chunked.h) ------- */
 
 typedef struct { size_t chunks, chunk_size; int count; } ring_geom_t;

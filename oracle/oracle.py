@@ -27,6 +27,7 @@ DTYPE_NAMES = {
 OP_NAMES = {SUM: "sum", PRODUCT: "product", MAX: "max", MIN: "min"}
 
 RING_CHUNKED, HALVING_DOUBLING = 0, 1
+RING = 9  # gloo::AllreduceRing<T> (the glx.h code GLX_ALGO_RING)
 
 _lib = None
 _ref = None
@@ -46,7 +47,8 @@ def _load_oracle():
         lib.oracle_sum_f32.restype = None
         lib.oracle_fill.argtypes = [i, i, ctypes.c_uint64, i, i, i, i, sz, vp]
         lib.oracle_fill.restype = None
-        for name in ("oracle_allreduce_ring_chunked", "oracle_allreduce_halving_doubling"):
+        for name in ("oracle_allreduce_ring_chunked", "oracle_allreduce_halving_doubling",
+                     "oracle_allreduce_ring"):
             f = getattr(lib, name)
             f.argtypes = [i, i, i, i, i, ctypes.POINTER(vp)]
             f.restype = i
@@ -135,7 +137,8 @@ def sum_f32(c, a, b):
 def allreduce(algo, op, dtype, inputs, use_ref=False, warmup=0, iters=1):
     """inputs: list (per rank) of lists (per ptr) of 1-D numpy arrays.
     Returns new arrays holding the allreduced result, same nesting.
-    algo: RING_CHUNKED or HALVING_DOUBLING."""
+    algo: RING_CHUNKED, HALVING_DOUBLING or RING (AllreduceRing: each rank's
+    own left fold, so float results may differ between ranks)."""
     P = len(inputs)
     nptrs = len(inputs[0])
     count = inputs[0][0].size
@@ -155,8 +158,9 @@ def allreduce(algo, op, dtype, inputs, use_ref=False, warmup=0, iters=1):
         allreduce.last_seconds = secs.value
     else:
         lib = _load_oracle()
-        f = (lib.oracle_allreduce_ring_chunked if algo == RING_CHUNKED
-             else lib.oracle_allreduce_halving_doubling)
+        f = {RING_CHUNKED: lib.oracle_allreduce_ring_chunked,
+             HALVING_DOUBLING: lib.oracle_allreduce_halving_doubling,
+             RING: lib.oracle_allreduce_ring}[algo]
         rc = f(op, dtype, P, nptrs, count, flat)
         if rc != 0:
             raise RuntimeError("oracle allreduce failed rc=%d" % rc)

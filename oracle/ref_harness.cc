@@ -8,22 +8,26 @@
 //   * gloo::sum/product/max/min<T>            (gloo/math.h:15-73)
 //   * gloo::AllreduceRingChunked<T>           (gloo/allreduce_ring_chunked.h:19)
 //   * gloo::AllreduceHalvingDoubling<T>       (gloo/allreduce_halving_doubling.h:37)
+//   * gloo::AllreduceRing<T>                  (gloo/allreduce_ring.h:20)
 //   * gloo::allreduce(AllreduceOptions)       (gloo/allreduce.cc:97-146, RING/BCUBE)
 // exactly the way the reference's tests do: P threads in one process, one
 // HashStore, tcp devices on loopback (gloo/test/base_test.h:91-166).
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdint>
 #include <cstring>
 #include <exception>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "gloo/allreduce.h"
 #include "gloo/allreduce_halving_doubling.h"
+#include "gloo/allreduce_ring.h"
 #include "gloo/allreduce_ring_chunked.h"
 #include "gloo/math.h"
 #include "gloo/rendezvous/context.h"
@@ -72,6 +76,9 @@ int allreduceT(int algo, int op, int P, int nptrs, int count, void** bufs,
   auto store = std::make_shared<gloo::rendezvous::HashStore>();
   std::vector<std::thread> threads;
   std::vector<std::string> errors(P);
+  std::mutex doneMu;
+  std::condition_variable doneCv;
+  int done = 0;
   for (int r = 0; r < P; r++) {
     threads.emplace_back([&, r]() {
       try {
@@ -86,6 +93,8 @@ int allreduceT(int algo, int op, int P, int nptrs, int count, void** bufs,
         std::unique_ptr<gloo::Algorithm> alg;
         if (algo == 0) {
           alg.reset(new gloo::AllreduceRingChunked<T>(ctx, ptrs, count, fn));
+        } else if (algo == 9) {
+          alg.reset(new gloo::AllreduceRing<T>(ctx, ptrs, count, fn));
         } else {
           alg.reset(new gloo::AllreduceHalvingDoubling<T>(ctx, ptrs, count, fn));
         }
@@ -96,8 +105,18 @@ int allreduceT(int algo, int op, int P, int nptrs, int count, void** bufs,
         if (r == 0 && seconds != nullptr) {
           *seconds = std::chrono::duration<double>(t1 - t0).count();
         }
+        // every rank's run() has returned before any tears its pairs down:
+        // AllreduceRing's last notification (allreduce_ring.h:104-108) may
+        // still be in flight when a neighbour is done
+        {
+          std::unique_lock<std::mutex> lk(doneMu);
+          if (++done >= P) doneCv.notify_all();
+          doneCv.wait(lk, [&] { return done >= P; });
+        }
       } catch (const std::exception& e) {
         errors[r] = e.what();
+        std::lock_guard<std::mutex> lk(doneMu);  // count this rank for the barrier
+        if (++done >= P) doneCv.notify_all();
       }
     });
   }
@@ -245,7 +264,7 @@ void ref_f16_to_f32(const uint16_t* in, float* out, size_t n) {
   }
 }
 
-// algo: 0 = AllreduceRingChunked, 1 = AllreduceHalvingDoubling.
+// algo: 0 = AllreduceRingChunked, 1 = AllreduceHalvingDoubling, 9 = AllreduceRing.
 int ref_allreduce(int algo, int op, int dtype, int P, int nptrs, int count,
                   void** bufs, int warmup, int iters, double* seconds) {
   switch (dtype) {

@@ -42,6 +42,7 @@
 
 #include "gloo/allreduce.h"
 #include "gloo/allreduce_halving_doubling.h"
+#include "gloo/allreduce_ring.h"
 #include "gloo/allreduce_ring_chunked.h"
 #include "gloo/hip_allreduce.h"
 #include "gloo/rendezvous/context.h"
@@ -541,6 +542,15 @@ int gpuMode() {
       kStreams);
   compare<float, HdDeviceWs, AllreduceHalvingDoubling>(
       "halving_doubling<float, HipDeviceWorkspace>", 3, 100003, 1, ReductionFunction<float>::sum);
+  // CudaAllreduceRing<T>(context, ptrs, count, streams) (cuda_allreduce_test.cc:75-91)
+  // against the CPU AllreduceRing<T>: every rank's own fold order
+  compare<float, HipAllreduceRing, AllreduceRing>(
+      "ring<float> (ctx, ptrs, count, streams)", 5, 100003, 2, ReductionFunction<float>::sum,
+      kStreams);
+  compare<float16, HipAllreduceRing, AllreduceRing>(
+      "ring<float16>", 3, 65539, 1, ReductionFunction<float16>::sum);
+  compare<float, HipAllreduceRing, AllreduceRing>(
+      "ring<float> max", 4, 4099, 1, ReductionFunction<float>::max);
   interleaved();
   using MathFn = void (*)(void*, const void*, const void*, size_t);
   compareFn<float>("allreduce(opts) RING float sum", 3, 100003, 0, 1,

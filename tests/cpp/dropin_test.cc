@@ -373,6 +373,7 @@ int main() {
   for (int P = 1; P <= 8; P++) {
     for (int N : {0, 4, 100, 1000, 10000}) {
       singlePointer<gloo_amd::HipAllreduceRingChunked>("ring_chunked", P, N);
+      singlePointer<gloo_amd::HipAllreduceRing>("ring", P, N);
     }
   }
   for (int P : {1, 2, 3, 4, 5, 6, 7, 8, 9, 13}) {

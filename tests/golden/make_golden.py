@@ -185,6 +185,62 @@ def make_allreduce():
                    "cases": index}, f, indent=1)
 
 
+# ---- gloo::AllreduceRing<T> (gloo/allreduce_ring.h) ----------------------
+# Each rank's result is its own left fold (x[r] op x[r-1] op ...), so float
+# outputs differ between ranks: every rank's output is recorded.  N = 0 is a
+# no-op (run() returns first, :72-74); the compiled reference's P >= 3 runs of
+# it end in a teardown race of its tcp pairs, so it is not generated here.
+RING_CASES = []
+for _P in range(1, 16):  # the reference test's own grid (allreduce_test.cc:241-249)
+    for _N in (4, 100, 1000, 10000):
+        RING_CASES.append((_P, _N, O.FLOAT32, O.SUM, 1, 2))  # value = rank (:156-158)
+for _P in (2, 3, 5, 8):
+    for _N in (1, 1000, 4099, 100003):
+        RING_CASES.append((_P, _N, O.FLOAT32, O.SUM, 1, 0))
+for _P in (3, 8):
+    RING_CASES.append((_P, 4099, O.FLOAT16, O.SUM, 1, 0))
+    RING_CASES.append((_P, 1000, O.FLOAT32, O.MAX, 1, 0))
+    RING_CASES.append((_P, 1000, O.FLOAT32, O.PRODUCT, 1, 0))
+RING_CASES.append((4, 4099, O.INT32, O.SUM, 1, 0))
+RING_CASES.append((4, 1000, O.FLOAT32, O.MIN, 2, 0))
+RING_CASES.append((2, 4099, O.FLOAT32, O.SUM, 3, 0))
+RING_CASES.append((5, 1000, O.FLOAT32, O.SUM, 2, 1))  # stride pattern (base_test.h:184-191)
+
+
+def ring_case_name(c):
+    P, N, dtype, op, nptrs, kind = c
+    return "allreduce_ring_P%d_N%d_%s_%s_p%d_k%d" % (P, N, O.DTYPE_NAMES[dtype],
+                                                     O.OP_NAMES[op], nptrs, kind)
+
+
+def make_ring():
+    out = {}
+    index = []
+    for c in RING_CASES:
+        P, N, dtype, op, nptrs, kind = c
+        ins = case_inputs(P, N, dtype, nptrs, kind)
+        res = O.allreduce(O.RING, op, dtype, ins, use_ref=True)
+        name = ring_case_name(c)
+        rec = {"name": name, "algo": O.RING, "P": P, "N": N, "dtype": dtype, "op": op,
+               "nptrs": nptrs, "kind": kind, "seed": SEED,
+               "input_sha256": sha([x for row in ins for x in row]),
+               "output_sha256": [sha(row) for row in res]}
+        for r in range(P):
+            for i in range(1, nptrs):  # the local broadcast
+                assert np.array_equal(res[r][i].view(np.uint8), res[r][0].view(np.uint8))
+            if N <= 4099:
+                out["%s_r%d" % (name, r)] = res[r][0]
+        index.append(rec)
+        print(name, flush=True)
+    np.savez_compressed(os.path.join(HERE, "allreduce_ring_golden.npz"), **out)
+    with open(os.path.join(HERE, "allreduce_ring_golden.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py ring",
+                   "source": "oracle/_ref/libgloo_ref.so (gloo::AllreduceRing<T> compiled "
+                             "from /root/reference by oracle/Makefile), P thread-ranks over "
+                             "TCP loopback",
+                   "cases": index}, f, indent=1)
+
+
 # ---- gloo::allreduce(AllreduceOptions) (gloo/allreduce.cc) ----------------
 # (algo, P, N, dtype, op, nin, nout, max_seg, kind, out_init)
 #   kind      0 seeded, 1 stride pattern (base_test.h:184-191)
@@ -372,7 +428,7 @@ def make_bench():
 if __name__ == "__main__":
     if not O.ref_available():
         sys.exit("oracle/_ref/libgloo_ref.so missing: make -C oracle ref")
-    which = sys.argv[1:] or ["reduce", "f16", "allreduce", "allreduce_fn"]
+    which = sys.argv[1:] or ["reduce", "f16", "allreduce", "allreduce_fn", "ring"]
     if "reduce" in which:
         make_reduce()
     if "f16" in which:
@@ -381,6 +437,8 @@ if __name__ == "__main__":
         make_allreduce()
     if "allreduce_fn" in which:
         make_allreduce_fn()
+    if "ring" in which:
+        make_ring()
     if "scale" in which:  # not in the default set: minutes and ~40 GiB of RAM
         make_scale()
     if "bench" in which:  # bench.py's N > 1 workloads (256 MiB fp32, P = 2, 4, 8)

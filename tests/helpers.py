@@ -26,6 +26,27 @@ def load_allreduce_golden():
     return index, data
 
 
+def load_ring_golden():
+    """gloo::AllreduceRing<T> fixtures (make_golden.py ring): per-rank output
+    digests (float results differ between ranks), full per-rank outputs for
+    N <= 4099 under '<name>_r<rank>'."""
+    with open(os.path.join(GOLDEN, "allreduce_ring_golden.json")) as f:
+        index = json.load(f)["cases"]
+    data = np.load(os.path.join(GOLDEN, "allreduce_ring_golden.npz"))
+    return index, data
+
+
+def check_ring_against_golden(rec, data, outs):
+    """outs: per rank, the list of its pointers' output arrays (the digest
+    covers all of them, the stored array is the first)."""
+    for r, row in enumerate(outs):
+        assert sha(row) == rec["output_sha256"][r], "%s rank %d: digest" % (rec["name"], r)
+        key = "%s_r%d" % (rec["name"], r)
+        if key in data.files:
+            assert np.array_equal(np.ascontiguousarray(row[0]).view(np.uint8),
+                                  data[key].view(np.uint8)), key
+
+
 def case_inputs(P, N, dtype, nptrs, kind, seed=SEED):
     ins = []
     for r in range(P):

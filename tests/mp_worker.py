@@ -336,11 +336,13 @@ def run_devsteps(store_dir, rank, size, eng="device"):
         fn = gloo_amd.ReductionFunction(op)
         if kind == O.HALVING_DOUBLING:
             return gloo_amd.AllreduceHalvingDoubling(ctx, [buf], fn=fn, dtype=dt)
+        if kind == O.RING:
+            return gloo_amd.AllreduceRing(ctx, [buf], fn=fn, dtype=dt)
         return gloo_amd.AllreduceRingChunked(ctx, [buf], fn=fn, dtype=dt,
                                              schedule="mesh" if kind == MESH else "ring")
 
     cases = []
-    kinds = (O.RING_CHUNKED, O.HALVING_DOUBLING)
+    kinds = (O.RING_CHUNKED, O.HALVING_DOUBLING, O.RING)
     for kind in kinds:
         for n in (1, 3, 255, 256, 1000, 4099, 65539, 1 << 20, (1 << 22) + 5):
             cases.append((kind, n, O.FLOAT32, O.SUM))

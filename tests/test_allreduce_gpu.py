@@ -13,7 +13,8 @@ import time
 import numpy as np
 import pytest
 
-from helpers import case_inputs, check_against_golden, load_allreduce_golden, rank_env, run_ranks
+from helpers import (case_inputs, check_against_golden, check_ring_against_golden,
+                     load_allreduce_golden, load_ring_golden, rank_env, run_ranks)
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -22,7 +23,8 @@ torch = pytest.importorskip("torch")
 
 from test_reduce_gpu import TORCH_VIEW, assert_same, from_dev, to_dev  # noqa: E402
 
-ALGOS = {O.RING_CHUNKED: "AllreduceRingChunked", O.HALVING_DOUBLING: "AllreduceHalvingDoubling"}
+ALGOS = {O.RING_CHUNKED: "AllreduceRingChunked", O.HALVING_DOUBLING: "AllreduceHalvingDoubling",
+         O.RING: "AllreduceRing"}
 
 
 MESH = 2  # ring_chunked semantics, mesh schedule
@@ -124,6 +126,47 @@ def test_reference_test_grid_single_pointer(algo, P, N):
     out = gpu_allreduce(algo, O.SUM, O.FLOAT32, ins, runs=2)
     for r in range(P):
         assert np.all(out[r][0] == P * (P - 1) // 2), "rank %d" % r
+
+
+# gloo::AllreduceRing<T> (gloo/allreduce_ring.h): every rank's own result
+# against the compiled reference's per-rank outputs (float results differ
+# between ranks, tests/golden/allreduce_ring_golden.json), the reference
+# test's grid (allreduce_test.cc:241-249, P = 1..15), dtypes x ops, several
+# pointers with streams.
+RING_INDEX, RING_DATA = load_ring_golden()
+
+
+@pytest.mark.parametrize("rec", RING_INDEX, ids=[r["name"] for r in RING_INDEX])
+def test_allreduce_ring_vs_reference_golden(rec):
+    ins = case_inputs(rec["P"], rec["N"], rec["dtype"], rec["nptrs"], rec["kind"], rec["seed"])
+    out = gpu_allreduce(O.RING, rec["op"], rec["dtype"], ins, runs=2)
+    check_ring_against_golden(rec, RING_DATA, out)
+
+
+@pytest.mark.parametrize("P", list(range(1, 16)))
+@pytest.mark.parametrize("N", [0, 4, 100, 1000, 10000])
+def test_allreduce_ring_reference_test_grid(P, N):
+    ins = [[np.full(N, r, dtype=np.float32)] for r in range(P)]
+    out = gpu_allreduce(O.RING, O.SUM, O.FLOAT32, ins, runs=2)
+    for r in range(P):
+        assert np.all(out[r][0] == P * (P - 1) // 2), "rank %d" % r
+
+
+@pytest.mark.parametrize("dtype", [O.INT8, O.INT32, O.INT64, O.UINT64, O.FLOAT64, O.FLOAT16,
+                                   O.BFLOAT16], ids=lambda d: O.DTYPE_NAMES[d])
+@pytest.mark.parametrize("op", [O.SUM, O.PRODUCT, O.MAX, O.MIN],
+                         ids=lambda o: O.OP_NAMES[o])
+def test_allreduce_ring_dtypes_ops(dtype, op):
+    ins = case_inputs(4, 4099, dtype, 1, 0, seed=33)
+    out = gpu_allreduce(O.RING, op, dtype, ins)
+    check_all(out, O.allreduce(O.RING, op, dtype, ins), dtype, op)
+
+
+@pytest.mark.parametrize("P,nptrs", [(1, 3), (3, 2), (5, 2)])
+def test_allreduce_ring_multi_pointer_streams(P, nptrs):
+    ins = case_inputs(P, 100003, O.FLOAT32, nptrs, 0, seed=34)
+    out = gpu_allreduce(O.RING, O.SUM, O.FLOAT32, ins, runs=2, streams=True)
+    check_all(out, O.allreduce(O.RING, O.SUM, O.FLOAT32, ins), O.FLOAT32, O.SUM)
 
 
 # The CUDA algorithms' test grid (gloo/test/cuda_allreduce_test.cc:148-170,

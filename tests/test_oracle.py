@@ -4,7 +4,8 @@ reference test-suite's own known answers."""
 import numpy as np
 import pytest
 
-from helpers import GOLDEN, case_inputs, check_against_golden, load_allreduce_golden, sha
+from helpers import (GOLDEN, case_inputs, check_against_golden, check_ring_against_golden,
+                     load_allreduce_golden, load_ring_golden, sha)
 from oracle import oracle as O
 
 INDEX, DATA = load_allreduce_golden()
@@ -148,3 +149,27 @@ def test_reduction_order_halving_doubling():
     exp = ((x[0] + x[1]) + (x[2] + x[3])) + ((x[4] + x[5]) + (x[6] + x[7]))
     out = O.allreduce(O.HALVING_DOUBLING, O.SUM, O.FLOAT32, ins)[0][0]
     assert np.array_equal(out, exp.astype(np.float32))
+
+
+RING_INDEX, RING_DATA = load_ring_golden()
+
+
+@pytest.mark.parametrize("rec", RING_INDEX, ids=[r["name"] for r in RING_INDEX])
+def test_oracle_allreduce_ring_matches_reference_golden(rec):
+    """gloo::AllreduceRing<T> (gloo/allreduce_ring.h:72-114): the oracle's
+    restatement against the compiled reference's per-rank outputs."""
+    ins = case_inputs(rec["P"], rec["N"], rec["dtype"], rec["nptrs"], rec["kind"])
+    assert sha([x for row in ins for x in row]) == rec["input_sha256"]
+    out = O.allreduce(O.RING, rec["op"], rec["dtype"], ins)
+    for r in range(rec["P"]):
+        for i in range(1, rec["nptrs"]):
+            assert np.array_equal(out[r][i].view(np.uint8), out[r][0].view(np.uint8))
+    check_ring_against_golden(rec, RING_DATA, out)
+
+
+def test_allreduce_ring_ranks_differ_for_floats():
+    """The reference's AllreduceRing leaves each rank its own summation order:
+    with seeded fp32 inputs at P = 8 the ranks' results are not all equal
+    (which is why its fixtures hold every rank's digest)."""
+    rec = next(r for r in RING_INDEX if r["P"] == 8 and r["N"] == 100003 and r["kind"] == 0)
+    assert len(set(rec["output_sha256"])) > 1

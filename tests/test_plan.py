@@ -161,3 +161,20 @@ def test_replicated_fn_ring_is_bit_identical(P, N, max_seg):
                          [[x] for x in ins], max_seg)
     for r in range(P):
         assert same_bits(got[r], exp[r][0]), r
+
+
+@pytest.mark.parametrize("P", list(range(1, 16)))
+@pytest.mark.parametrize("N", [0, 1, 4, 100, 1000, 4099])
+@pytest.mark.parametrize("dtype,op", [(O.FLOAT32, O.SUM), (O.FLOAT16, O.SUM), (O.INT32, O.MAX),
+                                      (O.FLOAT32, O.PRODUCT)], ids=str)
+def test_allreduce_ring_plan_replay_matches_oracle(P, N, dtype, op):
+    """gloo::AllreduceRing<T>: the step program (one round of whole-buffer
+    sends, then each rank's left fold r, r-1, ..., r-P+1) replayed on the
+    host equals the oracle's restatement of the reference's P-1 forwarding
+    rounds, rank by rank (the reference's test grid: P = 1..15)."""
+    ins = case_inputs(P, N, dtype, 1, 0, seed=98)
+    plans = [gloo_amd.plan("ring", r, P, N, with_folds=True) for r in range(P)]
+    got = replay_plans(plans, op, dtype, [ins[r][0] for r in range(P)])
+    exp = O.allreduce(O.RING, op, dtype, ins)
+    for r in range(P):
+        assert same_bits(got[r], exp[r][0]), "rank %d" % r
