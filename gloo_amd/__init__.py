@@ -12,9 +12,11 @@ required; there is no CPU fallback.
 from . import _lib  # noqa: F401  (raises ImportError if the HIP build is missing)
 from . import math, rendezvous  # noqa: F401
 from .algorithms import (  # noqa: F401
+    AllreduceBcube,
     AllreduceHalvingDoubling,
     AllreduceRing,
     AllreduceRingChunked,
+    HipAllreduceBcube,
     HipAllreduceHalvingDoubling,
     HipAllreduceRing,
     HipAllreduceRingChunked,

@@ -57,6 +57,9 @@ SIGNATURES = [
     ("glx_context_size", _i, [_vp]),
     ("glx_context_device", _i, [_vp]),
     ("glx_context_set_timeout", _i, [_vp, _i64]),
+    ("glx_context_set_base", _i, [_vp, _i]),
+    ("glx_plan_bcube", _i64, [_i, _i, _i64, _i, ctypes.POINTER(_i64), _i64,
+                              ctypes.POINTER(_i64)]),
     ("glx_context_get_timeout", _i64, [_vp]),
     ("glx_context_next_slot", _i, [_vp, _i]),
     ("glx_allreduce_ring_chunked_create", _vp,

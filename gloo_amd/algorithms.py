@@ -126,7 +126,9 @@ ALGO_CODES = {"ring_chunked": 0, "halving_doubling": 1, "ring_chunked_mesh": 2,
               # creation-time choice among the ring_chunked schedules
               "ring_chunked_auto": 8,
               # class AllreduceRing (whole buffers, each rank's own left fold)
-              "ring": 9}
+              "ring": 9,
+              # class AllreduceBcube (groups of the context's base ranks)
+              "bcube": 10}
 
 
 class Algorithm:
@@ -289,10 +291,19 @@ class AllreduceRing(Algorithm):
     _algo = ALGO_CODES["ring"]
 
 
+class AllreduceBcube(Algorithm):
+    """gloo::AllreduceBcube<T> (gloo/allreduce_bcube.h:256): log_base(P)
+    reduce-scatter steps within groups of `context.base` ranks (default 2,
+    gloo::Context::base), then the all-gather retracing them -- the
+    reference's groups, ranges and reduction order exactly."""
+    _algo = ALGO_CODES["bcube"]
+
+
 # The device classes under the names the reference's GPU path uses.
 HipAllreduceRingChunked = AllreduceRingChunked
 HipAllreduceHalvingDoubling = AllreduceHalvingDoubling
 HipAllreduceRing = AllreduceRing
+HipAllreduceBcube = AllreduceBcube
 
 
 DEFAULT_MIN_PIECE_BYTES = 4 << 20
@@ -305,9 +316,18 @@ def plan(algo, rank, size, count, with_folds=False, esize=4, max_segment_size=0,
     options' maxSegmentSize (0: default) and the ring's device piece size
     (0: the reference's own segments).  Returns (steps as 8-tuples,
     scratch_elems[, fold sources])."""
+    scratch = ctypes.c_int64(0)
+    if algo.startswith("bcube"):  # "bcube" or "bcube:<base>"
+        base = int(algo.split(":")[1]) if ":" in algo else 2
+        n = lib.glx_plan_bcube(rank, size, count, base, None, 0, ctypes.byref(scratch))
+        if n < 0:
+            check(_lib.ERR_INVALID, "plan")
+        buf = (ctypes.c_int64 * (8 * max(n, 1)))()
+        lib.glx_plan_bcube(rank, size, count, base, buf, n, ctypes.byref(scratch))
+        steps = [tuple(buf[8 * i: 8 * i + 8]) for i in range(n)]
+        return (steps, scratch.value, {}) if with_folds else (steps, scratch.value)
     code = ALGO_CODES[algo]
     args = (code, rank, size, count, esize, max_segment_size, min_piece_bytes)
-    scratch = ctypes.c_int64(0)
     n = lib.glx_plan_ex(*args, None, 0, ctypes.byref(scratch))
     if n < 0:
         check(_lib.ERR_INVALID, "plan")

@@ -331,6 +331,41 @@ int glx_context_rank(glx_context* ctx) { return ctx ? ctx->c->rank : -1; }
 int glx_context_size(glx_context* ctx) { return ctx ? ctx->c->size : -1; }
 int glx_context_device(glx_context* ctx) { return ctx ? ctx->c->device() : -1; }
 
+int glx_context_set_base(glx_context* ctx, int base) {
+  return guarded([&]() -> int {
+    GLX_ENFORCE(ctx != nullptr, "null context");
+    GLX_ENFORCE(base >= 2, "base must be at least 2");
+    ctx->c->setBase(base);
+    return GLX_OK;
+  });
+}
+
+int64_t glx_plan_bcube(int rank, int size, int64_t count, int base, int64_t* steps, int64_t cap,
+                       int64_t* scratch_elems) {
+  glx::PlanParams prm;
+  prm.base = base;
+  int64_t n = -1;
+  guarded([&]() -> int {
+    glx::Plan p = glx::makePlan(glx::ALGO_BCUBE, rank, size, count, prm);
+    n = (int64_t)p.steps.size();
+    if (scratch_elems) *scratch_elems = p.scratch_elems;
+    for (int64_t i = 0; i < n && i < cap && steps != nullptr; i++) {
+      const glx::Step& s = p.steps[(size_t)i];
+      int64_t* o = steps + 8 * i;
+      o[0] = s.kind;
+      o[1] = s.peer;
+      o[2] = s.channel;
+      o[3] = s.off;
+      o[4] = s.len;
+      o[5] = s.boff;
+      o[6] = s.dst_off;
+      o[7] = s.flags;
+    }
+    return GLX_OK;
+  });
+  return n;
+}
+
 int glx_context_set_timeout(glx_context* ctx, int64_t timeout_ms) {
   return guarded([&]() -> int {
     GLX_ENFORCE(ctx != nullptr, "null context");
@@ -381,7 +416,7 @@ glx_algorithm* glx_allreduce_create(glx_context* ctx, int algo, void* const* ptr
   }
   if (algo != GLX_ALGO_RING_CHUNKED && algo != GLX_ALGO_HALVING_DOUBLING &&
       algo != GLX_ALGO_RING_CHUNKED_MESH && algo != GLX_ALGO_RING_CHUNKED_REPL &&
-      algo != GLX_ALGO_RING) {
+      algo != GLX_ALGO_RING && algo != GLX_ALGO_BCUBE) {
     fail(GLX_ERR_INVALID, "glx_allreduce_create: unknown algorithm");
     return nullptr;
   }

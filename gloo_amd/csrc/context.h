@@ -119,6 +119,10 @@ class Context {
   const int size;
 
   int device() const { return device_; }
+  // gloo::Context::base (gloo/context.h:33): ranks per group of the class
+  // AllreduceBcube created afterwards (default 2)
+  int base() const { return base_; }
+  void setBase(int b) { base_ = b; }
 
   // gloo/rendezvous/context.cc:43-113
   void connectFullMesh(std::shared_ptr<rendezvous::Store> store);
@@ -190,6 +194,7 @@ class Context {
 
  private:
   int device_;
+  int base_ = 2;
   int slot_ = 0;
   bool connected_ = false;
   bool flagStores_ = false;

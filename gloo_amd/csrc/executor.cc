@@ -125,6 +125,7 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
             slot_, algo_, (long)count_, dtype_, op_);
   glx::PlanParams pp = prm;
   pp.esize = (int)esize_;
+  pp.base = ctx->base();
   plan_ = glx::makePlan(algo, contextRank_, contextSize_, count, pp);
   prm_ = pp;
 

@@ -136,7 +136,8 @@ int HipPlanExecutor::engineFor(const Context& ctx, int algo, int64_t count, int 
     return meshEngine();
   }
   if (algo == glx::ALGO_RING_CHUNKED || algo == glx::ALGO_HALVING_DOUBLING ||
-      algo == glx::ALGO_FN_RING || algo == glx::ALGO_FN_BCUBE || algo == glx::ALGO_RING) {
+      algo == glx::ALGO_FN_RING || algo == glx::ALGO_FN_BCUBE || algo == glx::ALGO_RING ||
+      algo == glx::ALGO_BCUBE) {
     const int e = stepsEngine();
     if (e >= 0) return e;
     // auto: the plan kernel, at every size when every rank has a GPU of its

@@ -8,6 +8,7 @@
 #include "plan.h"
 
 #include <algorithm>
+#include <cmath>
 #include <map>
 #include <cstdlib>
 #include <stdexcept>
@@ -410,6 +411,117 @@ Plan planRing(int rank, int size, int64_t count) {
   return p;
 }
 
+// AllreduceBcube's geometry (gloo/allreduce_bcube.h:620-695 setupNodes /
+// updateGroupNodes, :150-240 Node / Group): per rank and step its peers (in
+// group order), and the [offset, offset + count) it reduces and later sends.
+namespace {
+
+struct ClassBcubeGeom {
+  int steps = 0;
+  std::vector<std::vector<std::vector<int>>> peers;  // [rank][step]
+  std::vector<std::vector<int64_t>> num, off;        // [rank][step]
+
+  ClassBcubeGeom(int nodes, int base, int64_t total) {
+    // computeSteps (:514-519): float logs, as the reference computes them
+    const float lg2n = (float)std::log2((double)nodes);
+    const float lg2p = (float)std::log2((double)base);
+    const float q = lg2n / lg2p;
+    steps = (int)std::ceil(q);
+    peers.assign((size_t)nodes, std::vector<std::vector<int>>((size_t)steps));
+    num.assign((size_t)nodes, std::vector<int64_t>((size_t)steps, 0));
+    off.assign((size_t)nodes, std::vector<int64_t>((size_t)steps, 0));
+    int64_t peerDistance = 1;
+    for (int step = 0; step < steps; ++step) {
+      for (int first = 0; first < nodes; ++first) {
+        if (!peers[(size_t)first][(size_t)step].empty()) continue;  // not a group's first node
+        std::vector<int> ranks;  // Group::getNodeRanks
+        for (int i = 0; i < base; ++i) {
+          const int64_t pr = first + i * peerDistance;
+          if (pr < nodes) ranks.push_back((int)pr);
+        }
+        int64_t ptrOffset = step == 0 ? 0 : off[(size_t)first][(size_t)step - 1];
+        const int64_t groupCount = step == 0 ? total : num[(size_t)first][(size_t)step - 1];
+        const int64_t numElems = std::max<int64_t>(groupCount, (int64_t)ranks.size());
+        const int64_t sz = (int64_t)ranks.size();  // updateGroupNodes
+        int64_t cnt = numElems / sz;
+        const int64_t rem = numElems % sz;
+        if (cnt == 0) cnt = 1;
+        for (int64_t i = 0; i < sz; ++i) {
+          const size_t n = (size_t)ranks[(size_t)i];
+          for (int pr : ranks) {
+            if (pr != (int)n) peers[n][(size_t)step].push_back(pr);
+          }
+          const int64_t c = i != sz - 1 ? cnt : cnt + rem;
+          num[n][(size_t)step] = c;
+          off[n][(size_t)step] = ptrOffset;
+          ptrOffset = (ptrOffset + c) % total;
+        }
+      }
+      peerDistance *= base;
+    }
+  }
+};
+
+}  // namespace
+
+Plan planBcube(int rank, int size, int64_t count, int base) {
+  if (base < 2) fail("bcube: base must be at least 2");
+  if (count == 0 || size == 1) return Plan();  // :273-275, :343-351
+  const ClassBcubeGeom g(size, base, count);
+  Plan p;
+  // receive regions: one per (step, peer index), sized to the largest
+  // message (:289-296 size them max(mine, theirs) per pair)
+  int64_t maxLen = 0;
+  for (int r = 0; r < size; r++)
+    for (int s = 0; s < g.steps; s++) maxLen = std::max(maxLen, g.num[(size_t)r][(size_t)s]);
+  const int64_t region = maxLen + kPadElems;
+  const int perStep = base - 1;
+  p.scratch_elems = (int64_t)g.steps * perStep * region;
+  auto regionOf = [&](int receiver, int sender, int step) -> int64_t {
+    const auto& ps = g.peers[(size_t)receiver][(size_t)step];
+    for (size_t i = 0; i < ps.size(); i++) {
+      if (ps[i] == sender) return ((int64_t)step * perStep + (int64_t)i) * region;
+    }
+    fail("bcube: sender is not a peer of the receiver at this step");
+    return 0;
+  };
+  const auto& myPeers = g.peers[(size_t)rank];
+  // reduce-scatter (:354-381): sends first, then every peer's message folded
+  // into my range in group order
+  for (int s = 0; s < g.steps; ++s) {
+    for (int dest : myPeers[(size_t)s]) {
+      const int64_t n = g.num[(size_t)dest][(size_t)s];
+      p.steps.push_back({SEND, dest, 0, g.off[(size_t)dest][(size_t)s], n, 0,
+                         regionOf(dest, rank, s), 0});
+      p.bytes_sent += n;
+    }
+    for (int src : myPeers[(size_t)s]) {
+      const int64_t n = g.num[(size_t)rank][(size_t)s];
+      const int64_t at = regionOf(rank, src, s);
+      p.steps.push_back({RECV, src, 0, 0, n, at, 0, 0});
+      p.steps.push_back({REDUCE, 0, 0, g.off[(size_t)rank][(size_t)s], n, at, 0, 0});
+      p.steps.push_back({RELEASE, src, 0, 0, 0, 0, 0, 0});
+    }
+  }
+  // all-gather (:386-418): the steps in reverse, my range out, theirs in
+  for (int s = g.steps - 1; s >= 0; --s) {
+    for (int dest : myPeers[(size_t)s]) {
+      const int64_t n = g.num[(size_t)rank][(size_t)s];
+      p.steps.push_back({SEND, dest, 0, g.off[(size_t)rank][(size_t)s], n, 0,
+                         regionOf(dest, rank, s), 0});
+      p.bytes_sent += n;
+    }
+    for (int src : myPeers[(size_t)s]) {
+      const int64_t n = g.num[(size_t)src][(size_t)s];
+      const int64_t at = regionOf(rank, src, s);
+      p.steps.push_back({RECV, src, 0, 0, n, at, 0, 0});
+      p.steps.push_back({COPY, 0, 0, g.off[(size_t)src][(size_t)s], n, at, 0, 0});
+      p.steps.push_back({RELEASE, src, 0, 0, 0, 0, 0, 0});
+    }
+  }
+  return p;
+}
+
 // ring_chunked (gloo/allreduce_ring_chunked.h:106-158) reduces chunk pair j
 // (chunks 2j, 2j+1) along ranks j, j+1, ..., j+P-1: rank j+k computes
 // op(x[j+k], partial) in place.  The broadcast pass (:163-200) becomes the
@@ -759,6 +871,7 @@ Plan makePlan(int algo, int rank, int size, int64_t count, const PlanParams& prm
     case ALGO_RING_CHUNKED_REPL: return planRingChunkedReplicated(rank, size, count);
     case ALGO_FN_RING_REPL: return planFnRingReplicated(rank, size, count, prm);
     case ALGO_RING: return planRing(rank, size, count);
+    case ALGO_BCUBE: return planBcube(rank, size, count, prm.base);
   }
   fail("unknown algorithm");
   return Plan();

@@ -62,6 +62,7 @@ enum Algo {
   ALGO_RING_CHUNKED_REPL = 6,  // ring_chunked's result in one round (small buffers)
   ALGO_FN_RING_REPL = 7,       // RING's result in one round (small buffers)
   ALGO_RING = 9,               // class AllreduceRing (whole buffers, per-rank order)
+  ALGO_BCUBE = 10,             // class AllreduceBcube (groups of `base` ranks)
 };
 
 constexpr int64_t kFoldLeft = 1;  // FOLD flag, see above
@@ -81,6 +82,8 @@ struct PlanParams {
   // unchanged: they depend only on which rank owns which element, which
   // maxSegmentBytes fixes exactly as the reference does).
   int64_t minPieceBytes = 4 << 20;
+  // class AllreduceBcube: ranks per group (gloo::Context::base, default 2)
+  int base = 2;
 };
 
 // Region padding: room to land a message at any 16-byte phase after
@@ -119,6 +122,13 @@ Plan planFnBcube(int rank, int size, int64_t count);
 // rank sends its buffer to every peer in one round (P-1 links, S each) and
 // folds in the reference's order.
 Plan planRing(int rank, int size, int64_t count);
+// AllreduceBcube (gloo/allreduce_bcube.h:256-695): log_base(P) steps; in
+// step s each rank exchanges with the other members of its group (ranks
+// base^s apart) and reduces its own range, peers in group order; then the
+// all-gather retraces the steps.  Ranges, counts and the groups follow the
+// reference's Node / Group setup (:620-695, :60-240) exactly, including its
+// wrap-around offsets when there are fewer elements than group members.
+Plan planBcube(int rank, int size, int64_t count, int base);
 
 Plan makePlan(int algo, int rank, int size, int64_t count,
               const PlanParams& prm = PlanParams());

@@ -141,6 +141,17 @@ class Context:
         val = int(seconds_or_ms if ms else round(seconds_or_ms * 1000))
         check(lib.glx_context_set_timeout(self._h, val), "setTimeout")
 
+    @property
+    def base(self):
+        """gloo::Context::base (gloo/context.h:33): ranks per group of the
+        AllreduceBcube algorithms created afterwards (default 2)."""
+        return getattr(self, "_base", 2)
+
+    @base.setter
+    def base(self, value):
+        check(lib.glx_context_set_base(self._h, int(value)), "base")
+        self._base = int(value)
+
     def getTimeout(self):  # noqa: N802
         """Timeout in seconds."""
         return lib.glx_context_get_timeout(self._h) / 1000.0

@@ -179,10 +179,17 @@ class Context {
     return std::chrono::milliseconds(glx_context_get_timeout(c_));
   }
   int nextSlot(int numToSkip = 1) { return glx_context_next_slot(c_, numToSkip); }
+  // gloo::Context::base (gloo/context.h:33): HipAllreduceBcube's group size
+  void setBase(int b) {
+    check(glx_context_set_base(c_, b), "setBase");
+    base_ = b;
+  }
+  int base() const { return base_; }
   glx_context* handle() const { return c_; }
 
  private:
   glx_context* c_;
+  int base_ = 2;
 
  public:
   const int rank;
@@ -337,6 +344,10 @@ inline glx_algorithm* createRingWhole(glx_context* c, void* const* p, int n, int
                                       int op, const glx_stream_t* s, int ns) {
   return glx_allreduce_create(c, GLX_ALGO_RING, p, n, count, dt, op, s, ns);
 }
+inline glx_algorithm* createBcube(glx_context* c, void* const* p, int n, int count, int dt,
+                                  int op, const glx_stream_t* s, int ns) {
+  return glx_allreduce_create(c, GLX_ALGO_BCUBE, p, n, count, dt, op, s, ns);
+}
 }  // namespace detail
 
 // gloo::CudaHostWorkspace<T> / CudaDeviceWorkspace<T> analogs
@@ -408,6 +419,19 @@ class HipAllreduceRing : public detail::DeviceAllreduce<T> {
                    const std::vector<glx_stream_t>& streams = {},
                    const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
       : detail::DeviceAllreduce<T>(&detail::createRingWhole, ctx, ptrs, count, streams, fn) {}
+};
+
+// gloo::CudaAllreduceBcube<T, W> / AllreduceBcube<T> analog
+// (gloo/cuda_allreduce_bcube.h, gloo/allreduce_bcube.h:256): groups of the
+// context's base() ranks (Context::setBase, default 2).
+template <typename T, typename W = HipHostWorkspace<T>>
+class HipAllreduceBcube : public detail::DeviceAllreduce<T> {
+ public:
+  static const char* workspace() { return W::kName; }
+  HipAllreduceBcube(const std::shared_ptr<Context>& ctx, const std::vector<T*>& ptrs, int count,
+                    const std::vector<glx_stream_t>& streams = {},
+                    const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
+      : detail::DeviceAllreduce<T>(&detail::createBcube, ctx, ptrs, count, streams, fn) {}
 };
 
 // gloo::CudaAllreduceHalvingDoublingPipelined<T, W> analog

@@ -238,6 +238,9 @@ int glx_context_device(glx_context* ctx);
 /* gloo::Context::setTimeout/getTimeout (gloo/context.h:50-53); default 30 s
  * (gloo/context.cc:18). */
 int glx_context_set_timeout(glx_context* ctx, int64_t timeout_ms);
+/* gloo::Context::base (gloo/context.h:33): ranks per group of the
+ * GLX_ALGO_BCUBE algorithms created afterwards (default 2, >= 2). */
+int glx_context_set_base(glx_context* ctx, int base);
 int64_t glx_context_get_timeout(glx_context* ctx);
 /* gloo::Context::nextSlot(numToSkip), gloo/context.cc:49-54. */
 int glx_context_next_slot(glx_context* ctx, int num_to_skip);
@@ -290,7 +293,10 @@ enum glx_algo {
    * of the ranks' buffers starting from its own, r, r-1, ..., r-P+1 (float
    * results may differ between ranks, as in the reference); whole buffers,
    * one round over every link instead of P-1 forwarding rounds */
-  GLX_ALGO_RING = 9
+  GLX_ALGO_RING = 9,
+  /* gloo::AllreduceBcube<T> (gloo/allreduce_bcube.h:256): groups of the
+   * context's base ranks (glx_context_set_base, gloo::Context::base) */
+  GLX_ALGO_BCUBE = 10
 };
 glx_algorithm* glx_allreduce_create(glx_context* ctx, int algo, void* const* ptrs,
                                     int nptrs, int count, int dtype, int op,
@@ -506,6 +512,9 @@ int64_t glx_plan_fold(int algo, int rank, int size, int64_t count, int64_t fold,
 int64_t glx_plan_ex(int algo, int rank, int size, int64_t count, int esize,
                     int64_t max_segment_bytes, int64_t min_piece_bytes, int64_t* steps,
                     int64_t cap, int64_t* scratch_elems);
+/* AllreduceBcube's step program for a given base (glx_plan's layout). */
+int64_t glx_plan_bcube(int rank, int size, int64_t count, int base, int64_t* steps, int64_t cap,
+                       int64_t* scratch_elems);
 int64_t glx_plan_fold_ex(int algo, int rank, int size, int64_t count, int esize,
                          int64_t max_segment_bytes, int64_t min_piece_bytes, int64_t fold,
                          int64_t* srcs, int64_t cap);

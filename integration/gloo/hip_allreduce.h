@@ -9,6 +9,9 @@
 //                                       (gloo/cuda_allreduce_halving_doubling.h:22-30)
 //   HipAllreduceRing<T, W>            ~ CudaAllreduceRing<T, W>
 //                                       (gloo/cuda_allreduce_ring.h:17-24)
+//   HipAllreduceBcube<T, W>           ~ CudaAllreduceBcube<T, W>
+//                                       (gloo/cuda_allreduce_bcube.h), groups
+//                                       of the gloo context's `base` ranks
 //   HipAllreduceHalvingDoublingPipelined<T, W>
 //                                     ~ CudaAllreduceHalvingDoublingPipelined<T, W>
 //                                       (gloo/cuda_allreduce_halving_doubling_pipelined.h:13-27)
@@ -415,6 +418,8 @@ class Allreduce : public Algorithm {
       : Algorithm(context) {
     GLOO_ENFORCE(!ptrs.empty(), "at least one pointer is required");
     xgmi_ = XgmiContext::of(context, store, deviceOf(ptrs[0]));
+    // gloo::Context::base (gloo/context.h:33): AllreduceBcube's group size
+    check(glx_context_set_base(xgmi_->get(), std::max(2, context->base)), "base");
     std::vector<void*> p(ptrs.begin(), ptrs.end());
     std::vector<glx_stream_t> s(streams.begin(), streams.end());
     alg_ = glx_allreduce_create(xgmi_->get(), algo, p.data(), (int)p.size(), count,
@@ -627,6 +632,28 @@ class HipAllreduceRing : public hip::Allreduce<T> {
                    const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
                    const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
       : hip::Allreduce<T>(GLX_ALGO_RING, context, &store, ptrs, count, streams, fn) {}
+};
+
+// ~ CudaAllreduceBcube<T, W> (gloo/cuda_allreduce_bcube.h) and the CPU
+// AllreduceBcube<T> (gloo/allreduce_bcube.h:256): groups of context->base
+// ranks, the reference's ranges and reduction order.
+template <typename T, typename W = HipHostWorkspace<T>>
+class HipAllreduceBcube : public hip::Allreduce<T> {
+  static_assert(hip::IsWorkspace<T, W>::value,
+                "W must be HipHostWorkspace<T> or HipDeviceWorkspace<T>");
+
+ public:
+  static const char* workspace() { return W::kName; }
+  HipAllreduceBcube(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs,
+                    const int count,
+                    const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
+                    const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
+      : hip::Allreduce<T>(GLX_ALGO_BCUBE, context, nullptr, ptrs, count, streams, fn) {}
+  HipAllreduceBcube(const std::shared_ptr<Context>& context, rendezvous::Store& store,
+                    const std::vector<T*>& ptrs, const int count,
+                    const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
+                    const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
+      : hip::Allreduce<T>(GLX_ALGO_BCUBE, context, &store, ptrs, count, streams, fn) {}
 };
 
 // ~ CudaAllreduceHalvingDoublingPipelined<T, W>

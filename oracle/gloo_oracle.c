@@ -514,6 +514,153 @@ done:
   return rc;
 }
 
+/* ---- allreduce_bcube (gloo/allreduce_bcube.h) ---------------------- */
+
+/* setupNodes / updateGroupNodes (:620-695) with Node / Group (:60-240):
+ * per rank r and step s its peers (group order, without r), and the count /
+ * offset of the range it reduces.  Arrays are [r * steps + s]. */
+typedef struct {
+  int steps, base;
+  int* npeers;  /* [r * steps + s] */
+  int* peers;   /* [(r * steps + s) * base + i] */
+  long* num;
+  long* off;
+} bcube_geom_t;
+
+static void bcube_free(bcube_geom_t* g) {
+  free(g->npeers);
+  free(g->peers);
+  free(g->num);
+  free(g->off);
+}
+
+static int bcube_setup(int nodes, int base, long total, bcube_geom_t* g) {
+  /* computeSteps (:514-519): float logs, ceil of their quotient */
+  const float lg2n = (float)log2((double)nodes);
+  const float lg2p = (float)log2((double)base);
+  const float q = lg2n / lg2p;
+  int step, first, i;
+  long peer_distance = 1;
+  g->base = base;
+  g->steps = (int)ceil((double)q);
+  g->npeers = (int*)calloc((size_t)nodes * (size_t)(g->steps + 1), sizeof(int));
+  g->peers = (int*)calloc((size_t)nodes * (size_t)(g->steps + 1) * (size_t)base, sizeof(int));
+  g->num = (long*)calloc((size_t)nodes * (size_t)(g->steps + 1), sizeof(long));
+  g->off = (long*)calloc((size_t)nodes * (size_t)(g->steps + 1), sizeof(long));
+  if (!g->npeers || !g->peers || !g->num || !g->off) return -1;
+  for (step = 0; step < g->steps; step++) {
+    for (first = 0; first < nodes; first++) {
+      int ranks[64], sz = 0;
+      long ptr_offset, group_count, num_elems, cnt, rem;
+      if (g->npeers[first * g->steps + step] != 0) continue; /* not a first node */
+      for (i = 0; i < base && sz < 64; i++) {                 /* Group::getNodeRanks */
+        long pr = first + (long)i * peer_distance;
+        if (pr < nodes) ranks[sz++] = (int)pr;
+      }
+      ptr_offset = step == 0 ? 0 : g->off[first * g->steps + step - 1];
+      group_count = step == 0 ? total : g->num[first * g->steps + step - 1];
+      num_elems = group_count > sz ? group_count : sz;        /* computeNumElems */
+      cnt = num_elems / sz;                                   /* updateGroupNodes */
+      rem = num_elems % sz;
+      if (cnt == 0) cnt = 1;
+      for (i = 0; i < sz; i++) {
+        const int n = ranks[i];
+        const int at = n * g->steps + step;
+        const long c = i != sz - 1 ? cnt : cnt + rem;
+        int k;
+        for (k = 0; k < sz; k++)
+          if (ranks[k] != n) g->peers[at * base + g->npeers[at]++] = ranks[k];
+        g->num[at] = c;
+        g->off[at] = ptr_offset;
+        ptr_offset = (ptr_offset + c) % total;
+      }
+    }
+    peer_distance *= base;
+  }
+  return 0;
+}
+
+/* AllreduceBcube<T>::run() (:338-430): reduce-scatter -- every step sends
+ * each peer its range, then folds each peer's message into our range in
+ * group order (:354-381); all-gather -- the steps in reverse, our range out
+ * and theirs copied in (:386-418); local fold / broadcast around it. */
+int oracle_allreduce_bcube(int op, int dtype, int P, int nptrs, int count, int base,
+                           void** bufs) {
+  bcube_geom_t g = {0, 0, NULL, NULL, NULL, NULL};
+  prog_t* progs = NULL;
+  unsigned char** data = NULL;
+  unsigned char** scratch = NULL;
+  size_t* scratch_elems = NULL;
+  long max_len = 0;
+  int r, s, i, rc = 0;
+  if (P < 1 || nptrs < 1 || count < 0 || base < 2 || dtype < 0 || dtype >= OR_NDTYPES)
+    return -1;
+  if (count == 0) return 0;                                    /* :339-341 */
+  local_reduce_and(P, nptrs, op, dtype, (size_t)count, bufs);  /* :343-345 */
+  if (P == 1) {                                                /* :347-353 */
+    local_broadcast(P, nptrs, dtype, (size_t)count, bufs);
+    return 0;
+  }
+  if (bcube_setup(P, base, count, &g) != 0) { rc = -1; goto done; }
+  for (r = 0; r < P * g.steps; r++)
+    if (g.num[r] > max_len) max_len = g.num[r];
+  progs = (prog_t*)calloc((size_t)P, sizeof(prog_t));
+  data = (unsigned char**)calloc((size_t)P, sizeof(void*));
+  scratch = (unsigned char**)calloc((size_t)P, sizeof(void*));
+  scratch_elems = (size_t*)calloc((size_t)P, sizeof(size_t));
+  if (!progs || !data || !scratch || !scratch_elems) { rc = -1; goto done; }
+  for (r = 0; r < P; r++) {
+    prog_t* p = &progs[r];
+    data[r] = (unsigned char*)bufs[r * nptrs];
+    scratch_elems[r] = (size_t)max_len * (size_t)P; /* a region per source rank */
+    scratch[r] = (unsigned char*)calloc(scratch_elems[r], kSize[dtype]);
+    if (!scratch[r]) { rc = -1; goto done; }
+    for (s = 0; s < g.steps; s++) {
+      const int at = r * g.steps + s;
+      for (i = 0; i < g.npeers[at]; i++) {
+        const int d = g.peers[at * base + i];
+        step_t st = {ST_SEND, d, 0, (size_t)g.off[d * g.steps + s],
+                     (size_t)g.num[d * g.steps + s], 0};
+        prog_push(p, st);
+      }
+      for (i = 0; i < g.npeers[at]; i++) {
+        const int src = g.peers[at * base + i];
+        step_t rv = {ST_RECV, src, 0, 0, 0, (size_t)src * (size_t)max_len};
+        step_t red = {ST_REDUCE, 0, 0, (size_t)g.off[at], (size_t)g.num[at],
+                      (size_t)src * (size_t)max_len};
+        prog_push(p, rv);
+        prog_push(p, red);
+      }
+    }
+    for (s = g.steps - 1; s >= 0; s--) {
+      const int at = r * g.steps + s;
+      for (i = 0; i < g.npeers[at]; i++) {
+        step_t st = {ST_SEND, g.peers[at * base + i], 0, (size_t)g.off[at], (size_t)g.num[at], 0};
+        prog_push(p, st);
+      }
+      for (i = 0; i < g.npeers[at]; i++) {
+        const int src = g.peers[at * base + i];
+        step_t rv = {ST_RECV, src, 0, 0, 0, (size_t)src * (size_t)max_len};
+        step_t cp = {ST_COPY, 0, 0, (size_t)g.off[src * g.steps + s],
+                     (size_t)g.num[src * g.steps + s], (size_t)src * (size_t)max_len};
+        prog_push(p, rv);
+        prog_push(p, cp);
+      }
+    }
+  }
+  rc = simulate(P, progs, op, dtype, data, scratch, scratch_elems);
+  if (rc == 0) local_broadcast(P, nptrs, dtype, (size_t)count, bufs); /* :421-424 */
+done:
+  if (progs) for (r = 0; r < P; r++) free(progs[r].v);
+  if (scratch) for (r = 0; r < P; r++) free(scratch[r]);
+  free(progs);
+  free(data);
+  free(scratch);
+  free(scratch_elems);
+  bcube_free(&g);
+  return rc;
+}
+
 /* ---- allreduce_ring_chunked (gloo/allreduce_ring_chunked.h) ------- */
 
 typedef struct { size_t chunks, chunk_size; int count; } ring_geom_t;

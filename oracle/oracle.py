@@ -28,6 +28,7 @@ OP_NAMES = {SUM: "sum", PRODUCT: "product", MAX: "max", MIN: "min"}
 
 RING_CHUNKED, HALVING_DOUBLING = 0, 1
 RING = 9  # gloo::AllreduceRing<T> (the glx.h code GLX_ALGO_RING)
+BCUBE = 10  # gloo::AllreduceBcube<T> (GLX_ALGO_BCUBE; groups of `base` ranks)
 
 _lib = None
 _ref = None
@@ -52,6 +53,8 @@ def _load_oracle():
             f = getattr(lib, name)
             f.argtypes = [i, i, i, i, i, ctypes.POINTER(vp)]
             f.restype = i
+        lib.oracle_allreduce_bcube.argtypes = [i, i, i, i, i, i, ctypes.POINTER(vp)]
+        lib.oracle_allreduce_bcube.restype = i
         lib.oracle_allreduce_fn.argtypes = [i, i, i, i, i, i, sz, sz, ctypes.POINTER(vp),
                                             ctypes.POINTER(vp)]
         lib.oracle_allreduce_fn.restype = i
@@ -83,6 +86,8 @@ def _load_ref():
         lib.ref_allreduce.argtypes = [i, i, i, i, i, i, ctypes.POINTER(vp), i, i,
                                       ctypes.POINTER(ctypes.c_double)]
         lib.ref_allreduce.restype = i
+        lib.ref_set_bcube_base.argtypes = [i]
+        lib.ref_set_bcube_base.restype = None
         lib.ref_allreduce_fn.argtypes = [i, i, i, i, i, i, sz, sz, ctypes.POINTER(vp),
                                          ctypes.POINTER(vp)]
         lib.ref_allreduce_fn.restype = i
@@ -134,11 +139,12 @@ def sum_f32(c, a, b):
     _load_oracle().oracle_sum_f32(_ptr(c), _ptr(a), _ptr(b), a.size)
 
 
-def allreduce(algo, op, dtype, inputs, use_ref=False, warmup=0, iters=1):
+def allreduce(algo, op, dtype, inputs, use_ref=False, warmup=0, iters=1, base=2):
     """inputs: list (per rank) of lists (per ptr) of 1-D numpy arrays.
     Returns new arrays holding the allreduced result, same nesting.
-    algo: RING_CHUNKED, HALVING_DOUBLING or RING (AllreduceRing: each rank's
-    own left fold, so float results may differ between ranks)."""
+    algo: RING_CHUNKED, HALVING_DOUBLING, RING (AllreduceRing: each rank's
+    own left fold, so float results may differ between ranks) or BCUBE
+    (AllreduceBcube with groups of `base` ranks, gloo::Context::base)."""
     P = len(inputs)
     nptrs = len(inputs[0])
     count = inputs[0][0].size
@@ -150,6 +156,7 @@ def allreduce(algo, op, dtype, inputs, use_ref=False, warmup=0, iters=1):
     if use_ref:
         lib = _load_ref()
         secs = ctypes.c_double(0.0)
+        lib.ref_set_bcube_base(int(base))
         rc = lib.ref_allreduce(algo, op, dtype, P, nptrs, count, flat, warmup, iters,
                                ctypes.byref(secs))
         if rc != 0:
@@ -158,10 +165,13 @@ def allreduce(algo, op, dtype, inputs, use_ref=False, warmup=0, iters=1):
         allreduce.last_seconds = secs.value
     else:
         lib = _load_oracle()
-        f = {RING_CHUNKED: lib.oracle_allreduce_ring_chunked,
-             HALVING_DOUBLING: lib.oracle_allreduce_halving_doubling,
-             RING: lib.oracle_allreduce_ring}[algo]
-        rc = f(op, dtype, P, nptrs, count, flat)
+        if algo == BCUBE:
+            rc = lib.oracle_allreduce_bcube(op, dtype, P, nptrs, count, int(base), flat)
+        else:
+            f = {RING_CHUNKED: lib.oracle_allreduce_ring_chunked,
+                 HALVING_DOUBLING: lib.oracle_allreduce_halving_doubling,
+                 RING: lib.oracle_allreduce_ring}[algo]
+            rc = f(op, dtype, P, nptrs, count, flat)
         if rc != 0:
             raise RuntimeError("oracle allreduce failed rc=%d" % rc)
     return bufs

@@ -9,6 +9,7 @@
 //   * gloo::AllreduceRingChunked<T>           (gloo/allreduce_ring_chunked.h:19)
 //   * gloo::AllreduceHalvingDoubling<T>       (gloo/allreduce_halving_doubling.h:37)
 //   * gloo::AllreduceRing<T>                  (gloo/allreduce_ring.h:20)
+//   * gloo::AllreduceBcube<T>                 (gloo/allreduce_bcube.h:256)
 //   * gloo::allreduce(AllreduceOptions)       (gloo/allreduce.cc:97-146, RING/BCUBE)
 // exactly the way the reference's tests do: P threads in one process, one
 // HashStore, tcp devices on loopback (gloo/test/base_test.h:91-166).
@@ -27,6 +28,7 @@
 
 #include "gloo/allreduce.h"
 #include "gloo/allreduce_halving_doubling.h"
+#include "gloo/allreduce_bcube.h"
 #include "gloo/allreduce_ring.h"
 #include "gloo/allreduce_ring_chunked.h"
 #include "gloo/math.h"
@@ -36,6 +38,8 @@
 #include "gloo/types.h"
 
 namespace {
+
+int g_bcube_base = 2;  // gloo::Context::base for AllreduceBcube (ref_set_bcube_base)
 
 enum { R_INT8 = 0, R_UINT8, R_INT32, R_INT64, R_UINT64, R_FLOAT32, R_FLOAT64,
        R_FLOAT16, R_BFLOAT16 };
@@ -84,7 +88,7 @@ int allreduceT(int algo, int op, int P, int nptrs, int count, void** bufs,
       try {
         gloo::transport::tcp::attr attr("127.0.0.1");
         auto dev = gloo::transport::tcp::CreateDevice(attr);
-        auto ctx = std::make_shared<gloo::rendezvous::Context>(r, P);
+        auto ctx = std::make_shared<gloo::rendezvous::Context>(r, P, g_bcube_base);
         ctx->connectFullMesh(*store, dev);
         std::vector<T*> ptrs;
         for (int i = 0; i < nptrs; i++) {
@@ -95,6 +99,8 @@ int allreduceT(int algo, int op, int P, int nptrs, int count, void** bufs,
           alg.reset(new gloo::AllreduceRingChunked<T>(ctx, ptrs, count, fn));
         } else if (algo == 9) {
           alg.reset(new gloo::AllreduceRing<T>(ctx, ptrs, count, fn));
+        } else if (algo == 10) {
+          alg.reset(new gloo::AllreduceBcube<T>(ctx, ptrs, count, fn));
         } else {
           alg.reset(new gloo::AllreduceHalvingDoubling<T>(ctx, ptrs, count, fn));
         }
@@ -264,7 +270,13 @@ void ref_f16_to_f32(const uint16_t* in, float* out, size_t n) {
   }
 }
 
-// algo: 0 = AllreduceRingChunked, 1 = AllreduceHalvingDoubling, 9 = AllreduceRing.
+// gloo::Context::base of the contexts ref_allreduce creates (AllreduceBcube's
+// group size; the other algorithms ignore it)
+void ref_set_bcube_base(int base) { g_bcube_base = base; }
+
+// algo: 0 = AllreduceRingChunked, 1 = AllreduceHalvingDoubling, 9 = AllreduceRing,
+// 10 = AllreduceBcube (base: ref_set_bcube_base).
+
 int ref_allreduce(int algo, int op, int dtype, int P, int nptrs, int count,
                   void** bufs, int warmup, int iters, double* seconds) {
   switch (dtype) {

@@ -41,6 +41,7 @@
 #include <vector>
 
 #include "gloo/allreduce.h"
+#include "gloo/allreduce_bcube.h"
 #include "gloo/allreduce_halving_doubling.h"
 #include "gloo/allreduce_ring.h"
 #include "gloo/allreduce_ring_chunked.h"
@@ -52,6 +53,7 @@
 namespace {
 
 int failures = 0;
+int g_base = 2;  // gloo::Context::base of the contexts spawn() creates
 
 #define EXPECT(cond, ...)                                 \
   do {                                                    \
@@ -257,7 +259,7 @@ void spawn(int P, const std::function<void(std::shared_ptr<gloo::Context>,
       try {
         gloo::transport::tcp::attr attr("127.0.0.1");
         auto dev = gloo::transport::tcp::CreateDevice(attr);
-        auto ctx = std::make_shared<gloo::rendezvous::Context>(r, P);
+        auto ctx = std::make_shared<gloo::rendezvous::Context>(r, P, g_base);
         ctx->setTimeout(std::chrono::seconds(60));
         ctx->connectFullMesh(*store, dev);
         fn(ctx, *store, r);
@@ -551,6 +553,17 @@ int gpuMode() {
       "ring<float16>", 3, 65539, 1, ReductionFunction<float16>::sum);
   compare<float, HipAllreduceRing, AllreduceRing>(
       "ring<float> max", 4, 4099, 1, ReductionFunction<float>::max);
+  // CudaAllreduceBcube<T>(context, ptrs, count, streams) (cuda_allreduce_test.cc:
+  // 93-110) against the CPU AllreduceBcube<T>, contexts with base 2 and 3
+  compare<float, HipAllreduceBcube, AllreduceBcube>(
+      "bcube<float> base 2 (ctx, ptrs, count, streams)", 4, 100003, 2,
+      ReductionFunction<float>::sum, kStreams);
+  g_base = 3;
+  compare<float16, HipAllreduceBcube, AllreduceBcube>(
+      "bcube<float16> base 3", 9, 4099, 1, ReductionFunction<float16>::sum);
+  compare<float, HipAllreduceBcube, AllreduceBcube>(
+      "bcube<float> base 3, P = 5", 5, 1000, 1, ReductionFunction<float>::max);
+  g_base = 2;
   interleaved();
   using MathFn = void (*)(void*, const void*, const void*, size_t);
   compareFn<float>("allreduce(opts) RING float sum", 3, 100003, 0, 1,

@@ -381,6 +381,7 @@ int main() {
       singlePointer<gloo_amd::HipAllreduceHalvingDoubling>("halving_doubling", P, N);
       singlePointer<gloo_amd::HipAllreduceHalvingDoublingPipelined>("halving_doubling_pipelined",
                                                                       P, N);
+      singlePointer<gloo_amd::HipAllreduceBcube>("bcube", P, N);
     }
   }
   for (int P = 1; P <= 8; P++) {

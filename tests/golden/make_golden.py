@@ -241,6 +241,61 @@ def make_ring():
                    "cases": index}, f, indent=1)
 
 
+# ---- gloo::AllreduceBcube<T> (gloo/allreduce_bcube.h) --------------------
+# Groups of gloo::Context::base ranks.  The reference test's grid
+# (allreduce_test.cc:271-299: base 2 at P = 1, 2, 4, 8, 16; base 3 at 1, 3, 9,
+# 27; base 4 at 1, 4, 16; N = 1, 64, 1000 -- 0 is a no-op), plus seeded
+# order-sensitive inputs at other P (its groups need not be full).  With fewer
+# elements than group members the reference's ranges wrap and ranks can end
+# with differently ordered sums: every rank's digest is recorded.
+BCUBE_CASES = []
+for _b, _Ps in ((2, (1, 2, 4, 8, 16)), (3, (1, 3, 9, 27)), (4, (1, 4, 16))):
+    for _P in _Ps:
+        for _N in (1, 64, 1000):
+            BCUBE_CASES.append((_b, _P, _N, O.FLOAT32, O.SUM, 1, 2))
+for _b, _Ps in ((2, (3, 5, 8)), (3, (4, 9)), (4, (6,))):
+    for _P in _Ps:
+        for _N in (3, 1000, 100003):
+            BCUBE_CASES.append((_b, _P, _N, O.FLOAT32, O.SUM, 1, 0))
+for _b, _P in ((2, 8), (3, 9)):
+    BCUBE_CASES.append((_b, _P, 4099, O.FLOAT16, O.SUM, 1, 0))
+    BCUBE_CASES.append((_b, _P, 4099, O.INT32, O.MAX, 1, 0))
+    BCUBE_CASES.append((_b, _P, 1000, O.FLOAT32, O.PRODUCT, 2, 0))
+BCUBE_CASES.append((2, 4, 1000, O.FLOAT32, O.MIN, 3, 1))
+
+
+def bcube_case_name(c):
+    base, P, N, dtype, op, nptrs, kind = c
+    return "allreduce_bcube_b%d_P%d_N%d_%s_%s_p%d_k%d" % (base, P, N, O.DTYPE_NAMES[dtype],
+                                                          O.OP_NAMES[op], nptrs, kind)
+
+
+def make_bcube():
+    out = {}
+    index = []
+    for c in BCUBE_CASES:
+        base, P, N, dtype, op, nptrs, kind = c
+        ins = case_inputs(P, N, dtype, nptrs, kind)
+        res = O.allreduce(O.BCUBE, op, dtype, ins, use_ref=True, base=base)
+        name = bcube_case_name(c)
+        rec = {"name": name, "algo": O.BCUBE, "base": base, "P": P, "N": N, "dtype": dtype,
+               "op": op, "nptrs": nptrs, "kind": kind, "seed": SEED,
+               "input_sha256": sha([x for row in ins for x in row]),
+               "output_sha256": [sha(row) for row in res]}
+        for r in range(P):
+            if N <= 4099:
+                out["%s_r%d" % (name, r)] = res[r][0]
+        index.append(rec)
+        print(name, flush=True)
+    np.savez_compressed(os.path.join(HERE, "allreduce_bcube_golden.npz"), **out)
+    with open(os.path.join(HERE, "allreduce_bcube_golden.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py bcube",
+                   "source": "oracle/_ref/libgloo_ref.so (gloo::AllreduceBcube<T> compiled "
+                             "from /root/reference by oracle/Makefile), P thread-ranks over "
+                             "TCP loopback, gloo::Context::base = base",
+                   "cases": index}, f, indent=1)
+
+
 # ---- gloo::allreduce(AllreduceOptions) (gloo/allreduce.cc) ----------------
 # (algo, P, N, dtype, op, nin, nout, max_seg, kind, out_init)
 #   kind      0 seeded, 1 stride pattern (base_test.h:184-191)
@@ -428,7 +483,7 @@ def make_bench():
 if __name__ == "__main__":
     if not O.ref_available():
         sys.exit("oracle/_ref/libgloo_ref.so missing: make -C oracle ref")
-    which = sys.argv[1:] or ["reduce", "f16", "allreduce", "allreduce_fn", "ring"]
+    which = sys.argv[1:] or ["reduce", "f16", "allreduce", "allreduce_fn", "ring", "bcube"]
     if "reduce" in which:
         make_reduce()
     if "f16" in which:
@@ -439,6 +494,8 @@ if __name__ == "__main__":
         make_allreduce_fn()
     if "ring" in which:
         make_ring()
+    if "bcube" in which:
+        make_bcube()
     if "scale" in which:  # not in the default set: minutes and ~40 GiB of RAM
         make_scale()
     if "bench" in which:  # bench.py's N > 1 workloads (256 MiB fp32, P = 2, 4, 8)

@@ -26,13 +26,13 @@ def load_allreduce_golden():
     return index, data
 
 
-def load_ring_golden():
-    """gloo::AllreduceRing<T> fixtures (make_golden.py ring): per-rank output
-    digests (float results differ between ranks), full per-rank outputs for
-    N <= 4099 under '<name>_r<rank>'."""
-    with open(os.path.join(GOLDEN, "allreduce_ring_golden.json")) as f:
+def load_ring_golden(which="ring"):
+    """gloo::AllreduceRing<T> / AllreduceBcube<T> fixtures (make_golden.py
+    ring / bcube): per-rank output digests (results may differ between
+    ranks), full per-rank outputs for N <= 4099 under '<name>_r<rank>'."""
+    with open(os.path.join(GOLDEN, "allreduce_%s_golden.json" % which)) as f:
         index = json.load(f)["cases"]
-    data = np.load(os.path.join(GOLDEN, "allreduce_ring_golden.npz"))
+    data = np.load(os.path.join(GOLDEN, "allreduce_%s_golden.npz" % which))
     return index, data
 
 

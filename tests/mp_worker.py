@@ -338,11 +338,14 @@ def run_devsteps(store_dir, rank, size, eng="device"):
             return gloo_amd.AllreduceHalvingDoubling(ctx, [buf], fn=fn, dtype=dt)
         if kind == O.RING:
             return gloo_amd.AllreduceRing(ctx, [buf], fn=fn, dtype=dt)
+        if kind == O.BCUBE:
+            return gloo_amd.AllreduceBcube(ctx, [buf], fn=fn, dtype=dt)
         return gloo_amd.AllreduceRingChunked(ctx, [buf], fn=fn, dtype=dt,
                                              schedule="mesh" if kind == MESH else "ring")
 
     cases = []
-    kinds = (O.RING_CHUNKED, O.HALVING_DOUBLING, O.RING)
+    kinds = (O.RING_CHUNKED, O.HALVING_DOUBLING, O.RING, O.BCUBE)
+    ctx.base = 3 if size in (3, 9) else 2  # AllreduceBcube's groups
     for kind in kinds:
         for n in (1, 3, 255, 256, 1000, 4099, 65539, 1 << 20, (1 << 22) + 5):
             cases.append((kind, n, O.FLOAT32, O.SUM))
@@ -354,7 +357,8 @@ def run_devsteps(store_dir, rank, size, eng="device"):
     for seed, (kind, n, dt, op) in enumerate(cases):
         ins = case_inputs(size, n, dt, 1, 0, seed=200 + seed)
         # the mesh schedule computes ring_chunked's result (same chunks and chains)
-        exp = O.allreduce(O.RING_CHUNKED if kind == MESH else kind, op, dt, ins)[rank][0]
+        exp = O.allreduce(O.RING_CHUNKED if kind == MESH else kind, op, dt, ins,
+                          base=ctx.base)[rank][0]
         buf = to_dev(ins[rank][0], dt)
         alg = make(kind, buf, op, dt)
         # the plan kernel, or host-issued steps where a landing region would

@@ -24,7 +24,7 @@ torch = pytest.importorskip("torch")
 from test_reduce_gpu import TORCH_VIEW, assert_same, from_dev, to_dev  # noqa: E402
 
 ALGOS = {O.RING_CHUNKED: "AllreduceRingChunked", O.HALVING_DOUBLING: "AllreduceHalvingDoubling",
-         O.RING: "AllreduceRing"}
+         O.RING: "AllreduceRing", O.BCUBE: "AllreduceBcube"}
 
 
 MESH = 2  # ring_chunked semantics, mesh schedule
@@ -33,7 +33,7 @@ AUTO = 8  # ring_chunked semantics, schedule chosen by size
 
 
 def gpu_allreduce(algo, op, dtype, inputs, runs=1, streams=False, timeout_s=60,
-                  refill_between_runs=True):
+                  refill_between_runs=True, base=2):
     """Run one algorithm instance per rank thread; returns results per rank/ptr."""
     import gloo_amd
     P, nptrs = len(inputs), len(inputs[0])
@@ -59,6 +59,7 @@ def gpu_allreduce(algo, op, dtype, inputs, runs=1, streams=False, timeout_s=60,
         ctx = gloo_amd.rendezvous.Context(r, P, 0)
         ctx.setTimeout(timeout_s)
         ctx.connectFullMesh(store)
+        ctx.base = base  # gloo::Context::base (AllreduceBcube's group size)
         ptrs = [b.data_ptr() for b in bufs[r]]
         ss = [torch.cuda.Stream() for _ in range(nptrs)] if streams else None
         alg = cls(ctx, ptrs, N, fn, streams=ss, dtype=dtype)
@@ -167,6 +168,42 @@ def test_allreduce_ring_multi_pointer_streams(P, nptrs):
     ins = case_inputs(P, 100003, O.FLOAT32, nptrs, 0, seed=34)
     out = gpu_allreduce(O.RING, O.SUM, O.FLOAT32, ins, runs=2, streams=True)
     check_all(out, O.allreduce(O.RING, O.SUM, O.FLOAT32, ins), O.FLOAT32, O.SUM)
+
+
+# gloo::AllreduceBcube<T> (gloo/allreduce_bcube.h): groups of the context's
+# base ranks; the reference's per-rank outputs, its test grid (allreduce_
+# test.cc:271-299), dtypes x ops.
+BCUBE_INDEX, BCUBE_DATA = load_ring_golden("bcube")
+
+
+@pytest.mark.parametrize("rec", BCUBE_INDEX, ids=[r["name"] for r in BCUBE_INDEX])
+def test_allreduce_bcube_vs_reference_golden(rec):
+    ins = case_inputs(rec["P"], rec["N"], rec["dtype"], rec["nptrs"], rec["kind"], rec["seed"])
+    out = gpu_allreduce(O.BCUBE, rec["op"], rec["dtype"], ins, runs=2, base=rec["base"])
+    check_ring_against_golden(rec, BCUBE_DATA, out)
+
+
+BCUBE_REF_GRID = ([(2, P) for P in (1, 2, 4, 8, 16)] + [(3, P) for P in (1, 3, 9, 27)] +
+                  [(4, P) for P in (1, 4, 16)])
+
+
+@pytest.mark.parametrize("base,P", BCUBE_REF_GRID, ids=["b%d-P%d" % g for g in BCUBE_REF_GRID])
+@pytest.mark.parametrize("N", [0, 1, 64, 1000])
+def test_allreduce_bcube_reference_test_grid(base, P, N):
+    ins = [[np.full(N, r, dtype=np.float32)] for r in range(P)]
+    out = gpu_allreduce(O.BCUBE, O.SUM, O.FLOAT32, ins, runs=2, base=base)
+    for r in range(P):
+        assert np.all(out[r][0] == P * (P - 1) // 2), "rank %d" % r
+
+
+@pytest.mark.parametrize("dtype", [O.INT8, O.INT64, O.FLOAT64, O.FLOAT16, O.BFLOAT16],
+                         ids=lambda d: O.DTYPE_NAMES[d])
+@pytest.mark.parametrize("op", [O.SUM, O.PRODUCT, O.MAX, O.MIN],
+                         ids=lambda o: O.OP_NAMES[o])
+def test_allreduce_bcube_dtypes_ops(dtype, op):
+    ins = case_inputs(6, 4099, dtype, 1, 0, seed=35)
+    out = gpu_allreduce(O.BCUBE, op, dtype, ins, base=3)
+    check_all(out, O.allreduce(O.BCUBE, op, dtype, ins, base=3), dtype, op)
 
 
 # The CUDA algorithms' test grid (gloo/test/cuda_allreduce_test.cc:148-170,

@@ -173,3 +173,17 @@ def test_allreduce_ring_ranks_differ_for_floats():
     (which is why its fixtures hold every rank's digest)."""
     rec = next(r for r in RING_INDEX if r["P"] == 8 and r["N"] == 100003 and r["kind"] == 0)
     assert len(set(rec["output_sha256"])) > 1
+
+
+BCUBE_INDEX, BCUBE_DATA = load_ring_golden("bcube")
+
+
+@pytest.mark.parametrize("rec", BCUBE_INDEX, ids=[r["name"] for r in BCUBE_INDEX])
+def test_oracle_allreduce_bcube_matches_reference_golden(rec):
+    """gloo::AllreduceBcube<T> (gloo/allreduce_bcube.h:256-695) with the
+    context's base: the oracle's restatement against the compiled
+    reference's per-rank outputs."""
+    ins = case_inputs(rec["P"], rec["N"], rec["dtype"], rec["nptrs"], rec["kind"])
+    assert sha([x for row in ins for x in row]) == rec["input_sha256"]
+    out = O.allreduce(O.BCUBE, rec["op"], rec["dtype"], ins, base=rec["base"])
+    check_ring_against_golden(rec, BCUBE_DATA, out)

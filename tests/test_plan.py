@@ -178,3 +178,24 @@ def test_allreduce_ring_plan_replay_matches_oracle(P, N, dtype, op):
     exp = O.allreduce(O.RING, op, dtype, ins)
     for r in range(P):
         assert same_bits(got[r], exp[r][0]), "rank %d" % r
+
+
+BCUBE_GRID = ([(2, P) for P in (1, 2, 3, 4, 5, 6, 8, 16)] + [(3, P) for P in (1, 2, 3, 4, 7, 9, 27)]
+              + [(4, P) for P in (1, 4, 5, 8, 16)])
+
+
+@pytest.mark.parametrize("base,P", BCUBE_GRID, ids=["b%d-P%d" % g for g in BCUBE_GRID])
+@pytest.mark.parametrize("N", [0, 1, 3, 64, 1000, 4099])
+@pytest.mark.parametrize("dtype,op", [(O.FLOAT32, O.SUM), (O.FLOAT16, O.SUM), (O.INT32, O.MAX)],
+                         ids=str)
+def test_allreduce_bcube_plan_replay_matches_oracle(base, P, N, dtype, op):
+    """gloo::AllreduceBcube<T>: the step program (the reference's groups of
+    `base` ranks, its ranges incl. the wrap-around at tiny N, peers in group
+    order) replayed on the host equals the oracle's restatement, which
+    equals the compiled reference on the same grid."""
+    ins = case_inputs(P, N, dtype, 1, 0, seed=97)
+    plans = [gloo_amd.plan("bcube:%d" % base, r, P, N, with_folds=True) for r in range(P)]
+    got = replay_plans(plans, op, dtype, [ins[r][0] for r in range(P)])
+    exp = O.allreduce(O.BCUBE, op, dtype, ins, base=base)
+    for r in range(P):
+        assert same_bits(got[r], exp[r][0]), "rank %d" % r
