@@ -14,6 +14,7 @@ from . import math, rendezvous  # noqa: F401
 from .algorithms import (  # noqa: F401
     AllreduceBcube,
     AllreduceHalvingDoubling,
+    AllreduceLocal,
     AllreduceRing,
     AllreduceRingChunked,
     HipAllreduceBcube,

@@ -128,7 +128,9 @@ ALGO_CODES = {"ring_chunked": 0, "halving_doubling": 1, "ring_chunked_mesh": 2,
               # class AllreduceRing (whole buffers, each rank's own left fold)
               "ring": 9,
               # class AllreduceBcube (groups of the context's base ranks)
-              "bcube": 10}
+              "bcube": 10,
+              # class AllreduceLocal (this rank's pointers only)
+              "local": 11}
 
 
 class Algorithm:
@@ -297,6 +299,13 @@ class AllreduceBcube(Algorithm):
     gloo::Context::base), then the all-gather retracing them -- the
     reference's groups, ranges and reduction order exactly."""
     _algo = ALGO_CODES["bcube"]
+
+
+class AllreduceLocal(Algorithm):
+    """gloo::AllreduceLocal<T> (gloo/allreduce_local.cc:21-31): this rank's
+    pointers folded into ptrs[0] (((p0 op p1) op p2) ...) and copied back to
+    the others; nothing is exchanged with other ranks."""
+    _algo = ALGO_CODES["local"]
 
 
 # The device classes under the names the reference's GPU path uses.

@@ -414,6 +414,18 @@ glx_algorithm* glx_allreduce_create(glx_context* ctx, int algo, void* const* ptr
     algo = glx::autoRingSchedule(ctx->c->size, (int64_t)count * (int64_t)glx_dtype_size(dtype),
                                  /*fn=*/false, gloo::HipPlanExecutor::deviceEnginesAvailable(*ctx->c));
   }
+  if (algo == GLX_ALGO_LOCAL && ctx != nullptr) {
+    // gloo::AllreduceLocal<T> (gloo/allreduce_local.cc:21-31): this rank's
+    // pointers folded into ptrs[0] and copied back, nothing exchanged.  The
+    // P = 1 case of every class algorithm is exactly that fold and broadcast,
+    // so it runs on a private one-rank context on the same device (staging of
+    // host buffers, pointers on other GPUs of this rank, streams: as for the
+    // others) -- no peer is involved, whatever the caller's context size.
+    glx_context local{std::make_shared<gloo::Context>(0, 1, ctx->c->device())};
+    local.c->setTimeout(ctx->c->getTimeout());
+    return makeAlgorithm(glx::ALGO_RING_CHUNKED, &local, ptrs, nptrs, count, dtype, op, streams,
+                         nstreams);
+  }
   if (algo != GLX_ALGO_RING_CHUNKED && algo != GLX_ALGO_HALVING_DOUBLING &&
       algo != GLX_ALGO_RING_CHUNKED_MESH && algo != GLX_ALGO_RING_CHUNKED_REPL &&
       algo != GLX_ALGO_RING && algo != GLX_ALGO_BCUBE) {

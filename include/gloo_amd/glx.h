@@ -296,7 +296,10 @@ enum glx_algo {
   GLX_ALGO_RING = 9,
   /* gloo::AllreduceBcube<T> (gloo/allreduce_bcube.h:256): groups of the
    * context's base ranks (glx_context_set_base, gloo::Context::base) */
-  GLX_ALGO_BCUBE = 10
+  GLX_ALGO_BCUBE = 10,
+  /* gloo::AllreduceLocal<T> (gloo/allreduce_local.h:17): this rank's
+   * pointers folded into ptrs[0] and broadcast back; no exchange */
+  GLX_ALGO_LOCAL = 11
 };
 glx_algorithm* glx_allreduce_create(glx_context* ctx, int algo, void* const* ptrs,
                                     int nptrs, int count, int dtype, int op,

@@ -206,6 +206,35 @@ def test_allreduce_bcube_dtypes_ops(dtype, op):
     check_all(out, O.allreduce(O.BCUBE, op, dtype, ins, base=3), dtype, op)
 
 
+@pytest.mark.parametrize("P,nptrs", [(1, 1), (1, 3), (3, 2), (4, 4)])
+@pytest.mark.parametrize("dtype,op", [(O.FLOAT32, O.SUM), (O.FLOAT16, O.SUM), (O.INT32, O.MAX)],
+                         ids=str)
+def test_allreduce_local(P, nptrs, dtype, op):
+    """gloo::AllreduceLocal<T> (gloo/allreduce_local.cc:21-31): each rank's
+    own pointers folded and broadcast; ranks do not exchange anything."""
+    import gloo_amd
+    ins = case_inputs(P, 100003, dtype, nptrs, 0, seed=36)
+    store = gloo_amd.rendezvous.HashStore()
+    bufs = [[to_dev(x, dtype) for x in row] for row in ins]
+    torch.cuda.synchronize()
+
+    def rank_fn(r):
+        ctx = gloo_amd.rendezvous.Context(r, P, 0)
+        ctx.connectFullMesh(store)
+        alg = gloo_amd.AllreduceLocal(ctx, [b.data_ptr() for b in bufs[r]], 100003,
+                                      gloo_amd.ReductionFunction(op), dtype=dtype)
+        alg.run()
+        alg.close()
+        return True
+
+    run_ranks(P, rank_fn, timeout=90)
+    torch.cuda.synchronize()
+    for r in range(P):
+        exp = O.allreduce(O.RING_CHUNKED, op, dtype, [ins[r]])[0]  # one rank's fold
+        for i in range(nptrs):
+            assert_same(from_dev(bufs[r][i], dtype), exp[i], dtype, op)
+
+
 # The CUDA algorithms' test grid (gloo/test/cuda_allreduce_test.cc:148-170,
 # 281-309: the same ranks, N without 0) with CudaFixture's values, the stride
 # pattern (gloo/test/base_test.h:184-192) checked for exact equality
