@@ -23,6 +23,9 @@ algo: ring_chunked | halving_doubling | ring_chunked_mesh (class algorithms)
       every peer's connect-time view; then an allreduce on the same context)
       engine_choice (which engine the automatic policy picks on the shared
       GPU under this process's GPU_MAX_HW_QUEUES, and one exact run)
+      fuzz:<seed> (randomized algorithms / lengths / dtypes / ops / host
+      buffers on the device engines, every rank the same draw, each against
+      the oracle)
       big:fast | big:plain (the ring on the plan kernel over MORE than 2 GiB per
       rank, P = 2, the given stream policy: every 32-bit store offset the
       write-through path could form is exceeded; exact at P = 2 since fp32
@@ -59,6 +62,8 @@ def main():
         return run_churn(store_dir, rank, size)
     if algo.startswith("scale:"):
         return run_scale(store_dir, rank, size, algo[len("scale:"):])
+    if algo.startswith("fuzz:"):
+        return run_fuzz(store_dir, rank, size, int(algo[len("fuzz:"):]))
     if algo.startswith("big:"):
         return run_big(store_dir, rank, size, algo[len("big:"):])
     if algo == "linkprobe":
@@ -667,6 +672,100 @@ def run_engine_choice(store_dir, rank, size):
     ctx.close()
     if not ok:
         print("MISMATCH rank", rank)
+        sys.exit(1)
+    print("OK")
+
+
+def run_fuzz(store_dir, rank, size, seed):
+    """Randomized cases on the device engines, one process per rank: every
+    rank draws the same sequence (a shared seed) of (class or function-style
+    algorithm, schedule, length, dtype, op, host or device buffer, runs) and
+    compares its own output with the oracle bit for bit.  The grid tests fix
+    their sizes; this walks lengths and combinations off them."""
+    import random
+
+    import numpy as np
+    import torch
+
+    import gloo_amd
+    from helpers import case_inputs
+    from oracle import oracle as O
+    from test_reduce_gpu import from_dev, to_dev
+
+    store = gloo_amd.rendezvous.FileStore(store_dir)
+    ctx = gloo_amd.rendezvous.Context(rank, size, 0)
+    ctx.setTimeout(30)
+    ctx.connectFullMesh(store)
+    rng = random.Random(seed)
+    dtypes = [O.FLOAT32, O.FLOAT16, O.BFLOAT16, O.INT32, O.INT64, O.FLOAT64, O.INT8, O.UINT64]
+    ops = [O.SUM, O.PRODUCT, O.MAX, O.MIN]
+    kinds = ["ring_chunked", "halving_doubling", "mesh", "replicated", "ring", "bcube",
+             "fn_ring", "fn_bcube"]
+    bad = []
+    engines = {}
+    ncases = int(os.environ.get("FUZZ_CASES", "60"))
+    for case in range(ncases):
+        kind = rng.choice(kinds)
+        n = rng.choice([rng.randint(1, 64), rng.randint(65, 70000), rng.randint(70001, 1 << 21)])
+        dt = rng.choice(dtypes)
+        op = rng.choice(ops) if dt not in (O.FLOAT32,) else rng.choice([O.SUM, O.SUM, O.MAX])
+        host = rng.random() < 0.15 and dt not in (O.FLOAT16, O.BFLOAT16)
+        runs = rng.choice([1, 2])
+        base = rng.choice([2, 3]) if kind == "bcube" else 2
+        ins = case_inputs(size, n, dt, 1, 0, seed=1000 + case)
+        if kind.startswith("fn_"):
+            code = O.FN_BCUBE if kind == "fn_bcube" else O.FN_RING
+            exp = O.allreduce_fn(code, op, dt, [[] for _ in range(size)], ins)[rank][0]
+        else:
+            code = {"ring_chunked": O.RING_CHUNKED, "halving_doubling": O.HALVING_DOUBLING,
+                    "mesh": O.RING_CHUNKED, "replicated": O.RING_CHUNKED, "ring": O.RING,
+                    "bcube": O.BCUBE}[kind]
+            exp = O.allreduce(code, op, dt, ins, base=base)[rank][0]
+        ctx.base = base
+        fn = gloo_amd.ReductionFunction(op)
+        for it in range(runs):
+            buf = ins[rank][0].copy() if host else to_dev(ins[rank][0], dt)
+            torch.cuda.synchronize()
+            if kind.startswith("fn_"):
+                A = gloo_amd.AllreduceOptions.Algorithm
+                opts = gloo_amd.AllreduceOptions(ctx)
+                opts.setAlgorithm(A.BCUBE if kind == "fn_bcube" else A.RING)
+                opts.setOutput(buf)
+                opts.setReduceFunction(fn)
+                gloo_amd.allreduce(opts)
+                eng = "fn"
+            else:
+                dtype_arg = dt if host or dt in (O.FLOAT16, O.BFLOAT16) else None
+                if kind == "halving_doubling":
+                    alg = gloo_amd.AllreduceHalvingDoubling(ctx, [buf], fn=fn, dtype=dtype_arg)
+                elif kind == "ring":
+                    alg = gloo_amd.AllreduceRing(ctx, [buf], fn=fn, dtype=dtype_arg)
+                elif kind == "bcube":
+                    alg = gloo_amd.AllreduceBcube(ctx, [buf], fn=fn, dtype=dtype_arg)
+                else:
+                    sched = {"ring_chunked": "ring", "mesh": "mesh",
+                             "replicated": "replicated"}[kind]
+                    alg = gloo_amd.AllreduceRingChunked(ctx, [buf], fn=fn, dtype=dtype_arg,
+                                                        schedule=sched)
+                eng = alg.engine()
+                alg.run()
+                alg.close()
+            got = buf if host else from_dev(buf, dt)
+            ok = np.array_equal(np.ascontiguousarray(got).view(np.uint8),
+                                np.ascontiguousarray(exp).view(np.uint8))
+            engines[eng] = engines.get(eng, 0) + 1
+            if not ok:
+                bad.append((case, kind, n, dt, op, host, base, eng, it))
+        print("FUZZ rank %d case %d %s n %d dtype %d op %d host %s base %d engine %s %s"
+              % (rank, case, kind, n, dt, op, host, base, eng,
+                 "MISMATCH" if bad and bad[-1][0] == case else "ok"), flush=True)
+    store.set("done/%d" % rank, b"1")
+    for r in range(size):
+        store.get("done/%d" % r, timeout_ms=120000)
+    print("ENGINES rank %d %s" % (rank, engines), flush=True)
+    ctx.close()
+    if bad:
+        print("MISMATCH rank", rank, bad[:10])
         sys.exit(1)
     print("OK")
 

@@ -83,3 +83,36 @@ def test_allreduce_random_shapes(algo, P, N, nptrs, dtype, op):
     for r in range(P):
         for i in range(nptrs):
             assert same_bits(out[r][i], exp[r][i]), (r, i)
+
+
+@pytest.mark.parametrize("P,seed_", [(2, 1), (3, 2), (4, 3), (8, 4)])
+def test_device_engines_random_cases_multiprocess(P, seed_):
+    """One process per rank (the node's topology; the device engines run):
+    60 random (algorithm, schedule, length, dtype, op, host/device buffer)
+    cases per P, every rank against the oracle (mp_worker.py fuzz)."""
+    import os
+    import subprocess
+    import sys
+    import tempfile
+
+    from helpers import rank_env
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "mp_worker.py")
+    with tempfile.TemporaryDirectory() as d:
+        env = rank_env(P)
+        procs = [subprocess.Popen([sys.executable, worker, d, str(r), str(P), "fuzz:%d" % seed_],
+                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                 for r in range(P)]
+        outs = []
+        for p in procs:
+            try:
+                o, _ = p.communicate(timeout=420)
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+            outs.append(o.decode(errors="replace"))
+        every = "\n".join("---- rank %d (rc %s) ----\n%s" % (r, p.returncode, outs[r][-3000:])
+                          for r, p in enumerate(procs))
+        print(outs[0][-2000:])
+        for r, p in enumerate(procs):
+            assert p.returncode == 0 and "OK" in outs[r], "rank %d failed:\n%s" % (r, every)
