@@ -730,12 +730,12 @@ def run_fuzz(store_dir, rank, size, seed):
                 A = gloo_amd.AllreduceOptions.Algorithm
                 opts = gloo_amd.AllreduceOptions(ctx)
                 opts.setAlgorithm(A.BCUBE if kind == "fn_bcube" else A.RING)
-                opts.setOutput(buf)
+                opts.setOutputs([buf], dtype=dt)
                 opts.setReduceFunction(fn)
                 gloo_amd.allreduce(opts)
                 eng = "fn"
             else:
-                dtype_arg = dt if host or dt in (O.FLOAT16, O.BFLOAT16) else None
+                dtype_arg = dt  # explicit: uint64 data lives in an int64 tensor
                 if kind == "halving_doubling":
                     alg = gloo_amd.AllreduceHalvingDoubling(ctx, [buf], fn=fn, dtype=dtype_arg)
                 elif kind == "ring":
