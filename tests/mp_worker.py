@@ -703,7 +703,7 @@ def run_fuzz(store_dir, rank, size, seed):
              "fn_ring", "fn_bcube"]
     bad = []
     engines = {}
-    ncases = int(os.environ.get("FUZZ_CASES", "60"))
+    ncases = int(os.environ.get("FUZZ_CASES", "100"))
     for case in range(ncases):
         kind = rng.choice(kinds)
         n = rng.choice([rng.randint(1, 64), rng.randint(65, 70000), rng.randint(70001, 1 << 21)])

@@ -88,7 +88,7 @@ def test_allreduce_random_shapes(algo, P, N, nptrs, dtype, op):
 @pytest.mark.parametrize("P,seed_", [(2, 1), (3, 2), (4, 3), (8, 4)])
 def test_device_engines_random_cases_multiprocess(P, seed_):
     """One process per rank (the node's topology; the device engines run):
-    60 random (algorithm, schedule, length, dtype, op, host/device buffer)
+    100 random (algorithm, schedule, length, dtype, op, host/device buffer)
     cases per P, every rank against the oracle (mp_worker.py fuzz)."""
     import os
     import subprocess
