@@ -593,8 +593,9 @@ int oracle_allreduce_bcube(int op, int dtype, int P, int nptrs, int count, int b
   size_t* scratch_elems = NULL;
   long max_len = 0;
   int r, s, i, rc = 0;
-  if (P < 1 || nptrs < 1 || count < 0 || base < 2 || dtype < 0 || dtype >= OR_NDTYPES)
-    return -1;
+  if (P < 1 || nptrs < 1 || count < 0 || base < 2 || base > 64 || dtype < 0 ||
+      dtype >= OR_NDTYPES)
+    return -1; /* bcube_setup keeps a group's ranks in a 64-entry array */
   if (count == 0) return 0;                                    /* :339-341 */
   local_reduce_and(P, nptrs, op, dtype, (size_t)count, bufs);  /* :343-345 */
   if (P == 1) {                                                /* :347-353 */
