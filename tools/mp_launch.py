@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--pmc", default=None,
                     help="with --prof-dir: rank 0 runs under rocprofv3 --pmc <this> instead")
     ap.add_argument("--prof-name", default="rank0", help="rocprofv3 -o name")
+    ap.add_argument("--copies", action="store_true",
+                    help="with --prof-dir (no --pmc): also --memory-copy-trace")
     ap.add_argument("cmd", nargs=argparse.REMAINDER)
     a = ap.parse_args()
     cmd = a.cmd[1:] if a.cmd and a.cmd[0] == "--" else a.cmd
@@ -39,6 +41,8 @@ def main():
         argv = [sys.executable] + cmd
         if r == 0 and a.prof_dir:
             what = ["--pmc"] + a.pmc.split(",") if a.pmc else ["--kernel-trace", "--stats"]
+            if a.copies and not a.pmc:
+                what.append("--memory-copy-trace")
             argv = ["rocprofv3"] + what + ["--output-format", "csv",
                                            "-d", a.prof_dir, "-o", a.prof_name, "--"] + argv
         procs.append(subprocess.Popen(argv, env=env))
