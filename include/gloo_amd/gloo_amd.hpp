@@ -348,6 +348,10 @@ inline glx_algorithm* createBcube(glx_context* c, void* const* p, int n, int cou
                                   int op, const glx_stream_t* s, int ns) {
   return glx_allreduce_create(c, GLX_ALGO_BCUBE, p, n, count, dt, op, s, ns);
 }
+inline glx_algorithm* createLocal(glx_context* c, void* const* p, int n, int count, int dt,
+                                  int op, const glx_stream_t* s, int ns) {
+  return glx_allreduce_create(c, GLX_ALGO_LOCAL, p, n, count, dt, op, s, ns);
+}
 }  // namespace detail
 
 // gloo::CudaHostWorkspace<T> / CudaDeviceWorkspace<T> analogs
@@ -432,6 +436,20 @@ class HipAllreduceBcube : public detail::DeviceAllreduce<T> {
                     const std::vector<glx_stream_t>& streams = {},
                     const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
       : detail::DeviceAllreduce<T>(&detail::createBcube, ctx, ptrs, count, streams, fn) {}
+};
+
+// gloo::CudaAllreduceLocal<T> / AllreduceLocal<T> analog
+// (gloo/cuda_allreduce_local.h:21-27, gloo/allreduce_local.h:17-22): this
+// rank's pointers folded into ptrs[0] and copied back to the others; no peer
+// is involved, whatever the context's size (the context gives the device's
+// timeout only).
+template <typename T>
+class HipAllreduceLocal : public detail::DeviceAllreduce<T> {
+ public:
+  HipAllreduceLocal(const std::shared_ptr<Context>& ctx, const std::vector<T*>& ptrs, int count,
+                    const std::vector<glx_stream_t>& streams = {},
+                    const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
+      : detail::DeviceAllreduce<T>(&detail::createLocal, ctx, ptrs, count, streams, fn) {}
 };
 
 // gloo::CudaAllreduceHalvingDoublingPipelined<T, W> analog

@@ -12,6 +12,9 @@
 //   HipAllreduceBcube<T, W>           ~ CudaAllreduceBcube<T, W>
 //                                       (gloo/cuda_allreduce_bcube.h), groups
 //                                       of the gloo context's `base` ranks
+//   HipAllreduceLocal<T>              ~ CudaAllreduceLocal<T>
+//                                       (gloo/cuda_allreduce_local.h:21-27), this
+//                                       rank's pointers only, no exchange
 //   HipAllreduceHalvingDoublingPipelined<T, W>
 //                                     ~ CudaAllreduceHalvingDoublingPipelined<T, W>
 //                                       (gloo/cuda_allreduce_halving_doubling_pipelined.h:13-27)
@@ -654,6 +657,47 @@ class HipAllreduceBcube : public hip::Allreduce<T> {
                     const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
                     const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
       : hip::Allreduce<T>(GLX_ALGO_BCUBE, context, &store, ptrs, count, streams, fn) {}
+};
+
+// ~ CudaAllreduceLocal<T> (gloo/cuda_allreduce_local.h:21-27) and the CPU
+// AllreduceLocal<T> (gloo/allreduce_local.h:17-22, allreduce_local.cc:21-31):
+// this rank's pointers folded left into ptrs[0], then copied to the others.
+// Nothing is exchanged, so unlike the classes above it takes no part in the
+// xGMI context's exchanges: it runs on a one-rank glx context of its own (a
+// rank may create and run it alone, as with the reference's).
+template <typename T>
+class HipAllreduceLocal : public Algorithm {
+ public:
+  HipAllreduceLocal(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs,
+                    const int count,
+                    const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
+                    const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
+      : Algorithm(context) {
+    GLOO_ENFORCE(!ptrs.empty(), "at least one pointer is required");
+    local_ = glx_context_create(0, 1, hip::deviceOf(ptrs[0]));
+    GLOO_ENFORCE(local_ != nullptr, "glx_context_create: ", glx_last_error());
+    std::vector<void*> p(ptrs.begin(), ptrs.end());
+    std::vector<glx_stream_t> s(streams.begin(), streams.end());
+    if (glx_context_set_timeout(local_, (int64_t)context->getTimeout().count()) == GLX_OK) {
+      alg_ = glx_allreduce_create(local_, GLX_ALGO_LOCAL, p.data(), (int)p.size(), count,
+                                  hip::GlxType<T>::value, hip::glxOp(fn),
+                                  s.empty() ? nullptr : s.data(), (int)s.size());
+    }
+    if (alg_ == nullptr) {
+      const std::string err = glx_last_error();
+      glx_context_destroy(local_);
+      GLOO_ENFORCE(false, "glx_allreduce_create: ", err);
+    }
+  }
+  ~HipAllreduceLocal() override {
+    glx_algorithm_destroy(alg_);
+    glx_context_destroy(local_);
+  }
+  void run() override { hip::check(glx_algorithm_run(alg_), "run"); }
+
+ private:
+  glx_context* local_ = nullptr;
+  glx_algorithm* alg_ = nullptr;
 };
 
 // ~ CudaAllreduceHalvingDoublingPipelined<T, W>

@@ -43,6 +43,7 @@
 #include "gloo/allreduce.h"
 #include "gloo/allreduce_bcube.h"
 #include "gloo/allreduce_halving_doubling.h"
+#include "gloo/allreduce_local.h"
 #include "gloo/allreduce_ring.h"
 #include "gloo/allreduce_ring_chunked.h"
 #include "gloo/hip_allreduce.h"
@@ -324,13 +325,22 @@ void compare(const char* name, int P, int count, int nptrs, const gloo::Reductio
       constexpr bool withFn =
           std::is_constructible<Hip<T>, std::shared_ptr<gloo::Context>, std::vector<T*>, int,
                                 std::vector<hipStream_t>, const gloo::ReductionFunction<T>*>::value;
+      // HipAllreduceLocal exchanges nothing, so it has no store overload
+      constexpr bool withStore =
+          std::is_constructible<Hip<T>, std::shared_ptr<gloo::Context>, gloo::rendezvous::Store&,
+                                std::vector<T*>, int, std::vector<hipStream_t>,
+                                const gloo::ReductionFunction<T>*>::value;
       if (how == kStreams) {
         a.reset(new Hip<T>(ctx, dev, count, streams));  // gloo/test/cuda_allreduce_test.cc:85-144
       } else if (fn == gloo::ReductionFunction<T>::sum && !viaStore) {
         a.reset(new Hip<T>(ctx, dev, count));
       } else if constexpr (withFn) {
         if (viaStore) {
-          a.reset(new Hip<T>(ctx, store, dev, count, {}, fn));
+          if constexpr (withStore) {
+            a.reset(new Hip<T>(ctx, store, dev, count, {}, fn));
+          } else {
+            throw std::runtime_error("this class takes no store");
+          }
         } else {
           a.reset(new Hip<T>(ctx, dev, count, {}, fn));
         }
@@ -508,6 +518,55 @@ void interleaved() {
               bad ? "MISMATCH" : "ok");
 }
 
+// AllreduceLocal exchanges nothing: one rank creates and runs it while its
+// peer does no gloo work at all (a collective inside would wait out the
+// timeout), then the pair still runs a ring together.
+void localAlone() {
+  using namespace gloo;
+  const int count = 70001;
+  std::vector<float> a(count), b(count), want(count), got(count);
+  for (int i = 0; i < count; i++) {
+    a[(size_t)i] = value<float>(0, (size_t)i);
+    b[(size_t)i] = value<float>(1, (size_t)i);
+  }
+  {
+    std::vector<float> x = a, y = b;
+    std::vector<float*> ptrs = {x.data(), y.data()};
+    auto solo = std::make_shared<rendezvous::HashStore>();
+    // the CPU AllreduceLocal on a one-rank context as the expected value
+    auto ctx1 = std::make_shared<rendezvous::Context>(0, 1);
+    transport::tcp::attr attr("127.0.0.1");
+    auto dev = transport::tcp::CreateDevice(attr);
+    ctx1->connectFullMesh(*solo, dev);
+    AllreduceLocal<float>(ctx1, ptrs, count).run();
+    want = x;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  spawn(2, [&](std::shared_ptr<Context> ctx, rendezvous::Store&, int r) {
+    ctx->setTimeout(std::chrono::seconds(5));
+    if (r == 0) {
+      float* d[2];
+      for (int k = 0; k < 2; k++) {
+        if (hipMalloc((void**)&d[k], sizeof(float) * count) != hipSuccess) {
+          throw std::runtime_error("hipMalloc");
+        }
+        hipMemcpy(d[k], (k ? b : a).data(), sizeof(float) * count, hipMemcpyHostToDevice);
+      }
+      HipAllreduceLocal<float> l(ctx, {d[0], d[1]}, count);
+      l.run();
+      hipMemcpy(got.data(), d[1], sizeof(float) * count, hipMemcpyDeviceToHost);
+      for (float* p : d) hipFree(p);
+    }
+  });
+  const double secs =
+      std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  const bool same = std::memcmp(got.data(), want.data(), sizeof(float) * count) == 0;
+  EXPECT(same, "local alone: result differs from the reference");
+  EXPECT(secs < 4.0, "local alone took %.1f s (waited for the idle peer?)", secs);
+  std::printf("local<float> on one rank of two, peer idle: %s (%.2f s)\n",
+              same && secs < 4.0 ? "ok" : "FAILED", secs);
+}
+
 int gpuMode() {
   using namespace gloo;
   int n = 0;
@@ -564,6 +623,16 @@ int gpuMode() {
   compare<float, HipAllreduceBcube, AllreduceBcube>(
       "bcube<float> base 3, P = 5", 5, 1000, 1, ReductionFunction<float>::max);
   g_base = 2;
+  // CudaAllreduceLocal<T>(context, ptrs, count, streams) (cuda_allreduce_local.h:21-27)
+  // against the CPU AllreduceLocal<T> (allreduce_local.cc:21-31)
+  compare<float, HipAllreduceLocal, AllreduceLocal>(
+      "local<float> (ctx, ptrs, count, streams)", 2, 100003, 3, ReductionFunction<float>::sum,
+      kStreams);
+  compare<float16, HipAllreduceLocal, AllreduceLocal>(
+      "local<float16> max", 3, 65539, 4, ReductionFunction<float16>::max);
+  compare<int32_t, HipAllreduceLocal, AllreduceLocal>(
+      "local<int32> product", 1, 4099, 2, ReductionFunction<int32_t>::product);
+  localAlone();
   interleaved();
   using MathFn = void (*)(void*, const void*, const void*, size_t);
   compareFn<float>("allreduce(opts) RING float sum", 3, 100003, 0, 1,

@@ -130,6 +130,37 @@ void stridePattern(const char* name, int P, int nptrs, int N) {
   });
 }
 
+// HipAllreduceLocal (gloo/cuda_allreduce_local.h, allreduce_local.cc:21-31):
+// each rank's own pointers folded and copied back, nothing from the peers.
+void localPointers(int P, int nptrs, int N) {
+  spawn(P, [&](std::shared_ptr<gloo_amd::Context> ctx) {
+    std::vector<float*> devs(nptrs);
+    for (int i = 0; i < nptrs; i++) {
+      std::vector<float> host(N);
+      for (int j = 0; j < N; j++) host[j] = (float)(j * nptrs + i + ctx->rank * 1000);
+      hipCheck(hipMalloc(&devs[i], std::max(N, 1) * sizeof(float)), "hipMalloc");
+      hipCheck(hipMemcpy(devs[i], host.data(), N * sizeof(float), hipMemcpyHostToDevice), "h2d");
+    }
+    {
+      gloo_amd::HipAllreduceLocal<float> alg(ctx, devs, N);
+      alg.run();
+    }
+    for (int i = 0; i < nptrs; i++) {
+      std::vector<float> host(N);
+      hipCheck(hipMemcpy(host.data(), devs[i], N * sizeof(float), hipMemcpyDeviceToHost), "d2h");
+      hipFree(devs[i]);
+      for (int j = 0; j < N; j++) {
+        const float exp = (float)(nptrs * (j * nptrs + ctx->rank * 1000) + nptrs * (nptrs - 1) / 2);
+        if (host[j] != exp) {
+          EXPECT(false, "local P=%d ptrs=%d: rank %d [%d][%d] = %f expected %f", P, nptrs,
+                 ctx->rank, i, j, host[j], exp);
+          break;
+        }
+      }
+    }
+  });
+}
+
 void multipleAlgorithms() {
   const int P = 4, N = 1000;
   spawn(P, [&](std::shared_ptr<gloo_amd::Context> ctx) {
@@ -398,6 +429,9 @@ int main() {
       stridePattern<gloo_amd::HipAllreduceRingChunked>("ring_chunked", P, nptrs, 1000);
       stridePattern<gloo_amd::HipAllreduceHalvingDoubling>("halving_doubling", P, nptrs, 1000);
     }
+  }
+  for (int P : {1, 3}) {
+    for (int nptrs : {1, 2, 5}) localPointers(P, nptrs, 1000);
   }
   multipleAlgorithms();
   customAlgorithm();
