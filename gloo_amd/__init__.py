@@ -14,11 +14,14 @@ from . import math, rendezvous  # noqa: F401
 from .algorithms import (  # noqa: F401
     AllreduceBcube,
     AllreduceHalvingDoubling,
+    AllreduceHalvingDoublingPipelined,
     AllreduceLocal,
     AllreduceRing,
     AllreduceRingChunked,
     HipAllreduceBcube,
     HipAllreduceHalvingDoubling,
+    HipAllreduceHalvingDoublingPipelined,
+    HipAllreduceLocal,
     HipAllreduceRing,
     HipAllreduceRingChunked,
     ReductionFunction,

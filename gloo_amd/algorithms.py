@@ -308,11 +308,21 @@ class AllreduceLocal(Algorithm):
     _algo = ALGO_CODES["local"]
 
 
+class AllreduceHalvingDoublingPipelined(AllreduceHalvingDoubling):
+    """gloo::CudaAllreduceHalvingDoublingPipelined<T>
+    (gloo/cuda_allreduce_halving_doubling_pipelined.h:13-27): halving-doubling
+    with the local broadcast pipelined into the reduce.  Same result bits;
+    the device-driven schedule overlaps its steps either way."""
+    pipelined = True
+
+
 # The device classes under the names the reference's GPU path uses.
 HipAllreduceRingChunked = AllreduceRingChunked
 HipAllreduceHalvingDoubling = AllreduceHalvingDoubling
+HipAllreduceHalvingDoublingPipelined = AllreduceHalvingDoublingPipelined
 HipAllreduceRing = AllreduceRing
 HipAllreduceBcube = AllreduceBcube
+HipAllreduceLocal = AllreduceLocal
 
 
 DEFAULT_MIN_PIECE_BYTES = 4 << 20
