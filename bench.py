@@ -940,9 +940,14 @@ def element_sweep(torch, dist, gloo_amd, ctx, dev, schedules, dtype):
     return out
 
 
-DEFAULT_CANDIDATES = ["ring_chunked", "ring_chunked_mesh", "ring_chunked_host"]
-EXTRA_CANDIDATES = ["ring_chunked_fast", "ring_chunked_system", "ring_chunked_mesh_system",
-                    "ring_chunked_mesh_steps"]
+# the ring and the mesh each moved by CUs (the plan / two-shot kernels
+# storing into the peers' slots) and by DMA engines (host-issued
+# hipMemcpyPeerAsync steps): whether CU stores fill an xGMI link is the one
+# thing no one-GPU box can measure, so the first node run times both ways
+DEFAULT_CANDIDATES = ["ring_chunked", "ring_chunked_mesh", "ring_chunked_host",
+                      "ring_chunked_mesh_steps"]
+EXTRA_CANDIDATES = ["ring_chunked_fast", "ring_chunked_system", "ring_chunked_mesh_system"]
+DMA_CANDIDATES = ("ring_chunked_host", "ring_chunked_mesh_steps")
 DEFAULT_ALTS = ["halving_doubling"]
 EXTRA_ALTS = ["halving_doubling_host", "halving_doubling_system"]
 # host-issued steps' peer-copy transports: (engine, DMA split, copy-kernel workgroups)
@@ -957,10 +962,11 @@ TRANSPORTS_ALL = [("dma", 1, 0), ("dma", 2, 0), ("dma", 4, 0), ("kernel", 1, 32)
 
 def candidate_lists(args):
     """(candidates timed for `value`, schedules timed beside them).  The
-    default run keeps to four schedules -- the north star's ring on the plan
-    kernel, the mesh on the two-shot kernel, the ring as host-issued steps,
-    and halving-doubling on the plan kernel -- each one more chance for a
-    first run on new hardware to fail;
+    default run keeps to five schedules -- the north star's ring on the plan
+    kernel, the mesh on the two-shot kernel, both again as host-issued DMA
+    steps, and halving-doubling on the plan kernel -- each one more chance
+    for a first run on new hardware to fail (a failed
+    candidate is reported and dropped, the others stand);
     --candidates all adds the opt-in engines and stream policies."""
     if args.algo == "ring_chunked" and args.schedule == "auto":
         cands = list(DEFAULT_CANDIDATES)
@@ -1144,7 +1150,7 @@ def bench_multi(args):
         device_engine = probe.engine() != "steps"
         probe.close()
         if args.copy_split == "auto" and not device_engine:
-            for tr in (TRANSPORTS_DMA if algo == "ring_chunked_host" and args.calibrate != "all"
+            for tr in (TRANSPORTS_DMA if algo in DMA_CANDIDATES and args.calibrate != "all"
                        else transports):
                 set_transport(tr)
                 buf.copy_(src)
