@@ -96,7 +96,7 @@ def test_command_line_mirrors_the_reference():
         assert gb.parse_args([name]).benchmark == name
 
 
-def _run(tmp_path, P, args, timeout=240):
+def _run(tmp_path, P, args, timeout=150):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     if P > 1:
         env["GPU_MAX_HW_QUEUES"] = "1"

@@ -31,7 +31,8 @@ What matches the reference:
   this path reproduces the reference's bits, not the arithmetic sum;
 * sampling (runner.cc:270-357): warmup runs, then an iteration count from
   --iteration-count or from --iteration-time (default 2 s) over the warmup
-  median (agreed from rank 0), raised 1.2x until the samples cover the time;
+  median, raised 1.2x until the samples cover the time (rank 0 decides
+  both and every rank follows);
   each sample is one run() (results complete on return), between barriers;
 * output (runner.cc:400-520, rank 0): size (B), elements, min / p50 / p99 /
   max latency (us, or ns with --nanos), bandwidth = bytes * samples / total
@@ -278,12 +279,17 @@ def main(argv=None):
             iters = rdv.broadcast(max(1, a.iteration_time // max(1, med)))
         while True:
             res = sample(iters)
-            if a.iteration_count > 0 or sum(res) > a.iteration_time or iters >= K_MAX_ITERATIONS:
+            if a.iteration_count > 0:
                 break
-            nxt = int(K_ITERS_MULTIPLIER * iters)
-            if nxt <= iters:
-                nxt += 1
+            # rank 0 decides whether the samples cover the time and every rank
+            # follows (each rank judging its own samples could split them: one
+            # stops while another waits for the next round)
+            nxt = 0
+            if sum(res) <= a.iteration_time and iters < K_MAX_ITERATIONS:
+                nxt = max(int(K_ITERS_MULTIPLIER * iters), iters + 1)
             iters = rdv.broadcast(min(nxt, K_MAX_ITERATIONS))
+            if iters == 0:
+                break
         alg.close()
         if a.rank == 0:
             lat = sorted(res)
