@@ -544,17 +544,25 @@ def plan_hbm_bytes(gloo_amd, algo, rank, world, count, es, fused=False):
     mesh 6.375 S; halving-doubling 7.875 S.  fused: the plan
     kernel's reduce-and-forward -- a SEND of exactly the range the REDUCE or
     COPY before it (past RELEASEs only) just wrote reads nothing more, it only
-    writes the receiver's copy: the ring at P=8 then moves 6.125 S."""
+    writes the receiver's copy, and a fused REDUCE whose result the buffer
+    never reads again (plan.h StepSync::keep 0: the ring's partial sums)
+    writes only that copy: the ring at P=8 then moves 5.5 S (6.25 S before
+    round 4's dead-write elision)."""
     steps, _, folds = gloo_amd.plan(plan_name(algo), rank, world, count, with_folds=True)
+    keep = None
+    if fused:
+        sy = gloo_amd.plan_sync(plan_name(algo), rank, world, count, 1)
+        if sy["slots"] == 2:  # the kernel fuses only with two landing slots
+            keep = [st[8] for st in sy["steps"]]
     total = 0
     last = None  # (off, len) of the last REDUCE / COPY, while only RELEASEs follow it
-    for st in steps:
+    for i, st in enumerate(steps):
         kind, off, ln = st[0], st[3], st[4]
         if kind == 0:
             total += (1 if fused and last == (off, ln) else 2) * ln
             last = None
         elif kind == 2:
-            total += 3 * ln
+            total += (2 if keep is not None and keep[i] == 0 else 3) * ln
             last = (off, ln)
         elif kind == 3:
             total += 2 * ln

@@ -727,7 +727,7 @@ int64_t glx_plan_sync(int algo, int rank, int size, int64_t count, int esize,
     }
     for (int64_t i = 0; i < n && i < cap && steps != nullptr; i++) {
       const glx::StepSync& y = t.steps[(size_t)i];
-      int64_t* o = steps + 8 * i;
+      int64_t* o = steps + 9 * i;
       o[0] = y.chan;
       o[1] = y.seg0;
       o[2] = y.seg1;
@@ -736,6 +736,7 @@ int64_t glx_plan_sync(int algo, int rank, int size, int64_t count, int esize,
       o[5] = y.fuse;
       o[6] = (int64_t)y.rseq;
       o[7] = (int64_t)y.rperRun;
+      o[8] = y.keep;
     }
     return GLX_OK;
   });

@@ -386,7 +386,9 @@ void HipPlanExecutor::buildDevSteps() {
           const glx::Step& t = plan_.steps[(size_t)y.fuse];
           const glx::StepSync& ty = sync_.steps[(size_t)y.fuse];
           const OutChan& oc = out_[(size_t)ty.chan];
-          d.kind = s.kind == glx::REDUCE ? glx::kStepReduceSend : glx::kStepCopySend;
+          d.kind = s.kind == glx::COPY ? glx::kStepCopySend
+                   : y.keep != 0     ? glx::kStepReduceSend
+                                     : glx::kStepReduceForward;
           d.peer = (int32_t)t.peer;
           d.seq = ty.seq;
           d.perRun = ty.perRun;

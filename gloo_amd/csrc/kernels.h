@@ -124,8 +124,10 @@ struct DevSegment {
 // Step kinds of the plan kernel: glx::StepKind (0 SEND, 1 RECV, 2 REDUCE,
 // 3 COPY, 4 RELEASE, 5 FOLD) plus the reduce-and-forward forms (plan.h
 // StepSync::fuse): REDUCE or COPY and the SEND of the same range in one
-// pass, and the SEND they absorbed, which is then skipped.
-constexpr int32_t kStepReduceSend = 6, kStepCopySend = 7, kStepNop = 8;
+// pass, and the SEND they absorbed, which is then skipped; ReduceForward is
+// a ReduceSend whose result goes to the peer's slot only (StepSync::keep 0:
+// the buffer's copy would be overwritten unread).
+constexpr int32_t kStepReduceSend = 6, kStepCopySend = 7, kStepNop = 8, kStepReduceForward = 9;
 struct DevStep {
   int32_t kind;            // glx::StepKind or kStep* above
   int32_t peer;            // reported on timeout

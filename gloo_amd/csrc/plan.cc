@@ -1083,6 +1083,20 @@ SyncTable syncTable(int algo, int rank, int size, int64_t count, const PlanParam
       t.steps[j].fuse = (int32_t)i;
     }
   }
+  // a fused REDUCE's own copy of its result is dead when the range is next
+  // overwritten whole by a COPY before anything reads it (plan.h)
+  for (size_t i = 0; i < mine.steps.size(); i++) {
+    const Step& s = mine.steps[i];
+    if (s.kind != REDUCE || t.steps[i].fuse < 0) continue;
+    const int64_t lo = s.off, hi = s.off + s.len;
+    for (size_t k = (size_t)t.steps[i].fuse + 1; k < mine.steps.size(); k++) {
+      const Step& u = mine.steps[k];
+      if (u.kind == RECV || u.kind == RELEASE || u.len <= 0) continue;
+      if (u.off >= hi || u.off + u.len <= lo) continue;  // disjoint
+      if (u.kind == COPY && u.off <= lo && u.off + u.len >= hi) t.steps[i].keep = 0;
+      break;  // the first step touching the range decides
+    }
+  }
   return t;
 }
 

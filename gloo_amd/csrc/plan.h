@@ -203,12 +203,23 @@ DeviceLayout twoShotLayout(const Plan& plan, int rank, int size, int64_t count, 
 //
 // rseq/rperRun: for a REDUCE or COPY, the message number of the RECV whose
 // landing region it reads (its slot).
+//
+// keep: for a fused REDUCE, whether its result must also stay in the
+// buffer.  In the ring's reduce-scatter a rank forwards each partial sum and
+// never reads it again: the allgather's COPY overwrites the range with the
+// final value first (gloo/allreduce_ring_chunked.h:141-157 then :173-200).
+// keep = 0 when, scanning this rank's program past the fused SEND, the first
+// step touching any element of the range is a COPY covering all of it; any
+// read (REDUCE, SEND, FOLD) or partial overwrite first, or none at all (the
+// value is final), keeps it.  The plan kernel then stores the partial only
+// into the peer's slot: 0.75 S fewer HBM writes per rank at P = 8.
 struct StepSync {
   int32_t chan = -1;
   int32_t seg0 = 0, seg1 = 0;
   uint64_t seq = 0, perRun = 0;
   int32_t fuse = -1;  // REDUCE/COPY: the SEND fused into it; SEND: the step it is in
   uint64_t rseq = 0, rperRun = 0;
+  int32_t keep = 1;
 };
 struct SyncTable {
   std::vector<int64_t> bounds;

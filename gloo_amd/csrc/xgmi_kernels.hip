@@ -230,9 +230,11 @@ __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* 
 // (the ring's chain: the newer rank's value is the in-place destination)
 // or, LEFT, acc = op(acc, s_k) (a left fold, out = op(out, peer)).
 // The result also goes to every outs[d], d < nout.
-// dst is this rank's buffer (stores as FAST says); outs are other ranks'
-// landing slots (system write-through).
-template <typename T, int OP, bool FAST, bool LEFT = false, int MAXK = kOsMaxRanks>
+// dst is this rank's buffer (stores as FAST says; none when !KEEP: the
+// result goes to the outs only); outs are other ranks' landing slots
+// (system write-through).
+template <typename T, int OP, bool FAST, bool LEFT = false, int MAXK = kOsMaxRanks,
+          bool KEEP = true>
 __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
                                           const typename Elem<T, OP>::S* const* srcs, int P,
                                           char* const* outs, int nout, size_t a, size_t b,
@@ -254,7 +256,7 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
     for (int k = 1; k < MAXK; k++) {
       if (k < P) acc = LEFT ? E::apply(acc, y[k]) : E::apply(y[k], acc);
     }
-    put1<LSP>(dst + i, acc);
+    if (KEEP) put1<LSP>(dst + i, acc);
 #pragma unroll
     for (int d = 0; d < MAXK - 1; d++) {
       if (d < nout) put1<kStRemote>(reinterpret_cast<S*>(outs[d]) + i, acc);
@@ -286,9 +288,11 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
         }
       }
     }
-    const VecOut<LSP> od(dst, va);
+    if (KEEP) {
+      const VecOut<LSP> od(dst, va);
 #pragma unroll
-    for (int u = 0; u < U; u++) od.put(v + u * kBlock, acc[u]);
+      for (int u = 0; u < U; u++) od.put(v + u * kBlock, acc[u]);
+    }
 #pragma unroll
     for (int d = 0; d < MAXK - 1; d++) {
       if (d < nout) {
@@ -309,7 +313,7 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
     for (int k = 1; k < MAXK; k++) {
       if (k < P) acc = LEFT ? vec_apply<T, OP>(acc, y[k]) : vec_apply<T, OP>(y[k], acc);
     }
-    VecOut<LSP>(dst, va).put(v, acc);
+    if (KEEP) VecOut<LSP>(dst, va).put(v, acc);
 #pragma unroll
     for (int d = 0; d < MAXK - 1; d++) {
       if (d < nout) VecOut<kStRemote>(outs[d], va).put(v, acc);
@@ -638,9 +642,10 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
     const uint64_t seq = p.run * st.perRun + st.seq;
     stamp(2 * i);
     switch (st.kind) {
-      case 0:                  // SEND, once the receiver has consumed message seq-slots
-      case kStepReduceSend:    // REDUCE + SEND of its result in one pass
-      case kStepCopySend: {    // COPY + SEND of its result in one pass
+      case 0:                    // SEND, once the receiver has consumed message seq-slots
+      case kStepReduceSend:      // REDUCE + SEND of its result in one pass
+      case kStepReduceForward:   // the same, result to the peer only
+      case kStepCopySend: {      // COPY + SEND of its result in one pass
         if (seq > (uint64_t)p.slots &&
             !wait_flag(flag_at(st.credit, w), seq - p.slots, st.peer,
                        __builtin_amdgcn_s_memrealtime(), p.timeoutTicks, p.status, p.claim,
@@ -667,6 +672,8 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
             if (st.kind == kStepCopySend) {
               scatter_span<S, FAST, FAST ? kStLocalWt : kStPlain, 1, 2>(outs, 2, src, a, b,
                                                                         aligned);
+            } else if (st.kind == kStepReduceForward) {
+              fold_span<T, OP, FAST, true, 2, false>(buf, srcs, 2, outs + 1, 1, a, b, aligned);
             } else {
               fold_span<T, OP, FAST, true, 2>(buf, srcs, 2, outs + 1, 1, a, b, aligned);
             }

@@ -95,12 +95,14 @@ def simulate(name, P, N, G, op, ins, runs=2, es=4, fuse=True):
             return False
         i = pc[r][w]
         kind, peer, tag, off, ln, boff, dst_off, flags = steps[i]
-        chan, s0, s1, seq, per, fz, rseq, rper = syncs[r]["steps"][i]
+        chan, s0, s1, seq, per, fz, rseq, rper, keep = syncs[r]["steps"][i]
         s = run[r][w] * per + seq
         rslot = (run[r][w] * rper + rseq - 1) % K if kind in (REDUCE, COPY) else 0
 
-        def send(j):
-            """SEND step j's stores and delivery (its credit already held)."""
+        def send(j, vals=None):
+            """SEND step j's stores and delivery (its credit already held);
+            vals: the values per part when they are not in the buffer (a
+            fused REDUCE with keep 0 stores its result to the peer only)."""
             _, peer_, tag_, off_, _, _, dst_off_, _ = steps[j]
             _, s0_, s1_, seq_, per_ = syncs[r]["steps"][j][:5]
             m = run[r][w] * per_ + seq_
@@ -109,7 +111,7 @@ def simulate(name, P, N, G, op, ins, runs=2, es=4, fuse=True):
                 p0, p1 = pos(dst_off_, off_, a), pos(dst_off_, off_, b)
                 if pending[peer_][slot][p0:p1].any():
                     raise Clobber("rank %d wg %d overwrote unread data of rank %d" % (r, w, peer_))
-                scratch[peer_][slot][p0:p1] = bufs[r][a:b]
+                scratch[peer_][slot][p0:p1] = bufs[r][a:b] if vals is None else vals[(a, b)]
                 pending[peer_][slot][p0:p1] = True
             delivery[peer_][in_ch[peer_][(r, tag_)]][w] = m
 
@@ -129,7 +131,16 @@ def simulate(name, P, N, G, op, ins, runs=2, es=4, fuse=True):
         elif kind == RECV:
             if delivery[r][chan][w] < s:
                 return False
-        if kind == REDUCE:
+        if kind == REDUCE and fused and not keep:
+            # the kernel's ReduceForward: the partial goes to the peer only;
+            # the buffer keeps its old value, which must never be read again
+            vals = {}
+            for a, b in parts(s0, s1, w):
+                vals[(a, b)] = O.reduce(op, O.FLOAT32, bufs[r][a:b],
+                                        read(r, boff, off, a, b, rslot))
+                bufs[r][a:b] = np.nan  # poison: a later read would show in the result
+            send(fz, vals)
+        elif kind == REDUCE:
             for a, b in parts(s0, s1, w):
                 bufs[r][a:b] = O.reduce(op, O.FLOAT32, bufs[r][a:b],
                                         read(r, boff, off, a, b, rslot))
@@ -308,3 +319,25 @@ def test_ring_forwards_every_reduced_and_copied_chunk(name, P, N):
         assert all(steps[k][0] == RELEASE for k in range(j + 1, i))
     if name == "ring_chunked":
         assert len(sends) == 4 * P - 4 and len(fused) == 4 * P - 6  # all but the prelude
+
+
+@pytest.mark.parametrize("P", [2, 3, 4, 8])
+def test_ring_partial_sums_are_forwarded_not_stored(P):
+    """plan.h StepSync::keep: in ring_chunked's reduce-scatter a rank's
+    partial sums go only into the next rank's slot (kStepReduceForward);
+    only the two reductions that finish its own chunks stay in its buffer.
+    The protocol simulation above poisons every unstored range and still
+    matches the oracle bit for bit."""
+    N = 1 << 20
+    for r in range(P):
+        steps = gloo_amd.plan("ring_chunked", r, P, N)[0]
+        sy = gloo_amd.plan_sync("ring_chunked", r, P, N, 4)["steps"]
+        fused = [i for i, st in enumerate(steps) if st[0] == REDUCE and sy[i][5] >= 0]
+        dead = [i for i in fused if sy[i][8] == 0]
+        assert len(fused) == 2 * (P - 1) and len(dead) == 2 * (P - 2), (r, len(fused), len(dead))
+        for i in dead:  # the first later step touching the range overwrites it whole
+            lo, hi = steps[i][3], steps[i][3] + steps[i][4]
+            nxt = [st for st in steps[sy[i][5] + 1:]
+                   if st[0] not in (RECV, RELEASE) and st[4] > 0
+                   and st[3] < hi and st[3] + st[4] > lo][0]
+            assert nxt[0] == COPY and nxt[3] <= lo and nxt[3] + nxt[4] >= hi
