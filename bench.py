@@ -542,36 +542,35 @@ def plan_hbm_bytes(gloo_amd, algo, rank, world, count, es, fused=False):
     a FOLD of k sources reads k and writes 1 -- per element.  Ring at P=8:
     sends 2 x 1.75 S + reduces 3 x 0.875 S + copies 2 x 0.875 S = 7.875 S;
     mesh 6.375 S; halving-doubling 7.875 S.  fused: the plan
-    kernel's reduce-and-forward -- a SEND of exactly the range the REDUCE or
-    COPY before it (past RELEASEs only) just wrote reads nothing more, it only
-    writes the receiver's copy, and a fused REDUCE whose result the buffer
-    never reads again (plan.h StepSync::keep 0: the ring's partial sums)
-    writes only that copy: the ring at P=8 then moves 5.5 S (6.25 S before
-    round 4's dead-write elision)."""
+    kernel's reduce-and-forward (plan.h StepSync) -- a SEND done in the pass
+    of the REDUCE or COPY before it reads nothing more, it only writes the
+    receiver's copy (for a partial one, plan.h "pre", the overlap only), and
+    a REDUCE whose result (overlap) the buffer never reads again writes only
+    that copy: the ring at P=8 moves 5.5 S (6.25 S before round 4's
+    dead-write elision), halving-doubling 6.625 S."""
     steps, _, folds = gloo_amd.plan(plan_name(algo), rank, world, count, with_folds=True)
-    keep = None
+    sync = None
     if fused:
         sy = gloo_amd.plan_sync(plan_name(algo), rank, world, count, 1)
         if sy["slots"] == 2:  # the kernel fuses only with two landing slots
-            keep = [st[8] for st in sy["steps"]]
+            sync, bounds = sy["steps"], sy["bounds"]
     total = 0
-    last = None  # (off, len) of the last REDUCE / COPY, while only RELEASEs follow it
     for i, st in enumerate(steps):
-        kind, off, ln = st[0], st[3], st[4]
+        kind, ln = st[0], st[4]
+        y = sync[i] if sync is not None else None
+        over = (bounds[y[11]] - bounds[y[10]]) if y is not None and y[9] >= 0 else 0
         if kind == 0:
-            total += (1 if fused and last == (off, ln) else 2) * ln
-            last = None
+            if y is not None and y[5] >= 0:
+                total += ln          # done in the REDUCE / COPY pass: the peer's copy only
+            else:
+                total += 2 * ln - over  # the overlap was stored by the pass before
         elif kind == 2:
-            total += (2 if keep is not None and keep[i] == 0 else 3) * ln
-            last = (off, ln)
+            dead = (ln if y[5] >= 0 else over) if y is not None and y[8] == 0 else 0
+            total += 3 * ln - dead
         elif kind == 3:
             total += 2 * ln
-            last = (off, ln)
         elif kind == 5:
             total += (len(folds.get(st[5], [])) + 1) * ln
-            last = None
-        elif kind != 4:
-            last = None
     return total * es
 
 

@@ -397,10 +397,12 @@ def plan_sync(algo, rank, size, count, G, esize=4, max_segment_size=0,
     """The plan kernel's bookkeeping for one rank with G workgroups
     (glx_plan_sync, host logic): dict with bounds (segment bounds), slice,
     safe, slots (landing slots per channel), steps [(channel, seg0, seg1,
-    seq, per_run, fuse, rseq, rper_run, keep)] (fuse: the SEND a REDUCE/COPY
-    forwards in the same pass, or the step a SEND is done in, -1 otherwise;
-    rseq/rper_run: the message a REDUCE/COPY reads; keep: 0 for a fused
-    REDUCE whose result only goes to the peer, plan.h StepSync::keep)."""
+    seq, per_run, fuse, rseq, rper_run, keep, pre, pre0, pre1)] (fuse: the
+    SEND a REDUCE/COPY forwards in the same pass, or the step a SEND is done
+    in, -1 otherwise; rseq/rper_run: the message a REDUCE/COPY reads; keep: 0
+    for a fused REDUCE whose result (a partial one's overlap) only goes to
+    the peer; pre/pre0/pre1: partial reduce-and-forward, the overlap's
+    segments [pre0, pre1) -- plan.h StepSync)."""
     code = ALGO_CODES[algo]
     args = (code, rank, size, count, esize, max_segment_size, min_piece_bytes, G)
     nb = ctypes.c_int64(0)
@@ -409,10 +411,10 @@ def plan_sync(algo, rank, size, count, G, esize=4, max_segment_size=0,
     if n < 0:
         check(_lib.ERR_INVALID, "plan_sync")
     bb = (ctypes.c_int64 * max(nb.value, 1))()
-    sb = (ctypes.c_int64 * max(9 * n, 1))()
+    sb = (ctypes.c_int64 * max(12 * n, 1))()
     lib.glx_plan_sync(*args, bb, nb.value, ctypes.byref(nb), info, sb, n)
     return {"bounds": list(bb[:nb.value]), "slice": info[0], "safe": bool(info[1]),
-            "slots": info[2], "steps": [tuple(sb[9 * i:9 * i + 9]) for i in range(n)]}
+            "slots": info[2], "steps": [tuple(sb[12 * i:12 * i + 12]) for i in range(n)]}
 
 
 def stage_plan(algo, rank, size, count, esize=4, max_piece=None):

@@ -727,7 +727,7 @@ int64_t glx_plan_sync(int algo, int rank, int size, int64_t count, int esize,
     }
     for (int64_t i = 0; i < n && i < cap && steps != nullptr; i++) {
       const glx::StepSync& y = t.steps[(size_t)i];
-      int64_t* o = steps + 9 * i;
+      int64_t* o = steps + 12 * i;
       o[0] = y.chan;
       o[1] = y.seg0;
       o[2] = y.seg1;
@@ -737,6 +737,9 @@ int64_t glx_plan_sync(int algo, int rank, int size, int64_t count, int esize,
       o[6] = (int64_t)y.rseq;
       o[7] = (int64_t)y.rperRun;
       o[8] = y.keep;
+      o[9] = y.pre;
+      o[10] = y.pre0;
+      o[11] = y.pre1;
     }
     return GLX_OK;
   });

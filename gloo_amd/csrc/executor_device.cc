@@ -358,6 +358,7 @@ void HipPlanExecutor::buildDevSteps() {
     d.rseq = y.rseq;
     d.rperRun = y.rperRun;
     const bool fused = slots_ == 2 && y.fuse >= 0;
+    const bool pre = slots_ == 2 && y.pre >= 0;  // partial reduce-and-forward
     switch (s.kind) {
       case glx::SEND: {
         GLX_ENFORCE(y.chan == stepChan_[i], "plan kernel: channel numbering disagrees");
@@ -368,6 +369,10 @@ void HipPlanExecutor::buildDevSteps() {
         d.flag = oc.devDelivery;
         d.credit = rows + (size_t)oc.creditWord * G * glx::kFlagStride;
         if (fused) d.kind = glx::kStepNop;  // done inside step y.fuse
+        if (pre) {  // segments [pre0, pre1) were stored by step y.pre
+          d.pre0 = y.pre0;
+          d.pre1 = y.pre1;
+        }
         break;
       }
       case glx::RECV:
@@ -396,6 +401,21 @@ void HipPlanExecutor::buildDevSteps() {
           d.dstSlot = (int64_t)slotBytes(blockOf(peerBlocks_[oc.peer], t.dst_off));
           d.flag = oc.devDelivery;
           d.credit = rows + (size_t)oc.creditWord * G * glx::kFlagStride;
+        } else if (pre) {  // the overlap into the next SEND's slot, after its credit
+          const glx::Step& t = plan_.steps[(size_t)y.pre];
+          const glx::StepSync& ty = sync_.steps[(size_t)y.pre];
+          const OutChan& oc = out_[(size_t)ty.chan];
+          d.kind = s.kind == glx::COPY ? glx::kStepCopyPre
+                   : y.keep != 0     ? glx::kStepReducePre
+                                     : glx::kStepReducePreForward;
+          d.peer = (int32_t)t.peer;
+          d.seq = ty.seq;
+          d.perRun = ty.perRun;
+          d.dst = vbase(landing(peerBlocks_[oc.peer], t.dst_off, t.off), t.off);
+          d.dstSlot = (int64_t)slotBytes(blockOf(peerBlocks_[oc.peer], t.dst_off));
+          d.credit = rows + (size_t)oc.creditWord * G * glx::kFlagStride;
+          d.pre0 = y.pre0;
+          d.pre1 = y.pre1;
         }
         break;
       }

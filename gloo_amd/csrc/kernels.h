@@ -128,12 +128,18 @@ struct DevSegment {
 // a ReduceSend whose result goes to the peer's slot only (StepSync::keep 0:
 // the buffer's copy would be overwritten unread).
 constexpr int32_t kStepReduceSend = 6, kStepCopySend = 7, kStepNop = 8, kStepReduceForward = 9;
+// Partial reduce-and-forward (plan.h StepSync::pre): a REDUCE / COPY whose
+// segments [pre0, pre1) also go into the next SEND's slot (ReducePreForward:
+// into that slot only), and that SEND (kind 0 with pre0 < pre1) storing only
+// its other segments before it signals.
+constexpr int32_t kStepReducePre = 10, kStepReducePreForward = 11, kStepCopyPre = 12;
 struct DevStep {
   int32_t kind;            // glx::StepKind or kStep* above
   int32_t peer;            // reported on timeout
   int32_t seg0, seg1;      // the step's element range = segments [seg0, seg1)
   int32_t nsrc;            // FOLD: number of sources, first at foldSrc[srcIndex]
   int32_t left;            // FOLD: 1 = left fold (plan.h kFoldLeft), 0 = the ring's chain
+  int32_t pre0, pre1;      // partial reduce-and-forward: the overlap's segments
   int64_t srcIndex;
   const char* src;         // REDUCE / COPY: landing region (slot 0) as a virtual buffer
   char* dst;               // SEND: the peer's landing region (slot 0) as a virtual buffer

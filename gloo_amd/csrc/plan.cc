@@ -1083,13 +1083,33 @@ SyncTable syncTable(int algo, int rank, int size, int64_t count, const PlanParam
       t.steps[j].fuse = (int32_t)i;
     }
   }
-  // a fused REDUCE's own copy of its result is dead when the range is next
-  // overwritten whole by a COPY before anything reads it (plan.h)
+  // partial reduce-and-forward: the SEND after a REDUCE / COPY (past
+  // RELEASEs only) overlaps its range without equalling it (plan.h "pre")
+  for (size_t i = 0; i < mine.steps.size() && t.slots == 2; i++) {
+    const Step& s = mine.steps[i];
+    if ((s.kind != REDUCE && s.kind != COPY) || s.len <= 0 || t.steps[i].fuse >= 0) continue;
+    size_t j = i + 1;
+    while (j < mine.steps.size() && mine.steps[j].kind == RELEASE) j++;
+    if (j >= mine.steps.size()) continue;
+    const Step& u = mine.steps[j];
+    if (u.kind != SEND || u.len <= 0 || t.steps[j].fuse >= 0 || t.steps[j].pre >= 0) continue;
+    const int64_t lo = std::max(s.off, u.off), hi = std::min(s.off + s.len, u.off + u.len);
+    if (lo >= hi) continue;
+    t.steps[i].pre = (int32_t)j;
+    t.steps[j].pre = (int32_t)i;
+    t.steps[i].pre0 = t.steps[j].pre0 = segIndex(lo);
+    t.steps[i].pre1 = t.steps[j].pre1 = segIndex(hi);
+  }
+  // a fused REDUCE's own copy of its result (of the overlap, for a partial
+  // one) is dead when the range is next overwritten whole by a COPY before
+  // anything reads it (plan.h)
   for (size_t i = 0; i < mine.steps.size(); i++) {
     const Step& s = mine.steps[i];
-    if (s.kind != REDUCE || t.steps[i].fuse < 0) continue;
-    const int64_t lo = s.off, hi = s.off + s.len;
-    for (size_t k = (size_t)t.steps[i].fuse + 1; k < mine.steps.size(); k++) {
+    const StepSync& y = t.steps[i];
+    if (s.kind != REDUCE || (y.fuse < 0 && y.pre < 0)) continue;
+    const int64_t lo = y.fuse >= 0 ? s.off : t.bounds[(size_t)y.pre0];
+    const int64_t hi = y.fuse >= 0 ? s.off + s.len : t.bounds[(size_t)y.pre1];
+    for (size_t k = (size_t)(y.fuse >= 0 ? y.fuse : y.pre) + 1; k < mine.steps.size(); k++) {
       const Step& u = mine.steps[k];
       if (u.kind == RECV || u.kind == RELEASE || u.len <= 0) continue;
       if (u.off >= hi || u.off + u.len <= lo) continue;  // disjoint

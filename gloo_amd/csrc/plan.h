@@ -213,6 +213,16 @@ DeviceLayout twoShotLayout(const Plan& plan, int rank, int size, int64_t count, 
 // read (REDUCE, SEND, FOLD) or partial overwrite first, or none at all (the
 // value is final), keeps it.  The plan kernel then stores the partial only
 // into the peer's slot: 0.75 S fewer HBM writes per rank at P = 8.
+//
+// pre: partial reduce-and-forward, where the SEND after a REDUCE / COPY (past
+// RELEASEs only) covers part of its range, or more: halving-doubling's
+// reduce-scatter reduces a block and sends half of it on in the next step,
+// its allgather copies a block in and sends it on together with the rest.
+// The REDUCE / COPY names that SEND (pre) and stores the overlap's segments
+// [pre0, pre1) into the receiver's slot in the same pass, after the SEND's
+// credit; the SEND (pre = that step, same pre0 / pre1) stores only its other
+// segments and then signals the message.  keep applies to the overlap of a
+// REDUCE (0: the overlap's values go to the peer only).
 struct StepSync {
   int32_t chan = -1;
   int32_t seg0 = 0, seg1 = 0;
@@ -220,6 +230,8 @@ struct StepSync {
   int32_t fuse = -1;  // REDUCE/COPY: the SEND fused into it; SEND: the step it is in
   uint64_t rseq = 0, rperRun = 0;
   int32_t keep = 1;
+  int32_t pre = -1;           // see above
+  int32_t pre0 = 0, pre1 = 0;  // the overlap, in segments
 };
 struct SyncTable {
   std::vector<int64_t> bounds;

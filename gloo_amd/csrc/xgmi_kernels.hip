@@ -642,6 +642,42 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
     const uint64_t seq = p.run * st.perRun + st.seq;
     stamp(2 * i);
     switch (st.kind) {
+      case kStepReducePre:          // REDUCE, the overlap also into the next SEND's slot
+      case kStepReducePreForward:   // the same, the overlap into that slot only
+      case kStepCopyPre: {          // COPY, the overlap also into the next SEND's slot
+        if (seq > (uint64_t)p.slots &&
+            !wait_flag(flag_at(st.credit, w), seq - p.slots, st.peer,
+                       __builtin_amdgcn_s_memrealtime(), p.timeoutTicks, p.status, p.claim,
+                       &s_ok, narrow, /*acquire=*/false, 1 + i)) {
+          return;
+        }
+        stamp(2 * i + 1);
+        char* dst = st.dst + slotOf(seq) * (uint64_t)st.dstSlot;
+        const S* src = reinterpret_cast<const S*>(
+            st.src + slotOf(p.run * st.rperRun + st.rseq) * (uint64_t)st.srcSlot);
+        char* outs[2] = {reinterpret_cast<char*>(buf), dst};
+        const S* srcs[2] = {buf, src};
+        for (int g = st.seg0; g < st.seg1; g++) {
+          size_t a, b;
+          if (!seg_part(p.segs[g], w, a, b)) continue;
+          const bool over = g >= st.pre0 && g < st.pre1;
+          if (st.kind == kStepCopyPre) {
+            if (over) {
+              scatter_span<S, FAST, FAST ? kStLocalWt : kStPlain, 1, 2>(outs, 2, src, a, b,
+                                                                        aligned);
+            } else {
+              copy_span<S, FAST, FAST ? kStLocalWt : kStPlain>(buf, src, a, b, aligned);
+            }
+          } else if (!over) {
+            fold_span<T, OP, FAST, true, 2>(buf, srcs, 2, nullptr, 0, a, b, aligned);
+          } else if (st.kind == kStepReducePreForward) {
+            fold_span<T, OP, FAST, true, 2, false>(buf, srcs, 2, outs + 1, 1, a, b, aligned);
+          } else {
+            fold_span<T, OP, FAST, true, 2>(buf, srcs, 2, outs + 1, 1, a, b, aligned);
+          }
+        }
+        break;  // the SEND signals the message once its other segments are stored
+      }
       case 0:                    // SEND, once the receiver has consumed message seq-slots
       case kStepReduceSend:      // REDUCE + SEND of its result in one pass
       case kStepReduceForward:   // the same, result to the peer only
@@ -657,6 +693,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
         if (st.kind == 0) {
           for (int g = st.seg0; g < st.seg1; g++) {
             size_t a, b;
+            if (g >= st.pre0 && g < st.pre1) continue;  // stored by the step before
             if (seg_part(p.segs[g], w, a, b)) {
               copy_span<S, FAST, kStRemote>(reinterpret_cast<S*>(dst), buf, a, b, aligned);
             }

@@ -493,8 +493,9 @@ int64_t glx_device_layout(int algo, int rank, int size, int64_t count, int esize
  * their number), info = {slice, safe, slots} (3 int64: elements per
  * workgroup slice; 1 if no landing region is shared by two workgroups across
  * messages, else the executor keeps host-issued steps; landing slots per
- * channel, 1 or 2: message n lands in slot (n-1) % slots), and per step 9
- * int64 {channel, seg0, seg1, seq, perRun, fuse, rseq, rperRun, keep} (channel =
+ * channel, 1 or 2: message n lands in slot (n-1) % slots), and per step 12
+ * int64 {channel, seg0, seg1, seq, perRun, fuse, rseq, rperRun, keep, pre,
+ * pre0, pre1} (channel =
  * out-channel index for SEND, in-channel index for RECV/RELEASE, -1
  * otherwise; seq = message number within a run, 1-based; fuse = for a
  * REDUCE/COPY the index of the SEND of the same range the kernel does in the
@@ -502,8 +503,12 @@ int64_t glx_device_layout(int algo, int rank, int size, int64_t count, int esize
  * of the step it is done in, else -1; rseq/rperRun = for a REDUCE/COPY the
  * number of the message it reads; keep = 0 for a fused REDUCE whose result
  * is overwritten whole by a later COPY before anything reads it -- the
- * kernel then stores it only into the peer's slot -- else 1).  Returns the
- * number of steps or -1. */
+ * kernel then stores it only into the peer's slot -- else 1; for a partial
+ * one, of its overlap; pre / pre0 / pre1 = partial reduce-and-forward, where
+ * the SEND after a REDUCE / COPY overlaps its range without equalling it: the
+ * REDUCE / COPY names the SEND and stores the overlap's segments [pre0, pre1)
+ * into its slot, the SEND names the step and stores only its other segments;
+ * -1 / 0 / 0 otherwise, plan.h StepSync).  Returns the number of steps or -1. */
 int64_t glx_plan_sync(int algo, int rank, int size, int64_t count, int esize,
                       int64_t max_segment_bytes, int64_t min_piece_bytes, int G,
                       int64_t* bounds, int64_t bounds_cap, int64_t* nbounds, int64_t* info,

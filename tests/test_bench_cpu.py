@@ -108,6 +108,26 @@ def test_fused_hbm_bytes_ring_p8():
     assert hbm == 88 * S // 16
 
 
+def test_fused_hbm_bytes_halving_doubling_p8():
+    """Halving-doubling's partial reduce-and-forward (plan.h StepSync::pre):
+    a reduce-scatter step's reduction stores the half sent on next straight
+    into that peer's slot (and not into the buffer: the allgather overwrites
+    it), an allgather COPY also stores into the next peer's slot: 7.875 S -
+    1/16 S (the one exact fusion) - 1.125 S (reads and dead writes the
+    partial ones save) = 6.625 S at P = 8 (configs[3])."""
+    gloo_amd = pytest.importorskip("gloo_amd")
+    n, es = 1 << 20, 4
+    S = n * es
+    hbm = bench.plan_hbm_bytes(gloo_amd, "halving_doubling", 0, 8, n, es, fused=True)
+    assert hbm == 106 * S // 16
+    sy = gloo_amd.plan_sync("halving_doubling", 0, 8, n, 1)["steps"]
+    steps = gloo_amd.plan("halving_doubling", 0, 8, n)[0]
+    partial = [(i, y[9]) for i, y in enumerate(sy) if steps[i][0] in (2, 3) and y[9] >= 0]
+    assert len(partial) == 4
+    for i, j in partial:
+        assert steps[j][0] == 0 and sy[j][9] == i and sy[j][10:12] == sy[i][10:12]
+
+
 def test_north_star_block_p8():
     S = 256 << 20
     ns = bench.north_star_block(S, 8, 3.5e-3, 3.4e-3, "devsteps", 100 * S // 16)

@@ -41,8 +41,11 @@ def simulate(name, P, N, G, op, ins, runs=2, es=4, fuse=True):
     assert bounds[0] == 0 and bounds[-1] == N and bounds == sorted(set(bounds))
     assert sl % V == 0 and G * sl >= max(b - a for a, b in zip(bounds, bounds[1:]))
 
-    def parts(s0, s1, w):
+    def parts(s0, s1, w, segs=None):
+        """w's part of each segment in [s0, s1); segs: only those (a range)"""
         for g in range(s0, s1):
+            if segs is not None and not segs[0] <= g < segs[1]:
+                continue
             lo, hi = bounds[g], bounds[g + 1]
             a, b = min(lo + w * sl, hi), min(lo + (w + 1) * sl, hi)
             if a < b:
@@ -95,43 +98,70 @@ def simulate(name, P, N, G, op, ins, runs=2, es=4, fuse=True):
             return False
         i = pc[r][w]
         kind, peer, tag, off, ln, boff, dst_off, flags = steps[i]
-        chan, s0, s1, seq, per, fz, rseq, rper, keep = syncs[r]["steps"][i]
+        chan, s0, s1, seq, per, fz, rseq, rper, keep, pre, pre0, pre1 = syncs[r]["steps"][i]
         s = run[r][w] * per + seq
         rslot = (run[r][w] * rper + rseq - 1) % K if kind in (REDUCE, COPY) else 0
 
-        def send(j, vals=None):
+        def send(j, vals=None, only=None, skip=None, deliver=True):
             """SEND step j's stores and delivery (its credit already held);
             vals: the values per part when they are not in the buffer (a
-            fused REDUCE with keep 0 stores its result to the peer only)."""
+            fused REDUCE with keep 0 stores its result to the peer only);
+            only / skip: a segment range to store alone (a partial
+            reduce-and-forward's pass, which does not deliver) or to leave
+            out (the SEND after it)."""
             _, peer_, tag_, off_, _, _, dst_off_, _ = steps[j]
             _, s0_, s1_, seq_, per_ = syncs[r]["steps"][j][:5]
             m = run[r][w] * per_ + seq_
             slot = (m - 1) % K
-            for a, b in parts(s0_, s1_, w):
-                p0, p1 = pos(dst_off_, off_, a), pos(dst_off_, off_, b)
-                if pending[peer_][slot][p0:p1].any():
-                    raise Clobber("rank %d wg %d overwrote unread data of rank %d" % (r, w, peer_))
-                scratch[peer_][slot][p0:p1] = bufs[r][a:b] if vals is None else vals[(a, b)]
-                pending[peer_][slot][p0:p1] = True
-            delivery[peer_][in_ch[peer_][(r, tag_)]][w] = m
+            for g in range(s0_, s1_):
+                if only is not None and not only[0] <= g < only[1]:
+                    continue
+                if skip is not None and skip[0] <= g < skip[1]:
+                    continue
+                for a, b in parts(g, g + 1, w):
+                    p0, p1 = pos(dst_off_, off_, a), pos(dst_off_, off_, b)
+                    if pending[peer_][slot][p0:p1].any():
+                        raise Clobber("rank %d wg %d overwrote unread data of rank %d"
+                                      % (r, w, peer_))
+                    scratch[peer_][slot][p0:p1] = bufs[r][a:b] if vals is None else vals[(a, b)]
+                    pending[peer_][slot][p0:p1] = True
+            if deliver:
+                delivery[peer_][in_ch[peer_][(r, tag_)]][w] = m
 
         def credit_ok(j):
             chan_, _, _, seq_, per_ = syncs[r]["steps"][j][:5]
             return credit[r][chan_][w] >= run[r][w] * per_ + seq_ - K
 
         fused = fuse and fz >= 0
+        partial = fuse and pre >= 0  # partial reduce-and-forward (plan.h StepSync::pre)
         if kind == SEND and fused:
             pass  # done inside the REDUCE/COPY it was fused into
         elif kind == SEND:
             if not credit_ok(i):
                 return False
-            send(i)
+            send(i, skip=(pre0, pre1) if partial else None)
         elif kind in (REDUCE, COPY) and fused and not credit_ok(fz):
             return False  # the fused pass waits for the SEND's credit first
+        elif kind in (REDUCE, COPY) and partial and not credit_ok(pre):
+            return False  # so does the partial one
         elif kind == RECV:
             if delivery[r][chan][w] < s:
                 return False
-        if kind == REDUCE and fused and not keep:
+        if kind in (REDUCE, COPY) and partial:
+            # the whole range into the buffer, the overlap's segments also (a
+            # dead REDUCE overlap: only) into the next SEND's slot, no delivery
+            vals = {}
+            for a, b in parts(s0, s1, w):
+                land = read(r, boff, off, a, b, rslot)
+                vals[(a, b)] = (land if kind == COPY
+                                else O.reduce(op, O.FLOAT32, bufs[r][a:b], land))
+            for a, b in parts(s0, s1, w):
+                bufs[r][a:b] = vals[(a, b)]
+            send(pre, vals=vals, only=(pre0, pre1), deliver=False)
+            if kind == REDUCE and not keep:
+                for a, b in parts(s0, s1, w, segs=(pre0, pre1)):
+                    bufs[r][a:b] = np.nan  # poison the overlap the kernel does not store
+        elif kind == REDUCE and fused and not keep:
             # the kernel's ReduceForward: the partial goes to the peer only;
             # the buffer keeps its old value, which must never be read again
             vals = {}
