@@ -1010,6 +1010,7 @@ def north_star_block(S, world, t, p50, engine, hbm_bytes):
             "link_frac": round(t_star / t, 4),
             "link_bound_ms": round(t_star * 1e3, 4),
             "target_ms": round(t_star / 0.8 * 1e3, 4),
+            "meets_target": bool(t_star / t >= 0.8),
             "hbm_bytes_per_step": hbm_bytes,
             "hbm_frac": round(hbm_bytes / t / 1e9 / HBM_PEAK_GBPS, 4),
             "note": "link_frac = (2(P-1)/P * S / 153 GB/s) / ms_per_step; the north star "

@@ -136,6 +136,8 @@ def test_north_star_block_p8():
     assert abs(ns["link_bound_ms"] - 3.0704) < 1e-3
     assert abs(ns["target_ms"] - 3.838) < 1e-3
     assert abs(ns["link_frac"] - 3.0704 / 3.5) < 1e-3
+    assert ns["meets_target"] is True  # 3.5 ms <= 3.84 ms
+    assert bench.north_star_block(S, 8, 4.0e-3, 4.0e-3, "devsteps", 0)["meets_target"] is False
 
 
 def _ring_run(t, engine, tr):
