@@ -64,6 +64,8 @@ def main():
         return run_scale(store_dir, rank, size, algo[len("scale:"):])
     if algo.startswith("fuzz:"):
         return run_fuzz(store_dir, rank, size, int(algo[len("fuzz:"):]))
+    if algo.startswith("soak:"):
+        return run_soak(store_dir, rank, size, int(algo[len("soak:"):]))
     if algo.startswith("big:"):
         return run_big(store_dir, rank, size, algo[len("big:"):])
     if algo == "linkprobe":
@@ -672,6 +674,68 @@ def run_engine_choice(store_dir, rank, size):
     ctx.close()
     if not ok:
         print("MISMATCH rank", rank)
+        sys.exit(1)
+    print("OK")
+
+
+def run_soak(store_dir, rank, size, runs):
+    """One instance of each device engine's algorithm run `runs` times back to
+    back (a training job's shape: the run counter, the message numbers
+    j * perRun + seq and the landing slots alternate across many kernel
+    boundaries), fresh inputs every run: small integers in fp32, generated on
+    the device from a (rank, run) seed by every rank for every rank, so the
+    exact sum is each rank's own check -- any order gives the same bits, and
+    a stale slot, a lost flag or a message landing in the wrong run shows up
+    as a wrong element."""
+    import torch
+
+    import gloo_amd
+
+    store = gloo_amd.rendezvous.FileStore(store_dir)
+    ctx = gloo_amd.rendezvous.Context(rank, size, 0)
+    ctx.setTimeout(30)
+    ctx.connectFullMesh(store)
+    # 2^20: a length the plan kernel takes at every P here (ragged lengths
+    # whose chunks land at different 16-byte phases in one region keep the
+    # host-issued steps, plan.h SyncTable::safe; the fuzz covers those)
+    n = 1 << 20
+    dev = torch.device("cuda:0")
+
+    def inputs(r, it):
+        g = torch.Generator(device=dev)
+        g.manual_seed(1000003 * it + r)
+        return torch.randint(-64, 64, (n,), generator=g, device=dev, dtype=torch.int32)
+
+    bufs = {k: torch.empty(n, dtype=torch.float32, device=dev)
+            for k in ("ring", "hd", "mesh", "repl")}
+    algs = {
+        "ring": gloo_amd.AllreduceRingChunked(ctx, [bufs["ring"]], schedule="ring"),
+        "hd": gloo_amd.AllreduceHalvingDoubling(ctx, [bufs["hd"]]),
+        "mesh": gloo_amd.AllreduceRingChunked(ctx, [bufs["mesh"]], schedule="mesh"),
+        "repl": gloo_amd.AllreduceRingChunked(ctx, [bufs["repl"]], schedule="replicated"),
+    }
+    engines = {k: a.engine() for k, a in algs.items()}
+    bad = []
+    for it in range(runs):
+        mine = inputs(rank, it).to(torch.float32)
+        expect = sum(inputs(r, it).to(torch.int64) for r in range(size))
+        for k, a in algs.items():
+            bufs[k].copy_(mine)
+            torch.cuda.synchronize()
+            a.run()
+            got = bufs[k].to(torch.int64)
+            if not torch.equal(got, expect):
+                bad.append((k, it, int((got != expect).sum())))
+        if it % 50 == 0:
+            print("SOAK rank %d run %d ok so far: %s" % (rank, it, not bad), flush=True)
+    for a in algs.values():
+        a.close()
+    store.set("soak/done/%d" % rank, b"1")
+    for r in range(size):
+        store.get("soak/done/%d" % r, timeout_ms=60000)
+    print("ENGINES rank %d %s" % (rank, engines))
+    if bad:
+        print("MISMATCH rank %d %s" % (rank, bad[:10]))
         sys.exit(1)
     print("OK")
 

@@ -1,0 +1,39 @@
+"""Soak: one instance per device engine run hundreds of times back to back
+with fresh inputs each run, one process per rank (tests/mp_worker.py soak) --
+the shape of a training job, which the grid tests (a few runs per instance)
+do not reach: the plan kernel's run counter and per-run message numbers, the
+one- and two-shot kernels' epochs and double-buffered slots, across many
+kernel boundaries.  Every run is checked exactly (integer-valued inputs)."""
+import os
+import subprocess
+import sys
+import tempfile
+
+import pytest
+
+from helpers import rank_env
+
+WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "mp_worker.py")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,runs", [(2, 1000), (4, 600), (8, 300)])
+def test_device_engines_soak(P, runs):
+    with tempfile.TemporaryDirectory() as d:
+        procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), "soak:%d" % runs],
+                                  env=rank_env(P), stdout=subprocess.PIPE,
+                                  stderr=subprocess.STDOUT) for r in range(P)]
+        outs = []
+        for p in procs:
+            try:
+                o, _ = p.communicate(timeout=150)
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+            outs.append(o.decode(errors="replace"))
+    for r, (p, o) in enumerate(zip(procs, outs)):
+        assert p.returncode == 0 and "OK" in o, "rank %d rc=%d:\n%s" % (r, p.returncode, o[-3000:])
+    # one rank per process: the device engines ran (not a host-steps fallback)
+    eng = [l for l in outs[0].splitlines() if l.startswith("ENGINES")][0]
+    assert "devsteps" in eng and "twoshot" in eng and "oneshot" in eng, eng
