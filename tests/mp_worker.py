@@ -65,7 +65,8 @@ def main():
     if algo.startswith("fuzz:"):
         return run_fuzz(store_dir, rank, size, int(algo[len("fuzz:"):]))
     if algo.startswith("soak:"):
-        return run_soak(store_dir, rank, size, int(algo[len("soak:"):]))
+        parts = algo.split(":")
+        return run_soak(store_dir, rank, size, int(parts[1]), uneven=parts[2:] == ["uneven"])
     if algo.startswith("big:"):
         return run_big(store_dir, rank, size, algo[len("big:"):])
     if algo == "linkprobe":
@@ -678,7 +679,7 @@ def run_engine_choice(store_dir, rank, size):
     print("OK")
 
 
-def run_soak(store_dir, rank, size, runs):
+def run_soak(store_dir, rank, size, runs, uneven=False):
     """One instance of each device engine's algorithm run `runs` times back to
     back (a training job's shape: the run counter, the message numbers
     j * perRun + seq and the landing slots alternate across many kernel
@@ -686,7 +687,16 @@ def run_soak(store_dir, rank, size, runs):
     the device from a (rank, run) seed by every rank for every rank, so the
     exact sum is each rank's own check -- any order gives the same bits, and
     a stale slot, a lost flag or a message landing in the wrong run shows up
-    as a wrong element."""
+    as a wrong element.
+
+    uneven: the guide's hand-off test condition (MI355X_MICROARCH.md, "Test
+    every hand-off under UNEVEN load"): every rank starts each run after a
+    random delay of up to 2 ms, and rank 0 keeps a GEMM stream busy on its
+    GPU beside the collective, so workgroups arrive at their flags at
+    different times and some CUs are taken."""
+    import random
+    import time
+
     import torch
 
     import gloo_amd
@@ -715,6 +725,10 @@ def run_soak(store_dir, rank, size, runs):
         "repl": gloo_amd.AllreduceRingChunked(ctx, [bufs["repl"]], schedule="replicated"),
     }
     engines = {k: a.engine() for k, a in algs.items()}
+    rng = random.Random(rank)
+    side = torch.cuda.Stream() if uneven and rank == 0 else None
+    if side is not None:
+        x = torch.randn(2048, 2048, device=dev)
     bad = []
     for it in range(runs):
         mine = inputs(rank, it).to(torch.float32)
@@ -722,12 +736,20 @@ def run_soak(store_dir, rank, size, runs):
         for k, a in algs.items():
             bufs[k].copy_(mine)
             torch.cuda.synchronize()
+            if uneven:
+                if side is not None:
+                    with torch.cuda.stream(side):
+                        for _ in range(4):
+                            x = torch.tanh(x @ x)  # busy CUs while the collective runs
+                time.sleep(rng.random() * 2e-3)
             a.run()
             got = bufs[k].to(torch.int64)
             if not torch.equal(got, expect):
                 bad.append((k, it, int((got != expect).sum())))
         if it % 50 == 0:
             print("SOAK rank %d run %d ok so far: %s" % (rank, it, not bad), flush=True)
+    if side is not None:
+        side.synchronize()
     for a in algs.values():
         a.close()
     store.set("soak/done/%d" % rank, b"1")

@@ -17,10 +17,15 @@ WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "mp_worker.py"
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("P,runs", [(2, 1000), (4, 600), (8, 300)])
-def test_device_engines_soak(P, runs):
+@pytest.mark.parametrize("P,runs,mode", [(2, 1000, ""), (4, 600, ""), (8, 300, ""),
+                                         (4, 150, ":uneven"), (8, 100, ":uneven")])
+def test_device_engines_soak(P, runs, mode):
+    """mode ":uneven": random start delays per rank and run, and a GEMM
+    stream busy on rank 0's GPU beside the collective (the guide's
+    condition for testing hand-offs)."""
     with tempfile.TemporaryDirectory() as d:
-        procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), "soak:%d" % runs],
+        procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P),
+                                   "soak:%d%s" % (runs, mode)],
                                   env=rank_env(P), stdout=subprocess.PIPE,
                                   stderr=subprocess.STDOUT) for r in range(P)]
         outs = []
