@@ -717,13 +717,20 @@ def run_soak(store_dir, rank, size, runs, uneven=False):
         return torch.randint(-64, 64, (n,), generator=g, device=dev, dtype=torch.int32)
 
     bufs = {k: torch.empty(n, dtype=torch.float32, device=dev)
-            for k in ("ring", "hd", "mesh", "repl")}
+            for k in ("ring", "hd", "mesh", "repl", "ring_host")}
     algs = {
         "ring": gloo_amd.AllreduceRingChunked(ctx, [bufs["ring"]], schedule="ring"),
         "hd": gloo_amd.AllreduceHalvingDoubling(ctx, [bufs["hd"]]),
         "mesh": gloo_amd.AllreduceRingChunked(ctx, [bufs["mesh"]], schedule="mesh"),
         "repl": gloo_amd.AllreduceRingChunked(ctx, [bufs["repl"]], schedule="replicated"),
     }
+    # and the host-issued steps (shm delivery / credit counters across runs)
+    gloo_amd.set_steps_engine("host")
+    try:
+        algs["ring_host"] = gloo_amd.AllreduceRingChunked(ctx, [bufs["ring_host"]],
+                                                          schedule="ring")
+    finally:
+        gloo_amd.set_steps_engine("auto")
     engines = {k: a.engine() for k, a in algs.items()}
     rng = random.Random(rank)
     side = torch.cuda.Stream() if uneven and rank == 0 else None

@@ -42,3 +42,4 @@ def test_device_engines_soak(P, runs, mode):
     # one rank per process: the device engines ran (not a host-steps fallback)
     eng = [l for l in outs[0].splitlines() if l.startswith("ENGINES")][0]
     assert "devsteps" in eng and "twoshot" in eng and "oneshot" in eng, eng
+    assert "'ring_host': 'steps'" in eng, eng
