@@ -303,12 +303,21 @@ void HipPlanExecutor::drainCredits() noexcept {
         }
       }
     } else if (engine_ == kEngineDevSteps && devRuns_ > 0 && !ddBlocks_.empty()) {
-      // final credit of out-channel c on every workgroup: devRuns_ * perRun
+      // the runs the GPU completed (graph replays included: kernels.h runCtr)
+      uint64_t runs = devRuns_;
+      if (runCtr_ != nullptr && hipStreamSynchronize(compute_) == hipSuccess) {
+        uint64_t dev = 0;
+        if (hipMemcpy(&dev, runCtr_, sizeof(dev), hipMemcpyDeviceToHost) == hipSuccess) {
+          runs = std::max(runs, dev);
+        }
+      }
+      (void)hipGetLastError();
+      // final credit of out-channel c on every workgroup: runs * perRun
       std::vector<uint64_t> want(out_.size(), 0);
       for (size_t i = 0; i < plan_.steps.size() && i < sync_.steps.size(); i++) {
         if (plan_.steps[i].kind == glx::SEND) {
           const size_t c = (size_t)sync_.steps[i].chan;
-          if (c < want.size()) want[c] = devRuns_ * sync_.steps[i].perRun;
+          if (c < want.size()) want[c] = runs * sync_.steps[i].perRun;
         }
       }
       const size_t G = (size_t)pk_.G;

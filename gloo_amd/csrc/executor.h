@@ -363,6 +363,7 @@ class HipPlanExecutor : public Algorithm {
   glx::DevStep* devSteps_ = nullptr;
   std::vector<glx::DevStep> hostSteps_;  // host copy (timeout diagnostics)
   glx::DevSegment* devSegs_ = nullptr;
+  uint64_t* runCtr_ = nullptr;  // the plan kernel's run count (kernels.h), in the flag block
   const char** devFoldSrc_ = nullptr;
   uint64_t devRuns_ = 0;
   uint64_t ddEpoch_ = 0;
@@ -371,6 +372,7 @@ class HipPlanExecutor : public Algorithm {
   int* ddClaim_ = nullptr;  // device word: the first timed-out workgroup claims the report
   hipEvent_t ddDone_ = nullptr;
   bool ddLaunched_ = false;
+  hipStream_t ddLastStream_ = nullptr;  // the stream of the last device-engine launch
   int clockKhz_ = 100000;  // s_memrealtime rate
   uint64_t* trace_ = nullptr;  // GLOO_AMD_DEVTRACE=1: two-shot phase stamps (pinned host)
   static bool devTrace();

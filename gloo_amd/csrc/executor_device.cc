@@ -323,7 +323,15 @@ void HipPlanExecutor::setupDevSteps() {
   for (size_t k = 0; k < in_.size(); k++) in_[k].deliveryWord = (uint32_t)k;
   for (size_t k = 0; k < out_.size(); k++) out_[k].creditWord = (uint32_t)(in_.size() + k);
   const size_t rows = std::max<size_t>(1, in_.size() + out_.size());
-  ddAlloc(rows * G * glx::kFlagBytes);
+  // the flag rows, then the run count on lines of its own, uncached like the
+  // flags: the 8 XCDs' L2s are not coherent with each other, and the
+  // workgroup that advances the count and the ones that read it in the next
+  // launch may sit on different XCDs -- in memory no L2 holds, every read
+  // sees the last advance without relying on the cache maintenance at
+  // kernel boundaries
+  char* block = ddAlloc(rows * G * glx::kFlagBytes + 2 * glx::kFlagBytes);
+  runCtr_ = reinterpret_cast<uint64_t*>(block + rows * G * glx::kFlagBytes);
+  pk_.runCtr = runCtr_;
 
   pk_.trace = nullptr;
   if (devTrace()) {
@@ -635,8 +643,12 @@ void HipPlanExecutor::runDevice(char* ptr0) {
   const uint64_t e = ++ddEpoch_;
   const int par = (int)(e & 1);
   const uint64_t ticks = (uint64_t)effectiveTimeout().count() * (uint64_t)clockKhz_;
-  // epochs stay ordered even when calls come on different streams
-  if (ddLaunched_) GLX_HIP_CHECK(hipStreamWaitEvent(compute_, ddDone_, 0));
+  // epochs stay ordered even when calls come on different streams (on the
+  // same stream the order is the stream's -- and a launch being captured
+  // into a graph must not wait on an event recorded outside the capture)
+  if (ddLaunched_ && ddLastStream_ != compute_) {
+    GLX_HIP_CHECK(hipStreamWaitEvent(compute_, ddDone_, 0));
+  }
   if (staged_) waitH2D(compute_, computeH2dWaited_, 0, count_);
   if (engine_ == kEngineOneShot) {
     glx::OneShotParams p = os_;
@@ -711,6 +723,7 @@ void HipPlanExecutor::runDevice(char* ptr0) {
   }
   GLX_HIP_CHECK(hipEventRecord(ddDone_, compute_));
   ddLaunched_ = true;
+  ddLastStream_ = compute_;
   if (staged_) {
     GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, ddDone_, 0));
     copyBack({glx::Range{0, count_}});

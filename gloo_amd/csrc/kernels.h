@@ -160,7 +160,13 @@ struct PlanKernelParams {
   int nsteps, G;
   int slots;                   // landing slots per channel (1 or 2, plan.h SyncTable)
   int maxSrc;                  // most sources of a FOLD step (2 when there is none)
-  uint64_t run;                // runs completed before this one
+  uint64_t run;                // host's count of its launches (diagnostics only)
+  // uncached device memory, per algorithm: [0] runs completed, read by every
+  // workgroup at the start of a launch and advanced by the last workgroup to
+  // finish it ([kFlagStride] counts them) -- so the message numbers follow
+  // the launches the GPU actually ran, and a launch captured in a graph and
+  // replayed numbers its messages like an eager one
+  uint64_t* runCtr;
   uint64_t timeoutTicks;
   int* status;
   int* claim;

@@ -637,9 +637,16 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
   };
   // message m of a channel lands in slot (m - 1) % slots
   auto slotOf = [&](uint64_t m) -> uint64_t { return p.slots == 2 ? ((m - 1) & 1) : 0; };
+  // the runs completed before this launch (kernels.h PlanKernelParams::runCtr)
+  __shared__ uint64_t s_run;
+  if (threadIdx.x == 0) {
+    s_run = __hip_atomic_load(p.runCtr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const uint64_t run = s_run;
   for (int i = 0; i < p.nsteps; i++) {
     const DevStep st = p.steps[i];
-    const uint64_t seq = p.run * st.perRun + st.seq;
+    const uint64_t seq = run * st.perRun + st.seq;
     stamp(2 * i);
     switch (st.kind) {
       case kStepReducePre:          // REDUCE, the overlap also into the next SEND's slot
@@ -654,7 +661,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
         stamp(2 * i + 1);
         char* dst = st.dst + slotOf(seq) * (uint64_t)st.dstSlot;
         const S* src = reinterpret_cast<const S*>(
-            st.src + slotOf(p.run * st.rperRun + st.rseq) * (uint64_t)st.srcSlot);
+            st.src + slotOf(run * st.rperRun + st.rseq) * (uint64_t)st.srcSlot);
         char* outs[2] = {reinterpret_cast<char*>(buf), dst};
         const S* srcs[2] = {buf, src};
         for (int g = st.seg0; g < st.seg1; g++) {
@@ -700,7 +707,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
           }
         } else {
           const S* src = reinterpret_cast<const S*>(
-              st.src + slotOf(p.run * st.rperRun + st.rseq) * (uint64_t)st.srcSlot);
+              st.src + slotOf(run * st.rperRun + st.rseq) * (uint64_t)st.srcSlot);
           char* outs[2] = {reinterpret_cast<char*>(buf), dst};
           const S* srcs[2] = {buf, src};
           for (int g = st.seg0; g < st.seg1; g++) {
@@ -741,7 +748,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
           }
         } else {
           srcs[1] = reinterpret_cast<const S*>(
-              st.src + slotOf(p.run * st.rperRun + st.rseq) * (uint64_t)st.srcSlot);
+              st.src + slotOf(run * st.rperRun + st.rseq) * (uint64_t)st.srcSlot);
         }
         for (int g = st.seg0; g < st.seg1; g++) {
           size_t a, b;
@@ -765,6 +772,18 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
     }
   }
   stamp(2 * p.nsteps);
+  // the last workgroup to finish advances the run count for the next launch
+  // (every workgroup read it at its start, before it could finish)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t* doneCtr = p.runCtr + kFlagStride;  // a line of its own
+    const uint64_t done =
+        __hip_atomic_fetch_add(doneCtr, (uint64_t)1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (done == (uint64_t)p.G - 1) {
+      __hip_atomic_store(doneCtr, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(p.runCtr, (uint64_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 template <typename T, int OP, int MAXSRC>
@@ -903,6 +922,7 @@ hipError_t launch_oneshot(int op, int dtype, const OneShotParams& p, hipStream_t
 hipError_t launch_plan_kernel(int op, int dtype, const PlanKernelParams& p, hipStream_t s) {
   if (p.G < 1 || p.G > kOsMaxSlices || p.nsteps < 0 || p.steps == nullptr ||
       p.segs == nullptr || p.foldSrc == nullptr || p.status == nullptr || p.claim == nullptr ||
+      p.runCtr == nullptr ||
       (p.slots != 1 && p.slots != 2) || p.maxSrc < 2 || p.maxSrc > kOsMaxRanks) {
     return hipErrorInvalidValue;
   }

@@ -64,9 +64,12 @@ def main():
         return run_scale(store_dir, rank, size, algo[len("scale:"):])
     if algo.startswith("fuzz:"):
         return run_fuzz(store_dir, rank, size, int(algo[len("fuzz:"):]))
+    if algo.startswith("graph:"):
+        return run_graph(store_dir, rank, size, int(algo[len("graph:"):]))
     if algo.startswith("soak:"):
         parts = algo.split(":")
-        return run_soak(store_dir, rank, size, int(parts[1]), uneven=parts[2:] == ["uneven"])
+        return run_soak(store_dir, rank, size, int(parts[1]),
+                        uneven=parts[2] if len(parts) > 2 else "")
     if algo.startswith("big:"):
         return run_big(store_dir, rank, size, algo[len("big:"):])
     if algo == "linkprobe":
@@ -679,7 +682,81 @@ def run_engine_choice(store_dir, rank, size):
     print("OK")
 
 
-def run_soak(store_dir, rank, size, runs, uneven=False):
+def run_graph(store_dir, rank, size, replays):
+    """HIP graph capture of the plan kernel's run(): each algorithm (ring
+    and halving-doubling on a caller's stream) runs once eagerly, is captured
+    into a graph with torch.cuda.graph, and then the graph is replayed with
+    fresh inputs, mixed with eager runs -- the kernel numbers its messages
+    from the device-side run count (kernels.h PlanKernelParams::runCtr), so
+    replays and eager runs interleave in one sequence on every rank.  Exact
+    sums of integer-valued inputs as in the soak."""
+    import torch
+
+    import gloo_amd
+
+    store = gloo_amd.rendezvous.FileStore(store_dir)
+    ctx = gloo_amd.rendezvous.Context(rank, size, 0)
+    ctx.setTimeout(30)
+    ctx.connectFullMesh(store)
+    n = 1 << 20
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream()
+
+    def inputs(r, it):
+        g = torch.Generator(device=dev)
+        g.manual_seed(7919 * it + r)
+        return torch.randint(-64, 64, (n,), generator=g, device=dev, dtype=torch.int32)
+
+    bad, engines = [], {}
+    for kind in ("ring", "hd"):
+        buf = torch.empty(n, dtype=torch.float32, device=dev)
+        alg = (gloo_amd.AllreduceRingChunked(ctx, [buf], streams=[s], schedule="ring")
+               if kind == "ring" else gloo_amd.AllreduceHalvingDoubling(ctx, [buf], streams=[s]))
+        engines[kind] = alg.engine()
+
+        def check(it):
+            s.synchronize()
+            expect = sum(inputs(r, it).to(torch.int64) for r in range(size))
+            got = buf.to(torch.int64)
+            if not torch.equal(got, expect):
+                bad.append((kind, it, int((got != expect).sum())))
+
+        with torch.cuda.stream(s):
+            buf.copy_(inputs(rank, 0).to(torch.float32))
+        alg.run()  # eager: resolves the peers, builds the step table
+        check(0)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            buf.copy_(inputs(rank, 1).to(torch.float32))
+        s.synchronize()
+        with torch.cuda.graph(graph, stream=s):
+            alg.run()
+        # capturing launched nothing: the graph's first replay is run 1
+        with torch.cuda.stream(s):
+            graph.replay()
+        check(1)
+        for it in range(2, replays + 2):
+            with torch.cuda.stream(s):
+                buf.copy_(inputs(rank, it).to(torch.float32))
+                if it % 4 == 0:
+                    alg.run()       # eager runs between replays share the count
+                else:
+                    graph.replay()
+            check(it)
+        s.synchronize()
+        del graph
+        alg.close()
+    store.set("graph/done/%d" % rank, b"1")
+    for r in range(size):
+        store.get("graph/done/%d" % r, timeout_ms=60000)
+    print("ENGINES rank %d %s" % (rank, engines))
+    if bad:
+        print("MISMATCH rank %d %s" % (rank, bad[:10]))
+        sys.exit(1)
+    print("OK")
+
+
+def run_soak(store_dir, rank, size, runs, uneven=""):
     """One instance of each device engine's algorithm run `runs` times back to
     back (a training job's shape: the run counter, the message numbers
     j * perRun + seq and the landing slots alternate across many kernel
@@ -690,10 +767,14 @@ def run_soak(store_dir, rank, size, runs, uneven=False):
     as a wrong element.
 
     uneven: the guide's hand-off test condition (MI355X_MICROARCH.md, "Test
-    every hand-off under UNEVEN load"): every rank starts each run after a
-    random delay of up to 2 ms, and rank 0 keeps a GEMM stream busy on its
-    GPU beside the collective, so workgroups arrive at their flags at
-    different times and some CUs are taken."""
+    every hand-off under UNEVEN load"): "delays" -- every rank starts each
+    run after a random delay of up to 2 ms, so workgroups arrive at their
+    flags at different times; "uneven" -- also a GEMM stream busy on rank 0's
+    GPU beside the collective, so some CUs are taken.  The GEMM variant needs
+    two hardware queues per process: with one (8 ranks sharing the GPU) the
+    GEMM sits ahead of the collective in rank 0's only queue while the other
+    ranks' collectives hold the CUs waiting for rank 0 -- a cycle that exists
+    only when ranks share a GPU."""
     import random
     import time
 
@@ -733,7 +814,7 @@ def run_soak(store_dir, rank, size, runs, uneven=False):
         gloo_amd.set_steps_engine("auto")
     engines = {k: a.engine() for k, a in algs.items()}
     rng = random.Random(rank)
-    side = torch.cuda.Stream() if uneven and rank == 0 else None
+    side = torch.cuda.Stream() if uneven == "uneven" and rank == 0 else None
     if side is not None:
         x = torch.randn(2048, 2048, device=dev)
     bad = []

@@ -18,11 +18,15 @@ WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "mp_worker.py"
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("P,runs,mode", [(2, 1000, ""), (4, 600, ""), (8, 300, ""),
-                                         (4, 150, ":uneven"), (8, 100, ":uneven")])
+                                         (4, 300, ":uneven"), (8, 300, ":delays")])
 def test_device_engines_soak(P, runs, mode):
-    """mode ":uneven": random start delays per rank and run, and a GEMM
-    stream busy on rank 0's GPU beside the collective (the guide's
-    condition for testing hand-offs)."""
+    """The guide's condition for testing hand-offs, uneven load: ":delays",
+    random start delays per rank and run; ":uneven", also a GEMM stream busy
+    on rank 0's GPU beside the collective -- only where each process has two
+    hardware queues (with one, 8 ranks sharing the GPU, the GEMM ahead of
+    the collective in rank 0's only queue and the other ranks' collectives
+    holding the CUs wait on each other: a cycle only ranks sharing a GPU can
+    form; profiles/r9j_*, r9l_*)."""
     with tempfile.TemporaryDirectory() as d:
         procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P),
                                    "soak:%d%s" % (runs, mode)],
@@ -37,8 +41,10 @@ def test_device_engines_soak(P, runs, mode):
                     q.kill()
                 raise
             outs.append(o.decode(errors="replace"))
-    for r, (p, o) in enumerate(zip(procs, outs)):
-        assert p.returncode == 0 and "OK" in o, "rank %d rc=%d:\n%s" % (r, p.returncode, o[-3000:])
+    failed = [(r, p.returncode, o) for r, (p, o) in enumerate(zip(procs, outs))
+              if p.returncode != 0 or "OK" not in o]
+    # every failing rank's output: the first to fail is often not rank 0
+    assert not failed, "\n".join("rank %d rc=%d:\n%s" % (r, rc, o[-2500:]) for r, rc, o in failed)
     # one rank per process: the device engines ran (not a host-steps fallback)
     eng = [l for l in outs[0].splitlines() if l.startswith("ENGINES")][0]
     assert "devsteps" in eng and "twoshot" in eng and "oneshot" in eng, eng
