@@ -266,8 +266,11 @@ void HipPlanExecutor::setupOneShot() {
   ddSlot_ = ((size_t)count_ * esize_ + 255) & ~(size_t)255;
   ddAlloc((size_t)P * ddSlot_);
   ddAlloc((size_t)P * ddSlot_);
-  p.flagIn = reinterpret_cast<const uint64_t*>(
-      ddAlloc((size_t)P * (size_t)p.G * glx::kFlagBytes));
+  // the flag rows, then the launch count on lines of its own (kernels.h)
+  const size_t rows = (size_t)P * (size_t)p.G * glx::kFlagBytes;
+  char* flags = ddAlloc(rows + 2 * glx::kFlagBytes);
+  p.flagIn = reinterpret_cast<const uint64_t*>(flags);
+  p.epochCtr = reinterpret_cast<uint64_t*>(flags + rows);
 }
 
 void HipPlanExecutor::setupTwoShot() {
@@ -294,9 +297,12 @@ void HipPlanExecutor::setupTwoShot() {
   }
   ddSlot_ = ((size_t)d.maxLen * esize_ + 16 + 255) & ~(size_t)255;
   for (int k = 0; k < 4; k++) ddAlloc((size_t)P * ddSlot_);  // RS 0/1, AG 0/1
-  char* flags = ddAlloc(2 * (size_t)P * (size_t)p.G * glx::kFlagBytes);
+  // the A and B flag rows, then the launch count on lines of its own
+  const size_t rows = 2 * (size_t)P * (size_t)p.G * glx::kFlagBytes;
+  char* flags = ddAlloc(rows + 2 * glx::kFlagBytes);
   p.flagAIn = reinterpret_cast<const uint64_t*>(flags);
   p.flagBIn = reinterpret_cast<const uint64_t*>(flags) + (size_t)P * (size_t)p.G * glx::kFlagStride;
+  p.epochCtr = reinterpret_cast<uint64_t*>(flags + rows);
 }
 
 // The plan kernel: segments from every rank's program (plan.cc syncTable),
@@ -640,8 +646,7 @@ void HipPlanExecutor::runDevice(char* ptr0) {
   if (!resolved_) resolvePeers();
   checkDevice();  // an earlier asynchronous call that timed out
   const int P = contextSize_;
-  const uint64_t e = ++ddEpoch_;
-  const int par = (int)(e & 1);
+  const uint64_t e = ++ddEpoch_;  // the host's count (diagnostics); the kernels count on the GPU
   const uint64_t ticks = (uint64_t)effectiveTimeout().count() * (uint64_t)clockKhz_;
   // epochs stay ordered even when calls come on different streams (on the
   // same stream the order is the stream's -- and a launch being captured
@@ -657,14 +662,18 @@ void HipPlanExecutor::runDevice(char* ptr0) {
     p.timeoutTicks = ticks;
     for (int j = 0; j < P; j++) {
       if (j == contextRank_) {
-        p.push[j] = nullptr;
-        p.land[j] = ptr0;
+        for (int par = 0; par < 2; par++) {
+          p.push[par][j] = nullptr;
+          p.land[par][j] = ptr0;
+        }
         p.flagOut[j] = nullptr;
         continue;
       }
       const auto& pb = ddPeer_.at(j);
-      p.push[j] = pb[(size_t)par] + (size_t)contextRank_ * ddSlot_;
-      p.land[j] = ddBlocks_[(size_t)par] + (size_t)j * ddSlot_;
+      for (int par = 0; par < 2; par++) {  // the kernel picks by its epoch's parity
+        p.push[par][j] = pb[(size_t)par] + (size_t)contextRank_ * ddSlot_;
+        p.land[par][j] = ddBlocks_[(size_t)par] + (size_t)j * ddSlot_;
+      }
       p.flagOut[j] = reinterpret_cast<uint64_t*>(pb[2]) +
                      (size_t)contextRank_ * (size_t)p.G * glx::kFlagStride;
     }
@@ -700,17 +709,22 @@ void HipPlanExecutor::runDevice(char* ptr0) {
     };
     for (int j = 0; j < P; j++) {
       if (j == contextRank_) {
-        p.rsPush[j] = p.agPush[j] = nullptr;
-        p.rsLand[j] = p.agLand[j] = nullptr;
+        for (int par = 0; par < 2; par++) {
+          p.rsPush[par][j] = p.agPush[par][j] = nullptr;
+          p.rsLand[par][j] = p.agLand[par][j] = nullptr;
+        }
         p.flagAOut[j] = p.flagBOut[j] = nullptr;
         continue;
       }
       const auto& pb = ddPeer_.at(j);
       const size_t mine = (size_t)contextRank_ * ddSlot_, theirs = (size_t)j * ddSlot_;
-      p.rsPush[j] = vbase(pb[(size_t)par] + mine, j);             // my copy of range j
-      p.rsLand[j] = vbase(ddBlocks_[(size_t)par] + theirs, contextRank_);  // j's copy of mine
-      p.agPush[j] = vbase(pb[2 + (size_t)par] + mine, contextRank_);       // my result
-      p.agLand[j] = vbase(ddBlocks_[2 + (size_t)par] + theirs, j);         // j's result
+      for (int par = 0; par < 2; par++) {  // the kernel picks by its epoch's parity
+        const size_t q = (size_t)par;
+        p.rsPush[par][j] = vbase(pb[q] + mine, j);                      // my copy of range j
+        p.rsLand[par][j] = vbase(ddBlocks_[q] + theirs, contextRank_);  // j's copy of mine
+        p.agPush[par][j] = vbase(pb[2 + q] + mine, contextRank_);       // my result
+        p.agLand[par][j] = vbase(ddBlocks_[2 + q] + theirs, j);         // j's result
+      }
       uint64_t* pf = reinterpret_cast<uint64_t*>(pb[4]);
       p.flagAOut[j] = pf + (size_t)contextRank_ * G * glx::kFlagStride;
       p.flagBOut[j] = pf + ((size_t)P * G + (size_t)contextRank_ * G) * glx::kFlagStride;

@@ -62,15 +62,21 @@ constexpr int kFlagStride = 16;
 constexpr size_t kFlagBytes = kFlagStride * sizeof(uint64_t);
 struct OneShotParams {
   char* buf;                        // this rank's buffer: input and result
-  char* push[kOsMaxRanks];          // this rank's landing region in peer j (j != rank)
-  const char* land[kOsMaxRanks];    // rank k's landing region here (k != rank)
+  // by the epoch's parity (the two slot sets alternate between launches):
+  char* push[2][kOsMaxRanks];       // this rank's landing region in peer j (j != rank)
+  const char* land[2][kOsMaxRanks];  // rank k's landing region here (k != rank)
   uint64_t* flagOut[kOsMaxRanks];   // peer j's flag row for this rank ([G] flags)
   const uint64_t* flagIn;           // this rank's flags: [P][G] flags
   int* status;                      // host-visible: 1 + rank that never arrived
   int* claim;                       // device word: the first timed-out workgroup reports
   int flagStore;                    // 1: write peers' flags with stores (Context::flagStores)
   int narrow;                       // 1: narrow release / acquire around flags (below)
-  uint64_t epoch;                   // >= 1, +1 per call, equal on all ranks
+  uint64_t epoch;                   // host's count of its launches (diagnostics only)
+  // uncached device memory: [0] launches completed; the launch's epoch is
+  // that + 1 (>= 1, +1 per launch, equal on all ranks), advanced by the last
+  // workgroup to finish ([kFlagStride] counts them) -- graph-capturable, as
+  // PlanKernelParams::runCtr
+  uint64_t* epochCtr;
   uint64_t timeoutTicks;            // s_memrealtime ticks
   size_t count;                     // elements
   size_t slice;                     // elements per workgroup, multiple of 16 / esize
@@ -87,10 +93,11 @@ hipError_t launch_oneshot(int op, int dtype, const OneShotParams& p, hipStream_t
 // buffers": element i of range c at ptr + i * esize.
 struct TwoShotParams {
   char* buf;
-  char* rsPush[kOsMaxRanks];        // owner j's RS slot for this rank's copy of range j
-  const char* rsLand[kOsMaxRanks];  // this rank's RS slot holding rank k's copy of range rank
-  char* agPush[kOsMaxRanks];        // peer j's AG slot for this rank's finished range
-  const char* agLand[kOsMaxRanks];  // this rank's AG slot holding owner j's finished range
+  // by the epoch's parity (the two slot sets alternate between launches):
+  char* rsPush[2][kOsMaxRanks];        // owner j's RS slot for this rank's copy of range j
+  const char* rsLand[2][kOsMaxRanks];  // this rank's RS slot holding rank k's copy of range rank
+  char* agPush[2][kOsMaxRanks];        // peer j's AG slot for this rank's finished range
+  const char* agLand[2][kOsMaxRanks];  // this rank's AG slot holding owner j's finished range
   uint64_t* flagAOut[kOsMaxRanks];  // owner j's A-flag row for this rank ([G] flags)
   const uint64_t* flagAIn;          // [P][G]: rank k's copy of my range slice landed
   uint64_t* flagBOut[kOsMaxRanks];  // peer j's B-flag row for this rank as owner
@@ -99,7 +106,8 @@ struct TwoShotParams {
   int* claim;
   int flagStore;
   int narrow;                       // 1: narrow release / acquire around flags (below)
-  uint64_t epoch, timeoutTicks;
+  uint64_t epoch, timeoutTicks;     // epoch: the host's count (diagnostics only)
+  uint64_t* epochCtr;               // as OneShotParams::epochCtr
   size_t rangeOff[kOsMaxRanks], rangeLen[kOsMaxRanks];  // by owner
   uint8_t chain[kOsMaxRanks];       // this rank's fold order
   size_t slice;                     // elements per workgroup per range, multiple of 16 / esize

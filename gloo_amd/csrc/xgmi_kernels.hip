@@ -458,6 +458,36 @@ __device__ __forceinline__ bool wait_flag(const uint64_t* word, uint64_t epoch, 
   return *s_ok != 0;
 }
 
+// ---- launch counts kept on the device ------------------------------------------
+
+// The launches of this algorithm completed before this one (an uncached
+// counter: the workgroup advancing it and those reading it next may sit on
+// different XCDs, whose L2s are not coherent).  Every workgroup reads it at
+// its start; finish_launch advances it once the last one is done -- so the
+// numbers a launch uses come from the GPU, and a captured launch replays
+// correctly.
+__device__ __forceinline__ uint64_t launches_done(const uint64_t* ctr) {
+  __shared__ uint64_t s_n;
+  if (threadIdx.x == 0) {
+    s_n = __hip_atomic_load(const_cast<uint64_t*>(ctr), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return s_n;
+}
+
+__device__ __forceinline__ void finish_launch(uint64_t* ctr, int G) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t* done = ctr + kFlagStride;  // a line of its own
+    const uint64_t n =
+        __hip_atomic_fetch_add(done, (uint64_t)1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (n == (uint64_t)G - 1) {
+      __hip_atomic_store(done, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(ctr, (uint64_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // ---- one-shot ---------------------------------------------------------------
 
 template <typename T, int OP, bool FAST>
@@ -469,6 +499,8 @@ __device__ __forceinline__ void oneshot_body(const OneShotParams& p) {
   const size_t e1 = e0 + p.slice < p.count ? e0 + p.slice : p.count;
   S* buf = reinterpret_cast<S*>(p.buf);
   const bool aligned = ((uintptr_t)p.buf % 16) == 0;
+  const uint64_t epoch = launches_done(p.epochCtr) + 1;
+  const int par = (int)(epoch & 1);
 
   // 1. push (peers in ring order from rank+1)
   char* to[kOsMaxRanks - 1];
@@ -476,17 +508,17 @@ __device__ __forceinline__ void oneshot_body(const OneShotParams& p) {
   for (int d = 1; d < kOsMaxRanks; d++) {
     int j = p.rank + d;
     if (j >= p.P) j -= p.P;
-    to[d - 1] = d < p.P ? p.push[j] : nullptr;
+    to[d - 1] = d < p.P ? p.push[par][j] : nullptr;
   }
   scatter_span<S, FAST, kStPlain, 0>(to, p.P - 1, buf, e0, e1, aligned);
-  release_flags(p.flagOut, p.P, p.rank, w, p.epoch, p.flagStore != 0, [](int) { return true; },
+  release_flags(p.flagOut, p.P, p.rank, w, epoch, p.flagStore != 0, [](int) { return true; },
                 p.narrow != 0);
 
   // 2. wait
   const uint64_t start = __builtin_amdgcn_s_memrealtime();
   for (int k = 0; k < p.P; k++) {
     if (k == p.rank) continue;
-    if (!wait_flag(flag_at(p.flagIn, k * p.G + w), p.epoch, k, start, p.timeoutTicks,
+    if (!wait_flag(flag_at(p.flagIn, k * p.G + w), epoch, k, start, p.timeoutTicks,
                    p.status, p.claim, &s_ok, p.narrow != 0)) {
       return;
     }
@@ -501,10 +533,12 @@ __device__ __forceinline__ void oneshot_body(const OneShotParams& p) {
 #pragma unroll
     for (int i = 0; i < kOsMaxRanks; i++) {
       const int r = p.chain[q][i];
-      src[i] = i < p.P ? (r == p.rank ? buf : reinterpret_cast<const S*>(p.land[r])) : nullptr;
+      src[i] = i < p.P ? (r == p.rank ? buf : reinterpret_cast<const S*>(p.land[par][r]))
+                       : nullptr;
     }
     fold_span<T, OP, FAST>(buf, src, p.P, nullptr, 0, a, b, aligned);
   }
+  finish_launch(p.epochCtr, p.G);
 }
 
 // >= 2 waves per SIMD: every rank's grid (<= kOsMaxSlices workgroups) stays
@@ -529,6 +563,8 @@ __device__ __forceinline__ void twoshot_body(const TwoShotParams& p) {
   stamp(0);
   S* buf = reinterpret_cast<S*>(p.buf);
   const bool aligned = ((uintptr_t)p.buf % 16) == 0;
+  const uint64_t epoch = launches_done(p.epochCtr) + 1;
+  const int par = (int)(epoch & 1);
   auto span = [&](int c, size_t& a, size_t& b) {  // slice w of range c
     const size_t off = p.rangeOff[c], len = p.rangeLen[c];
     const size_t s0 = (size_t)w * p.slice;
@@ -545,10 +581,10 @@ __device__ __forceinline__ void twoshot_body(const TwoShotParams& p) {
     if (j >= p.P) j -= p.P;
     size_t a, b;
     if (span(j, a, b)) {
-      copy_span<S, FAST, kStRemote>(reinterpret_cast<S*>(p.rsPush[j]), buf, a, b, aligned);
+      copy_span<S, FAST, kStRemote>(reinterpret_cast<S*>(p.rsPush[par][j]), buf, a, b, aligned);
     }
   }
-  release_flags(p.flagAOut, p.P, p.rank, w, p.epoch, p.flagStore != 0, [&](int j) {
+  release_flags(p.flagAOut, p.P, p.rank, w, epoch, p.flagStore != 0, [&](int j) {
     size_t a, b;
     return span(j, a, b);
   }, p.narrow != 0);
@@ -561,7 +597,7 @@ __device__ __forceinline__ void twoshot_body(const TwoShotParams& p) {
   if (span(p.rank, a, b)) {
     for (int k = 0; k < p.P; k++) {
       if (k == p.rank) continue;
-      if (!wait_flag(flag_at(p.flagAIn, k * p.G + w), p.epoch, k, start, p.timeoutTicks,
+      if (!wait_flag(flag_at(p.flagAIn, k * p.G + w), epoch, k, start, p.timeoutTicks,
                      p.status, p.claim, &s_ok, p.narrow != 0)) {
         return;
       }
@@ -571,17 +607,18 @@ __device__ __forceinline__ void twoshot_body(const TwoShotParams& p) {
 #pragma unroll
     for (int i = 0; i < kOsMaxRanks; i++) {
       const int r = p.chain[i];
-      src[i] = i < p.P ? (r == p.rank ? buf : reinterpret_cast<const S*>(p.rsLand[r])) : nullptr;
+      src[i] = i < p.P ? (r == p.rank ? buf : reinterpret_cast<const S*>(p.rsLand[par][r]))
+                       : nullptr;
     }
     char* outs[kOsMaxRanks - 1];
 #pragma unroll
     for (int d = 1; d < kOsMaxRanks; d++) {
       int j = p.rank + d;
       if (j >= p.P) j -= p.P;
-      outs[d - 1] = d < p.P ? p.agPush[j] : nullptr;
+      outs[d - 1] = d < p.P ? p.agPush[par][j] : nullptr;
     }
     fold_span<T, OP, FAST>(buf, src, p.P, outs, p.P - 1, a, b, aligned);
-    release_flags(p.flagBOut, p.P, p.rank, w, p.epoch, p.flagStore != 0,
+    release_flags(p.flagBOut, p.P, p.rank, w, epoch, p.flagStore != 0,
                   [](int) { return true; }, p.narrow != 0);
   }
   stamp(3);
@@ -591,14 +628,16 @@ __device__ __forceinline__ void twoshot_body(const TwoShotParams& p) {
     int j = p.rank - d;
     if (j < 0) j += p.P;
     if (!span(j, a, b)) continue;
-    if (!wait_flag(flag_at(p.flagBIn, j * p.G + w), p.epoch, j, start, p.timeoutTicks,
+    if (!wait_flag(flag_at(p.flagBIn, j * p.G + w), epoch, j, start, p.timeoutTicks,
                    p.status, p.claim, &s_ok, p.narrow != 0)) {
       return;
     }
     if (d == 1) stamp(4);
-    copy_span<S, FAST, kStPlain>(buf, reinterpret_cast<const S*>(p.agLand[j]), a, b, aligned);
+    copy_span<S, FAST, kStPlain>(buf, reinterpret_cast<const S*>(p.agLand[par][j]), a, b,
+                                 aligned);
   }
   stamp(5);
+  finish_launch(p.epochCtr, p.G);
 }
 
 template <typename T, int OP>
@@ -638,12 +677,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
   // message m of a channel lands in slot (m - 1) % slots
   auto slotOf = [&](uint64_t m) -> uint64_t { return p.slots == 2 ? ((m - 1) & 1) : 0; };
   // the runs completed before this launch (kernels.h PlanKernelParams::runCtr)
-  __shared__ uint64_t s_run;
-  if (threadIdx.x == 0) {
-    s_run = __hip_atomic_load(p.runCtr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  const uint64_t run = s_run;
+  const uint64_t run = launches_done(p.runCtr);
   for (int i = 0; i < p.nsteps; i++) {
     const DevStep st = p.steps[i];
     const uint64_t seq = run * st.perRun + st.seq;
@@ -774,16 +808,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
   stamp(2 * p.nsteps);
   // the last workgroup to finish advances the run count for the next launch
   // (every workgroup read it at its start, before it could finish)
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint64_t* doneCtr = p.runCtr + kFlagStride;  // a line of its own
-    const uint64_t done =
-        __hip_atomic_fetch_add(doneCtr, (uint64_t)1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (done == (uint64_t)p.G - 1) {
-      __hip_atomic_store(doneCtr, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(p.runCtr, (uint64_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  finish_launch(p.runCtr, p.G);
 }
 
 template <typename T, int OP, int MAXSRC>
@@ -899,7 +924,9 @@ int device_engine_resident_blocks(int kernel, int op, int dtype) {
 }
 
 hipError_t launch_oneshot(int op, int dtype, const OneShotParams& p, hipStream_t s) {
-  if (p.status == nullptr || p.claim == nullptr) return hipErrorInvalidValue;
+  if (p.status == nullptr || p.claim == nullptr || p.epochCtr == nullptr) {
+    return hipErrorInvalidValue;
+  }
   if (p.P < 2 || p.P > kOsMaxRanks || p.G < 1 || p.G > kOsMaxSlices || p.njobs < 0 ||
       p.njobs > kOsMaxRanks || p.count == 0 || p.slice == 0 ||
       (size_t)p.G * p.slice < p.count || (size_t)(p.G - 1) * p.slice >= p.count) {
@@ -946,7 +973,8 @@ hipError_t launch_twoshot(int op, int dtype, const TwoShotParams& p, hipStream_t
     maxLen = p.rangeLen[c] > maxLen ? p.rangeLen[c] : maxLen;
   }
   if (p.P < 2 || p.P > kOsMaxRanks || p.G < 1 || p.G > kOsMaxSlices || p.slice == 0 ||
-      (size_t)p.G * p.slice < maxLen || p.status == nullptr || p.claim == nullptr) {
+      (size_t)p.G * p.slice < maxLen || p.status == nullptr || p.claim == nullptr ||
+      p.epochCtr == nullptr) {
     return hipErrorInvalidValue;  // the slices must cover every range
   }
   switch (dtype) {

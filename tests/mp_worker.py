@@ -683,13 +683,14 @@ def run_engine_choice(store_dir, rank, size):
 
 
 def run_graph(store_dir, rank, size, replays):
-    """HIP graph capture of the plan kernel's run(): each algorithm (ring
-    and halving-doubling on a caller's stream) runs once eagerly, is captured
-    into a graph with torch.cuda.graph, and then the graph is replayed with
-    fresh inputs, mixed with eager runs -- the kernel numbers its messages
-    from the device-side run count (kernels.h PlanKernelParams::runCtr), so
-    replays and eager runs interleave in one sequence on every rank.  Exact
-    sums of integer-valued inputs as in the soak."""
+    """HIP graph capture of run() on every device engine: each algorithm (ring
+    and halving-doubling on the plan kernel, the mesh on the two-shot kernel,
+    the replicated schedule on the one-shot kernel, on a caller's stream)
+    runs once eagerly, is captured into a graph with torch.cuda.graph, and
+    then the graph is replayed with fresh inputs, mixed with eager runs --
+    the kernels take their run count / epoch from the device (kernels.h
+    runCtr, epochCtr), so replays and eager runs interleave in one sequence
+    on every rank.  Exact sums of integer-valued inputs as in the soak."""
     import torch
 
     import gloo_amd
@@ -708,10 +709,13 @@ def run_graph(store_dir, rank, size, replays):
         return torch.randint(-64, 64, (n,), generator=g, device=dev, dtype=torch.int32)
 
     bad, engines = [], {}
-    for kind in ("ring", "hd"):
+    for kind in ("ring", "hd", "mesh", "repl"):
         buf = torch.empty(n, dtype=torch.float32, device=dev)
-        alg = (gloo_amd.AllreduceRingChunked(ctx, [buf], streams=[s], schedule="ring")
-               if kind == "ring" else gloo_amd.AllreduceHalvingDoubling(ctx, [buf], streams=[s]))
+        if kind == "hd":
+            alg = gloo_amd.AllreduceHalvingDoubling(ctx, [buf], streams=[s])
+        else:
+            sched = {"ring": "ring", "mesh": "mesh", "repl": "replicated"}[kind]
+            alg = gloo_amd.AllreduceRingChunked(ctx, [buf], streams=[s], schedule=sched)
         engines[kind] = alg.engine()
 
         def check(it):

@@ -1,11 +1,11 @@
-"""HIP graph capture of the plan-kernel allreduce (tests/mp_worker.py graph):
-one process per rank, each captures its algorithm's run() on its stream with
-torch.cuda.graph and replays it with fresh inputs, mixed with eager runs;
-every result exact.  The kernel numbers its messages from a device-side run
-count (kernels.h PlanKernelParams::runCtr), so a replay needs no host-side
-bookkeeping -- an MI355X-native way to put the allreduce inside a captured
-training step.  (The one- and two-shot kernels still take a host-side epoch
-and are not capturable)"""
+"""HIP graph capture of the device-engine allreduce (tests/mp_worker.py
+graph): one process per rank, each captures its algorithm's run() on its
+stream with torch.cuda.graph and replays it with fresh inputs, mixed with
+eager runs; every result exact, on every device engine (plan kernel: ring,
+halving-doubling; two-shot: mesh; one-shot: replicated).  The kernels take
+their run count / epoch from the device (kernels.h runCtr, epochCtr), so a
+replay needs no host-side bookkeeping -- an MI355X-native way to put the
+allreduce inside a captured training step."""
 import os
 import subprocess
 import sys
@@ -20,7 +20,7 @@ WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "mp_worker.py"
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("P", [2, 4])
-def test_plan_kernel_graph_replays(P):
+def test_device_engine_graph_replays(P):
     with tempfile.TemporaryDirectory() as d:
         procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), "graph:40"],
                                   env=rank_env(P), stdout=subprocess.PIPE,
@@ -40,3 +40,4 @@ def test_plan_kernel_graph_replays(P):
     assert not failed, "\n".join("rank %d rc=%d:\n%s" % (r, rc, o[-2500:]) for r, rc, o in failed)
     eng = [l for l in outs[0].splitlines() if l.startswith("ENGINES")][0]
     assert "'ring': 'devsteps'" in eng and "'hd': 'devsteps'" in eng, eng
+    assert "'mesh': 'twoshot'" in eng and "'repl': 'oneshot'" in eng, eng
