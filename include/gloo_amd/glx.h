@@ -351,7 +351,12 @@ int glx_allreduce(glx_context* ctx, int algorithm, int dtype, int op,
                   int num_outputs, size_t elements, uint32_t tag,
                   size_t max_segment_size, int64_t timeout_ms, glx_stream_t stream);
 
-/* Algorithm::run() (gloo/algorithm.h:26). */
+/* Algorithm::run() (gloo/algorithm.h:26).  With streams and a device engine
+ * (glx_algorithm_engine != GLX_ENGINE_STEPS) the call only enqueues one
+ * kernel on streams[0] and can be captured into a HIP graph
+ * (hipStreamBeginCapture on streams[0]) after one eager run: the kernels
+ * keep their run count / epoch on the device, so every replay is one more
+ * run on that rank, in sequence with eager runs. */
 int glx_algorithm_run(glx_algorithm* alg);
 
 /* Host-memory endpoint fed from a transport.  The reference receives socket
