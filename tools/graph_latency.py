@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Small-message allreduce latency, eager vs HIP graph: one
+process per rank (torchrun or tools/mp_launch.py), each with its device
+engine on a caller's stream.  Eager: `iters` run() calls back to back on the
+stream, one synchronize at the end.  Graph: `per_graph` run() calls captured
+into one torch.cuda.CUDAGraph, replayed iters / per_graph times.  Reports
+microseconds per allreduce (max over ranks), per size and schedule, as one
+JSON line on rank 0.
+
+    python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \\
+        tools/graph_latency.py [--sizes 256,4096,65536] [--iters 400]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sizes", default="256,4096,65536,1048576")
+    ap.add_argument("--iters", type=int, default=400)
+    ap.add_argument("--per-graph", type=int, default=20)
+    a = ap.parse_args()
+    import torch
+    import torch.distributed as dist
+
+    import gloo_amd
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo")
+    ctx = gloo_amd.rendezvous.Context(rank, world, dev)
+    ctx.connectFullMesh(gloo_amd.rendezvous.TorchStore(dist.distributed_c10d._get_default_store()))
+    s = torch.cuda.Stream()
+    out = {}
+
+    def timed(fn, n):
+        s.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        fn(n)
+        s.synchronize()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return el.item()
+
+    for n in [int(x) for x in a.sizes.split(",")]:
+        for sched in ("replicated", "ring"):
+            buf = torch.zeros(n, dtype=torch.float32, device="cuda")
+            alg = gloo_amd.AllreduceRingChunked(ctx, [buf], streams=[s], schedule=sched)
+            engine = alg.engine()
+            if engine == "steps":  # host-issued steps wait on the host: not capturable
+                alg.close()
+                continue
+            for _ in range(5):
+                alg.run()
+
+            def eager(k):
+                for _ in range(k):
+                    alg.run()
+            eager_s = timed(eager, a.iters)
+            g = torch.cuda.CUDAGraph()
+            s.synchronize()
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(a.per_graph):
+                    alg.run()
+
+            def replay(k):
+                with torch.cuda.stream(s):
+                    for _ in range(k // a.per_graph):
+                        g.replay()
+            graph_s = timed(replay, a.iters)
+            s.synchronize()
+            ok = bool((buf == 0).all().item())  # zeros stay zeros, run after run
+            del g
+            alg.close()
+            out.setdefault(str(n), {})[sched] = {
+                "engine": engine, "eager_us": round(eager_s / a.iters * 1e6, 2),
+                "graph_us": round(graph_s / (a.iters // a.per_graph * a.per_graph) * 1e6, 2),
+                "result_ok": ok}
+    if rank == 0:
+        print(json.dumps({"what": "allreduce latency per call, eager (back to back on a stream) "
+                                  "vs HIP graph replay (%d calls per graph), max over ranks"
+                                  % a.per_graph, "ranks": world, "sizes": out}))
+    dist.barrier()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
