@@ -822,7 +822,15 @@ void HipPlanExecutor::run() {
     GLX_HIP_CHECK(hipEventRecord(sideOut_, compute_));
     for (hipStream_t st : sideStreams_) GLX_HIP_CHECK(hipStreamWaitEvent(st, sideOut_, 0));
   }
-  noteDone(compute_);
+  if (engine_ == kEngineSteps || staged_ || ptrs_.size() > 1 || sideOut_ != nullptr ||
+      contextSize_ == 1) {
+    noteDone(compute_);
+  } else {
+    // nothing follows the device launch on compute_, which is this
+    // algorithm's stream for its life: release() synchronizes it, and an
+    // event record here would cost every call several microseconds
+    lastStream_ = compute_;
+  }
   GLX_TRACE("r%d sync", contextRank_);
   if (!userStream_) {
     waitDevice(compute_);
@@ -892,6 +900,10 @@ void HipPlanExecutor::runFn(const FnCall& call) {
       e->timeout_ = std::chrono::milliseconds(0);
     }
   } restore{this, compute_};
+  if (!fnCalls_ && ddLaunched_) {  // run() launches recorded no done event
+    GLX_HIP_CHECK(hipEventRecord(ddDone_, ddLastStream_));
+  }
+  fnCalls_ = true;
   if (call.stream != nullptr) compute_ = call.stream;
   timeout_ = call.timeout;
   localReduce(call.in, call.out);

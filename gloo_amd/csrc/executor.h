@@ -372,6 +372,9 @@ class HipPlanExecutor : public Algorithm {
   int* ddClaim_ = nullptr;  // device word: the first timed-out workgroup claims the report
   hipEvent_t ddDone_ = nullptr;
   bool ddLaunched_ = false;
+  // a function-style call came (runFn): the stream may change from call to
+  // call, so every device launch records ddDone_ for the next one to wait on
+  bool fnCalls_ = false;
   hipStream_t ddLastStream_ = nullptr;  // the stream of the last device-engine launch
   int clockKhz_ = 100000;  // s_memrealtime rate
   uint64_t* trace_ = nullptr;  // GLOO_AMD_DEVTRACE=1: two-shot phase stamps (pinned host)

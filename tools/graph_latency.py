@@ -41,14 +41,17 @@ def main():
     out = {}
 
     def timed(fn, n):
+        """(seconds for n calls including the GPU's, seconds to issue them),
+        each the max over ranks"""
         s.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
         fn(n)
+        t1 = time.perf_counter()
         s.synchronize()
-        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        el = torch.tensor([time.perf_counter() - t0, t1 - t0], dtype=torch.float64)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        return el.item()
+        return el[0].item(), el[1].item()
 
     for n in [int(x) for x in a.sizes.split(",")]:
         for sched in ("replicated", "ring"):
@@ -64,7 +67,7 @@ def main():
             def eager(k):
                 for _ in range(k):
                     alg.run()
-            eager_s = timed(eager, a.iters)
+            eager_s, issue_s = timed(eager, a.iters)
             g = torch.cuda.CUDAGraph()
             s.synchronize()
             with torch.cuda.graph(g, stream=s):
@@ -75,19 +78,32 @@ def main():
                 with torch.cuda.stream(s):
                     for _ in range(k // a.per_graph):
                         g.replay()
-            graph_s = timed(replay, a.iters)
+            graph_s = timed(replay, a.iters)[0]
             s.synchronize()
             ok = bool((buf == 0).all().item())  # zeros stay zeros, run after run
             del g
             alg.close()
             out.setdefault(str(n), {})[sched] = {
                 "engine": engine, "eager_us": round(eager_s / a.iters * 1e6, 2),
+                "eager_issue_us": round(issue_s / a.iters * 1e6, 2),
                 "graph_us": round(graph_s / (a.iters // a.per_graph * a.per_graph) * 1e6, 2),
                 "result_ok": ok}
+    # the floor for a kernel launched from Python on the same stream: a
+    # torch elementwise op of the smallest size, back to back
+    x = torch.zeros(256, dtype=torch.float32, device="cuda")
+
+    def torch_op(k):
+        with torch.cuda.stream(s):
+            for _ in range(k):
+                x.add_(0.0)
+    torch_op(20)  # loads the op's code object
+    op_s, op_issue_s = timed(torch_op, a.iters)
     if rank == 0:
         print(json.dumps({"what": "allreduce latency per call, eager (back to back on a stream) "
                                   "vs HIP graph replay (%d calls per graph), max over ranks"
-                                  % a.per_graph, "ranks": world, "sizes": out}))
+                                  % a.per_graph, "ranks": world, "sizes": out,
+                          "torch_add_us": round(op_s / a.iters * 1e6, 2),
+                          "torch_add_issue_us": round(op_issue_s / a.iters * 1e6, 2)}))
     dist.barrier()
     ctx.close()
 
