@@ -350,6 +350,7 @@ void HipPlanExecutor::release() noexcept {
   // the last call's work may sit on a caller's stream (runFn with a stream):
   // it reads our scratch until it completes
   if (lastDone_ != nullptr && lastStream_ != nullptr) hipEventSynchronize(lastDone_);
+  if (ddDone_ != nullptr && fnCalls_) hipEventSynchronize(ddDone_);
   if (compute_ != nullptr) hipStreamSynchronize(compute_);
   for (auto& c : copies_) hipStreamSynchronize(c.s);
   for (hipStream_t st : {h2d_, d2h_}) {
@@ -913,7 +914,11 @@ void HipPlanExecutor::runFn(const FnCall& call) {
     GLX_HIP_CHECK(hipMemcpyAsync(call.out[i], out0, (size_t)count_ * esize_,
                                  hipMemcpyDeviceToDevice, compute_));
   }
-  noteDone(compute_);
+  if (engine_ == kEngineSteps || staged_ || call.out.size() > 1 || contextSize_ == 1) {
+    noteDone(compute_);
+  } else {
+    lastStream_ = compute_;  // the launch's ddDone_ is the last thing on it
+  }
   if (call.stream == nullptr) {
     waitDevice(compute_);
     checkDevice();

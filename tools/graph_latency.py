@@ -88,6 +88,27 @@ def main():
                 "eager_issue_us": round(issue_s / a.iters * 1e6, 2),
                 "graph_us": round(graph_s / (a.iters // a.per_graph * a.per_graph) * 1e6, 2),
                 "result_ok": ok}
+        # the function-style call (gloo::allreduce(opts)) on the same stream,
+        # eager only: its executor comes from a cache keyed by the call
+        for name, algo in (("fn_replicated", gloo_amd.AllreduceOptions.Algorithm.RING_REPLICATED),
+                           ("fn_ring", gloo_amd.AllreduceOptions.Algorithm.RING)):
+            buf = torch.zeros(n, dtype=torch.float32, device="cuda")
+            opts = gloo_amd.AllreduceOptions(ctx)
+            opts.setAlgorithm(algo)
+            opts.setOutput(buf)
+            opts.setStream(s)
+            for _ in range(5):
+                gloo_amd.allreduce(opts)
+
+            def fn_calls(k):
+                for _ in range(k):
+                    gloo_amd.allreduce(opts)
+            fn_s, fn_issue_s = timed(fn_calls, a.iters)
+            s.synchronize()
+            out.setdefault(str(n), {})[name] = {
+                "eager_us": round(fn_s / a.iters * 1e6, 2),
+                "eager_issue_us": round(fn_issue_s / a.iters * 1e6, 2),
+                "result_ok": bool((buf == 0).all().item())}
     # the floor for a kernel launched from Python on the same stream: a
     # torch elementwise op of the smallest size, back to back
     x = torch.zeros(256, dtype=torch.float32, device="cuda")
