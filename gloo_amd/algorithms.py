@@ -229,12 +229,13 @@ class Algorithm:
         refused a mapping), kernel_copies (copy kernel into the peer's
         memory), device_kernels (device-driven engine launches), bytes, and
         host_folds (multi-pointer host buffers below kOnDeviceThreshold folded
-        on the host)."""
-        out = (ctypes.c_int64 * 6)()
-        if lib.glx_algorithm_transport_stats(self._h, out, 6) != 6:
+        on the host), done_events (event records after a run's work: none
+        for run() on a device engine)."""
+        out = (ctypes.c_int64 * 7)()
+        if lib.glx_algorithm_transport_stats(self._h, out, 7) != 7:
             check(_lib.ERR_INVALID, "transport_stats")
         return dict(zip(("peer_copies", "device_copies", "kernel_copies", "device_kernels",
-                         "bytes", "host_folds"), list(out)))
+                         "bytes", "host_folds", "done_events"), list(out)))
 
     def record(self, event):
         """Record `event` (gloo_amd.Event) at the end of the last run()'s

@@ -531,7 +531,9 @@ int glx_algorithm_transport_stats(glx_algorithm* alg, int64_t* out, int cap) {
   out[3] = t.deviceKernels;
   out[4] = t.bytes;
   out[5] = t.hostFolds;
-  return 6;
+  if (cap < 7) return 6;
+  out[6] = t.doneEvents;
+  return 7;
 }
 
 int glx_algorithm_record(glx_algorithm* alg, glx_event_t ev) {

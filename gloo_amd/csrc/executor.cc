@@ -903,6 +903,7 @@ void HipPlanExecutor::runFn(const FnCall& call) {
   } restore{this, compute_};
   if (!fnCalls_ && ddLaunched_) {  // run() launches recorded no done event
     GLX_HIP_CHECK(hipEventRecord(ddDone_, ddLastStream_));
+    transport_.doneEvents++;
   }
   fnCalls_ = true;
   if (call.stream != nullptr) compute_ = call.stream;
@@ -927,6 +928,7 @@ void HipPlanExecutor::runFn(const FnCall& call) {
 
 void HipPlanExecutor::noteDone(hipStream_t s) {
   GLX_HIP_CHECK(hipEventRecord(lastDone_, s));
+  transport_.doneEvents++;
   lastStream_ = s;
 }
 

@@ -95,6 +95,8 @@ class HipPlanExecutor : public Algorithm {
     int64_t deviceKernels = 0;  // one-shot / two-shot / plan kernel launches
     int64_t bytes = 0;          // bytes of the copies above
     int64_t hostFolds = 0;      // local reduces done on the host (kOnDeviceThreshold)
+    int64_t doneEvents = 0;     // hipEventRecords after a run's work (each costs
+                                // the stream several microseconds)
   };
   const TransportStats& transportStats() const { return transport_; }
   // Record `ev` after this algorithm's last enqueued work: the compute

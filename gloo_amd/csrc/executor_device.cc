@@ -738,7 +738,10 @@ void HipPlanExecutor::runDevice(char* ptr0) {
   // The done event serves a later call on another stream (function-style
   // calls) and the staged copy-back; run() keeps one stream for its life,
   // and each event record costs the stream several microseconds per call.
-  if (staged_ || fnCalls_) GLX_HIP_CHECK(hipEventRecord(ddDone_, compute_));
+  if (staged_ || fnCalls_) {
+    GLX_HIP_CHECK(hipEventRecord(ddDone_, compute_));
+    transport_.doneEvents++;
+  }
   ddLaunched_ = true;
   ddLastStream_ = compute_;
   if (staged_) {

@@ -245,7 +245,7 @@ class Event {
 
 // How an algorithm's messages moved (glx_algorithm_transport_stats).
 struct TransportStats {
-  int64_t peerCopies, deviceCopies, kernelCopies, deviceKernels, bytes, hostFolds;
+  int64_t peerCopies, deviceCopies, kernelCopies, deviceKernels, bytes, hostFolds, doneEvents;
 };
 
 namespace detail {
@@ -293,9 +293,9 @@ class DeviceAllreduce : public Algorithm {
   // record `ev` at the end of the last run's work (streams[0] with streams)
   void record(Event& ev) { check(glx_algorithm_record(a_, ev.handle()), "record"); }
   TransportStats transportStats() const {
-    int64_t o[6] = {0};
-    glx_algorithm_transport_stats(a_, o, 6);
-    return TransportStats{o[0], o[1], o[2], o[3], o[4], o[5]};
+    int64_t o[7] = {0};
+    glx_algorithm_transport_stats(a_, o, 7);
+    return TransportStats{o[0], o[1], o[2], o[3], o[4], o[5], o[6]};
   }
 
  private:

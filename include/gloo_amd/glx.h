@@ -413,9 +413,12 @@ int glx_algorithm_sync(glx_algorithm* alg);
  * device_kernels (launches of a device-driven engine, whose kernels store into
  * the peers' memory themselves), bytes (of the copies), host_folds (local
  * multi-pointer reduces done on the host: host buffers below
- * kOnDeviceThreshold = 256 KiB, gloo/algorithm.cc:16)}.  The peer-copy analog
- * of the reference's transport byte counters and of its intra-process peer
- * copies (gloo/cuda_collectives_native.h:205-276).  Returns 6 or -1. */
+ * kOnDeviceThreshold = 256 KiB, gloo/algorithm.cc:16), done_events (event
+ * records after a run's work: none for run() on a device engine, whose stream
+ * is fixed -- each record costs the stream microseconds per call)}.  The
+ * peer-copy analog of the reference's transport byte counters and of its
+ * intra-process peer copies (gloo/cuda_collectives_native.h:205-276).  Fills
+ * min(cap, 7) fields (cap >= 6); returns that count, or -1. */
 int glx_algorithm_transport_stats(glx_algorithm* alg, int64_t* out, int cap);
 void glx_algorithm_destroy(glx_algorithm* alg);
 
