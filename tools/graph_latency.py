@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--sizes", default="256,4096,65536,1048576")
     ap.add_argument("--iters", type=int, default=400)
     ap.add_argument("--per-graph", type=int, default=20)
+    ap.add_argument("--schedules", default="replicated,ring,fn_replicated,fn_ring")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -53,8 +54,9 @@ def main():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         return el[0].item(), el[1].item()
 
-    for n in [int(x) for x in a.sizes.split(",")]:
-        for sched in ("replicated", "ring"):
+    for idx, n in enumerate([int(x) for x in a.sizes.split(",")]):
+        key = str(n) if str(n) not in out else "%d#%d" % (n, idx)  # a size again
+        for sched in [x for x in a.schedules.split(",") if not x.startswith("fn_")]:
             buf = torch.zeros(n, dtype=torch.float32, device="cuda")
             alg = gloo_amd.AllreduceRingChunked(ctx, [buf], streams=[s], schedule=sched)
             engine = alg.engine()
@@ -83,15 +85,17 @@ def main():
             ok = bool((buf == 0).all().item())  # zeros stay zeros, run after run
             del g
             alg.close()
-            out.setdefault(str(n), {})[sched] = {
+            out.setdefault(key, {})[sched] = {
                 "engine": engine, "eager_us": round(eager_s / a.iters * 1e6, 2),
                 "eager_issue_us": round(issue_s / a.iters * 1e6, 2),
                 "graph_us": round(graph_s / (a.iters // a.per_graph * a.per_graph) * 1e6, 2),
                 "result_ok": ok}
         # the function-style call (gloo::allreduce(opts)) on the same stream,
         # eager only: its executor comes from a cache keyed by the call
-        for name, algo in (("fn_replicated", gloo_amd.AllreduceOptions.Algorithm.RING_REPLICATED),
-                           ("fn_ring", gloo_amd.AllreduceOptions.Algorithm.RING)):
+        fns = {"fn_replicated": gloo_amd.AllreduceOptions.Algorithm.RING_REPLICATED,
+               "fn_ring": gloo_amd.AllreduceOptions.Algorithm.RING}
+        for name in [x for x in a.schedules.split(",") if x.startswith("fn_")]:
+            algo = fns[name]
             buf = torch.zeros(n, dtype=torch.float32, device="cuda")
             opts = gloo_amd.AllreduceOptions(ctx)
             opts.setAlgorithm(algo)
@@ -104,9 +108,11 @@ def main():
                 for _ in range(k):
                     gloo_amd.allreduce(opts)
             fn_s, fn_issue_s = timed(fn_calls, a.iters)
+            again_s = timed(fn_calls, a.iters)[0]  # a one-time cost shows as a gap
             s.synchronize()
-            out.setdefault(str(n), {})[name] = {
+            out.setdefault(key, {})[name] = {
                 "eager_us": round(fn_s / a.iters * 1e6, 2),
+                "eager_again_us": round(again_s / a.iters * 1e6, 2),
                 "eager_issue_us": round(fn_issue_s / a.iters * 1e6, 2),
                 "result_ok": bool((buf == 0).all().item())}
     # the floor for a kernel launched from Python on the same stream: a
