@@ -49,6 +49,8 @@ class AllreduceOptions:
         self.max_segment_size = 0  # 0: the reference's 1 MiB default (allreduce.h:80)
         self.timeout_ms = 0        # 0: the context's timeout
         self.stream = None
+        self._in_ptrs = self._out_ptrs = None  # (ctypes array, count), from the setters
+        self._any_cuda = False
 
     def setAlgorithm(self, algorithm):
         self.algorithm = int(algorithm)
@@ -58,17 +60,20 @@ class AllreduceOptions:
 
     def setInputs(self, bufs, elements=None, dtype=None):
         self.inputs = list(bufs)
-        self._sizes(self.inputs, elements, dtype)
+        self._in_ptrs = self._sizes(self.inputs, elements, dtype)
 
     def setOutput(self, buf, elements=None):
         self.setOutputs([buf], elements)
 
     def setOutputs(self, bufs, elements=None, dtype=None):
         self.outputs = list(bufs)
-        self._sizes(self.outputs, elements, dtype)
+        self._out_ptrs = self._sizes(self.outputs, elements, dtype)
 
     def _sizes(self, bufs, elements, dtype):
-        _, dt, numel = _as_ptrs(bufs, dtype if dtype is not None else self.dtype)
+        """Checks the buffers and returns their pointers, taken now as the
+        reference's setInput/setOutput take them (gloo/allreduce.h:103-141):
+        allreduce() reuses them call after call."""
+        ptrs, dt, numel = _as_ptrs(bufs, dtype if dtype is not None else self.dtype)
         if self.dtype is not None and dt != self.dtype:
             raise TypeError("inputs and outputs must share one dtype")
         self.dtype = dt
@@ -79,6 +84,9 @@ class AllreduceOptions:
         if numel is not None and elements > numel:
             raise ValueError("elements %d exceeds buffer size %d" % (elements, numel))
         self.elements = int(elements)
+        self._any_cuda = any(getattr(b, "is_cuda", False)
+                             for b in list(self.outputs) + list(self.inputs))
+        return (ctypes.c_void_p * max(len(ptrs), 1))(*ptrs), len(ptrs)
 
     def setReduceFunction(self, fn):
         """ReductionFunction.sum/..., a ReductionType value, or
@@ -118,14 +126,11 @@ def allreduce(opts):
     if not opts.outputs:
         raise EnforceNotMet("allreduce: at least one output is required")
     op = opts.op if opts.op is not None else 1
-    inp, _, _ = _as_ptrs(opts.inputs, opts.dtype) if opts.inputs else ([], None, None)
-    outp, _, _ = _as_ptrs(opts.outputs, opts.dtype)
-    iarr = (ctypes.c_void_p * max(len(inp), 1))(*inp)
-    oarr = (ctypes.c_void_p * len(outp))(*outp)
+    iarr, ni = opts._in_ptrs if opts.inputs else ((ctypes.c_void_p * 1)(), 0)
+    oarr, no = opts._out_ptrs
     sync = None
     stream = _stream_ptr(opts.stream)
-    if stream is None and any(getattr(b, "is_cuda", False)
-                              for b in opts.outputs + opts.inputs):
+    if stream is None and opts._any_cuda:
         import torch
         cur = torch.cuda.current_stream()
         if cur.cuda_stream:
@@ -133,7 +138,7 @@ def allreduce(opts):
         else:
             cur.synchronize()  # the null stream: let its queued writes land first
     check(lib.glx_allreduce(opts.context.handle, opts.algorithm, opts.dtype, op,
-                            iarr, len(inp), oarr, len(outp), opts.elements or 0,
+                            iarr, ni, oarr, no, opts.elements or 0,
                             opts.tag, opts.max_segment_size, opts.timeout_ms, stream),
           "allreduce")
     if sync is not None:
