@@ -103,16 +103,42 @@ def set_device_sync(mode):
     errors.check(_lib.lib.glx_set_device_sync(code), "set_device_sync")
 
 
+_DEVICE_ENGINE_MODES = {"auto": -1, "off": 0, "on": 1, "shared": 2}
+
+
 def set_device_engines(mode):
     """Device-driven engines (plan, one-shot and two-shot kernels) for
-    algorithms created afterwards: "auto", "off" (host-issued steps only) or
-    "on".  "auto" (default): always with one rank per GPU; never for threads
-    of one process sharing a GPU; for processes sharing a GPU only while
-    ranks-on-the-GPU x (queues + 1) <= 20, where queues is the largest
-    GPU_MAX_HW_QUEUES any rank's process published at connect (default 4) --
-    every rank decides from the same endpoints."""
-    code = {"auto": -1, "off": 0, "on": 1}[mode]
-    errors.check(_lib.lib.glx_set_device_engines(code), "set_device_engines")
+    algorithms created afterwards (initially GLOO_AMD_DEVICE_ENGINES):
+    "auto" (default): only when every rank has a GPU of its own -- ranks
+    sharing a GPU run host-issued steps, since their device engines hold the
+    GPU's CUs while waiting for each other and can starve other work queued
+    ahead of one rank's collective; "shared": also
+    processes sharing a GPU while ranks-on-the-GPU x (queues + 1) <= 20,
+    where queues is the largest GPU_MAX_HW_QUEUES any rank's process
+    published at connect (default 4), for callers that queue no other GPU
+    work ahead of a collective there (rehearsals); "on" always; "off" never.
+    Every rank decides from the same endpoints and must use the same mode."""
+    errors.check(_lib.lib.glx_set_device_engines(_DEVICE_ENGINE_MODES[mode]),
+                 "set_device_engines")
+
+
+def get_device_engines():
+    """The current device-engine mode ("auto", "off", "on" or "shared")."""
+    code = _lib.lib.glx_get_device_engines()
+    return {v: k for k, v in _DEVICE_ENGINE_MODES.items()}[code]
+
+
+def device_engines_rule(mode, ranks, ranks_per_device, threads_share_device=False,
+                        max_hw_queues=4):
+    """Whether `mode` gives `ranks` ranks (at most `ranks_per_device` on one
+    GPU, the largest GPU_MAX_HW_QUEUES `max_hw_queues`) the device engines:
+    the rule set_device_engines applies (glx_device_engines_rule; no GPU)."""
+    r = _lib.lib.glx_device_engines_rule(_DEVICE_ENGINE_MODES[mode], int(ranks),
+                                         int(ranks_per_device), int(bool(threads_share_device)),
+                                         int(max_hw_queues))
+    if r < 0:
+        errors.check(_lib.ERR_INVALID, "device_engines_rule")
+    return bool(r)
 
 
 def peer_copy(dst_ptr, dst_dev, src_ptr, src_dev, nbytes, stream):

@@ -107,6 +107,8 @@ SIGNATURES = [
     ("glx_set_copy_engine", _i, [_i, _i]),
     ("glx_set_mesh_engine", _i, [_i]),
     ("glx_set_device_engines", _i, [_i]),
+    ("glx_get_device_engines", _i, []),
+    ("glx_device_engines_rule", _i, [_i, _i, _i, _i, _i]),
     ("glx_set_steps_engine", _i, [_i]),
     ("glx_set_engine_streams", _i, [_i]),
     ("glx_allreduce", _i, [_vp, _i, _i, _i, ctypes.POINTER(_vp), _i, ctypes.POINTER(_vp), _i,

@@ -413,7 +413,7 @@ def plan_sync(algo, rank, size, count, G, esize=4, max_segment_size=0,
         check(_lib.ERR_INVALID, "plan_sync")
     bb = (ctypes.c_int64 * max(nb.value, 1))()
     sb = (ctypes.c_int64 * max(12 * n, 1))()
-    lib.glx_plan_sync(*args, bb, nb.value, ctypes.byref(nb), info, sb, n)
+    lib.glx_plan_sync(*args, bb, nb.value, ctypes.byref(nb), info, sb, 12 * n)  # int64 slots
     return {"bounds": list(bb[:nb.value]), "slice": info[0], "safe": bool(info[1]),
             "slots": info[2], "steps": [tuple(sb[12 * i:12 * i + 12]) for i in range(n)]}
 

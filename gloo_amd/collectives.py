@@ -40,8 +40,7 @@ class AllreduceOptions:
     def __init__(self, context):
         self.context = context
         self.algorithm = self.Algorithm.UNSPECIFIED
-        self.inputs = []
-        self.outputs = []
+        self._inputs, self._outputs = [], []
         self.elements = None
         self.dtype = None
         self.op = None
@@ -59,15 +58,33 @@ class AllreduceOptions:
         self.setInputs([buf], elements)
 
     def setInputs(self, bufs, elements=None, dtype=None):
-        self.inputs = list(bufs)
-        self._in_ptrs = self._sizes(self.inputs, elements, dtype)
+        self._inputs = list(bufs)
+        self._in_ptrs = self._sizes(self._inputs, elements, dtype) if self._inputs else None
 
     def setOutput(self, buf, elements=None):
         self.setOutputs([buf], elements)
 
     def setOutputs(self, bufs, elements=None, dtype=None):
-        self.outputs = list(bufs)
-        self._out_ptrs = self._sizes(self.outputs, elements, dtype)
+        self._outputs = list(bufs)
+        self._out_ptrs = self._sizes(self._outputs, elements, dtype) if self._outputs else None
+
+    # Assigning the lists goes through the setters, so the pointers allreduce()
+    # uses always belong to the buffers the options hold.
+    @property
+    def inputs(self):
+        return list(self._inputs)
+
+    @inputs.setter
+    def inputs(self, bufs):
+        self.setInputs(bufs)
+
+    @property
+    def outputs(self):
+        return list(self._outputs)
+
+    @outputs.setter
+    def outputs(self, bufs):
+        self.setOutputs(bufs)
 
     def _sizes(self, bufs, elements, dtype):
         """Checks the buffers and returns their pointers, taken now as the
@@ -85,7 +102,7 @@ class AllreduceOptions:
             raise ValueError("elements %d exceeds buffer size %d" % (elements, numel))
         self.elements = int(elements)
         self._any_cuda = any(getattr(b, "is_cuda", False)
-                             for b in list(self.outputs) + list(self.inputs))
+                             for b in list(self._outputs) + list(self._inputs))
         return (ctypes.c_void_p * max(len(ptrs), 1))(*ptrs), len(ptrs)
 
     def setReduceFunction(self, fn):
@@ -123,10 +140,10 @@ def allreduce(opts):
     """gloo::allreduce(opts) (gloo/allreduce.cc:97-146).  Without a stream
     the call is ordered after the work queued on torch's current stream and
     returns with the outputs complete, like the reference's blocking call."""
-    if not opts.outputs:
+    if not opts._outputs:
         raise EnforceNotMet("allreduce: at least one output is required")
     op = opts.op if opts.op is not None else 1
-    iarr, ni = opts._in_ptrs if opts.inputs else ((ctypes.c_void_p * 1)(), 0)
+    iarr, ni = opts._in_ptrs if opts._inputs else ((ctypes.c_void_p * 1)(), 0)
     oarr, no = opts._out_ptrs
     sync = None
     stream = _stream_ptr(opts.stream)

@@ -223,9 +223,26 @@ int glx_set_steps_engine(int engine) {
 }
 
 int glx_set_device_engines(int mode) {
-  if (mode < -1 || mode > 1) return fail(GLX_ERR_INVALID, "device engine mode must be -1, 0 or 1");
+  if (mode < GLX_DEVICE_ENGINES_AUTO || mode > GLX_DEVICE_ENGINES_SHARED) {
+    return fail(GLX_ERR_INVALID, "device engine mode must be -1 (auto), 0 (off), 1 (on) or 2 (shared)");
+  }
   gloo::HipPlanExecutor::setDeviceEngines(mode);
   return GLX_OK;
+}
+
+int glx_get_device_engines(void) { return gloo::HipPlanExecutor::deviceEngines(); }
+
+int glx_device_engines_rule(int mode, int ranks, int ranks_per_device, int threads_share_device,
+                            int max_hw_queues) {
+  if (mode < GLX_DEVICE_ENGINES_AUTO || mode > GLX_DEVICE_ENGINES_SHARED || ranks < 1 ||
+      ranks_per_device < 1 || ranks_per_device > ranks) {
+    (void)fail(GLX_ERR_INVALID, "glx_device_engines_rule: invalid argument");
+    return -1;
+  }
+  return gloo::HipPlanExecutor::deviceEnginesRule(mode, ranks, ranks_per_device,
+                                                  threads_share_device != 0, max_hw_queues)
+             ? 1
+             : 0;
 }
 
 int glx_set_copy_split(int k) {
@@ -727,9 +744,11 @@ int64_t glx_plan_sync(int algo, int rank, int size, int64_t count, int esize,
          i++) {
       bounds[i] = t.bounds[(size_t)i];
     }
-    for (int64_t i = 0; i < n && i < cap && steps != nullptr; i++) {
+    // cap counts int64 slots: step i is written only when all of
+    // its GLX_PLAN_SYNC_WIDTH words fit
+    for (int64_t i = 0; i < n && (i + 1) * GLX_PLAN_SYNC_WIDTH <= cap && steps != nullptr; i++) {
       const glx::StepSync& y = t.steps[(size_t)i];
-      int64_t* o = steps + 12 * i;
+      int64_t* o = steps + GLX_PLAN_SYNC_WIDTH * i;
       o[0] = y.chan;
       o[1] = y.seg0;
       o[2] = y.seg1;

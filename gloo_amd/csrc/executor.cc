@@ -302,16 +302,12 @@ void HipPlanExecutor::drainCredits() noexcept {
           pause();
         }
       }
-    } else if (engine_ == kEngineDevSteps && devRuns_ > 0 && !ddBlocks_.empty()) {
-      // the runs the GPU completed (graph replays included: kernels.h runCtr)
-      uint64_t runs = devRuns_;
-      if (runCtr_ != nullptr && hipStreamSynchronize(compute_) == hipSuccess) {
-        uint64_t dev = 0;
-        if (hipMemcpy(&dev, runCtr_, sizeof(dev), hipMemcpyDeviceToHost) == hipSuccess) {
-          runs = std::max(runs, dev);
-        }
-      }
-      (void)hipGetLastError();
+    } else if (engine_ != kEngineSteps) {
+      // the launches the GPU completed, graph replays on other streams
+      // included: wait until every started launch finished
+      const uint64_t settled = settleLaunches(deadline);
+      if (engine_ != kEngineDevSteps || devRuns_ == 0 || ddBlocks_.empty()) return;
+      const uint64_t runs = std::max<uint64_t>(devRuns_, settled);
       // final credit of out-channel c on every workgroup: runs * perRun
       std::vector<uint64_t> want(out_.size(), 0);
       for (size_t i = 0; i < plan_.steps.size() && i < sync_.steps.size(); i++) {
@@ -340,6 +336,29 @@ void HipPlanExecutor::drainCredits() noexcept {
       }
     }
   } catch (...) {
+  }
+}
+
+uint64_t HipPlanExecutor::settleLaunches(std::chrono::steady_clock::time_point deadline) noexcept {
+  if (launchCtr_ == nullptr) return 0;
+  if (hipStreamSynchronize(compute_) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  const int G = engine_ == kEngineOneShot ? os_.G : (engine_ == kEngineTwoShot ? ts_.G : pk_.G);
+  std::vector<uint64_t> ctr((size_t)glx::kLaunchCtrLines * glx::kFlagStride);
+  for (;;) {
+    if (hipMemcpy(ctr.data(), launchCtr_, ctr.size() * sizeof(uint64_t),
+                  hipMemcpyDeviceToHost) != hipSuccess) {
+      (void)hipGetLastError();
+      return 0;
+    }
+    const uint64_t done = ctr[0], started = ctr[2 * (size_t)glx::kFlagStride];
+    if (started <= done * (uint64_t)G || std::chrono::steady_clock::now() >= deadline) {
+      return done;
+    }
+    context_->checkPeersAlive();  // throws if a peer exited: stop waiting
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
 }
 

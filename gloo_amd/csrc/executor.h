@@ -366,6 +366,12 @@ class HipPlanExecutor : public Algorithm {
   std::vector<glx::DevStep> hostSteps_;  // host copy (timeout diagnostics)
   glx::DevSegment* devSegs_ = nullptr;
   uint64_t* runCtr_ = nullptr;  // the plan kernel's run count (kernels.h), in the flag block
+  // the device engine's launch counters (kernels.h kLaunchCtrLines), any engine
+  uint64_t* launchCtr_ = nullptr;
+  // Wait (bounded by the deadline) until every launch of the device engine
+  // that has started -- graph replays on any stream included -- completed;
+  // returns the launches completed (0 if unknown).
+  uint64_t settleLaunches(std::chrono::steady_clock::time_point deadline) noexcept;
   const char** devFoldSrc_ = nullptr;
   uint64_t devRuns_ = 0;
   uint64_t ddEpoch_ = 0;
@@ -401,12 +407,31 @@ class HipPlanExecutor : public Algorithm {
  public:
   static constexpr int kEngineSteps = 0, kEngineOneShot = 1, kEngineTwoShot = 2,
                        kEngineDevSteps = 3;
-  // Whether device-driven engines can run on this context: setDeviceEngines
-  // (0 = never, 1 = always), by default when every rank has a GPU of its
-  // own, or ranks that share one are processes whose hardware queues fit
-  // kSharedQueueBudget (their kernels must all run at once).  P <= 8.
+  // Whether device-driven engines can run on this context:
+  // deviceEnginesRule over the context's endpoints and setDeviceEngines.
   static bool deviceEnginesAvailable(const Context& ctx);
-  // Processes sharing one GPU get the device engines by default only while
+  // The rule itself (glx_device_engines_rule), a pure function so every rank
+  // derives the same answer from the same endpoints and the CPU tests can
+  // walk it.  mode: kDevEnginesAuto / Off / On / Shared.
+  //  * auto (default): only when every rank has a GPU of its own.  Ranks
+  //    sharing a GPU wait for each other's kernels while holding its CUs, so
+  //    any other work queued ahead of one rank's collective -- on its stream
+  //    or in a hardware queue its stream shares -- can be starved by the
+  //    peers' resident grids until the timeout (8 x 1 queue,
+  //    a GEMM ahead of rank 0's collective, profiles/r9j_*, r9l_*).  No
+  //    queue count rules that out (a GEMM on the collective's own stream
+  //    forms the same cycle), so the default keeps such ranks on the
+  //    host-issued steps, which hold no CUs while they wait.
+  //  * shared: also processes sharing a GPU, while ranks-on-the-GPU x
+  //    (queues + 1) <= kSharedQueueBudget -- for rehearsals and callers that
+  //    run nothing else on the shared GPU while a collective is in flight.
+  //    Never threads of one process (their launches may serialise).
+  //  * on: always (the caller guarantees co-residency); off: never.
+  static bool deviceEnginesRule(int mode, int size, int ranksPerDevice, bool threadsShareDevice,
+                                int maxQueues);
+  static constexpr int kDevEnginesAuto = -1, kDevEnginesOff = 0, kDevEnginesOn = 1,
+                       kDevEnginesShared = 2;
+  // Processes sharing one GPU (shared mode) get the device engines only while
   // ranks-on-the-GPU x (hwQueuesPerProcess() + 1) stays within this many
   // hardware queues, leaving room for one more process's (measured on one
   // MI355X with a busy parent process: 2x4, 3x4, 4x4, 5x2, 6x2, 8x1
@@ -414,9 +439,10 @@ class HipPlanExecutor : public Algorithm {
   static constexpr int kSharedQueueBudget = 20;
   static int hwQueuesPerProcess();
   void enforceSpan(size_t sliceElems) const;
-  // Override for algorithms created afterwards: 0 = never, 1 = always
-  // (caller guarantees co-residency), -1 = automatic (the default).
+  // Mode for algorithms created afterwards (kDevEngines*); the initial value
+  // comes from GLOO_AMD_DEVICE_ENGINES=auto|off|on|shared.
   static void setDeviceEngines(int mode);
+  static int deviceEngines();
   // Engine of the mesh schedule when available: kEngineTwoShot (default)
   // or kEngineSteps.  Read at construction.
   static void setMeshEngine(int engine);

@@ -92,37 +92,56 @@ int HipPlanExecutor::engineStreams() { return g_engine_streams.load(); }
 
 namespace {
 
-std::atomic<int> g_device_engines{-1};  // glx_set_device_engines
+// glx_set_device_engines; GLOO_AMD_DEVICE_ENGINES=auto|off|on|shared
+std::atomic<int> g_device_engines{[] {
+  const char* e = std::getenv("GLOO_AMD_DEVICE_ENGINES");
+  if (e != nullptr && std::strcmp(e, "off") == 0) return HipPlanExecutor::kDevEnginesOff;
+  if (e != nullptr && std::strcmp(e, "on") == 0) return HipPlanExecutor::kDevEnginesOn;
+  if (e != nullptr && std::strcmp(e, "shared") == 0) return HipPlanExecutor::kDevEnginesShared;
+  return HipPlanExecutor::kDevEnginesAuto;
+}()};
 
 }  // namespace
 
 void HipPlanExecutor::setDeviceEngines(int mode) {
-  g_device_engines.store(mode < 0 ? -1 : (mode > 0 ? 1 : 0));
+  g_device_engines.store(mode < kDevEnginesAuto || mode > kDevEnginesShared ? kDevEnginesAuto
+                                                                            : mode);
 }
+
+int HipPlanExecutor::deviceEngines() { return g_device_engines.load(); }
 
 // Hardware queues one process opens (HIP's GPU_MAX_HW_QUEUES, default 4).
 int HipPlanExecutor::hwQueuesPerProcess() { return hwQueuesOfProcess(); }
 
-bool HipPlanExecutor::deviceEnginesAvailable(const Context& ctx) {
-  if (ctx.size < 2 || ctx.size > glx::kOsMaxRanks) return false;
-  const int mode = g_device_engines.load();
-  if (mode >= 0) return mode == 1;
+bool HipPlanExecutor::deviceEnginesRule(int mode, int size, int ranksPerDevice,
+                                        bool threadsShareDevice, int maxQueues) {
+  if (size < 2 || size > glx::kOsMaxRanks) return false;
+  if (mode == kDevEnginesOff) return false;
+  if (mode == kDevEnginesOn) return true;
   // The device engines' kernels wait on each other, so every rank's kernel
-  // must be running at once.  One rank per GPU: always.  Threads of one
-  // process sharing a GPU: never (their launches may serialise).  Processes
-  // sharing a GPU: only while all their hardware queues fit what the GPU's
-  // scheduler maps at once; beyond that it time-slices the queues and every
-  // dependent step waits for a rotation (8 processes x 4 queues on one
-  // MI355X: ~170 ms per 1-element allreduce, 8 x 2: ~60 ms, 8 x 1 and
-  // 4 x 4: < 1 ms; the suite's P=8 test timed out at 20 s: DESIGN.md 9,
-  // profiles/r7e_*, r7g_queue_sweep.txt).
-  if (ctx.maxRanksPerDevice() == 1) return true;
-  if (ctx.ranksShareDevice()) return false;
+  // must be running at once.  One rank per GPU: always.
+  if (ranksPerDevice <= 1) return true;
+  // Ranks sharing a GPU: not by default (executor.h: work queued ahead of a
+  // rank's collective can be starved by its peers' spinning grids).
+  if (mode != kDevEnginesShared) return false;
+  // Threads of one process sharing a GPU: never (their launches may
+  // serialise).  Processes sharing a GPU: only while all their hardware
+  // queues fit what the GPU's scheduler maps at once; beyond that it
+  // time-slices the queues and every dependent step waits for a rotation
+  // (8 processes x 4 queues on one MI355X: ~170 ms per 1-element allreduce,
+  // 8 x 2: ~60 ms, 8 x 1 and 4 x 4: < 1 ms; DESIGN.md 9, profiles/r7e_*,
+  // r7g_queue_sweep.txt).
+  if (threadsShareDevice) return false;
   // each process: its hardware queues plus an allowance of one (the
   // measurements need it; 8 x 2 time-slices although 4 x 4 does not).  The
   // largest queue count any rank published, so ranks launched with
   // different GPU_MAX_HW_QUEUES still choose alike.
-  return ctx.maxRanksPerDevice() * (ctx.maxHwQueues() + 1) <= kSharedQueueBudget;
+  return ranksPerDevice * (std::max(1, maxQueues) + 1) <= kSharedQueueBudget;
+}
+
+bool HipPlanExecutor::deviceEnginesAvailable(const Context& ctx) {
+  return deviceEnginesRule(g_device_engines.load(), ctx.size, ctx.maxRanksPerDevice(),
+                           ctx.ranksShareDevice(), ctx.maxHwQueues());
 }
 
 // The inputs are the same on every rank, so every rank makes the same choice
@@ -266,11 +285,12 @@ void HipPlanExecutor::setupOneShot() {
   ddSlot_ = ((size_t)count_ * esize_ + 255) & ~(size_t)255;
   ddAlloc((size_t)P * ddSlot_);
   ddAlloc((size_t)P * ddSlot_);
-  // the flag rows, then the launch count on lines of its own (kernels.h)
+  // the flag rows, then the launch counters on lines of their own (kernels.h)
   const size_t rows = (size_t)P * (size_t)p.G * glx::kFlagBytes;
-  char* flags = ddAlloc(rows + 2 * glx::kFlagBytes);
+  char* flags = ddAlloc(rows + glx::kLaunchCtrLines * glx::kFlagBytes);
   p.flagIn = reinterpret_cast<const uint64_t*>(flags);
   p.epochCtr = reinterpret_cast<uint64_t*>(flags + rows);
+  launchCtr_ = p.epochCtr;
 }
 
 void HipPlanExecutor::setupTwoShot() {
@@ -297,12 +317,13 @@ void HipPlanExecutor::setupTwoShot() {
   }
   ddSlot_ = ((size_t)d.maxLen * esize_ + 16 + 255) & ~(size_t)255;
   for (int k = 0; k < 4; k++) ddAlloc((size_t)P * ddSlot_);  // RS 0/1, AG 0/1
-  // the A and B flag rows, then the launch count on lines of its own
+  // the A and B flag rows, then the launch counters on lines of their own
   const size_t rows = 2 * (size_t)P * (size_t)p.G * glx::kFlagBytes;
-  char* flags = ddAlloc(rows + 2 * glx::kFlagBytes);
+  char* flags = ddAlloc(rows + glx::kLaunchCtrLines * glx::kFlagBytes);
   p.flagAIn = reinterpret_cast<const uint64_t*>(flags);
   p.flagBIn = reinterpret_cast<const uint64_t*>(flags) + (size_t)P * (size_t)p.G * glx::kFlagStride;
   p.epochCtr = reinterpret_cast<uint64_t*>(flags + rows);
+  launchCtr_ = p.epochCtr;
 }
 
 // The plan kernel: segments from every rank's program (plan.cc syncTable),
@@ -335,9 +356,10 @@ void HipPlanExecutor::setupDevSteps() {
   // launch may sit on different XCDs -- in memory no L2 holds, every read
   // sees the last advance without relying on the cache maintenance at
   // kernel boundaries
-  char* block = ddAlloc(rows * G * glx::kFlagBytes + 2 * glx::kFlagBytes);
+  char* block = ddAlloc(rows * G * glx::kFlagBytes + glx::kLaunchCtrLines * glx::kFlagBytes);
   runCtr_ = reinterpret_cast<uint64_t*>(block + rows * G * glx::kFlagBytes);
   pk_.runCtr = runCtr_;
+  launchCtr_ = runCtr_;
 
   pk_.trace = nullptr;
   if (devTrace()) {
@@ -510,6 +532,15 @@ void HipPlanExecutor::waitDevice(hipStream_t s) {
 void HipPlanExecutor::checkDevice() {
   if (engine_ == kEngineSteps) return;
   const int st = *reinterpret_cast<volatile int*>(ddStatus_);
+  if (st == glx::kStatusOverlap) {
+    broken_ = true;
+    const volatile uint64_t* d = reinterpret_cast<const volatile uint64_t*>(ddStatus_);
+    GLX_ENFORCE(false, "device-driven allreduce (rank ", contextRank_, "): launch ", d[2],
+                " started while launch ", d[1],
+                " of the same algorithm was still running -- its runs and graph replays "
+                "must be stream-ordered (issue them on the algorithm's stream, or make "
+                "the other stream wait for it); the algorithm is unusable now");
+  }
   if (st != 0) {
     broken_ = true;
     const int peer = (st & 255) - 1, step = (st >> 8) - 1;

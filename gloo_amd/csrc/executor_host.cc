@@ -246,12 +246,12 @@ char* takePinned(size_t* bytes) {
   return p;
 }
 
-size_t g_mirrorLimit = 0;  // glx_set_pinned_mirror_limit
+std::atomic<size_t> g_mirrorLimit{0};  // glx_set_pinned_mirror_limit
 }  // namespace
 
 namespace exec {
-size_t pinnedMirrorLimit() { return g_mirrorLimit; }
-void setPinnedMirrorLimit(size_t bytes) { g_mirrorLimit = bytes; }
+size_t pinnedMirrorLimit() { return g_mirrorLimit.load(); }
+void setPinnedMirrorLimit(size_t bytes) { g_mirrorLimit.store(bytes); }
 }  // namespace exec
 
 void HipPlanExecutor::givePinned(char* p, size_t bytes) {

@@ -60,6 +60,13 @@ constexpr int kFlagStride = 16;
 // (1) only completes the stores (s_waitcnt vmcnt(0)) before a flag and
 // invalidates the CU's L1 after a wait (agent scope).
 constexpr size_t kFlagBytes = kFlagStride * sizeof(uint64_t);
+// A device engine's launch counters (xgmi_kernels.hip launch_number): three
+// uncached lines after its flag rows -- launches completed, workgroups
+// finished in the current launch, workgroups ever started.
+constexpr int kLaunchCtrLines = 3;
+// status code of a launch that started while the previous launch of the same
+// algorithm was still running (words 1, 2: launches completed, its number)
+constexpr int kStatusOverlap = 0x7fff0000;
 struct OneShotParams {
   char* buf;                        // this rank's buffer: input and result
   // by the epoch's parity (the two slot sets alternate between launches):
@@ -72,10 +79,9 @@ struct OneShotParams {
   int flagStore;                    // 1: write peers' flags with stores (Context::flagStores)
   int narrow;                       // 1: narrow release / acquire around flags (below)
   uint64_t epoch;                   // host's count of its launches (diagnostics only)
-  // uncached device memory: [0] launches completed; the launch's epoch is
-  // that + 1 (>= 1, +1 per launch, equal on all ranks), advanced by the last
-  // workgroup to finish ([kFlagStride] counts them) -- graph-capturable, as
-  // PlanKernelParams::runCtr
+  // uncached device memory, kLaunchCtrLines lines: the launch's epoch is its
+  // launch number + 1 (>= 1, +1 per launch, equal on all ranks) --
+  // graph-capturable, as PlanKernelParams::runCtr
   uint64_t* epochCtr;
   uint64_t timeoutTicks;            // s_memrealtime ticks
   size_t count;                     // elements
@@ -169,11 +175,13 @@ struct PlanKernelParams {
   int slots;                   // landing slots per channel (1 or 2, plan.h SyncTable)
   int maxSrc;                  // most sources of a FOLD step (2 when there is none)
   uint64_t run;                // host's count of its launches (diagnostics only)
-  // uncached device memory, per algorithm: [0] runs completed, read by every
-  // workgroup at the start of a launch and advanced by the last workgroup to
-  // finish it ([kFlagStride] counts them) -- so the message numbers follow
-  // the launches the GPU actually ran, and a launch captured in a graph and
-  // replayed numbers its messages like an eager one
+  // uncached device memory, per algorithm, kLaunchCtrLines lines: [0] runs
+  // completed, advanced by the last workgroup to finish a launch; the launch's
+  // run number is the workgroups started before it / G -- so the message
+  // numbers follow the launches the GPU actually ran, a launch captured in a
+  // graph and replayed numbers its messages like an eager one, and a launch
+  // overlapping the previous one reports kStatusOverlap (xgmi_kernels.hip
+  // launch_number)
   uint64_t* runCtr;
   uint64_t timeoutTicks;
   int* status;

@@ -460,19 +460,35 @@ __device__ __forceinline__ bool wait_flag(const uint64_t* word, uint64_t epoch, 
 
 // ---- launch counts kept on the device ------------------------------------------
 
-// The launches of this algorithm completed before this one (an uncached
-// counter: the workgroup advancing it and those reading it next may sit on
-// different XCDs, whose L2s are not coherent).  Every workgroup reads it at
-// its start; finish_launch advances it once the last one is done -- so the
-// numbers a launch uses come from the GPU, and a captured launch replays
-// correctly.
-__device__ __forceinline__ uint64_t launches_done(const uint64_t* ctr) {
+// The launch's number: launches of this algorithm before it.  Three uncached
+// counters on lines of their own (the workgroup advancing one and those
+// reading it next may sit on different XCDs, whose L2s are not coherent):
+// ctr[0] launches completed, advanced by finish_launch once the last
+// workgroup is done; ctr[kFlagStride] workgroups finished in the current
+// launch; ctr[2 kFlagStride] workgroups ever started.  Each workgroup counts
+// itself in at its start, so its launch number is (starts before it) / G and
+// the numbers a launch uses come from the GPU: a captured launch replays
+// correctly.  Launches of one algorithm must not overlap (a graph replayed
+// on another stream than eager runs): every launch's workgroups
+// start after the previous launch completed, so the completed count then
+// equals the launch number; a workgroup that sees fewer completions reports
+// kStatusOverlap and its launch does nothing more (returns false).
+__device__ __forceinline__ bool launch_number(uint64_t* ctr, int G, int* status, int* claim,
+                                              uint64_t* number) {
   __shared__ uint64_t s_n;
+  __shared__ int s_in_order;
   if (threadIdx.x == 0) {
-    s_n = __hip_atomic_load(const_cast<uint64_t*>(ctr), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t started = __hip_atomic_fetch_add(ctr + 2 * kFlagStride, (uint64_t)1,
+                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t n = started / (uint64_t)G;
+    const uint64_t done = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_n = n;
+    s_in_order = done == n ? 1 : 0;
+    if (done != n) report_timeout(status, claim, kStatusOverlap, done, n);
   }
   __syncthreads();
-  return s_n;
+  *number = s_n;
+  return s_in_order != 0;
 }
 
 __device__ __forceinline__ void finish_launch(uint64_t* ctr, int G) {
@@ -499,7 +515,9 @@ __device__ __forceinline__ void oneshot_body(const OneShotParams& p) {
   const size_t e1 = e0 + p.slice < p.count ? e0 + p.slice : p.count;
   S* buf = reinterpret_cast<S*>(p.buf);
   const bool aligned = ((uintptr_t)p.buf % 16) == 0;
-  const uint64_t epoch = launches_done(p.epochCtr) + 1;
+  uint64_t launched;
+  if (!launch_number(p.epochCtr, p.G, p.status, p.claim, &launched)) return;
+  const uint64_t epoch = launched + 1;
   const int par = (int)(epoch & 1);
 
   // 1. push (peers in ring order from rank+1)
@@ -563,7 +581,9 @@ __device__ __forceinline__ void twoshot_body(const TwoShotParams& p) {
   stamp(0);
   S* buf = reinterpret_cast<S*>(p.buf);
   const bool aligned = ((uintptr_t)p.buf % 16) == 0;
-  const uint64_t epoch = launches_done(p.epochCtr) + 1;
+  uint64_t launched;
+  if (!launch_number(p.epochCtr, p.G, p.status, p.claim, &launched)) return;
+  const uint64_t epoch = launched + 1;
   const int par = (int)(epoch & 1);
   auto span = [&](int c, size_t& a, size_t& b) {  // slice w of range c
     const size_t off = p.rangeOff[c], len = p.rangeLen[c];
@@ -677,7 +697,8 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
   // message m of a channel lands in slot (m - 1) % slots
   auto slotOf = [&](uint64_t m) -> uint64_t { return p.slots == 2 ? ((m - 1) & 1) : 0; };
   // the runs completed before this launch (kernels.h PlanKernelParams::runCtr)
-  const uint64_t run = launches_done(p.runCtr);
+  uint64_t run;
+  if (!launch_number(p.runCtr, p.G, p.status, p.claim, &run)) return;
   for (int i = 0; i < p.nsteps; i++) {
     const DevStep st = p.steps[i];
     const uint64_t seq = run * st.perRun + st.seq;

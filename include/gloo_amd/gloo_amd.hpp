@@ -315,8 +315,10 @@ class DeviceAllreduce : public Algorithm {
 enum class Schedule { RING, MESH, REPLICATED, AUTO };
 
 // Engine knobs for algorithms created afterwards (process-wide; every rank
-// must set them alike).  mode: -1 automatic, 0 never, 1 always.
+// must set them alike).  mode: GLX_DEVICE_ENGINES_AUTO (one rank per GPU),
+// _OFF, _ON, _SHARED (also processes sharing a GPU within the queue budget).
 inline void setDeviceEngines(int mode) { check(glx_set_device_engines(mode), "setDeviceEngines"); }
+inline int deviceEngines() { return glx_get_device_engines(); }
 // GLX_ENGINE_TWOSHOT (default) or GLX_ENGINE_STEPS for the MESH schedule.
 inline void setMeshEngine(int engine) { check(glx_set_mesh_engine(engine), "setMeshEngine"); }
 // GLX_ENGINE_DEVSTEPS (default) or GLX_ENGINE_STEPS for RING,

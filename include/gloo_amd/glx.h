@@ -153,13 +153,34 @@ int glx_set_copy_engine(int engine, int blocks);
  * device-driven kernel per rank, default) or GLX_ENGINE_STEPS (host-issued
  * copies and fold kernels). */
 int glx_set_mesh_engine(int engine);
-/* Device-driven engines for algorithms created afterwards: 0 = never (every
- * schedule runs as host-issued steps), 1 = always (the caller guarantees the
- * ranks' kernels can run concurrently), -1 = automatic (default: one rank
- * per GPU always; processes sharing a GPU while ranks x (queues + 1) <= 20,
- * queues = the largest GPU_MAX_HW_QUEUES any rank published; never threads
- * sharing one device). */
+/* Device-driven engines for algorithms created afterwards (initially from
+ * GLOO_AMD_DEVICE_ENGINES=auto|off|on|shared):
+ *   GLX_DEVICE_ENGINES_AUTO (default): when every rank has a GPU of its own.
+ *     Ranks sharing a GPU run host-issued steps: their device engines wait
+ *     for each other while holding the GPU's CUs, so other work queued ahead
+ *     of one rank's collective can be starved until the timeout.
+ *   GLX_DEVICE_ENGINES_SHARED: also processes sharing a GPU while
+ *     ranks x (queues + 1) <= 20, queues = the largest GPU_MAX_HW_QUEUES any
+ *     rank published (never threads sharing one device) -- for callers that
+ *     queue no other GPU work ahead of a collective on the shared GPU.
+ *   GLX_DEVICE_ENGINES_ON: always (the caller guarantees the ranks' kernels
+ *     run concurrently).  GLX_DEVICE_ENGINES_OFF: never.
+ * Every rank must use the same mode (a mismatch fails at the first run with
+ * "schedules disagree"). */
+#define GLX_DEVICE_ENGINES_AUTO (-1)
+#define GLX_DEVICE_ENGINES_OFF 0
+#define GLX_DEVICE_ENGINES_ON 1
+#define GLX_DEVICE_ENGINES_SHARED 2
 int glx_set_device_engines(int mode);
+/* The current mode (GLX_DEVICE_ENGINES_*). */
+int glx_get_device_engines(void);
+/* The rule glx_set_device_engines' modes apply, for `ranks` ranks of which
+ * at most `ranks_per_device` share one GPU (`threads_share_device`: two
+ * ranks of one process on one GPU), with the largest GPU_MAX_HW_QUEUES any
+ * rank's process uses: 1 = device engines, 0 = host-issued steps, -1 =
+ * invalid argument.  No GPU needed. */
+int glx_device_engines_rule(int mode, int ranks, int ranks_per_device, int threads_share_device,
+                            int max_hw_queues);
 /* Engine of the ring, halving-doubling, bcube and function-style ring
  * schedules for algorithms created afterwards, when device-driven engines
  * are available: -1 = automatic (default: the plan kernel -- at every size
@@ -516,7 +537,10 @@ int64_t glx_device_layout(int algo, int rank, int size, int64_t count, int esize
  * the SEND after a REDUCE / COPY overlaps its range without equalling it: the
  * REDUCE / COPY names the SEND and stores the overlap's segments [pre0, pre1)
  * into its slot, the SEND names the step and stores only its other segments;
- * -1 / 0 / 0 otherwise, plan.h StepSync).  Returns the number of steps or -1. */
+ * -1 / 0 / 0 otherwise, plan.h StepSync).  `cap` counts int64 slots of
+ * `steps` (GLX_PLAN_SYNC_WIDTH per step; a step is written only if it fits
+ * whole).  Returns the number of steps or -1. */
+#define GLX_PLAN_SYNC_WIDTH 12
 int64_t glx_plan_sync(int algo, int rank, int size, int64_t count, int esize,
                       int64_t max_segment_bytes, int64_t min_piece_bytes, int G,
                       int64_t* bounds, int64_t bounds_cap, int64_t* nbounds, int64_t* info,

@@ -17,6 +17,9 @@ os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
     config.addinivalue_line("markers", "slow: long-running case")
+    config.addinivalue_line("markers", "widening: GPU tests of code outside the SURVEY 8 "
+                            "contract (AllreduceRing / AllreduceBcube / AllreduceLocal); "
+                            "not part of -m gpu")
 
 
 def _have_gpu():
@@ -32,5 +35,5 @@ def pytest_collection_modifyitems(config, items):
         return
     skip = pytest.mark.skip(reason="no GPU in this environment")
     for item in items:
-        if "gpu" in item.keywords:
+        if "gpu" in item.keywords or "widening" in item.keywords:
             item.add_marker(skip)

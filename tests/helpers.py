@@ -200,15 +200,23 @@ def run_ranks(P, fn, timeout=120):
     return results
 
 
-def rank_env(P):
-    """Environment of P rank processes sharing the box's one GPU.  Device
+def rank_env(P, device_engines="shared"):
+    """Environment of P rank processes sharing the box's one GPU: a
+    rehearsal of the node's one-process-per-GPU run.  By default the ranks
+    opt in to the device engines on the shared GPU (GLOO_AMD_DEVICE_ENGINES=
+    shared: the tests queue no other GPU work ahead of a collective), which
+    the library's automatic mode gives only to ranks with a GPU of their own
+    (DESIGN.md 5a, 9); device_engines=None keeps the automatic mode.  Device
     engines need every rank's kernel running at once; the GPU's scheduler
     maps a bounded number of hardware queues and time-slices the rest, so
-    above 4 ranks each process keeps to one queue (the product's default
-    budget, HipPlanExecutor::kSharedQueueBudget: ranks x (queues + 1) <= 20;
-    8 ranks x 2 queues measured time-sliced, profiles/r7g_queue_sweep.txt)."""
+    above 4 ranks each process keeps to one queue (the shared mode's budget,
+    HipPlanExecutor::kSharedQueueBudget: ranks x (queues + 1) <= 20; 8 ranks
+    x 2 queues measured time-sliced, profiles/r7g_queue_sweep.txt)."""
     import os
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("GLOO_AMD_DEVICE_ENGINES", None)
+    if device_engines is not None:
+        env["GLOO_AMD_DEVICE_ENGINES"] = device_engines
     if P > 4:
         env["GPU_MAX_HW_QUEUES"] = "1"
     return env

@@ -74,6 +74,8 @@ def main():
         return run_big(store_dir, rank, size, algo[len("big:"):])
     if algo == "linkprobe":
         return run_linkprobe(store_dir, rank, size)
+    if algo.startswith("graph_overlap:"):
+        return run_graph_overlap(store_dir, rank, size, algo.split(":")[1])
     if algo == "engine_choice":
         return run_engine_choice(store_dir, rank, size)
     if algo.startswith("fn_"):
@@ -764,6 +766,83 @@ def run_graph(store_dir, rank, size, replays):
     print("OK")
 
 
+def run_graph_overlap(store_dir, rank, size, kind):
+    """launches of one algorithm must not overlap -- a
+    graph captured on the algorithm's stream but replayed on another stream
+    while an eager run is still in flight would take the same run number /
+    epoch and share landing slots.  The kernels now detect it
+    (xgmi_kernels.hip launch_number): rank 0 starts an eager run that waits
+    for rank 1 (which starts its own 0.5 s later) and replays the captured
+    run on a second stream meanwhile; one of the two launches must report
+    the overlap, and rank 0's next call raises EnforceNotMet naming it.
+    Rank 1's run then either completes or times out (IoException) within
+    the context's 5 s timeout; nothing hangs."""
+    import time
+
+    import torch
+
+    import gloo_amd
+    store = gloo_amd.rendezvous.FileStore(store_dir)
+    ctx = gloo_amd.rendezvous.Context(rank, size, 0)
+    ctx.setTimeout(5)
+    ctx.connectFullMesh(store)
+    n = 1 << 16
+    dev = torch.device("cuda:0")
+    # s2 at another priority: a hardware queue of its own, so the replay can
+    # run beside the eager launch instead of queueing behind it
+    s, s2 = torch.cuda.Stream(), torch.cuda.Stream(priority=-1)
+    buf = torch.full((n,), float(rank + 1), device=dev)
+    sched = {"ring": "ring", "mesh": "mesh", "repl": "replicated"}[kind]
+    alg = gloo_amd.AllreduceRingChunked(ctx, [buf], streams=[s], schedule=sched)
+    engine = alg.engine()
+    torch.cuda.synchronize()
+    alg.run()  # eager run 0 on every rank: resolves the peers
+    s.synchronize()
+    ok0 = bool((buf == size * (size + 1) / 2).all().item())
+    verdict = "none"
+    if rank == 0:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=s):
+            alg.run()
+        store.set("overlap/go", b"1")
+        alg.run()  # eager run 1 on s: waits for rank 1
+        with torch.cuda.stream(s2):
+            graph.replay()  # NOT ordered after the eager run
+        s.synchronize()
+        s2.synchronize()
+        try:
+            alg.run()
+            s.synchronize()
+            alg.run()
+            s.synchronize()
+            verdict = "no error"
+        except gloo_amd.EnforceNotMet as e:
+            verdict = "overlap" if "still running" in str(e) else "enforce: " + str(e)[:200]
+        except gloo_amd.IoException as e:
+            verdict = "io: " + str(e)[:200]
+        del graph
+    else:
+        store.get("overlap/go", timeout_ms=60000)
+        time.sleep(0.5)
+        try:
+            alg.run()
+            s.synchronize()
+            verdict = "completed"
+        except gloo_amd.IoException:
+            verdict = "timed out"
+    print("VERDICT rank %d %s engine %s first %s" % (rank, verdict, engine, ok0), flush=True)
+    try:
+        alg.close()
+    except gloo_amd.Exception:
+        pass
+    store.set("overlap/done/%d" % rank, b"1")
+    for r in range(size):
+        store.get("overlap/done/%d" % r, timeout_ms=60000)
+    if not ok0 or (rank == 0 and verdict != "overlap"):
+        sys.exit(1)
+    print("OK")
+
+
 def run_soak(store_dir, rank, size, runs, uneven=""):
     """One instance of each device engine's algorithm run `runs` times back to
     back (a training job's shape: the run counter, the message numbers
@@ -778,11 +857,13 @@ def run_soak(store_dir, rank, size, runs, uneven=""):
     every hand-off under UNEVEN load"): "delays" -- every rank starts each
     run after a random delay of up to 2 ms, so workgroups arrive at their
     flags at different times; "uneven" -- also a GEMM stream busy on rank 0's
-    GPU beside the collective, so some CUs are taken.  The GEMM variant needs
-    two hardware queues per process: with one (8 ranks sharing the GPU) the
-    GEMM sits ahead of the collective in rank 0's only queue while the other
+    GPU beside the collective, so some CUs are taken.  On the device engines
+    (the rehearsal's opt-in, GLOO_AMD_DEVICE_ENGINES=shared) this needs two
+    hardware queues per process: with one (8 ranks sharing the GPU) the GEMM
+    sits ahead of the collective in rank 0's only queue while the other
     ranks' collectives hold the CUs waiting for rank 0 -- a cycle that exists
-    only when ranks share a GPU."""
+    only when ranks share a GPU, which is why the automatic choice keeps such
+    ranks on host-issued steps."""
     import random
     import time
 

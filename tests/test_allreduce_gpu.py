@@ -13,8 +13,7 @@ import time
 import numpy as np
 import pytest
 
-from helpers import (case_inputs, check_against_golden, check_ring_against_golden,
-                     load_allreduce_golden, load_ring_golden, rank_env, run_ranks)
+from helpers import case_inputs, check_against_golden, load_allreduce_golden, rank_env, run_ranks
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -127,112 +126,6 @@ def test_reference_test_grid_single_pointer(algo, P, N):
     out = gpu_allreduce(algo, O.SUM, O.FLOAT32, ins, runs=2)
     for r in range(P):
         assert np.all(out[r][0] == P * (P - 1) // 2), "rank %d" % r
-
-
-# gloo::AllreduceRing<T> (gloo/allreduce_ring.h): every rank's own result
-# against the compiled reference's per-rank outputs (float results differ
-# between ranks, tests/golden/allreduce_ring_golden.json), the reference
-# test's grid (allreduce_test.cc:241-249, P = 1..15), dtypes x ops, several
-# pointers with streams.
-RING_INDEX, RING_DATA = load_ring_golden()
-
-
-@pytest.mark.parametrize("rec", RING_INDEX, ids=[r["name"] for r in RING_INDEX])
-def test_allreduce_ring_vs_reference_golden(rec):
-    ins = case_inputs(rec["P"], rec["N"], rec["dtype"], rec["nptrs"], rec["kind"], rec["seed"])
-    out = gpu_allreduce(O.RING, rec["op"], rec["dtype"], ins, runs=2)
-    check_ring_against_golden(rec, RING_DATA, out)
-
-
-@pytest.mark.parametrize("P", list(range(1, 16)))
-@pytest.mark.parametrize("N", [0, 4, 100, 1000, 10000])
-def test_allreduce_ring_reference_test_grid(P, N):
-    ins = [[np.full(N, r, dtype=np.float32)] for r in range(P)]
-    out = gpu_allreduce(O.RING, O.SUM, O.FLOAT32, ins, runs=2)
-    for r in range(P):
-        assert np.all(out[r][0] == P * (P - 1) // 2), "rank %d" % r
-
-
-@pytest.mark.parametrize("dtype", [O.INT8, O.INT32, O.INT64, O.UINT64, O.FLOAT64, O.FLOAT16,
-                                   O.BFLOAT16], ids=lambda d: O.DTYPE_NAMES[d])
-@pytest.mark.parametrize("op", [O.SUM, O.PRODUCT, O.MAX, O.MIN],
-                         ids=lambda o: O.OP_NAMES[o])
-def test_allreduce_ring_dtypes_ops(dtype, op):
-    ins = case_inputs(4, 4099, dtype, 1, 0, seed=33)
-    out = gpu_allreduce(O.RING, op, dtype, ins)
-    check_all(out, O.allreduce(O.RING, op, dtype, ins), dtype, op)
-
-
-@pytest.mark.parametrize("P,nptrs", [(1, 3), (3, 2), (5, 2)])
-def test_allreduce_ring_multi_pointer_streams(P, nptrs):
-    ins = case_inputs(P, 100003, O.FLOAT32, nptrs, 0, seed=34)
-    out = gpu_allreduce(O.RING, O.SUM, O.FLOAT32, ins, runs=2, streams=True)
-    check_all(out, O.allreduce(O.RING, O.SUM, O.FLOAT32, ins), O.FLOAT32, O.SUM)
-
-
-# gloo::AllreduceBcube<T> (gloo/allreduce_bcube.h): groups of the context's
-# base ranks; the reference's per-rank outputs, its test grid (allreduce_
-# test.cc:271-299), dtypes x ops.
-BCUBE_INDEX, BCUBE_DATA = load_ring_golden("bcube")
-
-
-@pytest.mark.parametrize("rec", BCUBE_INDEX, ids=[r["name"] for r in BCUBE_INDEX])
-def test_allreduce_bcube_vs_reference_golden(rec):
-    ins = case_inputs(rec["P"], rec["N"], rec["dtype"], rec["nptrs"], rec["kind"], rec["seed"])
-    out = gpu_allreduce(O.BCUBE, rec["op"], rec["dtype"], ins, runs=2, base=rec["base"])
-    check_ring_against_golden(rec, BCUBE_DATA, out)
-
-
-BCUBE_REF_GRID = ([(2, P) for P in (1, 2, 4, 8, 16)] + [(3, P) for P in (1, 3, 9, 27)] +
-                  [(4, P) for P in (1, 4, 16)])
-
-
-@pytest.mark.parametrize("base,P", BCUBE_REF_GRID, ids=["b%d-P%d" % g for g in BCUBE_REF_GRID])
-@pytest.mark.parametrize("N", [0, 1, 64, 1000])
-def test_allreduce_bcube_reference_test_grid(base, P, N):
-    ins = [[np.full(N, r, dtype=np.float32)] for r in range(P)]
-    out = gpu_allreduce(O.BCUBE, O.SUM, O.FLOAT32, ins, runs=2, base=base)
-    for r in range(P):
-        assert np.all(out[r][0] == P * (P - 1) // 2), "rank %d" % r
-
-
-@pytest.mark.parametrize("dtype", [O.INT8, O.INT64, O.FLOAT64, O.FLOAT16, O.BFLOAT16],
-                         ids=lambda d: O.DTYPE_NAMES[d])
-@pytest.mark.parametrize("op", [O.SUM, O.PRODUCT, O.MAX, O.MIN],
-                         ids=lambda o: O.OP_NAMES[o])
-def test_allreduce_bcube_dtypes_ops(dtype, op):
-    ins = case_inputs(6, 4099, dtype, 1, 0, seed=35)
-    out = gpu_allreduce(O.BCUBE, op, dtype, ins, base=3)
-    check_all(out, O.allreduce(O.BCUBE, op, dtype, ins, base=3), dtype, op)
-
-
-@pytest.mark.parametrize("P,nptrs", [(1, 1), (1, 3), (3, 2), (4, 4)])
-@pytest.mark.parametrize("dtype,op", [(O.FLOAT32, O.SUM), (O.FLOAT16, O.SUM), (O.INT32, O.MAX)],
-                         ids=str)
-def test_allreduce_local(P, nptrs, dtype, op):
-    """gloo::AllreduceLocal<T> (gloo/allreduce_local.cc:21-31): each rank's
-    own pointers folded and broadcast; ranks do not exchange anything."""
-    import gloo_amd
-    ins = case_inputs(P, 100003, dtype, nptrs, 0, seed=36)
-    store = gloo_amd.rendezvous.HashStore()
-    bufs = [[to_dev(x, dtype) for x in row] for row in ins]
-    torch.cuda.synchronize()
-
-    def rank_fn(r):
-        ctx = gloo_amd.rendezvous.Context(r, P, 0)
-        ctx.connectFullMesh(store)
-        alg = gloo_amd.AllreduceLocal(ctx, [b.data_ptr() for b in bufs[r]], 100003,
-                                      gloo_amd.ReductionFunction(op), dtype=dtype)
-        alg.run()
-        alg.close()
-        return True
-
-    run_ranks(P, rank_fn, timeout=90)
-    torch.cuda.synchronize()
-    for r in range(P):
-        exp = O.allreduce(O.RING_CHUNKED, op, dtype, [ins[r]])[0]  # one rank's fold
-        for i in range(nptrs):
-            assert_same(from_dev(bufs[r][i], dtype), exp[i], dtype, op)
 
 
 # The CUDA algorithms' test grid (gloo/test/cuda_allreduce_test.cc:148-170,
@@ -880,16 +773,21 @@ def test_multidev_check_script_on_one_device():
     assert d["ok"] is True and len(d["cases"]) == 6, d
 
 
-@pytest.mark.parametrize("P,queues,engine", [(8, "4", "steps"), (8, "1", "devsteps"),
-                                             (4, "4", "devsteps")])
-def test_device_engines_respect_the_shared_gpu_queue_budget(P, queues, engine):
-    """Processes sharing one GPU get the device engines only while ranks x
+@pytest.mark.parametrize("P,queues,mode,engine", [
+    (8, "4", "shared", "steps"), (8, "1", "shared", "devsteps"), (4, "4", "shared", "devsteps"),
+    (8, "1", None, "steps"), (4, "2", None, "steps")])
+def test_device_engines_respect_the_shared_gpu_queue_budget(P, queues, mode, engine):
+    """Processes sharing one GPU get the device engines only when they opt in
+    (GLOO_AMD_DEVICE_ENGINES=shared) and only while ranks x
     (GPU_MAX_HW_QUEUES + 1) <= 20 (beyond the GPU's 24 user
     queues the scheduler time-slices them and every dependent step waits for
-    a rotation).  8 x 4 must fall back to host-issued steps; 8 x 1 and 4 x 4
-    keep the plan kernel; every rank agrees and the result is exact."""
+    a rotation).  Shared mode: 8 x 4 falls back to host-issued steps, 8 x 1
+    and 4 x 4 keep the plan kernel.  The automatic mode (None) keeps ranks
+    sharing a GPU on host-issued steps whatever the queue count (8 x 1 is
+    the configuration that starved a GEMM, profiles/r9j_*, r9l_*).  Every
+    rank agrees and the result is exact."""
     with tempfile.TemporaryDirectory() as d:
-        env = dict(rank_env(P), GPU_MAX_HW_QUEUES=queues)
+        env = dict(rank_env(P, device_engines=mode), GPU_MAX_HW_QUEUES=queues)
         procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), "engine_choice"],
                                   env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
                  for r in range(P)]

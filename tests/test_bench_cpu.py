@@ -1,6 +1,7 @@
 """bench.py's host-side logic on CPU: the per-candidate result check (a
 world_size-2 gloo process group, as the N>1 bench runs it), candidate
 naming, and the algorithmic byte counts the roofline fields are built from."""
+import json
 import os
 import socket
 import sys
@@ -313,3 +314,117 @@ def test_live_pmc_traffic_off_and_failure_paths(monkeypatch):
     import shutil
     monkeypatch.setattr(shutil, "which", lambda name: None)
     assert bench.live_pmc_traffic(A) is None
+
+
+# ---------------------------------------------------------------------------
+# The N > 1 line's claims: what a rehearsal and a
+# degraded node transport may say.
+# ---------------------------------------------------------------------------
+def _stats(peer=0, device=0, kernel=0, kernels=0, nbytes=0):
+    return {"peer_copies": peer, "device_copies": device, "kernel_copies": kernel,
+            "device_kernels": kernels, "bytes": nbytes, "host_folds": 0, "done_events": 0}
+
+
+def _line(world=8):
+    """The N > 1 line's north-star and roofline parts, as bench_multi builds
+    them, for a healthy-looking 3.5 ms plan-kernel ring and a 3.3 ms DMA ring."""
+    S = 256 << 20
+    links = {"ring_dma_GBps": 140.0, "ring_kernel_GBps": 120.0}
+    runs = {"ring_chunked": _ring_run(3.5e-3, "devsteps", ("dma", 1, 0)),
+            "ring_chunked_host": _ring_run(3.3e-3, "steps", ("dma", 1, 0))}
+    ns = bench.north_star_section(S, world, runs, links,
+                                  {"ring_chunked": True, "ring_chunked_host": True}, {})
+    return {"value": S / 3.3e-3 / 1e9, "north_star": ns,
+            "roofline": {"frac": 0.93, "link_measured": dict(links, frac=0.97)}}
+
+
+def _node_stats(host_stats):
+    return {"ring_chunked": _stats(kernels=24, nbytes=7 << 28),
+            "ring_chunked_mesh": _stats(kernels=24, nbytes=7 << 28),
+            "ring_chunked_host": host_stats,
+            "ring_chunked_mesh_steps": _stats(peer=14 * 24, nbytes=7 << 28)}
+
+
+def _meets(res):
+    ns = res["north_star"]
+    return [b.get("meets_target") for b in [ns] + list(ns["rings"].values())]
+
+
+def _infos(world, **kw):
+    return [[_info(False, **kw) for _ in range(world - 1)] for _ in range(world)]
+
+
+def test_node_line_healthy_transport_keeps_its_claims():
+    """8 ranks on 8 distinct GPUs, every DMA candidate made peer copies,
+    native atomics everywhere: no error, the north-star verdict stands."""
+    world = 8
+    health, err = bench.transport_health(
+        _infos(world), [_node_stats(_stats(peer=28 * 24, nbytes=7 << 28))] * world)
+    res = bench.apply_transport_verdict(_line(world), health, err)
+    assert err is None and "error" not in res and "rehearsal" not in res
+    assert all(m is True for m in _meets(res))
+    assert res["roofline"]["frac"] == 0.93
+    assert res["north_star"]["link_frac"] is not None
+
+
+@pytest.mark.parametrize("case", ["device_copies", "no_atomics", "no_peer_copies", "no_access"])
+def test_node_line_degraded_transport_carries_an_error_and_no_verdict(case):
+    """a synthetic 8-distinct-GPU record whose transport is
+    degraded -- a hipMemcpyAsync fallback in the DMA ring, a link without
+    native atomics, a DMA ring that made no peer copies, a peer GPU that
+    cannot be accessed -- puts an error in the line and never a
+    meets_target."""
+    world = 8
+    host = _stats(peer=28 * 24, nbytes=7 << 28)
+    kw = {}
+    if case == "device_copies":
+        host = _stats(peer=20, device=8, nbytes=7 << 28)
+    elif case == "no_peer_copies":
+        host = _stats(nbytes=7 << 28)
+    elif case == "no_atomics":
+        kw = {"atomics": False, "stores": True}
+    else:
+        kw = {"access": False}
+    stats = [_node_stats(_stats(peer=28 * 24, nbytes=7 << 28))] * (world - 1) + [_node_stats(host)]
+    health, err = bench.transport_health(_infos(world, **kw), stats)
+    assert health["ranks_on_distinct_gpus"] and err is not None
+    res = bench.apply_transport_verdict(_line(world), health, err)
+    assert res["error"] == err
+    assert all(m is None for m in _meets(res)), _meets(res)
+    assert res["north_star"]["error"] == err
+    line = json.loads(json.dumps(res))
+    assert "meets_target\": true" not in json.dumps(line)
+
+
+def test_rehearsal_line_makes_no_link_claims():
+    """ranks sharing one GPU moved no byte over a link, so
+    link_frac, meets_target, measured_link_frac and roofline.frac are null
+    and the line says it is a rehearsal (the shared-GPU copies are not an
+    error)."""
+    world = 8
+    same = [[_info(True) for _ in range(world - 1)] for _ in range(world)]
+    health, err = bench.transport_health(
+        same, [_node_stats(_stats(device=28 * 24, nbytes=7 << 28))] * world)
+    assert err is None and not health["ranks_on_distinct_gpus"]
+    res = bench.apply_transport_verdict(_line(world), health, err)
+    assert res["rehearsal"] == bench.REHEARSAL_NOTE
+    assert res["roofline"]["frac"] is None and res["roofline"]["link_measured"]["frac"] is None
+    for b in [res["north_star"]] + list(res["north_star"]["rings"].values()):
+        for k in bench.LINK_CLAIMS:
+            assert b[k] is None, (k, b)
+    assert res["value"] > 0  # the measured time itself stands
+
+
+def test_multi_line_value_is_algbw_and_workload_names_the_schedule():
+    """value = algbw = S / t (SURVEY 8d, gloo/benchmark/runner.cc:488-496);
+    the mesh headline is named as such in config.workload."""
+    import inspect
+    src = inspect.getsource(bench.bench_multi)
+    assert '"value": round(algbw, 3)' in src and "world * S / t" in src  # aggregate kept aside
+    assert '"aggregate_GBps"' in src
+    assert bench.multi_workload("ring_chunked", "ring_chunked", "f32", 256) == \
+        "allreduce_ring_chunked_fp32_256MiB_per_rank"
+    assert bench.multi_workload("ring_chunked", "ring_chunked_mesh", "f32", 256) == \
+        "allreduce_ring_chunked_mesh_schedule_fp32_256MiB_per_rank"
+    assert bench.multi_workload("halving_doubling", "halving_doubling", "f16", 1024) == \
+        "allreduce_halving_doubling_f16_1024MiB_per_rank"

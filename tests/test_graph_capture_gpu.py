@@ -41,3 +41,33 @@ def test_device_engine_graph_replays(P):
     eng = [l for l in outs[0].splitlines() if l.startswith("ENGINES")][0]
     assert "'ring': 'devsteps'" in eng and "'hd': 'devsteps'" in eng, eng
     assert "'mesh': 'twoshot'" in eng and "'repl': 'oneshot'" in eng, eng
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,engine", [("ring", "devsteps"), ("mesh", "twoshot"),
+                                         ("repl", "oneshot")])
+def test_graph_replay_overlapping_an_eager_run_is_reported(kind, engine):
+    """a replay on a stream that is not ordered after the
+    algorithm's eager runs overlaps them; the device engine's launch counters
+    detect it (xgmi_kernels.hip launch_number) and rank 0's next call raises
+    EnforceNotMet instead of silently sharing a run number and landing slots.
+    P = 2; rank 1 either completes or times out within 5 s."""
+    P = 2
+    with tempfile.TemporaryDirectory() as d:
+        procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P),
+                                   "graph_overlap:" + kind],
+                                  env=rank_env(P), stdout=subprocess.PIPE,
+                                  stderr=subprocess.STDOUT) for r in range(P)]
+        outs = []
+        for p in procs:
+            try:
+                o, _ = p.communicate(timeout=120)
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+            outs.append(o.decode(errors="replace"))
+    every = "\n".join("---- rank %d (rc %s) ----\n%s" % (r, p.returncode, outs[r][-2500:])
+                       for r, p in enumerate(procs))
+    assert procs[0].returncode == 0 and "VERDICT rank 0 overlap engine %s" % engine in outs[0], every
+    assert procs[1].returncode == 0 and "OK" in outs[1], every

@@ -139,3 +139,84 @@ def test_library_never_registers_or_copies_caller_host_pages():
         if kind not in ("hipMemcpyHostToDevice", "hipMemcpyDeviceToHost"):
             continue
         assert re.search(r"\.dma\b|\bb\.p\b|\bsrc\b|\bout\b|outDma\[i\]", host), (host, args)
+
+
+# (ranks, ranks per GPU, threads share a GPU, largest GPU_MAX_HW_QUEUES) ->
+# device engines under (auto, shared, on, off).  8 x 1 is the configuration
+# whose collectives starved a GEMM queued ahead of one rank's collective
+# (profiles/r9j_*, r9l_*); 8 x 2 time-slices the queues
+# (profiles/r7g_queue_sweep.txt); 4 x 2 fits the queue budget.
+ENGINE_RULE = [
+    ((8, 8, False, 1), (False, True, True, False)),
+    ((8, 8, False, 2), (False, False, True, False)),
+    ((4, 4, False, 2), (False, True, True, False)),
+    ((4, 4, False, 4), (False, True, True, False)),
+    ((8, 8, False, 4), (False, False, True, False)),
+    ((4, 2, True, 4), (False, False, True, False)),   # threads of one process
+    ((8, 1, False, 4), (True, True, True, False)),    # the node: one rank per GPU
+    ((2, 1, False, 1), (True, True, True, False)),
+    ((1, 1, False, 4), (False, False, False, False)),  # nothing to exchange
+]
+
+
+@pytest.mark.parametrize("shape,expect", ENGINE_RULE)
+def test_device_engine_rule(shape, expect):
+    """The chooser every rank applies to the context's endpoints
+    (HipPlanExecutor::deviceEnginesRule via glx_device_engines_rule): the
+    automatic mode gives the device engines only to ranks with a GPU of
+    their own, whatever the queue count; the shared mode also to processes
+    sharing a GPU within ranks x (queues + 1) <= 20."""
+    ranks, per_dev, threads, queues = shape
+    got = tuple(gloo_amd.device_engines_rule(m, ranks, per_dev, threads, queues)
+                for m in ("auto", "shared", "on", "off"))
+    assert got == expect, (shape, got)
+
+
+def test_device_engine_mode_round_trip_and_rejects():
+    before = gloo_amd.get_device_engines()
+    try:
+        for m in ("shared", "on", "off", "auto"):
+            gloo_amd.set_device_engines(m)
+            assert gloo_amd.get_device_engines() == m
+    finally:
+        gloo_amd.set_device_engines(before)
+    with pytest.raises(gloo_amd.EnforceNotMet):
+        gloo_amd.errors.check(_lib.lib.glx_set_device_engines(3))
+    with pytest.raises(gloo_amd.EnforceNotMet):
+        gloo_amd.device_engines_rule("auto", 4, 5)  # more ranks on a GPU than ranks
+
+
+def test_device_engine_mode_from_environment():
+    """GLOO_AMD_DEVICE_ENGINES sets the initial mode (the rehearsal harness's
+    opt-in); unset means automatic."""
+    import subprocess
+    import sys
+    code = "import gloo_amd; print(gloo_amd.get_device_engines())"
+    for val, want in (("shared", "shared"), ("off", "off"), (None, "auto")):
+        env = dict(os.environ)
+        env.pop("GLOO_AMD_DEVICE_ENGINES", None)
+        if val is not None:
+            env["GLOO_AMD_DEVICE_ENGINES"] = val
+        out = subprocess.run([sys.executable, "-c", code], env=env, cwd=ROOT,
+                             capture_output=True, text=True, timeout=60)
+        assert out.returncode == 0, out.stderr
+        assert out.stdout.strip() == want
+
+
+def test_allreduce_options_assignment_goes_through_the_setters():
+    """allreduce() uses the pointers taken by setInputs /
+    setOutputs; assigning opts.inputs / opts.outputs must refresh them, not
+    leave the old buffers' pointers behind."""
+    import numpy as np
+    ctx = object()
+    opts = gloo_amd.AllreduceOptions(ctx)
+    a, b = np.zeros(8, np.float32), np.ones(16, np.float32)
+    opts.setOutputs([a])
+    assert opts._out_ptrs[0][0] == a.ctypes.data and opts.elements == 8
+    opts.outputs = [b]
+    assert opts._out_ptrs[0][0] == b.ctypes.data and opts.elements == 16
+    assert opts.outputs == [b] and opts.outputs is not opts._outputs
+    opts.inputs = [b.copy()]
+    assert opts._in_ptrs[1] == 1
+    opts.inputs = []
+    assert opts._in_ptrs is None and opts.inputs == []

@@ -17,20 +17,25 @@ WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "mp_worker.py"
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("P,runs,mode", [(2, 1000, ""), (4, 600, ""), (8, 300, ""),
-                                         (4, 300, ":uneven"), (8, 300, ":delays")])
-def test_device_engines_soak(P, runs, mode):
+@pytest.mark.parametrize("P,runs,mode,engines", [
+    (2, 1000, "", "shared"), (4, 600, "", "shared"), (8, 300, "", "shared"),
+    (4, 300, ":uneven", "shared"), (8, 300, ":delays", "shared"),
+    (8, 100, ":uneven", None)])
+def test_device_engines_soak(P, runs, mode, engines):
     """The guide's condition for testing hand-offs, uneven load: ":delays",
     random start delays per rank and run; ":uneven", also a GEMM stream busy
-    on rank 0's GPU beside the collective -- only where each process has two
-    hardware queues (with one, 8 ranks sharing the GPU, the GEMM ahead of
-    the collective in rank 0's only queue and the other ranks' collectives
-    holding the CUs wait on each other: a cycle only ranks sharing a GPU can
-    form; profiles/r9j_*, r9l_*)."""
+    on rank 0's GPU beside the collective.  engines: the ranks' device-engine
+    mode ("shared": the rehearsal's opt-in to the device engines on the
+    shared GPU; None: the library's automatic choice).  (8, 100, ":uneven")
+    under the automatic choice is the configuration of the round-4 timeouts
+    (8 ranks, one hardware queue each, a GEMM ahead of rank 0's collective
+    while the other ranks' device engines held the CUs, profiles/r9j_*,
+    r9l_*): the library now keeps ranks sharing a GPU on host-issued steps,
+    which hold no CUs while they wait."""
     with tempfile.TemporaryDirectory() as d:
         procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P),
                                    "soak:%d%s" % (runs, mode)],
-                                  env=rank_env(P), stdout=subprocess.PIPE,
+                                  env=rank_env(P, device_engines=engines), stdout=subprocess.PIPE,
                                   stderr=subprocess.STDOUT) for r in range(P)]
         outs = []
         for p in procs:
@@ -45,7 +50,11 @@ def test_device_engines_soak(P, runs, mode):
               if p.returncode != 0 or "OK" not in o]
     # every failing rank's output: the first to fail is often not rank 0
     assert not failed, "\n".join("rank %d rc=%d:\n%s" % (r, rc, o[-2500:]) for r, rc, o in failed)
-    # one rank per process: the device engines ran (not a host-steps fallback)
     eng = [l for l in outs[0].splitlines() if l.startswith("ENGINES")][0]
-    assert "devsteps" in eng and "twoshot" in eng and "oneshot" in eng, eng
+    if engines == "shared":
+        # one rank per process: the device engines ran (not a host-steps fallback)
+        assert "devsteps" in eng and "twoshot" in eng and "oneshot" in eng, eng
+    else:
+        # the automatic choice for ranks sharing a GPU: host-issued steps only
+        assert "devsteps" not in eng and "twoshot" not in eng and "oneshot" not in eng, eng
     assert "'ring_host': 'steps'" in eng, eng
