@@ -77,6 +77,9 @@ def parse():
                    help="seconds before dumping stacks and exiting")
     p.add_argument("--kernel-only", action="store_true",
                    help="N=1: run only the timed kernel loop (for rocprofv3 --pmc)")
+    p.add_argument("--pairs", type=int, default=None,
+                   help="N=1: buffer pairs the timed loop rotates (default COLD_PAIRS; 1 = back "
+                        "to back over one pair, the warm loop -- for PMC comparisons)")
     p.add_argument("--no-pmc", action="store_true",
                    help="N=1: do not measure roofline.traffic with rocprofv3 --pmc child "
                         "passes (the stored figure is reported instead)")
@@ -468,21 +471,22 @@ def bench_single(args):
     # reads inputs last touched COLD_PAIRS launches earlier, long evicted
     # from the 256 MB Infinity Cache, so the timed rate is HBM's (VERDICT r4
     # #3: back to back over one pair, part of the inputs came from the cache)
+    npairs = max(1, args.pairs or COLD_PAIRS)
     pairs = [(synthetic(torch, n, args.dtype, dev, 1234 + 2 * k),
-              synthetic(torch, n, args.dtype, dev, 4321 + 2 * k)) for k in range(COLD_PAIRS)]
+              synthetic(torch, n, args.dtype, dev, 4321 + 2 * k)) for k in range(npairs)]
     a, b = pairs[0]
     a0 = a.clone()
     stream = torch.cuda.current_stream(dev)
     # in place, a = op(a, b): the form the allreduce runs (gloo::sum(T* a,
     # const T* b, n), gloo/math.h:25-28); 2 reads + 1 write per element
-    for i in range(max(args.warmup, COLD_PAIRS)):
-        x, y = pairs[i % COLD_PAIRS]
+    for i in range(max(args.warmup, npairs)):
+        x, y = pairs[i % npairs]
         gloo_amd.math.sum(x, x, y, stream=stream)
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record(stream)  # the kernels are launched on this stream
     for i in range(steps):
-        x, y = pairs[i % COLD_PAIRS]
+        x, y = pairs[i % npairs]
         gloo_amd.math.sum(x, x, y, stream=stream)
     ev1.record(stream)
     torch.cuda.synchronize()

@@ -362,10 +362,35 @@ uint64_t HipPlanExecutor::settleLaunches(std::chrono::steady_clock::time_point d
   }
 }
 
+void HipPlanExecutor::reportPolls() noexcept {
+  if (polls_ == nullptr) return;
+  const size_t G = (size_t)pk_.G;
+  std::vector<uint64_t> v(G, 0);
+  uint64_t ctr = 0;
+  if (hipMemcpy(v.data(), polls_, G * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess &&
+      (runCtr_ == nullptr ||
+       hipMemcpy(&ctr, runCtr_, sizeof(ctr), hipMemcpyDeviceToHost) == hipSuccess)) {
+    uint64_t sum = 0, mx = 0;
+    for (uint64_t x : v) {
+      sum += x;
+      mx = std::max(mx, x);
+    }
+    std::fprintf(stderr,
+                 "[polls r%d] plan kernel G=%zu steps=%zu launches=%lu flag_reads=%lu "
+                 "per_launch=%.1f max_per_workgroup=%lu\n",
+                 contextRank_, G, plan_.steps.size(), (unsigned long)ctr, (unsigned long)sum,
+                 ctr > 0 ? (double)sum / (double)ctr : 0.0, (unsigned long)mx);
+  }
+  (void)hipGetLastError();
+  hipFree(polls_);
+  polls_ = nullptr;
+}
+
 void HipPlanExecutor::release() noexcept {
   if (device_ < 0) return;  // nothing was acquired
   hipSetDevice(device_);
   drainCredits();
+  reportPolls();
   // the last call's work may sit on a caller's stream (runFn with a stream):
   // it reads our scratch until it completes
   if (lastDone_ != nullptr && lastStream_ != nullptr) hipEventSynchronize(lastDone_);

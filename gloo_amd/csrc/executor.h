@@ -368,6 +368,10 @@ class HipPlanExecutor : public Algorithm {
   uint64_t* runCtr_ = nullptr;  // the plan kernel's run count (kernels.h), in the flag block
   // the device engine's launch counters (kernels.h kLaunchCtrLines), any engine
   uint64_t* launchCtr_ = nullptr;
+  // GLOO_AMD_COUNT_POLLS=1: the plan kernel's flag reads per workgroup
+  // (PlanKernelParams::polls), reported on stderr when the algorithm is freed
+  uint64_t* polls_ = nullptr;
+  void reportPolls() noexcept;
   // Wait (bounded by the deadline) until every launch of the device engine
   // that has started -- graph replays on any stream included -- completed;
   // returns the launches completed (0 if unknown).

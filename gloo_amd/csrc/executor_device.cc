@@ -361,6 +361,12 @@ void HipPlanExecutor::setupDevSteps() {
   pk_.runCtr = runCtr_;
   launchCtr_ = runCtr_;
 
+  pk_.polls = nullptr;
+  if (const char* e = std::getenv("GLOO_AMD_COUNT_POLLS"); e != nullptr && e[0] == '1') {
+    GLX_HIP_CHECK(hipMalloc((void**)&polls_, G * sizeof(uint64_t)));
+    GLX_HIP_CHECK(hipMemset(polls_, 0, G * sizeof(uint64_t)));
+    pk_.polls = polls_;
+  }
   pk_.trace = nullptr;
   if (devTrace()) {
     const size_t n = G * (2 * plan_.steps.size() + 1);

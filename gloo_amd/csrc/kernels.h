@@ -194,6 +194,9 @@ struct PlanKernelParams {
   // stamps per workgroup: step i started (2i), its wait was satisfied
   // (2i + 1; RECV / SEND only), the kernel ended (2 nsteps)
   uint64_t* trace;
+  // diagnostics (GLOO_AMD_COUNT_POLLS=1): [G] device words, += the flag reads
+  // (memory-side compare-exchanges) each workgroup's waits made per launch
+  uint64_t* polls;
 };
 hipError_t launch_plan_kernel(int op, int dtype, const PlanKernelParams& p, hipStream_t s);
 

@@ -429,14 +429,17 @@ __device__ __forceinline__ void report_timeout(int* status, int* claim, int code
 // Lane 0 waits until word >= epoch (bounded); the whole workgroup learns
 // the outcome.  Returns false after a timeout (reported).
 
+// `polls` (lane 0's, may be null): += the flag reads this wait made
+// (diagnostics: PlanKernelParams::polls).
 __device__ __forceinline__ bool wait_flag(const uint64_t* word, uint64_t epoch, int peer,
                                           uint64_t start, uint64_t timeoutTicks, int* status,
                                           int* claim, int* s_ok, bool narrow, bool acquire = true,
-                                          int where = 0) {
+                                          int where = 0, uint32_t* polls = nullptr) {
   if (threadIdx.x == 0) {
     int ok = 1;
     uint64_t v;
-    for (uint32_t spin = 1; (v = get_flag(word)) < epoch; spin++) {
+    uint32_t spin = 1;
+    for (; (v = get_flag(word)) < epoch; spin++) {
       if (__builtin_amdgcn_s_memrealtime() - start > timeoutTicks) {
         ok = 0;
         report_timeout(status, claim, 1 + peer + 256 * where, v, epoch);
@@ -450,6 +453,7 @@ __device__ __forceinline__ bool wait_flag(const uint64_t* word, uint64_t epoch, 
       }
       __builtin_amdgcn_s_sleep(2);
     }
+    if (polls != nullptr) *polls += spin;
     // drop any stale copy of the landing lines before anyone reads them
     if (acquire) acquire_loads(narrow);
     *s_ok = ok;
@@ -699,6 +703,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
   // the runs completed before this launch (kernels.h PlanKernelParams::runCtr)
   uint64_t run;
   if (!launch_number(p.runCtr, p.G, p.status, p.claim, &run)) return;
+  uint32_t polls = 0;  // lane 0's flag reads (diagnostics: p.polls)
   for (int i = 0; i < p.nsteps; i++) {
     const DevStep st = p.steps[i];
     const uint64_t seq = run * st.perRun + st.seq;
@@ -710,7 +715,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
         if (seq > (uint64_t)p.slots &&
             !wait_flag(flag_at(st.credit, w), seq - p.slots, st.peer,
                        __builtin_amdgcn_s_memrealtime(), p.timeoutTicks, p.status, p.claim,
-                       &s_ok, narrow, /*acquire=*/false, 1 + i)) {
+                       &s_ok, narrow, /*acquire=*/false, 1 + i, &polls)) {
           return;
         }
         stamp(2 * i + 1);
@@ -747,7 +752,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
         if (seq > (uint64_t)p.slots &&
             !wait_flag(flag_at(st.credit, w), seq - p.slots, st.peer,
                        __builtin_amdgcn_s_memrealtime(), p.timeoutTicks, p.status, p.claim,
-                       &s_ok, narrow, /*acquire=*/false, 1 + i)) {
+                       &s_ok, narrow, /*acquire=*/false, 1 + i, &polls)) {
           return;
         }
         stamp(2 * i + 1);
@@ -783,7 +788,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
       }
       case 1:  // RECV
         if (!wait_flag(flag_at(st.flag, w), seq, st.peer, __builtin_amdgcn_s_memrealtime(),
-                       p.timeoutTicks, p.status, p.claim, &s_ok, narrow, true, 1 + i)) {
+                       p.timeoutTicks, p.status, p.claim, &s_ok, narrow, true, 1 + i, &polls)) {
           return;
         }
         stamp(2 * i + 1);
@@ -827,6 +832,10 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
     }
   }
   stamp(2 * p.nsteps);
+  if (p.polls != nullptr && threadIdx.x == 0) {
+    __hip_atomic_fetch_add(p.polls + w, (uint64_t)polls, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  }
   // the last workgroup to finish advances the run count for the next launch
   // (every workgroup read it at its start, before it could finish)
   finish_launch(p.runCtr, p.G);

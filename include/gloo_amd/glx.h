@@ -377,7 +377,14 @@ int glx_allreduce(glx_context* ctx, int algorithm, int dtype, int op,
  * kernel on streams[0] and can be captured into a HIP graph
  * (hipStreamBeginCapture on streams[0]) after one eager run: the kernels
  * keep their run count / epoch on the device, so every replay is one more
- * run on that rank, in sequence with eager runs. */
+ * run on that rank, in sequence with eager runs.  Runs and replays of one
+ * algorithm must be stream-ordered (replay on streams[0], or make the
+ * replay's stream wait for the previous run): a launch that starts while
+ * the previous one is still running is detected on the device, does
+ * nothing, and the next call returns GLX_ERR_ENFORCE ("... still running");
+ * the algorithm is unusable afterwards.  Every replay must have been issued
+ * before the algorithm is destroyed (its destructor waits for every
+ * started launch). */
 int glx_algorithm_run(glx_algorithm* alg);
 
 /* Host-memory endpoint fed from a transport.  The reference receives socket
