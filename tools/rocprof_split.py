@@ -6,11 +6,12 @@ every loop of the run (warm, cold, staged legs).
 
     python tools/rocprof_split.py TRACE.csv [--warmup 5] [--steps 100] [--kernel reduce_kernel]
 
-The bench launches the kernel `warmup` times untimed, then `steps` timed
-(HIP events around them), then the cold loop (4 untimed warm-ups, then
-min(steps, 40) launches over rotating buffer pairs), then one check launch
-and the host-staged legs.  Only launches with the largest grid are counted
-(the staged legs fold 8 MiB pieces with a smaller grid).
+The bench (round 5) launches the kernel max(warmup, 4) times untimed over
+its 4 rotating buffer pairs, then `steps` timed over the same rotation (HBM
+only: the headline), then the warm loop back to back over one pair (2
+untimed, then min(steps, 20) timed), then one check launch and the
+host-staged legs.  Only launches with the largest grid are counted (the
+staged legs fold 8 MiB pieces with a smaller grid).
 """
 import argparse
 import csv
@@ -29,15 +30,15 @@ def main():
     dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows
            if int(r.get("Grid_Size") or r["Grid_Size_X"]) == grid]
     avg = lambda xs: sum(xs) / len(xs) if xs else float("nan")  # noqa: E731
-    w, s = a.warmup, a.steps
+    w, s = max(a.warmup, 4), a.steps
     timed = dur[w:w + s]
-    cold_n = min(s, 40)
-    cold = dur[w + s + 4:w + s + 4 + cold_n]
+    warm_n = min(s, 20)
+    warm = dur[w + s + 2:w + s + 2 + warm_n]
     print("kernel %s..., grid %d: %d launches" % (a.kernel, grid, len(dur)))
-    print("  timed loop (launches %d..%d): %d launches, avg %.1f ns"
+    print("  timed loop, 4 rotating pairs (launches %d..%d): %d launches, avg %.1f ns"
           % (w + 1, w + s, len(timed), avg(timed)))
-    print("  cold loop (launches %d..%d, after 4 untimed): %d launches, avg %.1f ns"
-          % (w + s + 5, w + s + 4 + cold_n, len(cold), avg(cold)))
+    print("  warm loop, one pair (launches %d..%d, after 2 untimed): %d launches, avg %.1f ns"
+          % (w + s + 3, w + s + 2 + warm_n, len(warm), avg(warm)))
     print("  all launches of that grid (the --stats line mixes every loop): avg %.1f ns"
           % avg(dur))
 
