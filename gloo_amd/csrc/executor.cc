@@ -291,6 +291,9 @@ HipPlanExecutor::~HipPlanExecutor() noexcept(false) { release(); }
 
 void HipPlanExecutor::drainCredits() noexcept {
   if (broken_) return;  // a peer timed out or exited: nothing more will come
+  // a device launch reported a timeout or an overlap that no call has
+  // raised yet: its grid stopped early, so its counts will never settle
+  if (deviceReported()) return;
   const auto deadline = std::chrono::steady_clock::now() + effectiveTimeout();
   auto pause = [] { std::this_thread::sleep_for(std::chrono::microseconds(50)); };
   try {
@@ -354,7 +357,8 @@ uint64_t HipPlanExecutor::settleLaunches(std::chrono::steady_clock::time_point d
       return 0;
     }
     const uint64_t done = ctr[0], started = ctr[2 * (size_t)glx::kFlagStride];
-    if (started <= done * (uint64_t)G || std::chrono::steady_clock::now() >= deadline) {
+    if (started <= done * (uint64_t)G || std::chrono::steady_clock::now() >= deadline ||
+        deviceReported()) {
       return done;
     }
     context_->checkPeersAlive();  // throws if a peer exited: stop waiting

@@ -376,6 +376,11 @@ class HipPlanExecutor : public Algorithm {
   // that has started -- graph replays on any stream included -- completed;
   // returns the launches completed (0 if unknown).
   uint64_t settleLaunches(std::chrono::steady_clock::time_point deadline) noexcept;
+  // A device-engine launch wrote the status word (a timed-out wait or an
+  // overlapping launch): its workgroups stopped early.
+  bool deviceReported() const noexcept {
+    return ddStatus_ != nullptr && *reinterpret_cast<const volatile int*>(ddStatus_) != 0;
+  }
   const char** devFoldSrc_ = nullptr;
   uint64_t devRuns_ = 0;
   uint64_t ddEpoch_ = 0;

@@ -75,7 +75,9 @@ def main():
     if algo == "linkprobe":
         return run_linkprobe(store_dir, rank, size)
     if algo.startswith("graph_overlap:"):
-        return run_graph_overlap(store_dir, rank, size, algo.split(":")[1])
+        parts = algo.split(":")
+        return run_graph_overlap(store_dir, rank, size, parts[1],
+                                 close_first=len(parts) > 2 and parts[2] == "close")
     if algo == "engine_choice":
         return run_engine_choice(store_dir, rank, size)
     if algo.startswith("fn_"):
@@ -766,7 +768,7 @@ def run_graph(store_dir, rank, size, replays):
     print("OK")
 
 
-def run_graph_overlap(store_dir, rank, size, kind):
+def run_graph_overlap(store_dir, rank, size, kind, close_first=False):
     """launches of one algorithm must not overlap -- a
     graph captured on the algorithm's stream but replayed on another stream
     while an eager run is still in flight would take the same run number /
@@ -776,7 +778,12 @@ def run_graph_overlap(store_dir, rank, size, kind):
     run on a second stream meanwhile; one of the two launches must report
     the overlap, and rank 0's next call raises EnforceNotMet naming it.
     Rank 1's run then either completes or times out (IoException) within
-    the context's 5 s timeout; nothing hangs."""
+    the context's 5 s timeout; nothing hangs.
+
+    close_first: rank 0 frees the algorithm right after the overlap instead
+    of calling it again, and rank 1 never starts its run; the free must not
+    wait out the (20 s) timeout for launches that stopped early
+    (HipPlanExecutor::deviceReported)."""
     import time
 
     import torch
@@ -784,7 +791,7 @@ def run_graph_overlap(store_dir, rank, size, kind):
     import gloo_amd
     store = gloo_amd.rendezvous.FileStore(store_dir)
     ctx = gloo_amd.rendezvous.Context(rank, size, 0)
-    ctx.setTimeout(5)
+    ctx.setTimeout(20 if close_first else 5)
     ctx.connectFullMesh(store)
     n = 1 << 16
     dev = torch.device("cuda:0")
@@ -810,6 +817,18 @@ def run_graph_overlap(store_dir, rank, size, kind):
             graph.replay()  # NOT ordered after the eager run
         s.synchronize()
         s2.synchronize()
+        if close_first:
+            t0 = time.time()
+            alg.close()
+            took = time.time() - t0
+            verdict = "closed in %.2f s" % took
+            print("VERDICT rank 0 %s engine %s first %s" % (verdict, engine, ok0), flush=True)
+            store.set("overlap/done/0", b"1")
+            store.get("overlap/done/1", timeout_ms=60000)
+            if not ok0 or took > 3.0:
+                sys.exit(1)
+            print("OK")
+            return
         try:
             alg.run()
             s.synchronize()
@@ -821,6 +840,9 @@ def run_graph_overlap(store_dir, rank, size, kind):
         except gloo_amd.IoException as e:
             verdict = "io: " + str(e)[:200]
         del graph
+    elif close_first:
+        store.get("overlap/done/0", timeout_ms=60000)
+        verdict = "idle"
     else:
         store.get("overlap/go", timeout_ms=60000)
         time.sleep(0.5)

@@ -28,3 +28,14 @@ def test_dropin_reference_cases_on_gpu(tmp_path):
     p = subprocess.run([exe], capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "all passed" in p.stdout
+
+
+@pytest.mark.widening
+def test_dropin_widening_cases_on_gpu(tmp_path):
+    """The round-4 widening outside the contract (HipAllreduceRing / Bcube /
+    Local): `pytest -m widening` on a GPU box."""
+    exe = str(tmp_path / "dropin_test")
+    build(exe)
+    p = subprocess.run([exe, "--widening"], capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "all passed" in p.stdout

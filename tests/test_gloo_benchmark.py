@@ -116,7 +116,9 @@ def _run(tmp_path, P, args, timeout=150):
     return [p.returncode for p in procs], outs
 
 
-@pytest.mark.gpu
+# the reference benchmark's command line is outside the SURVEY 8 contract
+# (DESIGN.md 8): its GPU runs carry the `widening` marker, not `gpu`
+@pytest.mark.widening
 @pytest.mark.parametrize("bench,P,extra", [
     ("cuda_allreduce_ring_chunked", 2, ["--inputs", "2"]),
     ("cuda_allreduce_halving_doubling_pipelined", 3, []),
@@ -137,7 +139,7 @@ def test_benchmark_runs_and_verifies(tmp_path, bench, P, extra):
     assert "BENCHMARK RESULTS" in outs[0] and bench.upper() in outs[0]
 
 
-@pytest.mark.gpu
+@pytest.mark.widening
 def test_benchmark_sweep_with_iteration_time(tmp_path):
     rcs, outs = _run(tmp_path, 2, ["--iteration-time", "20ms", "--json",
                                    "cuda_allreduce_ring_chunked"])

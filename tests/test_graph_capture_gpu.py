@@ -71,3 +71,29 @@ def test_graph_replay_overlapping_an_eager_run_is_reported(kind, engine):
                        for r, p in enumerate(procs))
     assert procs[0].returncode == 0 and "VERDICT rank 0 overlap engine %s" % engine in outs[0], every
     assert procs[1].returncode == 0 and "OK" in outs[1], every
+
+
+@pytest.mark.gpu
+def test_freeing_after_a_reported_overlap_does_not_wait_out_the_timeout():
+    """After an overlap stopped a launch early, its counters never settle:
+    freeing the algorithm must see the device's report and return at once
+    instead of draining until the context's 20 s timeout."""
+    P = 2
+    with tempfile.TemporaryDirectory() as d:
+        procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P),
+                                   "graph_overlap:ring:close"],
+                                  env=rank_env(P), stdout=subprocess.PIPE,
+                                  stderr=subprocess.STDOUT) for r in range(P)]
+        outs = []
+        for p in procs:
+            try:
+                o, _ = p.communicate(timeout=120)
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+            outs.append(o.decode(errors="replace"))
+    every = "\n".join("---- rank %d (rc %s) ----\n%s" % (r, p.returncode, outs[r][-2500:])
+                       for r, p in enumerate(procs))
+    assert all(p.returncode == 0 and "OK" in o for p, o in zip(procs, outs)), every
+    assert "closed in" in outs[0], every
