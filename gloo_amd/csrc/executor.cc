@@ -349,14 +349,16 @@ uint64_t HipPlanExecutor::settleLaunches(std::chrono::steady_clock::time_point d
     return 0;
   }
   const int G = engine_ == kEngineOneShot ? os_.G : (engine_ == kEngineTwoShot ? ts_.G : pk_.G);
-  std::vector<uint64_t> ctr((size_t)glx::kLaunchCtrLines * glx::kFlagStride);
+  std::vector<uint64_t> ctr(glx::kLaunchStartsOffset + (size_t)G);
   for (;;) {
     if (hipMemcpy(ctr.data(), launchCtr_, ctr.size() * sizeof(uint64_t),
                   hipMemcpyDeviceToHost) != hipSuccess) {
       (void)hipGetLastError();
       return 0;
     }
-    const uint64_t done = ctr[0], started = ctr[2 * (size_t)glx::kFlagStride];
+    const uint64_t done = ctr[0];
+    uint64_t started = 0;  // workgroup starts, every index
+    for (int w = 0; w < G; w++) started += ctr[glx::kLaunchStartsOffset + (size_t)w];
     if (started <= done * (uint64_t)G || std::chrono::steady_clock::now() >= deadline ||
         deviceReported()) {
       return done;

@@ -366,7 +366,7 @@ class HipPlanExecutor : public Algorithm {
   std::vector<glx::DevStep> hostSteps_;  // host copy (timeout diagnostics)
   glx::DevSegment* devSegs_ = nullptr;
   uint64_t* runCtr_ = nullptr;  // the plan kernel's run count (kernels.h), in the flag block
-  // the device engine's launch counters (kernels.h kLaunchCtrLines), any engine
+  // the device engine's launch counters (kernels.h launchCtrBytes), any engine
   uint64_t* launchCtr_ = nullptr;
   // GLOO_AMD_COUNT_POLLS=1: the plan kernel's flag reads per workgroup
   // (PlanKernelParams::polls), reported on stderr when the algorithm is freed

@@ -287,7 +287,7 @@ void HipPlanExecutor::setupOneShot() {
   ddAlloc((size_t)P * ddSlot_);
   // the flag rows, then the launch counters on lines of their own (kernels.h)
   const size_t rows = (size_t)P * (size_t)p.G * glx::kFlagBytes;
-  char* flags = ddAlloc(rows + glx::kLaunchCtrLines * glx::kFlagBytes);
+  char* flags = ddAlloc(rows + glx::launchCtrBytes(p.G));
   p.flagIn = reinterpret_cast<const uint64_t*>(flags);
   p.epochCtr = reinterpret_cast<uint64_t*>(flags + rows);
   launchCtr_ = p.epochCtr;
@@ -319,7 +319,7 @@ void HipPlanExecutor::setupTwoShot() {
   for (int k = 0; k < 4; k++) ddAlloc((size_t)P * ddSlot_);  // RS 0/1, AG 0/1
   // the A and B flag rows, then the launch counters on lines of their own
   const size_t rows = 2 * (size_t)P * (size_t)p.G * glx::kFlagBytes;
-  char* flags = ddAlloc(rows + glx::kLaunchCtrLines * glx::kFlagBytes);
+  char* flags = ddAlloc(rows + glx::launchCtrBytes(p.G));
   p.flagAIn = reinterpret_cast<const uint64_t*>(flags);
   p.flagBIn = reinterpret_cast<const uint64_t*>(flags) + (size_t)P * (size_t)p.G * glx::kFlagStride;
   p.epochCtr = reinterpret_cast<uint64_t*>(flags + rows);
@@ -356,7 +356,7 @@ void HipPlanExecutor::setupDevSteps() {
   // launch may sit on different XCDs -- in memory no L2 holds, every read
   // sees the last advance without relying on the cache maintenance at
   // kernel boundaries
-  char* block = ddAlloc(rows * G * glx::kFlagBytes + glx::kLaunchCtrLines * glx::kFlagBytes);
+  char* block = ddAlloc(rows * G * glx::kFlagBytes + glx::launchCtrBytes((int)G));
   runCtr_ = reinterpret_cast<uint64_t*>(block + rows * G * glx::kFlagBytes);
   pk_.runCtr = runCtr_;
   launchCtr_ = runCtr_;

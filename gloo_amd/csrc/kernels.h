@@ -60,10 +60,15 @@ constexpr int kFlagStride = 16;
 // (1) only completes the stores (s_waitcnt vmcnt(0)) before a flag and
 // invalidates the CU's L1 after a wait (agent scope).
 constexpr size_t kFlagBytes = kFlagStride * sizeof(uint64_t);
-// A device engine's launch counters (xgmi_kernels.hip launch_number): three
-// uncached lines after its flag rows -- launches completed, workgroups
-// finished in the current launch, workgroups ever started.
-constexpr int kLaunchCtrLines = 3;
+// A device engine's launch counters (xgmi_kernels.hip launch_number), uncached,
+// after its flag rows: a line with the launches completed, a line with the
+// workgroups finished in the current launch, then one word per workgroup
+// index: the launches that index has started.
+constexpr size_t kLaunchStartsOffset = 2 * kFlagStride;  // in uint64 words
+inline size_t launchCtrBytes(int G) {
+  return kLaunchStartsOffset * sizeof(uint64_t) +
+         (((size_t)G * sizeof(uint64_t) + kFlagBytes - 1) / kFlagBytes) * kFlagBytes;
+}
 // status code of a launch that started while the previous launch of the same
 // algorithm was still running (words 1, 2: launches completed, its number)
 constexpr int kStatusOverlap = 0x7fff0000;
@@ -79,7 +84,7 @@ struct OneShotParams {
   int flagStore;                    // 1: write peers' flags with stores (Context::flagStores)
   int narrow;                       // 1: narrow release / acquire around flags (below)
   uint64_t epoch;                   // host's count of its launches (diagnostics only)
-  // uncached device memory, kLaunchCtrLines lines: the launch's epoch is its
+  // uncached device memory, launchCtrBytes(G): the launch's epoch is its
   // launch number + 1 (>= 1, +1 per launch, equal on all ranks) --
   // graph-capturable, as PlanKernelParams::runCtr
   uint64_t* epochCtr;
@@ -175,9 +180,9 @@ struct PlanKernelParams {
   int slots;                   // landing slots per channel (1 or 2, plan.h SyncTable)
   int maxSrc;                  // most sources of a FOLD step (2 when there is none)
   uint64_t run;                // host's count of its launches (diagnostics only)
-  // uncached device memory, per algorithm, kLaunchCtrLines lines: [0] runs
-  // completed, advanced by the last workgroup to finish a launch; the launch's
-  // run number is the workgroups started before it / G -- so the message
+  // uncached device memory, per algorithm, launchCtrBytes(G): [0] runs
+  // completed, advanced by the last workgroup to finish a launch; a
+  // workgroup's run number is the launches its index started before -- so the message
   // numbers follow the launches the GPU actually ran, a launch captured in a
   // graph and replayed numbers its messages like an eager one, and a launch
   // overlapping the previous one reports kStatusOverlap (xgmi_kernels.hip

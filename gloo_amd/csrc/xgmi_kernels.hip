@@ -464,27 +464,31 @@ __device__ __forceinline__ bool wait_flag(const uint64_t* word, uint64_t epoch, 
 
 // ---- launch counts kept on the device ------------------------------------------
 
-// The launch's number: launches of this algorithm before it.  Three uncached
-// counters on lines of their own (the workgroup advancing one and those
+// The launch's number: launches of this algorithm before it.  Uncached
+// counters after the flag rows (the workgroup advancing one and those
 // reading it next may sit on different XCDs, whose L2s are not coherent):
 // ctr[0] launches completed, advanced by finish_launch once the last
 // workgroup is done; ctr[kFlagStride] workgroups finished in the current
-// launch; ctr[2 kFlagStride] workgroups ever started.  Each workgroup counts
-// itself in at its start, so its launch number is (starts before it) / G and
-// the numbers a launch uses come from the GPU: a captured launch replays
-// correctly.  Launches of one algorithm must not overlap (a graph replayed
-// on another stream than eager runs): every launch's workgroups
-// start after the previous launch completed, so the completed count then
-// equals the launch number; a workgroup that sees fewer completions reports
-// kStatusOverlap and its launch does nothing more (returns false).
-__device__ __forceinline__ bool launch_number(uint64_t* ctr, int G, int* status, int* claim,
+// launch; ctr[kLaunchStartsOffset + w] the launches workgroup index w has
+// started.  A workgroup takes its index's count as its launch number, so the
+// numbers come from the GPU and a captured launch replays correctly.
+// Launches of one algorithm must not overlap (a graph replayed on another
+// stream than eager runs): in stream order every workgroup starts
+// after the previous launch completed, so the completed count equals its
+// number.  Otherwise either the two launches' workgroups happen to form runs
+// one after the other -- each number taken by one workgroup per index, a run
+// starting only once the one before completed: a valid serialisation of the
+// same algorithm on the same buffer -- or some workgroup sees fewer completed
+// launches than its number: it reports kStatusOverlap and its launch does
+// nothing more (returns false).  (tests/test_plan_kernel_sim.py models it.)
+__device__ __forceinline__ bool launch_number(uint64_t* ctr, int* status, int* claim,
                                               uint64_t* number) {
   __shared__ uint64_t s_n;
   __shared__ int s_in_order;
   if (threadIdx.x == 0) {
-    const uint64_t started = __hip_atomic_fetch_add(ctr + 2 * kFlagStride, (uint64_t)1,
-                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t n = started / (uint64_t)G;
+    const uint64_t n = __hip_atomic_fetch_add(ctr + kLaunchStartsOffset + blockIdx.x,
+                                              (uint64_t)1, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t done = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_n = n;
     s_in_order = done == n ? 1 : 0;
@@ -520,7 +524,7 @@ __device__ __forceinline__ void oneshot_body(const OneShotParams& p) {
   S* buf = reinterpret_cast<S*>(p.buf);
   const bool aligned = ((uintptr_t)p.buf % 16) == 0;
   uint64_t launched;
-  if (!launch_number(p.epochCtr, p.G, p.status, p.claim, &launched)) return;
+  if (!launch_number(p.epochCtr, p.status, p.claim, &launched)) return;
   const uint64_t epoch = launched + 1;
   const int par = (int)(epoch & 1);
 
@@ -586,7 +590,7 @@ __device__ __forceinline__ void twoshot_body(const TwoShotParams& p) {
   S* buf = reinterpret_cast<S*>(p.buf);
   const bool aligned = ((uintptr_t)p.buf % 16) == 0;
   uint64_t launched;
-  if (!launch_number(p.epochCtr, p.G, p.status, p.claim, &launched)) return;
+  if (!launch_number(p.epochCtr, p.status, p.claim, &launched)) return;
   const uint64_t epoch = launched + 1;
   const int par = (int)(epoch & 1);
   auto span = [&](int c, size_t& a, size_t& b) {  // slice w of range c
@@ -702,7 +706,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
   auto slotOf = [&](uint64_t m) -> uint64_t { return p.slots == 2 ? ((m - 1) & 1) : 0; };
   // the runs completed before this launch (kernels.h PlanKernelParams::runCtr)
   uint64_t run;
-  if (!launch_number(p.runCtr, p.G, p.status, p.claim, &run)) return;
+  if (!launch_number(p.runCtr, p.status, p.claim, &run)) return;
   uint32_t polls = 0;  // lane 0's flag reads (diagnostics: p.polls)
   for (int i = 0; i < p.nsteps; i++) {
     const DevStep st = p.steps[i];

@@ -371,3 +371,106 @@ def test_ring_partial_sums_are_forwarded_not_stored(P):
                    if st[0] not in (RECV, RELEASE) and st[4] > 0
                    and st[3] < hi and st[3] + st[4] > lo][0]
             assert nxt[0] == COPY and nxt[3] <= lo and nxt[3] + nxt[4] >= hi
+
+
+# ---------------------------------------------------------------------------
+# The device engines' launch numbering (xgmi_kernels.hip launch_number /
+# finish_launch), restated: launches completed, workgroups finished in the
+# current launch, and per workgroup index the launches it started.  A
+# workgroup takes its index's count as its number and reports an overlap
+# when fewer launches completed; a reporting workgroup does nothing more
+# (it never finishes).
+# ---------------------------------------------------------------------------
+class LaunchCounters:
+    def __init__(self, G):
+        self.G, self.done, self.finished = G, 0, 0
+        self.starts = [0] * G
+        self.reports = []
+
+    def start(self, w):
+        n = self.starts[w]
+        self.starts[w] += 1
+        ok = self.done == n
+        if not ok:
+            self.reports.append((w, self.done, n))
+        return n, ok
+
+    def finish(self):
+        self.finished += 1
+        if self.finished == self.G:
+            self.finished = 0
+            self.done += 1
+
+
+def _run_launches(G, nlaunch, overlap_at, rng):
+    """nlaunch launches of G workgroups; launch `overlap_at` (or none) is
+    released before the previous one completed -- the two launches'
+    workgroups start and finish interleaved at random (each starts before it
+    finishes; one that reported never finishes) -- every other launch starts
+    after the previous one finished (stream order).  Returns the (number,
+    index, start time, finish time) of every workgroup that did not report,
+    and the counters."""
+    c = LaunchCounters(G)
+    runs = []
+    t = 0
+    k = 0
+    while k < nlaunch:
+        group = [k, k + 1] if overlap_at is not None and k + 1 == overlap_at else [k]
+        todo = [(lid, w) for lid in group for w in range(G)]
+        live = []  # [number, index, start]
+        while todo or live:
+            t += 1
+            if todo and (not live or rng.random() < 0.5):
+                lid, w = todo.pop(rng.randrange(len(todo)))
+                n, ok = c.start(w)
+                if ok:
+                    live.append([n, w, t])
+            else:
+                n, w, t0 = live.pop(rng.randrange(len(live)))
+                runs.append((n, w, t0, t))
+                c.finish()
+        k += len(group)
+    return runs, c
+
+
+def _is_serial(runs, G):
+    """Every number taken by one workgroup per index, and no workgroup of
+    number n started before every workgroup of number n - 1 finished."""
+    by = {}
+    for n, w, t0, t1 in runs:
+        by.setdefault(n, []).append((w, t0, t1))
+    for n, wgs in by.items():
+        if sorted(w for w, _, _ in wgs) != list(range(G)):
+            return False
+        if n - 1 in by and min(t0 for _, t0, _ in wgs) < max(t1 for _, _, t1 in by[n - 1]):
+            return False
+    return True
+
+
+@pytest.mark.parametrize("G", [1, 2, 7, 72, 512])
+def test_launch_numbers_in_stream_order_need_no_host_count(G):
+    """Launches in stream order: launch k's workgroups all take number k and
+    nothing is reported -- graph replays and eager runs share one sequence."""
+    import random
+    runs, c = _run_launches(G, 6, None, random.Random(G))
+    assert c.reports == [] and c.done == 6
+    assert _is_serial(runs, G) and sorted({n for n, _, _, _ in runs}) == list(range(6))
+
+
+@pytest.mark.parametrize("G", [1, 2, 7, 72, 512])
+@pytest.mark.parametrize("seed", range(40))
+def test_overlapping_launches_are_serialised_or_reported(G, seed):
+    """Two launches of one algorithm released together (a replay on another
+    stream than the eager runs), their workgroups interleaved at
+    random: either nothing is reported and the workgroups formed runs one
+    after the other (each number taken by one workgroup per index, a run
+    starting only once the previous completed -- the same algorithm on the
+    same buffer, so a valid serialisation), or some workgroup reported, and
+    the rank's next call raises.  Never two workgroups of one index in one
+    run, never a run starting before the one before it ended, unreported."""
+    import random
+    rng = random.Random(1000 * G + seed)
+    at = rng.randrange(1, 5)
+    runs, c = _run_launches(G, 5, at, rng)
+    if not c.reports:
+        assert _is_serial(runs, G) and c.done == 5

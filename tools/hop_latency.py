@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""Per-hop hand-off cost of the ring on each engine (VERDICT r4 weak #5:
+the host-issued DMA ring's hand-off was argued, not measured).  One process
+per rank (torchrun); the reference's ring data movement (schedule="ring") as
+host-issued steps (hipMemcpyPeerAsync sends, reduce kernels, the host's
+progress loop) and as the plan kernel, at sizes where the bytes cost next to
+nothing, so the time per allreduce is the ring's chain of dependent hops:
+reduce-scatter P-1 rounds + allgather P-1 rounds, each a transfer that waits
+for the previous one's hand-off.  Reports us per allreduce (max over ranks,
+runs back to back, each waited for, as run() without streams does) and
+us per dependent round = t / (2 (P - 1)).  On the node a round of the
+256 MiB north-star ring is one 16 MiB chunk on a 153 GB/s link (110 us) and
+the two channels interleave, so the link idles only where a round's hand-off
+exceeds that.
+
+    GPU_MAX_HW_QUEUES=1 python -m torch.distributed.run --nproc-per-node 8 \\
+        --master-addr 127.0.0.1 tools/hop_latency.py [--sizes 1024,65536]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sizes", default="1024,65536,1048576")
+    ap.add_argument("--iters", type=int, default=200)
+    a = ap.parse_args()
+    import torch
+    import torch.distributed as dist
+
+    import gloo_amd
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    if torch.cuda.device_count() < world and "GLOO_AMD_DEVICE_ENGINES" not in os.environ:
+        gloo_amd.set_device_engines("shared")  # a rehearsal on one GPU
+    dist.init_process_group("gloo")
+    ctx = gloo_amd.rendezvous.Context(rank, world, dev)
+    ctx.connectFullMesh(gloo_amd.rendezvous.TorchStore(dist.distributed_c10d._get_default_store()))
+    rounds = 2 * (world - 1)
+    out = {}
+    for n in [int(x) for x in a.sizes.split(",")]:
+        row = {}
+        for label, steps in (("host_steps", "host"), ("plan_kernel", "device")):
+            buf = torch.zeros(n, dtype=torch.float32, device="cuda")
+            gloo_amd.set_steps_engine(steps)
+            try:
+                alg = gloo_amd.AllreduceRingChunked(ctx, [buf], schedule="ring")
+            finally:
+                gloo_amd.set_steps_engine("auto")
+            engine = alg.engine()
+            for _ in range(10):
+                alg.run()
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(a.iters):
+                alg.run()
+            torch.cuda.synchronize()
+            el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+            us = el.item() / a.iters * 1e6
+            ok = bool((buf == 0).all().item())
+            alg.close()
+            row[label] = {"engine": engine, "us_per_allreduce": round(us, 2),
+                          "us_per_round": round(us / rounds, 2), "result_ok": ok}
+        out[str(n)] = row
+    if rank == 0:
+        print(json.dumps({"what": "ring (schedule=ring) per allreduce and per dependent round "
+                                  "(2(P-1) rounds), back to back, max over ranks",
+                          "ranks": world, "rounds": rounds,
+                          "gpus": torch.cuda.device_count(),
+                          "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "4"),
+                          "sizes": out}))
+    dist.barrier()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
