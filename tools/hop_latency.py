@@ -30,6 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sizes", default="1024,65536,1048576")
     ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--engines", default="host_steps,plan_kernel")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -49,6 +50,8 @@ def main():
     for n in [int(x) for x in a.sizes.split(",")]:
         row = {}
         for label, steps in (("host_steps", "host"), ("plan_kernel", "device")):
+            if label not in a.engines.split(","):
+                continue
             buf = torch.zeros(n, dtype=torch.float32, device="cuda")
             gloo_amd.set_steps_engine(steps)
             try:

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--prof-name", default="rank0", help="rocprofv3 -o name")
     ap.add_argument("--copies", action="store_true",
                     help="with --prof-dir (no --pmc): also --memory-copy-trace")
+    ap.add_argument("--api", action="store_true",
+                    help="with --prof-dir (no --pmc): also --hip-runtime-trace")
     ap.add_argument("cmd", nargs=argparse.REMAINDER)
     a = ap.parse_args()
     cmd = a.cmd[1:] if a.cmd and a.cmd[0] == "--" else a.cmd
@@ -43,6 +45,8 @@ def main():
             what = ["--pmc"] + a.pmc.split(",") if a.pmc else ["--kernel-trace", "--stats"]
             if a.copies and not a.pmc:
                 what.append("--memory-copy-trace")
+            if a.api and not a.pmc:
+                what.append("--hip-runtime-trace")
             argv = ["rocprofv3"] + what + ["--output-format", "csv",
                                            "-d", a.prof_dir, "-o", a.prof_name, "--"] + argv
         procs.append(subprocess.Popen(argv, env=env))
