@@ -77,7 +77,7 @@ def main():
         out["P%d" % P] = row
     print(json.dumps({"what": "ring (schedule=ring), P rank threads of one process on one GPU, "
                               "host-issued steps; us per allreduce (slowest rank) and per "
-                              "dependent round", "iters": a.iters, "results": out}))
+                              "dependent round", "iters": a.iters, "results": out}), flush=True)
 
 
 if __name__ == "__main__":
