@@ -494,7 +494,9 @@ def bench_single(args):
     if args.kernel_only:
         return None
     del pairs[1:]
-    warm = warm_rate(torch, gloo_amd, a, b, stream, steps=min(steps, 20))
+    # few launches: rocprofv3 --stats averages every launch of the kernel, and
+    # the timed (HBM-only) loop is the one that line must agree with
+    warm = warm_rate(torch, gloo_amd, a, b, stream, steps=min(steps, 10))
     # correctness of one launch on the original inputs
     a.copy_(a0)
     gloo_amd.math.sum(a, a, b, stream=stream)

@@ -9,7 +9,7 @@ every loop of the run (warm, cold, staged legs).
 The bench (round 5) launches the kernel max(warmup, 4) times untimed over
 its 4 rotating buffer pairs, then `steps` timed over the same rotation (HBM
 only: the headline), then the warm loop back to back over one pair (2
-untimed, then min(steps, 20) timed), then one check launch and the
+untimed, then min(steps, 10) timed), then one check launch and the
 host-staged legs.  Only launches with the largest grid are counted (the
 staged legs fold 8 MiB pieces with a smaller grid).
 """
@@ -32,7 +32,7 @@ def main():
     avg = lambda xs: sum(xs) / len(xs) if xs else float("nan")  # noqa: E731
     w, s = max(a.warmup, 4), a.steps
     timed = dur[w:w + s]
-    warm_n = min(s, 20)
+    warm_n = min(s, 10)
     warm = dur[w + s + 2:w + s + 2 + warm_n]
     print("kernel %s..., grid %d: %d launches" % (a.kernel, grid, len(dur)))
     print("  timed loop, 4 rotating pairs (launches %d..%d): %d launches, avg %.1f ns"

@@ -4,7 +4,7 @@ set -o pipefail
 # loop vs the bench's HIP events; --no-pmc: no profiler children inside the
 # profiled process), and the N > 1 rehearsals (ranks sharing the box's one
 # GPU, torchrun as the driver launches it) at P = 8, 4, 2.
-O=gpurun_out/r10g
+O=${O:-gpurun_out/r10g}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python bench.py > $O/bench1.json 2> $O/bench1.err || exit 1
