@@ -363,7 +363,9 @@ uint64_t HipPlanExecutor::settleLaunches(std::chrono::steady_clock::time_point d
         deviceReported()) {
       return done;
     }
-    context_->checkPeersAlive();  // throws if a peer exited: stop waiting
+    // a peer that exited ends the wait (this function must not throw: it
+    // runs from the destructor's drain)
+    if (context_->deadPeer() >= 0) return done;
     std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
 }
