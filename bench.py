@@ -620,7 +620,7 @@ SEED = 1234  # SURVEY 8d's synthetic-input seed
 
 def plan_name(algo):
     """Schedule name of a bench candidate for gloo_amd.plan()."""
-    for suffix in ("_narrow", "_system", "_host", "_fast", "_plain"):
+    for suffix in ("_narrow", "_system", "_host", "_dma", "_fast", "_plain"):
         if algo.endswith(suffix):
             algo = algo[:-len(suffix)]
     return {"ring_chunked_mesh_steps": "ring_chunked_mesh",
@@ -639,7 +639,9 @@ def make_alg(gloo_amd, ctx, buf, algo):
     halving_doubling run their step programs in the plan kernel (devsteps) at
     every size and P, ring_chunked_mesh on the two-shot kernel, ring_chunked_repl on
     the one-shot kernel.  *_host and ring_chunked_mesh_steps are the same
-    schedules with host-issued steps (calibrated peer-copy transport);
+    schedules with host-issued steps (calibrated peer-copy transport); *_dma
+    the host-issued steps' copies (hipMemcpyPeerAsync) and reduce launches
+    with their hand-offs on the GPU (the dmasteps engine);
     *_fast / *_plain the plan kernel with a forced stream policy
     (set_engine_streams), *_narrow / *_system the device engines with a
     forced flag sync (set_device_sync; the run's default is RUN_SYNC)."""
@@ -660,6 +662,8 @@ def make_alg(gloo_amd, ctx, buf, algo):
     engine = None
     if algo.endswith("_host"):
         engine, algo = "host", algo[:-len("_host")]
+    elif algo.endswith("_dma"):
+        engine, algo = "dma", algo[:-len("_dma")]
     elif algo in ("ring_chunked", "halving_doubling"):
         engine = "device"  # the plan kernel (the step program in one kernel per rank)
     if engine is not None:
@@ -981,13 +985,16 @@ def element_sweep(torch, dist, gloo_amd, ctx, dev, schedules, dtype):
 # the ring and the mesh each moved by CUs (the plan / two-shot kernels
 # storing into the peers' slots) and by DMA engines (host-issued
 # hipMemcpyPeerAsync steps): whether CU stores fill an xGMI link is the one
-# thing no one-GPU box can measure, so the first node run times both ways
+# thing no one-GPU box can measure, so the first node run times both ways.
+# The ring's DMA steps with on-GPU hand-offs (dmasteps) is opt-in: on the
+# one-GPU box it measured slower than the host-issued steps
 DEFAULT_CANDIDATES = ["ring_chunked", "ring_chunked_mesh", "ring_chunked_host",
                       "ring_chunked_mesh_steps"]
-EXTRA_CANDIDATES = ["ring_chunked_fast", "ring_chunked_system", "ring_chunked_mesh_system"]
-DMA_CANDIDATES = ("ring_chunked_host", "ring_chunked_mesh_steps")
+EXTRA_CANDIDATES = ["ring_chunked_dma", "ring_chunked_fast", "ring_chunked_system",
+                    "ring_chunked_mesh_system"]
+DMA_CANDIDATES = ("ring_chunked_host", "ring_chunked_dma", "ring_chunked_mesh_steps")
 DEFAULT_ALTS = ["halving_doubling"]
-EXTRA_ALTS = ["halving_doubling_host", "halving_doubling_system"]
+EXTRA_ALTS = ["halving_doubling_host", "halving_doubling_dma", "halving_doubling_system"]
 # host-issued steps' peer-copy transports: (engine, DMA split, copy-kernel workgroups)
 TRANSPORTS_DEFAULT = [("dma", 1, 0), ("kernel", 1, 128)]
 # the north star's own transport for the host-issued ring: hipMemcpyPeerAsync
@@ -1017,7 +1024,7 @@ def candidate_lists(args):
     elif args.algo == "ring_chunked" and args.schedule == "mesh":
         cands, alts = ["ring_chunked_mesh", "ring_chunked_mesh_steps"], []
     elif args.algo == "ring_chunked" and args.schedule == "ring":
-        cands, alts = ["ring_chunked", "ring_chunked_host"], []
+        cands, alts = ["ring_chunked", "ring_chunked_host", "ring_chunked_dma"], []
     else:
         cands, alts = [args.algo], []
     if args.no_alt:
@@ -1059,7 +1066,10 @@ def measured_link_for(engine, transport_tr, links):
     return "ring_dma_GBps", links.get("ring_dma_GBps")
 
 
-NS_RINGS = ("ring_chunked", "ring_chunked_host")  # plan kernel (CU stores), host-issued DMA
+# plan kernel (CU stores), host-issued DMA steps; the DMA steps with on-GPU
+# hand-offs join them when timed (--candidates all or a list naming it)
+NS_RINGS = ("ring_chunked", "ring_chunked_host")
+NS_RINGS_OPT = ("ring_chunked_dma",)
 
 
 def north_star_section(S, world, ring_runs, links, refdig, failed):
@@ -1073,7 +1083,8 @@ def north_star_section(S, world, ring_runs, links, refdig, failed):
     for its transport) and its reference-digest match.  The top level repeats
     the faster one's block."""
     rings = {}
-    for cand in NS_RINGS:
+    names = NS_RINGS + tuple(c for c in NS_RINGS_OPT if c in ring_runs or c in failed)
+    for cand in names:
         rr = ring_runs.get(cand)
         if rr is None:
             rings[cand] = {"error": failed.get(cand, "not timed")}
@@ -1087,9 +1098,9 @@ def north_star_section(S, world, ring_runs, links, refdig, failed):
             b["measured_link_GBps"] = best
             b["measured_link_frac"] = round(b["link_GBps"] / best, 4)
         rings[cand] = b
-    timed = [c for c in NS_RINGS if "error" not in rings[c]]
+    timed = [c for c in names if "error" not in rings[c]]
     if not timed:
-        return {"error": "; ".join("%s: %s" % (c, rings[c]["error"]) for c in NS_RINGS),
+        return {"error": "; ".join("%s: %s" % (c, rings[c]["error"]) for c in names),
                 "rings": rings}
     fastest = min(timed, key=lambda c: rings[c]["ms_per_step"])
     ns = dict(rings[fastest])
@@ -1237,10 +1248,12 @@ def bench_multi(args):
         calib = {}
         log("%s: creating" % algo)
         probe = make_alg(gloo_amd, ctx, buf, algo)
-        # no peer-copy transport to tune for the kernels that store themselves
-        device_engine = probe.engine() != "steps"
+        # no peer-copy transport to tune for the kernels that store themselves;
+        # the dmasteps engine copies with hipMemcpyPeerAsync, one copy per send
+        engine = probe.engine()
+        device_engine = engine not in ("steps", "dmasteps")
         probe.close()
-        if args.copy_split == "auto" and not device_engine:
+        if args.copy_split == "auto" and engine == "steps":
             for tr in (TRANSPORTS_DMA if algo in DMA_CANDIDATES and args.calibrate != "all"
                        else transports):
                 set_transport(tr)
@@ -1266,7 +1279,8 @@ def bench_multi(args):
         return {"t": t, "sent": sent, "p50": p50,
                 "transport": ("device-driven kernel stores (%s)" % ENGINES[algo]
                               if device_engine else tname(best) +
-                              ""), "tr": best,
+                              (", hand-offs on the GPU (dmasteps)" if engine == "dmasteps"
+                               else "")), "tr": best,
                 "calib_ms": {tname(k): round(v * 1e3, 3) for k, v in calib.items()},
                 "result": result}
 
@@ -1422,7 +1436,7 @@ def bench_multi(args):
                                                fused=ENGINES.get(a) == "devsteps"),
                          "transport": runs[a]["transport"], "tr": runs[a]["tr"],
                          "fast": FAST.get(a), "sync": SYNC.get(a)}
-                     for a in runs if a in NS_RINGS}
+                     for a in runs if a in NS_RINGS + NS_RINGS_OPT}
         ns = north_star_section(S, world, ring_runs, links, REFDIG, failed)
         res = {
             "metric": metric_name(args.dtype),

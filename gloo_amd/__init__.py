@@ -77,9 +77,11 @@ def set_steps_engine(engine):
     processes: "auto" (default: the plan kernel; at every size with one rank
     per GPU, up to 32 MiB per rank when ranks share a GPU, host-issued steps
     above), "device" (the plan kernel, one device-driven
-    launch per rank) or "host" (host-issued steps).  Same results either
-    way."""
-    code = {"host": 0, "device": 3, "auto": -1}[engine]
+    launch per rank), "host" (host-issued steps) or "dma" (the host-issued
+    steps' copies and reduce launches with their hand-offs made on the GPU by
+    flag kernels; not for rank threads sharing a device, which then get
+    "host").  Same results either way."""
+    code = {"host": 0, "device": 3, "dma": 4, "auto": -1}[engine]
     errors.check(_lib.lib.glx_set_steps_engine(code), "set_steps_engine")
 
 

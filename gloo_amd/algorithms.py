@@ -208,9 +208,10 @@ class Algorithm:
         schedule as one device-driven kernel per rank), "twoshot" (the mesh
         schedule as one device-driven kernel per rank), "devsteps" (any
         other schedule's step program walked by one device-driven kernel per
-        rank)."""
-        return {0: "steps", 1: "oneshot", 2: "twoshot",
-                3: "devsteps"}[lib.glx_algorithm_engine(self._h)]
+        rank), "dmasteps" (the host-issued steps' copies and reduce launches,
+        their hand-offs made on the GPU by flag kernels)."""
+        return {0: "steps", 1: "oneshot", 2: "twoshot", 3: "devsteps",
+                4: "dmasteps"}[lib.glx_algorithm_engine(self._h)]
 
     def fast_streams(self):
         """True when the plan kernel runs nontemporal loads and write-through
@@ -230,12 +231,13 @@ class Algorithm:
         memory), device_kernels (device-driven engine launches), bytes, and
         host_folds (multi-pointer host buffers below kOnDeviceThreshold folded
         on the host), done_events (event records after a run's work: none
-        for run() on a device engine)."""
-        out = (ctypes.c_int64 * 7)()
-        if lib.glx_algorithm_transport_stats(self._h, out, 7) != 7:
+        for run() on a device engine), flag_kernels (the dmasteps engine's
+        hand-off launches)."""
+        out = (ctypes.c_int64 * 8)()
+        if lib.glx_algorithm_transport_stats(self._h, out, 8) != 8:
             check(_lib.ERR_INVALID, "transport_stats")
         return dict(zip(("peer_copies", "device_copies", "kernel_copies", "device_kernels",
-                         "bytes", "host_folds", "done_events"), list(out)))
+                         "bytes", "host_folds", "done_events", "flag_kernels"), list(out)))
 
     def record(self, event):
         """Record `event` (gloo_amd.Event) at the end of the last run()'s

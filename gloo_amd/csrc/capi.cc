@@ -214,9 +214,11 @@ int glx_set_engine_streams(int fast) {
 }
 
 int glx_set_steps_engine(int engine) {
-  if (engine != GLX_ENGINE_STEPS && engine != GLX_ENGINE_DEVSTEPS && engine != -1) {
+  if (engine != GLX_ENGINE_STEPS && engine != GLX_ENGINE_DEVSTEPS &&
+      engine != GLX_ENGINE_DMASTEPS && engine != -1) {
     return fail(GLX_ERR_INVALID,
-                "steps engine must be GLX_ENGINE_STEPS, GLX_ENGINE_DEVSTEPS or -1 (by size)");
+                "steps engine must be GLX_ENGINE_STEPS, GLX_ENGINE_DEVSTEPS, "
+                "GLX_ENGINE_DMASTEPS or -1 (by size)");
   }
   gloo::HipPlanExecutor::setStepsEngine(engine);
   return GLX_OK;
@@ -550,7 +552,9 @@ int glx_algorithm_transport_stats(glx_algorithm* alg, int64_t* out, int cap) {
   out[5] = t.hostFolds;
   if (cap < 7) return 6;
   out[6] = t.doneEvents;
-  return 7;
+  if (cap < 8) return 7;
+  out[7] = t.flagKernels;
+  return 8;
 }
 
 int glx_algorithm_record(glx_algorithm* alg, glx_event_t ev) {

@@ -187,6 +187,7 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
   }
 
   engine_ = engineFor(*ctx, algo, count_, (int)esize_);
+  if (engine_ == kEngineDmaSteps) split_ = 1;  // one copy (one done word) per SEND
   if (engine_ == kEngineDevSteps) {
     // the plan kernel's grid and bookkeeping; when a landing region would be
     // shared by two workgroups across messages, keep the host-issued steps
@@ -232,7 +233,7 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
   auto& ctl = ctx->localControl();
   stepChan_.assign(plan_.steps.size(), -1);
   const bool hostSteps = engine_ == kEngineSteps;
-  const bool copyStreams = hostSteps;
+  const bool copyStreams = hostSteps || engine_ == kEngineDmaSteps;
   for (size_t i = 0; i < plan_.steps.size() &&
                      (copyStreams || engine_ == kEngineDevSteps);
        i++) {
@@ -243,8 +244,9 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
         OutChan oc;
         oc.peer = (int)s.peer;
         oc.tag = (int)s.channel;
-        // plan kernel: no control-block words or copy streams (its flag
-        // rows are assigned in setupDevSteps)
+        // device engines: no control-block words (their flag rows are
+        // assigned in setupDevSteps / setupDmaSteps); the plan kernel has no
+        // copy streams
         oc.creditWord = hostSteps ? ctl.allocWord() : 0;
         oc.credit = hostSteps ? ctl.word(oc.creditWord) : nullptr;
         // one copy stream per destination peer: copies to different peers
@@ -279,7 +281,7 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
       stepChan_[i] = idx;
     }
   }
-  if (engine_ == kEngineDevSteps) setupDevice();
+  if (engine_ == kEngineDevSteps || engine_ == kEngineDmaSteps) setupDevice();
   events_.resize(plan_.steps.size() * (size_t)split_, nullptr);
   for (auto& e : events_) GLX_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   GLX_HIP_CHECK(hipEventCreateWithFlags(&computeMark_, hipEventDisableTiming));
@@ -305,7 +307,30 @@ void HipPlanExecutor::drainCredits() noexcept {
           pause();
         }
       }
-    } else if (engine_ != kEngineSteps) {
+    } else if (engine_ == kEngineDmaSteps) {
+      // our last run's work (its copies and signals included: the compute
+      // stream waits for them), then every receiver's credit for our last
+      // message into our flag words
+      if (hipStreamSynchronize(compute_) != hipSuccess) {
+        (void)hipGetLastError();
+        return;
+      }
+      for (auto& oc : out_) {
+        for (;;) {
+          uint64_t v = 0;
+          if (hipMemcpy(&v, dmaWord(oc.creditWord), sizeof(v), hipMemcpyDeviceToHost) !=
+              hipSuccess) {
+            (void)hipGetLastError();
+            break;
+          }
+          if (v >= oc.sent || deviceReported() || std::chrono::steady_clock::now() >= deadline) {
+            break;
+          }
+          context_->checkPeersAlive();  // throws if a peer exited: stop waiting
+          pause();
+        }
+      }
+    } else {
       // the launches the GPU completed, graph replays on other streams
       // included: wait until every started launch finished
       const uint64_t settled = settleLaunches(deadline);
@@ -397,6 +422,12 @@ void HipPlanExecutor::reportPolls() noexcept {
 void HipPlanExecutor::release() noexcept {
   if (device_ < 0) return;  // nothing was acquired
   hipSetDevice(device_);
+  // DMA steps engine after a failed run: flag waits of it may still be queued
+  // for messages that will never come; stop them at once
+  if (engine_ == kEngineDmaSteps && broken_ && ddStatus_ != nullptr &&
+      *reinterpret_cast<volatile int*>(ddStatus_) == 0) {
+    *reinterpret_cast<volatile int*>(ddStatus_) = 1 + contextRank_;
+  }
   drainCredits();
   reportPolls();
   // the last call's work may sit on a caller's stream (runFn with a stream):
@@ -642,10 +673,10 @@ void HipPlanExecutor::resolvePeers() {
       }
     }
     if (engine_ != kEngineSteps) ddPeer_[r] = blocks;
-    if (engine_ == kEngineDevSteps) {  // the peer's flag rows
+    if (engine_ == kEngineDevSteps || engine_ == kEngineDmaSteps) {  // the peer's flag rows
       GLX_ENFORCE(!blocks.empty(), "rank ", r, " published no flag rows");
       uint64_t* rows = reinterpret_cast<uint64_t*>(blocks[0]);
-      const size_t G = (size_t)pk_.G;
+      const size_t G = engine_ == kEngineDevSteps ? (size_t)pk_.G : 1;  // DMA steps: one word
       for (auto& oc : out_) {
         if (oc.peer == r && oc.peerRow >= 0) {
           oc.devDelivery = rows + (size_t)oc.peerRow * G * glx::kFlagStride;
@@ -658,7 +689,7 @@ void HipPlanExecutor::resolvePeers() {
       }
     }
   }
-  const bool dev = engine_ == kEngineDevSteps;
+  const bool dev = engine_ == kEngineDevSteps || engine_ == kEngineDmaSteps;
   for (auto& oc : out_) {
     GLX_ENFORCE(dev ? oc.devDelivery != nullptr : oc.delivery != nullptr, "rank ", oc.peer,
                 " has no receive channel ", oc.tag, " from rank ", contextRank_,
@@ -989,7 +1020,255 @@ void HipPlanExecutor::recordDone(hipEvent_t ev) {
   GLX_HIP_CHECK(hipEventRecord(ev, lastStream_ != nullptr ? lastStream_ : compute_));
 }
 
+void HipPlanExecutor::issueCopy(char* dst, const char* src, size_t len, OutChan& oc,
+                                hipStream_t s) {
+  hipError_t ce = hipErrorUnknown;
+  if (copyEngine_ == kCopyKernel) {
+    ce = glx::launch_copy(dst, src, len, s);
+    GLX_HIP_CHECK(ce);
+    transport_.kernelCopies++;
+  } else if (peerCopyOk_ && oc.peerDevice >= 0 && oc.peerDevice != device_) {
+    ce = hipMemcpyPeerAsync(dst, oc.peerDevice, src, device_, len, s);
+    if (ce == hipSuccess) {
+      transport_.peerCopies++;
+    } else {
+      (void)hipGetLastError();
+      // e.g. an IPC mapping the peer API rejects: the copy still crosses
+      // xGMI (the destination is the peer's memory), now as a plain device
+      // copy; say so once and count every one
+      peerCopyOk_ = false;
+      std::fprintf(stderr,
+                   "[gloo_amd] rank %d: hipMemcpyPeerAsync to device %d refused "
+                   "(%s: %s); peer copies of this algorithm use hipMemcpyAsync\n",
+                   contextRank_, oc.peerDevice, hipGetErrorName(ce), hipGetErrorString(ce));
+    }
+  }
+  if (ce != hipSuccess) {
+    GLX_HIP_CHECK(hipMemcpyAsync(dst, src, len, hipMemcpyDeviceToDevice, s));
+    transport_.deviceCopies++;
+  }
+  transport_.bytes += (int64_t)len;
+}
+
+void HipPlanExecutor::setupDmaSteps() {
+  for (size_t k = 0; k < in_.size(); k++) in_[k].deliveryWord = (uint32_t)k;
+  for (size_t k = 0; k < out_.size(); k++) out_[k].creditWord = (uint32_t)(in_.size() + k);
+  markWord_ = (uint32_t)(in_.size() + out_.size());
+  for (size_t j = 0; j < copies_.size(); j++) copies_[j].doneWord = markWord_ + 1 + (uint32_t)j;
+  ddAlloc(((size_t)markWord_ + 1 + copies_.size()) * glx::kFlagBytes);
+}
+
+void HipPlanExecutor::dmaOp(hipStream_t s, int32_t kind, uint64_t* word, uint64_t value,
+                            int32_t code) {
+  if (!dmaOps_.empty() && (dmaOpsStream_ != s || dmaOps_.size() == (size_t)glx::kFlagOpsMax)) {
+    dmaFlush();
+  }
+  dmaOpsStream_ = s;
+  dmaOps_.push_back(glx::FlagOp{word, value, kind, code});
+}
+
+void HipPlanExecutor::dmaFlush() {
+  if (dmaOps_.empty()) return;
+  glx::FlagOpsParams p{};
+  for (size_t k = 0; k < dmaOps_.size(); k++) p.ops[k] = dmaOps_[k];
+  p.n = (int)dmaOps_.size();
+  p.flagStore = context_->flagStores() ? 1 : 0;
+  p.timeoutTicks = dmaTicks_;
+  p.status = ddStatusDev_;
+  p.claim = ddClaim_;
+  dmaOps_.clear();
+  GLX_HIP_CHECK(glx::launch_flag_ops(p, dmaOpsStream_));
+  transport_.flagKernels++;
+}
+
+// exchange() with its hand-offs on the GPU (executor.h, DMA steps engine).
+// Each wait of the host-issued steps becomes a flag wait on the stream whose
+// next work needs it, each counter the host would bump a flag signal on the
+// stream whose work it announces:
+//   SEND     copy stream: wait for the compute mark (the chunk's producer)
+//            and for the receiver's credit of the previous message; the copy;
+//            signal the receiver's delivery word and our done word
+//   RECV     compute stream: wait for our delivery word
+//   REDUCE / FOLD / COPY  compute stream: wait for the done words of sends
+//            still reading the range it overwrites; the launch
+//   RELEASE  compute stream: signal the sender's credit word
+// Consecutive ops of one stream go out as one kernel, before anything else
+// is enqueued (dmaOp / dmaFlush), so the rank enqueues everything in program
+// order; at the end the compute stream also waits for every copy.  Each
+// stream runs in program order and every wait is for an earlier step of this
+// rank or for a peer's signal the host-issued steps wait for at the same
+// point, so this engine cannot deadlock where those cannot (they, with copies
+// that complete at once, are the program run in order); streams that share a
+// hardware queue -- with each other or with the staging streams -- merely run
+// closer to that order.  (A first version queued a copy's signals until that
+// stream's next copy: in a hardware queue shared with the compute stream they
+// then sat behind a later wait whose peer waited for them -- a cycle the
+// staged host-buffer runs hit, tests/mp_worker.py dmasteps.)
+void HipPlanExecutor::exchangeDma(char* ptr0) {
+  if (!resolved_) resolvePeers();
+  checkDevice();  // an earlier asynchronous call that timed out
+  dmaTicks_ = (uint64_t)effectiveTimeout().count() * (uint64_t)clockKhz_;
+  // calls on different streams (function style) stay in call order
+  if (ddLaunched_ && ddLastStream_ != compute_) {
+    GLX_HIP_CHECK(hipStreamWaitEvent(compute_, ddDone_, 0));
+  }
+  auto code = [](int peer, size_t step) { return (int32_t)(1 + peer + 256 * (1 + (int)step)); };
+  const int self = contextRank_;
+  bool computeSinceMark = true;  // the caller's writes to ptr0 count as compute
+  auto waitSends = [&](int64_t off, int64_t len, size_t step) {
+    for (size_t k = 0; k < inflight_.size();) {
+      const InflightSend& f = inflight_[k];
+      if (f.off < off + len && off < f.off + f.len) {
+        dmaOp(compute_, glx::kFlagWait, dmaWord(copies_[(size_t)f.stream].doneWord), f.done,
+              code(self, step));
+        inflight_.erase(inflight_.begin() + (long)k);
+      } else {
+        k++;
+      }
+    }
+  };
+  auto finalValues = [&](size_t step) {  // host mode: copy the step's final ranges back
+    if (staged_ && !stage_.d2h[step].empty()) {
+      dmaFlush();
+      GLX_HIP_CHECK(hipEventRecord(d2hEvents_[step], compute_));
+      GLX_HIP_CHECK(hipStreamWaitEvent(d2h_, d2hEvents_[step], 0));
+      copyBack(stage_.d2h[step]);
+    }
+  };
+  auto h2d = [&](hipStream_t st, int& waited, int64_t off, int64_t len) {
+    dmaFlush();  // (a fed run may block here until the range is fed)
+    waitH2D(st, waited, off, len);
+  };
+  const auto& steps = plan_.steps;
+  for (size_t i = 0; i < steps.size(); i++) {
+    const glx::Step& s = steps[i];
+    switch (s.kind) {
+      case glx::SEND: {
+        OutChan& oc = out_[stepChan_[i]];
+        const uint64_t n = ++oc.sent;
+        CopyStream& cs = copies_[(size_t)oc.stream];
+        if (computeSinceMark) {  // the chunk may have been produced by compute work
+          dmaOp(compute_, glx::kFlagSignal, dmaWord(markWord_), ++marks_);
+          computeSinceMark = false;
+        }
+        if (cs.waitedMark != marks_) {
+          dmaOp(cs.s, glx::kFlagWait, dmaWord(markWord_), marks_, code(self, i));
+          cs.waitedMark = marks_;
+        }
+        // one receive region per channel: message n lands once the receiver
+        // has consumed message n - 1
+        if (n > 1) {
+          dmaOp(cs.s, glx::kFlagWait, dmaWord(oc.creditWord), n - 1, code(oc.peer, i));
+        }
+        if (staged_) h2d(cs.s, cs.h2dWaited, s.off, s.len);
+        dmaFlush();
+        const size_t nbytes = (size_t)s.len * esize_;
+        if (nbytes > 0) {
+          issueCopy(landing(peerBlocks_[oc.peer], s.dst_off, s.off, s.len),
+                    ptr0 + (size_t)s.off * esize_, nbytes, oc, cs.s);
+        }
+        dmaOp(cs.s, glx::kFlagSignal, oc.devDelivery, n);
+        dmaOp(cs.s, glx::kFlagSignal, dmaWord(cs.doneWord), ++cs.copies);
+        InflightSend f{s.off, s.len, nullptr};
+        f.stream = oc.stream;
+        f.done = cs.copies;
+        inflight_.push_back(f);
+        break;
+      }
+      case glx::RECV: {
+        InChan& ic = in_[stepChan_[i]];
+        dmaOp(compute_, glx::kFlagWait, dmaWord(ic.deliveryWord), ++ic.received,
+              code(ic.peer, i));
+        break;
+      }
+      case glx::REDUCE:
+      case glx::COPY: {
+        waitSends(s.off, s.len, i);
+        if (staged_) h2d(compute_, computeH2dWaited_, s.off, s.len);
+        dmaFlush();
+        char* dst = ptr0 + (size_t)s.off * esize_;
+        const char* src = landing(blocks_, s.boff, s.off, s.len);
+        if (s.kind == glx::REDUCE) {
+          GLX_HIP_CHECK(
+              glx::launch_reduce(op_, dtype_, dst, dst, src, (size_t)s.len, compute_));
+        } else {  // the landing region is uncached: our copy kernel (exchange())
+          GLX_HIP_CHECK(glx::launch_copy(dst, src, (size_t)s.len * esize_, compute_));
+        }
+        computeSinceMark = true;
+        finalValues(i);
+        break;
+      }
+      case glx::FOLD: {
+        size_t last = i;  // consecutive FOLDs of one kind: one batched launch
+        while (last + 1 < steps.size() && steps[last + 1].kind == glx::FOLD &&
+               steps[last + 1].flags == s.flags) {
+          last++;
+        }
+        const bool rev = (s.flags & glx::kFoldLeft) == 0;
+        const bool whole = (s.flags & glx::kFoldWhole) != 0;
+        std::vector<glx::FoldSpec> specs;
+        for (size_t q = i; q <= last; q++) {
+          const glx::Step& f = steps[q];
+          waitSends(f.off, f.len, q);
+          if (staged_) h2d(compute_, computeH2dWaited_, f.off, f.len);
+          glx::FoldSpec spec;
+          spec.dst = ptr0 + (size_t)f.off * esize_;
+          spec.n = (size_t)f.len;
+          for (int64_t r : plan_.folds[(size_t)f.boff]) {
+            if (r < 0) {
+              spec.srcs.push_back(spec.dst);
+            } else if (whole) {
+              spec.srcs.push_back(landing(blocks_, r, 0) + (size_t)f.off * esize_);
+            } else {
+              spec.srcs.push_back(landing(blocks_, r, f.off, f.len));
+            }
+          }
+          spec.k = (int)spec.srcs.size();
+          specs.push_back(std::move(spec));
+        }
+        dmaFlush();
+        if (specs.size() == 1) {
+          const glx::FoldSpec& f = specs[0];
+          GLX_HIP_CHECK(
+              glx::launch_reduce_n(op_, dtype_, f.dst, f.srcs.data(), f.k, f.n, compute_, rev));
+        } else {
+          GLX_HIP_CHECK(glx::launch_reduce_n_batch(op_, dtype_, specs, compute_, rev));
+        }
+        computeSinceMark = true;
+        for (size_t q = i; q <= last; q++) finalValues(q);
+        i = last;
+        break;
+      }
+      case glx::RELEASE: {
+        InChan& ic = in_[stepChan_[i]];
+        dmaOp(compute_, glx::kFlagSignal, ic.devCredit, ++ic.consumed);
+        break;
+      }
+      default:
+        GLX_ENFORCE(false, "bad plan step kind ", s.kind);
+    }
+  }
+  // the caller's stream must not run ahead of copies still reading ptr0
+  for (auto& cs : copies_) {
+    if (cs.copies > 0) {
+      dmaOp(compute_, glx::kFlagWait, dmaWord(cs.doneWord), cs.copies, code(self, steps.size()));
+    }
+  }
+  dmaFlush();
+  inflight_.clear();
+  if (staged_ || fnCalls_) {  // for a later call on another stream
+    GLX_HIP_CHECK(hipEventRecord(ddDone_, compute_));
+    transport_.doneEvents++;
+  }
+  ddLaunched_ = true;
+  ddLastStream_ = compute_;
+}
+
 void HipPlanExecutor::exchange(char* ptr0) {
+  if (engine_ == kEngineDmaSteps) {
+    exchangeDma(ptr0);
+    return;
+  }
   if (engine_ != kEngineSteps) {
     runDevice(ptr0);
     return;
@@ -1036,34 +1315,7 @@ void HipPlanExecutor::exchange(char* ptr0) {
               cs.waitedMark = markEpoch_;
             }
             if (staged_) waitH2D(cs.s, cs.h2dWaited, s.off, s.len);
-            hipError_t ce = hipErrorUnknown;
-            if (copyEngine_ == kCopyKernel) {
-              ce = glx::launch_copy(dst + at, src + at, len, cs.s);
-              GLX_HIP_CHECK(ce);
-              transport_.kernelCopies++;
-            } else if (peerCopyOk_ && oc.peerDevice >= 0 && oc.peerDevice != device_) {
-              ce = hipMemcpyPeerAsync(dst + at, oc.peerDevice, src + at, device_, len, cs.s);
-              if (ce == hipSuccess) {
-                transport_.peerCopies++;
-              } else {
-                (void)hipGetLastError();
-                // e.g. an IPC mapping the peer API rejects: the copy still
-                // crosses xGMI (the destination is the peer's memory), now as
-                // a plain device copy; say so once and count every one
-                peerCopyOk_ = false;
-                std::fprintf(stderr,
-                             "[gloo_amd] rank %d: hipMemcpyPeerAsync to device %d refused "
-                             "(%s: %s); peer copies of this algorithm use hipMemcpyAsync\n",
-                             contextRank_, oc.peerDevice, hipGetErrorName(ce),
-                             hipGetErrorString(ce));
-              }
-            }
-            if (ce != hipSuccess) {
-              GLX_HIP_CHECK(hipMemcpyAsync(dst + at, src + at, len, hipMemcpyDeviceToDevice,
-                                           cs.s));
-              transport_.deviceCopies++;
-            }
-            transport_.bytes += (int64_t)len;
+            issueCopy(dst + at, src + at, len, oc, cs.s);
             GLX_TRACE("r%d   copy part %d issued (%zu bytes)", contextRank_, j, len);
             hipEvent_t ev = events_[i * (size_t)split_ + (size_t)j];
             GLX_HIP_CHECK(hipEventRecord(ev, cs.s));

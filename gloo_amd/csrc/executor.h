@@ -97,6 +97,7 @@ class HipPlanExecutor : public Algorithm {
     int64_t hostFolds = 0;      // local reduces done on the host (kOnDeviceThreshold)
     int64_t doneEvents = 0;     // hipEventRecords after a run's work (each costs
                                 // the stream several microseconds)
+    int64_t flagKernels = 0;    // DMA steps engine: flag-op launches (hand-offs)
   };
   const TransportStats& transportStats() const { return transport_; }
   // Record `ev` after this algorithm's last enqueued work: the compute
@@ -137,6 +138,10 @@ class HipPlanExecutor : public Algorithm {
     uint64_t waitedMark = 0;      // last compute mark this stream waited on
     hipEvent_t last = nullptr;    // last copy recorded in the current run
     int h2dWaited = -1;           // host mode: last H2D piece waited on this run
+    // DMA steps engine: this stream's done word (copies completed, counted
+    // across runs)
+    uint32_t doneWord = 0;
+    uint64_t copies = 0;
   };
   struct InChan {  // peer -> this rank
     int peer, tag;
@@ -167,6 +172,8 @@ class HipPlanExecutor : public Algorithm {
   struct InflightSend {
     int64_t off, len;
     hipEvent_t event;
+    int stream = -1;    // DMA steps engine: the copy stream and its done count
+    uint64_t done = 0;  // once this send's copy completed
   };
 
   void publish();
@@ -182,6 +189,36 @@ class HipPlanExecutor : public Algorithm {
   char* landing(const std::vector<ScratchBlock>& blocks, int64_t boff, int64_t off,
                 int64_t len = -1) const;
   void exchange(char* ptr0);
+  // One SEND's bytes (or one split part of them) to oc's peer on stream s:
+  // the copy kernel, hipMemcpyPeerAsync, or hipMemcpyAsync (same device, or
+  // after the peer API refused a mapping)
+  void issueCopy(char* dst, const char* src, size_t len, OutChan& oc, hipStream_t s);
+  // DMA steps engine (kEngineDmaSteps): the host-issued program -- the same
+  // copies on the copy streams, the same reduce launches on the compute
+  // stream -- with every hand-off made on the GPU by flag-op kernels
+  // (kernels.h FlagOpsParams) instead of by the host, so run() only enqueues.
+  // Flag words, one per 128-byte line, in one uncached block peers map
+  // (ddBlocks_[0]): our in-channels' delivery words, our out-channels' credit
+  // words, the compute mark, each copy stream's done word; all count across
+  // runs.
+  void setupDmaSteps();
+  void exchangeDma(char* ptr0);
+  uint64_t* dmaWord(uint32_t w) const {
+    return reinterpret_cast<uint64_t*>(ddBlocks_[0]) + (size_t)w * glx::kFlagStride;
+  }
+  // Flag ops wait in ONE list, for one stream at a time, and go out as a
+  // kernel before anything else is enqueued: on any stream, or by the host
+  // (a flush whenever the next op or enqueue is for another stream).  So every
+  // rank enqueues its ops in program order, and streams that share a hardware
+  // queue run them in that order -- a signal queued behind a later wait of
+  // another stream could hold up a peer that this wait is for.
+  void dmaOp(hipStream_t s, int32_t kind, uint64_t* word, uint64_t value, int32_t code = 0);
+  void dmaFlush();
+  std::vector<glx::FlagOp> dmaOps_;
+  hipStream_t dmaOpsStream_ = nullptr;
+  uint32_t markWord_ = 0;
+  uint64_t marks_ = 0;     // compute marks signalled
+  uint64_t dmaTicks_ = 0;  // the current run's wait timeout in s_memrealtime ticks
   std::chrono::milliseconds effectiveTimeout() const {
     return timeout_.count() > 0 ? timeout_ : context_->getTimeout();
   }  // the plan's steps on ptr0 (contextSize_ > 1)
@@ -415,7 +452,13 @@ class HipPlanExecutor : public Algorithm {
 
  public:
   static constexpr int kEngineSteps = 0, kEngineOneShot = 1, kEngineTwoShot = 2,
-                       kEngineDevSteps = 3;
+                       kEngineDevSteps = 3, kEngineDmaSteps = 4;
+  // Whether the DMA steps engine can run on this context: not for rank
+  // threads sharing a device (their streams share the process's hardware
+  // queues, where one rank's flag wait would hold up a peer's copy it waits
+  // for), not under the device-engine mode "off".  Processes sharing a GPU
+  // may: a flag wait holds one wave, not the GPU's CUs.
+  static bool dmaStepsAvailable(const Context& ctx);
   // Whether device-driven engines can run on this context:
   // deviceEnginesRule over the context's endpoints and setDeviceEngines.
   static bool deviceEnginesAvailable(const Context& ctx);
@@ -472,9 +515,10 @@ class HipPlanExecutor : public Algorithm {
   static int deviceSync();
   static constexpr bool kAutoNarrow = true;
   // 1 when the device engine runs the narrow release / acquire, 0 system
-  // scope, -1 host-issued steps
+  // scope, -1 host-issued steps (and the DMA steps engine: its flags follow
+  // completed stream work, no fences)
   int syncMode() const {
-    return engine_ == kEngineSteps
+    return engine_ == kEngineSteps || engine_ == kEngineDmaSteps
                ? -1
                : (engine_ == kEngineDevSteps ? pk_.narrow
                                               : (engine_ == kEngineOneShot ? os_.narrow : ts_.narrow));

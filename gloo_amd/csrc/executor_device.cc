@@ -51,7 +51,10 @@ void HipPlanExecutor::setMeshEngine(int engine) {
 int HipPlanExecutor::meshEngine() { return g_mesh_engine.load(); }
 
 void HipPlanExecutor::setStepsEngine(int engine) {
-  g_steps_engine.store(engine < 0 ? -1 : (engine == kEngineSteps ? engine : kEngineDevSteps));
+  g_steps_engine.store(engine < 0 ? -1
+                                  : (engine == kEngineSteps || engine == kEngineDmaSteps
+                                         ? engine
+                                         : kEngineDevSteps));
 }
 
 int HipPlanExecutor::stepsEngine() { return g_steps_engine.load(); }
@@ -144,9 +147,20 @@ bool HipPlanExecutor::deviceEnginesAvailable(const Context& ctx) {
                            ctx.ranksShareDevice(), ctx.maxHwQueues());
 }
 
+bool HipPlanExecutor::dmaStepsAvailable(const Context& ctx) {
+  return ctx.size >= 2 && g_device_engines.load() != kDevEnginesOff && !ctx.ranksShareDevice();
+}
+
 // The inputs are the same on every rank, so every rank makes the same choice
 // (and publish/resolve checks that they did).
 int HipPlanExecutor::engineFor(const Context& ctx, int algo, int64_t count, int esize) {
+  const bool stepsAlgo = algo == glx::ALGO_RING_CHUNKED || algo == glx::ALGO_HALVING_DOUBLING ||
+                         algo == glx::ALGO_FN_RING || algo == glx::ALGO_FN_BCUBE ||
+                         algo == glx::ALGO_RING || algo == glx::ALGO_BCUBE;
+  // the DMA steps engine only when asked for (glx_set_steps_engine)
+  if (count > 0 && stepsAlgo && stepsEngine() == kEngineDmaSteps) {
+    return dmaStepsAvailable(ctx) ? kEngineDmaSteps : kEngineSteps;
+  }
   if (count <= 0 || !deviceEnginesAvailable(ctx)) return kEngineSteps;
   if (algo == glx::ALGO_RING_CHUNKED_REPL || algo == glx::ALGO_FN_RING_REPL) {
     return kEngineOneShot;
@@ -187,6 +201,8 @@ void HipPlanExecutor::setupDevice() {
     setupOneShot();
   } else if (engine_ == kEngineTwoShot) {
     setupTwoShot();
+  } else if (engine_ == kEngineDmaSteps) {
+    setupDmaSteps();
   } else {
     setupDevSteps();
   }
@@ -554,7 +570,9 @@ void HipPlanExecutor::checkDevice() {
     if (step >= 0 && (size_t)step < plan_.steps.size()) {
       const glx::Step& s = plan_.steps[(size_t)step];
       where = std::string(", ") + (s.kind == glx::SEND ? "credit for send" : "receive") +
-              " step " + std::to_string(step) + " of run " + std::to_string(devRuns_ - 1);
+              " step " + std::to_string(step) +
+              (engine_ == kEngineDmaSteps ? std::string(" (DMA steps engine)")
+                                          : " of run " + std::to_string(devRuns_ - 1));
     }
     const volatile uint64_t* d = reinterpret_cast<const volatile uint64_t*>(ddStatus_);
     // The flag words as the host reads them now (the kernel has finished):

@@ -205,6 +205,35 @@ struct PlanKernelParams {
 };
 hipError_t launch_plan_kernel(int op, int dtype, const PlanKernelParams& p, hipStream_t s);
 
+// Stream-ordered flag operations of the DMA steps engine (engine dmasteps,
+// executor.cc exchange): the host-issued program's copies (hipMemcpyPeerAsync
+// on the copy streams) and reduce launches, with every hand-off between them
+// -- a copy waiting for the receiver's credit or for the reduce that produced
+// its chunk, a reduce waiting for its message, the credit back to the sender
+// -- made on the GPU by this one-wave kernel on the stream it orders, instead
+// of by the host.  Lane 0 performs the ops in order: kFlagWait waits (bounded)
+// until *word >= value, kFlagSignal writes value into word (a flag word in
+// this rank's or a peer's uncached flag block).  The stream's earlier work
+// has completed when the kernel starts (stream order; its writes are visible
+// agent-wide), so a signal publishes it without a fence of its own.
+constexpr int kFlagOpsMax = 8;
+constexpr int32_t kFlagWait = 0, kFlagSignal = 1;
+struct FlagOp {
+  uint64_t* word;
+  uint64_t value;
+  int32_t kind;  // kFlagWait / kFlagSignal
+  int32_t code;  // wait: status code on timeout, 1 + peer + 256 * (1 + step)
+};
+struct FlagOpsParams {
+  FlagOp ops[kFlagOpsMax];
+  int n;
+  int flagStore;          // 1: signals are stores (Context::flagStores), else exchanges
+  uint64_t timeoutTicks;  // s_memrealtime ticks, each wait from the kernel's start
+  int* status;            // host-visible: a timeout's code; nonzero stops every wait
+  int* claim;             // device word: the first timed-out wait reports
+};
+hipError_t launch_flag_ops(const FlagOpsParams& p, hipStream_t s);
+
 // Workgroups of a device-engine kernel (kernel 0 = one-shot, 1 = two-shot,
 // 2 = plan kernel, 3 = plan kernel for programs without FOLD steps) for
 // (op, dtype) that fit on the current device at once

@@ -854,6 +854,36 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
   }
 }
 
+// ---- flag operations of the DMA steps engine (kernels.h FlagOpsParams) ------
+
+// One wave; lane 0 walks the ops in order.  A wait polls memory-side
+// (get_flag) with a short sleep, gives up after the timeout (reported like
+// the device engines' waits) or as soon as the status word is nonzero (another
+// wait gave up, or the host saw a peer exit): the ops after it are skipped, so
+// no signal claims work that did not happen, and the stream drains.
+__global__ __launch_bounds__(64) void flag_ops_kernel(FlagOpsParams p) {
+  if (threadIdx.x != 0) return;
+  const uint64_t start = __builtin_amdgcn_s_memrealtime();
+  const volatile int* status = reinterpret_cast<const volatile int*>(p.status);
+  if (*status != 0) return;
+  for (int i = 0; i < p.n; i++) {
+    const FlagOp& o = p.ops[i];
+    if (o.kind == kFlagSignal) {
+      put_flag(o.word, o.value, p.flagStore != 0);
+      continue;
+    }
+    uint64_t v;
+    for (uint32_t spin = 1; (v = get_flag(o.word)) < o.value; spin++) {
+      if (__builtin_amdgcn_s_memrealtime() - start > p.timeoutTicks) {
+        report_timeout(p.status, p.claim, o.code, v, o.value);
+        return;
+      }
+      if ((spin & 127) == 0 && *status != 0) return;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+}
+
 // ---- launch -------------------------------------------------------------------
 
 template <typename T>
@@ -1023,6 +1053,20 @@ hipError_t launch_twoshot(int op, int dtype, const TwoShotParams& p, hipStream_t
     case GLX_BFLOAT16: return launch_ts_op<bf16_t>(op, p, s);
   }
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_flag_ops(const FlagOpsParams& p, hipStream_t s) {
+  if (p.n < 1 || p.n > kFlagOpsMax || p.status == nullptr || p.claim == nullptr) {
+    return hipErrorInvalidValue;
+  }
+  for (int i = 0; i < p.n; i++) {
+    if (p.ops[i].word == nullptr ||
+        (p.ops[i].kind != kFlagWait && p.ops[i].kind != kFlagSignal)) {
+      return hipErrorInvalidValue;
+    }
+  }
+  hipLaunchKernelGGL(flag_ops_kernel, dim3(1), dim3(64), 0, s, p);
+  return hipGetLastError();
 }
 
 }  // namespace glx

@@ -245,7 +245,8 @@ class Event {
 
 // How an algorithm's messages moved (glx_algorithm_transport_stats).
 struct TransportStats {
-  int64_t peerCopies, deviceCopies, kernelCopies, deviceKernels, bytes, hostFolds, doneEvents;
+  int64_t peerCopies, deviceCopies, kernelCopies, deviceKernels, bytes, hostFolds, doneEvents,
+      flagKernels;
 };
 
 namespace detail {
@@ -269,7 +270,7 @@ class DeviceAllreduce : public Algorithm {
   ~DeviceAllreduce() override { glx_algorithm_destroy(a_); }
   void run() override { check(glx_algorithm_run(a_), "run"); }
   int64_t bytesSentPerRun() const { return glx_algorithm_bytes_sent(a_); }
-  // GLX_ENGINE_STEPS / _ONESHOT / _TWOSHOT / _DEVSTEPS (glx.h)
+  // GLX_ENGINE_STEPS / _ONESHOT / _TWOSHOT / _DEVSTEPS / _DMASTEPS (glx.h)
   int engine() const { return glx_algorithm_engine(a_); }
   // Host buffer fed from a transport: runFed() runs while feed() (any
   // thread) reports which elements have arrived; doneRanges() lists the
@@ -293,9 +294,9 @@ class DeviceAllreduce : public Algorithm {
   // record `ev` at the end of the last run's work (streams[0] with streams)
   void record(Event& ev) { check(glx_algorithm_record(a_, ev.handle()), "record"); }
   TransportStats transportStats() const {
-    int64_t o[7] = {0};
-    glx_algorithm_transport_stats(a_, o, 7);
-    return TransportStats{o[0], o[1], o[2], o[3], o[4], o[5], o[6]};
+    int64_t o[8] = {0};
+    glx_algorithm_transport_stats(a_, o, 8);
+    return TransportStats{o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7]};
   }
 
  private:
@@ -321,8 +322,9 @@ inline void setDeviceEngines(int mode) { check(glx_set_device_engines(mode), "se
 inline int deviceEngines() { return glx_get_device_engines(); }
 // GLX_ENGINE_TWOSHOT (default) or GLX_ENGINE_STEPS for the MESH schedule.
 inline void setMeshEngine(int engine) { check(glx_set_mesh_engine(engine), "setMeshEngine"); }
-// GLX_ENGINE_DEVSTEPS (default) or GLX_ENGINE_STEPS for RING,
-// halving-doubling, bcube and the function-style ring.
+// -1 (automatic, default), GLX_ENGINE_DEVSTEPS, GLX_ENGINE_STEPS or
+// GLX_ENGINE_DMASTEPS for RING, halving-doubling, bcube and the
+// function-style ring.
 inline void setStepsEngine(int engine) { check(glx_set_steps_engine(engine), "setStepsEngine"); }
 
 namespace detail {

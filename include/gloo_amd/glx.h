@@ -185,8 +185,11 @@ int glx_device_engines_rule(int mode, int ranks, int ranks_per_device, int threa
  * schedules for algorithms created afterwards, when device-driven engines
  * are available: -1 = automatic (default: the plan kernel -- at every size
  * with one rank per GPU, up to 32 MiB per rank when ranks share a GPU,
- * host-issued steps above), GLX_ENGINE_DEVSTEPS (the plan kernel) or
- * GLX_ENGINE_STEPS (host-issued steps). */
+ * host-issued steps above), GLX_ENGINE_DEVSTEPS (the plan kernel),
+ * GLX_ENGINE_STEPS (host-issued steps) or GLX_ENGINE_DMASTEPS (the
+ * host-issued program -- hipMemcpyPeerAsync on side streams, reduce kernels --
+ * with its hand-offs made on the GPU; chosen whenever it can run: not for rank
+ * threads sharing a device, not under device-engine mode "off"). */
 int glx_set_steps_engine(int engine);
 /* Cache policy of the plan kernel's own loads and stores for algorithms
  * created afterwards: -1 automatic (default: plain, except nontemporal loads
@@ -372,9 +375,12 @@ int glx_allreduce(glx_context* ctx, int algorithm, int dtype, int op,
                   int num_outputs, size_t elements, uint32_t tag,
                   size_t max_segment_size, int64_t timeout_ms, glx_stream_t stream);
 
-/* Algorithm::run() (gloo/algorithm.h:26).  With streams and a device engine
- * (glx_algorithm_engine != GLX_ENGINE_STEPS) the call only enqueues one
- * kernel on streams[0] and can be captured into a HIP graph
+/* Algorithm::run() (gloo/algorithm.h:26).  With streams and the
+ * GLX_ENGINE_DMASTEPS engine the call only enqueues (copies, reduce and flag
+ * kernels on streams[0] and the algorithm's copy streams; message numbers
+ * are the host's, so it is not graph-capturable).  With streams and a
+ * one-kernel device engine (GLX_ENGINE_ONESHOT, _TWOSHOT, _DEVSTEPS) the
+ * call only enqueues one kernel on streams[0] and can be captured into a HIP graph
  * (hipStreamBeginCapture on streams[0]) after one eager run: the kernels
  * keep their run count / epoch on the device, so every replay is one more
  * run on that rank, in sequence with eager runs.  Runs and replays of one
@@ -426,6 +432,13 @@ int64_t glx_algorithm_bytes_sent(glx_algorithm* alg);
  * function-style ring) run as ONE device-driven kernel per rank that walks
  * the schedule's step program (the plan kernel). */
 #define GLX_ENGINE_DEVSTEPS 3
+/* GLX_ENGINE_DMASTEPS = the host-issued steps' copies (hipMemcpyPeerAsync on
+ * per-peer side streams) and reduce launches, enqueued by run() in one pass:
+ * every wait between them -- a copy for the receiver's credit and for the
+ * reduce that produced its chunk, a reduce for its message -- is a one-wave
+ * flag kernel on the waiting stream, every counter a flag word written by
+ * one, instead of the host's progress loop (glx_set_steps_engine). */
+#define GLX_ENGINE_DMASTEPS 4
 int glx_algorithm_engine(glx_algorithm* alg);
 /* 1 when the algorithm's plan kernel runs nontemporal loads and write-through
  * stores (glx_set_engine_streams), else 0. */
@@ -443,10 +456,11 @@ int glx_algorithm_sync(glx_algorithm* alg);
  * multi-pointer reduces done on the host: host buffers below
  * kOnDeviceThreshold = 256 KiB, gloo/algorithm.cc:16), done_events (event
  * records after a run's work: none for run() on a device engine, whose stream
- * is fixed -- each record costs the stream microseconds per call)}.  The
+ * is fixed -- each record costs the stream microseconds per call),
+ * flag_kernels (GLX_ENGINE_DMASTEPS: flag-op launches, the hand-offs)}.  The
  * peer-copy analog of the reference's transport byte counters and of its
  * intra-process peer copies (gloo/cuda_collectives_native.h:205-276).  Fills
- * min(cap, 7) fields (cap >= 6); returns that count, or -1. */
+ * min(cap, 8) fields (cap >= 6); returns that count, or -1. */
 int glx_algorithm_transport_stats(glx_algorithm* alg, int64_t* out, int cap);
 void glx_algorithm_destroy(glx_algorithm* alg);
 

@@ -12,6 +12,8 @@ algo: ring_chunked | halving_doubling | ring_chunked_mesh (class algorithms)
       through the plan kernel: dtypes x ops x sizes, device and host buffers,
       repeated runs; prints per-op latencies of the plan kernel vs the
       host-issued steps)
+      dmasteps (the same cases through the DMA steps engine: the host-issued
+      program's copies and reduce launches with on-GPU hand-offs)
       devtimeout (rank 0 runs both device engines while the other ranks never
       call run(): its kernels must give up after the timeout and run() must
       raise IoException)
@@ -58,6 +60,8 @@ def main():
         return run_killpeer(store_dir, rank, size, *algo.split(":")[1:])
     if algo == "devsteps":
         return run_devsteps(store_dir, rank, size)
+    if algo == "dmasteps":
+        return run_devsteps(store_dir, rank, size, eng="dma")
     if algo == "churn":
         return run_churn(store_dir, rank, size)
     if algo.startswith("scale:"):
@@ -199,7 +203,8 @@ def run_killpeer(store_dir, rank, size, engine, when):
     """TransportMultiProcTest.IoErrors (gloo/test/transport_test.cc:53-110):
     rank 0 is SIGKILLed; the survivors' next run() must raise IoException
     within 2x the timeout.  engine: host (host-issued ring steps), device
-    (the ring's plan kernel), twoshot (the mesh kernel).  when: idle (rank 0
+    (the ring's plan kernel), dma (the DMA steps engine), twoshot (the mesh
+    kernel).  when: idle (rank 0
     dies while the others are already waiting in run()) or mid (rank 0 dies
     while its own run() is in flight)."""
     import os
@@ -224,7 +229,8 @@ def run_killpeer(store_dir, rank, size, engine, when):
         gloo_amd.set_steps_engine(engine)
         alg = gloo_amd.AllreduceRingChunked(ctx, [buf], schedule="ring")
         gloo_amd.set_steps_engine("auto")
-    want = {"host": "steps", "device": "devsteps", "twoshot": "twoshot"}[engine]
+    want = {"host": "steps", "device": "devsteps", "dma": "dmasteps",
+            "twoshot": "twoshot"}[engine]
     ok = alg.engine() == want
     if not ok:
         print("engine %s, expected %s" % (alg.engine(), want))
@@ -285,7 +291,7 @@ def run_churn(store_dir, rank, size):
         return len(os.listdir("/proc/self/fd"))
 
     kinds = [("replicated", "auto"), ("mesh", "auto"), ("ring", "device"), ("ring", "host"),
-             ("hd", "device"), ("hd", "host")]
+             ("hd", "device"), ("hd", "host"), ("ring", "dma"), ("hd", "dma")]
     sizes = [1000, 4096, 65539, 12345, 1 << 16, 777]
     bad, fds = [], []
     for it in range(36):
@@ -344,7 +350,7 @@ def run_devsteps(store_dir, rank, size, eng="device"):
         return np.array_equal(np.ascontiguousarray(got).view(np.uint8),
                               np.ascontiguousarray(exp).view(np.uint8))
 
-    label = "devsteps" if eng == "device" else eng
+    label = {"device": "devsteps", "dma": "dmasteps"}.get(eng, eng)
     MESH = 100  # the mesh schedule (ring_chunked semantics)
 
     def make(kind, buf, op=O.SUM, dt=None):
@@ -1111,8 +1117,8 @@ def run_scale(store_dir, rank, size, group):
             bad.append(("input", c["name"]))
             continue
         ring = c["algo"] == O.RING_CHUNKED
-        engines = [("device", "ring"), ("host", "ring"), ("device", "mesh")] if ring else \
-            [("device", "hd"), ("host", "hd")]
+        engines = [("device", "ring"), ("host", "ring"), ("dma", "ring"), ("device", "mesh")] \
+            if ring else [("device", "hd"), ("host", "hd"), ("dma", "hd")]
         for eng, sched in engines:
             buf = to_dev(x, dt)
             del_src = None

@@ -379,8 +379,8 @@ def test_multiprocess_ipc(algo):
 
 
 @pytest.mark.parametrize("P,mode", [(P, m) for P in (2, 3, 4)
-                                    for m in ("oneshot", "twoshot", "devsteps")] +
-                         [(8, "devsteps")])
+                                    for m in ("oneshot", "twoshot", "devsteps", "dmasteps")] +
+                         [(8, "devsteps"), (8, "dmasteps")])
 def test_device_engine_multiprocess(P, mode):
     """The replicated (one-shot) and mesh (two-shot) schedules, and the ring,
     halving-doubling and bcube step programs (plan kernel), as one
@@ -388,7 +388,9 @@ def test_device_engine_multiprocess(P, mode):
     peers' kernels push into each other's IPC-mapped uncached regions and
     wait on flags.  Bit-exact with the reference ring's chains for every
     dtype/op, device and host buffers, class and function style, repeated
-    runs, ranges left empty at small sizes (mp_worker.py)."""
+    runs, ranges left empty at small sizes (mp_worker.py).  dmasteps: the
+    same cases through the DMA steps engine (the host-issued program, its
+    hand-offs made on the GPU by flag kernels)."""
     with tempfile.TemporaryDirectory() as d:
         env = rank_env(P)
         procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), mode],
@@ -414,6 +416,7 @@ def test_device_engine_multiprocess(P, mode):
 
 @pytest.mark.parametrize("P,engine,when", [(2, "host", "idle"), (3, "host", "mid"),
                                            (3, "device", "idle"), (3, "device", "mid"),
+                                           (3, "dma", "idle"), (3, "dma", "mid"),
                                            (3, "twoshot", "idle"), (3, "twoshot", "mid")])
 def test_peer_killed_raises_io_exception(P, engine, when):
     """Fault injection as TransportMultiProcTest.IoErrors
@@ -754,6 +757,41 @@ def test_transport_stats_name_the_mechanism():
         st, sent, eng = stats[(r, "kernel")]
         assert st["kernel_copies"] > 0 and st["device_copies"] == 0
         assert st["bytes"] == 3 * sent
+
+
+def test_dma_engine_falls_back_for_threads_sharing_a_device():
+    """Rank threads of one process on one device share its hardware queues,
+    where one rank's flag wait could hold up the very copy of a peer it waits
+    for: asking for the DMA steps engine gives them host-issued steps
+    (HipPlanExecutor::dmaStepsAvailable), with the same bits."""
+    import gloo_amd
+    P, N = 2, 100003
+    ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=25)
+    exp = O.allreduce(O.RING_CHUNKED, O.SUM, O.FLOAT32, ins)
+    store = gloo_amd.rendezvous.HashStore()
+    bufs = [to_dev(ins[r][0], O.FLOAT32) for r in range(P)]
+    torch.cuda.synchronize()
+    engines = {}
+
+    def rank_fn(r):
+        ctx = gloo_amd.rendezvous.Context(r, P, 0)
+        ctx.setTimeout(60)
+        ctx.connectFullMesh(store)
+        alg = gloo_amd.AllreduceRingChunked(ctx, [bufs[r]], schedule="ring")
+        engines[r] = alg.engine()
+        alg.run()
+        alg.close()
+        return True
+
+    gloo_amd.set_steps_engine("dma")
+    try:
+        run_ranks(P, rank_fn, timeout=90)
+    finally:
+        gloo_amd.set_steps_engine("auto")
+    for r in range(P):
+        assert engines[r] == "steps"
+        assert np.array_equal(from_dev(bufs[r], O.FLOAT32).view(np.uint32),
+                              exp[r][0].view(np.uint32))
 
 
 def test_multidev_check_script_on_one_device():

@@ -146,24 +146,26 @@ def _ring_run(t, engine, tr):
             "transport": "x", "tr": tr, "fast": False, "sync": "narrow"}
 
 
-def test_north_star_section_carries_both_rings():
-    """the plan kernel (CU stores) and the host-issued DMA ring
-    both appear, each with its own link fraction, measured-link fraction
-    against the probe of ITS transport, and reference-digest match; the top
-    level repeats the faster one."""
+def test_north_star_section_carries_every_ring():
+    """the plan kernel (CU stores), the host-issued DMA ring
+    and the DMA ring with on-GPU hand-offs all appear, each with its own link
+    fraction, measured-link fraction against the probe of ITS transport, and
+    reference-digest match; the top level repeats the fastest one."""
     S = 256 << 20
     links = {"ring_dma_GBps": 140.0, "ring_kernel_GBps": 120.0}
     runs = {"ring_chunked": _ring_run(3.5e-3, "devsteps", ("dma", 1, 0)),
-            "ring_chunked_host": _ring_run(3.3e-3, "steps", ("dma", 1, 0))}
-    ns = bench.north_star_section(S, 8, runs, links,
-                                  {"ring_chunked": True, "ring_chunked_host": True}, {})
+            "ring_chunked_host": _ring_run(3.4e-3, "steps", ("dma", 1, 0)),
+            "ring_chunked_dma": _ring_run(3.3e-3, "dmasteps", ("dma", 1, 0))}
+    ns = bench.north_star_section(S, 8, runs, links, {a: True for a in runs}, {})
     pk, host = ns["rings"]["ring_chunked"], ns["rings"]["ring_chunked_host"]
-    for b in (pk, host):
+    dma = ns["rings"]["ring_chunked_dma"]
+    for b in (pk, host, dma):
         for k in ("ms_per_step", "link_frac", "measured_link_frac", "reference_digest_match"):
             assert k in b, (k, b)
     assert pk["measured_link"] == "ring_kernel_GBps" and host["measured_link"] == "ring_dma_GBps"
+    assert dma["measured_link"] == "ring_dma_GBps"
     assert abs(pk["measured_link_frac"] - pk["link_GBps"] / 120.0) < 1e-3
-    assert ns["candidate"] == "ring_chunked_host"  # the faster one
+    assert ns["candidate"] == "ring_chunked_dma"  # the fastest one
     # one of them failed: it still appears, with its error
     ns = bench.north_star_section(S, 8, {"ring_chunked": runs["ring_chunked"]}, None, {},
                                   {"ring_chunked_host": "IoException: boom"})
@@ -171,6 +173,9 @@ def test_north_star_section_carries_both_rings():
     assert ns["candidate"] == "ring_chunked" and "measured_link_frac" not in ns
     ns = bench.north_star_section(S, 8, {}, None, {}, {})
     assert "error" in ns and set(ns["rings"]) == set(bench.NS_RINGS)
+    # the opt-in DMA-steps ring appears only when it was timed (or failed)
+    ns = bench.north_star_section(S, 8, {"ring_chunked": runs["ring_chunked"]}, None, {}, {})
+    assert set(ns["rings"]) == set(bench.NS_RINGS)
 
 
 @pytest.mark.parametrize("world", [2, 3, 4, 5, 8])
@@ -211,10 +216,11 @@ def test_candidate_lists_default_is_small():
     # the ring and the mesh both by CU stores and by DMA (the node run's open question)
     assert {"ring_chunked", "ring_chunked_mesh", "ring_chunked_host",
             "ring_chunked_mesh_steps"} <= set(c)
-    assert set(bench.DMA_CANDIDATES) <= set(c)
+    assert set(bench.DMA_CANDIDATES) - set(bench.NS_RINGS_OPT) <= set(c)
     A.candidates = "all"
     c, alts = bench.candidate_lists(A)
     assert "ring_chunked_fast" in c and "ring_chunked_system" in c
+    assert "ring_chunked_dma" in c  # the DMA steps with on-GPU hand-offs (opt-in)
     assert "halving_doubling_host" in alts
 
 
@@ -327,13 +333,13 @@ def _stats(peer=0, device=0, kernel=0, kernels=0, nbytes=0):
 
 def _line(world=8):
     """The N > 1 line's north-star and roofline parts, as bench_multi builds
-    them, for a healthy-looking 3.5 ms plan-kernel ring and a 3.3 ms DMA ring."""
+    them, for a healthy-looking 3.5 ms plan-kernel ring and 3.3 ms DMA rings."""
     S = 256 << 20
     links = {"ring_dma_GBps": 140.0, "ring_kernel_GBps": 120.0}
     runs = {"ring_chunked": _ring_run(3.5e-3, "devsteps", ("dma", 1, 0)),
-            "ring_chunked_host": _ring_run(3.3e-3, "steps", ("dma", 1, 0))}
-    ns = bench.north_star_section(S, world, runs, links,
-                                  {"ring_chunked": True, "ring_chunked_host": True}, {})
+            "ring_chunked_host": _ring_run(3.3e-3, "steps", ("dma", 1, 0)),
+            "ring_chunked_dma": _ring_run(3.3e-3, "dmasteps", ("dma", 1, 0))}
+    ns = bench.north_star_section(S, world, runs, links, {a: True for a in runs}, {})
     return {"value": S / 3.3e-3 / 1e9, "north_star": ns,
             "roofline": {"frac": 0.93, "link_measured": dict(links, frac=0.97)}}
 
@@ -342,6 +348,7 @@ def _node_stats(host_stats):
     return {"ring_chunked": _stats(kernels=24, nbytes=7 << 28),
             "ring_chunked_mesh": _stats(kernels=24, nbytes=7 << 28),
             "ring_chunked_host": host_stats,
+            "ring_chunked_dma": _stats(peer=28 * 24, nbytes=7 << 28),
             "ring_chunked_mesh_steps": _stats(peer=14 * 24, nbytes=7 << 28)}
 
 

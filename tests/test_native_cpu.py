@@ -186,6 +186,23 @@ def test_device_engine_mode_round_trip_and_rejects():
         gloo_amd.device_engines_rule("auto", 4, 5)  # more ranks on a GPU than ranks
 
 
+def test_steps_engine_setter_takes_every_engine_and_rejects_others():
+    """glx_set_steps_engine: automatic, host-issued steps, the plan kernel and
+    the DMA steps engine (GLX_ENGINE_DMASTEPS); anything else is refused."""
+    try:
+        for e in ("host", "device", "dma", "auto"):
+            gloo_amd.set_steps_engine(e)
+        for code in (-1, 0, 3, 4):
+            assert _lib.lib.glx_set_steps_engine(code) == 0
+        for code in (1, 2, 5, -2):
+            with pytest.raises(gloo_amd.EnforceNotMet):
+                gloo_amd.errors.check(_lib.lib.glx_set_steps_engine(code))
+    finally:
+        gloo_amd.set_steps_engine("auto")
+    header = open(os.path.join(ROOT, "include", "gloo_amd", "glx.h")).read()
+    assert "#define GLX_ENGINE_DMASTEPS 4" in header
+
+
 def test_device_engine_mode_from_environment():
     """GLOO_AMD_DEVICE_ENGINES sets the initial mode (the rehearsal harness's
     opt-in); unset means automatic."""

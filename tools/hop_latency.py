@@ -3,7 +3,8 @@
 the host-issued DMA ring's hand-off was argued, not measured).  One process
 per rank (torchrun); the reference's ring data movement (schedule="ring") as
 host-issued steps (hipMemcpyPeerAsync sends, reduce kernels, the host's
-progress loop) and as the plan kernel, at sizes where the bytes cost next to
+progress loop), as the plan kernel, and as the DMA steps engine (the same
+copies and reduce kernels, hand-offs by flag kernels on the GPU), at sizes where the bytes cost next to
 nothing, so the time per allreduce is the ring's chain of dependent hops:
 reduce-scatter P-1 rounds + allgather P-1 rounds, each a transfer that waits
 for the previous one's hand-off.  Reports us per allreduce (max over ranks,
@@ -30,7 +31,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sizes", default="1024,65536,1048576")
     ap.add_argument("--iters", type=int, default=200)
-    ap.add_argument("--engines", default="host_steps,plan_kernel")
+    ap.add_argument("--engines", default="host_steps,plan_kernel,dma_steps")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -49,7 +50,8 @@ def main():
     out = {}
     for n in [int(x) for x in a.sizes.split(",")]:
         row = {}
-        for label, steps in (("host_steps", "host"), ("plan_kernel", "device")):
+        for label, steps in (("host_steps", "host"), ("plan_kernel", "device"),
+                             ("dma_steps", "dma")):
             if label not in a.engines.split(","):
                 continue
             buf = torch.zeros(n, dtype=torch.float32, device="cuda")

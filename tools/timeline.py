@@ -12,9 +12,9 @@ import os
 
 
 def short(name):
-    name = name.split("(")[0]
+    name = name.replace("(anonymous namespace)::", "").split("(")[0]
     for k in ("reduce_kernel", "copy_kernel", "reduce_n_kernel", "plan_kernel", "twoshot_kernel",
-              "oneshot_kernel", "copyBuffer", "elementwise_kernel", "fill"):
+              "oneshot_kernel", "flag_ops_kernel", "copyBuffer", "elementwise_kernel", "fill"):
         if k in name:
             return k
     return name[-40:]
