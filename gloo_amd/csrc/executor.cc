@@ -250,10 +250,13 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
         oc.creditWord = hostSteps ? ctl.allocWord() : 0;
         oc.credit = hostSteps ? ctl.word(oc.creditWord) : nullptr;
         // one copy stream per destination peer: copies to different peers
-        // run concurrently on different xGMI links
+        // run concurrently on different xGMI links.  The DMA steps engine
+        // gives every channel its own (its copies wait on the GPU, so the
+        // ring's two channels to one peer overlap their copies' fixed
+        // start-up costs instead of queueing behind each other)
         oc.stream = copyStreams ? -1 : 0;
         for (const auto& o : out_) {
-          if (copyStreams && o.peer == oc.peer) oc.stream = o.stream;
+          if (copyStreams && o.peer == oc.peer && engine_ != kEngineDmaSteps) oc.stream = o.stream;
         }
         if (oc.stream < 0) {
           oc.stream = (int)copies_.size();
@@ -1105,6 +1108,13 @@ void HipPlanExecutor::dmaFlush() {
 // then sat behind a later wait whose peer waited for them -- a cycle the
 // staged host-buffer runs hit, tests/mp_worker.py dmasteps.)
 void HipPlanExecutor::exchangeDma(char* ptr0) {
+  // the message numbers are the host's: a captured run would replay stale
+  // ones (checked first: resolving the peers makes synchronous copies)
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  GLX_HIP_CHECK(hipStreamIsCapturing(compute_, &cap));
+  GLX_ENFORCE(cap == hipStreamCaptureStatusNone,
+              "the DMA steps engine cannot be captured into a HIP graph (its message numbers "
+              "are counted on the host); capture an algorithm on a one-kernel engine");
   if (!resolved_) resolvePeers();
   checkDevice();  // an earlier asynchronous call that timed out
   dmaTicks_ = (uint64_t)effectiveTimeout().count() * (uint64_t)clockKhz_;

@@ -444,6 +444,41 @@ def run_devsteps(store_dir, rank, size, eng="device"):
                 print("LAT rank %d P %d %s elems %d engine %s us %.1f"
                       % (rank, size, label, n, alg.engine(), us), flush=True)
                 alg.close()
+    if eng == "dma":
+        gloo_amd.set_steps_engine("dma")
+        # with a caller's stream run() only enqueues: K runs back to back on
+        # one buffer, one wait at the end; each run reduces the previous
+        # run's result (int32 sums wrap alike on every rank and in the oracle)
+        s = torch.cuda.Stream()
+        n, K = 65539, 5
+        ins = case_inputs(size, n, O.INT32, 1, 0, seed=41)
+        exp = ins[rank][0]
+        cur = ins
+        for _ in range(K):
+            exp = O.allreduce(O.RING_CHUNKED, O.SUM, O.INT32, cur)[rank][0]
+            cur = [[exp.copy()] for _ in range(size)]
+        buf = to_dev(ins[rank][0], O.INT32)
+        torch.cuda.synchronize()
+        alg = gloo_amd.AllreduceRingChunked(ctx, [buf], streams=[s], dtype=O.INT32)
+        for _ in range(K):
+            alg.run()
+        s.synchronize()
+        if alg.engine() != "dmasteps" or not same(from_dev(buf, O.INT32), exp):
+            bad.append(("async stream runs", alg.engine()))
+        # a captured run would replay host-counted message numbers: refused
+        graph = torch.cuda.CUDAGraph()
+        refused = ""
+        try:
+            with torch.cuda.graph(graph, stream=s):
+                alg.run()
+        except gloo_amd.EnforceNotMet as e:
+            refused = str(e)
+        except RuntimeError as e:  # the capture's end after the refusal
+            refused = refused or str(e)
+        if "HIP graph" not in refused:
+            bad.append(("capture not refused", refused[:120]))
+        s.synchronize()
+        alg.close()
     gloo_amd.set_steps_engine("auto")
     gloo_amd.set_mesh_engine("device")
     store.set("done/%d" % rank, b"1")
