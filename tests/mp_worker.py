@@ -459,7 +459,8 @@ def run_devsteps(store_dir, rank, size, eng="device"):
             cur = [[exp.copy()] for _ in range(size)]
         buf = to_dev(ins[rank][0], O.INT32)
         torch.cuda.synchronize()
-        alg = gloo_amd.AllreduceRingChunked(ctx, [buf], streams=[s], dtype=O.INT32)
+        alg = gloo_amd.AllreduceRingChunked(ctx, [buf], streams=[s], dtype=O.INT32,
+                                            schedule="ring")
         for _ in range(K):
             alg.run()
         s.synchronize()
