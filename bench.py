@@ -983,15 +983,16 @@ def element_sweep(torch, dist, gloo_amd, ctx, dev, schedules, dtype):
 
 
 # the ring and the mesh each moved by CUs (the plan / two-shot kernels
-# storing into the peers' slots) and by DMA engines (host-issued
-# hipMemcpyPeerAsync steps): whether CU stores fill an xGMI link is the one
-# thing no one-GPU box can measure, so the first node run times both ways.
-# The ring's DMA steps with on-GPU hand-offs (dmasteps) is opt-in: on the
-# one-GPU box it measured slower than the host-issued steps
+# storing into the peers' slots) and by DMA engines (hipMemcpyPeerAsync
+# steps, the ring's with its hand-offs made by the host and -- dmasteps -- on
+# the GPU): whether CU stores fill an xGMI link, and what a DMA ring's
+# hand-off costs across xGMI, no one-GPU box can measure, so the first node
+# run times every way (on one GPU the dmasteps ring wins over the host's
+# only where its streams get hardware queues of their own, as on the node:
+# DESIGN.md 5d)
 DEFAULT_CANDIDATES = ["ring_chunked", "ring_chunked_mesh", "ring_chunked_host",
-                      "ring_chunked_mesh_steps"]
-EXTRA_CANDIDATES = ["ring_chunked_dma", "ring_chunked_fast", "ring_chunked_system",
-                    "ring_chunked_mesh_system"]
+                      "ring_chunked_dma", "ring_chunked_mesh_steps"]
+EXTRA_CANDIDATES = ["ring_chunked_fast", "ring_chunked_system", "ring_chunked_mesh_system"]
 DMA_CANDIDATES = ("ring_chunked_host", "ring_chunked_dma", "ring_chunked_mesh_steps")
 DEFAULT_ALTS = ["halving_doubling"]
 EXTRA_ALTS = ["halving_doubling_host", "halving_doubling_dma", "halving_doubling_system"]
@@ -1007,9 +1008,10 @@ TRANSPORTS_ALL = [("dma", 1, 0), ("dma", 2, 0), ("dma", 4, 0), ("kernel", 1, 32)
 
 def candidate_lists(args):
     """(candidates timed for `value`, schedules timed beside them).  The
-    default run keeps to five schedules -- the north star's ring on the plan
+    default run keeps to six schedules -- the north star's ring on the plan
     kernel, the mesh on the two-shot kernel, both again as host-issued DMA
-    steps, and halving-doubling on the plan kernel -- each one more chance
+    steps, the ring's DMA steps with on-GPU hand-offs, and halving-doubling
+    on the plan kernel -- each one more chance
     for a first run on new hardware to fail (a failed
     candidate is reported and dropped, the others stand);
     --candidates all adds the opt-in engines and stream policies."""
@@ -1066,8 +1068,8 @@ def measured_link_for(engine, transport_tr, links):
     return "ring_dma_GBps", links.get("ring_dma_GBps")
 
 
-# plan kernel (CU stores), host-issued DMA steps; the DMA steps with on-GPU
-# hand-offs join them when timed (--candidates all or a list naming it)
+# plan kernel (CU stores), host-issued DMA steps, DMA steps with on-GPU
+# hand-offs (reported when timed: the default candidates and --schedule ring)
 NS_RINGS = ("ring_chunked", "ring_chunked_host")
 NS_RINGS_OPT = ("ring_chunked_dma",)
 

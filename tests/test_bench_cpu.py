@@ -211,16 +211,15 @@ def test_candidate_lists_default_is_small():
     class A:
         algo, schedule, candidates, no_alt = "ring_chunked", "auto", "default", False
     c, alts = bench.candidate_lists(A)
-    assert c[0] == "ring_chunked" and len(c) + len(alts) <= 5
+    assert c[0] == "ring_chunked" and len(c) + len(alts) <= 6
     assert not any(x.endswith(("_fast", "_system")) for x in c + alts)
     # the ring and the mesh both by CU stores and by DMA (the node run's open question)
-    assert {"ring_chunked", "ring_chunked_mesh", "ring_chunked_host",
+    assert {"ring_chunked", "ring_chunked_mesh", "ring_chunked_host", "ring_chunked_dma",
             "ring_chunked_mesh_steps"} <= set(c)
-    assert set(bench.DMA_CANDIDATES) - set(bench.NS_RINGS_OPT) <= set(c)
+    assert set(bench.DMA_CANDIDATES) <= set(c)
     A.candidates = "all"
     c, alts = bench.candidate_lists(A)
     assert "ring_chunked_fast" in c and "ring_chunked_system" in c
-    assert "ring_chunked_dma" in c  # the DMA steps with on-GPU hand-offs (opt-in)
     assert "halving_doubling_host" in alts
 
 
