@@ -1115,6 +1115,15 @@ void HipPlanExecutor::exchangeDma(char* ptr0) {
   GLX_ENFORCE(cap == hipStreamCaptureStatusNone,
               "the DMA steps engine cannot be captured into a HIP graph (its message numbers "
               "are counted on the host); capture an algorithm on a one-kernel engine");
+  // a failure part way leaves peers waiting for messages this run will never
+  // send: the algorithm is unusable, and release() stops its queued waits
+  struct Broken {
+    HipPlanExecutor* e;
+    bool done = false;
+    ~Broken() {
+      if (!done) e->broken_ = true;
+    }
+  } broken{this};
   if (!resolved_) resolvePeers();
   checkDevice();  // an earlier asynchronous call that timed out
   dmaTicks_ = (uint64_t)effectiveTimeout().count() * (uint64_t)clockKhz_;
@@ -1275,6 +1284,7 @@ void HipPlanExecutor::exchangeDma(char* ptr0) {
   }
   ddLaunched_ = true;
   ddLastStream_ = compute_;
+  broken.done = true;
 }
 
 void HipPlanExecutor::exchange(char* ptr0) {
