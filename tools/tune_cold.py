@@ -9,7 +9,7 @@ back to back over one pair, where write-through stores win by keeping lines
 in the Infinity Cache; this one asks which shape is best when nothing is
 cached.
 
-    python tools/tune_cold.py [MiB]   (GPU box)
+    python tools/tune_cold.py [MiB] [f32|f16|bf16]   (GPU box)
 """
 import json
 import os
@@ -27,12 +27,20 @@ PAIRS = 4
 
 def main():
     mib = int(sys.argv[1]) if len(sys.argv) > 1 else 256
-    n = (mib << 20) // 4
+    dt = sys.argv[2] if len(sys.argv) > 2 else "f32"
+    tdt = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}[dt]
+    n = (mib << 20) // torch.tensor([], dtype=tdt).element_size()
     g = torch.Generator(device="cuda").manual_seed(7)
-    pairs = [(torch.rand(n, device="cuda", generator=g) * 2 - 1,
-              torch.rand(n, device="cuda", generator=g) * 2 - 1) for _ in range(PAIRS)]
+    pairs = [((torch.rand(n, device="cuda", generator=g) * 2 - 1).to(tdt),
+              (torch.rand(n, device="cuda", generator=g) * 2 - 1).to(tdt)) for _ in range(PAIRS)]
     a0 = pairs[0][0].clone()
-    ref = a0 + pairs[0][1]
+    # the product's own bits once with the shipped defaults (torch rounds the
+    # 16-bit types alike for a sum; fp16's assignment quirk never changes a sum
+    # of values in (-1, 1) -- checked against the default launch instead)
+    pairs[0][0].copy_(a0)
+    gloo_amd.math.sum(pairs[0][0], pairs[0][0], pairs[0][1])
+    torch.cuda.synchronize()
+    ref = pairs[0][0].clone()
     best = None
     for pol in POLICIES:
         for bpc in (8, 16, 32, 64):
@@ -58,7 +66,7 @@ def main():
                     torch.cuda.synchronize()
                     meds.append(e0.elapsed_time(e1) / 40 * 1e3)
                 us = sorted(meds)[2]
-                rec = {"MiB": mib, "policy": POLICIES[pol], "blocks_per_cu": bpc,
+                rec = {"MiB": mib, "dtype": dt, "policy": POLICIES[pol], "blocks_per_cu": bpc,
                        "unroll": unroll, "us": round(us, 2),
                        "TBps": round(3 * (mib << 20) / us / 1e6, 3), "bit_exact": ok}
                 print(json.dumps(rec), flush=True)
