@@ -412,6 +412,15 @@ def multidev_check(torch, timeout=120):
     return json.loads(lines[-1])
 
 
+def reduce_segments(stream_bytes):
+    """Kernel dispatches one glx_reduce call over `stream_bytes` per stream
+    makes (equal segments of at most glx_reduce_segment_bytes(); DESIGN.md
+    4a).  Reads the library without touching a GPU."""
+    from gloo_amd import _lib
+    seg = int(_lib.lib.glx_reduce_segment_bytes())
+    return max(1, -(-stream_bytes // seg))
+
+
 def live_pmc_traffic(args, timeout=90):
     """HBM bytes per launch of the timed reduce kernel, measured in THIS run
     (the figure used to come from a stored pass):
@@ -449,9 +458,13 @@ def live_pmc_traffic(args, timeout=90):
         shutil.rmtree(d, ignore_errors=True)
     fetch_kib, nf = got["fetch"]
     write_kib, nw = got["write"]
-    return {"hbm_bytes_per_launch": int((2 * fetch_kib + write_kib) * 1024),
-            "fetch_bytes": int(2 * fetch_kib * 1024), "write_bytes": int(write_kib * 1024),
-            "dispatches": {"fetch": nf, "write": nw},
+    # a call over more than glx_reduce_segment_bytes() per stream is that
+    # many equal dispatches (the counters are per dispatch): bytes per call
+    seg = reduce_segments(args.size_mib << 20)
+    return {"hbm_bytes_per_launch": int((2 * fetch_kib + write_kib) * 1024 * seg),
+            "fetch_bytes": int(2 * fetch_kib * 1024 * seg),
+            "write_bytes": int(write_kib * 1024 * seg),
+            "dispatches": {"fetch": nf, "write": nw}, "dispatches_per_call": seg,
             "source": "live: rocprofv3 --pmc FETCH_SIZE (x2) and WRITE_SIZE passes of this "
                       "command's kernel loop, run as child processes of this run"}
 

@@ -40,6 +40,7 @@ SIGNATURES = [
     ("glx_copy", _i, [_vp, _vp, _sz, _i, _vp]),
     ("glx_enable_peer", _i, [_i, _i]),
     ("glx_tune_reduce", _i, [_i, _i, _i]),
+    ("glx_reduce_segment_bytes", _sz, []),
     ("glx_set_copy_split", _i, [_i]),
     ("glx_set_pinned_mirror_limit", _i, [_sz]),
     ("glx_device_count", _i, [ctypes.POINTER(_i)]),

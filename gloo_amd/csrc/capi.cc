@@ -181,6 +181,8 @@ int glx_enable_peer(int a, int b) {
   return GLX_OK;
 }
 
+size_t glx_reduce_segment_bytes(void) { return glx::reduce_segment_bytes(); }
+
 int glx_tune_reduce(int unroll, int blocks_per_cu, int nontemporal) {
   if (unroll != 1 && unroll != 2 && unroll != 4 && unroll != 8) {
     return fail(GLX_ERR_INVALID, "glx_tune_reduce: unroll must be 1, 2, 4 or 8");

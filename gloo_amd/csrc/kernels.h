@@ -241,6 +241,11 @@ hipError_t launch_flag_ops(const FlagOpsParams& p, hipStream_t s);
 // resident as a whole.
 int device_engine_resident_blocks(int kernel, int op, int dtype);
 
+// Streams longer than this go out as consecutive launches of the reduce
+// kernel over equal segments of at most this many bytes (reduce_kernels.hip
+// kSegBytes).
+size_t reduce_segment_bytes();
+
 // Tuning knobs of the vector kernel (lanes' unroll depth, grid cap per CU,
 // nontemporal loads/stores: 0/1, -1 = keep).
 void set_reduce_tuning(int unroll, int blocks_per_cu, int nontemporal);

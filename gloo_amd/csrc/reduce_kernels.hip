@@ -331,9 +331,17 @@ size_t grid_for(size_t work_items, int unroll) {
   return blocks;
 }
 
+// Streams longer than this go out as consecutive launches over equal
+// segments of at most this many bytes each (the policy still chosen for the
+// whole stream).  One grid-stride launch over 1 GiB fp32 on the HBM-only loop
+// took 526 us, four launches over 256 MiB segments 497 us (6.12 vs 6.48
+// TB/s; 128 MiB: 502, 512 MiB: 505; at 256 MiB one launch stays best:
+// tools/seg_1GiB.py, profiles/r10/reduce_segments.jsonl).
+constexpr size_t kSegBytes = size_t(256) << 20;
+
 template <typename T, int OP, int UNROLL>
 hipError_t launch_vec(void* dst, const void* a, const void* b, size_t head,
-                      size_t nvec, size_t tail, hipStream_t s) {
+                      size_t nvec, size_t tail, hipStream_t s, int pol) {
   using S = typename Elem<T, OP>::S;
   size_t blocks = grid_for(nvec, UNROLL);
   size_t edge_blocks = (std::max(head, tail) + kBlock - 1) / kBlock;
@@ -344,7 +352,7 @@ hipError_t launch_vec(void* dst, const void* a, const void* b, size_t head,
                        (S*)dst, (const S*)a, (const S*)b, head, nvec, tail);
     return hipGetLastError();
   }
-  switch (policy_for(nvec * 16)) {
+  switch (pol) {
     case kPolPlain:
       hipLaunchKernelGGL((reduce_kernel<T, OP, UNROLL, false, kPolPlain>), grid, block, 0, s,
                          (S*)dst, (const S*)a, (const S*)b, head, nvec, tail);
@@ -376,12 +384,31 @@ hipError_t launch_typed(void* dst, const void* a, const void* b, size_t n,
     if (head > n) head = n;
     size_t nvec = (n - head) / V;
     size_t tail = n - head - nvec * V;
-    switch (g_unroll) {
-      case 1: return launch_vec<T, OP, 1>(dst, a, b, head, nvec, tail, s);
-      case 2: return launch_vec<T, OP, 2>(dst, a, b, head, nvec, tail, s);
-      case 8: return launch_vec<T, OP, 8>(dst, a, b, head, nvec, tail, s);
-      default: return launch_vec<T, OP, 4>(dst, a, b, head, nvec, tail, s);
+    const int pol = policy_for(nvec * 16);  // the whole stream's
+    // equal segments of at most kSegBytes (kSegBytes above): the head goes
+    // with the first, the tail with the last
+    const size_t nseg = (nvec * 16 + kSegBytes - 1) / kSegBytes;
+    const size_t segVec = nseg > 1 ? (nvec + nseg - 1) / nseg : nvec;
+    size_t at = 0;  // elements before this segment's first
+    for (size_t v0 = 0; v0 < nvec || v0 == 0; v0 += segVec) {
+      const size_t nv = std::min(segVec, nvec - v0);
+      const size_t h = v0 == 0 ? head : 0;
+      const size_t t = v0 + nv >= nvec ? tail : 0;
+      S* d = static_cast<S*>(dst) + at;
+      const S* x = static_cast<const S*>(a) + at;
+      const S* y = static_cast<const S*>(b) + at;
+      hipError_t e;
+      switch (g_unroll) {
+        case 1: e = launch_vec<T, OP, 1>(d, x, y, h, nv, t, s, pol); break;
+        case 2: e = launch_vec<T, OP, 2>(d, x, y, h, nv, t, s, pol); break;
+        case 8: e = launch_vec<T, OP, 8>(d, x, y, h, nv, t, s, pol); break;
+        default: e = launch_vec<T, OP, 4>(d, x, y, h, nv, t, s, pol);
+      }
+      if (e != hipSuccess) return e;
+      at += h + nv * V;
+      if (nv == 0) break;  // nvec == 0: the one launch did head and tail
     }
+    return hipSuccess;
   }
   size_t blocks = grid_for(n, 4);
   hipLaunchKernelGGL((reduce_scalar_kernel<T, OP>), dim3((unsigned)blocks),
@@ -626,6 +653,8 @@ hipError_t launch_reduce_n(int op, int dtype, void* dst, const void* const* srcs
   }
   return hipErrorInvalidValue;
 }
+
+size_t reduce_segment_bytes() { return kSegBytes; }
 
 void set_reduce_tuning(int unroll, int blocks_per_cu, int nontemporal) {
   if (unroll == 1 || unroll == 2 || unroll == 4 || unroll == 8) g_unroll = unroll;

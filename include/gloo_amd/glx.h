@@ -131,6 +131,11 @@ int glx_enable_peer(int dev_a, int dev_b);
  * (default: 2 while one stream is at most 256 MiB -- the Infinity Cache's
  * size -- and 1 above). */
 int glx_tune_reduce(int unroll, int blocks_per_cu, int nontemporal);
+/* glx_reduce on more than this many bytes per stream goes out as consecutive
+ * kernel launches over equal segments of at most this size (one grid-stride
+ * launch over 1 GiB streams ran 6 % slower on MI355X): a
+ * profiler sees that many dispatches per call. */
+size_t glx_reduce_segment_bytes(void);
 
 /* Split every peer copy of algorithms created afterwards over k streams per
  * destination (k DMA engines feeding one link; parts >= 1 MiB).  Default 1,

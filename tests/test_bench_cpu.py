@@ -434,3 +434,12 @@ def test_multi_line_value_is_algbw_and_workload_names_the_schedule():
         "allreduce_ring_chunked_mesh_schedule_fp32_256MiB_per_rank"
     assert bench.multi_workload("halving_doubling", "halving_doubling", "f16", 1024) == \
         "allreduce_halving_doubling_f16_1024MiB_per_rank"
+
+
+def test_reduce_segments_follow_the_library():
+    """bench.py scales the per-dispatch PMC bytes by the dispatches one
+    glx_reduce call makes: equal segments of at most
+    glx_reduce_segment_bytes() (256 MiB) per stream."""
+    assert bench.reduce_segments(256 << 20) == 1
+    assert bench.reduce_segments((256 << 20) + 16) == 2
+    assert bench.reduce_segments(1 << 30) == 4

@@ -134,6 +134,37 @@ def test_large_fp32_sum_matches_torch():
     assert torch.equal(a, torch.where(a0 < b, b, a0))
 
 
+def test_segmented_long_streams_match_torch():
+    """Streams over 256 MiB go out as equal segments (reduce_kernels.hip
+    kSegBytes): 600 MiB fp32 at a 4-byte offset (a scalar head, three
+    segments, a scalar tail), out of place and in place -- an element done
+    twice in place would show as a + 2b -- and 520 MiB bf16 in place, all
+    equal to torch's IEEE adds."""
+    import gloo_amd
+    n = (600 << 20) // 4 + 5
+    g = torch.Generator(device="cuda").manual_seed(5)
+    A = torch.rand(n + 1, device="cuda", generator=g) * 2 - 1
+    B = torch.rand(n + 1, device="cuda", generator=g) * 2 - 1
+    a, b = A[1:], B[1:]  # 4 bytes past a 16-byte boundary: a scalar head
+    c = torch.empty_like(A)[1:]
+    gloo_amd.math.sum(c, a, b)
+    torch.cuda.synchronize()
+    assert torch.equal(c, a + b)
+    del c
+    a0 = a.clone()
+    gloo_amd.math.sum(a, a, b)
+    torch.cuda.synchronize()
+    assert torch.equal(a, a0 + b)
+    del A, B, a, b, a0
+    m = (520 << 20) // 2
+    x = (torch.rand(m, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+    y = (torch.rand(m, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+    want = x + y
+    gloo_amd.math.sum(x, x, y)
+    torch.cuda.synchronize()
+    assert torch.equal(x, want)
+
+
 def test_reduce_n_left_fold():
     import gloo_amd
     for dtype in (O.FLOAT32, O.FLOAT16, O.INT32):
