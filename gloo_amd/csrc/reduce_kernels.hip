@@ -449,17 +449,36 @@ hipError_t launch_n_pass(void* dst, const void* const* srcs, int k, size_t n,
   if (head > n) head = n;
   size_t nvec = (n - head) / V;
   size_t tail = n - head - nvec * V;
-  size_t blocks = grid_for(nvec, 4);
-  size_t edge_blocks = (std::max(head, tail) + kBlock - 1) / kBlock;
-  if (blocks < edge_blocks) blocks = edge_blocks;
-  if (use_wt(nvec * 16)) {
-    hipLaunchKernelGGL((reduce_n_kernel<T, OP, 4, REV, true>), dim3((unsigned)blocks),
-                       dim3(kBlock), 0, s, (S*)dst, sp, k, head, nvec, tail);
-  } else {
-    hipLaunchKernelGGL((reduce_n_kernel<T, OP, 4, REV, false>), dim3((unsigned)blocks),
-                       dim3(kBlock), 0, s, (S*)dst, sp, k, head, nvec, tail);
+  const bool wt = use_wt(nvec * 16);  // the whole stream's policy
+  // equal segments of at most kSegBytes, as launch_typed (1 GiB fp32, two
+  // sources: 532 -> 500 us; four: 919 -> 886 us -- tools/seg_fold.py,
+  // profiles/r10/fold_segments.jsonl)
+  const size_t nseg = (nvec * 16 + kSegBytes - 1) / kSegBytes;
+  const size_t segVec = nseg > 1 ? (nvec + nseg - 1) / nseg : nvec;
+  size_t at = 0;  // elements before this segment's first
+  for (size_t v0 = 0; v0 < nvec || v0 == 0; v0 += segVec) {
+    const size_t nv = std::min(segVec, nvec - v0);
+    const size_t h = v0 == 0 ? head : 0;
+    const size_t t = v0 + nv >= nvec ? tail : 0;
+    SrcPtrs q{};
+    for (int j = 0; j < k; j++) q.p[j] = static_cast<const S*>(srcs[j]) + at;
+    S* d = static_cast<S*>(dst) + at;
+    size_t blocks = grid_for(nv, 4);
+    size_t edge_blocks = (std::max(h, t) + kBlock - 1) / kBlock;
+    if (blocks < edge_blocks) blocks = edge_blocks;
+    if (wt) {
+      hipLaunchKernelGGL((reduce_n_kernel<T, OP, 4, REV, true>), dim3((unsigned)blocks),
+                         dim3(kBlock), 0, s, d, q, k, h, nv, t);
+    } else {
+      hipLaunchKernelGGL((reduce_n_kernel<T, OP, 4, REV, false>), dim3((unsigned)blocks),
+                         dim3(kBlock), 0, s, d, q, k, h, nv, t);
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    at += h + nv * V;
+    if (nv == 0) break;  // nvec == 0: the one launch did head and tail
   }
-  return hipGetLastError();
+  return hipSuccess;
 }
 
 // Folds of more than kMaxSrc sources continue from dst in further passes.

@@ -138,8 +138,8 @@ def test_segmented_long_streams_match_torch():
     """Streams over 256 MiB go out as equal segments (reduce_kernels.hip
     kSegBytes): 600 MiB fp32 at a 4-byte offset (a scalar head, three
     segments, a scalar tail), out of place and in place -- an element done
-    twice in place would show as a + 2b -- and 520 MiB bf16 in place, all
-    equal to torch's IEEE adds."""
+    twice in place would show as a + 2b -- the fold of three sources in
+    place, and 520 MiB bf16 in place, all equal to torch's IEEE adds."""
     import gloo_amd
     n = (600 << 20) // 4 + 5
     g = torch.Generator(device="cuda").manual_seed(5)
@@ -155,7 +155,16 @@ def test_segmented_long_streams_match_torch():
     gloo_amd.math.sum(a, a, b)
     torch.cuda.synchronize()
     assert torch.equal(a, a0 + b)
-    del A, B, a, b, a0
+    # the fold kernel (several local pointers) segments alike: a left fold
+    # of three sources into the first, in place
+    C = torch.rand(n + 1, device="cuda", generator=g) * 2 - 1
+    c = C[1:]
+    a.copy_(a0)
+    want = (a0 + b) + c
+    gloo_amd.math.reduce_n(gloo_amd.ReductionType.SUM, a, [a, b, c])
+    torch.cuda.synchronize()
+    assert torch.equal(a, want)
+    del A, B, C, a, b, c, a0, want
     m = (520 << 20) // 2
     x = (torch.rand(m, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
     y = (torch.rand(m, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
