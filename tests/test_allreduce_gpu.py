@@ -453,6 +453,7 @@ def test_peer_killed_raises_io_exception(P, engine, when):
 
 
 @pytest.mark.parametrize("mode,knob", [("devsteps", "GLOO_AMD_FLAG_WRITE=store"),
+                                       ("dmasteps", "GLOO_AMD_FLAG_WRITE=store"),
                                        ("twoshot", "GLOO_AMD_FLAG_WRITE=store"),
                                        ("oneshot", "GLOO_AMD_FLAG_WRITE=store"),
                                        ("devsteps", "GLOO_AMD_FUSE=0"),
