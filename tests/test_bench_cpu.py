@@ -80,6 +80,13 @@ def test_plan_names():
     assert bench.plan_name("ring_chunked_mesh_steps") == "ring_chunked_mesh"
     assert bench.plan_name("ring_chunked_mesh_system") == "ring_chunked_mesh"
     assert bench.plan_name("halving_doubling_host") == "halving_doubling"
+    assert bench.plan_name("ring_chunked_dma") == "ring_chunked"
+    assert bench.plan_name("halving_doubling_dma") == "halving_doubling"
+    assert bench.golden_plan("ring_chunked_dma") == "ring_chunked"
+    # every default and opt-in candidate names a schedule the planner knows
+    for c in bench.DEFAULT_CANDIDATES + bench.EXTRA_CANDIDATES + bench.EXTRA_ALTS:
+        assert bench.plan_name(c) in ("ring_chunked", "ring_chunked_mesh",
+                                      "halving_doubling"), c
 
 
 def test_roofline_byte_counts_ring_p8():
