@@ -951,7 +951,7 @@ def run_soak(store_dir, rank, size, runs, uneven=""):
         return torch.randint(-64, 64, (n,), generator=g, device=dev, dtype=torch.int32)
 
     bufs = {k: torch.empty(n, dtype=torch.float32, device=dev)
-            for k in ("ring", "hd", "mesh", "repl", "ring_host")}
+            for k in ("ring", "hd", "mesh", "repl", "ring_host", "ring_dma", "hd_dma")}
     algs = {
         "ring": gloo_amd.AllreduceRingChunked(ctx, [bufs["ring"]], schedule="ring"),
         "hd": gloo_amd.AllreduceHalvingDoubling(ctx, [bufs["hd"]]),
@@ -963,6 +963,15 @@ def run_soak(store_dir, rank, size, runs, uneven=""):
     try:
         algs["ring_host"] = gloo_amd.AllreduceRingChunked(ctx, [bufs["ring_host"]],
                                                           schedule="ring")
+    finally:
+        gloo_amd.set_steps_engine("auto")
+    # and the DMA steps engine (flag words counting across runs; allowed for
+    # processes sharing a GPU in every mode but "off": its waits hold one wave)
+    gloo_amd.set_steps_engine("dma")
+    try:
+        algs["ring_dma"] = gloo_amd.AllreduceRingChunked(ctx, [bufs["ring_dma"]],
+                                                         schedule="ring")
+        algs["hd_dma"] = gloo_amd.AllreduceHalvingDoubling(ctx, [bufs["hd_dma"]])
     finally:
         gloo_amd.set_steps_engine("auto")
     engines = {k: a.engine() for k, a in algs.items()}

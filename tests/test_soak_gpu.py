@@ -3,7 +3,9 @@ with fresh inputs each run, one process per rank (tests/mp_worker.py soak) --
 the shape of a training job, which the grid tests (a few runs per instance)
 do not reach: the plan kernel's run counter and per-run message numbers, the
 one- and two-shot kernels' epochs and double-buffered slots, across many
-kernel boundaries.  Every run is checked exactly (integer-valued inputs)."""
+kernel boundaries -- and the host-issued and DMA steps engines' counters
+across as many runs.  Every run is checked exactly (integer-valued
+inputs)."""
 import os
 import subprocess
 import sys
@@ -58,3 +60,7 @@ def test_device_engines_soak(P, runs, mode, engines):
         # the automatic choice for ranks sharing a GPU: host-issued steps only
         assert "devsteps" not in eng and "twoshot" not in eng and "oneshot" not in eng, eng
     assert "'ring_host': 'steps'" in eng, eng
+    # the DMA steps engine in every mode (its flag waits hold one wave, so the
+    # shared-GPU starvation cycle cannot form: the (8, 100, ":uneven")
+    # automatic case runs it beside rank 0's GEMMs)
+    assert "'ring_dma': 'dmasteps'" in eng and "'hd_dma': 'dmasteps'" in eng, eng
