@@ -1015,8 +1015,9 @@ def run_soak(store_dir, rank, size, runs, uneven=""):
 def run_fuzz(store_dir, rank, size, seed):
     """Randomized cases on the device engines, one process per rank: every
     rank draws the same sequence (a shared seed) of (class or function-style
-    algorithm, schedule, length, dtype, op, host or device buffer, runs) and
-    compares its own output with the oracle bit for bit.  The grid tests fix
+    algorithm, schedule, length, dtype, op, host or device buffer, runs, and
+    -- for the step schedules -- the DMA steps engine in about a third of the
+    cases) and compares its own output with the oracle bit for bit.  The grid tests fix
     their sizes; this walks lengths and combinations off them."""
     import random
 
@@ -1040,8 +1041,12 @@ def run_fuzz(store_dir, rank, size, seed):
     bad = []
     engines = {}
     ncases = int(os.environ.get("FUZZ_CASES", "100"))
+    # a second stream of draws (so the cases above stay the seed's): whether
+    # the step schedules run on the DMA steps engine this case
+    erng = random.Random(seed * 7919 + 1)
     for case in range(ncases):
         kind = rng.choice(kinds)
+        dma = erng.random() < 0.35 and kind not in ("mesh", "replicated")
         n = rng.choice([rng.randint(1, 64), rng.randint(65, 70000), rng.randint(70001, 1 << 21)])
         dt = rng.choice(dtypes)
         op = rng.choice(ops) if dt not in (O.FLOAT32,) else rng.choice([O.SUM, O.SUM, O.MAX])
@@ -1059,6 +1064,7 @@ def run_fuzz(store_dir, rank, size, seed):
             exp = O.allreduce(code, op, dt, ins, base=base)[rank][0]
         ctx.base = base
         fn = gloo_amd.ReductionFunction(op)
+        gloo_amd.set_steps_engine("dma" if dma else "auto")
         for it in range(runs):
             buf = ins[rank][0].copy() if host else to_dev(ins[rank][0], dt)
             torch.cuda.synchronize()
@@ -1092,6 +1098,7 @@ def run_fuzz(store_dir, rank, size, seed):
             engines[eng] = engines.get(eng, 0) + 1
             if not ok:
                 bad.append((case, kind, n, dt, op, host, base, eng, it))
+        gloo_amd.set_steps_engine("auto")
         print("FUZZ rank %d case %d %s n %d dtype %d op %d host %s base %d engine %s %s"
               % (rank, case, kind, n, dt, op, host, base, eng,
                  "MISMATCH" if bad and bad[-1][0] == case else "ok"), flush=True)
