@@ -116,3 +116,6 @@ def test_device_engines_random_cases_multiprocess(P, seed_):
         print(outs[0][-2000:])
         for r, p in enumerate(procs):
             assert p.returncode == 0 and "OK" in outs[r], "rank %d failed:\n%s" % (r, every)
+        # the DMA steps engine took part (about a third of the step-schedule cases)
+        eng = [line for line in outs[0].splitlines() if line.startswith("ENGINES")][-1]
+        assert "'dmasteps'" in eng, eng
