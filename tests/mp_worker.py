@@ -14,9 +14,9 @@ algo: ring_chunked | halving_doubling | ring_chunked_mesh (class algorithms)
       host-issued steps)
       dmasteps (the same cases through the DMA steps engine: the host-issued
       program's copies and reduce launches with on-GPU hand-offs)
-      devtimeout (rank 0 runs both device engines while the other ranks never
-      call run(): its kernels must give up after the timeout and run() must
-      raise IoException)
+      devtimeout (rank 0 runs the one- and two-shot kernels and the DMA steps
+      engine while the other ranks never call run(): its kernels must give up
+      after the timeout and run() must raise IoException)
       scale:cfg34 | scale:cfg5 (BASELINE.json configs at full size, 8 ranks:
       every engine's output SHA-256 against tests/golden/scale_golden.json)
       scale:ns (the north-star size, 256 MiB fp32 per rank, ring and HD at
@@ -173,9 +173,14 @@ def run_device_timeout(store_dir, rank, size):
     ctx.setTimeout(3)
     ctx.connectFullMesh(store)
     ok = True
-    for sched, eng, n in (("replicated", "oneshot", 4099), ("mesh", "twoshot", 1 << 20)):
+    for sched, eng, n in (("replicated", "oneshot", 4099), ("mesh", "twoshot", 1 << 20),
+                          ("ring", "dmasteps", 1 << 20)):
         buf = torch.ones(n, device="cuda")
-        alg = gloo_amd.AllreduceRingChunked(ctx, [buf], schedule=sched)
+        gloo_amd.set_steps_engine("dma" if eng == "dmasteps" else "auto")
+        try:
+            alg = gloo_amd.AllreduceRingChunked(ctx, [buf], schedule=sched)
+        finally:
+            gloo_amd.set_steps_engine("auto")
         ok = ok and alg.engine() == eng
         if rank == 0:
             t0 = time.time()

@@ -550,7 +550,8 @@ def test_algorithm_churn_multiprocess(P):
 
 def test_device_engine_timeout_raises_io_exception():
     """A device-driven kernel whose peers never arrive gives up after the
-    context timeout (every wave exits), and run() raises IoException."""
+    context timeout (every wave exits), and run() raises IoException -- the
+    one- and two-shot kernels and the DMA steps engine's flag waits."""
     P = 2
     with tempfile.TemporaryDirectory() as d:
         env = rank_env(P)
