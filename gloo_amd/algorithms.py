@@ -62,6 +62,8 @@ def torch_dtype_code(t):
     return table[t.dtype]
 
 
+INT_MAX = (1 << 31) - 1  # the class algorithms' count is a C int
+
 NUMPY_CODES = {"int8": INT8, "uint8": UINT8, "int32": INT32, "int64": INT64,
                "uint64": UINT64, "float32": FLOAT32, "float64": FLOAT64, "float16": FLOAT16}
 
@@ -155,6 +157,14 @@ class Algorithm:
             count = numel
         if numel is not None and count > numel:
             raise ValueError("count %d exceeds buffer size %d" % (count, numel))
+        if not 0 <= count <= INT_MAX:
+            # the reference's constructors take `const int count`
+            # (gloo/allreduce_ring_chunked.h:25, allreduce_halving_doubling.h:
+            # 70); ctypes would wrap a larger value silently (2^32 + 5 -> 5)
+            raise ValueError(
+                "count %d is outside [0, %d], the class algorithms' int count; pass "
+                "count= explicitly or use gloo_amd.allreduce (size_t elements)"
+                % (count, INT_MAX))
         self.count = int(count)
         self.dtype = dt
         self.fn = fn

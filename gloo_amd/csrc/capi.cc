@@ -79,6 +79,7 @@ glx_algorithm* makeAlgorithm(int algo, glx_context* ctx, void* const* ptrs, int 
   guarded([&]() -> int {
     GLX_ENFORCE(ctx != nullptr, "null context");
     GLX_ENFORCE(ptrs != nullptr && nptrs > 0, "need at least one pointer");
+    GLX_ENFORCE(count >= 0, "negative element count");
     GLX_ENFORCE(nstreams == 0 || streams != nullptr, "null streams array");
     std::vector<void*> p(ptrs, ptrs + nptrs);
     std::vector<hipStream_t> s;

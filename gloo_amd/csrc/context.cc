@@ -174,7 +174,7 @@ KindCache& kindCache() {
   return *c;
 }
 
-char* takeCached(int device, unsigned flags, size_t bytes, size_t* got) {
+char* takeCached(int device, unsigned flags, size_t bytes, size_t* got, size_t cap) {
   KindCache& c = kindCache();
   std::lock_guard<std::mutex> g(c.mu);
   const size_t most = std::max(2 * bytes, bytes + (size_t(4) << 20));
@@ -182,7 +182,7 @@ char* takeCached(int device, unsigned flags, size_t bytes, size_t* got) {
   for (size_t i = 0; i < c.free.size(); i++) {
     const auto& e = c.free[i];
     if (e.device == device && e.flags == flags && e.bytes >= bytes && e.bytes <= most &&
-        (best == c.free.size() || e.bytes < c.free[best].bytes)) {
+        e.bytes < cap && (best == c.free.size() || e.bytes < c.free[best].bytes)) {
       best = i;
     }
   }
@@ -215,11 +215,12 @@ void freeBlock(int device, char* p, size_t bytes, unsigned flags) {
 }
 
 // `bytes` in, the block's real size out (a cached block may be larger).
-char* allocBlock(int device, size_t* bytes, unsigned flags) {
+// cap: take no recycled block of cap bytes or more
+char* allocBlock(int device, size_t* bytes, unsigned flags, size_t cap = SIZE_MAX) {
   char* d = nullptr;
   if (flags != 0) {
     size_t got = 0;
-    d = takeCached(device, flags, *bytes, &got);
+    d = takeCached(device, flags, *bytes, &got, cap);
     if (d != nullptr) {
       *bytes = got;
       return d;
@@ -244,6 +245,7 @@ namespace {
 
 // Free pooled bytes kept beyond this are returned to the runtime.
 constexpr size_t kMaxFreeSharedBytes = size_t(8) << 30;
+
 
 // Allocation granule of a shared block: one 4 KiB page.  Round 1 rounded every block up to 2 MiB after a
 // peer's mapping of a small block was seen pointing elsewhere; with every
@@ -273,6 +275,15 @@ SharedBlock Context::acquireShared(size_t bytes, unsigned flags) {
   const size_t alloc =
       (std::max<size_t>(bytes, 1) + kCanaryBytes + granule - 1) / granule * granule;
   bytes = alloc - kCanaryBytes;
+  // A peer process's hipIpcOpenMemHandle of an allocation of 2^31 bytes or
+  // more never returns under the HIP runtime torch ships (ROCm 7.0; the
+  // image's 7.2 runtime maps it: tools/micro/ipc_size_probe.py),
+  // so such a block is refused here rather than hanging both ranks.
+  GLX_ENFORCE(!sharesAcrossProcesses() || alloc < kIpcMaxBlockBytes, "rank ", rank,
+              ": a landing block of ", alloc, " bytes would have to be shared with another "
+              "process, and IPC imports of 2 GiB or more hang in the HIP runtime; this "
+              "schedule's largest receive region needs it (use a smaller buffer per call, "
+              "more ranks, or the ring / halving-doubling schedule)");
   std::lock_guard<std::mutex> g(sharedMutex_);
   // the smallest free block of this kind that fits without wasting much
   SharedBlock* best = nullptr;
@@ -289,7 +300,8 @@ SharedBlock Context::acquireShared(size_t bytes, unsigned flags) {
   }
   SharedBlock nb;
   size_t got = alloc;
-  nb.ptr = allocBlock(device_, &got, flags);  // a recycled block may be larger
+  // a recycled block may be larger (never as large as the IPC limit)
+  nb.ptr = allocBlock(device_, &got, flags, kIpcMaxBlockBytes);
   bytes = got - kCanaryBytes;
   nb.bytes = bytes;
   nb.flags = flags;
@@ -371,7 +383,10 @@ char* Context::importShared(int r, const SharedRef& ref) {
   GLX_ENFORCE(ref.ipcStatus == 1, "rank ", r, " published shared block ", ref.id,
               " without an IPC handle");
   void* p = nullptr;
+  GLX_TRACE("r%d import: rank %d shared block %ld (%lu bytes)", rank, r, (long)ref.id,
+            (unsigned long)ref.canaryOff);
   GLX_HIP_CHECK(hipIpcOpenMemHandle(&p, ref.ipc, hipIpcMemLazyEnablePeerAccess));
+  GLX_TRACE("r%d import: opened at %p", rank, p);
   auto canaryAt = [&](const char* at) -> uint64_t {
     uint64_t v = 0;
     const hipError_t e = hipMemcpy(&v, at + ref.canaryOff, sizeof(v), hipMemcpyDeviceToHost);

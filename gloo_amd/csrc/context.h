@@ -169,6 +169,13 @@ class Context {
   // importer checks it before using the mapping and throws EnforceNotMet if
   // the mapping does not hold it (a mapping of some other memory would
   // otherwise corrupt data or lose flags silently).
+  //
+  // A block another process imports stays below kIpcMaxBlockBytes (with its
+  // canary and page rounding): larger ones are refused with EnforceNotMet,
+  // since a peer's hipIpcOpenMemHandle of 2^31 bytes or more never returned
+  // under torch's HIP runtime (2^31 - 2 MiB mapped).
+  static constexpr size_t kIpcMaxBlockBytes = size_t(1) << 31;
+  bool sharesAcrossProcesses() const { return size > 1 && crossProcess_; }
   SharedBlock acquireShared(size_t bytes, unsigned flags);
   void releaseShared(int64_t id);
   char* importShared(int rank, const SharedRef& ref);

@@ -215,6 +215,13 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
       return !(e != nullptr && e[0] == '0');
     }();
     slots_ = fuse ? sync_.slots : 1;
+    // two landing slots per region must stay shareable (Context::
+    // kIpcMaxBlockBytes): a larger region runs with one slot and no
+    // reduce-and-forward, which every rank derives alike from the geometry
+    if (slots_ > 1 && ctx->sharesAcrossProcesses()) {
+      const ScratchBlock whole{0, maxRegionElems(), nullptr, {}};
+      if ((size_t)slots_ * slotBytes(whole) + 4096 >= Context::kIpcMaxBlockBytes) slots_ = 1;
+    }
     if (!sync_.safe) engine_ = kEngineSteps;
   }
   if (engine_ == kEngineOneShot || engine_ == kEngineTwoShot) {
@@ -754,6 +761,19 @@ const HipPlanExecutor::ScratchBlock& HipPlanExecutor::blockOf(
   }
   GLX_ENFORCE(false, "no receive block holds region ", boff);
   return blocks.front();
+}
+
+// The largest receive region of the plan (elements): RECV steps land at
+// their region's start, regions run to the next start (allocScratch).
+int64_t HipPlanExecutor::maxRegionElems() const {
+  std::vector<int64_t> starts{0, plan_.scratch_elems};
+  for (const auto& s : plan_.steps) {
+    if (s.kind == glx::RECV) starts.push_back(s.boff);
+  }
+  std::sort(starts.begin(), starts.end());
+  int64_t m = 0;
+  for (size_t i = 0; i + 1 < starts.size(); i++) m = std::max(m, starts[i + 1] - starts[i]);
+  return m;
 }
 
 void HipPlanExecutor::allocScratch(bool uncached, int slots) {

@@ -227,6 +227,7 @@ class HipPlanExecutor : public Algorithm {
   // landing slots, plan.h SyncTable::slots), slotBytes() apart.
   void allocScratch(bool uncached = false, int slots = 1);
   size_t slotBytes(const ScratchBlock& b) const;
+  int64_t maxRegionElems() const;
   const ScratchBlock& blockOf(const std::vector<ScratchBlock>& blocks, int64_t boff) const;
   int slots_ = 1;  // plan kernel: landing slots per channel
   void waitWar(int64_t off, int64_t len);

@@ -28,6 +28,9 @@ algo: ring_chunked | halving_doubling | ring_chunked_mesh (class algorithms)
       fuzz:<seed> (randomized algorithms / lengths / dtypes / ops / host
       buffers on the device engines, every rank the same draw, each against
       the oracle)
+      maxcount (the class algorithms at the largest count the reference's
+      `const int count` takes, INT_MAX elements, int8 and float16, P = 2, on
+      every engine: exact, the result must equal x0 + x1)
       big:fast | big:plain (the ring on the plan kernel over MORE than 2 GiB per
       rank, P = 2, the given stream policy: every 32-bit store offset the
       write-through path could form is exceeded; exact at P = 2 since fp32
@@ -76,6 +79,8 @@ def main():
                         uneven=parts[2] if len(parts) > 2 else "")
     if algo.startswith("big:"):
         return run_big(store_dir, rank, size, algo[len("big:"):])
+    if algo == "maxcount":
+        return run_maxcount(store_dir, rank, size)
     if algo == "linkprobe":
         return run_linkprobe(store_dir, rank, size)
     if algo.startswith("graph_overlap:"):
@@ -649,6 +654,107 @@ def run_big(store_dir, rank, size, policy):
         del exp
         torch.cuda.empty_cache()
     alg.close()
+    store.set("done/%d" % rank, b"1")
+    for r in range(size):
+        store.get("done/%d" % r, timeout_ms=120000)
+    ctx.close()
+    if bad:
+        print("MISMATCH rank", rank, bad[:10])
+        sys.exit(1)
+    print("OK")
+
+
+def run_maxcount(store_dir, rank, size):
+    """count = INT_MAX (2^31 - 1, odd), the largest the reference's class
+    constructors take (gloo/allreduce_ring_chunked.h:25,
+    allreduce_halving_doubling.h:70): int8 (2 GiB - 1 B per rank) and float16
+    (4 GiB - 2 B: element offsets times the element size pass 2^32) through
+    the ring on the plan kernel, the host-issued steps and the DMA steps
+    engine, the mesh and halving-doubling on the plan kernel.  P = 2: the
+    sum commutes, so the result is x0 + x1 bit for bit (int8 wraps; float16
+    adds in fp32 and rounds once, as torch does).  A schedule whose landing
+    block another process would have to import at 2 GiB or more (the IPC
+    import hangs there: Context::kIpcMaxBlockBytes) must be refused at
+    creation with EnforceNotMet on every rank, not hang."""
+    import time
+
+    import torch
+
+    import gloo_amd
+    assert size == 2, "maxcount: P = 2 (the result is x0 + x1 exactly)"
+    # diagnostics: MAXCOUNT_N / _SCHED / _DTYPE / _TIMEOUT narrow the run
+    n = int(os.environ.get("MAXCOUNT_N", (1 << 31) - 1))
+    only = os.environ.get("MAXCOUNT_SCHED", "").split(",")
+    dts = os.environ.get("MAXCOUNT_DTYPE", "int8,float16").split(",")
+    dev = torch.device("cuda", 0)
+
+    def inp(r, dt):
+        g = torch.Generator(device=dev).manual_seed(4242 + r)
+        if dt == torch.int8:
+            return torch.randint(-128, 128, (n,), dtype=dt, device=dev, generator=g)
+        return torch.rand(n, dtype=dt, device=dev, generator=g) * 2 - 1
+    store = gloo_amd.rendezvous.FileStore(store_dir)
+    ctx = gloo_amd.rendezvous.Context(rank, size, 0)
+    ctx.setTimeout(int(os.environ.get("MAXCOUNT_TIMEOUT", 120)))
+    ctx.connectFullMesh(store)
+    bad = []
+    # (steps engine, schedule, engine it must get or "refused") per dtype:
+    # the mesh lands a whole range per peer slot array (4 arrays of P x ~S/P);
+    # float16's halving-doubling receives half its 4 GiB buffer in one region
+    cases = {
+        torch.int8: (("device", "ring", "devsteps"), ("host", "ring", "steps"),
+                     ("dma", "ring", "dmasteps"), ("auto", "mesh", "refused"),
+                     ("device", "hd", "devsteps")),
+        torch.float16: (("device", "ring", "devsteps"), ("host", "ring", "steps"),
+                        ("dma", "ring", "dmasteps"), ("auto", "mesh", "refused"),
+                        ("device", "hd", "refused")),
+    }
+    for dt, bits in ((torch.int8, torch.int8), (torch.float16, torch.int16)):
+        if str(dt).split(".")[1] not in dts:
+            continue
+        exp = inp(0, dt) + inp(1, dt)
+        buf = inp(rank, dt)
+        for eng, sched, want in cases[dt]:
+            if only != [""] and sched not in only:
+                continue
+            gloo_amd.set_steps_engine(eng)
+            try:
+                if sched == "hd":
+                    alg = gloo_amd.AllreduceHalvingDoubling(ctx, [buf])
+                else:
+                    alg = gloo_amd.AllreduceRingChunked(ctx, [buf], schedule=sched)
+            except gloo_amd.EnforceNotMet as e:
+                alg = None
+                msg = str(e)
+            finally:
+                gloo_amd.set_steps_engine("auto")
+            if alg is None:
+                ok = want == "refused" and "IPC imports of 2 GiB" in msg
+                print("maxcount rank %d %s %s refused (%s): %s" % (
+                    rank, dt, sched, "expected" if ok else "UNEXPECTED", msg[:160]), flush=True)
+                if not ok:
+                    bad.append(("refused", str(dt), sched, msg[:200]))
+                continue
+            if want == "refused" or alg.count != n or alg.engine() != want:
+                bad.append(("engine", str(dt), sched, alg.count, alg.engine(), want))
+            buf.copy_(inp(rank, dt))
+            torch.cuda.synchronize()
+            print("maxcount rank %d %s %s engine %s: run" % (rank, dt, sched, alg.engine()),
+                  flush=True)
+            t0 = time.perf_counter()
+            alg.run()
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) * 1e3
+            diff = int((buf.view(bits) != exp.view(bits)).sum().item())
+            if diff:
+                first = int((buf.view(bits) != exp.view(bits)).nonzero()[0].item())
+                bad.append(("run", str(dt), sched, alg.engine(), diff, first))
+            print("maxcount rank %d %s %s engine %s %.1f ms %s" % (
+                rank, dt, sched, alg.engine(), ms, "ok" if not diff else "MISMATCH %d" % diff),
+                flush=True)
+            alg.close()
+        del exp, buf
+        torch.cuda.empty_cache()
     store.set("done/%d" % rank, b"1")
     for r in range(size):
         store.get("done/%d" % r, timeout_ms=120000)

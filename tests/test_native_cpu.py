@@ -109,6 +109,21 @@ def test_algorithm_needs_connected_context():
         gloo_amd.AllreduceRingChunked(c, [1 << 20], count=16, dtype=5)
 
 
+@pytest.mark.parametrize("count", [-1, 1 << 31, (1 << 32) + 5])
+def test_class_count_outside_c_int_is_refused(count):
+    """The class algorithms take the reference's `const int count`
+    (gloo/allreduce_ring_chunked.h:25): a count ctypes would wrap (2^32 + 5
+    -> 5, a silent partial reduce) is refused before any native call; the C
+    ABI refuses a negative one itself."""
+    c = gloo_amd.rendezvous.Context(0, 2)
+    for cls in (gloo_amd.AllreduceRingChunked, gloo_amd.AllreduceHalvingDoubling):
+        with pytest.raises(ValueError, match="int count"):
+            cls(c, [1 << 20], count=count, dtype=0)
+    arr = (ctypes.c_void_p * 1)(1 << 20)
+    assert not _lib.lib.glx_allreduce_ring_chunked_create(c.handle, arr, 1, -1, 0, 1, None, 0)
+    assert "count" in _lib.lib.glx_last_error().decode()
+
+
 def test_library_never_registers_or_copies_caller_host_pages():
     """DESIGN.md 9 (the round-3 illegal address): the library must not hand
     a caller's host pages to the runtime.  It imports neither
