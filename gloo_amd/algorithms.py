@@ -270,8 +270,10 @@ class AllreduceRingChunked(Algorithm):
 
     schedule="auto" (default) picks the data movement by size: replicated
     up to 16 MiB per rank at P=2, 2 MiB at P<=4, 1 MiB at P<=8 when the
-    device-driven engines are available (256 KiB otherwise), mesh above;
-    the other schedules force one.
+    device-driven engines are available (256 KiB otherwise), mesh above,
+    the ring from 2 GiB - 64 MiB per rank (the mesh's landing block would
+    reach the 2 GiB a peer process can import); the other schedules force
+    one.
     schedule="ring" moves chunks around the ring exactly as the
     reference does (one link per direction); schedule="mesh" computes the
     identical result (same chunks, same reduction chain and operand order)

@@ -856,7 +856,13 @@ int autoRingSchedule(int size, int64_t bytes, bool fn, bool deviceDriven) {
                                                           : (int64_t(1) << 20);
   }
   if (size <= 1) return ring;
-  return bytes <= maxRepl ? repl : mesh;
+  if (bytes <= maxRepl) return repl;
+  // the mesh lands about S per rank in one block (the two-shot's slot
+  // arrays; 2S/P regions on the steps engines), and a block shared between
+  // processes stays below 2 GiB (Context::kIpcMaxBlockBytes): larger
+  // buffers take the ring, whose regions are S/2P (class) or 4 MiB pieces
+  // (function-style)
+  return bytes < kMeshMaxBytes ? mesh : ring;
 }
 
 Plan makePlan(int algo, int rank, int size, int64_t count, const PlanParams& prm) {

@@ -135,11 +135,13 @@ Plan makePlan(int algo, int rank, int size, int64_t count,
 
 // Automatic data movement for the ring's result (all bit-identical): the
 // one-round replicated schedule up to a threshold per rank, the all-links
-// mesh above.  fn: the function-style RING family instead of the class
+// mesh above, the ring itself from kMeshMaxBytes.  fn: the function-style RING family instead of the class
 // ring_chunked one.  deviceDriven: the replicated schedule will run as the
 // one-shot kernel (no host round trips), which moves the threshold from
 // 256 KiB to 16 MiB (P = 2), 2 MiB (P <= 4) or 1 MiB (P <= 8).  (An
 // explicit schedule -- "ring", "mesh", "replicated" -- forces one.)
+// Largest buffer (bytes per rank) the automatic choice gives the mesh.
+constexpr int64_t kMeshMaxBytes = (int64_t(2) << 30) - (int64_t(64) << 20);
 int autoRingSchedule(int size, int64_t bytes, bool fn, bool deviceDriven = false);
 
 // Geometry of the device-driven engines (xgmi_kernels.hip), read off a

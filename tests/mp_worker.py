@@ -700,14 +700,16 @@ def run_maxcount(store_dir, rank, size):
     bad = []
     # (steps engine, schedule, engine it must get or "refused") per dtype:
     # the mesh lands a whole range per peer slot array (4 arrays of P x ~S/P);
-    # float16's halving-doubling receives half its 4 GiB buffer in one region
+    # float16's halving-doubling receives half its 4 GiB buffer in one region;
+    # the automatic schedule takes the ring at these sizes (plan.h
+    # kMeshMaxBytes), on the host-issued steps (ranks share the GPU, > 32 MiB)
     cases = {
         torch.int8: (("device", "ring", "devsteps"), ("host", "ring", "steps"),
                      ("dma", "ring", "dmasteps"), ("auto", "mesh", "refused"),
-                     ("device", "hd", "devsteps")),
+                     ("device", "hd", "devsteps"), ("auto", "auto", "steps")),
         torch.float16: (("device", "ring", "devsteps"), ("host", "ring", "steps"),
                         ("dma", "ring", "dmasteps"), ("auto", "mesh", "refused"),
-                        ("device", "hd", "refused")),
+                        ("device", "hd", "refused"), ("auto", "auto", "steps")),
     }
     for dt, bits in ((torch.int8, torch.int8), (torch.float16, torch.int16)):
         if str(dt).split(".")[1] not in dts:
