@@ -626,7 +626,8 @@ TRANSPORT = {}  # bench name -> the algorithm's transport_stats() after its time
 FAST = {}  # bench name -> whether its plan kernel ran the fast streams
 SYNC = {}  # bench name -> its device engine's flag sync ("narrow" / "system" / None)
 RUN_SYNC = ["auto"]  # the run's flag sync (probe_device_engines may fall back to "system")
-CHECKS = {}  # bench name -> result_check() of its post-timing run
+CHECKS = {}  # bench name -> refill_checks() detail of its post-timing runs
+STALE = {}  # bench name -> the wrong (run, rank) entries of its refilled runs
 REFDIG = {}  # bench name -> its output's SHA-256 equals the reference's (bench_golden.json)
 SEED = 1234  # SURVEY 8d's synthetic-input seed
 
@@ -900,13 +901,74 @@ def result_check(torch, dist, src, result):
     return err <= tol, err / tol if tol > 0 else float(err > 0)
 
 
+def checksum_of(torch, t):
+    """Integer sum of a result's bits (16- or 32-bit words): equal on every
+    rank iff the ranks almost surely hold the same bits."""
+    w = torch.int16 if t.element_size() == 2 else torch.int32
+    return int(t.view(w).to(torch.int64).sum().item())
+
+
+REFILL_RUNS = 5  # refilled runs checked per timed candidate (VERDICT r5 #1: K >= 5)
+
+
+def refill_checks(torch, dist, src, run_once, runs=REFILL_RUNS, golden_sha=None):
+    """After a candidate's timing: `runs` runs on fresh inputs, each checked
+    on EVERY rank -- result_check (the weighted sum against every rank's
+    input), the reference's output digest where one exists (each rank hashes
+    its own result: the reduction order is rank-independent, so every rank
+    holds the reference's bits), and a cross-rank checksum.  A hand-off that
+    goes stale now and then on the node (a rate of 1e-4..1e-2 per hand-off is
+    what near-miss sync forms show, MI355X_MICROARCH.md) must show up here, on
+    whichever rank it hits, not only in one post-timing run on rank 0.
+    run_once() refills the buffer from src, runs once and returns the result.
+    Returns (ok for every run on every rank, detail, last result)."""
+    world = dist.get_world_size()
+    bad, worst, last = [], 0.0, None
+    for k in range(runs):
+        res = run_once()
+        ok, rel = result_check(torch, dist, src, res)
+        worst = max(worst, rel)
+        dig = None if golden_sha is None else sha256_of(res) == golden_sha
+        cs = torch.tensor([checksum_of(torch, res)], dtype=torch.int64)
+        allcs = [torch.zeros_like(cs) for _ in range(world)]
+        dist.all_gather(allcs, cs)
+        same = all(torch.equal(x, cs) for x in allcs)
+        mine = torch.tensor([int(ok), -1 if dig is None else int(dig), int(same)],
+                            dtype=torch.int64)
+        every = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(every, mine)
+        for r, e in enumerate(every):
+            okr, digr, samer = [int(v) for v in e.tolist()]
+            if not okr or digr == 0 or not samer:
+                bad.append({"run": k, "rank": r, "result_check": bool(okr),
+                            "digest": None if digr < 0 else bool(digr),
+                            "ranks_agree": bool(samer)})
+        last = res
+    detail = {"runs": runs, "bad": bad[:8], "bad_count": len(bad),
+              "worst_err_over_tol": round(worst, 4), "digest_checked": golden_sha is not None,
+              "note": "refilled runs after the timing, each checked on every rank "
+                      "(result_check, reference digest where one exists, cross-rank checksum)"}
+    return not bad, detail, last
+
+
 SWEEP_ELEMS = [1 << 10, 1 << 12, 1 << 14, 1 << 16, 1 << 18, 1 << 20, 1 << 22, 1 << 24]
 
 
-def probe_device_engines(torch, dist, gloo_amd, connect, dev, dtype):
+# the probe's small-buffer case: a few KB per workgroup of a landing slot that
+# its CU read two messages before, within one launch (the ring at P >= 3 has
+# 2(P-1) messages per channel per run and two slots): the L1-warm re-read
+# that a missing acquire turns stale in every run on one GPU
+# (tests/test_sync_control_gpu.py, DESIGN.md 4)
+PROBE_SMALL = (4096, 20)  # (elements, refilled runs)
+
+
+def probe_device_engines(torch, dist, gloo_amd, connect, dev, dtype, n_full=None):
     """Before timing them, check the device-driven engines (one-shot,
     two-shot and plan kernels) on this machine: short timeout, results
-    bit-identical to the host-issued steps engine over three refilled runs.
+    bit-identical to the host-issued steps engine over refilled runs -- three
+    per case at 64 K / 1 M elements and, given n_full, at the timed size
+    itself (the north star's 256 MiB per rank: VERDICT r5 #1), and twenty of
+    the ring at PROBE_SMALL's L1-warm size.
     Each attempt runs on a context of its own (`connect(tag)`), so a failed
     attempt cannot leave the ranks' algorithm slots out of step for the run.
     The default narrow flag sync is tried first; if any rank fails, the
@@ -919,9 +981,12 @@ def probe_device_engines(torch, dist, gloo_amd, connect, dev, dtype):
         ctx = connect(tag)
         ctx.setTimeout(15)
         try:
-            for algo, n in (("ring_chunked_repl", 65536 + 3),
-                            ("ring_chunked_mesh", (1 << 20) + 5),
-                            ("ring_chunked", 1 << 20), ("halving_doubling", 1 << 20)):
+            cases = [("ring_chunked_repl", 65536 + 3, 3), ("ring_chunked_mesh", (1 << 20) + 5, 3),
+                     ("ring_chunked", 1 << 20, 3), ("halving_doubling", 1 << 20, 3),
+                     ("ring_chunked", PROBE_SMALL[0], PROBE_SMALL[1])]
+            if n_full:
+                cases += [("ring_chunked", n_full, 3), ("halving_doubling", n_full, 3)]
+            for algo, n, reps in cases:
                 x = synthetic(torch, n, dtype, dev, 99 + int(os.environ.get("RANK", "0")))
                 ref = x.clone()
                 torch.cuda.synchronize()  # run() does not order itself after torch's stream
@@ -936,13 +1001,14 @@ def probe_device_engines(torch, dist, gloo_amd, connect, dev, dtype):
                 y = x.clone()
                 a = make_alg(gloo_amd, ctx, y, algo)
                 eng = a.engine()
-                for _ in range(3):
+                for _ in range(reps):
                     y.copy_(x)
                     torch.cuda.synchronize()
                     a.run()
                     torch.cuda.synchronize()
                     if not torch.equal(y.view(torch.uint8), ref.view(torch.uint8)):
-                        ok, note = 0, "%s (%s) differs from the steps engine" % (algo, eng)
+                        ok, note = 0, "%s (%s, n=%d) differs from the steps engine" % (
+                            algo, eng, n)
                 a.close()
         except Exception as e:  # timeout (IoException) or HIP error on this rank
             ok, note = 0, "%s: %s" % (type(e).__name__, str(e)[:200])
@@ -1225,7 +1291,8 @@ def bench_multi(args):
             "gloo_amd_probe_" + tag,
             gloo_amd.rendezvous.TorchStore(dist.distributed_c10d._get_default_store())))
         return c
-    device_engines = probe_device_engines(torch, dist, gloo_amd, connect, dev, args.dtype)
+    device_engines = probe_device_engines(torch, dist, gloo_amd, connect, dev, args.dtype,
+                                          n_full=n)
 
     # A failure on any rank (a timeout, a HIP error) is agreed on by all, so
     # every rank takes the same branch; the JSON line names it.
@@ -1282,25 +1349,37 @@ def bench_multi(args):
         torch.cuda.synchronize()
         t, sent = time_schedule(torch, dist, gloo_amd, ctx, buf, algo, steps, args.warmup)
         p50 = P50[algo]  # the sweep re-times the same names at other sizes later
-        # correctness after the timing: one run on fresh inputs; every rank
-        # must hold the same bits (the reduction order is rank-independent)
-        buf.copy_(src)
-        torch.cuda.synchronize()
-        alg = make_alg(gloo_amd, ctx, buf, algo)
-        alg.run()
-        torch.cuda.synchronize()
-        alg.close()
-        result = buf.clone()
-        return {"t": t, "sent": sent, "p50": p50,
+        # correctness after the timing: REFILL_RUNS runs on fresh inputs, each
+        # checked on every rank (refill_checks)
+        refill = checked_runs(algo)
+        return {"t": t, "sent": sent, "p50": p50, "refill": refill[:2], "result": refill[2],
                 "transport": ("device-driven kernel stores (%s)" % ENGINES[algo]
                               if device_engine else tname(best) +
                               (", hand-offs on the GPU (dmasteps)" if engine == "dmasteps"
                                else "")), "tr": best,
-                "calib_ms": {tname(k): round(v * 1e3, 3) for k, v in calib.items()},
-                "result": result}
+                "calib_ms": {tname(k): round(v * 1e3, 3) for k, v in calib.items()}}
+
+    def checked_runs(algo):
+        """refill_checks on a fresh instance of the candidate (the engine
+        the timing used); the reference's digest where one exists."""
+        alg = make_alg(gloo_amd, ctx, buf, algo)
+
+        def run_once():
+            buf.copy_(src)
+            torch.cuda.synchronize()
+            alg.run()
+            torch.cuda.synchronize()
+            return buf
+        gc = golden.get(golden_plan(algo)) if gin else None
+        try:
+            ok, detail, last = refill_checks(torch, dist, src, run_once,
+                                             golden_sha=gc["output_sha256"] if gc else None)
+        finally:
+            alg.close()
+        return ok, detail, last.clone()
 
     def checksum(t):
-        return int(t.view(torch.int16 if es == 2 else torch.int32).to(torch.int64).sum().item())
+        return checksum_of(torch, t)
 
     candidates, alt_list = candidate_lists(args)
     runs = {}
@@ -1309,23 +1388,20 @@ def bench_multi(args):
         if not agreed(err is None):
             failed[a] = err or "failed on another rank"
             continue
-        # every rank is here: the collective check of the result
-        ok, rel = result_check(torch, dist, src, r["result"])
-        CHECKS[a] = {"ok": ok, "err_over_tol": round(rel, 4)}
+        # every rank is here: the refilled runs were checked on every rank
+        ok, detail = r["refill"]
+        CHECKS[a] = dict(detail, ok=ok)
         gc = golden.get(golden_plan(a))
         if gc is not None and gin:
-            # every rank holds the same bits; rank 0's digest speaks for all
-            # (the cross-rank checksum below compares them)
-            REFDIG[a] = sha256_of(r["result"]) == gc["output_sha256"]
-        digest_ok = REFDIG.get(a) is not False
-        if not agreed(digest_ok):
-            # bits differ from the reference's output for the same inputs: never
-            # a headline
-            failed[a] = "output differs from the reference's digest (%s)" % gc["name"]
-        elif agreed(ok):
+            REFDIG[a] = not any(b["digest"] is False for b in detail["bad"])
+        if ok:
             runs[a] = r
         else:
-            failed[a] = "result check failed (weighted sum off by %.3g tolerances)" % rel
+            # a wrong or stale result in any refilled run on any rank: never a
+            # headline, and the line carries the error
+            STALE[a] = detail["bad"]
+            failed[a] = ("%d of %d refilled runs x ranks wrong (first: %s)"
+                         % (detail["bad_count"], detail["runs"], detail["bad"][:1]))
     if not runs:
         raise RuntimeError("every candidate failed: %s" % failed)
     candidates = [a for a in candidates if a in runs]
@@ -1366,19 +1442,17 @@ def bench_multi(args):
             continue
         ta, sent_a = got
         gc = golden.get(golden_plan(other))
-        if gc is not None and gin:
-            # one run on fresh inputs: its output against the reference's digest
-            def digest_run():
-                buf.copy_(src)
-                torch.cuda.synchronize()
-                alg = make_alg(gloo_amd, ctx, buf, other)
-                alg.run()
-                torch.cuda.synchronize()
-                alg.close()
-                return sha256_of(buf) == gc["output_sha256"]
-            match, err = attempt(other + " digest", digest_run)
-            if agreed(err is None):
-                REFDIG[other] = match
+        # refilled runs checked on every rank, as for the candidates
+        chk, err = attempt(other + " refill checks", lambda: checked_runs(other))
+        if agreed(err is None):
+            CHECKS[other] = dict(chk[1], ok=chk[0])
+            if gc is not None and gin:
+                REFDIG[other] = not any(b["digest"] is False for b in chk[1]["bad"])
+            if not chk[0]:
+                STALE[other] = chk[1]["bad"]
+        else:
+            failed[other + " refill checks"] = err or "failed on another rank"
+
         lm = busiest_link_bytes(gloo_amd, other, rank, world, n, es)
         eng = ENGINES.get(other)
         alts[other] = {"value": round(S / ta / 1e9, 3),
@@ -1526,6 +1600,13 @@ def bench_multi(args):
             "verified": verified,
         }
         apply_transport_verdict(res, health, health_err)
+        if STALE:
+            # a candidate's refilled runs came out wrong on some rank: the
+            # line is in error whatever else was measured
+            msg = "wrong results in refilled runs: %s" % "; ".join(
+                "%s: %s" % (k, v[:2]) for k, v in sorted(STALE.items()))
+            res["error"] = msg if "error" not in res else res["error"] + "; " + msg
+            res["verified"] = False
         if staged is not None:
             res["host_staged"] = staged
         if failed:

@@ -100,11 +100,18 @@ def set_device_sync(mode):
     created afterwards: "auto" (default: narrow), "system" (L2 written back before
     and invalidated after every flag) or "narrow" (stores completed before a
     flag, the CU's L1 invalidated after a wait: enough because every flag
-    publishes data in the receiver's uncached landing slots)."""
-    code = {"auto": -1, "system": 0, "narrow": 1}[mode]
+    publishes data in the receiver's uncached landing slots).
+
+    TEST ONLY: "unsafe_noacquire", "unsafe_norelease", "unsafe_test" and
+    "unsafe_cached" are
+    deliberately broken positive controls for the suite's stale-data checks
+    (glx.h glx_set_device_sync); their results may be wrong."""
+    code = _SYNC_MODES[mode]
     errors.check(_lib.lib.glx_set_device_sync(code), "set_device_sync")
 
 
+_SYNC_MODES = {"auto": -1, "system": 0, "narrow": 1, "unsafe_noacquire": 2,
+               "unsafe_norelease": 3, "unsafe_test": 4, "unsafe_cached": 5}
 _DEVICE_ENGINE_MODES = {"auto": -1, "off": 0, "on": 1, "shared": 2}
 
 

@@ -27,6 +27,7 @@ if not os.path.exists(LIB_PATH):
 lib = ctypes.CDLL(LIB_PATH)
 
 _vp, _sz, _i, _i64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int64
+_pi = ctypes.POINTER(ctypes.c_int)
 
 # (name, restype, argtypes) for every symbol declared in include/gloo_amd/glx.h
 SIGNATURES = [
@@ -40,6 +41,7 @@ SIGNATURES = [
     ("glx_copy", _i, [_vp, _vp, _sz, _i, _vp]),
     ("glx_enable_peer", _i, [_i, _i]),
     ("glx_tune_reduce", _i, [_i, _i, _i]),
+    ("glx_reduce_tuning", _i, [_pi, _pi, _pi]),
     ("glx_reduce_segment_bytes", _sz, []),
     ("glx_set_copy_split", _i, [_i]),
     ("glx_set_pinned_mirror_limit", _i, [_sz]),

@@ -230,8 +230,10 @@ class Algorithm:
 
     def sync_mode(self):
         """Release / acquire of its device engine around flags: "narrow",
-        "system", or None for host-issued steps (set_device_sync)."""
-        return {1: "narrow", 0: "system", -1: None}[lib.glx_algorithm_sync(self._h)]
+        "system", a test-only "unsafe_*" mode, or None for host-issued steps
+        (set_device_sync)."""
+        return {1: "narrow", 0: "system", 2: "unsafe_noacquire", 3: "unsafe_norelease",
+                4: "unsafe_test", 5: "unsafe_cached", -1: None}[lib.glx_algorithm_sync(self._h)]
 
     def transport_stats(self):
         """How this algorithm's messages moved since it was created:

@@ -193,6 +193,14 @@ int glx_tune_reduce(int unroll, int blocks_per_cu, int nontemporal) {
   return GLX_OK;
 }
 
+int glx_reduce_tuning(int* unroll, int* blocks_per_cu, int* policy) {
+  if (unroll == nullptr || blocks_per_cu == nullptr || policy == nullptr) {
+    return fail(GLX_ERR_INVALID, "glx_reduce_tuning: null argument");
+  }
+  glx::reduce_tuning(unroll, blocks_per_cu, policy);
+  return GLX_OK;
+}
+
 int glx_set_copy_engine(int engine, int blocks) {
   if (engine != 0 && engine != 1) return fail(GLX_ERR_INVALID, "copy engine must be 0 or 1");
   gloo::HipPlanExecutor::setCopyEngine(engine);
@@ -530,7 +538,7 @@ int glx_algorithm_engine(glx_algorithm* alg) {
 }
 
 int glx_set_device_sync(int mode) {
-  if (mode < -1 || mode > 1) return fail(GLX_ERR_INVALID, "glx_set_device_sync: -1, 0 or 1");
+  if (mode < -1 || mode > 5) return fail(GLX_ERR_INVALID, "glx_set_device_sync: -1 .. 5");
   gloo::HipPlanExecutor::setDeviceSync(mode);
   return GLX_OK;
 }

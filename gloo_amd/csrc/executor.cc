@@ -233,7 +233,7 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
     // plan kernel reads its `slots_` landing slots inside the launch right
     // after an in-kernel flag wait, where nothing else could drop such a
     // line.)
-    allocScratch(true, engine_ == kEngineDevSteps ? slots_ : 1);
+    allocScratch(!cachedSlotsForTest(), engine_ == kEngineDevSteps ? slots_ : 1);
   }
 
   // Channels named by the plan; allocate our counter words.

@@ -437,7 +437,11 @@ class HipPlanExecutor : public Algorithm {
   void traceTwoShot(const glx::TwoShotParams& launched);
   void traceDevSteps(const glx::PlanKernelParams& launched);
   static int engineFor(const Context& ctx, int algo, int64_t count, int esize);
-  char* ddAlloc(size_t bytes);
+  // uncached device memory from the context's pool (flag rows; landing slots
+  // when `slots`, which the test-only kSyncCachedSlots allocates cached)
+  char* ddAlloc(size_t bytes, bool slots = false);
+  // the test-only kSyncCachedSlots mode is in force (kernels.h)
+  static bool cachedSlotsForTest();
   void setupDevice();
   size_t maxSlices(int kernel) const;
   void setupOneShot();
@@ -511,19 +515,21 @@ class HipPlanExecutor : public Algorithm {
   // stores (glx_set_engine_streams).
   static void setEngineStreams(int fast);
   // release / acquire around the device engines' flags: -1 auto, 0 system
-  // scope, 1 narrow (kernels.h); for algorithms created afterwards
+  // scope, 1 narrow, 2-4 the test-only broken modes (kernels.h kSync*); for
+  // algorithms created afterwards
   static void setDeviceSync(int mode);
   static int deviceSync();
   static constexpr bool kAutoNarrow = true;
-  // 1 when the device engine runs the narrow release / acquire, 0 system
-  // scope, -1 host-issued steps (and the DMA steps engine: its flags follow
+  // the device engine's kernels.h kSync* mode (1 narrow, 0 system scope,
+  // 2-4 test-only), -1 host-issued steps (and the DMA steps engine: its flags follow
   // completed stream work, no fences)
   int syncMode() const {
-    return engine_ == kEngineSteps || engine_ == kEngineDmaSteps
-               ? -1
-               : (engine_ == kEngineDevSteps ? pk_.narrow
-                                              : (engine_ == kEngineOneShot ? os_.narrow : ts_.narrow));
+    if (engine_ == kEngineSteps || engine_ == kEngineDmaSteps) return -1;
+    if (cachedSlots_) return glx::kSyncCachedSlots;
+    return engine_ == kEngineDevSteps ? pk_.narrow
+                                      : (engine_ == kEngineOneShot ? os_.narrow : ts_.narrow);
   }
+  bool cachedSlots_ = false;  // landing slots allocated cached (test-only mode)
   static int engineStreams();
 };
 

@@ -72,17 +72,27 @@ std::atomic<int> g_engine_streams{[] {
 
 namespace {
 // -1 auto, 0 system-scope release / acquire around the device engines' flags,
-// 1 narrow (kernels.h).  GLOO_AMD_SYNC=system|narrow.
+// 1 narrow, 2-4 the test-only broken modes (kernels.h kSync*).
+// GLOO_AMD_SYNC=system|narrow|unsafe_noacquire|unsafe_norelease|unsafe_test.
 std::atomic<int> g_device_sync{[] {
   const char* e = std::getenv("GLOO_AMD_SYNC");
-  if (e != nullptr && std::strcmp(e, "narrow") == 0) return 1;
-  if (e != nullptr && std::strcmp(e, "system") == 0) return 0;
+  if (e == nullptr) return -1;
+  if (std::strcmp(e, "narrow") == 0) return glx::kSyncNarrow;
+  if (std::strcmp(e, "system") == 0) return glx::kSyncSystem;
+  if (std::strcmp(e, "unsafe_noacquire") == 0) return glx::kSyncNoAcquire;
+  if (std::strcmp(e, "unsafe_norelease") == 0) return glx::kSyncNoRelease;
+  if (std::strcmp(e, "unsafe_test") == 0) return glx::kSyncUnsafe;
+  if (std::strcmp(e, "unsafe_cached") == 0) return glx::kSyncCachedSlots;
   return -1;
 }()};
 }  // namespace
 
 void HipPlanExecutor::setDeviceSync(int mode) {
-  g_device_sync.store(mode < 0 ? -1 : (mode != 0 ? 1 : 0));
+  g_device_sync.store(mode < 0 || mode > glx::kSyncCachedSlots ? -1 : mode);
+}
+
+bool HipPlanExecutor::cachedSlotsForTest() {
+  return g_device_sync.load() == glx::kSyncCachedSlots;
 }
 
 int HipPlanExecutor::deviceSync() { return g_device_sync.load(); }
@@ -186,9 +196,10 @@ int HipPlanExecutor::engineFor(const Context& ctx, int algo, int64_t count, int 
 
 // Peers' stores land in our HBM behind our caches' back: uncached memory,
 // which no L2 holds -- the narrow flag sync relies on it (kernels.h).
-char* HipPlanExecutor::ddAlloc(size_t bytes) {
+char* HipPlanExecutor::ddAlloc(size_t bytes, bool slots) {
   SharedRef ref;
-  char* d = allocShared(bytes, hipDeviceMallocUncached, &ref);
+  if (slots && cachedSlotsForTest()) cachedSlots_ = true;
+  char* d = allocShared(bytes, slots && cachedSlots_ ? 0u : hipDeviceMallocUncached, &ref);
   ddRefs_.push_back(ref);
   GLX_TRACE("r%d ddAlloc %zu bytes at %p", contextRank_, bytes, (void*)d);
   ddBlocks_.push_back(d);
@@ -228,8 +239,22 @@ void HipPlanExecutor::setupDevice() {
   // write-through stores, or plain.  The one-shot and two-shot kernels are
   // always plain.
   // release / acquire around the flags (kernels.h): automatic = kAutoNarrow
-  const int sync = deviceSync();
-  const int narrow = sync < 0 ? (kAutoNarrow ? 1 : 0) : sync;
+  int sync = deviceSync();
+  if (sync == glx::kSyncCachedSlots) {
+    cachedSlots_ = true;  // allocScratch / ddAlloc took cached slots; narrow kernels
+    sync = glx::kSyncNarrow;
+    std::fprintf(stderr,
+                 "[gloo_amd] rank %d: TEST-ONLY cached landing slots (GLOO_AMD_SYNC="
+                 "unsafe_cached): results may be stale\n",
+                 contextRank_);
+  }
+  const int narrow = sync < 0 ? (kAutoNarrow ? glx::kSyncNarrow : glx::kSyncSystem) : sync;
+  if (narrow >= glx::kSyncNoAcquire) {
+    std::fprintf(stderr,
+                 "[gloo_amd] rank %d: TEST-ONLY broken flag sync %d (GLOO_AMD_SYNC=unsafe_*): "
+                 "results may be stale\n",
+                 contextRank_, narrow);
+  }
   os_.narrow = narrow;
   ts_.narrow = narrow;
   pk_.narrow = narrow;
@@ -240,6 +265,7 @@ void HipPlanExecutor::setupDevice() {
   const int pol = engineStreams();
   const bool ring = algo_ == glx::ALGO_RING_CHUNKED || algo_ == glx::ALGO_FN_RING;
   pk_.fast = (pol > 0 || (pol < 0 && ring && !narrow)) ? 1 : 0;
+  if (narrow == glx::kSyncUnsafe) pk_.fast = 0;  // its build has plain streams only
   GLX_HIP_CHECK(hipEventCreateWithFlags(&ddDone_, hipEventDisableTiming));
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) == hipSuccess &&
@@ -299,8 +325,8 @@ void HipPlanExecutor::setupOneShot() {
     for (int i = 0; i < P; i++) p.chain[q][i] = (uint8_t)d.chain[q][i];
   }
   ddSlot_ = ((size_t)count_ * esize_ + 255) & ~(size_t)255;
-  ddAlloc((size_t)P * ddSlot_);
-  ddAlloc((size_t)P * ddSlot_);
+  ddAlloc((size_t)P * ddSlot_, true);
+  ddAlloc((size_t)P * ddSlot_, true);
   // the flag rows, then the launch counters on lines of their own (kernels.h)
   const size_t rows = (size_t)P * (size_t)p.G * glx::kFlagBytes;
   char* flags = ddAlloc(rows + glx::launchCtrBytes(p.G));
@@ -332,7 +358,7 @@ void HipPlanExecutor::setupTwoShot() {
     p.trace = trace_;
   }
   ddSlot_ = ((size_t)d.maxLen * esize_ + 16 + 255) & ~(size_t)255;
-  for (int k = 0; k < 4; k++) ddAlloc((size_t)P * ddSlot_);  // RS 0/1, AG 0/1
+  for (int k = 0; k < 4; k++) ddAlloc((size_t)P * ddSlot_, true);  // RS 0/1, AG 0/1
   // the A and B flag rows, then the launch counters on lines of their own
   const size_t rows = 2 * (size_t)P * (size_t)p.G * glx::kFlagBytes;
   char* flags = ddAlloc(rows + glx::launchCtrBytes(p.G));

@@ -59,6 +59,21 @@ constexpr int kFlagStride = 16;
 // sc1) and invalidates the L2 after each wait (buffer_inv sc0 sc1); narrow
 // (1) only completes the stores (s_waitcnt vmcnt(0)) before a flag and
 // invalidates the CU's L1 after a wait (agent scope).
+//
+// The `narrow` field of the engines' parameters holds one of these modes.
+// Modes 2-4 are TEST ONLY positive controls (GLOO_AMD_SYNC=unsafe_*): each
+// breaks one premise of the narrow form, so the GPU suite can show that its
+// checks catch a stale hand-off (tests/test_sync_control_gpu.py).
+constexpr int kSyncSystem = 0;
+constexpr int kSyncNarrow = 1;
+constexpr int kSyncNoAcquire = 2;  // narrow without the consumer's L1 invalidate
+constexpr int kSyncNoRelease = 3;  // narrow without the producer's store-completion wait and
+                                   // the workgroup barrier before its flag
+constexpr int kSyncUnsafe = 4;     // neither, and plain (write-back) stores into peers' slots
+// narrow, with every engine's landing slots in CACHED memory (hipMalloc): the
+// narrow form's premise (no L2 holds a slot line) broken on the host side;
+// the kernels run kSyncNarrow
+constexpr int kSyncCachedSlots = 5;
 constexpr size_t kFlagBytes = kFlagStride * sizeof(uint64_t);
 // A device engine's launch counters (xgmi_kernels.hip launch_number), uncached,
 // after its flag rows: a line with the launches completed, a line with the
@@ -205,6 +220,16 @@ struct PlanKernelParams {
 };
 hipError_t launch_plan_kernel(int op, int dtype, const PlanKernelParams& p, hipStream_t s);
 
+// kSyncUnsafe's kernels: the same engines compiled with plain stores into
+// peers' slots (xgmi_kernels.hip built a second time with
+// GLX_XGMI_UNSAFE_TU; the launchers above dispatch to them).
+hipError_t launch_oneshot_unsafe_stores(int op, int dtype, const OneShotParams& p,
+                                        hipStream_t s);
+hipError_t launch_twoshot_unsafe_stores(int op, int dtype, const TwoShotParams& p,
+                                        hipStream_t s);
+hipError_t launch_plan_kernel_unsafe_stores(int op, int dtype, const PlanKernelParams& p,
+                                            hipStream_t s);
+
 // Stream-ordered flag operations of the DMA steps engine (engine dmasteps,
 // executor.cc exchange): the host-issued program's copies (hipMemcpyPeerAsync
 // on the copy streams) and reduce launches, with every hand-off between them
@@ -249,5 +274,7 @@ size_t reduce_segment_bytes();
 // Tuning knobs of the vector kernel (lanes' unroll depth, grid cap per CU,
 // nontemporal loads/stores: 0/1, -1 = keep).
 void set_reduce_tuning(int unroll, int blocks_per_cu, int nontemporal);
+// The settings now in force (policy: 0..3 a fixed one, 4 automatic).
+void reduce_tuning(int* unroll, int* blocks_per_cu, int* policy);
 
 }  // namespace glx

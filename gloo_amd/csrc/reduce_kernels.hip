@@ -23,6 +23,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
+#include <mutex>
 #include <cstdlib>
 #include <type_traits>
 #include <vector>
@@ -274,13 +276,18 @@ __global__ __launch_bounds__(kBlock) void copy_bytes_kernel(char* __restrict__ d
   for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += step) dst[i] = src[i];
 }
 
-int g_copy_blocks = 64;  // grid of the copy kernel (workgroups)
-
 // ---- launch ---------------------------------------------------------------
 
-int g_unroll = 4;         // tuned on MI355X: tools/tune_reduce.py, profiles/r1_tune_reduce_nt.log
-int g_blocks_per_cu = 64; // grid cap = CUs * this (256 MiB fp32: one vector pass per lane)
-int g_num_cus = 0;
+// Process-wide launch settings.  Rank threads of one process launch
+// concurrently while glx_tune_reduce / glx_set_copy_blocks may write them, so
+// every setting is atomic (relaxed: each is read once per launch and any
+// value written is a valid one), and the CU count is read once
+// (executor*.cc keeps its settings the same way).
+std::atomic<int> g_copy_blocks{64};  // grid of the copy kernel (workgroups)
+std::atomic<int> g_unroll{4};  // tuned on MI355X: tools/tune_reduce.py, profiles/r1_tune_reduce_nt.log
+std::atomic<int> g_blocks_per_cu{64};  // grid cap = CUs * this (256 MiB fp32: one vector pass per lane)
+std::once_flag g_num_cus_once;
+int g_num_cus = 256;  // written once under g_num_cus_once
 // Cache policy of the reduce kernel's streams (StreamPolicy, or kPolAuto).
 // Measured on MI355X with uniform random fp32 (tools/tune_policy.py,
 // profiles/r4j_*, r4k_*): nontemporal loads always win; for the stores,
@@ -289,15 +296,16 @@ int g_num_cus = 0;
 // nontemporal stores are fastest beyond it (320 MiB: 161.9 vs 163.7 us;
 // 1 GiB: 527 vs 543 us).
 constexpr int kPolAuto = 4;
-int g_policy = kPolAuto;
-size_t g_wt_max_bytes = size_t(256) << 20;  // per stream, write-through up to here
+std::atomic<int> g_policy{kPolAuto};
+constexpr size_t kWtMaxBytes = size_t(256) << 20;  // per stream, write-through up to here
 
 int policy_for(size_t stream_bytes) {
-  if (g_policy != kPolAuto) {
+  const int pol = g_policy.load(std::memory_order_relaxed);
+  if (pol != kPolAuto) {
     // write-through streams are addressed by 32-bit buffer offsets
-    return g_policy == kPolNtWt && stream_bytes > kWtMaxStream ? kPolNt : g_policy;
+    return pol == kPolNtWt && stream_bytes > kWtMaxStream ? kPolNt : pol;
   }
-  return stream_bytes <= g_wt_max_bytes ? kPolNtWt : kPolNt;
+  return stream_bytes <= kWtMaxBytes ? kPolNtWt : kPolNt;
 }
 
 // Write-through stores for the fold (reduce_n) and copy kernels: the
@@ -308,7 +316,7 @@ bool use_wt(size_t stream_bytes) {
 }
 
 int num_cus() {
-  if (g_num_cus == 0) {
+  std::call_once(g_num_cus_once, [] {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
@@ -316,16 +324,16 @@ int num_cus() {
         n > 0) {
       g_num_cus = n;
     } else {
-      g_num_cus = 256;
+      (void)hipGetLastError();
     }
-  }
+  });
   return g_num_cus;
 }
 
 size_t grid_for(size_t work_items, int unroll) {
   size_t per_block = (size_t)kBlock * unroll;
   size_t blocks = (work_items + per_block - 1) / per_block;
-  size_t cap = (size_t)num_cus() * g_blocks_per_cu;
+  size_t cap = (size_t)num_cus() * (size_t)g_blocks_per_cu.load(std::memory_order_relaxed);
   if (blocks > cap) blocks = cap;
   if (blocks == 0) blocks = 1;
   return blocks;
@@ -398,7 +406,7 @@ hipError_t launch_typed(void* dst, const void* a, const void* b, size_t n,
       const S* x = static_cast<const S*>(a) + at;
       const S* y = static_cast<const S*>(b) + at;
       hipError_t e;
-      switch (g_unroll) {
+      switch (g_unroll.load(std::memory_order_relaxed)) {
         case 1: e = launch_vec<T, OP, 1>(d, x, y, h, nv, t, s, pol); break;
         case 2: e = launch_vec<T, OP, 2>(d, x, y, h, nv, t, s, pol); break;
         case 8: e = launch_vec<T, OP, 8>(d, x, y, h, nv, t, s, pol); break;
@@ -588,7 +596,8 @@ hipError_t launch_copy_blocks(void* dst, const void* src, size_t bytes, int grid
                               hipStream_t s) {
   if (bytes == 0) return hipSuccess;
   const uintptr_t pd = (uintptr_t)dst, ps = (uintptr_t)src;
-  const unsigned blocks = (unsigned)std::max(1, grid > 0 ? grid : g_copy_blocks);
+  const unsigned blocks =
+      (unsigned)std::max(1, grid > 0 ? grid : g_copy_blocks.load(std::memory_order_relaxed));
   if (pd % 16 != ps % 16) {
     hipLaunchKernelGGL(copy_bytes_kernel, dim3(blocks), dim3(kBlock), 0, s, (char*)dst,
                        (const char*)src, bytes);
@@ -609,10 +618,10 @@ hipError_t launch_copy_blocks(void* dst, const void* src, size_t bytes, int grid
 }
 
 void set_copy_blocks(int blocks) {
-  if (blocks > 0) g_copy_blocks = blocks;
+  if (blocks > 0) g_copy_blocks.store(blocks, std::memory_order_relaxed);
 }
 
-int copy_blocks() { return g_copy_blocks; }
+int copy_blocks() { return g_copy_blocks.load(std::memory_order_relaxed); }
 
 hipError_t launch_reduce(int op, int dtype, void* dst, const void* a,
                          const void* b, size_t n, hipStream_t s) {
@@ -676,9 +685,19 @@ hipError_t launch_reduce_n(int op, int dtype, void* dst, const void* const* srcs
 size_t reduce_segment_bytes() { return kSegBytes; }
 
 void set_reduce_tuning(int unroll, int blocks_per_cu, int nontemporal) {
-  if (unroll == 1 || unroll == 2 || unroll == 4 || unroll == 8) g_unroll = unroll;
-  if (blocks_per_cu > 0) g_blocks_per_cu = blocks_per_cu;
-  if (nontemporal >= 0 && nontemporal <= kPolAuto) g_policy = nontemporal;
+  if (unroll == 1 || unroll == 2 || unroll == 4 || unroll == 8) {
+    g_unroll.store(unroll, std::memory_order_relaxed);
+  }
+  if (blocks_per_cu > 0) g_blocks_per_cu.store(blocks_per_cu, std::memory_order_relaxed);
+  if (nontemporal >= 0 && nontemporal <= kPolAuto) {
+    g_policy.store(nontemporal, std::memory_order_relaxed);
+  }
+}
+
+void reduce_tuning(int* unroll, int* blocks_per_cu, int* policy) {
+  *unroll = g_unroll.load(std::memory_order_relaxed);
+  *blocks_per_cu = g_blocks_per_cu.load(std::memory_order_relaxed);
+  *policy = g_policy.load(std::memory_order_relaxed);
 }
 
 }  // namespace glx

@@ -170,7 +170,8 @@ __device__ __forceinline__ void copy_span(S* dst, const S* src, size_t a, size_t
 // Copy [a, b) of src to every dsts[d] for d < n (one load, n stores):
 // dsts[0 .. FIRST_REMOTE-1] are this rank's (policy LSP), the rest other
 // ranks' landing slots (system write-through).
-template <typename S, bool FAST, int LSP, int FIRST_REMOTE, int MAXD = kOsMaxRanks - 1>
+template <typename S, bool FAST, int LSP, int FIRST_REMOTE, int MAXD = kOsMaxRanks - 1,
+          int RSP = kStRemote>
 __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* src, size_t a,
                                              size_t b, bool aligned) {
   const Span sp = split_span<16 / sizeof(S)>(a, b, aligned);
@@ -182,7 +183,7 @@ __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* 
     for (int d = 0; d < MAXD; d++) {
       if (d < n) {
         if (d >= FIRST_REMOTE) {
-          put1<kStRemote>(reinterpret_cast<S*>(dsts[d]) + i, x);
+          put1<RSP>(reinterpret_cast<S*>(dsts[d]) + i, x);
         } else {
           put1<LSP>(reinterpret_cast<S*>(dsts[d]) + i, x);
         }
@@ -200,7 +201,7 @@ __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* 
     for (int d = 0; d < MAXD; d++) {
       if (d < n) {
         if (d >= FIRST_REMOTE) {
-          const VecOut<kStRemote> o(dsts[d], va);
+          const VecOut<RSP> o(dsts[d], va);
 #pragma unroll
           for (int u = 0; u < U; u++) o.put(i + u * kBlock, x[u]);
         } else {
@@ -217,7 +218,7 @@ __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* 
     for (int d = 0; d < MAXD; d++) {
       if (d < n) {
         if (d >= FIRST_REMOTE) {
-          VecOut<kStRemote>(dsts[d], va).put(i, x);
+          VecOut<RSP>(dsts[d], va).put(i, x);
         } else {
           VecOut<LSP>(dsts[d], va).put(i, x);
         }
@@ -234,7 +235,7 @@ __device__ __forceinline__ void scatter_span(char* const* dsts, int n, const S* 
 // result goes to the outs only); outs are other ranks' landing slots
 // (system write-through).
 template <typename T, int OP, bool FAST, bool LEFT = false, int MAXK = kOsMaxRanks,
-          bool KEEP = true>
+          bool KEEP = true, int RSP = kStRemote>
 __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
                                           const typename Elem<T, OP>::S* const* srcs, int P,
                                           char* const* outs, int nout, size_t a, size_t b,
@@ -259,7 +260,7 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
     if (KEEP) put1<LSP>(dst + i, acc);
 #pragma unroll
     for (int d = 0; d < MAXK - 1; d++) {
-      if (d < nout) put1<kStRemote>(reinterpret_cast<S*>(outs[d]) + i, acc);
+      if (d < nout) put1<RSP>(reinterpret_cast<S*>(outs[d]) + i, acc);
     }
   }
   // U vectors per lane, all U*P loads in flight before the chains: 4 for
@@ -296,7 +297,7 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
 #pragma unroll
     for (int d = 0; d < MAXK - 1; d++) {
       if (d < nout) {
-        const VecOut<kStRemote> o(outs[d], va);
+        const VecOut<RSP> o(outs[d], va);
 #pragma unroll
         for (int u = 0; u < U; u++) o.put(v + u * kBlock, acc[u]);
       }
@@ -316,7 +317,7 @@ __device__ __forceinline__ void fold_span(typename Elem<T, OP>::S* dst,
     if (KEEP) VecOut<LSP>(dst, va).put(v, acc);
 #pragma unroll
     for (int d = 0; d < MAXK - 1; d++) {
-      if (d < nout) VecOut<kStRemote>(outs[d], va).put(v, acc);
+      if (d < nout) VecOut<RSP>(outs[d], va).put(v, acc);
     }
   }
 }
@@ -364,12 +365,19 @@ __device__ __forceinline__ const uint64_t* flag_at(const uint64_t* row, int w) {
 // completed only -- enough when everything the flag publishes was stored into
 // the receiver's landing slot, uncached memory (MTYPE UC) that no L2 holds
 // (the device engines' protocol); the workgroup fence keeps
-// the compiler from moving the stores past the flag.
-__device__ __forceinline__ void release_stores(bool narrow) {
-  if (narrow) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  } else {
+// the compiler from moving the stores past the flag.  (sync: kernels.h
+// kSync*; the test-only modes kSyncNoRelease / kSyncUnsafe keep only a
+// compiler barrier, and their flag skips the workgroup barrier too
+// (flag_barrier): it may overtake the other waves' stores.)
+__device__ __forceinline__ void release_stores(int sync) {
+  if (sync == kSyncNoRelease || sync == kSyncUnsafe) {
+    asm volatile("" ::: "memory");
+    return;
+  }
+  if (sync == kSyncSystem) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   }
   // the compiler may drop the wait after the write-back when it can prove no
   // store is outstanding (MI355X_MICROARCH.md, compiler hazard): keep it
@@ -378,21 +386,32 @@ __device__ __forceinline__ void release_stores(bool narrow) {
 
 // Acquire after a flag.  system: this CU's L1 and this XCD's L2 invalidated
 // (buffer_inv sc0 sc1).  narrow: the L1 only (agent scope, buffer_inv sc1):
-// the landing slots are uncached, so no L2 line of them can be stale.
-__device__ __forceinline__ void acquire_loads(bool narrow) {
-  if (narrow) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  } else {
+// the landing slots are uncached, so no L2 line of them can be stale.  The
+// test-only kSyncNoAcquire / kSyncUnsafe keep a compiler barrier only.
+__device__ __forceinline__ void acquire_loads(int sync) {
+  if (sync == kSyncNoAcquire || sync == kSyncUnsafe) {
+    asm volatile("" ::: "memory");
+  } else if (sync == kSyncSystem) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
+}
+
+// The workgroup barrier between every wave's stores and the flag lane.  The
+// test-only kSyncNoRelease / kSyncUnsafe skip it: lane 0's flag then goes out
+// as soon as ITS wave has issued its stores -- the hazard of a flag that
+// overtakes the data, amplified so a one-GPU run can show the checks see it.
+__device__ __forceinline__ void flag_barrier(int sync) {
+  if (sync != kSyncNoRelease && sync != kSyncUnsafe) __syncthreads();
 }
 
 template <typename Want>
 __device__ __forceinline__ void release_flags(uint64_t* const* rows, int P, int rank, int w,
                                               uint64_t epoch, bool store, Want want,
-                                              bool narrow) {
-  release_stores(narrow);
-  __syncthreads();
+                                              int sync) {
+  release_stores(sync);
+  flag_barrier(sync);
   const int t = (int)threadIdx.x;
   if (t < P && t != rank && want(t)) put_flag(flag_at(rows[t], w), epoch, store);
 }
@@ -400,9 +419,9 @@ __device__ __forceinline__ void release_flags(uint64_t* const* rows, int P, int 
 // Every wave's stores complete and visible system-wide, then lane 0 stores
 // `value` into `word` (a flag in a peer's memory).
 __device__ __forceinline__ void signal_flag(uint64_t* word, uint64_t value, bool store,
-                                            bool narrow) {
-  release_stores(narrow);
-  __syncthreads();
+                                            int sync) {
+  release_stores(sync);
+  flag_barrier(sync);
   if (threadIdx.x == 0) put_flag(word, value, store);
 }
 
@@ -433,7 +452,7 @@ __device__ __forceinline__ void report_timeout(int* status, int* claim, int code
 // (diagnostics: PlanKernelParams::polls).
 __device__ __forceinline__ bool wait_flag(const uint64_t* word, uint64_t epoch, int peer,
                                           uint64_t start, uint64_t timeoutTicks, int* status,
-                                          int* claim, int* s_ok, bool narrow, bool acquire = true,
+                                          int* claim, int* s_ok, int sync, bool acquire = true,
                                           int where = 0, uint32_t* polls = nullptr) {
   if (threadIdx.x == 0) {
     int ok = 1;
@@ -455,7 +474,7 @@ __device__ __forceinline__ bool wait_flag(const uint64_t* word, uint64_t epoch, 
     }
     if (polls != nullptr) *polls += spin;
     // drop any stale copy of the landing lines before anyone reads them
-    if (acquire) acquire_loads(narrow);
+    if (acquire) acquire_loads(sync);
     *s_ok = ok;
   }
   __syncthreads();
@@ -514,7 +533,7 @@ __device__ __forceinline__ void finish_launch(uint64_t* ctr, int G) {
 
 // ---- one-shot ---------------------------------------------------------------
 
-template <typename T, int OP, bool FAST>
+template <typename T, int OP, bool FAST, int RSP>
 __device__ __forceinline__ void oneshot_body(const OneShotParams& p) {
   using S = typename Elem<T, OP>::S;
   __shared__ int s_ok;
@@ -536,16 +555,16 @@ __device__ __forceinline__ void oneshot_body(const OneShotParams& p) {
     if (j >= p.P) j -= p.P;
     to[d - 1] = d < p.P ? p.push[par][j] : nullptr;
   }
-  scatter_span<S, FAST, kStPlain, 0>(to, p.P - 1, buf, e0, e1, aligned);
+  scatter_span<S, FAST, kStPlain, 0, kOsMaxRanks - 1, RSP>(to, p.P - 1, buf, e0, e1, aligned);
   release_flags(p.flagOut, p.P, p.rank, w, epoch, p.flagStore != 0, [](int) { return true; },
-                p.narrow != 0);
+                p.narrow);
 
   // 2. wait
   const uint64_t start = __builtin_amdgcn_s_memrealtime();
   for (int k = 0; k < p.P; k++) {
     if (k == p.rank) continue;
     if (!wait_flag(flag_at(p.flagIn, k * p.G + w), epoch, k, start, p.timeoutTicks,
-                   p.status, p.claim, &s_ok, p.narrow != 0)) {
+                   p.status, p.claim, &s_ok, p.narrow)) {
       return;
     }
   }
@@ -569,14 +588,14 @@ __device__ __forceinline__ void oneshot_body(const OneShotParams& p) {
 
 // >= 2 waves per SIMD: every rank's grid (<= kOsMaxSlices workgroups) stays
 // resident even when a few ranks share one GPU
-template <typename T, int OP>
+template <typename T, int OP, int RSP>
 __global__ __launch_bounds__(kBlock, 2) void oneshot_kernel(OneShotParams p) {
-  oneshot_body<T, OP, false>(p);
+  oneshot_body<T, OP, false, RSP>(p);
 }
 
 // ---- two-shot ---------------------------------------------------------------
 
-template <typename T, int OP, bool FAST>
+template <typename T, int OP, bool FAST, int RSP>
 __device__ __forceinline__ void twoshot_body(const TwoShotParams& p) {
   using S = typename Elem<T, OP>::S;
   __shared__ int s_ok;
@@ -609,13 +628,13 @@ __device__ __forceinline__ void twoshot_body(const TwoShotParams& p) {
     if (j >= p.P) j -= p.P;
     size_t a, b;
     if (span(j, a, b)) {
-      copy_span<S, FAST, kStRemote>(reinterpret_cast<S*>(p.rsPush[par][j]), buf, a, b, aligned);
+      copy_span<S, FAST, RSP>(reinterpret_cast<S*>(p.rsPush[par][j]), buf, a, b, aligned);
     }
   }
   release_flags(p.flagAOut, p.P, p.rank, w, epoch, p.flagStore != 0, [&](int j) {
     size_t a, b;
     return span(j, a, b);
-  }, p.narrow != 0);
+  }, p.narrow);
   stamp(1);
 
   // 2. fold my range's slice from every peer's copy; result to my buffer
@@ -626,7 +645,7 @@ __device__ __forceinline__ void twoshot_body(const TwoShotParams& p) {
     for (int k = 0; k < p.P; k++) {
       if (k == p.rank) continue;
       if (!wait_flag(flag_at(p.flagAIn, k * p.G + w), epoch, k, start, p.timeoutTicks,
-                     p.status, p.claim, &s_ok, p.narrow != 0)) {
+                     p.status, p.claim, &s_ok, p.narrow)) {
         return;
       }
     }
@@ -645,9 +664,9 @@ __device__ __forceinline__ void twoshot_body(const TwoShotParams& p) {
       if (j >= p.P) j -= p.P;
       outs[d - 1] = d < p.P ? p.agPush[par][j] : nullptr;
     }
-    fold_span<T, OP, FAST>(buf, src, p.P, outs, p.P - 1, a, b, aligned);
+    fold_span<T, OP, FAST, false, kOsMaxRanks, true, RSP>(buf, src, p.P, outs, p.P - 1, a, b, aligned);
     release_flags(p.flagBOut, p.P, p.rank, w, epoch, p.flagStore != 0,
-                  [](int) { return true; }, p.narrow != 0);
+                  [](int) { return true; }, p.narrow);
   }
   stamp(3);
 
@@ -657,7 +676,7 @@ __device__ __forceinline__ void twoshot_body(const TwoShotParams& p) {
     if (j < 0) j += p.P;
     if (!span(j, a, b)) continue;
     if (!wait_flag(flag_at(p.flagBIn, j * p.G + w), epoch, j, start, p.timeoutTicks,
-                   p.status, p.claim, &s_ok, p.narrow != 0)) {
+                   p.status, p.claim, &s_ok, p.narrow)) {
       return;
     }
     if (d == 1) stamp(4);
@@ -668,9 +687,9 @@ __device__ __forceinline__ void twoshot_body(const TwoShotParams& p) {
   finish_launch(p.epochCtr, p.G);
 }
 
-template <typename T, int OP>
+template <typename T, int OP, int RSP>
 __global__ __launch_bounds__(kBlock, 2) void twoshot_kernel(TwoShotParams p) {
-  twoshot_body<T, OP, false>(p);
+  twoshot_body<T, OP, false, RSP>(p);
 }
 
 // ---- plan kernel --------------------------------------------------------------
@@ -688,14 +707,14 @@ __device__ __forceinline__ bool seg_part(const DevSegment& sg, int w, size_t& a,
 // programs without FOLD steps (ring, halving-doubling, function-style ring):
 // the 8-way fold's registers would cut the resident workgroups per CU from
 // the 2-source variant's count (kernel-resource-usage) to 3.
-template <typename T, int OP, int MAXSRC, bool FAST>
+template <typename T, int OP, int MAXSRC, bool FAST, int RSP>
 __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
   using S = typename Elem<T, OP>::S;
   __shared__ int s_ok;
   const int w = blockIdx.x;
   S* buf = reinterpret_cast<S*>(p.buf);
   const bool aligned = ((uintptr_t)p.buf % 16) == 0;
-  const bool narrow = p.narrow != 0;
+  const int sync = p.narrow;  // kernels.h kSync*
   // diagnostics (GLOO_AMD_DEVTRACE=1): per workgroup and step, when the step
   // started and when its wait (if any) was satisfied
   uint64_t* tr = p.trace != nullptr ? p.trace + (size_t)w * (2 * (size_t)p.nsteps + 1) : nullptr;
@@ -719,7 +738,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
         if (seq > (uint64_t)p.slots &&
             !wait_flag(flag_at(st.credit, w), seq - p.slots, st.peer,
                        __builtin_amdgcn_s_memrealtime(), p.timeoutTicks, p.status, p.claim,
-                       &s_ok, narrow, /*acquire=*/false, 1 + i, &polls)) {
+                       &s_ok, sync, /*acquire=*/false, 1 + i, &polls)) {
           return;
         }
         stamp(2 * i + 1);
@@ -734,7 +753,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
           const bool over = g >= st.pre0 && g < st.pre1;
           if (st.kind == kStepCopyPre) {
             if (over) {
-              scatter_span<S, FAST, FAST ? kStLocalWt : kStPlain, 1, 2>(outs, 2, src, a, b,
+              scatter_span<S, FAST, FAST ? kStLocalWt : kStPlain, 1, 2, RSP>(outs, 2, src, a, b,
                                                                         aligned);
             } else {
               copy_span<S, FAST, FAST ? kStLocalWt : kStPlain>(buf, src, a, b, aligned);
@@ -742,9 +761,9 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
           } else if (!over) {
             fold_span<T, OP, FAST, true, 2>(buf, srcs, 2, nullptr, 0, a, b, aligned);
           } else if (st.kind == kStepReducePreForward) {
-            fold_span<T, OP, FAST, true, 2, false>(buf, srcs, 2, outs + 1, 1, a, b, aligned);
+            fold_span<T, OP, FAST, true, 2, false, RSP>(buf, srcs, 2, outs + 1, 1, a, b, aligned);
           } else {
-            fold_span<T, OP, FAST, true, 2>(buf, srcs, 2, outs + 1, 1, a, b, aligned);
+            fold_span<T, OP, FAST, true, 2, true, RSP>(buf, srcs, 2, outs + 1, 1, a, b, aligned);
           }
         }
         break;  // the SEND signals the message once its other segments are stored
@@ -756,7 +775,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
         if (seq > (uint64_t)p.slots &&
             !wait_flag(flag_at(st.credit, w), seq - p.slots, st.peer,
                        __builtin_amdgcn_s_memrealtime(), p.timeoutTicks, p.status, p.claim,
-                       &s_ok, narrow, /*acquire=*/false, 1 + i, &polls)) {
+                       &s_ok, sync, /*acquire=*/false, 1 + i, &polls)) {
           return;
         }
         stamp(2 * i + 1);
@@ -766,7 +785,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
             size_t a, b;
             if (g >= st.pre0 && g < st.pre1) continue;  // stored by the step before
             if (seg_part(p.segs[g], w, a, b)) {
-              copy_span<S, FAST, kStRemote>(reinterpret_cast<S*>(dst), buf, a, b, aligned);
+              copy_span<S, FAST, RSP>(reinterpret_cast<S*>(dst), buf, a, b, aligned);
             }
           }
         } else {
@@ -778,21 +797,21 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
             size_t a, b;
             if (!seg_part(p.segs[g], w, a, b)) continue;
             if (st.kind == kStepCopySend) {
-              scatter_span<S, FAST, FAST ? kStLocalWt : kStPlain, 1, 2>(outs, 2, src, a, b,
+              scatter_span<S, FAST, FAST ? kStLocalWt : kStPlain, 1, 2, RSP>(outs, 2, src, a, b,
                                                                         aligned);
             } else if (st.kind == kStepReduceForward) {
-              fold_span<T, OP, FAST, true, 2, false>(buf, srcs, 2, outs + 1, 1, a, b, aligned);
+              fold_span<T, OP, FAST, true, 2, false, RSP>(buf, srcs, 2, outs + 1, 1, a, b, aligned);
             } else {
-              fold_span<T, OP, FAST, true, 2>(buf, srcs, 2, outs + 1, 1, a, b, aligned);
+              fold_span<T, OP, FAST, true, 2, true, RSP>(buf, srcs, 2, outs + 1, 1, a, b, aligned);
             }
           }
         }
-        signal_flag(flag_at(st.flag, w), seq, p.flagStore != 0, narrow);
+        signal_flag(flag_at(st.flag, w), seq, p.flagStore != 0, sync);
         break;
       }
       case 1:  // RECV
         if (!wait_flag(flag_at(st.flag, w), seq, st.peer, __builtin_amdgcn_s_memrealtime(),
-                       p.timeoutTicks, p.status, p.claim, &s_ok, narrow, true, 1 + i, &polls)) {
+                       p.timeoutTicks, p.status, p.claim, &s_ok, sync, true, 1 + i, &polls)) {
           return;
         }
         stamp(2 * i + 1);
@@ -845,15 +864,18 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
   finish_launch(p.runCtr, p.G);
 }
 
-template <typename T, int OP, int MAXSRC>
+template <typename T, int OP, int MAXSRC, int RSP>
 __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
-  if (p.fast) {
-    plan_body<T, OP, MAXSRC, true>(p);
-  } else {
-    plan_body<T, OP, MAXSRC, false>(p);
+  if constexpr (RSP == kStRemote) {  // the test-only plain-store build runs plain streams
+    if (p.fast) {
+      plan_body<T, OP, MAXSRC, true, RSP>(p);
+      return;
+    }
   }
+  plan_body<T, OP, MAXSRC, false, RSP>(p);
 }
 
+#ifndef GLX_XGMI_UNSAFE_TU
 // ---- flag operations of the DMA steps engine (kernels.h FlagOpsParams) ------
 
 // One wave; lane 0 walks the ops in order.  A wait polls memory-side
@@ -883,19 +905,33 @@ __global__ __launch_bounds__(64) void flag_ops_kernel(FlagOpsParams p) {
     }
   }
 }
+#endif
 
 // ---- launch -------------------------------------------------------------------
+
+// This file is compiled twice (Makefile): as the product's engines, whose
+// stores into peers' slots are system-scope write-through (kStRemote), and
+// with GLX_XGMI_UNSAFE_TU as the TEST-ONLY kSyncUnsafe build of the same
+// engines with plain stores there (kernels.h, tests/test_sync_control_gpu.py);
+// the product launchers hand kSyncUnsafe launches to the second build.
+#ifdef GLX_XGMI_UNSAFE_TU
+constexpr int kTuRsp = kStPlain;
+#define GLX_TU_NAME(f) f##_unsafe_stores
+#else
+constexpr int kTuRsp = kStRemote;
+#define GLX_TU_NAME(f) f
+#endif
 
 template <typename T>
 hipError_t launch_os_op(int op, const OneShotParams& p, hipStream_t s) {
   const dim3 grid((unsigned)p.G), block(kBlock);
   switch (op) {
-    case GLX_SUM: hipLaunchKernelGGL((oneshot_kernel<T, GLX_SUM>), grid, block, 0, s, p); break;
+    case GLX_SUM: hipLaunchKernelGGL((oneshot_kernel<T, GLX_SUM, kTuRsp>), grid, block, 0, s, p); break;
     case GLX_PRODUCT:
-      hipLaunchKernelGGL((oneshot_kernel<T, GLX_PRODUCT>), grid, block, 0, s, p);
+      hipLaunchKernelGGL((oneshot_kernel<T, GLX_PRODUCT, kTuRsp>), grid, block, 0, s, p);
       break;
-    case GLX_MAX: hipLaunchKernelGGL((oneshot_kernel<T, GLX_MAX>), grid, block, 0, s, p); break;
-    case GLX_MIN: hipLaunchKernelGGL((oneshot_kernel<T, GLX_MIN>), grid, block, 0, s, p); break;
+    case GLX_MAX: hipLaunchKernelGGL((oneshot_kernel<T, GLX_MAX, kTuRsp>), grid, block, 0, s, p); break;
+    case GLX_MIN: hipLaunchKernelGGL((oneshot_kernel<T, GLX_MIN, kTuRsp>), grid, block, 0, s, p); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -905,23 +941,24 @@ template <typename T>
 hipError_t launch_ts_op(int op, const TwoShotParams& p, hipStream_t s) {
   const dim3 grid((unsigned)p.G), block(kBlock);
   switch (op) {
-    case GLX_SUM: hipLaunchKernelGGL((twoshot_kernel<T, GLX_SUM>), grid, block, 0, s, p); break;
+    case GLX_SUM: hipLaunchKernelGGL((twoshot_kernel<T, GLX_SUM, kTuRsp>), grid, block, 0, s, p); break;
     case GLX_PRODUCT:
-      hipLaunchKernelGGL((twoshot_kernel<T, GLX_PRODUCT>), grid, block, 0, s, p);
+      hipLaunchKernelGGL((twoshot_kernel<T, GLX_PRODUCT, kTuRsp>), grid, block, 0, s, p);
       break;
-    case GLX_MAX: hipLaunchKernelGGL((twoshot_kernel<T, GLX_MAX>), grid, block, 0, s, p); break;
-    case GLX_MIN: hipLaunchKernelGGL((twoshot_kernel<T, GLX_MIN>), grid, block, 0, s, p); break;
+    case GLX_MAX: hipLaunchKernelGGL((twoshot_kernel<T, GLX_MAX, kTuRsp>), grid, block, 0, s, p); break;
+    case GLX_MIN: hipLaunchKernelGGL((twoshot_kernel<T, GLX_MIN, kTuRsp>), grid, block, 0, s, p); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
+#ifndef GLX_XGMI_UNSAFE_TU
 template <typename T, int OP>
 const void* engine_kernel(int kernel) {
-  if (kernel == 0) return (const void*)oneshot_kernel<T, OP>;
-  if (kernel == 1) return (const void*)twoshot_kernel<T, OP>;
-  if (kernel == 3) return (const void*)plan_kernel<T, OP, 2>;
-  return (const void*)plan_kernel<T, OP, kOsMaxRanks>;
+  if (kernel == 0) return (const void*)oneshot_kernel<T, OP, kStRemote>;
+  if (kernel == 1) return (const void*)twoshot_kernel<T, OP, kStRemote>;
+  if (kernel == 3) return (const void*)plan_kernel<T, OP, 2, kStRemote>;
+  return (const void*)plan_kernel<T, OP, kOsMaxRanks, kStRemote>;
 }
 
 template <typename T>
@@ -944,21 +981,23 @@ int resident_typed(int kernel, int op) {
   return perCu * cus;
 }
 
+#endif
+
 template <typename T, int MAXSRC>
 hipError_t launch_pk_src(int op, const PlanKernelParams& p, hipStream_t s) {
   const dim3 grid((unsigned)p.G), block(kBlock);
   switch (op) {
     case GLX_SUM:
-      hipLaunchKernelGGL((plan_kernel<T, GLX_SUM, MAXSRC>), grid, block, 0, s, p);
+      hipLaunchKernelGGL((plan_kernel<T, GLX_SUM, MAXSRC, kTuRsp>), grid, block, 0, s, p);
       break;
     case GLX_PRODUCT:
-      hipLaunchKernelGGL((plan_kernel<T, GLX_PRODUCT, MAXSRC>), grid, block, 0, s, p);
+      hipLaunchKernelGGL((plan_kernel<T, GLX_PRODUCT, MAXSRC, kTuRsp>), grid, block, 0, s, p);
       break;
     case GLX_MAX:
-      hipLaunchKernelGGL((plan_kernel<T, GLX_MAX, MAXSRC>), grid, block, 0, s, p);
+      hipLaunchKernelGGL((plan_kernel<T, GLX_MAX, MAXSRC, kTuRsp>), grid, block, 0, s, p);
       break;
     case GLX_MIN:
-      hipLaunchKernelGGL((plan_kernel<T, GLX_MIN, MAXSRC>), grid, block, 0, s, p);
+      hipLaunchKernelGGL((plan_kernel<T, GLX_MIN, MAXSRC, kTuRsp>), grid, block, 0, s, p);
       break;
     default: return hipErrorInvalidValue;
   }
@@ -972,6 +1011,7 @@ hipError_t launch_pk_op(int op, const PlanKernelParams& p, hipStream_t s) {
 
 }  // namespace
 
+#ifndef GLX_XGMI_UNSAFE_TU
 int device_engine_resident_blocks(int kernel, int op, int dtype) {
   switch (dtype) {
     case GLX_INT8: return resident_typed<int8_t>(kernel, op);
@@ -987,7 +1027,12 @@ int device_engine_resident_blocks(int kernel, int op, int dtype) {
   return 0;
 }
 
-hipError_t launch_oneshot(int op, int dtype, const OneShotParams& p, hipStream_t s) {
+#endif
+
+hipError_t GLX_TU_NAME(launch_oneshot)(int op, int dtype, const OneShotParams& p, hipStream_t s) {
+#ifndef GLX_XGMI_UNSAFE_TU
+  if (p.narrow == kSyncUnsafe) return launch_oneshot_unsafe_stores(op, dtype, p, s);
+#endif
   if (p.status == nullptr || p.claim == nullptr || p.epochCtr == nullptr) {
     return hipErrorInvalidValue;
   }
@@ -1010,7 +1055,11 @@ hipError_t launch_oneshot(int op, int dtype, const OneShotParams& p, hipStream_t
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_plan_kernel(int op, int dtype, const PlanKernelParams& p, hipStream_t s) {
+hipError_t GLX_TU_NAME(launch_plan_kernel)(int op, int dtype, const PlanKernelParams& p,
+                                           hipStream_t s) {
+#ifndef GLX_XGMI_UNSAFE_TU
+  if (p.narrow == kSyncUnsafe) return launch_plan_kernel_unsafe_stores(op, dtype, p, s);
+#endif
   if (p.G < 1 || p.G > kOsMaxSlices || p.nsteps < 0 || p.steps == nullptr ||
       p.segs == nullptr || p.foldSrc == nullptr || p.status == nullptr || p.claim == nullptr ||
       p.runCtr == nullptr ||
@@ -1031,7 +1080,10 @@ hipError_t launch_plan_kernel(int op, int dtype, const PlanKernelParams& p, hipS
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_twoshot(int op, int dtype, const TwoShotParams& p, hipStream_t s) {
+hipError_t GLX_TU_NAME(launch_twoshot)(int op, int dtype, const TwoShotParams& p, hipStream_t s) {
+#ifndef GLX_XGMI_UNSAFE_TU
+  if (p.narrow == kSyncUnsafe) return launch_twoshot_unsafe_stores(op, dtype, p, s);
+#endif
   size_t maxLen = 0;
   for (int c = 0; c < p.P && c < kOsMaxRanks; c++) {
     maxLen = p.rangeLen[c] > maxLen ? p.rangeLen[c] : maxLen;
@@ -1055,6 +1107,7 @@ hipError_t launch_twoshot(int op, int dtype, const TwoShotParams& p, hipStream_t
   return hipErrorInvalidValue;
 }
 
+#ifndef GLX_XGMI_UNSAFE_TU
 hipError_t launch_flag_ops(const FlagOpsParams& p, hipStream_t s) {
   if (p.n < 1 || p.n > kFlagOpsMax || p.status == nullptr || p.claim == nullptr) {
     return hipErrorInvalidValue;
@@ -1068,5 +1121,6 @@ hipError_t launch_flag_ops(const FlagOpsParams& p, hipStream_t s) {
   hipLaunchKernelGGL(flag_ops_kernel, dim3(1), dim3(64), 0, s, p);
   return hipGetLastError();
 }
+#endif
 
 }  // namespace glx

@@ -131,6 +131,10 @@ int glx_enable_peer(int dev_a, int dev_b);
  * (default: 2 while one stream is at most 256 MiB -- the Infinity Cache's
  * size -- and 1 above). */
 int glx_tune_reduce(int unroll, int blocks_per_cu, int nontemporal);
+/* The reduce kernel's settings now in force (policy 4 = automatic).  The
+ * settings are process-wide and atomic: rank threads may launch while
+ * another thread tunes. */
+int glx_reduce_tuning(int* unroll, int* blocks_per_cu, int* policy);
 /* glx_reduce on more than this many bytes per stream goes out as consecutive
  * kernel launches over equal segments of at most this size (one grid-stride
  * launch over 1 GiB streams ran 6 % slower on MI355X): a
@@ -214,7 +218,13 @@ int glx_set_engine_streams(int fast);
  * (s_waitcnt vmcnt(0)) before a flag and the CU's L1 invalidated after a wait
  * (agent scope); -1 = automatic (default: narrow).  Env
  * GLOO_AMD_SYNC=system|narrow.
- * Every rank may choose independently (the protocol is the same). */
+ * Every rank may choose independently (the protocol is the same).
+ * TEST ONLY, deliberately broken positive controls for the suite's stale-data
+ * checks (results may be wrong; never for use): 2 = narrow without the
+ * consumer's acquire, 3 = narrow without the producer's store-completion
+ * wait, 4 = neither, with plain (write-back) stores into peers' slots, 5 =
+ * narrow with every engine's landing slots in cached memory.  Env
+ * GLOO_AMD_SYNC=unsafe_noacquire|unsafe_norelease|unsafe_test|unsafe_cached. */
 int glx_set_device_sync(int mode);
 
 /* Number of visible HIP devices (0 when no GPU). */

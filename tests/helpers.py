@@ -214,6 +214,7 @@ def rank_env(P, device_engines="shared"):
     x 2 queues measured time-sliced, profiles/r7g_queue_sweep.txt)."""
     import os
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.setdefault("PYTHONFAULTHANDLER", "1")  # a crashing rank prints its stacks
     env.pop("GLOO_AMD_DEVICE_ENGINES", None)
     if device_engines is not None:
         env["GLOO_AMD_DEVICE_ENGINES"] = device_engines

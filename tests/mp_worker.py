@@ -46,6 +46,8 @@ sys.path.insert(0, HERE)
 
 
 def main():
+    import faulthandler
+    faulthandler.enable()  # a crash of any rank prints its threads' stacks
     store_dir, rank, size, algo = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
     import numpy as np
     import torch
@@ -76,7 +78,8 @@ def main():
     if algo.startswith("soak:"):
         parts = algo.split(":")
         return run_soak(store_dir, rank, size, int(parts[1]),
-                        uneven=parts[2] if len(parts) > 2 else "")
+                        uneven=parts[2] if len(parts) > 2 else "",
+                        n=int(parts[3]) if len(parts) > 3 and parts[3] else 1 << 20)
     if algo.startswith("big:"):
         return run_big(store_dir, rank, size, algo[len("big:"):])
     if algo == "maxcount":
@@ -1020,7 +1023,7 @@ def run_graph_overlap(store_dir, rank, size, kind, close_first=False):
     print("OK")
 
 
-def run_soak(store_dir, rank, size, runs, uneven=""):
+def run_soak(store_dir, rank, size, runs, uneven="", n=1 << 20):
     """One instance of each device engine's algorithm run `runs` times back to
     back (a training job's shape: the run counter, the message numbers
     j * perRun + seq and the landing slots alternate across many kernel
@@ -1040,7 +1043,14 @@ def run_soak(store_dir, rank, size, runs, uneven=""):
     sits ahead of the collective in rank 0's only queue while the other
     ranks' collectives hold the CUs waiting for rank 0 -- a cycle that exists
     only when ranks share a GPU, which is why the automatic choice keeps such
-    ranks on host-issued steps."""
+    ranks on host-issued steps.
+
+    n: elements per rank.  A small n (a few thousand) makes every
+    workgroup's share of a landing slot a few hundred bytes that its CU read
+    two runs before (the slots alternate): L1-warm re-reads, the guide's
+    near-certain stale case without an acquire (MI355X_MICROARCH.md,
+    "Stale without an agent-scope acquire") -- the sharp detector for the
+    test-only broken sync modes (tests/test_sync_control_gpu.py)."""
     import random
     import time
 
@@ -1052,10 +1062,9 @@ def run_soak(store_dir, rank, size, runs, uneven=""):
     ctx = gloo_amd.rendezvous.Context(rank, size, 0)
     ctx.setTimeout(30)
     ctx.connectFullMesh(store)
-    # 2^20: a length the plan kernel takes at every P here (ragged lengths
-    # whose chunks land at different 16-byte phases in one region keep the
-    # host-issued steps, plan.h SyncTable::safe; the fuzz covers those)
-    n = 1 << 20
+    # 2^20 (default): a length the plan kernel takes at every P here (ragged
+    # lengths whose chunks land at different 16-byte phases in one region keep
+    # the host-issued steps, plan.h SyncTable::safe; the fuzz covers those)
     dev = torch.device("cuda:0")
 
     def inputs(r, it):
@@ -1119,6 +1128,10 @@ def run_soak(store_dir, rank, size, runs, uneven=""):
     for r in range(size):
         store.get("soak/done/%d" % r, timeout_ms=60000)
     print("ENGINES rank %d %s" % (rank, engines))
+    counts = {}
+    for k, _, _ in bad:
+        counts[k] = counts.get(k, 0) + 1
+    print("BADRUNS rank %d %s of %d runs each" % (rank, counts, runs), flush=True)
     if bad:
         print("MISMATCH rank %d %s" % (rank, bad[:10]))
         sys.exit(1)

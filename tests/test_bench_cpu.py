@@ -450,3 +450,81 @@ def test_reduce_segments_follow_the_library():
     assert bench.reduce_segments(256 << 20) == 1
     assert bench.reduce_segments((256 << 20) + 16) == 2
     assert bench.reduce_segments(1 << 30) == 4
+
+
+def _refill_worker(rank, world, port, fault, use_digest, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 1 << 14
+    srcs = [bench.synthetic(torch, n, "f32", torch.device("cpu"), 77 + r) for r in range(world)]
+    total = srcs[0].clone()
+    for x in srcs[1:]:
+        total = total + x
+    golden = bench.sha256_of(total) if use_digest else None
+    buf = torch.empty_like(total)
+    calls = [0]
+
+    def run_once():
+        k = calls[0]
+        calls[0] += 1
+        buf.copy_(total)
+        if fault == "stale_run" and k == 3 and rank == 1:
+            # one rank's run 3 kept a chunk of its own input (a stale hand-off)
+            buf[:n // 8] = srcs[rank][:n // 8]
+        elif fault == "one_ulp" and k == 1 and rank == 0:
+            # one element one ulp off: below result_check's tolerance, but the
+            # ranks' bits now differ (and the reference digest, if any)
+            buf[5] = torch.nextafter(buf[5], torch.tensor(2.0))
+        return buf
+
+    ok, detail, last = bench.refill_checks(torch, dist, srcs[rank], run_once, runs=5,
+                                           golden_sha=golden)
+    q.put((rank, ok, detail, calls[0]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fault,use_digest", [(None, True), (None, False),
+                                              ("stale_run", True), ("stale_run", False),
+                                              ("one_ulp", True), ("one_ulp", False)])
+def test_refill_checks_catch_a_wrong_run_on_any_rank(fault, use_digest):
+    """after a candidate's timing, K >= 5 refilled runs are
+    checked on EVERY rank (bench.refill_checks) -- a stale hand-off on one
+    rank in one run fails the candidate on all ranks alike, and says which
+    run and rank; a one-ulp difference below result_check's tolerance is
+    still caught by the cross-rank checksum (and the digest)."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_refill_worker, args=(r, 2, port, fault, use_digest, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [o[3] for o in out] == [bench.REFILL_RUNS] * 2 and bench.REFILL_RUNS >= 5
+    oks = [o[1] for o in out]
+    details = [o[2] for o in out]
+    assert details[0]["bad"] == details[1]["bad"]  # every rank reaches the same verdict
+    if fault is None:
+        assert oks == [True, True] and details[0]["bad_count"] == 0
+        assert details[0]["digest_checked"] is use_digest
+    elif fault == "stale_run":
+        assert oks == [False, False]
+        b = details[0]["bad"]
+        assert {(e["run"], e["rank"]) for e in b} >= {(3, 1)}
+        assert not [e for e in b if e["run"] != 3]
+        assert any(e["result_check"] is False for e in b if e["rank"] == 1)
+        if use_digest:
+            assert any(e["digest"] is False for e in b if e["rank"] == 1)
+    else:
+        assert oks == [False, False]
+        b = details[0]["bad"]
+        assert b and all(e["run"] == 1 and not e["ranks_agree"] for e in b)
+        assert all(e["result_check"] for e in b)  # below the weighted sum's resolution
+        if use_digest:
+            assert [e["digest"] for e in b if e["rank"] == 0] == [False]

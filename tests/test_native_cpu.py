@@ -252,3 +252,59 @@ def test_allreduce_options_assignment_goes_through_the_setters():
     assert opts._in_ptrs[1] == 1
     opts.inputs = []
     assert opts._in_ptrs is None and opts.inputs == []
+
+
+def test_reduce_tuning_is_atomic_across_threads():
+    """the reduce kernel's process-wide settings are written by
+    glx_tune_reduce while rank threads launch; every read sees a value some
+    thread wrote (std::atomic, reduce_kernels.hip), never a torn or stale
+    default, and the defaults come back."""
+    u, b, p = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    assert _lib.lib.glx_reduce_tuning(ctypes.byref(u), ctypes.byref(b), ctypes.byref(p)) == 0
+    defaults = (u.value, b.value, p.value)
+    assert defaults == (4, 64, 4)
+    choices = [(1, 8, 0), (2, 16, 1), (4, 32, 2), (8, 48, 3), (4, 64, 4)]
+    seen, errs = [], []
+
+    def worker(k):
+        uu, bb, pp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        for i in range(3000):
+            c = choices[(k + i) % len(choices)]
+            if _lib.lib.glx_tune_reduce(*c) != 0:
+                errs.append(c)
+            _lib.lib.glx_reduce_tuning(ctypes.byref(uu), ctypes.byref(bb), ctypes.byref(pp))
+            seen.append((uu.value, bb.value, pp.value))
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+    try:
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    finally:
+        assert _lib.lib.glx_tune_reduce(*defaults) == 0
+    assert not errs
+    assert {s[0] for s in seen} <= {c[0] for c in choices}
+    assert {s[1] for s in seen} <= {c[1] for c in choices}
+    assert {s[2] for s in seen} <= {c[2] for c in choices}
+    assert _lib.lib.glx_reduce_tuning(ctypes.byref(u), ctypes.byref(b), ctypes.byref(p)) == 0
+    assert (u.value, b.value, p.value) == defaults
+    with pytest.raises(gloo_amd.EnforceNotMet):
+        gloo_amd.errors.check(_lib.lib.glx_tune_reduce(3, 64, 4))
+
+
+def test_device_sync_modes_round_trip_and_reject():
+    """The product's modes (auto, system, narrow) and the test-only broken
+    positive controls (unsafe_*: kernels.h kSyncNoAcquire .. kSyncUnsafe) are
+    accepted; anything else is refused."""
+    try:
+        for m in ("system", "narrow", "unsafe_noacquire", "unsafe_norelease", "unsafe_test",
+                  "unsafe_cached", "auto"):
+            gloo_amd.set_device_sync(m)
+        for code in (6, -2):
+            with pytest.raises(gloo_amd.EnforceNotMet):
+                gloo_amd.errors.check(_lib.lib.glx_set_device_sync(code))
+        with pytest.raises(KeyError):
+            gloo_amd.set_device_sync("broken")
+    finally:
+        gloo_amd.set_device_sync("auto")

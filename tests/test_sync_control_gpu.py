@@ -1,0 +1,83 @@
+"""Positive controls for the suite's stale-data checks.
+
+The device engines hand data over through flag words with the narrow sync
+(xgmi_kernels.hip release_stores / acquire_loads).  A check that
+cannot fail a deliberately broken hand-off certifies nothing, so the library
+carries TEST-ONLY broken sync modes (kernels.h kSyncNoAcquire ..
+kSyncCachedSlots, GLOO_AMD_SYNC=unsafe_*) and these tests show which of them
+the checks catch on one GPU:
+
+* the soak at a small buffer (4096 elements: every workgroup re-reads a few KB
+  of landing slot its CU read two messages before within the same launch --
+  L1-warm, the guide's near-certain stale case) is exact under the product's
+  narrow sync at P = 4 and 8, and wrong in (nearly) every run of the ring on
+  every rank once the consumer's acquire is dropped (unsafe_noacquire;
+  profiles/round6/sync_control_*.json: 200 of 200 runs at P = 4 and 8);
+* dropping the producer's store-completion wait (unsafe_norelease, even with
+  the workgroup barrier before the flag removed) was NOT caught on one GPU in
+  200 runs at P = 2, 4 and 8: the stores land long before a consumer's poll,
+  acquire and loads; that hazard needs the node's xGMI latency to show, which
+  is what bench.py's refilled checks on every rank watch for there.
+"""
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+import pytest
+
+from helpers import rank_env
+
+WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "mp_worker.py")
+SMALL = 4096
+
+
+def small_soak(P, runs, sync):
+    env = rank_env(P)
+    env["GLOO_AMD_SYNC"] = sync
+    with tempfile.TemporaryDirectory() as d:
+        procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P),
+                                   "soak:%d:delays:%d" % (runs, SMALL)],
+                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                 for r in range(P)]
+        outs = []
+        for p in procs:
+            try:
+                o, _ = p.communicate(timeout=150)
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+            outs.append(o.decode(errors="replace"))
+    bad = []
+    for o in outs:
+        m = re.search(r"BADRUNS rank \d+ (\{.*?\}) of", o)
+        assert m, o[-2000:]
+        bad.append(eval(m.group(1)))  # noqa: S307 - the worker's own dict literal
+    eng = [line for line in outs[0].splitlines() if line.startswith("ENGINES")][0]
+    return [p.returncode for p in procs], bad, eng, outs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [4, 8])
+def test_small_buffer_soak_exact_under_the_product_sync(P):
+    """The sharp detector on the product: L1-warm re-reads of landing slots
+    within one launch, 200 runs of every engine, every run exact."""
+    rcs, bad, eng, outs = small_soak(P, 200, "narrow")
+    assert "'ring': 'devsteps'" in eng, eng
+    assert rcs == [0] * P and all(b == {} for b in bad), (rcs, bad, outs[0][-2000:])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [4, 8])
+def test_small_buffer_soak_catches_a_missing_acquire(P):
+    """Positive control: with the consumer's acquire dropped (test-only
+    kSyncNoAcquire) the same soak fails -- the plan kernel's ring reads stale
+    L1 lines of its landing slot; measured 200 of 200 runs on every rank."""
+    runs = 100
+    rcs, bad, eng, _ = small_soak(P, runs, "unsafe_noacquire")
+    assert "'ring': 'devsteps'" in eng, eng
+    assert all(rc != 0 for rc in rcs), rcs
+    for r, b in enumerate(bad):
+        assert b.get("ring", 0) >= runs // 2, (r, b)
