@@ -95,6 +95,18 @@ def set_engine_streams(policy):
     errors.check(_lib.lib.glx_set_engine_streams(code), "set_engine_streams")
 
 
+def set_max_message_bytes(nbytes):
+    """Messages above nbytes go as consecutive pieces, each landing in a
+    receive region of its own (glx.h glx_set_max_message_bytes; default
+    512 MiB, 0 restores it).  For algorithms created afterwards; every rank
+    must use the same value.  Results are unchanged."""
+    errors.check(_lib.lib.glx_set_max_message_bytes(int(nbytes)), "set_max_message_bytes")
+
+
+def max_message_bytes():
+    return int(_lib.lib.glx_max_message_bytes())
+
+
 def set_device_sync(mode):
     """Release / acquire around the device engines' flags for algorithms
     created afterwards: "auto" (default: narrow), "system" (L2 written back before

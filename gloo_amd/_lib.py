@@ -42,6 +42,8 @@ SIGNATURES = [
     ("glx_enable_peer", _i, [_i, _i]),
     ("glx_tune_reduce", _i, [_i, _i, _i]),
     ("glx_reduce_tuning", _i, [_pi, _pi, _pi]),
+    ("glx_set_max_message_bytes", _i, [_i64]),
+    ("glx_max_message_bytes", _i64, []),
     ("glx_reduce_segment_bytes", _sz, []),
     ("glx_set_copy_split", _i, [_i]),
     ("glx_set_pinned_mirror_limit", _i, [_sz]),

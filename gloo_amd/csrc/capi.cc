@@ -193,6 +193,16 @@ int glx_tune_reduce(int unroll, int blocks_per_cu, int nontemporal) {
   return GLX_OK;
 }
 
+int glx_set_max_message_bytes(int64_t bytes) {
+  if (bytes < 0 || (bytes > 0 && bytes < 4096)) {
+    return fail(GLX_ERR_INVALID, "glx_set_max_message_bytes: 0 (default) or at least 4096");
+  }
+  glx::setMaxMessageBytes(bytes);
+  return GLX_OK;
+}
+
+int64_t glx_max_message_bytes(void) { return glx::maxMessageBytes(); }
+
 int glx_reduce_tuning(int* unroll, int* blocks_per_cu, int* policy) {
   if (unroll == nullptr || blocks_per_cu == nullptr || policy == nullptr) {
     return fail(GLX_ERR_INVALID, "glx_reduce_tuning: null argument");

@@ -187,6 +187,26 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
   }
 
   engine_ = engineFor(*ctx, algo, count_, (int)esize_);
+  if ((engine_ == kEngineOneShot || engine_ == kEngineTwoShot) && count_ > 0) {
+    // Their layouts read whole ranges off the plan (no split messages), and
+    // each of their slot arrays holds P ranges (two-shot) or P whole buffers
+    // (one-shot) in one block, which must stay shareable between processes
+    // (Context::kIpcMaxBlockBytes).  Otherwise the same schedule runs as
+    // host-issued steps -- from every rank's unsplit program, so all agree.
+    glx::PlanParams whole = prm_;
+    whole.maxMessageBytes = INT64_MAX;
+    int64_t maxMsg = 0;
+    for (int q = 0; q < contextSize_; q++) {
+      for (const auto& s : glx::makePlan(algo, q, contextSize_, count_, whole).steps) {
+        if (s.kind == glx::SEND) maxMsg = std::max(maxMsg, s.len);
+      }
+    }
+    const size_t arr = (size_t)contextSize_ * ((size_t)maxMsg * esize_ + 512) + 4096;
+    if (maxMsg * (int64_t)esize_ > prm_.maxMessageBytes ||
+        (ctx->sharesAcrossProcesses() && arr >= Context::kIpcMaxBlockBytes)) {
+      engine_ = kEngineSteps;
+    }
+  }
   if (engine_ == kEngineDmaSteps) split_ = 1;  // one copy (one done word) per SEND
   if (engine_ == kEngineDevSteps) {
     // the plan kernel's grid and bookkeeping; when a landing region would be
@@ -219,7 +239,8 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
     // kIpcMaxBlockBytes): a larger region runs with one slot and no
     // reduce-and-forward, which every rank derives alike from the geometry
     if (slots_ > 1 && ctx->sharesAcrossProcesses()) {
-      const ScratchBlock whole{0, maxRegionElems(), nullptr, {}};
+      // from the largest region of EVERY rank's program, so all ranks agree
+      const ScratchBlock whole{0, sync_.maxRegionElems, nullptr, {}};
       if ((size_t)slots_ * slotBytes(whole) + 4096 >= Context::kIpcMaxBlockBytes) slots_ = 1;
     }
     if (!sync_.safe) engine_ = kEngineSteps;
@@ -554,6 +575,7 @@ void HipPlanExecutor::publish() {
   }
   putPod<int32_t>(b, engine_);
   putPod<int32_t>(b, (int32_t)slots_);
+  putPod<int64_t>(b, prm_.maxMessageBytes);  // how this rank's program cut its messages
   putPod<int32_t>(b, (int32_t)copyEngine_);
   putPod<int32_t>(b, (int32_t)ddBlocks_.size());
   for (size_t k = 0; k < ddBlocks_.size(); k++) putRef(b, ddRefs_[k]);
@@ -584,6 +606,7 @@ std::vector<int64_t> HipPlanExecutor::retiredIn(const std::vector<char>& rec) co
   at += (size_t)nchan * 4 * sizeof(int32_t);
   getPod<int32_t>(rec, at);  // engine
   getPod<int32_t>(rec, at);  // slots
+  getPod<int64_t>(rec, at);  // max message bytes
   getPod<int32_t>(rec, at);  // copy engine
   const int32_t nb = getPod<int32_t>(rec, at);
   for (int32_t k = 0; k < nb; k++) getRef(rec, at);
@@ -595,6 +618,7 @@ std::vector<int64_t> HipPlanExecutor::retiredIn(const std::vector<char>& rec) co
 
 void HipPlanExecutor::resolvePeers() {
   std::map<int, bool> peers;
+  std::map<int, uint64_t*> abortWords;  // DMA steps engine: peer -> its abort word
   for (auto& oc : out_) peers[oc.peer] = true;
   for (auto& ic : in_) peers[ic.peer] = true;
   for (int r = 0; r < contextSize_ && engine_ != kEngineSteps; r++) {
@@ -670,7 +694,12 @@ void HipPlanExecutor::resolvePeers() {
     const int32_t peerSlots = getPod<int32_t>(b, at);
     GLX_ENFORCE(engine_ != kEngineDevSteps || peerSlots == slots_, "rank ", r, " keeps ",
                 peerSlots, " landing slot(s) per channel, rank ", contextRank_, " ", slots_,
-                " (GLOO_AMD_FUSE must be the same on every rank)");
+                " (GLOO_AMD_FUSE must be the same on every rank; two slots are kept only "
+                "while two of the largest region stay below the 2 GiB IPC block limit)");
+    const int64_t peerMaxMsg = getPod<int64_t>(b, at);
+    GLX_ENFORCE(peerMaxMsg == prm_.maxMessageBytes, "rank ", r, " cuts messages above ",
+                peerMaxMsg, " bytes, rank ", contextRank_, " above ", prm_.maxMessageBytes,
+                " (glx_set_max_message_bytes must be the same on every rank)");
     getPod<int32_t>(b, at);  // the peer's copy engine (recorded for diagnostics)
     const int32_t nb = getPod<int32_t>(b, at);
     std::vector<char*> blocks;
@@ -697,7 +726,22 @@ void HipPlanExecutor::resolvePeers() {
           ic.devCredit = rows + (size_t)ic.peerRow * G * glx::kFlagStride;
         }
       }
+      if (engine_ == kEngineDmaSteps) abortWords[r] = rows;  // word 0: its abort word
     }
+  }
+  if (engine_ == kEngineDmaSteps) {
+    // every peer's abort word; with more peers than a flag kernel carries,
+    // those our copies land in (the ones a stray copy could overwrite)
+    dmaAbortOut_.clear();
+    for (const auto& kv : abortWords) {
+      bool out = false;
+      for (const auto& oc : out_) out = out || oc.peer == kv.first;
+      if (abortWords.size() <= (size_t)glx::kFlagAbortMax || out) {
+        dmaAbortOut_.push_back(kv.second);
+      }
+    }
+    GLX_ENFORCE(dmaAbortOut_.size() <= (size_t)glx::kFlagAbortMax, "DMA steps engine: ",
+                dmaAbortOut_.size(), " receiving peers (at most ", glx::kFlagAbortMax, ")");
   }
   const bool dev = engine_ == kEngineDevSteps || engine_ == kEngineDmaSteps;
   for (auto& oc : out_) {
@@ -765,16 +809,6 @@ const HipPlanExecutor::ScratchBlock& HipPlanExecutor::blockOf(
 
 // The largest receive region of the plan (elements): RECV steps land at
 // their region's start, regions run to the next start (allocScratch).
-int64_t HipPlanExecutor::maxRegionElems() const {
-  std::vector<int64_t> starts{0, plan_.scratch_elems};
-  for (const auto& s : plan_.steps) {
-    if (s.kind == glx::RECV) starts.push_back(s.boff);
-  }
-  std::sort(starts.begin(), starts.end());
-  int64_t m = 0;
-  for (size_t i = 0; i + 1 < starts.size(); i++) m = std::max(m, starts[i + 1] - starts[i]);
-  return m;
-}
 
 void HipPlanExecutor::allocScratch(bool uncached, int slots) {
   if (plan_.scratch_elems <= 0) return;
@@ -787,16 +821,23 @@ void HipPlanExecutor::allocScratch(bool uncached, int slots) {
   std::sort(starts.begin(), starts.end());
   starts.erase(std::unique(starts.begin(), starts.end()), starts.end());
   starts.push_back(plan_.scratch_elems);  // sentinel
+  // Only what messages land in gets memory: a region runs from a RECV's
+  // landing start to the next start, but no further than its longest
+  // message plus the landing pad -- a layout slot no message lands in (a mesh
+  // rank's own range) gets none (at 2 GiB it crossed the IPC limit).
+  // Consecutive regions share a block up to kMaxBlockBytes.
   ScratchBlock cur;
   cur.start = 0;
   for (size_t i = 0; i + 1 < starts.size(); i++) {
-    const int64_t regionElems = starts[i + 1] - starts[i];
+    const int64_t regionElems = glx::landedRegionElems(plan_, starts[i], starts[i + 1]);
+    if (regionElems == 0) continue;  // nothing lands here
     const size_t curBytes = (size_t)cur.elems * esize_;
-    if (cur.elems > 0 && curBytes + (size_t)regionElems * esize_ > kMaxBlockBytes) {
+    if (cur.elems > 0 && (cur.start + cur.elems != starts[i] ||
+                          curBytes + (size_t)regionElems * esize_ > kMaxBlockBytes)) {
       blocks_.push_back(cur);
       cur = ScratchBlock();
-      cur.start = starts[i];
     }
+    if (cur.elems == 0) cur.start = starts[i];
     cur.elems += regionElems;
   }
   if (cur.elems > 0) blocks_.push_back(cur);
@@ -1074,9 +1115,10 @@ void HipPlanExecutor::issueCopy(char* dst, const char* src, size_t len, OutChan&
 }
 
 void HipPlanExecutor::setupDmaSteps() {
-  for (size_t k = 0; k < in_.size(); k++) in_[k].deliveryWord = (uint32_t)k;
-  for (size_t k = 0; k < out_.size(); k++) out_[k].creditWord = (uint32_t)(in_.size() + k);
-  markWord_ = (uint32_t)(in_.size() + out_.size());
+  // word 0: the abort word (kernels.h abort marks), at the same place on every rank
+  for (size_t k = 0; k < in_.size(); k++) in_[k].deliveryWord = (uint32_t)(1 + k);
+  for (size_t k = 0; k < out_.size(); k++) out_[k].creditWord = (uint32_t)(1 + in_.size() + k);
+  markWord_ = (uint32_t)(1 + in_.size() + out_.size());
   for (size_t j = 0; j < copies_.size(); j++) copies_[j].doneWord = markWord_ + 1 + (uint32_t)j;
   ddAlloc(((size_t)markWord_ + 1 + copies_.size()) * glx::kFlagBytes);
 }
@@ -1099,6 +1141,10 @@ void HipPlanExecutor::dmaFlush() {
   p.timeoutTicks = dmaTicks_;
   p.status = ddStatusDev_;
   p.claim = ddClaim_;
+  p.abortIn = dmaWord(0);
+  p.nAbort = (int)dmaAbortOut_.size();
+  for (size_t k = 0; k < dmaAbortOut_.size(); k++) p.abortOut[k] = dmaAbortOut_[k];
+  p.abortValue = 1 + (uint64_t)contextRank_;
   dmaOps_.clear();
   GLX_HIP_CHECK(glx::launch_flag_ops(p, dmaOpsStream_));
   transport_.flagKernels++;

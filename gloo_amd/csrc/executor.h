@@ -198,8 +198,9 @@ class HipPlanExecutor : public Algorithm {
   // stream -- with every hand-off made on the GPU by flag-op kernels
   // (kernels.h FlagOpsParams) instead of by the host, so run() only enqueues.
   // Flag words, one per 128-byte line, in one uncached block peers map
-  // (ddBlocks_[0]): our in-channels' delivery words, our out-channels' credit
-  // words, the compute mark, each copy stream's done word; all count across
+  // (ddBlocks_[0]): our abort word (word 0, kernels.h abort marks), our
+  // in-channels' delivery words, our out-channels' credit words, the compute
+  // mark, each copy stream's done word; all but the abort word count across
   // runs.
   void setupDmaSteps();
   void exchangeDma(char* ptr0);
@@ -218,6 +219,7 @@ class HipPlanExecutor : public Algorithm {
   hipStream_t dmaOpsStream_ = nullptr;
   uint32_t markWord_ = 0;
   uint64_t marks_ = 0;     // compute marks signalled
+  std::vector<uint64_t*> dmaAbortOut_;  // peers' abort words (their flag blocks' word 0)
   uint64_t dmaTicks_ = 0;  // the current run's wait timeout in s_memrealtime ticks
   std::chrono::milliseconds effectiveTimeout() const {
     return timeout_.count() > 0 ? timeout_ : context_->getTimeout();
@@ -227,7 +229,6 @@ class HipPlanExecutor : public Algorithm {
   // landing slots, plan.h SyncTable::slots), slotBytes() apart.
   void allocScratch(bool uncached = false, int slots = 1);
   size_t slotBytes(const ScratchBlock& b) const;
-  int64_t maxRegionElems() const;
   const ScratchBlock& blockOf(const std::vector<ScratchBlock>& blocks, int64_t boff) const;
   int slots_ = 1;  // plan kernel: landing slots per channel
   void waitWar(int64_t off, int64_t len);

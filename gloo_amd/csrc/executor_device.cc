@@ -589,6 +589,14 @@ void HipPlanExecutor::checkDevice() {
                 "must be stream-ordered (issue them on the algorithm's stream, or make "
                 "the other stream wait for it); the algorithm is unusable now");
   }
+  if ((st & ~0xffff) == glx::kStatusPeerAbort) {
+    broken_ = true;
+    GLX_THROW_IO("Rank ", st & 0xffff, " gave up on its DMA steps run (a wait of its timed "
+                      "out, or it saw a peer exit), so its copies to rank ", contextRank_,
+                      " may have landed without their credit; rank ", contextRank_,
+                      " stopped its run rather than return that data (DMA steps engine, abort "
+                      "mark)");
+  }
   if (st != 0) {
     broken_ = true;
     const int peer = (st & 255) - 1, step = (st >> 8) - 1;

@@ -239,9 +239,26 @@ hipError_t launch_plan_kernel_unsafe_stores(int op, int dtype, const PlanKernelP
 // of by the host.  Lane 0 performs the ops in order: kFlagWait waits (bounded)
 // until *word >= value, kFlagSignal writes value into word (a flag word in
 // this rank's or a peer's uncached flag block).  The stream's earlier work
-// has completed when the kernel starts (stream order; its writes are visible
-// agent-wide), so a signal publishes it without a fence of its own.
+// has completed when the kernel starts (stream order); before its first
+// signal the kernel also releases at system scope (buffer_wbl2 sc0 sc1), so
+// the signal publishes that work to SDMA engines and peers whatever scope the
+// runtime's release between kernels had.
+//
+// Abort marks: a copy waits for its receiver's credit in the flag
+// kernel before it, but HIP runs the copy whatever that kernel found.  So a
+// flag kernel that gives up -- a wait timed out, the status word was set (a
+// peer exited, another wait gave up, release() of a broken algorithm) or a
+// peer's abort mark arrived -- first writes 1 + rank into the abort word of
+// every peer (abortOut) and completes that write before it ends, i.e. before
+// the copy queued behind it can start.  Every flag kernel reads its own abort
+// word (abortIn) at its start and while it waits: a receiver whose landing
+// region such a copy may have overwritten reaches the RELEASE of that region
+// only after the reduce reading it has finished, so if the copy landed during
+// the reduce the mark was already there, and the run fails with
+// kStatusPeerAbort + sender instead of returning the overwritten data.
 constexpr int kFlagOpsMax = 8;
+constexpr int kFlagAbortMax = 32;
+constexpr int kStatusPeerAbort = 0x7ffe0000;  // | the aborting peer's rank
 constexpr int32_t kFlagWait = 0, kFlagSignal = 1;
 struct FlagOp {
   uint64_t* word;
@@ -256,6 +273,10 @@ struct FlagOpsParams {
   uint64_t timeoutTicks;  // s_memrealtime ticks, each wait from the kernel's start
   int* status;            // host-visible: a timeout's code; nonzero stops every wait
   int* claim;             // device word: the first timed-out wait reports
+  const uint64_t* abortIn;              // this rank's abort word (nonzero: a peer gave up)
+  uint64_t* abortOut[kFlagAbortMax];    // peers' abort words, written when this rank gives up
+  int nAbort;
+  uint64_t abortValue;                  // 1 + this rank
 };
 hipError_t launch_flag_ops(const FlagOpsParams& p, hipStream_t s);
 

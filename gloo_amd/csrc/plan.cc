@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <atomic>
 #include <map>
 #include <cstdlib>
 #include <stdexcept>
@@ -865,22 +866,177 @@ int autoRingSchedule(int size, int64_t bytes, bool fn, bool deviceDriven) {
   return bytes < kMeshMaxBytes ? mesh : ring;
 }
 
+namespace {
+// GLOO_AMD_MAX_MESSAGE_BYTES sets the initial value (tests: split programs at
+// small sizes in every rank process)
+std::atomic<int64_t> g_maxMessageBytes{[] {
+  const char* e = std::getenv("GLOO_AMD_MAX_MESSAGE_BYTES");
+  const int64_t v = e != nullptr ? std::atoll(e) : 0;
+  return v >= 4096 ? v : kMaxMessageBytes;
+}()};
+}  // namespace
+
+int64_t maxMessageBytes() { return g_maxMessageBytes.load(); }
+
+void setMaxMessageBytes(int64_t bytes) {
+  g_maxMessageBytes.store(bytes > 0 ? bytes : kMaxMessageBytes);
+}
+
+void splitMessages(Plan& p, int64_t M, int64_t V) {
+  if (M <= 0 || V <= 0 || M % V != 0) fail("splitMessages: bad piece length");
+  for (const Step& s : p.steps) {
+    if (s.kind == FOLD && (s.flags & kFoldWhole) != 0) return;  // left whole (plan.h)
+  }
+  // A message for [off, off + len) lands at its region's 16-byte base plus
+  // the phase ph = off mod V; sub-region q of the region is [qM, (q+1)M)
+  // past that base, so piece q holds the message's elements
+  // [off - ph + qM, off - ph + (q+1)M) clipped to it: every piece after the
+  // first starts at phase 0 exactly at its sub-region's base, and the
+  // sub-regions are the same for every message of the region.
+  auto pieces = [&](int64_t off, int64_t len) {  // (no overflow for any M)
+    const int64_t span = off % V + len;
+    return span <= M ? (int64_t)1 : (span - 1) / M + 1;
+  };
+  auto piece = [&](int64_t off, int64_t len, int64_t q, int64_t* o, int64_t* l) {
+    const int64_t a = q == 0 ? off : off - off % V + q * M;
+    const int64_t b = std::min(off + len, off - off % V + (q + 1) * M);
+    *o = a;
+    *l = std::max<int64_t>(0, b - a);
+  };
+  std::vector<Step> out;
+  out.reserve(p.steps.size() * 2);
+  const std::vector<Step>& in = p.steps;
+  for (size_t i = 0; i < in.size();) {
+    const Step& s = in[i];
+    if (s.kind == SEND) {
+      for (int64_t q = 0; q < pieces(s.off, s.len); q++) {
+        Step t = s;
+        t.channel = s.channel + q * kPieceChannelStride;
+        piece(s.off, s.len, q, &t.off, &t.len);
+        t.dst_off = s.dst_off + q * M;
+        out.push_back(t);
+      }
+      i++;
+      continue;
+    }
+    if (s.kind != RECV) {
+      out.push_back(s);
+      i++;
+      continue;
+    }
+    // a receive group: RECVs, the steps reading their regions, and their
+    // RELEASEs, up to the RELEASE that leaves no message of the group
+    // unreleased (every schedule's shape)
+    std::map<int64_t, int64_t> region;                    // region -> its message's length
+    std::map<int64_t, int64_t> regionOff;                 // region -> its message's offset
+    std::map<std::pair<int64_t, int64_t>, int64_t> open;  // (peer, channel) -> region
+    std::vector<int64_t> released;                        // per group step: RELEASE's region
+    size_t j = i;
+    for (; j < in.size(); j++) {
+      const Step& t = in[j];
+      released.push_back(-1);
+      if (t.kind == RECV) {
+        region[t.boff] = t.len;
+        open[{t.peer, t.channel}] = t.boff;
+      } else if (t.kind == RELEASE) {
+        auto it = open.find({t.peer, t.channel});
+        if (it == open.end()) fail("splitMessages: a RELEASE without its RECV in the group");
+        released.back() = it->second;
+        open.erase(it);
+        if (open.empty()) break;
+      } else if (t.kind == SEND) {
+        fail("splitMessages: a SEND inside a receive group");
+      }
+    }
+    if (j == in.size()) fail("splitMessages: a receive group without its RELEASE");
+    // the receiver learns a message's offset from the steps that read it
+    auto reads = [&](int64_t boff, int64_t off, int64_t len) {
+      auto it = region.find(boff);
+      if (it == region.end() || it->second != len) {
+        fail("splitMessages: a step reads a region other than its group's whole message");
+      }
+      auto ot = regionOff.find(boff);
+      if (ot != regionOff.end() && ot->second != off) {
+        fail("splitMessages: two steps read one message at different offsets");
+      }
+      regionOff[boff] = off;
+    };
+    for (size_t k = i; k <= j; k++) {
+      const Step& t = in[k];
+      if (t.kind == REDUCE || t.kind == COPY) reads(t.boff, t.off, t.len);
+      if (t.kind == FOLD) {
+        for (int64_t r : p.folds[(size_t)t.boff]) {
+          if (r >= 0) reads(r, t.off, t.len);
+        }
+      }
+    }
+    auto piecesOf = [&](int64_t boff) {
+      const int64_t len = region.at(boff);
+      if (len == 0) return (int64_t)1;
+      auto ot = regionOff.find(boff);
+      if (ot == regionOff.end()) fail("splitMessages: a message no step reads");
+      return pieces(ot->second, len);
+    };
+    int64_t K = 1;
+    for (const auto& kv : region) K = std::max(K, piecesOf(kv.first));
+    for (int64_t q = 0; q < K; q++) {
+      for (size_t k = i; k <= j; k++) {
+        const Step& t = in[k];
+        Step u = t;
+        if (t.kind == RECV) {
+          if (q >= piecesOf(t.boff)) continue;
+          int64_t o = 0;
+          if (t.len > 0) piece(regionOff.at(t.boff), t.len, q, &o, &u.len);
+          u.channel = t.channel + q * kPieceChannelStride;
+          u.boff = t.boff + q * M;
+        } else if (t.kind == RELEASE) {
+          if (q >= piecesOf(released[k - i])) continue;
+          u.channel = t.channel + q * kPieceChannelStride;
+        } else if (t.kind == REDUCE || t.kind == COPY) {
+          if (q >= piecesOf(t.boff)) continue;
+          piece(t.off, t.len, q, &u.off, &u.len);
+          u.boff = t.boff + q * M;
+        } else if (t.kind == FOLD) {
+          const int64_t n = pieces(t.off, t.len);
+          if (q >= n) continue;
+          std::vector<int64_t> srcs;
+          for (int64_t r : p.folds[(size_t)t.boff]) srcs.push_back(r < 0 ? r : r + q * M);
+          if (n > 1) {
+            p.folds.push_back(srcs);
+            u.boff = (int64_t)p.folds.size() - 1;
+          }
+          piece(t.off, t.len, q, &u.off, &u.len);
+        }
+        out.push_back(u);
+      }
+    }
+    i = j + 1;
+  }
+  p.steps = std::move(out);
+}
+
 Plan makePlan(int algo, int rank, int size, int64_t count, const PlanParams& prm) {
   if (size < 1 || rank < 0 || rank >= size || count < 0) fail("bad geometry");
+  Plan p;
   switch (algo) {
-    case ALGO_RING_CHUNKED: return planRingChunked(rank, size, count);
-    case ALGO_HALVING_DOUBLING: return planHalvingDoubling(rank, size, count);
-    case ALGO_RING_CHUNKED_MESH: return planRingChunkedMesh(rank, size, count);
-    case ALGO_FN_RING: return planFnRing(rank, size, count, prm);
-    case ALGO_FN_RING_MESH: return planFnRingMesh(rank, size, count, prm);
-    case ALGO_FN_BCUBE: return planFnBcube(rank, size, count);
-    case ALGO_RING_CHUNKED_REPL: return planRingChunkedReplicated(rank, size, count);
-    case ALGO_FN_RING_REPL: return planFnRingReplicated(rank, size, count, prm);
-    case ALGO_RING: return planRing(rank, size, count);
-    case ALGO_BCUBE: return planBcube(rank, size, count, prm.base);
+    case ALGO_RING_CHUNKED: p = planRingChunked(rank, size, count); break;
+    case ALGO_HALVING_DOUBLING: p = planHalvingDoubling(rank, size, count); break;
+    case ALGO_RING_CHUNKED_MESH: p = planRingChunkedMesh(rank, size, count); break;
+    case ALGO_FN_RING: p = planFnRing(rank, size, count, prm); break;
+    case ALGO_FN_RING_MESH: p = planFnRingMesh(rank, size, count, prm); break;
+    case ALGO_FN_BCUBE: p = planFnBcube(rank, size, count); break;
+    case ALGO_RING_CHUNKED_REPL: p = planRingChunkedReplicated(rank, size, count); break;
+    case ALGO_FN_RING_REPL: p = planFnRingReplicated(rank, size, count, prm); break;
+    case ALGO_RING: p = planRing(rank, size, count); break;
+    case ALGO_BCUBE: p = planBcube(rank, size, count, prm.base); break;
+    default: fail("unknown algorithm");
   }
-  fail("unknown algorithm");
-  return Plan();
+  // pieces of a whole number of 16-byte vectors (the landing phase rule)
+  const int64_t es = std::max(1, prm.esize);
+  const int64_t V = 16 / std::min<int64_t>(16, es);
+  const int64_t M = std::max<int64_t>(V, prm.maxMessageBytes / es / V * V);
+  splitMessages(p, M, V);
+  return p;
 }
 
 // ---------------------------------------------------------------------------
@@ -977,6 +1133,28 @@ bool regionsSafe(const std::vector<Plan>& all, const std::vector<int64_t>& bound
 
 }  // namespace
 
+int64_t landedRegionElems(const Plan& plan, int64_t start, int64_t next) {
+  int64_t longest = -1;
+  for (const auto& s : plan.steps) {
+    if (s.kind == RECV && s.boff == start) longest = std::max(longest, s.len);
+  }
+  return longest < 0 ? 0 : std::min(next - start, longest + kPadElems);
+}
+
+int64_t maxRegionOf(const Plan& plan) {
+  std::vector<int64_t> starts{0, plan.scratch_elems};
+  for (const auto& s : plan.steps) {
+    if (s.kind == RECV) starts.push_back(s.boff);
+  }
+  std::sort(starts.begin(), starts.end());
+  starts.erase(std::unique(starts.begin(), starts.end()), starts.end());
+  int64_t m = 0;  // over the regions some message lands in (the executor's blocks)
+  for (size_t i = 0; i + 1 < starts.size(); i++) {
+    m = std::max(m, landedRegionElems(plan, starts[i], starts[i + 1]));
+  }
+  return m;
+}
+
 SyncTable syncTable(int algo, int rank, int size, int64_t count, const PlanParams& prm,
                     int G) {
   SyncTable t;
@@ -992,6 +1170,7 @@ SyncTable syncTable(int algo, int rank, int size, int64_t count, const PlanParam
       t.bounds.push_back(s.off + s.len);
     }
     if (q == rank) mine = p;
+    t.maxRegionElems = std::max(t.maxRegionElems, maxRegionOf(p));
     all.push_back(std::move(p));
   }
   std::sort(t.bounds.begin(), t.bounds.end());

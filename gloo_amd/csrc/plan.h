@@ -73,6 +73,18 @@ constexpr int64_t kFoldWhole = 2;
 // gloo/allreduce.h:80 (AllreduceOptionsImpl::kMaxSegmentSize)
 constexpr int64_t kMaxSegmentBytes = 1 << 20;
 
+// Messages longer than this go as consecutive pieces (splitMessages below),
+// so no receive region -- hence no shared block another process imports --
+// reaches the 2 GiB at which the HIP runtime's IPC import hangs
+// (Context::kIpcMaxBlockBytes), whatever count the reference accepts
+// (VERDICT r5 #3); two landing slots of a piece still fit below it.
+constexpr int64_t kMaxMessageBytes = int64_t(512) << 20;
+// The process-wide setting (glx_set_max_message_bytes; every rank must use
+// the same): kMaxMessageBytes unless changed -- tests lower it to run split
+// programs at small sizes.
+int64_t maxMessageBytes();
+void setMaxMessageBytes(int64_t bytes);
+
 // Inputs of the function-style schedules besides (rank, size, count).
 struct PlanParams {
   int esize = 4;                                // bytes per element
@@ -84,7 +96,31 @@ struct PlanParams {
   int64_t minPieceBytes = 4 << 20;
   // class AllreduceBcube: ranks per group (gloo::Context::base, default 2)
   int base = 2;
+  // messages above this many bytes are split (kMaxMessageBytes)
+  int64_t maxMessageBytes = glx::maxMessageBytes();
 };
+
+// Cut every message whose landing spans more than maxElems elements into
+// consecutive pieces.  A message for ptr0[off, off + len) lands at its
+// region's 16-byte base plus the phase off mod V (V = 16 / esize elements);
+// sub-region q of a region is [q * maxElems, (q + 1) * maxElems) past that
+// base (maxElems a multiple of V), and piece q is the part of the message
+// landing there -- so every piece after the first starts at phase 0 at its
+// sub-region's base, and the sub-regions are the same for every message of
+// the region.  The sender's SEND becomes one SEND per piece (dst + q *
+// maxElems); on the receiver, each group of RECVs, the REDUCE / COPY / FOLD
+// steps reading their regions and their RELEASEs (every schedule's shape) is
+// repeated per piece, every step narrowed to piece q (the offset of each
+// message is taken from the steps reading it).  Piece q travels on channel
+// tag + q * kPieceChannelStride: one channel per sub-region, so each credit
+// protects exactly the bytes it guards, and a piece never waits for an
+// earlier piece of its own message, which the receiver may release only after
+// its own sends (halving-doubling's exchanges would deadlock).  The
+// per-element reduction chains are untouched: results are bit-identical.
+// Plans folding whole-buffer messages (kFoldWhole: AllreduceRing, the
+// replicated schedules) are left whole.
+constexpr int64_t kPieceChannelStride = int64_t(1) << 16;
+void splitMessages(Plan& p, int64_t maxElems, int64_t V);
 
 // Region padding: room to land a message at any 16-byte phase after
 // rounding its region base up to 16 bytes (<= 30 bytes for 1-byte elements).
@@ -241,11 +277,21 @@ struct SyncTable {
   bool safe = true;
   int slots = 1;
   bool anyFold = false;  // some rank's program has a FOLD step
+  // the largest receive region (elements) of ANY rank's program: every rank
+  // derives the plan kernel's landing-slot count from it alike
+  int64_t maxRegionElems = 0;
   std::vector<std::pair<int, int>> outChans, inChans;  // (peer, tag)
   std::vector<StepSync> steps;
 };
 SyncTable syncTable(int algo, int rank, int size, int64_t count, const PlanParams& prm,
                     int G);
+// The receive region some message lands in at `start` (RECV steps land at
+// their region's start): up to the next start, but no further than its
+// longest message plus the landing pad; 0 if nothing lands there.  The
+// executor allocates exactly these (allocScratch).
+int64_t landedRegionElems(const Plan& plan, int64_t start, int64_t next);
+// The largest of them in one program.
+int64_t maxRegionOf(const Plan& plan);
 
 // Host-memory endpoints: when the user's buffer is in host
 // memory the executor stages it through a device buffer.  This derives from

@@ -883,14 +883,51 @@ __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
 // the device engines' waits) or as soon as the status word is nonzero (another
 // wait gave up, or the host saw a peer exit): the ops after it are skipped, so
 // no signal claims work that did not happen, and the stream drains.
+//
+// Giving up also posts this rank's abort mark to every peer, completed before
+// the kernel ends -- before a copy queued behind it on the stream can start
+// (kernels.h, abort marks); a peer's mark makes this kernel give up too.
+__device__ __forceinline__ void post_aborts(const FlagOpsParams& p) {
+  for (int k = 0; k < p.nAbort; k++) put_flag(p.abortOut[k], p.abortValue, p.flagStore != 0);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+
+// A peer's abort mark (0: none): a system-scope load of our own uncached word.
+__device__ __forceinline__ uint64_t peer_abort(const FlagOpsParams& p) {
+  return p.abortIn != nullptr
+             ? __hip_atomic_load(p.abortIn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+             : 0;
+}
+
 __global__ __launch_bounds__(64) void flag_ops_kernel(FlagOpsParams p) {
   if (threadIdx.x != 0) return;
   const uint64_t start = __builtin_amdgcn_s_memrealtime();
   const volatile int* status = reinterpret_cast<const volatile int*>(p.status);
-  if (*status != 0) return;
+  auto abandoned = [&]() {  // a peer's mark: report it, pass it on
+    const uint64_t a = peer_abort(p);
+    if (a == 0) return false;
+    report_timeout(p.status, p.claim, kStatusPeerAbort | (int)((a - 1) & 0xffff), a, 0);
+    post_aborts(p);
+    return true;
+  };
+  if (*status != 0) {
+    post_aborts(p);
+    return;
+  }
+  if (abandoned()) return;
+  bool released = false;
   for (int i = 0; i < p.n; i++) {
     const FlagOp& o = p.ops[i];
     if (o.kind == kFlagSignal) {
+      if (!released) {
+        // once per kernel, before its first signal: the stream's earlier
+        // work (a reduce writing the chunk an SDMA copy on another stream
+        // reads next, which no L2 sees) written back system-wide; HIP's own
+        // release between same-stream kernels may be agent scope
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        released = true;
+      }
       put_flag(o.word, o.value, p.flagStore != 0);
       continue;
     }
@@ -898,9 +935,16 @@ __global__ __launch_bounds__(64) void flag_ops_kernel(FlagOpsParams p) {
     for (uint32_t spin = 1; (v = get_flag(o.word)) < o.value; spin++) {
       if (__builtin_amdgcn_s_memrealtime() - start > p.timeoutTicks) {
         report_timeout(p.status, p.claim, o.code, v, o.value);
+        post_aborts(p);
         return;
       }
-      if ((spin & 127) == 0 && *status != 0) return;
+      if ((spin & 127) == 0) {
+        if (*status != 0) {
+          post_aborts(p);
+          return;
+        }
+        if (abandoned()) return;
+      }
       __builtin_amdgcn_s_sleep(1);
     }
   }
@@ -1109,8 +1153,12 @@ hipError_t GLX_TU_NAME(launch_twoshot)(int op, int dtype, const TwoShotParams& p
 
 #ifndef GLX_XGMI_UNSAFE_TU
 hipError_t launch_flag_ops(const FlagOpsParams& p, hipStream_t s) {
-  if (p.n < 1 || p.n > kFlagOpsMax || p.status == nullptr || p.claim == nullptr) {
+  if (p.n < 1 || p.n > kFlagOpsMax || p.status == nullptr || p.claim == nullptr ||
+      p.nAbort < 0 || p.nAbort > kFlagAbortMax) {
     return hipErrorInvalidValue;
+  }
+  for (int k = 0; k < p.nAbort; k++) {
+    if (p.abortOut[k] == nullptr) return hipErrorInvalidValue;
   }
   for (int i = 0; i < p.n; i++) {
     if (p.ops[i].word == nullptr ||

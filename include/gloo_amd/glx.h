@@ -135,6 +135,14 @@ int glx_tune_reduce(int unroll, int blocks_per_cu, int nontemporal);
  * settings are process-wide and atomic: rank threads may launch while
  * another thread tunes. */
 int glx_reduce_tuning(int* unroll, int* blocks_per_cu, int* policy);
+/* Messages above this many bytes go as consecutive pieces, each a message of
+ * its own landing in a receive region of its own (plan.h splitMessages), so
+ * no block another process must import reaches 2 GiB whatever the count
+ * (default 512 MiB; 0 restores it; at least 4096).  Process-wide, for
+ * algorithms created afterwards; every rank must use the same value (checked
+ * when the algorithm's peers resolve).  Results are unchanged. */
+int glx_set_max_message_bytes(int64_t bytes);
+int64_t glx_max_message_bytes(void);
 /* glx_reduce on more than this many bytes per stream goes out as consecutive
  * kernel launches over equal segments of at most this size (one grid-stride
  * launch over 1 GiB streams ran 6 % slower on MI355X): a

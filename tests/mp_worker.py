@@ -61,6 +61,8 @@ def main():
         return run_device(store_dir, rank, size, algo)
     if algo == "devtimeout":
         return run_device_timeout(store_dir, rank, size)
+    if algo == "dmaabort":
+        return run_dma_abort(store_dir, rank, size)
     if algo.startswith("killpeer:"):
         return run_killpeer(store_dir, rank, size, *algo.split(":")[1:])
     if algo == "devsteps":
@@ -205,6 +207,76 @@ def run_device_timeout(store_dir, rank, size):
             store.get("timeout_done/%s" % sched, timeout_ms=120000)
         torch.cuda.synchronize()  # the kernels that gave up have exited
         alg.close()
+    ctx.close()
+    if not ok:
+        print("MISMATCH rank", rank)
+        sys.exit(1)
+    print("OK")
+
+
+def run_dma_abort(store_dir, rank, size):
+    """the DMA steps engine enqueues a copy behind the flag
+    kernel that waits for its receiver's credit, and HIP runs the copy whatever
+    that wait found.  Rank 0 (1 s timeout) gives up on a credit while rank 1
+    (30 s) is healthy but late -- its stream is held by a sleep kernel -- so
+    rank 0's next copy lands in rank 1's region before rank 1 consumed the
+    message there.  Rank 1 must not return that data: the abort mark rank 0
+    posted before the copy could start stops rank 1's run, which raises
+    IoException naming rank 0 -- long before its own 30 s timeout."""
+    import time
+
+    import torch
+
+    import gloo_amd
+
+    store = gloo_amd.rendezvous.FileStore(store_dir)
+    ctx = gloo_amd.rendezvous.Context(rank, size, 0)
+    ctx.setTimeout(1 if rank == 0 else 30)
+    ctx.connectFullMesh(store)
+    n = 1 << 20
+    s = torch.cuda.Stream()
+    buf = torch.ones(n, device="cuda")
+    gloo_amd.set_steps_engine("dma")
+    try:
+        alg = gloo_amd.AllreduceRingChunked(ctx, [buf], schedule="ring", streams=[s])
+    finally:
+        gloo_amd.set_steps_engine("auto")
+    ok = alg.engine() == "dmasteps"
+    torch.cuda.synchronize()
+    alg.run()  # a clean run first: every rank holds P everywhere
+    s.synchronize()
+    ok = ok and bool((buf == size).all().item())
+    # cycles of torch.cuda._sleep per second on this GPU
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    torch.cuda._sleep(1 << 22)
+    e1.record()
+    e1.synchronize()
+    per_s = (1 << 22) / max(1e-6, e0.elapsed_time(e1) / 1e3)
+    buf.fill_(1)
+    torch.cuda.synchronize()
+    barrier(store, rank, size, "armed")
+    if rank == 1:
+        with torch.cuda.stream(s):
+            torch.cuda._sleep(int(per_s * 4))  # rank 1 consumes nothing for ~4 s
+    t0 = time.time()
+    msg = None
+    try:
+        alg.run()
+        s.synchronize()
+        alg.run()  # reports how the run before ended
+        s.synchronize()
+    except gloo_amd.IoException as e:
+        msg = str(e)
+    dt = time.time() - t0
+    print("rank %d after %.1f s: %s" % (rank, dt, msg), flush=True)
+    if rank == 0:
+        ok = ok and msg is not None and "Timed out" in msg
+    else:
+        ok = (ok and msg is not None and "Rank 0 gave up on its DMA steps run" in msg
+              and dt < 20)
+    barrier(store, rank, size, "reported")
+    alg.close()
     ctx.close()
     if not ok:
         print("MISMATCH rank", rank)
@@ -675,10 +747,10 @@ def run_maxcount(store_dir, rank, size):
     the ring on the plan kernel, the host-issued steps and the DMA steps
     engine, the mesh and halving-doubling on the plan kernel.  P = 2: the
     sum commutes, so the result is x0 + x1 bit for bit (int8 wraps; float16
-    adds in fp32 and rounds once, as torch does).  A schedule whose landing
-    block another process would have to import at 2 GiB or more (the IPC
-    import hangs there: Context::kIpcMaxBlockBytes) must be refused at
-    creation with EnforceNotMet on every rank, not hang."""
+    adds in fp32 and rounds once, as torch does).  Every case runs: messages
+    above 512 MiB go as pieces in regions of their own (plan.h
+    splitMessages), so no landing block another process imports reaches the
+    2 GiB at which the IPC import hangs (Context::kIpcMaxBlockBytes)."""
     import time
 
     import torch
@@ -706,13 +778,18 @@ def run_maxcount(store_dir, rank, size):
     # float16's halving-doubling receives half its 4 GiB buffer in one region;
     # the automatic schedule takes the ring at these sizes (plan.h
     # kMeshMaxBytes), on the host-issued steps (ranks share the GPU, > 32 MiB)
+    # round 6: messages above 512 MiB go as pieces, each in a
+    # region of its own (plan.h splitMessages), so nothing is refused: the
+    # mesh (whose two-shot kernel would need ~S per slot array) runs as
+    # host-issued steps; float16's ring and both halving-doublings split
     cases = {
         torch.int8: (("device", "ring", "devsteps"), ("host", "ring", "steps"),
-                     ("dma", "ring", "dmasteps"), ("auto", "mesh", "refused"),
+                     ("dma", "ring", "dmasteps"), ("auto", "mesh", "steps"),
                      ("device", "hd", "devsteps"), ("auto", "auto", "steps")),
         torch.float16: (("device", "ring", "devsteps"), ("host", "ring", "steps"),
-                        ("dma", "ring", "dmasteps"), ("auto", "mesh", "refused"),
-                        ("device", "hd", "refused"), ("auto", "auto", "steps")),
+                        ("dma", "ring", "dmasteps"), ("auto", "mesh", "steps"),
+                        ("device", "hd", "devsteps"), ("dma", "hd", "dmasteps"),
+                        ("auto", "auto", "steps")),
     }
     for dt, bits in ((torch.int8, torch.int8), (torch.float16, torch.int16)):
         if str(dt).split(".")[1] not in dts:

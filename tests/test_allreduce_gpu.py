@@ -573,6 +573,32 @@ def test_device_engine_timeout_raises_io_exception():
             assert "OK" in outs[r]
 
 
+def test_dma_steps_copy_after_a_failed_credit_wait_is_reported_by_the_receiver():
+    """a DMA steps copy enqueued behind a credit wait that
+    gave up still runs; the receiver's run must fail (the sender's abort
+    mark, kernels.h) instead of returning the overwritten region
+    (mp_worker.py dmaabort)."""
+    P = 2
+    with tempfile.TemporaryDirectory() as d:
+        env = rank_env(P)
+        procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P), "dmaabort"],
+                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                 for r in range(P)]
+        outs = []
+        for p in procs:
+            try:
+                o, _ = p.communicate(timeout=120)
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+            outs.append(o.decode(errors="replace"))
+        for r, p in enumerate(procs):
+            print(outs[r])
+            assert p.returncode == 0, "rank %d failed:\n%s" % (r, outs[r])
+            assert "OK" in outs[r]
+
+
 @pytest.mark.parametrize("split", [2, 4])
 @pytest.mark.parametrize("algo", [O.RING_CHUNKED, O.HALVING_DOUBLING, MESH],
                          ids=["ring_chunked", "halving_doubling", "mesh"])

@@ -241,3 +241,27 @@ def test_deferred_copy_signals_stall_under_a_shared_queue():
     for qmap_r in itertools.product(range(2), repeat=len(streams_of(pks[0]))):
         qmap = [dict(zip(streams_of(pk), qmap_r)) for pk in pks]
         assert not run_ranks(pks, qmap)
+
+
+@pytest.mark.parametrize("algo,P,N", [("ring_chunked", 2, 20000), ("ring_chunked", 4, 40000),
+                                      ("halving_doubling", 2, 20000),
+                                      ("halving_doubling", 4, 40000), ("fn_bcube", 4, 40000)])
+@pytest.mark.parametrize("staged", [False, True])
+def test_program_order_rule_with_split_messages(algo, P, N, staged):
+    """split programs (4 KiB pieces, one channel per piece
+    index) under the DMA steps engine's enqueue rule and every mapping of its
+    streams onto hardware queues: no stall."""
+    gloo_amd.set_max_message_bytes(4096)
+    try:
+        progs = [gloo_amd.plan(algo, r, P, N)[0] for r in range(P)]
+    finally:
+        gloo_amd.set_max_message_bytes(0)
+    assert max(s[4] for pr in progs for s in pr if s[0] in (0, 1)) <= 1024
+    pks = [packets(r, progs[r], 2, staged, "ordered") for r in range(P)]
+    rng = random.Random(hash((algo, P, N, staged, "split")) & 0xffff)
+    for Q in (1, 2, 3, 4):
+        per_rank = [mappings(streams_of(pk), Q, rng, 4) for pk in pks]
+        for choice in range(len(per_rank[0])):
+            qmap = [m[min(choice, len(m) - 1)] for m in per_rank]
+            stuck = run_ranks(pks, qmap)
+            assert not stuck, (algo, P, N, staged, Q, qmap, stuck)

@@ -119,3 +119,41 @@ def test_device_engines_random_cases_multiprocess(P, seed_):
         # the DMA steps engine took part (about a third of the step-schedule cases)
         eng = [line for line in outs[0].splitlines() if line.startswith("ENGINES")][-1]
         assert "'dmasteps'" in eng, eng
+
+
+@pytest.mark.parametrize("P,seed_", [(2, 5), (4, 6)])
+def test_device_engines_random_cases_with_split_messages(P, seed_):
+    """The multi-process fuzz with messages split at 64 KiB
+    (GLOO_AMD_MAX_MESSAGE_BYTES, plan.h splitMessages): the
+    plan kernel, the host-issued and DMA steps run split programs (each piece
+    its own channel and sub-region), every rank bit for bit against the
+    oracle."""
+    import os
+    import subprocess
+    import sys
+    import tempfile
+
+    from helpers import rank_env
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "mp_worker.py")
+    with tempfile.TemporaryDirectory() as d:
+        env = rank_env(P)
+        env["GLOO_AMD_MAX_MESSAGE_BYTES"] = str(64 << 10)
+        env["FUZZ_CASES"] = "60"
+        procs = [subprocess.Popen([sys.executable, worker, d, str(r), str(P), "fuzz:%d" % seed_],
+                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                 for r in range(P)]
+        outs = []
+        for p in procs:
+            try:
+                o, _ = p.communicate(timeout=420)
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+            outs.append(o.decode(errors="replace"))
+        every = "\n".join("---- rank %d (rc %s) ----\n%s" % (r, p.returncode, outs[r][-3000:])
+                          for r, p in enumerate(procs))
+        for r, p in enumerate(procs):
+            assert p.returncode == 0 and "OK" in outs[r], "rank %d failed:\n%s" % (r, every)
+        eng = [line for line in outs[0].splitlines() if line.startswith("ENGINES")][-1]
+        assert "'devsteps'" in eng and "'dmasteps'" in eng, eng

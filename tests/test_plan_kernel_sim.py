@@ -474,3 +474,27 @@ def test_overlapping_launches_are_serialised_or_reported(G, seed):
     runs, c = _run_launches(G, 5, at, rng)
     if not c.reports:
         assert _is_serial(runs, G) and c.done == 5
+
+
+@pytest.mark.parametrize("name", ["ring_chunked", "halving_doubling", "ring_chunked_mesh",
+                                  "fn_bcube"])
+@pytest.mark.parametrize("P", [2, 3, 4, 8])
+@pytest.mark.parametrize("N,G", [(4099, 1), (16384, 4), (65536, 2)])
+def test_plan_kernel_protocol_with_split_messages(name, P, N, G):
+    """with messages cut into 4 KiB pieces (plan.h
+    splitMessages; each piece its own channel and region), the plan kernel's
+    protocol -- fused reduce-and-forward, two landing slots, per-(channel,
+    workgroup) credits -- still finishes and matches the oracle."""
+    gloo_amd.set_max_message_bytes(4096)
+    try:
+        if not all(gloo_amd.plan_sync(name, r, P, N, G)["safe"] for r in range(P)):
+            pytest.skip("the executor keeps host-issued steps for this program")
+        steps = [s for r in range(P) for s in gloo_amd.plan(name, r, P, N)[0]]
+        assert max(s[4] for s in steps if s[0] in (0, 1)) <= 1024
+        ins = case_inputs(P, N, O.FLOAT32, 1, 0, seed=93)
+        got = simulate(name, P, N, G, O.SUM, ins, fuse=True)
+    finally:
+        gloo_amd.set_max_message_bytes(0)
+    exp = expected(name, P, O.SUM, ins, 2)
+    for r in range(P):
+        assert same_bits(got[r], exp[r][0]), "rank %d" % r

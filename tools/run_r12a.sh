@@ -1,14 +1,6 @@
-# round 6: positive controls for the device engines' flag sync
 set -o pipefail
-O=gpurun_out/r12c; mkdir -p $O
-timeout -k 10 300 python -u -m pytest -v --timeout 170 --timeout-method thread tests/test_sync_control_gpu.py > $O/sync_control_tests.txt 2>&1 || { tail -30 $O/sync_control_tests.txt; exit 1; }
-grep -E "PASSED|FAILED" $O/sync_control_tests.txt
-L="python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1"
-GLOO_AMD_SYNC=unsafe_noacquire timeout -k 10 300 $L --master-port 29511 bench.py --gpus 4 --steps 5 --warmup 2 --no-sweep --no-staged > $O/bench4_unsafe_noacquire.json 2> $O/bench4_unsafe_noacquire.err || { tail -20 $O/bench4_unsafe_noacquire.err; exit 1; }
-timeout -k 10 300 $L --master-port 29512 bench.py --gpus 4 --steps 5 --warmup 2 --no-sweep --no-staged > $O/bench4_narrow.json 2> $O/bench4_narrow.err || { tail -20 $O/bench4_narrow.err; exit 1; }
-python - <<'PY'
-import json
-for f in ("bench4_unsafe_noacquire", "bench4_narrow"):
-    d = json.loads(open("gpurun_out/r12c/%s.json" % f).read().strip().splitlines()[-1])
-    print(f, d.get("value"), d.get("error"), json.dumps(d.get("device_engines")), {k: (v.get("ok"), v.get("bad_count")) for k, v in d.get("result_checks", {}).items()})
-PY
+O=gpurun_out/r12f; mkdir -p $O
+timeout -k 10 400 python -u -m pytest -v --timeout 350 --timeout-method thread tests/test_scale_gpu.py::test_max_int_count_every_engine > $O/maxcount.txt 2>&1 || { grep -E "maxcount rank 0|FAILED" $O/maxcount.txt | tail -30; exit 1; }
+grep -E "maxcount rank 0.*(ok|MISMATCH|refused)" $O/maxcount.txt
+timeout -k 10 700 python -u -m pytest -q -x --timeout 170 --timeout-method thread tests/test_allreduce_gpu.py tests/test_allreduce_fn_gpu.py tests/test_host_endpoints_gpu.py > $O/suite_part.txt 2>&1; rc=$?
+tail -3 $O/suite_part.txt; exit $rc
