@@ -43,6 +43,8 @@ SIGNATURES = [
     ("glx_tune_reduce", _i, [_i, _i, _i]),
     ("glx_reduce_tuning", _i, [_pi, _pi, _pi]),
     ("glx_set_max_message_bytes", _i, [_i64]),
+    ("glx_allreduce_host_fn", _i, [_vp, _i, _sz, _vp, _vp, ctypes.POINTER(_vp), _i,
+                                   ctypes.POINTER(_vp), _i, _sz, ctypes.c_uint32, _sz, _i64]),
     ("glx_max_message_bytes", _i64, []),
     ("glx_reduce_segment_bytes", _sz, []),
     ("glx_set_copy_split", _i, [_i]),

@@ -7,12 +7,14 @@ buffers (gloo/allreduce.h:89-193, gloo/allreduce.cc:97-146).
     opts.setAlgorithm(AllreduceOptions.Algorithm.RING)
     allreduce(opts)
 
-Differences forced by the device: the reduce function is one of the
-gloo/math.h ops (ReductionFunction / ReductionType / gloo_amd.math.sum ...),
-not an arbitrary host callable.  Buffers are device tensors, or host memory
-as in the reference (numpy arrays, CPU tensors: staged through the GPU per
-call), or raw pointers with an explicit dtype.  Results are bit-identical to the
-reference's for the same inputs, ring and bcube.
+On device buffers the reduce function is one of the gloo/math.h ops
+(ReductionFunction / ReductionType / gloo_amd.math.sum ...): a device cannot
+run a host callable.  On host buffers (numpy arrays, CPU tensors, raw host
+pointers) any callable works as the reference's AllreduceOptions::Func
+(gloo/allreduce.h:36,69,171): fn(c, a, b, n) with raw addresses, c = f(a, b)
+over n elements, called in the reference's order on the host
+(glx_allreduce_host_fn).  Results are bit-identical to the reference's for
+the same inputs, ring and bcube.
 """
 import ctypes
 import datetime
@@ -50,6 +52,7 @@ class AllreduceOptions:
         self.stream = None
         self._in_ptrs = self._out_ptrs = None  # (ctypes array, count), from the setters
         self._any_cuda = False
+        self.custom = None  # a host callable fn(c, a, b, n) (setReduceFunction)
 
     def setAlgorithm(self, algorithm):
         self.algorithm = int(algorithm)
@@ -69,10 +72,12 @@ class AllreduceOptions:
         self._out_ptrs = self._sizes(self._outputs, elements, dtype) if self._outputs else None
 
     # Assigning the lists goes through the setters, so the pointers allreduce()
-    # uses always belong to the buffers the options hold.
+    # uses always belong to the buffers the options hold; reading
+    # them gives a tuple, so an in-place edit raises instead of being lost
+    # (ADVICE r5).
     @property
     def inputs(self):
-        return list(self._inputs)
+        return tuple(self._inputs)
 
     @inputs.setter
     def inputs(self, bufs):
@@ -80,7 +85,7 @@ class AllreduceOptions:
 
     @property
     def outputs(self):
-        return list(self._outputs)
+        return tuple(self._outputs)
 
     @outputs.setter
     def outputs(self, bufs):
@@ -106,17 +111,21 @@ class AllreduceOptions:
         return (ctypes.c_void_p * max(len(ptrs), 1))(*ptrs), len(ptrs)
 
     def setReduceFunction(self, fn):
-        """ReductionFunction.sum/..., a ReductionType value, or
-        gloo_amd.math.sum/product/max/min."""
+        """ReductionFunction.sum/..., a ReductionType value,
+        gloo_amd.math.sum/product/max/min -- or, for host buffers, any
+        callable fn(c, a, b, n) on raw addresses (the reference's Func)."""
+        self.custom = None
         if isinstance(fn, ReductionFunction):
             self.op = fn.type()
         elif isinstance(fn, int) and 1 <= fn <= 4:
             self.op = fn
         elif fn in _MATH_FUNCS:
             self.op = _MATH_FUNCS[fn]
+        elif callable(fn):
+            self.op, self.custom = None, fn
         else:
-            raise EnforceNotMet("only the gloo/math.h reductions run on the device "
-                                "(sum, product, max, min); got %r" % (fn,))
+            raise EnforceNotMet("reduce function must be a gloo/math.h reduction or a "
+                                "callable fn(c, a, b, n); got %r" % (fn,))
 
     def setTag(self, tag):
         self.tag = int(tag) & 0xFFFFFFFF
@@ -142,6 +151,8 @@ def allreduce(opts):
     returns with the outputs complete, like the reference's blocking call."""
     if not opts._outputs:
         raise EnforceNotMet("allreduce: at least one output is required")
+    if opts.custom is not None:
+        return _allreduce_host_fn(opts)
     op = opts.op if opts.op is not None else 1
     iarr, ni = opts._in_ptrs if opts._inputs else ((ctypes.c_void_p * 1)(), 0)
     oarr, no = opts._out_ptrs
@@ -160,3 +171,40 @@ def allreduce(opts):
           "allreduce")
     if sync is not None:
         sync.synchronize()
+
+
+# glx.h glx_reduce_fn: (user, c, a, b, n)
+_REDUCE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                              ctypes.c_void_p, ctypes.c_size_t)
+
+
+def _allreduce_host_fn(opts):
+    """A caller's reduction function on host buffers (glx_allreduce_host_fn):
+    the reference's step order on the host, fn(c, a, b, n) per reduction."""
+    if opts._any_cuda:
+        raise EnforceNotMet("allreduce: a host reduction function needs host buffers "
+                            "(a device cannot run it); device buffers take gloo::sum/"
+                            "product/max/min")
+    user_fn = opts.custom
+    errors = []
+
+    def tramp(_user, c, a, b, n):
+        try:
+            user_fn(c, a, b, n)
+        except BaseException as e:  # noqa: BLE001 - re-raised after the call
+            errors.append(e)
+    cb = _REDUCE_FN(tramp)
+    iarr, ni = opts._in_ptrs if opts._inputs else ((ctypes.c_void_p * 1)(), 0)
+    oarr, no = opts._out_ptrs
+    es = int(lib.glx_dtype_size(opts.dtype))
+    algorithm = opts.algorithm
+    if algorithm not in (AllreduceOptions.Algorithm.UNSPECIFIED,
+                         AllreduceOptions.Algorithm.RING, AllreduceOptions.Algorithm.BCUBE):
+        raise EnforceNotMet("allreduce with a host reduction function: RING or BCUBE")
+    rc = lib.glx_allreduce_host_fn(opts.context.handle, algorithm, es,
+                                   ctypes.cast(cb, ctypes.c_void_p), None, iarr, ni,
+                                   oarr, no, opts.elements or 0, opts.tag,
+                                   opts.max_segment_size, opts.timeout_ms)
+    if errors:
+        raise errors[0]
+    check(rc, "allreduce")

@@ -13,6 +13,7 @@
 #include "context.h"
 #include "executor.h"
 #include "executor_internal.h"
+#include "host_fn.h"
 #include "host_ops.h"
 #include "kernels.h"
 #include "linkprobe.h"
@@ -495,6 +496,60 @@ int glx_allreduce(glx_context* ctx, int algorithm, int dtype, int op, void* cons
     o.timeout = std::chrono::milliseconds(timeout_ms > 0 ? timeout_ms : 0);
     o.stream = (hipStream_t)stream;
     gloo::allreduce(o);
+    return GLX_OK;
+  });
+}
+
+int glx_allreduce_host_fn(glx_context* ctx, int algorithm, size_t element_size,
+                          glx_reduce_fn fn, void* user, void* const* inputs, int num_inputs,
+                          void* const* outputs, int num_outputs, size_t elements, uint32_t tag,
+                          size_t max_segment_size, int64_t timeout_ms) {
+  return guarded([&]() -> int {
+    GLX_ENFORCE(ctx != nullptr, "null context");
+    GLX_ENFORCE(fn != nullptr, "allreduce: null reduction function");
+    GLX_ENFORCE(num_inputs >= 0 && (num_inputs == 0 || inputs != nullptr), "bad inputs");
+    GLX_ENFORCE(num_outputs > 0 && outputs != nullptr, "allreduce: at least one output");
+    GLX_ENFORCE(element_size > 0, "allreduce: element size must be positive");
+    GLX_ENFORCE(algorithm == GLX_ALLREDUCE_UNSPECIFIED || algorithm == GLX_ALLREDUCE_RING ||
+                    algorithm == GLX_ALLREDUCE_BCUBE,
+                "allreduce with a host reduction function: RING or BCUBE");
+    GLX_ENFORCE(elements <= ((size_t)1 << 40), "allreduce: too many elements");
+    std::vector<const void*> in(inputs, inputs + num_inputs);
+    std::vector<void*> out(outputs, outputs + num_outputs);
+    for (const void* p : in) {
+      GLX_ENFORCE(gloo::exec::isHostPointer(p),
+                  "allreduce: a host reduction function needs host buffers (a device cannot "
+                  "run it); device buffers take gloo::sum/product/max/min");
+    }
+    for (const void* p : out) {
+      GLX_ENFORCE(gloo::exec::isHostPointer(p),
+                  "allreduce: a host reduction function needs host buffers (a device cannot "
+                  "run it); device buffers take gloo::sum/product/max/min");
+    }
+    if (elements == 0) return GLX_OK;  // gloo/allreduce.cc:98-100
+    auto& c = *ctx->c;
+    GLX_ENFORCE(c.size == 1 || c.connected(),
+                "allreduce: context must be connected (connectFullMesh)");
+    const int algo = algorithm == GLX_ALLREDUCE_BCUBE ? glx::ALGO_FN_BCUBE : glx::ALGO_FN_RING;
+    const size_t maxSeg = max_segment_size == 0 ? (size_t)glx::kMaxSegmentBytes
+                                                : max_segment_size;
+    const std::string key = "hostfn/" + std::to_string(algo) + "/" +
+                            std::to_string(element_size) + "/" + std::to_string(elements) +
+                            "/" + std::to_string(tag) + "/" + std::to_string(maxSeg);
+    std::shared_ptr<gloo::Algorithm> alg;
+    {
+      std::lock_guard<std::mutex> g(c.opsMutex);
+      auto it = c.ops.find(key);
+      if (it != c.ops.end()) {
+        alg = it->second;
+      } else {
+        alg = std::make_shared<gloo::HostFnExecutor>(ctx->c, algo, element_size, elements,
+                                                     maxSeg);
+        c.ops.emplace(key, alg);
+      }
+    }
+    static_cast<gloo::HostFnExecutor&>(*alg).call(
+        fn, user, in, out, std::chrono::milliseconds(timeout_ms > 0 ? timeout_ms : 0));
     return GLX_OK;
   });
 }

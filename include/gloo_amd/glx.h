@@ -398,6 +398,25 @@ int glx_allreduce(glx_context* ctx, int algorithm, int dtype, int op,
                   int num_outputs, size_t elements, uint32_t tag,
                   size_t max_segment_size, int64_t timeout_ms, glx_stream_t stream);
 
+/* A caller's reduction function c = f(a, b) over n elements -- the
+ * reference's AllreduceOptions::Func (gloo/allreduce.h:36,69,171), which may
+ * be any host std::function (bitwise ops, user types, non-commutative ops);
+ * `user` is passed through. */
+typedef void (*glx_reduce_fn)(void* user, void* c, const void* a, const void* b, size_t n);
+/* gloo::allreduce(opts) with such a function, on HOST buffers: the same step
+ * program as glx_allreduce (RING, or BCUBE; UNSPECIFIED = RING) run on the
+ * host -- messages through shared memory, every reduction a call of `fn` in
+ * the reference's order and operand order (gloo/allreduce.cc:44-95,
+ * :286-297, :580-596), so the result bits are the reference's for any
+ * function.  element_size: bytes per element (any, as opts.elementSize).
+ * Device buffers are refused (GLX_ERR_INVALID): a device cannot run a host
+ * function; use glx_allreduce with sum/product/max/min there.  Every rank
+ * must make the same sequence of calls (as in the reference). */
+int glx_allreduce_host_fn(glx_context* ctx, int algorithm, size_t element_size,
+                          glx_reduce_fn fn, void* user, void* const* inputs, int num_inputs,
+                          void* const* outputs, int num_outputs, size_t elements, uint32_t tag,
+                          size_t max_segment_size, int64_t timeout_ms);
+
 /* Algorithm::run() (gloo/algorithm.h:26).  With streams and the
  * GLX_ENGINE_DMASTEPS engine the call only enqueues (copies, reduce and flag
  * kernels on streams[0] and the algorithm's copy streams; message numbers

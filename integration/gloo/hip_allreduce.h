@@ -485,25 +485,71 @@ inline size_t glxElementSize(int dtype) {
   }
 }
 
+// A caller's AllreduceOptions::Func through glx_reduce_fn: the call's
+// function, and the first exception it threw (never unwound through the C
+// ABI; rethrown after the call).
+struct HostFnCall {
+  const AllreduceOptions::Func* fn;
+  std::exception_ptr error;
+  static void trampoline(void* user, void* c, const void* a, const void* b, size_t n) {
+    HostFnCall* call = static_cast<HostFnCall*>(user);
+    if (call->error) return;
+    try {
+      (*call->fn)(c, a, b, n);
+    } catch (...) {
+      call->error = std::current_exception();
+    }
+  }
+};
+
 // gloo::allreduce(const AllreduceOptions&) (gloo/allreduce.h:193,
-// gloo/allreduce.cc:97-146) on device buffers.  Same options, same checks
-// (gloo/allreduce.cc:113-119), same result bits; opts.setAlgorithm picks
-// the reference's schedule (RING, BCUBE; UNSPECIFIED = RING's result with
-// the data movement chosen by size).  stream == nullptr: the outputs are
-// complete on return; else the work is ordered on `stream`.
+// gloo/allreduce.cc:97-146).  Same options, same checks (gloo/allreduce.cc:
+// 113-119), same result bits; opts.setAlgorithm picks the reference's
+// schedule (RING, BCUBE; UNSPECIFIED = RING's result with the data movement
+// chosen by size).  With gloo/math.h's sum/product/max/min<T> the buffers
+// may be device memory (the xGMI path); stream == nullptr: the outputs are
+// complete on return, else the work is ordered on `stream`.  With any other
+// Func (gloo/allreduce.h:36,69,171) the buffers must be host memory: the
+// same step program runs on the host, calling the function in the
+// reference's order (glx_allreduce_host_fn).
 inline void allreduce(const AllreduceOptions& opts, hipStream_t stream = nullptr) {
   const detail::AllreduceOptionsImpl& o = OptionsAccess::of(opts);
   GLOO_ENFORCE(o.context, "allreduce: no context");
   GLOO_ENFORCE(!o.out.empty(), "allreduce: no output buffer");
   GLOO_ENFORCE(o.elementSize > 0);
+  GLOO_ENFORCE(o.reduce, "allreduce: no reduce function");
   int dtype = -1, op = -1;
-  GLOO_ENFORCE(o.reduce && mathFunction(o.reduce, &dtype, &op),
-               "HIP allreduce: the reduce function must be one of gloo/math.h's "
-               "sum/product/max/min<T> (a host std::function cannot run on the device)");
+  if (!mathFunction(o.reduce, &dtype, &op)) {
+    GLOO_ENFORCE(stream == nullptr,
+                 "HIP allreduce: a caller's reduce function runs on the host, with host "
+                 "buffers; there is no stream to order it on");
+    const size_t bytes = o.elements * o.elementSize;
+    std::vector<void*> in, out;
+    for (const auto& b : o.in) {
+      GLOO_ENFORCE_EQ(b->size, bytes, "input buffers must all hold the element count");
+      in.push_back(b->ptr);
+    }
+    for (const auto& b : o.out) {
+      GLOO_ENFORCE_EQ(b->size, bytes, "output buffers must all hold the element count");
+      out.push_back(b->ptr);
+    }
+    int algorithm = GLX_ALLREDUCE_UNSPECIFIED;
+    if (o.algorithm == detail::AllreduceOptionsImpl::RING) algorithm = GLX_ALLREDUCE_RING;
+    if (o.algorithm == detail::AllreduceOptionsImpl::BCUBE) algorithm = GLX_ALLREDUCE_BCUBE;
+    auto x = XgmiContext::of(o.context, nullptr, deviceOf(out[0]));
+    HostFnCall call{&o.reduce, nullptr};
+    const int rc = glx_allreduce_host_fn(
+        x->get(), algorithm, o.elementSize, &HostFnCall::trampoline, &call,
+        in.empty() ? nullptr : in.data(), (int)in.size(), out.data(), (int)out.size(),
+        o.elements, o.tag, o.maxSegmentSize, (int64_t)o.timeout.count());
+    if (call.error) std::rethrow_exception(call.error);
+    check(rc, "allreduce");
+    return;
+  }
   GLOO_ENFORCE_EQ(glxElementSize(dtype), o.elementSize,
                   "reduce function's element type differs from the buffers'");
   const size_t bytes = o.elements * o.elementSize;
-  std::vector<void*> in, out;
+  std::vector<void*> in, out;  // device buffers (or host ones, staged per call)
   for (const auto& b : o.in) {
     GLOO_ENFORCE_EQ(b->size, bytes, "input buffers must all hold the element count");
     in.push_back(b->ptr);

@@ -44,6 +44,25 @@ int g_bcube_base = 2;  // gloo::Context::base for AllreduceBcube (ref_set_bcube_
 enum { R_INT8 = 0, R_UINT8, R_INT32, R_INT64, R_UINT64, R_FLOAT32, R_FLOAT64,
        R_FLOAT16, R_BFLOAT16 };
 enum { R_SUM = 1, R_PRODUCT = 2, R_MAX = 3, R_MIN = 4 };
+// Caller-supplied reduction functions (AllreduceOptions::Func,
+// gloo/allreduce.h:36,69,171) for the custom-function fixtures, over 32-bit
+// words: a bitwise or, and c = 3a + b (mod 2^32) -- neither commutative nor
+// associative, so the output bits pin the order and operands of every call.
+enum { R_CUSTOM_OR = 100, R_CUSTOM_3A_PLUS_B = 101 };
+
+void customOr(void* c, const void* a, const void* b, size_t n) {
+  const uint32_t* x = static_cast<const uint32_t*>(a);
+  const uint32_t* y = static_cast<const uint32_t*>(b);
+  uint32_t* z = static_cast<uint32_t*>(c);
+  for (size_t i = 0; i < n; i++) z[i] = x[i] | y[i];
+}
+
+void custom3aPlusB(void* c, const void* a, const void* b, size_t n) {
+  const uint32_t* x = static_cast<const uint32_t*>(a);
+  const uint32_t* y = static_cast<const uint32_t*>(b);
+  uint32_t* z = static_cast<uint32_t*>(c);
+  for (size_t i = 0; i < n; i++) z[i] = 3u * x[i] + y[i];
+}
 
 thread_local std::string g_err;
 
@@ -140,6 +159,8 @@ template <typename T>
 gloo::AllreduceOptions::Func mathFn(int op) {
   void (*f)(void*, const void*, const void*, size_t) = nullptr;
   switch (op) {
+    case R_CUSTOM_OR: f = &customOr; break;
+    case R_CUSTOM_3A_PLUS_B: f = &custom3aPlusB; break;
     case R_SUM: f = &gloo::sum<T>; break;
     case R_PRODUCT: f = &gloo::product<T>; break;
     case R_MAX: f = &gloo::max<T>; break;
@@ -153,7 +174,8 @@ gloo::AllreduceOptions::Func mathFn(int op) {
 template <typename T>
 int allreduceFnT(int algo, int op, int P, int nin, int nout, size_t count, size_t maxSeg,
                  void** ins, void** outs) {
-  if (op < R_SUM || op > R_MIN) return -1;
+  const bool custom = op == R_CUSTOM_OR || op == R_CUSTOM_3A_PLUS_B;
+  if (custom ? sizeof(T) != 4 : (op < R_SUM || op > R_MIN)) return -1;
   auto store = std::make_shared<gloo::rendezvous::HashStore>();
   std::vector<std::thread> threads;
   std::vector<std::string> errors(P);

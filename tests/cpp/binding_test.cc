@@ -90,6 +90,9 @@ template <> gloo::float16 value<gloo::float16>(int r, size_t i) {
 void spawn(int P, const std::function<void(std::shared_ptr<gloo::Context>,
                                            gloo::rendezvous::Store&, int)>& fn);
 
+void compareCustom(int P, int count, int nin, int nout, gloo::AllreduceOptions::Algorithm algo,
+                   size_t maxSeg);
+
 void spawnCpu2(const std::function<void(std::shared_ptr<gloo::Context>,
                                         gloo::rendezvous::Store&, int)>& fn) {
   spawn(2, fn);
@@ -244,6 +247,12 @@ int cpuMode() {
     for (auto& t : ts) t.join();
     EXPECT(rcs[0] == GLX_OK && rcs[1] == GLX_OK, "connect through the bridge: %d %d (%s)",
            rcs[0], rcs[1], glx_last_error());
+  }
+  // a caller's Func on host buffers needs no GPU (glx_allreduce_host_fn)
+  for (auto algo : {AllreduceOptions::Algorithm::RING, AllreduceOptions::Algorithm::BCUBE}) {
+    compareCustom(2, 1000, 0, 1, algo, 0);
+    compareCustom(3, 4099, 2, 1, algo, 1024);
+    compareCustom(4, 65537, 1, 2, algo, 0);
   }
   std::printf("binding_test cpu: %s\n", failures ? "FAILED" : "OK");
   return failures ? 1 : 0;
@@ -457,6 +466,73 @@ void compareFn(const char* name, int P, int count, int nin, int nout,
   EXPECT(bad == 0, "%s: %zu buffers differ from the reference", name, bad);
   std::printf("%s P=%d count=%d in=%d out=%d: %s\n", name, P, count, nin, nout,
               bad ? "MISMATCH" : "ok");
+}
+
+// A caller's AllreduceOptions::Func (gloo/allreduce.h:36,69,171) on HOST
+// buffers: gloo::hip::allreduce runs it on the host in the reference's
+// order; the reference's gloo::allreduce with the same std::function (a
+// capturing closure, c = k*a + b over 32-bit words, neither commutative nor
+// associative) on host copies gives the bits to match.  Two calls per rank,
+// the second reusing the cached executor.
+void compareCustom(int P, int count, int nin, int nout, gloo::AllreduceOptions::Algorithm algo,
+                   size_t maxSeg) {
+  const uint32_t k = 3;
+  gloo::AllreduceOptions::Func f = [k](void* c, const void* a, const void* b, size_t n) {
+    const uint32_t* x = static_cast<const uint32_t*>(a);
+    const uint32_t* y = static_cast<const uint32_t*>(b);
+    uint32_t* z = static_cast<uint32_t*>(c);
+    for (size_t i = 0; i < n; i++) z[i] = k * x[i] + y[i];
+  };
+  using T = int32_t;
+  std::vector<std::vector<std::vector<T>>> in(P), out0(P), ref(P), got(P);
+  for (int r = 0; r < P; r++) {
+    for (int j = 0; j < nin; j++) {
+      std::vector<T> v((size_t)count);
+      for (int i = 0; i < count; i++) v[(size_t)i] = value<T>(r * 8 + j, (size_t)i);
+      in[r].push_back(v);
+    }
+    for (int j = 0; j < nout; j++) {
+      std::vector<T> v((size_t)count);
+      for (int i = 0; i < count; i++) v[(size_t)i] = value<T>(r * 8 + 4 + j, (size_t)i);
+      out0[r].push_back(v);
+    }
+    ref[r] = out0[r];
+  }
+  auto run = [&](bool hip, std::vector<std::vector<std::vector<T>>>& outs) {
+    spawn(P, [&](std::shared_ptr<gloo::Context> ctx, gloo::rendezvous::Store&, int r) {
+      for (int it = 0; it < (hip ? 2 : 1); it++) {
+        std::vector<std::vector<T>> hin = in[r];
+        outs[r] = out0[r];
+        std::vector<T*> ins, os;
+        for (auto& v : hin) ins.push_back(v.data());
+        for (auto& v : outs[r]) os.push_back(v.data());
+        gloo::AllreduceOptions o(ctx);
+        o.setAlgorithm(algo);
+        if (!ins.empty()) o.setInputs(ins, (size_t)count);
+        o.setOutputs(os, (size_t)count);
+        o.setReduceFunction(f);
+        if (maxSeg > 0) o.setMaxSegmentSize(maxSeg);
+        if (hip) {
+          gloo::hip::allreduce(o);
+        } else {
+          gloo::allreduce(o);
+        }
+      }
+    });
+  };
+  run(false, ref);
+  run(true, got);
+  size_t bad = 0;
+  for (int r = 0; r < P; r++) {
+    for (int j = 0; j < nout; j++) {
+      bad += std::memcmp(got[r][(size_t)j].data(), ref[r][(size_t)j].data(),
+                         sizeof(T) * (size_t)count) != 0;
+    }
+  }
+  EXPECT(bad == 0, "custom Func: %zu buffers differ from the reference", bad);
+  std::printf("custom Func (host) %s P=%d count=%d in=%d out=%d seg=%zu: %s\n",
+              algo == gloo::AllreduceOptions::Algorithm::BCUBE ? "bcube" : "ring", P, count,
+              nin, nout, maxSeg, bad ? "MISMATCH" : "ok");
 }
 
 template <typename T>

@@ -380,6 +380,73 @@ def make_allreduce_fn():
     print("allreduce_fn: %d cases" % len(index))
 
 
+# ---- gloo::allreduce(opts) with a caller's reduction function --------------
+# oracle/ref_harness.cc's custom Funcs over 32-bit words: 100 = a | b, 101 =
+# 3a + b (mod 2^32; neither commutative nor associative, so the output bits
+# pin every call's order and operands).  The product runs them on host
+# buffers (glx_allreduce_host_fn).
+CUSTOM_OR, CUSTOM_3A_PLUS_B = 100, 101
+CUSTOM_CASES = []
+for _algo in (O.FN_RING, O.FN_BCUBE):
+    for _P in (1, 2, 3, 4, 5, 8):
+        for _N, _nin, _nout, _ms in ((1, 0, 1, 0), (17, 1, 1, 0), (1000, 2, 1, 0),
+                                     (4099, 0, 1, 1024), (4099, 3, 2, 0), (65537, 0, 3, 4096)):
+            for _op in (CUSTOM_OR, CUSTOM_3A_PLUS_B):
+                CUSTOM_CASES.append((_algo, _P, _N, _op, _nin, _nout, _ms))
+
+
+def custom_case_buffers(c):
+    """(inputs, outputs) per rank of a CUSTOM_CASES entry (int32 words): the
+    tests rebuild them with the same calls."""
+    algo, P, N, op, nin, nout, ms = c
+    ins = [[O.fill(O.INT32, N, 0, seed=SEED + 7, rank=r, ptr_index=i) for i in range(nin)]
+           for r in range(P)]
+    outs = [[O.fill(O.INT32, N, 0, seed=SEED + 8, rank=r, ptr_index=i) for i in range(nout)]
+            for r in range(P)]
+    return ins, outs
+
+
+def custom_case_name(c):
+    algo, P, N, op, nin, nout, ms = c
+    return "%s_P%d_N%d_%s_in%d_out%d_seg%d" % (
+        "ring" if algo == O.FN_RING else "bcube", P, N,
+        {CUSTOM_OR: "or", CUSTOM_3A_PLUS_B: "3a_plus_b"}[op], nin, nout, ms)
+
+
+def make_allreduce_custom():
+    out = {}
+    index = []
+    for c in CUSTOM_CASES:
+        algo, P, N, op, nin, nout, ms = c
+        ins, outs = custom_case_buffers(c)
+        res = O.allreduce_fn(algo, op, O.INT32, ins, outs, ms, use_ref=True)
+        first = res[0][0]
+        for r in range(P):
+            for i in range(nout):
+                assert np.array_equal(res[r][i], first), \
+                    "reference ranks disagree in %s" % custom_case_name(c)
+        name = custom_case_name(c)
+        index.append({"name": name, "algo": algo, "P": P, "N": N, "op": op, "nin": nin,
+                      "nout": nout, "max_segment_size": ms, "seed": SEED,
+                      "input_sha256": sha([x for row in ins + outs for x in row]),
+                      "output_sha256": sha([first])})
+        if N <= 4099:
+            out[name] = first
+        else:  # the digest pins it; a sample says where a mismatch starts
+            idx = np.linspace(0, N - 1, 257).astype(np.int64)
+            out[name + "_idx"] = idx
+            out[name + "_sample"] = first[idx]
+    np.savez_compressed(os.path.join(HERE, "allreduce_custom_golden.npz"), **out)
+    with open(os.path.join(HERE, "allreduce_custom_golden.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py (make_allreduce_custom)",
+                   "source": "gloo::allreduce(AllreduceOptions) with oracle/ref_harness.cc's "
+                             "custom Funcs (100: a | b, 101: 3a + b mod 2^32 on 32-bit words) "
+                             "of oracle/_ref/libgloo_ref.so (reference compiled from "
+                             "/root/reference by oracle/Makefile)",
+                   "cases": index}, f, indent=1)
+    print("allreduce_custom: %d cases" % len(index))
+
+
 # ---- BASELINE.json configs at full size (digests, not arrays) -------------
 # cfg3: ring_chunked fp32, 8 ranks, the 1K..16M element sweep;
 # cfg4: halving_doubling fp32, 8 ranks, 256 MiB per rank;
@@ -483,7 +550,8 @@ def make_bench():
 if __name__ == "__main__":
     if not O.ref_available():
         sys.exit("oracle/_ref/libgloo_ref.so missing: make -C oracle ref")
-    which = sys.argv[1:] or ["reduce", "f16", "allreduce", "allreduce_fn", "ring", "bcube"]
+    which = sys.argv[1:] or ["reduce", "f16", "allreduce", "allreduce_fn", "ring", "bcube",
+                             "custom"]
     if "reduce" in which:
         make_reduce()
     if "f16" in which:
@@ -496,6 +564,8 @@ if __name__ == "__main__":
         make_ring()
     if "bcube" in which:
         make_bcube()
+    if "custom" in which:
+        make_allreduce_custom()
     if "scale" in which:  # not in the default set: minutes and ~40 GiB of RAM
         make_scale()
     if "bench" in which:  # bench.py's N > 1 workloads (256 MiB fp32, P = 2, 4, 8)

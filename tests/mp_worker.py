@@ -63,6 +63,8 @@ def main():
         return run_device_timeout(store_dir, rank, size)
     if algo == "dmaabort":
         return run_dma_abort(store_dir, rank, size)
+    if algo == "custom":
+        return run_custom(store_dir, rank, size)
     if algo.startswith("killpeer:"):
         return run_killpeer(store_dir, rank, size, *algo.split(":")[1:])
     if algo == "devsteps":
@@ -209,6 +211,34 @@ def run_device_timeout(store_dir, rank, size):
         alg.close()
     ctx.close()
     if not ok:
+        print("MISMATCH rank", rank)
+        sys.exit(1)
+    print("OK")
+
+
+def run_custom(store_dir, rank, size):
+    """Every custom-function fixture case at P = size (tests/
+    test_allreduce_custom.py): gloo::allreduce with a caller's function on
+    host buffers, one process per rank, each output against the reference's."""
+    import gloo_amd
+    from test_allreduce_custom import CASES, buffers, check_result, run_rank
+    store = gloo_amd.rendezvous.FileStore(store_dir)
+    ctx = gloo_amd.rendezvous.Context(rank, size, 0)
+    ctx.setTimeout(60)
+    ctx.connectFullMesh(store)
+    bad, n = [], 0
+    for c in CASES:
+        if c["P"] != size:
+            continue
+        ins, outs = buffers(c)
+        run_rank(ctx, c, ins[rank], outs[rank])
+        n += 1
+        if not all(check_result(c, o) for o in outs[rank]):
+            bad.append(c["name"])
+    barrier(store, rank, size, "custom")
+    ctx.close()
+    print("custom cases %d, wrong %s" % (n, bad[:5]))
+    if bad or n == 0:
         print("MISMATCH rank", rank)
         sys.exit(1)
     print("OK")

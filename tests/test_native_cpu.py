@@ -247,11 +247,13 @@ def test_allreduce_options_assignment_goes_through_the_setters():
     assert opts._out_ptrs[0][0] == a.ctypes.data and opts.elements == 8
     opts.outputs = [b]
     assert opts._out_ptrs[0][0] == b.ctypes.data and opts.elements == 16
-    assert opts.outputs == [b] and opts.outputs is not opts._outputs
+    assert opts.outputs == (b,) and opts.outputs is not opts._outputs
+    with pytest.raises(AttributeError):
+        opts.outputs.append(a)  # an in-place edit raises, never lost
     opts.inputs = [b.copy()]
     assert opts._in_ptrs[1] == 1
     opts.inputs = []
-    assert opts._in_ptrs is None and opts.inputs == []
+    assert opts._in_ptrs is None and opts.inputs == ()
 
 
 def test_reduce_tuning_is_atomic_across_threads():
