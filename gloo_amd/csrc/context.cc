@@ -270,6 +270,15 @@ uint64_t makeCanary(int rank, int64_t id) {
 }
 }  // namespace
 
+size_t Context::ipcMaxBlockBytes() {
+  static const size_t v = [] {
+    const char* e = std::getenv("GLOO_AMD_IPC_MAX_BLOCK_BYTES");
+    const long long x = e != nullptr ? std::atoll(e) : 0;
+    return x >= (1 << 20) ? (size_t)x : kIpcMaxBlockBytes;
+  }();
+  return v;
+}
+
 SharedBlock Context::acquireShared(size_t bytes, unsigned flags) {
   const size_t granule = sharedGranule();
   const size_t alloc =
@@ -279,11 +288,13 @@ SharedBlock Context::acquireShared(size_t bytes, unsigned flags) {
   // more never returns under the HIP runtime torch ships (ROCm 7.0; the
   // image's 7.2 runtime maps it: tools/micro/ipc_size_probe.py),
   // so such a block is refused here rather than hanging both ranks.
-  GLX_ENFORCE(!sharesAcrossProcesses() || alloc < kIpcMaxBlockBytes, "rank ", rank,
+  GLX_ENFORCE(!sharesAcrossProcesses() || alloc < ipcMaxBlockBytes(), "rank ", rank,
               ": a landing block of ", alloc, " bytes would have to be shared with another "
-              "process, and IPC imports of 2 GiB or more hang in the HIP runtime; this "
-              "schedule's largest receive region needs it (use a smaller buffer per call, "
-              "more ranks, or the ring / halving-doubling schedule)");
+              "process, and IPC imports of ", ipcMaxBlockBytes(), " bytes or more hang in "
+              "the HIP runtime torch ships (GLOO_AMD_IPC_MAX_BLOCK_BYTES raises the limit "
+              "for a runtime that maps more); this schedule's largest receive region needs "
+              "it (use a smaller buffer per call, more ranks, or the ring / "
+              "halving-doubling schedule, whose messages are split)");
   std::lock_guard<std::mutex> g(sharedMutex_);
   // the smallest free block of this kind that fits without wasting much
   SharedBlock* best = nullptr;
@@ -301,7 +312,7 @@ SharedBlock Context::acquireShared(size_t bytes, unsigned flags) {
   SharedBlock nb;
   size_t got = alloc;
   // a recycled block may be larger (never as large as the IPC limit)
-  nb.ptr = allocBlock(device_, &got, flags, kIpcMaxBlockBytes);
+  nb.ptr = allocBlock(device_, &got, flags, ipcMaxBlockBytes());
   bytes = got - kCanaryBytes;
   nb.bytes = bytes;
   nb.flags = flags;

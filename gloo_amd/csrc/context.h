@@ -174,7 +174,13 @@ class Context {
   // canary and page rounding): larger ones are refused with EnforceNotMet,
   // since a peer's hipIpcOpenMemHandle of 2^31 bytes or more never returned
   // under torch's HIP runtime (2^31 - 2 MiB mapped).
+  // GLOO_AMD_IPC_MAX_BLOCK_BYTES raises it for a runtime that maps more (the
+  // image's ROCm 7.2 runtime maps 4 GiB); every rank must use the
+  // same value.  Messages above 512 MiB are split (plan.h kMaxMessageBytes),
+  // so the default limit is reached only by an explicit schedule's own slot
+  // arrays (the one-shot's whole buffers) or glx_set_max_message_bytes.
   static constexpr size_t kIpcMaxBlockBytes = size_t(1) << 31;
+  static size_t ipcMaxBlockBytes();
   bool sharesAcrossProcesses() const { return size > 1 && crossProcess_; }
   SharedBlock acquireShared(size_t bytes, unsigned flags);
   void releaseShared(int64_t id);

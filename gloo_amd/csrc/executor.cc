@@ -203,7 +203,7 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
     }
     const size_t arr = (size_t)contextSize_ * ((size_t)maxMsg * esize_ + 512) + 4096;
     if (maxMsg * (int64_t)esize_ > prm_.maxMessageBytes ||
-        (ctx->sharesAcrossProcesses() && arr >= Context::kIpcMaxBlockBytes)) {
+        (ctx->sharesAcrossProcesses() && arr >= Context::ipcMaxBlockBytes())) {
       engine_ = kEngineSteps;
     }
   }
@@ -241,7 +241,7 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
     if (slots_ > 1 && ctx->sharesAcrossProcesses()) {
       // from the largest region of EVERY rank's program, so all ranks agree
       const ScratchBlock whole{0, sync_.maxRegionElems, nullptr, {}};
-      if ((size_t)slots_ * slotBytes(whole) + 4096 >= Context::kIpcMaxBlockBytes) slots_ = 1;
+      if ((size_t)slots_ * slotBytes(whole) + 4096 >= Context::ipcMaxBlockBytes()) slots_ = 1;
     }
     if (!sync_.safe) engine_ = kEngineSteps;
   }

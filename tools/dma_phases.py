@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Where a DMA-driven ring's rounds go, from one rank's rocprofv3 kernel and
 memory-copy traces of tools/hop_latency.py (--engines host_steps,dma_steps;
-tools/run_r11c.sh): the trace is cut into its four phases (host-issued steps
+tools/gpu_recipes.sh timeline): the trace is cut into its four phases (host-issued steps
 and DMA steps with on-GPU hand-offs, at each of two sizes, in the tool's
 order), and for each phase the median duration of the SDMA copies, reduce and
 copy kernels and flag-op kernels, and -- for the DMA steps -- the median time
@@ -70,4 +70,6 @@ def main():
 
 
 if __name__ == "__main__":
+    import faulthandler
+    faulthandler.enable()  # a crash prints every thread's stack
     main()

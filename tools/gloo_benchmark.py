@@ -321,4 +321,6 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
+    import faulthandler
+    faulthandler.enable()  # a crash prints every thread's stack
     sys.exit(main())

@@ -59,4 +59,6 @@ def main():
 
 
 if __name__ == "__main__":
+    import faulthandler
+    faulthandler.enable()  # a crash prints every thread's stack
     main()

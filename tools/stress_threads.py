@@ -23,7 +23,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=30)
     ap.add_argument("--runs", type=int, default=50)
+    ap.add_argument("--close", default="explicit", choices=["explicit", "gc"],
+                    help="explicit: each rank closes its algorithm and context at once; "
+                         "gc: each rank drops them and the garbage collector destroys the "
+                         "native handles from whichever thread runs it")
     a = ap.parse_args()
+    import gc
     import torch
 
     import gloo_amd
@@ -43,8 +48,11 @@ def main():
                     alg = gloo_amd.AllreduceRingChunked(ctx, [bufs[r]], schedule="ring")
                     for _ in range(a.runs):
                         alg.run()
-                    alg.close()
-                    ctx.close()
+                    if a.close == "explicit":
+                        alg.close()
+                        ctx.close()
+                    else:
+                        del alg, ctx  # __del__ (Algorithm, Context) wherever GC runs
                 except BaseException as e:  # noqa: BLE001
                     errors.append(repr(e)[:300])
             ts = [threading.Thread(target=rank, args=(r,)) for r in range(P)]
@@ -52,6 +60,7 @@ def main():
                 t.start()
             for t in ts:
                 t.join()
+            gc.collect()
             # the runs fold the values again and again: only the bits'
             # agreement across ranks is checked
             same = all(torch.equal(bufs[0], b) for b in bufs[1:])
@@ -65,4 +74,6 @@ def main():
 
 
 if __name__ == "__main__":
+    import faulthandler
+    faulthandler.enable()  # a crash prints every thread's stack
     sys.exit(main())

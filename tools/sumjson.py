@@ -1,6 +1,9 @@
 """Summarise bench.py JSON lines (N>1): value, schedule/engine, alternatives, sweep."""
+import faulthandler
 import json
 import sys
+
+faulthandler.enable()  # a crash prints every thread's stack
 
 for f in sys.argv[1:]:
     lines = [l for l in open(f) if l.startswith("{")]

@@ -1,7 +1,10 @@
 """Sweep the reduce kernel's unroll depth and grid cap on the cfg2 workload
 (c = a + b, 256 MiB fp32) and a 16 MiB chunk; prints achieved HBM GB/s."""
+import faulthandler
 import json
 import sys
+
+faulthandler.enable()  # a crash prints every thread's stack
 import os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
