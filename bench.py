@@ -634,7 +634,7 @@ SEED = 1234  # SURVEY 8d's synthetic-input seed
 
 def plan_name(algo):
     """Schedule name of a bench candidate for gloo_amd.plan()."""
-    for suffix in ("_narrow", "_system", "_host", "_dma", "_fast", "_plain"):
+    for suffix in ("_pipe", "_narrow", "_system", "_host", "_dma", "_fast", "_plain"):
         if algo.endswith(suffix):
             algo = algo[:-len(suffix)]
     return {"ring_chunked_mesh_steps": "ring_chunked_mesh",
@@ -648,6 +648,10 @@ def golden_plan(algo):
     return "halving_doubling" if plan_name(algo) == "halving_doubling" else "ring_chunked"
 
 
+# the pipelined DMA rings' piece size (BENCH_PIPE_BYTES overrides)
+PIPE_BYTES = int(os.environ.get("BENCH_PIPE_BYTES", 4 << 20))
+
+
 def make_alg(gloo_amd, ctx, buf, algo):
     """With the ranks on distinct devices/processes: ring_chunked and
     halving_doubling run their step programs in the plan kernel (devsteps) at
@@ -658,7 +662,16 @@ def make_alg(gloo_amd, ctx, buf, algo):
     with their hand-offs on the GPU (the dmasteps engine);
     *_fast / *_plain the plan kernel with a forced stream policy
     (set_engine_streams), *_narrow / *_system the device engines with a
-    forced flag sync (set_device_sync; the run's default is RUN_SYNC)."""
+    forced flag sync (set_device_sync; the run's default is RUN_SYNC);
+    *_pipe (after _host / _dma) those engines pipelined below chunk
+    granularity: pieces of PIPE_BYTES, each reduced and forwarded on its own
+    (set_pipeline_bytes, VERDICT r5 #4)."""
+    if algo.endswith("_pipe"):
+        gloo_amd.set_pipeline_bytes(PIPE_BYTES)
+        try:
+            return make_alg(gloo_amd, ctx, buf, algo[:-len("_pipe")])
+        finally:
+            gloo_amd.set_pipeline_bytes(0)
     for suffix, policy in (("_narrow", "narrow"), ("_system", "system")):
         if algo.endswith(suffix):  # the device engines with a forced flag sync
             gloo_amd.set_device_sync(policy)
@@ -1071,8 +1084,10 @@ def element_sweep(torch, dist, gloo_amd, ctx, dev, schedules, dtype):
 # DESIGN.md 5d)
 DEFAULT_CANDIDATES = ["ring_chunked", "ring_chunked_mesh", "ring_chunked_host",
                       "ring_chunked_dma", "ring_chunked_mesh_steps"]
-EXTRA_CANDIDATES = ["ring_chunked_fast", "ring_chunked_system", "ring_chunked_mesh_system"]
-DMA_CANDIDATES = ("ring_chunked_host", "ring_chunked_dma", "ring_chunked_mesh_steps")
+EXTRA_CANDIDATES = ["ring_chunked_fast", "ring_chunked_system", "ring_chunked_mesh_system",
+                    "ring_chunked_host_pipe", "ring_chunked_dma_pipe"]
+DMA_CANDIDATES = ("ring_chunked_host", "ring_chunked_dma", "ring_chunked_mesh_steps",
+                  "ring_chunked_host_pipe", "ring_chunked_dma_pipe")
 DEFAULT_ALTS = ["halving_doubling"]
 EXTRA_ALTS = ["halving_doubling_host", "halving_doubling_dma", "halving_doubling_system"]
 # host-issued steps' peer-copy transports: (engine, DMA split, copy-kernel workgroups)
@@ -1150,7 +1165,7 @@ def measured_link_for(engine, transport_tr, links):
 # plan kernel (CU stores), host-issued DMA steps, DMA steps with on-GPU
 # hand-offs (reported when timed: the default candidates and --schedule ring)
 NS_RINGS = ("ring_chunked", "ring_chunked_host")
-NS_RINGS_OPT = ("ring_chunked_dma",)
+NS_RINGS_OPT = ("ring_chunked_dma", "ring_chunked_host_pipe", "ring_chunked_dma_pipe")
 
 
 def north_star_section(S, world, ring_runs, links, refdig, failed):

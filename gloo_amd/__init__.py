@@ -107,6 +107,18 @@ def max_message_bytes():
     return int(_lib.lib.glx_max_message_bytes())
 
 
+def set_pipeline_bytes(nbytes):
+    """Pipelining below chunk granularity for the host-issued and DMA steps
+    engines (glx.h glx_set_pipeline_bytes): messages as pieces of about
+    nbytes, each reduced and forwarded on its own; 0 = off.  For algorithms
+    created afterwards; every rank must use the same value."""
+    errors.check(_lib.lib.glx_set_pipeline_bytes(int(nbytes)), "set_pipeline_bytes")
+
+
+def pipeline_bytes():
+    return int(_lib.lib.glx_pipeline_bytes())
+
+
 def set_device_sync(mode):
     """Release / acquire around the device engines' flags for algorithms
     created afterwards: "auto" (default: narrow), "system" (L2 written back before

@@ -46,6 +46,8 @@ SIGNATURES = [
     ("glx_allreduce_host_fn", _i, [_vp, _i, _sz, _vp, _vp, ctypes.POINTER(_vp), _i,
                                    ctypes.POINTER(_vp), _i, _sz, ctypes.c_uint32, _sz, _i64]),
     ("glx_max_message_bytes", _i64, []),
+    ("glx_set_pipeline_bytes", _i, [_i64]),
+    ("glx_pipeline_bytes", _i64, []),
     ("glx_reduce_segment_bytes", _sz, []),
     ("glx_set_copy_split", _i, [_i]),
     ("glx_set_pinned_mirror_limit", _i, [_sz]),

@@ -98,6 +98,9 @@ glx::PlanParams planParams(int esize, int64_t maxSegmentBytes, int64_t minPieceB
   p.esize = esize;
   if (maxSegmentBytes > 0) p.maxSegmentBytes = maxSegmentBytes;
   p.minPieceBytes = minPieceBytes < 0 ? 0 : minPieceBytes;
+  // the programs the host-issued / DMA steps engines run under
+  // glx_set_pipeline_bytes (the CPU tests replay them)
+  p.pipelineBytes = glx::pipelineBytes();
   return p;
 }
 
@@ -203,6 +206,16 @@ int glx_set_max_message_bytes(int64_t bytes) {
 }
 
 int64_t glx_max_message_bytes(void) { return glx::maxMessageBytes(); }
+
+int glx_set_pipeline_bytes(int64_t bytes) {
+  if (bytes < 0 || (bytes > 0 && bytes < 4096)) {
+    return fail(GLX_ERR_INVALID, "glx_set_pipeline_bytes: 0 (off) or at least 4096");
+  }
+  glx::setPipelineBytes(bytes);
+  return GLX_OK;
+}
+
+int64_t glx_pipeline_bytes(void) { return glx::pipelineBytes(); }
 
 int glx_reduce_tuning(int* unroll, int* blocks_per_cu, int* policy) {
   if (unroll == nullptr || blocks_per_cu == nullptr || policy == nullptr) {

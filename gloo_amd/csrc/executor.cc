@@ -245,6 +245,15 @@ void HipPlanExecutor::construct(const std::shared_ptr<Context>& ctx,
     }
     if (!sync_.safe) engine_ = kEngineSteps;
   }
+  // Pipelining below chunk granularity (glx_set_pipeline_bytes): the
+  // host-issued and DMA steps engines on device buffers run the program with
+  // its messages cut into pieces and reduce-and-forward per piece (plan.h
+  // splitMessages); every rank reaches the same engine, hence the same plan
+  if ((engine_ == kEngineSteps || engine_ == kEngineDmaSteps) && !hostMode_ &&
+      contextSize_ > 1 && count_ > 0 && glx::pipelineBytes() > 0) {
+    prm_.pipelineBytes = glx::pipelineBytes();
+    plan_ = glx::makePlan(algo, contextRank_, contextSize_, count_, prm_);
+  }
   if (engine_ == kEngineOneShot || engine_ == kEngineTwoShot) {
     setupDevice();
   } else {
@@ -576,6 +585,7 @@ void HipPlanExecutor::publish() {
   putPod<int32_t>(b, engine_);
   putPod<int32_t>(b, (int32_t)slots_);
   putPod<int64_t>(b, prm_.maxMessageBytes);  // how this rank's program cut its messages
+  putPod<int64_t>(b, prm_.pipelineBytes);
   putPod<int32_t>(b, (int32_t)copyEngine_);
   putPod<int32_t>(b, (int32_t)ddBlocks_.size());
   for (size_t k = 0; k < ddBlocks_.size(); k++) putRef(b, ddRefs_[k]);
@@ -607,6 +617,7 @@ std::vector<int64_t> HipPlanExecutor::retiredIn(const std::vector<char>& rec) co
   getPod<int32_t>(rec, at);  // engine
   getPod<int32_t>(rec, at);  // slots
   getPod<int64_t>(rec, at);  // max message bytes
+  getPod<int64_t>(rec, at);  // pipeline bytes
   getPod<int32_t>(rec, at);  // copy engine
   const int32_t nb = getPod<int32_t>(rec, at);
   for (int32_t k = 0; k < nb; k++) getRef(rec, at);
@@ -697,6 +708,10 @@ void HipPlanExecutor::resolvePeers() {
                 " (GLOO_AMD_FUSE must be the same on every rank; two slots are kept only "
                 "while two of the largest region stay below the 2 GiB IPC block limit)");
     const int64_t peerMaxMsg = getPod<int64_t>(b, at);
+    const int64_t peerPipe = getPod<int64_t>(b, at);
+    GLX_ENFORCE(peerPipe == prm_.pipelineBytes, "rank ", r, " pipelines in pieces of ",
+                peerPipe, " bytes, rank ", contextRank_, " in ", prm_.pipelineBytes,
+                " (glx_set_pipeline_bytes must be the same on every rank)");
     GLX_ENFORCE(peerMaxMsg == prm_.maxMessageBytes, "rank ", r, " cuts messages above ",
                 peerMaxMsg, " bytes, rank ", contextRank_, " above ", prm_.maxMessageBytes,
                 " (glx_set_max_message_bytes must be the same on every rank)");

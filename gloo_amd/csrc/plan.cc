@@ -882,7 +882,7 @@ void setMaxMessageBytes(int64_t bytes) {
   g_maxMessageBytes.store(bytes > 0 ? bytes : kMaxMessageBytes);
 }
 
-void splitMessages(Plan& p, int64_t M, int64_t V) {
+void splitMessages(Plan& p, int64_t M, int64_t V, bool forward) {
   if (M <= 0 || V <= 0 || M % V != 0) fail("splitMessages: bad piece length");
   for (const Step& s : p.steps) {
     if (s.kind == FOLD && (s.flags & kFoldWhole) != 0) return;  // left whole (plan.h)
@@ -979,6 +979,22 @@ void splitMessages(Plan& p, int64_t M, int64_t V) {
     };
     int64_t K = 1;
     for (const auto& kv : region) K = std::max(K, piecesOf(kv.first));
+    // the SENDs right after the group forwarding one of its results, sent
+    // per piece inside the loop below (forward)
+    size_t fwdEnd = j + 1;
+    if (forward) {
+      while (fwdEnd < in.size() && in[fwdEnd].kind == SEND && in[fwdEnd].len > 0) {
+        bool result = false;
+        for (size_t k = i; k <= j; k++) {
+          result = result || ((in[k].kind == REDUCE || in[k].kind == COPY ||
+                               in[k].kind == FOLD) &&
+                              in[k].off == in[fwdEnd].off && in[k].len == in[fwdEnd].len);
+        }
+        if (!result) break;
+        fwdEnd++;
+      }
+    }
+    for (size_t f = j + 1; f < fwdEnd; f++) K = std::max(K, pieces(in[f].off, in[f].len));
     for (int64_t q = 0; q < K; q++) {
       for (size_t k = i; k <= j; k++) {
         const Step& t = in[k];
@@ -1009,11 +1025,32 @@ void splitMessages(Plan& p, int64_t M, int64_t V) {
         }
         out.push_back(u);
       }
+      for (size_t f = j + 1; f < fwdEnd; f++) {  // the forwards of piece q
+        const Step& t = in[f];
+        if (q >= pieces(t.off, t.len)) continue;
+        Step u = t;
+        u.channel = t.channel + q * kPieceChannelStride;
+        piece(t.off, t.len, q, &u.off, &u.len);
+        u.dst_off = t.dst_off + q * M;
+        out.push_back(u);
+      }
     }
-    i = j + 1;
+    i = fwdEnd;
   }
   p.steps = std::move(out);
 }
+
+namespace {
+std::atomic<int64_t> g_pipelineBytes{[] {
+  const char* e = std::getenv("GLOO_AMD_PIPELINE_BYTES");
+  const int64_t v = e != nullptr ? std::atoll(e) : 0;
+  return v >= 4096 ? v : (int64_t)0;
+}()};
+}  // namespace
+
+int64_t pipelineBytes() { return g_pipelineBytes.load(); }
+
+void setPipelineBytes(int64_t bytes) { g_pipelineBytes.store(bytes >= 4096 ? bytes : 0); }
 
 Plan makePlan(int algo, int rank, int size, int64_t count, const PlanParams& prm) {
   if (size < 1 || rank < 0 || rank >= size || count < 0) fail("bad geometry");
@@ -1034,8 +1071,10 @@ Plan makePlan(int algo, int rank, int size, int64_t count, const PlanParams& prm
   // pieces of a whole number of 16-byte vectors (the landing phase rule)
   const int64_t es = std::max(1, prm.esize);
   const int64_t V = 16 / std::min<int64_t>(16, es);
-  const int64_t M = std::max<int64_t>(V, prm.maxMessageBytes / es / V * V);
-  splitMessages(p, M, V);
+  int64_t bytesPer = prm.maxMessageBytes;
+  if (prm.pipelineBytes > 0) bytesPer = std::min(bytesPer, prm.pipelineBytes);
+  const int64_t M = std::max<int64_t>(V, bytesPer / es / V * V);
+  splitMessages(p, M, V, prm.pipelineBytes > 0);
   return p;
 }
 

@@ -98,6 +98,11 @@ struct PlanParams {
   int base = 2;
   // messages above this many bytes are split (kMaxMessageBytes)
   int64_t maxMessageBytes = glx::maxMessageBytes();
+  // > 0: pipelining below chunk granularity (the executor sets it for the
+  // host-issued and DMA steps engines, glx_set_pipeline_bytes): messages are
+  // cut into pieces of about this many bytes, and a reduce-and-forward is
+  // done per piece (splitMessages' `forward`)
+  int64_t pipelineBytes = 0;
 };
 
 // Cut every message whose landing spans more than maxElems elements into
@@ -119,8 +124,20 @@ struct PlanParams {
 // per-element reduction chains are untouched: results are bit-identical.
 // Plans folding whole-buffer messages (kFoldWhole: AllreduceRing, the
 // replicated schedules) are left whole.
+//
+// forward: the SENDs right after a receive group that send one of its
+// REDUCE / COPY results on (the ring's "reduce, notify, forward",
+// gloo/allreduce_ring_chunked.h:141-157; the mesh's result to every peer)
+// go out per piece too, right after that piece's RELEASE -- the next rank
+// starts on piece 0 while this one reduces piece 1 (the reference's own
+// segmented ring keeps two segments in flight, gloo/allreduce.cc:279-321).
+// Each piece index is its own ring of messages, so this adds no credit cycle.
 constexpr int64_t kPieceChannelStride = int64_t(1) << 16;
-void splitMessages(Plan& p, int64_t maxElems, int64_t V);
+void splitMessages(Plan& p, int64_t maxElems, int64_t V, bool forward = false);
+
+// glx_set_pipeline_bytes / GLOO_AMD_PIPELINE_BYTES: 0 (default) = off.
+int64_t pipelineBytes();
+void setPipelineBytes(int64_t bytes);
 
 // Region padding: room to land a message at any 16-byte phase after
 // rounding its region base up to 16 bytes (<= 30 bytes for 1-byte elements).

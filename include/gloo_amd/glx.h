@@ -143,6 +143,15 @@ int glx_reduce_tuning(int* unroll, int* blocks_per_cu, int* policy);
  * when the algorithm's peers resolve).  Results are unchanged. */
 int glx_set_max_message_bytes(int64_t bytes);
 int64_t glx_max_message_bytes(void);
+/* Pipelining below chunk granularity for the host-issued and DMA steps
+ * engines on device buffers: each message goes as pieces of about this many
+ * bytes, each reduced and forwarded on its own (plan.h splitMessages with
+ * forward; the reference's segmented ring keeps two segments in flight,
+ * gloo/allreduce.cc:279-321).  0 = off (default; GLOO_AMD_PIPELINE_BYTES).
+ * Process-wide, for algorithms created afterwards; every rank must use the
+ * same value (checked).  Results are unchanged. */
+int glx_set_pipeline_bytes(int64_t bytes);
+int64_t glx_pipeline_bytes(void);
 /* glx_reduce on more than this many bytes per stream goes out as consecutive
  * kernel launches over equal segments of at most this size (one grid-stride
  * launch over 1 GiB streams ran 6 % slower on MI355X): a

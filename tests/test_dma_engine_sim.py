@@ -265,3 +265,25 @@ def test_program_order_rule_with_split_messages(algo, P, N, staged):
             qmap = [m[min(choice, len(m) - 1)] for m in per_rank]
             stuck = run_ranks(pks, qmap)
             assert not stuck, (algo, P, N, staged, Q, qmap, stuck)
+
+
+@pytest.mark.parametrize("algo,P,N", [("ring_chunked", 2, 20000), ("ring_chunked", 4, 40000),
+                                      ("ring_chunked", 8, 80000),
+                                      ("halving_doubling", 4, 40000)])
+def test_program_order_rule_with_pipelined_messages(algo, P, N):
+    """the pipelined programs (4 KiB pieces, reduce-and-forward
+    per piece) under the DMA steps engine's enqueue rule: no stall on any
+    mapping of its streams onto 1-4 hardware queues."""
+    gloo_amd.set_pipeline_bytes(4096)
+    try:
+        progs = [gloo_amd.plan(algo, r, P, N)[0] for r in range(P)]
+    finally:
+        gloo_amd.set_pipeline_bytes(0)
+    pks = [packets(r, progs[r], 2, False, "ordered") for r in range(P)]
+    rng = random.Random(hash((algo, P, N, "pipe")) & 0xffff)
+    for Q in (1, 2, 3, 4):
+        per_rank = [mappings(streams_of(pk), Q, rng, 4) for pk in pks]
+        for choice in range(len(per_rank[0])):
+            qmap = [m[min(choice, len(m) - 1)] for m in per_rank]
+            stuck = run_ranks(pks, qmap)
+            assert not stuck, (algo, P, N, Q, qmap, stuck)

@@ -110,3 +110,38 @@ def test_huge_threshold_leaves_every_message_whole():
             assert max(s[4] for s in whole) >= n // 4
     finally:
         gloo_amd.set_max_message_bytes(0)
+
+
+@pytest.fixture
+def pipelined():
+    gloo_amd.set_pipeline_bytes(SMALL)
+    try:
+        yield SMALL
+    finally:
+        gloo_amd.set_pipeline_bytes(0)
+    assert gloo_amd.pipeline_bytes() == 0
+
+
+@pytest.mark.parametrize("name", sorted(CLASS))
+@pytest.mark.parametrize("P", [2, 3, 4, 8])
+@pytest.mark.parametrize("N", [4099, 65537])
+@pytest.mark.parametrize("dtype,op", [(O.FLOAT32, O.SUM), (O.FLOAT16, O.SUM), (O.INT8, O.MAX)])
+def test_pipelined_programs_match_the_oracle(pipelined, name, P, N, dtype, op):
+    """pipelining below chunk granularity (glx_set_pipeline_bytes,
+    splitMessages with forward): pieces of 4 KiB, the ring's reduce-and-forward
+    (and the mesh's result sends) per piece -- no credit cycle, the oracle's
+    bits."""
+    es = np.dtype(O.NP_DTYPE[dtype]).itemsize
+    plans = [gloo_amd.plan(name, r, P, N, with_folds=True, esize=es) for r in range(P)]
+    assert max(s[4] for pl in plans for s in pl[0] if s[0] in (0, 1)) <= SMALL // es
+    if name == "ring_chunked":
+        # a forward right after each piece's RELEASE: RECV, REDUCE, RELEASE, SEND
+        st = plans[0][0]
+        fwd = [i for i in range(3, len(st)) if st[i][0] == 0 and st[i - 1][0] == 4
+               and st[i - 2][0] == 2 and st[i][3] == st[i - 2][3] and st[i][4] == st[i - 2][4]]
+        assert len(fwd) >= 2
+    ins = case_inputs(P, N, dtype, 1, 0, seed=P * 13 + N % 89)
+    got = replay_plans(plans, op, dtype, [ins[r][0] for r in range(P)])
+    exp = O.allreduce(CLASS[name], op, dtype, ins)
+    for r in range(P):
+        assert same_bits(got[r], exp[r][0]), "rank %d" % r
