@@ -898,6 +898,11 @@ void splitMessages(Plan& p, int64_t M, int64_t V, bool forward) {
     return span <= M ? (int64_t)1 : (span - 1) / M + 1;
   };
   auto piece = [&](int64_t off, int64_t len, int64_t q, int64_t* o, int64_t* l) {
+    if (off % V + len <= M) {  // one piece (and no (q + 1) * M to overflow)
+      *o = off;
+      *l = len;
+      return;
+    }
     const int64_t a = q == 0 ? off : off - off % V + q * M;
     const int64_t b = std::min(off + len, off - off % V + (q + 1) * M);
     *o = a;

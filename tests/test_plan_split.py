@@ -100,8 +100,11 @@ def test_huge_threshold_leaves_every_message_whole():
     """The executor compiles every rank's unsplit program (threshold 2^62) to
     decide whether the one- and two-shot kernels may run: the piece count
     must not overflow there (it once did, and the two-shot ran a split plan)."""
-    gloo_amd.set_max_message_bytes(1 << 62)
+    gloo_amd.set_max_message_bytes((1 << 63) - 1)  # the executor's own probe value
     try:
+        for es in (1, 2, 4):  # small buffers too: no (q + 1) * M overflow
+            st = gloo_amd.plan("ring_chunked_mesh", 0, 2, 4099, esize=es)[0]
+            assert max(s[4] for s in st if s[0] in (0, 1)) == 2050
         n = (1 << 31) - 1
         for name, es in (("ring_chunked_mesh", 1), ("ring_chunked_mesh", 2),
                          ("halving_doubling", 8), ("ring_chunked", 2)):
