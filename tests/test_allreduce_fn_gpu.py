@@ -207,12 +207,21 @@ def test_timeout_raises_io_exception():
     assert time.time() - t0 < 5
 
 
-def test_custom_reduce_function_is_rejected():
+def test_custom_reduce_function_needs_host_buffers():
+    """A caller's function runs on the host (glx_allreduce_host_fn,
+    tests/test_allreduce_custom.py): with device buffers allreduce() refuses
+    it, naming why; something that is not a function is refused at once."""
+    import torch
+
     import gloo_amd
     ctx = gloo_amd.rendezvous.Context(0, 1, 0)
     opts = gloo_amd.AllreduceOptions(ctx)
     with pytest.raises(gloo_amd.EnforceNotMet):
-        opts.setReduceFunction(lambda a, b, c, n: None)
+        opts.setReduceFunction("sum")
+    opts.setReduceFunction(lambda c, a, b, n: None)
+    opts.setOutput(torch.zeros(8, device="cuda"))
+    with pytest.raises(gloo_amd.EnforceNotMet, match="host buffers"):
+        gloo_amd.allreduce(opts)
 
 
 WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "mp_worker.py")
