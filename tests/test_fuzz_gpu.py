@@ -121,13 +121,22 @@ def test_device_engines_random_cases_multiprocess(P, seed_):
         assert "'dmasteps'" in eng, eng
 
 
+SPLIT_ENVS = {
+    # messages split at 64 KiB (GLOO_AMD_MAX_MESSAGE_BYTES, plan.cc
+    # splitMessages): each piece its own channel and sub-region
+    "split": {"GLOO_AMD_MAX_MESSAGE_BYTES": str(64 << 10)},
+    # pipelined at 16 KiB (GLOO_AMD_PIPELINE_BYTES): the
+    # host-issued and DMA steps forward every piece of a chunk on its own
+    "pipelined": {"GLOO_AMD_PIPELINE_BYTES": str(16 << 10)},
+}
+
+
+@pytest.mark.parametrize("variant", sorted(SPLIT_ENVS))
 @pytest.mark.parametrize("P,seed_", [(2, 5), (4, 6)])
-def test_device_engines_random_cases_with_split_messages(P, seed_):
-    """The multi-process fuzz with messages split at 64 KiB
-    (GLOO_AMD_MAX_MESSAGE_BYTES, plan.h splitMessages): the
-    plan kernel, the host-issued and DMA steps run split programs (each piece
-    its own channel and sub-region), every rank bit for bit against the
-    oracle."""
+def test_device_engines_random_cases_with_split_messages(P, seed_, variant):
+    """The multi-process fuzz on split programs: the plan kernel, the
+    host-issued and DMA steps (pipelined: the steps engines only), every rank
+    bit for bit against the oracle."""
     import os
     import subprocess
     import sys
@@ -137,7 +146,7 @@ def test_device_engines_random_cases_with_split_messages(P, seed_):
     worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "mp_worker.py")
     with tempfile.TemporaryDirectory() as d:
         env = rank_env(P)
-        env["GLOO_AMD_MAX_MESSAGE_BYTES"] = str(64 << 10)
+        env.update(SPLIT_ENVS[variant])
         env["FUZZ_CASES"] = "60"
         procs = [subprocess.Popen([sys.executable, worker, d, str(r), str(P), "fuzz:%d" % seed_],
                                   env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)

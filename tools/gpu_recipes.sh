@@ -13,6 +13,9 @@
 #   bench1_rocprof     bench.py --no-pmc under rocprofv3 --kernel-trace --stats -> $O/n1prof
 #   rehearsals         bench.py --gpus P at P = 8, 4, 2 (ranks share the GPU) -> $O/mp<P>_shared_gpu.json
 #   rings              the three rings at 256 MiB, P = 2, 4, 8 -> $O/mp<P>_rings.json
+#   pipe               the rings with and without pipelining below chunk granularity, P = 2
+#                      at piece sizes $PIPES (MiB, default "1 4 16"), P = 4, 8 at 4 MiB
+#                      -> $O/pipe_p<P>_<MiB>MiB.json
 #   hop                tools/hop_latency.py at P = 2, 4 (ENGINES=...) -> $O/hop_p<P>.json
 #   dma_tests          the DMA steps engine's GPU tests -> $O/dma_tests.txt
 #   soak               tests/test_soak_gpu.py -> $O/soak.txt
@@ -60,6 +63,16 @@ recipe() {
       mp 2 4 29541 $a > "$O/mp2_rings.json" 2> "$O/mp2_rings.err" &&
         mp 4 2 29542 $a > "$O/mp4_rings.json" 2> "$O/mp4_rings.err" &&
         mp 8 1 29543 $a > "$O/mp8_rings.json" 2> "$O/mp8_rings.err" ;;
+    pipe)
+      local a="--candidates ring_chunked,ring_chunked_host,ring_chunked_host_pipe"
+      a="$a,ring_chunked_dma,ring_chunked_dma_pipe --no-alt --no-link-probe --no-sweep --no-staged"
+      a="$a --steps 10 --warmup 3"
+      for m in ${PIPES:-1 4 16}; do
+        BENCH_PIPE_BYTES=$((m << 20)) mp 2 4 29561 $a > "$O/pipe_p2_${m}MiB.json" \
+          2> "$O/pipe_p2_${m}MiB.err" || return 1
+      done
+      BENCH_PIPE_BYTES=$((4 << 20)) mp 4 2 29562 $a > "$O/pipe_p4_4MiB.json" 2> "$O/pipe_p4_4MiB.err" &&
+        BENCH_PIPE_BYTES=$((4 << 20)) mp 8 1 29563 $a > "$O/pipe_p8_4MiB.json" 2> "$O/pipe_p8_4MiB.err" ;;
     hop)
       for pq in "2 4" "4 2"; do
         set -- $pq
