@@ -389,12 +389,6 @@ void HipPlanExecutor::setupDevSteps() {
   GLX_HIP_CHECK(hipMemcpy(devSegs_, segs.data(), segs.size() * sizeof(glx::DevSegment),
                           hipMemcpyHostToDevice));
   pk_.segs = devSegs_;
-  pk_.nsegs = (int)segs.size();
-  // the program's head in LDS (kernels.h kPkStepCache); GLOO_AMD_PK_LDS=0
-  // reads every descriptor from global memory (A/B measurements)
-  const char* lds = std::getenv("GLOO_AMD_PK_LDS");
-  const bool useLds = lds == nullptr || lds[0] != '0';
-  pk_.ldsSegs = useLds ? std::min(pk_.nsegs, glx::kPkSegCache) : 0;
   for (size_t k = 0; k < in_.size(); k++) in_[k].deliveryWord = (uint32_t)k;
   for (size_t k = 0; k < out_.size(); k++) out_[k].creditWord = (uint32_t)(in_.size() + k);
   const size_t rows = std::max<size_t>(1, in_.size() + out_.size());
@@ -545,7 +539,6 @@ void HipPlanExecutor::buildDevSteps() {
   pk_.steps = devSteps_;
   pk_.foldSrc = devFoldSrc_;
   pk_.nsteps = (int)plan_.steps.size();
-  pk_.ldsSteps = pk_.ldsSegs > 0 ? std::min(pk_.nsteps, glx::kPkStepCache) : 0;
   pk_.slots = slots_;
 }
 

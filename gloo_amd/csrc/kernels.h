@@ -186,24 +186,12 @@ struct DevStep {
   int64_t srcSlot;         // REDUCE / COPY: bytes from one landing slot to the next
   int64_t dstSlot;         // SEND: the same in the peer's region
 };
-// The plan kernel copies the first kPkStepCache steps and kPkSegCache
-// segments of its program into LDS once per workgroup (round 6, VERDICT r5
-// weak #5): every acquire invalidates the XCD's L2 lines of ordinary device
-// memory, so a descriptor read from global memory after a wait was a fresh
-// memory round trip on every step's critical path (one 128-byte line per
-// workgroup and step in the read counters).  Longer programs read the rest
-// from global memory as before.  ~27 KiB of static LDS: below what the
-// register-bound occupancy (3-4 workgroups per CU) leaves per workgroup.
-constexpr int kPkStepCache = 128, kPkSegCache = 512;
 struct PlanKernelParams {
   char* buf;
   const DevStep* steps;        // device memory
   const DevSegment* segs;      // device memory
   const char* const* foldSrc;  // device memory; nullptr = buf
   int nsteps, G;
-  int nsegs;                   // entries of segs
-  int ldsSteps, ldsSegs;       // the head copied into LDS: <= kPkStepCache / kPkSegCache
-                               // (0: none, GLOO_AMD_PK_LDS=0, an A/B switch)
   int slots;                   // landing slots per channel (1 or 2, plan.h SyncTable)
   int maxSrc;                  // most sources of a FOLD step (2 when there is none)
   uint64_t run;                // host's count of its launches (diagnostics only)

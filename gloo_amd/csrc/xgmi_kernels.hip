@@ -708,8 +708,7 @@ __device__ __forceinline__ bool seg_part(const DevSegment& sg, int w, size_t& a,
 // the 8-way fold's registers would cut the resident workgroups per CU from
 // the 2-source variant's count (kernel-resource-usage) to 3.
 template <typename T, int OP, int MAXSRC, bool FAST, int RSP>
-__device__ __forceinline__ void plan_body(const PlanKernelParams& p, DevStep* s_steps,
-                                          DevSegment* s_segs) {
+__device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
   using S = typename Elem<T, OP>::S;
   __shared__ int s_ok;
   const int w = blockIdx.x;
@@ -724,27 +723,12 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p, DevStep* s_
   };
   // message m of a channel lands in slot (m - 1) % slots
   auto slotOf = [&](uint64_t m) -> uint64_t { return p.slots == 2 ? ((m - 1) & 1) : 0; };
-  // the program's head into LDS, once (kernels.h kPkStepCache): no acquire
-  // below invalidates it
-  static_assert(sizeof(DevStep) % 8 == 0 && sizeof(DevSegment) % 8 == 0, "8-byte words");
-  {
-    const int nst = p.ldsSteps, nsg = p.ldsSegs;
-    const int wst = nst * (int)(sizeof(DevStep) / 8), wsg = nsg * (int)(sizeof(DevSegment) / 8);
-    const uint64_t* gst = reinterpret_cast<const uint64_t*>(p.steps);
-    const uint64_t* gsg = reinterpret_cast<const uint64_t*>(p.segs);
-    uint64_t* lst = reinterpret_cast<uint64_t*>(s_steps);
-    uint64_t* lsg = reinterpret_cast<uint64_t*>(s_segs);
-    for (int k = threadIdx.x; k < wst; k += kBlock) lst[k] = gst[k];
-    for (int k = threadIdx.x; k < wsg; k += kBlock) lsg[k] = gsg[k];
-    __syncthreads();
-  }
-  auto segAt = [&](int g) -> DevSegment { return g < p.ldsSegs ? s_segs[g] : p.segs[g]; };
   // the runs completed before this launch (kernels.h PlanKernelParams::runCtr)
   uint64_t run;
   if (!launch_number(p.runCtr, p.status, p.claim, &run)) return;
   uint32_t polls = 0;  // lane 0's flag reads (diagnostics: p.polls)
   for (int i = 0; i < p.nsteps; i++) {
-    const DevStep st = i < p.ldsSteps ? s_steps[i] : p.steps[i];
+    const DevStep st = p.steps[i];
     const uint64_t seq = run * st.perRun + st.seq;
     stamp(2 * i);
     switch (st.kind) {
@@ -765,7 +749,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p, DevStep* s_
         const S* srcs[2] = {buf, src};
         for (int g = st.seg0; g < st.seg1; g++) {
           size_t a, b;
-          if (!seg_part(segAt(g), w, a, b)) continue;
+          if (!seg_part(p.segs[g], w, a, b)) continue;
           const bool over = g >= st.pre0 && g < st.pre1;
           if (st.kind == kStepCopyPre) {
             if (over) {
@@ -800,7 +784,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p, DevStep* s_
           for (int g = st.seg0; g < st.seg1; g++) {
             size_t a, b;
             if (g >= st.pre0 && g < st.pre1) continue;  // stored by the step before
-            if (seg_part(segAt(g), w, a, b)) {
+            if (seg_part(p.segs[g], w, a, b)) {
               copy_span<S, FAST, RSP>(reinterpret_cast<S*>(dst), buf, a, b, aligned);
             }
           }
@@ -811,7 +795,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p, DevStep* s_
           const S* srcs[2] = {buf, src};
           for (int g = st.seg0; g < st.seg1; g++) {
             size_t a, b;
-            if (!seg_part(segAt(g), w, a, b)) continue;
+            if (!seg_part(p.segs[g], w, a, b)) continue;
             if (st.kind == kStepCopySend) {
               scatter_span<S, FAST, FAST ? kStLocalWt : kStPlain, 1, 2, RSP>(outs, 2, src, a, b,
                                                                         aligned);
@@ -851,7 +835,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p, DevStep* s_
         }
         for (int g = st.seg0; g < st.seg1; g++) {
           size_t a, b;
-          if (!seg_part(segAt(g), w, a, b)) continue;
+          if (!seg_part(p.segs[g], w, a, b)) continue;
           if (st.kind == 3) {
             copy_span<S, FAST, FAST ? kStLocalWt : kStPlain>(buf, srcs[1], a, b, aligned);
           } else if (st.kind == 2 || st.left) {
@@ -882,16 +866,13 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p, DevStep* s_
 
 template <typename T, int OP, int MAXSRC, int RSP>
 __global__ __launch_bounds__(kBlock, 2) void plan_kernel(PlanKernelParams p) {
-  // one LDS copy of the program's head for both stream variants
-  __shared__ DevStep s_steps[kPkStepCache];
-  __shared__ DevSegment s_segs[kPkSegCache];
   if constexpr (RSP == kStRemote) {  // the test-only plain-store build runs plain streams
     if (p.fast) {
-      plan_body<T, OP, MAXSRC, true, RSP>(p, s_steps, s_segs);
+      plan_body<T, OP, MAXSRC, true, RSP>(p);
       return;
     }
   }
-  plan_body<T, OP, MAXSRC, false, RSP>(p, s_steps, s_segs);
+  plan_body<T, OP, MAXSRC, false, RSP>(p);
 }
 
 #ifndef GLX_XGMI_UNSAFE_TU
@@ -1124,9 +1105,7 @@ hipError_t GLX_TU_NAME(launch_plan_kernel)(int op, int dtype, const PlanKernelPa
   if (p.narrow == kSyncUnsafe) return launch_plan_kernel_unsafe_stores(op, dtype, p, s);
 #endif
   if (p.G < 1 || p.G > kOsMaxSlices || p.nsteps < 0 || p.steps == nullptr ||
-      p.segs == nullptr || p.nsegs < 1 || p.ldsSteps < 0 || p.ldsSteps > kPkStepCache ||
-      p.ldsSteps > p.nsteps || p.ldsSegs < 0 || p.ldsSegs > kPkSegCache || p.ldsSegs > p.nsegs ||
-      p.foldSrc == nullptr || p.status == nullptr || p.claim == nullptr ||
+      p.segs == nullptr || p.foldSrc == nullptr || p.status == nullptr || p.claim == nullptr ||
       p.runCtr == nullptr ||
       (p.slots != 1 && p.slots != 2) || p.maxSrc < 2 || p.maxSrc > kOsMaxRanks) {
     return hipErrorInvalidValue;
