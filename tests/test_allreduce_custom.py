@@ -146,10 +146,12 @@ def test_custom_function_exception_propagates():
         gloo_amd.allreduce(opts)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("P", [2, 4])
+@pytest.mark.parametrize("P", [3, pytest.param(2, marks=pytest.mark.gpu),
+                               pytest.param(4, marks=pytest.mark.gpu)])
 def test_custom_function_one_process_per_rank(P):
-    """The fixtures' cases at P, one process per rank (mp_worker.py custom)."""
+    """The fixtures' cases at P, one process per rank (mp_worker.py custom):
+    the function runs on the host, so P = 3 runs in the CPU suite as well;
+    the GPU suite runs P = 2 and 4 on the box."""
     worker = os.path.join(HERE, "mp_worker.py")
     with tempfile.TemporaryDirectory() as d:
         from helpers import rank_env
