@@ -979,9 +979,10 @@ def probe_device_engines(torch, dist, gloo_amd, connect, dev, dtype, n_full=None
     """Before timing them, check the device-driven engines (one-shot,
     two-shot and plan kernels) on this machine: short timeout, results
     bit-identical to the host-issued steps engine over refilled runs -- three
-    per case at 64 K / 1 M elements and, given n_full, at the timed size
-    itself (the north star's 256 MiB per rank: VERDICT r5 #1), and twenty of
-    the ring at PROBE_SMALL's L1-warm size.
+    per case at 64 K / 1 M elements (ten of the mesh at 1 M, where a missing
+    release shows) and, given n_full, at the timed size itself (the north
+    star's 256 MiB per rank: VERDICT r5 #1), and twenty of the ring at
+    PROBE_SMALL's L1-warm size (where a missing acquire shows).
     Each attempt runs on a context of its own (`connect(tag)`), so a failed
     attempt cannot leave the ranks' algorithm slots out of step for the run.
     The default narrow flag sync is tried first; if any rank fails, the
@@ -994,7 +995,7 @@ def probe_device_engines(torch, dist, gloo_amd, connect, dev, dtype, n_full=None
         ctx = connect(tag)
         ctx.setTimeout(15)
         try:
-            cases = [("ring_chunked_repl", 65536 + 3, 3), ("ring_chunked_mesh", (1 << 20) + 5, 3),
+            cases = [("ring_chunked_repl", 65536 + 3, 3), ("ring_chunked_mesh", (1 << 20) + 5, 10),
                      ("ring_chunked", 1 << 20, 3), ("halving_doubling", 1 << 20, 3),
                      ("ring_chunked", PROBE_SMALL[0], PROBE_SMALL[1])]
             if n_full:

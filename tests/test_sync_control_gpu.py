@@ -13,11 +13,14 @@ the checks catch on one GPU:
   narrow sync at P = 4 and 8, and wrong in (nearly) every run of the ring on
   every rank once the consumer's acquire is dropped (unsafe_noacquire;
   profiles/round6/sync_control_*.json: 200 of 200 runs at P = 4 and 8);
-* dropping the producer's store-completion wait (unsafe_norelease, even with
-  the workgroup barrier before the flag removed) was NOT caught on one GPU in
-  200 runs at P = 2, 4 and 8: the stores land long before a consumer's poll,
-  acquire and loads; that hazard needs the node's xGMI latency to show, which
-  is what bench.py's refilled checks on every rank watch for there.
+* dropping the producer's store-completion wait and the workgroup barrier
+  before the flag (unsafe_norelease) is NOT caught at 4096 or 65,536
+  elements -- a workgroup's slice is then one wave's, and it lands before any
+  consumer's poll -- but IS caught at 1 M elements, where a slice spans every
+  wave of the workgroup and the flag can overtake the other waves' stores:
+  the two-shot mesh wrong in 91-100 of 100 runs on every rank at P = 4 and 8
+  (the plan kernel's ring and halving-doubling in 0-2; 16 M elements: the
+  mesh in 25-46; profiles/round6/sync_control_release_1M_16M.json).
 """
 import os
 import re
@@ -31,14 +34,15 @@ from helpers import rank_env
 
 WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "mp_worker.py")
 SMALL = 4096
+LARGE = 1 << 20
 
 
-def small_soak(P, runs, sync):
+def small_soak(P, runs, sync, n=SMALL):
     env = rank_env(P)
     env["GLOO_AMD_SYNC"] = sync
     with tempfile.TemporaryDirectory() as d:
         procs = [subprocess.Popen([sys.executable, WORKER, d, str(r), str(P),
-                                   "soak:%d:delays:%d" % (runs, SMALL)],
+                                   "soak:%d:delays:%d" % (runs, n)],
                                   env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
                  for r in range(P)]
         outs = []
@@ -81,3 +85,29 @@ def test_small_buffer_soak_catches_a_missing_acquire(P):
     assert all(rc != 0 for rc in rcs), rcs
     for r, b in enumerate(bad):
         assert b.get("ring", 0) >= runs // 2, (r, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [4, 8])
+def test_large_buffer_soak_exact_under_the_product_sync(P):
+    """The release-side detector on the product: 1 M elements, every
+    workgroup's slice spread over all its waves, 100 runs of every engine,
+    every run exact."""
+    rcs, bad, eng, outs = small_soak(P, 100, "narrow", LARGE)
+    assert "'mesh': 'twoshot'" in eng, eng
+    assert rcs == [0] * P and all(b == {} for b in bad), (rcs, bad, outs[0][-2000:])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [4, 8])
+def test_large_buffer_soak_catches_a_missing_release(P):
+    """Positive control for the producer side: with every wave's store wait
+    and the barrier before the flag dropped (test-only kSyncNoRelease) the
+    two-shot mesh hands over data still in flight; measured wrong in 91-100
+    of 100 runs on every rank."""
+    runs = 40
+    rcs, bad, eng, _ = small_soak(P, runs, "unsafe_norelease", LARGE)
+    assert "'mesh': 'twoshot'" in eng, eng
+    assert all(rc != 0 for rc in rcs), rcs
+    for r, b in enumerate(bad):
+        assert b.get("mesh", 0) >= runs // 2, (r, b)
