@@ -45,6 +45,8 @@ SIGNATURES = [
     ("glx_set_max_message_bytes", _i, [_i64]),
     ("glx_allreduce_host_fn", _i, [_vp, _i, _sz, _vp, _vp, ctypes.POINTER(_vp), _i,
                                    ctypes.POINTER(_vp), _i, _sz, ctypes.c_uint32, _sz, _i64]),
+    ("glx_allreduce_create_host_fn", _vp, [_vp, _i, ctypes.POINTER(_vp), _i, _i, _sz, _vp,
+                                           _vp]),
     ("glx_max_message_bytes", _i64, []),
     ("glx_set_pipeline_bytes", _i, [_i64]),
     ("glx_pipeline_bytes", _i64, []),
@@ -133,6 +135,9 @@ STORE_SET_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_char_p,
                                 ctypes.c_void_p, ctypes.c_size_t)
 STORE_GET_FN = ctypes.CFUNCTYPE(ctypes.c_int64, ctypes.c_void_p, ctypes.c_char_p,
                                 ctypes.c_void_p, ctypes.c_size_t)
+# glx_reduce_fn: (user, c, a, b, n)
+REDUCE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.c_void_p, ctypes.c_size_t)
 
 # status codes (glx_status), and GLX_NOT_READY of glx_event_query
 OK, ERR_INVALID, ERR_HIP, ERR_TIMEOUT, ERR_IO, ERR_ENFORCE, ERR_INTERNAL, NOT_READY = range(8)

@@ -25,20 +25,35 @@ class ReductionType:
     PRODUCT = 2
     MAX = 3
     MIN = 4
+    CUSTOM = 1000
 
 
 class ReductionFunction:
-    """gloo::ReductionFunction<T> singletons (gloo/algorithm.h:59-96).  The
-    element type comes from the buffers, so one object serves every T."""
+    """gloo::ReductionFunction<T> (gloo/algorithm.h:59-96).  The singletons
+    sum / product / max / min serve every element type (it comes from the
+    buffers).  ReductionFunction(ReductionType.CUSTOM, fn) wraps a caller's
+    fn(x, y, n) -- addresses of x and y, n elements, x = f(x, y) in place,
+    the reference's Function(T* x, const T* y, size_t n) -- which runs on the
+    host: such an algorithm needs host buffers (glx_allreduce_create_host_fn)."""
 
-    def __init__(self, type_):
+    def __init__(self, type_, fn=None):
+        if type_ == ReductionType.CUSTOM:
+            if not callable(fn):
+                raise TypeError("a CUSTOM ReductionFunction needs a callable fn(x, y, n)")
+        elif fn is not None:
+            raise TypeError("only a CUSTOM ReductionFunction takes a function")
         self._type = type_
+        self.fn = fn
 
     def type(self):
         return self._type
 
+    def call(self, x, y, n):
+        """x = f(x, y) over n elements at addresses x, y (CUSTOM only)."""
+        self.fn(x, y, n)
+
     def __repr__(self):
-        names = {1: "sum", 2: "product", 3: "max", 4: "min"}
+        names = {1: "sum", 2: "product", 3: "max", 4: "min", 1000: "custom"}
         return "ReductionFunction.%s" % names[self._type]
 
 
@@ -169,6 +184,10 @@ class Algorithm:
         self.dtype = dt
         self.fn = fn
         arr = (ctypes.c_void_p * len(pp))(*pp)
+        self._hostfn = None
+        if fn.type() == ReductionType.CUSTOM:
+            self._create_custom(context, arr, len(pp), dt, fn, streams)
+            return
         if streams:
             sp = [_stream_ptr(s) for s in streams]
             sarr = (ctypes.c_void_p * len(sp))(*sp)
@@ -180,8 +199,35 @@ class Algorithm:
             self._create(context.handle, arr, len(pp), self.count, dt, fn.type(), sarr, ns),
             type(self).__name__)
 
+    def _create_custom(self, context, arr, nptrs, dt, fn, streams):
+        """A CUSTOM function: the algorithm's program runs on the host over
+        host buffers (glx_allreduce_create_host_fn), calling fn.call(x, y, n)
+        where the reference calls fn_->call (x is also the output)."""
+        if streams:
+            raise ValueError("a CUSTOM reduction function runs on the host: no streams")
+        errors = []
+
+        def trampoline(user, c, a, b, n):
+            if errors:
+                return
+            try:
+                fn.call(c, b, n)  # c == a: x = f(x, y)
+            except BaseException as e:  # noqa: BLE001 - re-raised by run()
+                errors.append(e)
+        self._hostfn = (_lib.REDUCE_FN(trampoline), errors)
+        self._h = check_handle(
+            lib.glx_allreduce_create_host_fn(
+                context.handle, self._algo, arr, nptrs, self.count, lib.glx_dtype_size(dt),
+                ctypes.cast(self._hostfn[0], ctypes.c_void_p), None),
+            type(self).__name__)
+
     def run(self):
-        check(lib.glx_algorithm_run(self._h), type(self).__name__ + ".run")
+        rc = lib.glx_algorithm_run(self._h)
+        if self._hostfn is not None and self._hostfn[1]:
+            e = self._hostfn[1][0]
+            del self._hostfn[1][:]
+            raise e
+        check(rc, type(self).__name__ + ".run")
 
     def run_fed(self):
         """run() on a host buffer that is still being filled (by a transport
@@ -221,7 +267,7 @@ class Algorithm:
         rank), "dmasteps" (the host-issued steps' copies and reduce launches,
         their hand-offs made on the GPU by flag kernels)."""
         return {0: "steps", 1: "oneshot", 2: "twoshot", 3: "devsteps",
-                4: "dmasteps"}[lib.glx_algorithm_engine(self._h)]
+                4: "dmasteps", 5: "hostfn"}[lib.glx_algorithm_engine(self._h)]
 
     def fast_streams(self):
         """True when the plan kernel runs nontemporal loads and write-through

@@ -173,9 +173,7 @@ def allreduce(opts):
         sync.synchronize()
 
 
-# glx.h glx_reduce_fn: (user, c, a, b, n)
-_REDUCE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                              ctypes.c_void_p, ctypes.c_size_t)
+_REDUCE_FN = _lib.REDUCE_FN  # glx.h glx_reduce_fn: (user, c, a, b, n)
 
 
 def _allreduce_host_fn(opts):

@@ -28,6 +28,12 @@ struct glx_context {
 };
 struct glx_algorithm {
   std::unique_ptr<gloo::HipPlanExecutor> a;
+  // or a class algorithm with a caller's function on host buffers
+  // (glx_allreduce_create_host_fn): the executor, its buffers and function
+  std::shared_ptr<gloo::HostFnExecutor> hostFn;
+  std::vector<void*> ptrs;
+  glx_reduce_fn fn = nullptr;
+  void* user = nullptr;
 };
 struct glx_link_probe {
   std::unique_ptr<gloo::LinkProbe> p;
@@ -567,26 +573,80 @@ int glx_allreduce_host_fn(glx_context* ctx, int algorithm, size_t element_size,
   });
 }
 
+glx_algorithm* glx_allreduce_create_host_fn(glx_context* ctx, int algo, void* const* ptrs,
+                                            int nptrs, int count, size_t element_size,
+                                            glx_reduce_fn fn, void* user) {
+  glx_algorithm* out = nullptr;
+  guarded([&]() -> int {
+    GLX_ENFORCE(ctx != nullptr, "null context");
+    GLX_ENFORCE(ptrs != nullptr && nptrs > 0, "need at least one pointer");
+    GLX_ENFORCE(count >= 0, "negative element count");
+    GLX_ENFORCE(fn != nullptr, "null reduction function");
+    GLX_ENFORCE(element_size > 0 && element_size <= ((size_t)1 << 20), "bad element size");
+    // every ring_chunked schedule computes the reference ring's bits: the
+    // host runs the ring's own program
+    int a = -1;
+    if (algo == GLX_ALGO_RING_CHUNKED || algo == GLX_ALGO_RING_CHUNKED_MESH ||
+        algo == GLX_ALGO_RING_CHUNKED_REPL || algo == GLX_ALGO_RING_CHUNKED_AUTO) {
+      a = glx::ALGO_RING_CHUNKED;
+    } else if (algo == GLX_ALGO_HALVING_DOUBLING) {
+      a = glx::ALGO_HALVING_DOUBLING;
+    }
+    GLX_ENFORCE(a >= 0,
+                "a CUSTOM reduction function runs with AllreduceRingChunked or "
+                "AllreduceHalvingDoubling (algorithm ", algo, ")");
+    std::vector<void*> p(ptrs, ptrs + nptrs);
+    for (const void* q : p) {
+      GLX_ENFORCE(q != nullptr, "null pointer");
+      GLX_ENFORCE(gloo::exec::isHostPointer(q),
+                  "a CUSTOM reduction function needs host buffers (a device cannot run "
+                  "it); device buffers take SUM, PRODUCT, MAX or MIN");
+    }
+    auto& c = *ctx->c;
+    GLX_ENFORCE(c.size == 1 || c.connected(),
+                "allreduce: context must be connected (connectFullMesh)");
+    out = new glx_algorithm{};
+    out->hostFn = std::make_shared<gloo::HostFnExecutor>(ctx->c, a, element_size,
+                                                         (size_t)count, 0);
+    out->ptrs = std::move(p);
+    out->fn = fn;
+    out->user = user;
+    return GLX_OK;
+  });
+  return out;
+}
+
 int glx_algorithm_run(glx_algorithm* alg) {
   return guarded([&]() -> int {
     GLX_ENFORCE(alg != nullptr, "null algorithm");
+    if (alg->hostFn) {
+      alg->hostFn->call(alg->fn, alg->user, {}, alg->ptrs, std::chrono::milliseconds(0));
+      return GLX_OK;
+    }
     alg->a->run();
     return GLX_OK;
   });
 }
 
+namespace {
+gloo::HipPlanExecutor& planExecutor(glx_algorithm* alg, const char* what) {
+  GLX_ENFORCE(alg != nullptr, "null algorithm");
+  GLX_ENFORCE(alg->a != nullptr, what, ": not available for an algorithm with a CUSTOM "
+              "reduction function (it runs on the host)");
+  return *alg->a;
+}
+}  // namespace
+
 int glx_algorithm_run_fed(glx_algorithm* alg) {
   return guarded([&]() -> int {
-    GLX_ENFORCE(alg != nullptr, "null algorithm");
-    alg->a->runFed();
+    planExecutor(alg, "run_fed").runFed();
     return GLX_OK;
   });
 }
 
 int glx_algorithm_feed(glx_algorithm* alg, int64_t off, int64_t len) {
   return guarded([&]() -> int {
-    GLX_ENFORCE(alg != nullptr, "null algorithm");
-    alg->a->feed(off, len);
+    planExecutor(alg, "feed").feed(off, len);
     return GLX_OK;
   });
 }
@@ -594,8 +654,7 @@ int glx_algorithm_feed(glx_algorithm* alg, int64_t off, int64_t len) {
 int64_t glx_algorithm_done_ranges(glx_algorithm* alg, int64_t* out, int64_t cap) {
   int64_t n = -1;
   guarded([&]() -> int {
-    GLX_ENFORCE(alg != nullptr, "null algorithm");
-    const std::vector<glx::Range> r = alg->a->doneRanges();
+    const std::vector<glx::Range> r = planExecutor(alg, "done_ranges").doneRanges();
     n = (int64_t)r.size();
     for (int64_t i = 0; i < n && i < cap && out != nullptr; i++) {
       out[2 * i] = r[(size_t)i].off;
@@ -607,12 +666,12 @@ int64_t glx_algorithm_done_ranges(glx_algorithm* alg, int64_t* out, int64_t cap)
 }
 
 int64_t glx_algorithm_bytes_sent(glx_algorithm* alg) {
-  return alg ? alg->a->bytesSentPerRun() : -1;
+  return alg && alg->a ? alg->a->bytesSentPerRun() : -1;
 }
 
 int glx_algorithm_engine(glx_algorithm* alg) {
   if (alg == nullptr) return -1;
-  return alg->a->engine();
+  return alg->a ? alg->a->engine() : GLX_ENGINE_HOSTFN;
 }
 
 int glx_set_device_sync(int mode) {
@@ -621,16 +680,22 @@ int glx_set_device_sync(int mode) {
   return GLX_OK;
 }
 
-int glx_algorithm_sync(glx_algorithm* alg) { return alg != nullptr ? alg->a->syncMode() : -1; }
+int glx_algorithm_sync(glx_algorithm* alg) {
+  return alg != nullptr && alg->a ? alg->a->syncMode() : -1;
+}
 
 int glx_algorithm_fast_streams(glx_algorithm* alg) {
-  return alg != nullptr && alg->a->fastStreams() ? 1 : 0;
+  return alg != nullptr && alg->a && alg->a->fastStreams() ? 1 : 0;
 }
 
 int glx_algorithm_transport_stats(glx_algorithm* alg, int64_t* out, int cap) {
   if (alg == nullptr || out == nullptr || cap < 6) {
     fail(GLX_ERR_INVALID, "glx_algorithm_transport_stats: null algorithm/output or cap < 6");
     return -1;
+  }
+  if (!alg->a) {  // a host-function algorithm moves nothing over the links
+    for (int i = 0; i < cap && i < 8; i++) out[i] = 0;
+    return cap < 8 ? cap : 8;
   }
   const auto& t = alg->a->transportStats();
   out[0] = t.peerCopies;
@@ -648,8 +713,8 @@ int glx_algorithm_transport_stats(glx_algorithm* alg, int64_t* out, int cap) {
 
 int glx_algorithm_record(glx_algorithm* alg, glx_event_t ev) {
   return guarded([&]() -> int {
-    GLX_ENFORCE(alg != nullptr && ev != nullptr, "null algorithm/event");
-    alg->a->recordDone((hipEvent_t)ev);
+    GLX_ENFORCE(ev != nullptr, "null event");
+    planExecutor(alg, "record").recordDone((hipEvent_t)ev);
     return GLX_OK;
   });
 }

@@ -60,8 +60,10 @@ char* mapShm(const std::string& name, size_t bytes, bool create) {
 HostFnExecutor::HostFnExecutor(const std::shared_ptr<Context>& ctx, int algo,
                                size_t elementSize, size_t elements, size_t maxSegmentBytes)
     : Algorithm(ctx), algo_(algo), es_(elementSize), elements_(elements) {
-  GLX_ENFORCE(algo == glx::ALGO_FN_RING || algo == glx::ALGO_FN_BCUBE,
-              "host-fn allreduce: RING or BCUBE");
+  const bool cls = algo == glx::ALGO_RING_CHUNKED || algo == glx::ALGO_HALVING_DOUBLING;
+  GLX_ENFORCE(algo == glx::ALGO_FN_RING || algo == glx::ALGO_FN_BCUBE || cls,
+              "host-fn allreduce: RING or BCUBE, or the class ring_chunked / "
+              "halving_doubling");
   GLX_ENFORCE(es_ > 0 && es_ <= (size_t(1) << 20), "host-fn allreduce: bad element size ", es_);
   glx::PlanParams prm;
   prm.esize = (int)es_;
@@ -71,6 +73,9 @@ HostFnExecutor::HostFnExecutor(const std::shared_ptr<Context>& ctx, int algo,
   for (const auto& s : plan_.steps) {
     GLX_ENFORCE(s.kind != glx::FOLD || (s.flags & glx::kFoldWhole) == 0,
                 "host-fn allreduce: whole-buffer folds are not expected here");
+    // a class algorithm's function is x = f(x, y) (host_fn.h): its programs
+    // reduce in place only
+    GLX_ENFORCE(!cls || s.kind != glx::FOLD, "host-fn allreduce: a class program folds");
   }
   slot_ = ctx->nextSlot();
   regionBytes_ = std::max<size_t>(64, (size_t)plan_.scratch_elems * es_ + 64);

@@ -14,6 +14,15 @@
 // caller's function, COPY = memcpy.  Bits equal the reference's for any
 // function (tests/golden/allreduce_custom_golden.*, made by the reference
 // itself).  Device buffers with such a function are refused (glx.h).
+//
+// The class algorithms AllreduceRingChunked<T> / AllreduceHalvingDoubling<T>
+// with a ReductionFunction<T> of type CUSTOM (gloo/algorithm.h:58-83) run the
+// same way over their own programs (plan.h planRingChunked /
+// planHalvingDoubling): their function is x = f(x, y) in place
+// (allreduce_ring_chunked.h:89-99,141-157; allreduce_halving_doubling.h:
+// 231-273), which is this executor's call with c == a -- the local
+// multi-pointer fold, every REDUCE step, and no FOLD step in those programs
+// (tests/golden/allreduce_class_custom_golden.*).
 #pragma once
 
 #include <chrono>
@@ -33,7 +42,10 @@ using HostReduceFn = void (*)(void* user, void* c, const void* a, const void* b,
 
 class HostFnExecutor : public Algorithm {
  public:
-  // algo: glx::ALGO_FN_RING or glx::ALGO_FN_BCUBE.  Built on the first call
+  // algo: glx::ALGO_FN_RING or glx::ALGO_FN_BCUBE (built on the first call
+  // ...), or glx::ALGO_RING_CHUNKED / ALGO_HALVING_DOUBLING (a class
+  // algorithm: built by its constructor, capi.cc glx_allreduce_create_host_fn,
+  // maxSegmentBytes unused).  Function-style: built on the first call
   // of a (schedule, element size, elements, tag, maxSegmentSize) and kept in
   // the context (collectives.cc's rule: every rank makes the same calls).
   HostFnExecutor(const std::shared_ptr<Context>& ctx, int algo, size_t elementSize,

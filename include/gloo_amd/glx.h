@@ -426,6 +426,25 @@ int glx_allreduce_host_fn(glx_context* ctx, int algorithm, size_t element_size,
                           void* const* outputs, int num_outputs, size_t elements, uint32_t tag,
                           size_t max_segment_size, int64_t timeout_ms);
 
+/* The class algorithms with a ReductionFunction<T> of type CUSTOM
+ * (gloo/algorithm.h:56,58-83: Function(T* x, const T* y, n), x = f(x, y) in
+ * place) -- replaces gloo::AllreduceRingChunked<T>(context, ptrs, count, fn)
+ * (gloo/allreduce_ring_chunked.h:22-26) and gloo::AllreduceHalvingDoubling<T>
+ * (gloo/allreduce_halving_doubling.h:67-81) with such an fn.  A device cannot
+ * run a host function, so the buffers must be HOST memory: the algorithm's
+ * program runs on the host (shared-memory messages, the context's counters),
+ * calling fn(user, x, x, y, n) exactly where the reference calls fn_->call(x,
+ * y, n) -- the local fold of ptrs[1..] into ptrs[0], every reduce-scatter
+ * step -- so the result bits are the reference's for any function.  algo:
+ * GLX_ALGO_RING_CHUNKED (any of its schedules: the ring's program) or
+ * GLX_ALGO_HALVING_DOUBLING.  Created in the same order on every rank (it
+ * takes a context slot, like the others); glx_algorithm_run runs it;
+ * run_fed / feed / done_ranges / record are not available (GLX_ERR_ENFORCE),
+ * glx_algorithm_engine returns GLX_ENGINE_HOSTFN.  NULL on error. */
+glx_algorithm* glx_allreduce_create_host_fn(glx_context* ctx, int algo, void* const* ptrs,
+                                            int nptrs, int count, size_t element_size,
+                                            glx_reduce_fn fn, void* user);
+
 /* Algorithm::run() (gloo/algorithm.h:26).  With streams and the
  * GLX_ENGINE_DMASTEPS engine the call only enqueues (copies, reduce and flag
  * kernels on streams[0] and the algorithm's copy streams; message numbers
@@ -490,6 +509,9 @@ int64_t glx_algorithm_bytes_sent(glx_algorithm* alg);
  * flag kernel on the waiting stream, every counter a flag word written by
  * one, instead of the host's progress loop (glx_set_steps_engine). */
 #define GLX_ENGINE_DMASTEPS 4
+/* GLX_ENGINE_HOSTFN = a class algorithm with a CUSTOM reduction function on
+ * host buffers (glx_allreduce_create_host_fn): its program run on the host. */
+#define GLX_ENGINE_HOSTFN 5
 int glx_algorithm_engine(glx_algorithm* alg);
 /* 1 when the algorithm's plan kernel runs nontemporal loads and write-through
  * stores (glx_set_engine_streams), else 0. */

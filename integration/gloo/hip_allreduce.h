@@ -34,8 +34,11 @@
 // the element count, optional streams (outputs valid once streams[0] reaches
 // the end of run(); without streams, when run() returns -- docs/cuda.md:9-11)
 // and a gloo::ReductionFunction<T> accepted by its type() (SUM, PRODUCT, MAX,
-// MIN; the reference's accelerated paths do the same, gloo/algorithm.h:40-48:
-// a CUSTOM function cannot run on the device and is refused).
+// MIN run on the device; the reference's accelerated paths do the same,
+// gloo/algorithm.h:40-48).  A CUSTOM function cannot run on the device: with
+// HOST buffers the ring-chunked and halving-doubling classes run their
+// program on the host, calling it exactly where the reference's CPU classes
+// do (glx_allreduce_create_host_fn); with device buffers it is refused.
 //
 // The constructors are the CUDA ones, argument for argument (plus the
 // optional ReductionFunction of the CPU algorithms).  The xGMI transport
@@ -397,15 +400,35 @@ inline int deviceOf(const void* p) {
   return d;
 }
 
+// A class algorithm's ReductionFunction<T> of type CUSTOM through
+// glx_reduce_fn: the reference calls fn_->call(x, y, n), x = f(x, y); the
+// host-run program calls (c = x, a = x, b = y).  The first exception the
+// function throws is kept (never unwound through the C ABI) and rethrown
+// by run().
+template <typename T>
+struct ClassFnCall {
+  const ReductionFunction<T>* fn;
+  std::exception_ptr error;
+  static void trampoline(void* user, void* c, const void* /*a == c*/, const void* b, size_t n) {
+    ClassFnCall* call = static_cast<ClassFnCall*>(user);
+    if (call->error) return;
+    try {
+      call->fn->call(static_cast<T*>(c), static_cast<const T*>(b), n);
+    } catch (...) {
+      call->error = std::current_exception();
+    }
+  }
+};
+
 template <typename T>
 class Allreduce : public Algorithm {
  public:
   void run() override {
     if (ran_) {
-      check(glx_algorithm_run(alg_), "run");
+      runOnce();
       return;
     }
-    xgmi_->firstRun([&] { check(glx_algorithm_run(alg_), "run"); });
+    xgmi_->firstRun([&] { runOnce(); });
     ran_ = true;
   }
   ~Allreduce() override { glx_algorithm_destroy(alg_); }
@@ -425,6 +448,18 @@ class Allreduce : public Algorithm {
     check(glx_context_set_base(xgmi_->get(), std::max(2, context->base)), "base");
     std::vector<void*> p(ptrs.begin(), ptrs.end());
     std::vector<glx_stream_t> s(streams.begin(), streams.end());
+    GLOO_ENFORCE(fn != nullptr, "null reduction function");
+    if (fn->type() == CUSTOM) {
+      // a host function: host buffers, the algorithm's program run on the
+      // host (glx_allreduce_create_host_fn; device buffers are refused there)
+      GLOO_ENFORCE(s.empty(), "HIP allreduce: a CUSTOM reduction function runs on the host, "
+                   "with host buffers; there are no streams to order it on");
+      custom_.reset(new ClassFnCall<T>{fn, nullptr});
+      alg_ = glx_allreduce_create_host_fn(xgmi_->get(), algo, p.data(), (int)p.size(), count,
+                                          sizeof(T), &ClassFnCall<T>::trampoline, custom_.get());
+      GLOO_ENFORCE(alg_ != nullptr, "glx_allreduce_create_host_fn: ", glx_last_error());
+      return;
+    }
     alg_ = glx_allreduce_create(xgmi_->get(), algo, p.data(), (int)p.size(), count,
                                 GlxType<T>::value, glxOp(fn), s.empty() ? nullptr : s.data(),
                                 (int)s.size());
@@ -432,8 +467,19 @@ class Allreduce : public Algorithm {
   }
 
  private:
+  void runOnce() {
+    const int rc = glx_algorithm_run(alg_);
+    if (custom_ && custom_->error) {
+      std::exception_ptr e = custom_->error;
+      custom_->error = nullptr;
+      std::rethrow_exception(e);
+    }
+    check(rc, "run");
+  }
+
   std::shared_ptr<XgmiContext> xgmi_;
   glx_algorithm* alg_ = nullptr;
+  std::unique_ptr<ClassFnCall<T>> custom_;
   bool ran_ = false;
 };
 

@@ -64,6 +64,14 @@ void custom3aPlusB(void* c, const void* a, const void* b, size_t n) {
   for (size_t i = 0; i < n; i++) z[i] = 3u * x[i] + y[i];
 }
 
+// The same two functions as ReductionFunction<T>s of type CUSTOM for the
+// class algorithms (gloo/algorithm.h:58-83: Function(T* x, const T* y, n),
+// x = f(x, y) in place), over 4-byte T.
+template <typename T>
+void classOr(T* x, const T* y, size_t n) { customOr(x, x, y, n); }
+template <typename T>
+void class3aPlusB(T* x, const T* y, size_t n) { custom3aPlusB(x, x, y, n); }
+
 thread_local std::string g_err;
 
 template <typename T>
@@ -84,6 +92,12 @@ const gloo::ReductionFunction<T>* fnFor(int op) {
     case R_PRODUCT: return gloo::ReductionFunction<T>::product;
     case R_MAX: return gloo::ReductionFunction<T>::max;
     case R_MIN: return gloo::ReductionFunction<T>::min;
+  }
+  if constexpr (sizeof(T) == 4) {
+    static const gloo::ReductionFunction<T> orFn(gloo::CUSTOM, &classOr<T>);
+    static const gloo::ReductionFunction<T> threeAPlusBFn(gloo::CUSTOM, &class3aPlusB<T>);
+    if (op == R_CUSTOM_OR) return &orFn;
+    if (op == R_CUSTOM_3A_PLUS_B) return &threeAPlusBFn;
   }
   return nullptr;
 }
@@ -297,7 +311,8 @@ void ref_f16_to_f32(const uint16_t* in, float* out, size_t n) {
 void ref_set_bcube_base(int base) { g_bcube_base = base; }
 
 // algo: 0 = AllreduceRingChunked, 1 = AllreduceHalvingDoubling, 9 = AllreduceRing,
-// 10 = AllreduceBcube (base: ref_set_bcube_base).
+// 10 = AllreduceBcube (base: ref_set_bcube_base).  op: R_SUM..R_MIN, or the
+// CUSTOM functions R_CUSTOM_OR / R_CUSTOM_3A_PLUS_B for 4-byte types.
 
 int ref_allreduce(int algo, int op, int dtype, int P, int nptrs, int count,
                   void** bufs, int warmup, int iters, double* seconds) {

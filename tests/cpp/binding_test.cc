@@ -6,7 +6,9 @@
 // binding` into oracle/_ref/binding_test.
 //
 //   binding_test cpu   no GPU: type / reduction-type mapping, CUSTOM refused
-//                      with gloo::EnforceNotMet, the store bridge both ways
+//                      on the device with gloo::EnforceNotMet and run on
+//                      host buffers against the reference's own classes and
+//                      gloo::allreduce, the store bridge both ways
 //                      the endpoint exchange over the gloo context itself
 //                      (ContextStore: gloo::allgather on the tcp pairs)
 //   binding_test gpu   P thread-ranks on one GPU bootstrapped exactly like
@@ -92,6 +94,7 @@ void spawn(int P, const std::function<void(std::shared_ptr<gloo::Context>,
 
 void compareCustom(int P, int count, int nin, int nout, gloo::AllreduceOptions::Algorithm algo,
                    size_t maxSeg);
+void compareClassCustom(int P, int count, int nptrs, bool hd);
 
 void spawnCpu2(const std::function<void(std::shared_ptr<gloo::Context>,
                                         gloo::rendezvous::Store&, int)>& fn) {
@@ -253,6 +256,12 @@ int cpuMode() {
     compareCustom(2, 1000, 0, 1, algo, 0);
     compareCustom(3, 4099, 2, 1, algo, 1024);
     compareCustom(4, 65537, 1, 2, algo, 0);
+  }
+  // the class algorithms with a CUSTOM ReductionFunction on host buffers
+  for (bool hd : {false, true}) {
+    compareClassCustom(2, 1000, 1, hd);
+    compareClassCustom(3, 4099, 2, hd);
+    compareClassCustom(5, 65537, 1, hd);
   }
   std::printf("binding_test cpu: %s\n", failures ? "FAILED" : "OK");
   return failures ? 1 : 0;
@@ -533,6 +542,65 @@ void compareCustom(int P, int count, int nin, int nout, gloo::AllreduceOptions::
   std::printf("custom Func (host) %s P=%d count=%d in=%d out=%d seg=%zu: %s\n",
               algo == gloo::AllreduceOptions::Algorithm::BCUBE ? "bcube" : "ring", P, count,
               nin, nout, maxSeg, bad ? "MISMATCH" : "ok");
+}
+
+// HipAllreduceRingChunked / HipAllreduceHalvingDoubling with a CUSTOM
+// ReductionFunction<int32_t> (gloo/algorithm.h:56,58-83; x = 3x + y over
+// 32-bit words, neither commutative nor associative) on HOST buffers,
+// against the reference's own AllreduceRingChunked / AllreduceHalvingDoubling
+// with the same function on copies of the same inputs.  Two runs of the
+// HIP instance.
+void classTimes3Plus(int32_t* x, const int32_t* y, size_t n) {
+  for (size_t i = 0; i < n; i++) x[i] = (int32_t)(3u * (uint32_t)x[i] + (uint32_t)y[i]);
+}
+
+void compareClassCustom(int P, int count, int nptrs, bool hd) {
+  using T = int32_t;
+  static const gloo::ReductionFunction<T> fn(gloo::CUSTOM, &classTimes3Plus);
+  std::vector<std::vector<std::vector<T>>> init(P), ref(P), got(P);
+  for (int r = 0; r < P; r++) {
+    for (int j = 0; j < nptrs; j++) {
+      std::vector<T> v((size_t)count);
+      for (int i = 0; i < count; i++) v[(size_t)i] = value<T>(r * 8 + j, (size_t)i);
+      init[r].push_back(v);
+    }
+  }
+  auto run = [&](bool hip, std::vector<std::vector<std::vector<T>>>& outs) {
+    spawn(P, [&](std::shared_ptr<gloo::Context> ctx, gloo::rendezvous::Store&, int r) {
+      std::vector<T*> ptrs;
+      outs[r] = init[r];
+      for (auto& v : outs[r]) ptrs.push_back(v.data());
+      std::unique_ptr<gloo::Algorithm> a;
+      if (hip && hd) {
+        a.reset(new gloo::HipAllreduceHalvingDoubling<T>(ctx, ptrs, count, {}, &fn));
+      } else if (hip) {
+        a.reset(new gloo::HipAllreduceRingChunked<T>(ctx, ptrs, count, {}, &fn));
+      } else if (hd) {
+        a.reset(new gloo::AllreduceHalvingDoubling<T>(ctx, ptrs, count, &fn));
+      } else {
+        a.reset(new gloo::AllreduceRingChunked<T>(ctx, ptrs, count, &fn));
+      }
+      for (int it = 0; it < (hip ? 2 : 1); it++) {
+        if (it > 0) {
+          for (int j = 0; j < nptrs; j++) outs[r][(size_t)j] = init[r][(size_t)j];
+        }
+        a->run();
+      }
+    });
+  };
+  run(false, ref);
+  run(true, got);
+  size_t bad = 0;
+  for (int r = 0; r < P; r++) {
+    for (int j = 0; j < nptrs; j++) {
+      bad += std::memcmp(got[r][(size_t)j].data(), ref[r][(size_t)j].data(),
+                         sizeof(T) * (size_t)count) != 0;
+    }
+  }
+  EXPECT(bad == 0, "CUSTOM ReductionFunction: %zu buffers differ from the reference", bad);
+  std::printf("CUSTOM ReductionFunction (host) %s P=%d count=%d ptrs=%d: %s\n",
+              hd ? "halving_doubling" : "ring_chunked", P, count, nptrs,
+              bad ? "MISMATCH" : "ok");
 }
 
 template <typename T>

@@ -447,6 +447,62 @@ def make_allreduce_custom():
     print("allreduce_custom: %d cases" % len(index))
 
 
+# ---- the class algorithms with a CUSTOM ReductionFunction<T> ---------------
+# gloo::AllreduceRingChunked<T> / AllreduceHalvingDoubling<T> constructed with
+# ReductionFunction<T>(CUSTOM, fn), fn(T* x, const T* y, n): x = f(x, y)
+# (gloo/algorithm.h:58-83) -- oracle/ref_harness.cc's classOr / class3aPlusB
+# over int32 words.  Host buffers; every pointer of every rank ends equal.
+CLASS_CUSTOM_CASES = []
+for _algo in (O.RING_CHUNKED, O.HALVING_DOUBLING):
+    for _op in (CUSTOM_OR, CUSTOM_3A_PLUS_B):
+        for _P in (1, 2, 3, 4, 5, 8):
+            for _N in (7, 1000, 4099):
+                for _np in (1, 2):
+                    CLASS_CUSTOM_CASES.append((_algo, _P, _N, _op, _np))
+        for _P in (3, 8):
+            CLASS_CUSTOM_CASES.append((_algo, _P, 100003, _op, 1))
+        CLASS_CUSTOM_CASES.append((_algo, 6, 4099, _op, 3))
+
+
+def class_custom_case_name(c):
+    algo, P, N, op, nptrs = c
+    return "%s_P%d_N%d_%s_p%d" % ("ring" if algo == O.RING_CHUNKED else "hd", P, N,
+                                  {CUSTOM_OR: "or", CUSTOM_3A_PLUS_B: "3a_plus_b"}[op], nptrs)
+
+
+def make_allreduce_class_custom():
+    out = {}
+    index = []
+    for c in CLASS_CUSTOM_CASES:
+        algo, P, N, op, nptrs = c
+        ins = case_inputs(P, N, O.INT32, nptrs, 0)
+        res = O.allreduce(algo, op, O.INT32, ins, use_ref=True)
+        first = res[0][0]
+        for r in range(P):
+            for i in range(nptrs):
+                assert np.array_equal(res[r][i], first), \
+                    "reference ranks disagree in %s" % class_custom_case_name(c)
+        name = class_custom_case_name(c)
+        index.append({"name": name, "algo": algo, "P": P, "N": N, "op": op, "nptrs": nptrs,
+                      "seed": SEED, "input_sha256": sha([x for row in ins for x in row]),
+                      "output_sha256": sha([first])})
+        if N <= 4099:
+            out[name] = first
+        else:
+            idx = np.linspace(0, N - 1, 257).astype(np.int64)
+            out[name + "_idx"] = idx
+            out[name + "_sample"] = first[idx]
+    np.savez_compressed(os.path.join(HERE, "allreduce_class_custom_golden.npz"), **out)
+    with open(os.path.join(HERE, "allreduce_class_custom_golden.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py (make_allreduce_class_custom)",
+                   "source": "gloo::AllreduceRingChunked<int32_t> / AllreduceHalvingDoubling"
+                             "<int32_t> with oracle/ref_harness.cc's CUSTOM ReductionFunctions "
+                             "(100: x | y, 101: 3x + y mod 2^32) of oracle/_ref/libgloo_ref.so "
+                             "(reference compiled from /root/reference by oracle/Makefile)",
+                   "cases": index}, f, indent=1)
+    print("allreduce_class_custom: %d cases" % len(index))
+
+
 # ---- BASELINE.json configs at full size (digests, not arrays) -------------
 # cfg3: ring_chunked fp32, 8 ranks, the 1K..16M element sweep;
 # cfg4: halving_doubling fp32, 8 ranks, 256 MiB per rank;
@@ -551,7 +607,7 @@ if __name__ == "__main__":
     if not O.ref_available():
         sys.exit("oracle/_ref/libgloo_ref.so missing: make -C oracle ref")
     which = sys.argv[1:] or ["reduce", "f16", "allreduce", "allreduce_fn", "ring", "bcube",
-                             "custom"]
+                             "custom", "class_custom"]
     if "reduce" in which:
         make_reduce()
     if "f16" in which:
@@ -566,6 +622,8 @@ if __name__ == "__main__":
         make_bcube()
     if "custom" in which:
         make_allreduce_custom()
+    if "class_custom" in which:
+        make_allreduce_class_custom()
     if "scale" in which:  # not in the default set: minutes and ~40 GiB of RAM
         make_scale()
     if "bench" in which:  # bench.py's N > 1 workloads (256 MiB fp32, P = 2, 4, 8)

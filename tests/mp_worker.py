@@ -65,6 +65,8 @@ def main():
         return run_dma_abort(store_dir, rank, size)
     if algo == "custom":
         return run_custom(store_dir, rank, size)
+    if algo == "class_custom":
+        return run_class_custom(store_dir, rank, size)
     if algo.startswith("killpeer:"):
         return run_killpeer(store_dir, rank, size, *algo.split(":")[1:])
     if algo == "devsteps":
@@ -238,6 +240,37 @@ def run_custom(store_dir, rank, size):
     barrier(store, rank, size, "custom")
     ctx.close()
     print("custom cases %d, wrong %s" % (n, bad[:5]))
+    if bad or n == 0:
+        print("MISMATCH rank", rank)
+        sys.exit(1)
+    print("OK")
+
+
+def run_class_custom(store_dir, rank, size):
+    """Every class-custom fixture case at P = size (tests/
+    test_allreduce_class_custom.py): AllreduceRingChunked /
+    AllreduceHalvingDoubling with a CUSTOM ReductionFunction on host buffers,
+    one process per rank, every pointer against the reference's output."""
+    import gloo_amd
+    from test_allreduce_class_custom import CASES, buffers, check_result, make_alg
+    store = gloo_amd.rendezvous.FileStore(store_dir)
+    ctx = gloo_amd.rendezvous.Context(rank, size, 0)
+    ctx.setTimeout(60)
+    ctx.connectFullMesh(store)
+    bad, n = [], 0
+    for c in CASES:
+        if c["P"] != size:
+            continue
+        bufs = buffers(c)[rank]
+        alg = make_alg(ctx, c, bufs)
+        alg.run()
+        alg.close()
+        n += 1
+        if not all(check_result(c, b) for b in bufs):
+            bad.append(c["name"])
+    barrier(store, rank, size, "class_custom")
+    ctx.close()
+    print("class custom cases %d, wrong %s" % (n, bad[:5]))
     if bad or n == 0:
         print("MISMATCH rank", rank)
         sys.exit(1)
