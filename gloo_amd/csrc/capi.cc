@@ -605,12 +605,13 @@ glx_algorithm* glx_allreduce_create_host_fn(glx_context* ctx, int algo, void* co
     auto& c = *ctx->c;
     GLX_ENFORCE(c.size == 1 || c.connected(),
                 "allreduce: context must be connected (connectFullMesh)");
-    out = new glx_algorithm{};
-    out->hostFn = std::make_shared<gloo::HostFnExecutor>(ctx->c, a, element_size,
-                                                         (size_t)count, 0);
-    out->ptrs = std::move(p);
-    out->fn = fn;
-    out->user = user;
+    auto h = std::make_unique<glx_algorithm>();
+    h->hostFn = std::make_shared<gloo::HostFnExecutor>(ctx->c, a, element_size,
+                                                       (size_t)count, 0);
+    h->ptrs = std::move(p);
+    h->fn = fn;
+    h->user = user;
+    out = h.release();
     return GLX_OK;
   });
   return out;

@@ -102,6 +102,24 @@ HostFnExecutor::HostFnExecutor(const std::shared_ptr<Context>& ctx, int algo,
 
 HostFnExecutor::~HostFnExecutor() noexcept(false) {
   auto& ctl = context_->localControl();
+  // every receiver's credit for our last message before our credit words go
+  // back to the control block: a credit landing late in a word a later
+  // algorithm was given would corrupt that algorithm's counts (a class
+  // algorithm can be freed and another created on the same context)
+  if (!broken_) {
+    const auto deadline = std::chrono::steady_clock::now() + context_->getTimeout();
+    try {
+      for (auto& c : out_) {
+        std::atomic<uint64_t>* credit = ctl.word(c.word);
+        while (credit->load(std::memory_order_acquire) < c.count &&
+               std::chrono::steady_clock::now() < deadline) {
+          context_->checkPeersAlive();  // throws if a peer exited: stop waiting
+          std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+      }
+    } catch (...) {
+    }
+  }
   for (auto& c : out_) ctl.freeWord(c.word);
   for (auto& c : in_) ctl.freeWord(c.word);
   for (size_t r = 0; r < peerRegion_.size(); r++) {
@@ -265,6 +283,9 @@ void HostFnExecutor::call(HostReduceFn fn, void* user, const std::vector<const v
   }
   if (contextSize_ > 1) {
     const auto wait = timeout.count() > 0 ? timeout : context_->getTimeout();
+    // a call that fails part-way leaves counts the peers never match: the
+    // destructor then does not wait for credits
+    broken_ = true;
     if (!resolved_) resolve();
     for (size_t i = 0; i < plan_.steps.size(); i++) {
       const glx::Step& s = plan_.steps[i];
@@ -329,6 +350,7 @@ void HostFnExecutor::call(HostReduceFn fn, void* user, const std::vector<const v
       ::shm_unlink(shmName_.c_str());
       unlinked_ = true;
     }
+    broken_ = false;
   }
   for (size_t i = 1; i < out.size(); i++) std::memcpy(out[i], out0, bytes);  // :87-96
   calls_++;

@@ -82,6 +82,7 @@ class HostFnExecutor : public Algorithm {
   size_t regionBytes_ = 0;
   bool unlinked_ = false;
   bool resolved_ = false;
+  bool broken_ = false;  // the last call failed part-way (no credit drain at destruction)
   uint64_t calls_ = 0;
   std::vector<Chan> out_, in_;
   std::vector<int> stepChan_;

@@ -128,6 +128,42 @@ def test_class_custom_function_runs_again_and_again():
             assert check_result(c, bufs[r][i])
 
 
+def test_class_custom_algorithms_created_and_freed_on_one_context():
+    """Churn on one context: each rank builds an algorithm, runs it, frees it
+    at once (no barrier) and builds the next, 30 times, alternating schedules
+    and sizes.  A freed executor's counter words go back to the context and
+    the next algorithm gets them: every receiver's last credit must have
+    landed first (HostFnExecutor's destructor), else a late credit corrupts
+    the next algorithm's counts.  Every run equals the reference's bits
+    (the fixtures' cases at P = 4)."""
+    cases = [c for c in CASES if c["P"] == 4]
+    P = 4
+    store = gloo_amd.rendezvous.HashStore()
+    errs, bad = [], []
+
+    def body(r):
+        try:
+            ctx = gloo_amd.rendezvous.Context(r, P)
+            ctx.setTimeout(60)
+            ctx.connectFullMesh(store)
+            for k in range(30):
+                c = cases[(k * 7) % len(cases)]
+                bufs = buffers(c)[r]
+                alg = make_alg(ctx, c, bufs)
+                alg.run()
+                alg.close()
+                if not all(check_result(c, b) for b in bufs):
+                    bad.append((r, k, c["name"]))
+            ctx.close()
+        except BaseException as e:  # noqa: BLE001
+            errs.append((r, e))
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(P)]
+    [t.start() for t in ts]
+    [t.join(300) for t in ts]
+    assert not errs, errs
+    assert not bad, bad[:5]
+
+
 def test_class_custom_function_on_device_buffers_is_refused():
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
