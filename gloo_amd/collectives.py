@@ -116,6 +116,11 @@ class AllreduceOptions:
         callable fn(c, a, b, n) on raw addresses (the reference's Func)."""
         self.custom = None
         if isinstance(fn, ReductionFunction):
+            if fn.type() not in (1, 2, 3, 4):
+                raise EnforceNotMet(
+                    "a CUSTOM ReductionFunction is a class algorithm's x = f(x, y); "
+                    "gloo::allreduce takes the reference's Func: pass a callable "
+                    "fn(c, a, b, n)")
             self.op = fn.type()
         elif isinstance(fn, int) and 1 <= fn <= 4:
             self.op = fn

@@ -185,6 +185,9 @@ def test_class_custom_function_refusals():
         gloo_amd.AllreduceHalvingDoubling(ctx, [x], fn=class_fn(OR), streams=[0])
     with pytest.raises(TypeError):
         ReductionFunction(ReductionType.CUSTOM, None)
+    opts = gloo_amd.AllreduceOptions(ctx)
+    with pytest.raises(gloo_amd.EnforceNotMet, match="callable fn"):
+        opts.setReduceFunction(class_fn(OR))  # the function style takes a Func
     alg = gloo_amd.AllreduceRingChunked(ctx, [x], fn=class_fn(OR))
     with pytest.raises(gloo_amd.EnforceNotMet, match="runs on the host"):
         alg.run_fed()
