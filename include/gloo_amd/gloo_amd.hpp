@@ -20,6 +20,8 @@
 #include <chrono>
 #include <cstdint>
 #include <algorithm>
+#include <exception>
+#include <functional>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -91,14 +93,40 @@ template <> struct DType<double> { static constexpr int value = GLX_FLOAT64; };
 template <> struct DType<float16> { static constexpr int value = GLX_FLOAT16; };
 template <> struct DType<bfloat16> { static constexpr int value = GLX_BFLOAT16; };
 
-enum ReductionType { SUM = GLX_SUM, PRODUCT = GLX_PRODUCT, MAX = GLX_MAX, MIN = GLX_MIN };
+// The glx dtype of T, or -1 for an element type the device ops do not have
+// (a caller's host Func takes any T, as the reference's does).
+template <typename T, typename = void>
+struct DTypeOrNone {
+  static constexpr int value = -1;
+};
+template <typename T>
+struct DTypeOrNone<T, std::void_t<decltype(DType<T>::value)>> {
+  static constexpr int value = DType<T>::value;
+};
 
-// gloo::ReductionFunction<T>: the device kernel is selected by type().
+enum ReductionType {
+  SUM = GLX_SUM,
+  PRODUCT = GLX_PRODUCT,
+  MAX = GLX_MAX,
+  MIN = GLX_MIN,
+  CUSTOM = 1000  // gloo/algorithm.h:56
+};
+
+// gloo::ReductionFunction<T> (gloo/algorithm.h:58-83): the device kernel is
+// selected by type(); a CUSTOM one carries the caller's fn(x, y, n), x =
+// f(x, y), which runs on the host -- the ring-chunked and halving-doubling
+// classes then need host buffers (glx_allreduce_create_host_fn).
 template <typename T>
 class ReductionFunction {
  public:
-  explicit ReductionFunction(ReductionType t) : type_(t) {}
+  using Function = void(T*, const T*, size_t n);
+  explicit ReductionFunction(ReductionType t, Function* fn = nullptr) : type_(t), fn_(fn) {
+    if ((t == CUSTOM) != (fn != nullptr)) {
+      throw EnforceNotMet("ReductionFunction: a function goes with CUSTOM, and only there");
+    }
+  }
   ReductionType type() const { return type_; }
+  void call(T* x, const T* y, size_t n) const { fn_(x, y, n); }
   static const ReductionFunction<T>* sum;
   static const ReductionFunction<T>* product;
   static const ReductionFunction<T>* min;
@@ -106,6 +134,7 @@ class ReductionFunction {
 
  private:
   ReductionType type_;
+  Function* fn_;
 };
 template <typename T>
 const ReductionFunction<T>* ReductionFunction<T>::sum = new ReductionFunction<T>(SUM);
@@ -255,11 +284,30 @@ class DeviceAllreduce : public Algorithm {
  protected:
   using Create = glx_algorithm* (*)(glx_context*, void* const*, int, int, int, int,
                                     const glx_stream_t*, int);
+  // customAlgo: the glx algorithm a CUSTOM function runs as on host buffers
+  // (GLX_ALGO_RING_CHUNKED / _HALVING_DOUBLING; -1: refused)
   DeviceAllreduce(Create create, const std::shared_ptr<Context>& ctx,
                   const std::vector<T*>& ptrs, int count,
-                  const std::vector<glx_stream_t>& streams, const ReductionFunction<T>* fn)
+                  const std::vector<glx_stream_t>& streams, const ReductionFunction<T>* fn,
+                  int customAlgo = -1)
       : Algorithm(ctx) {
     std::vector<void*> p(ptrs.begin(), ptrs.end());
+    if (fn == nullptr) throw EnforceNotMet("allreduce: null reduction function");
+    if (fn->type() == CUSTOM) {
+      if (customAlgo < 0) {
+        throw EnforceNotMet("a CUSTOM reduction function runs with HipAllreduceRingChunked or "
+                            "HipAllreduceHalvingDoubling on host buffers");
+      }
+      if (!streams.empty()) {
+        throw EnforceNotMet("a CUSTOM reduction function runs on the host: no streams");
+      }
+      custom_.reset(new CustomCall{fn, nullptr});
+      a_ = checkHandle(glx_allreduce_create_host_fn(ctx->handle(), customAlgo, p.data(),
+                                                    (int)p.size(), count, sizeof(T),
+                                                    &CustomCall::trampoline, custom_.get()),
+                       "allreduce");
+      return;
+    }
     a_ = checkHandle(create(ctx->handle(), p.data(), (int)p.size(), count, DType<T>::value,
                             fn->type(), streams.empty() ? nullptr : streams.data(),
                             (int)streams.size()),
@@ -268,7 +316,15 @@ class DeviceAllreduce : public Algorithm {
 
  public:
   ~DeviceAllreduce() override { glx_algorithm_destroy(a_); }
-  void run() override { check(glx_algorithm_run(a_), "run"); }
+  void run() override {
+    const int rc = glx_algorithm_run(a_);
+    if (custom_ && custom_->error) {  // the function's own exception, not a glx error
+      std::exception_ptr e = custom_->error;
+      custom_->error = nullptr;
+      std::rethrow_exception(e);
+    }
+    check(rc, "run");
+  }
   int64_t bytesSentPerRun() const { return glx_algorithm_bytes_sent(a_); }
   // GLX_ENGINE_STEPS / _ONESHOT / _TWOSHOT / _DEVSTEPS / _DMASTEPS (glx.h)
   int engine() const { return glx_algorithm_engine(a_); }
@@ -300,7 +356,24 @@ class DeviceAllreduce : public Algorithm {
   }
 
  private:
+  // glx_reduce_fn -> the CUSTOM function: x = f(x, y) is the host program's
+  // c = f(a = c, b); the first exception it throws is kept and rethrown by
+  // run() (never unwound through the C ABI)
+  struct CustomCall {
+    const ReductionFunction<T>* fn;
+    std::exception_ptr error;
+    static void trampoline(void* user, void* c, const void*, const void* b, size_t n) {
+      CustomCall* call = static_cast<CustomCall*>(user);
+      if (call->error) return;
+      try {
+        call->fn->call(static_cast<T*>(c), static_cast<const T*>(b), n);
+      } catch (...) {
+        call->error = std::current_exception();
+      }
+    }
+  };
   glx_algorithm* a_ = nullptr;
+  std::unique_ptr<CustomCall> custom_;
 };
 }  // namespace detail
 
@@ -386,7 +459,7 @@ class HipAllreduceRingChunked : public detail::DeviceAllreduce<T> {
                                    : schedule == Schedule::REPLICATED ? &detail::createRepl
                                    : schedule == Schedule::RING       ? &detail::createRing
                                                                       : &detail::createAuto,
-                                   ctx, ptrs, count, streams, fn) {}
+                                   ctx, ptrs, count, streams, fn, GLX_ALGO_RING_CHUNKED) {}
 };
 
 // gloo::CudaAllreduceHalvingDoubling<T, W> analog (gloo/cuda_allreduce_halving_doubling.h:22-30).
@@ -399,7 +472,7 @@ class HipAllreduceHalvingDoubling : public detail::DeviceAllreduce<T> {
                               const std::vector<glx_stream_t>& streams = {},
                               const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
       : detail::DeviceAllreduce<T>(&glx_allreduce_halving_doubling_create, ctx, ptrs, count,
-                                   streams, fn) {}
+                                   streams, fn, GLX_ALGO_HALVING_DOUBLING) {}
   // the CUDA constructor's pipelineBroadcastAndReduce: recorded, same result
   // (the device-driven schedule overlaps its steps either way)
   HipAllreduceHalvingDoubling(const std::shared_ptr<Context>& ctx,
@@ -505,14 +578,18 @@ void min(void* c, const void* a, const void* b, size_t n) {
   check(glx_reduce(GLX_MIN, DType<T>::value, c, a, b, n, nullptr), "min");
 }
 
-// gloo::AllreduceOptions (gloo/allreduce.h:89-193) for device buffers.  The
-// reduction is one of the gloo/math.h ops: pass &gloo_amd::sum<T> (the
-// reference's idiom, allreduce_test.cc:380-383), a ReductionFunction<T>, or a
-// ReductionType.  setStream() is an addition: without it allreduce() returns
-// with the outputs complete, like the reference.
+// gloo::AllreduceOptions (gloo/allreduce.h:89-193).  The reduction is one of
+// the gloo/math.h ops -- pass &gloo_amd::sum<T> (the reference's idiom,
+// allreduce_test.cc:380-383), a ReductionFunction<T>, or a ReductionType --
+// on device (or staged host) buffers; or, as the reference's Func
+// (gloo/allreduce.h:36,69), any other c = f(a, b) callable on HOST buffers,
+// run on the host in the reference's order (glx_allreduce_host_fn).
+// setStream() is an addition: without it allreduce() returns with the
+// outputs complete, like the reference.
 class AllreduceOptions {
  public:
-  using Func = void (*)(void*, const void*, const void*, size_t);
+  using Func = std::function<void(void*, const void*, const void*, size_t)>;
+  using MathFn = void (*)(void*, const void*, const void*, size_t);
   enum Algorithm {
     UNSPECIFIED = GLX_ALLREDUCE_UNSPECIFIED,
     RING = GLX_ALLREDUCE_RING,
@@ -572,37 +649,58 @@ class AllreduceOptions {
  private:
   template <typename T>
   void setType(size_t elements) {
-    dtype_ = DType<T>::value;
+    dtype_ = DTypeOrNone<T>::value;
+    elementSize_ = sizeof(T);
     elements_ = elements;
   }
   template <typename T>
-  static int opOf(Func f) {
-    if (f == static_cast<Func>(&sum<T>)) return GLX_SUM;
-    if (f == static_cast<Func>(&product<T>)) return GLX_PRODUCT;
-    if (f == static_cast<Func>(&max<T>)) return GLX_MAX;
-    if (f == static_cast<Func>(&min<T>)) return GLX_MIN;
+  static int opOf(MathFn f) {
+    if (f == static_cast<MathFn>(&sum<T>)) return GLX_SUM;
+    if (f == static_cast<MathFn>(&product<T>)) return GLX_PRODUCT;
+    if (f == static_cast<MathFn>(&max<T>)) return GLX_MAX;
+    if (f == static_cast<MathFn>(&min<T>)) return GLX_MIN;
     return -1;
   }
+  // the device op of a gloo/math.h function of the buffers' type; -1 for any
+  // other function (a host Func)
   int resolveOp() const {
-    if (fn_ == nullptr) return op_ < 0 ? GLX_SUM : op_;
+    if (!fn_) return op_ < 0 ? GLX_SUM : op_;
+    const MathFn* t = fn_.target<MathFn>();
+    if (t == nullptr || *t == nullptr) return -1;
     switch (dtype_) {
-      case GLX_INT8: return opOf<int8_t>(fn_);
-      case GLX_UINT8: return opOf<uint8_t>(fn_);
-      case GLX_INT32: return opOf<int32_t>(fn_);
-      case GLX_INT64: return opOf<int64_t>(fn_);
-      case GLX_UINT64: return opOf<uint64_t>(fn_);
-      case GLX_FLOAT32: return opOf<float>(fn_);
-      case GLX_FLOAT64: return opOf<double>(fn_);
-      case GLX_FLOAT16: return opOf<float16>(fn_);
-      case GLX_BFLOAT16: return opOf<bfloat16>(fn_);
+      case GLX_INT8: return opOf<int8_t>(*t);
+      case GLX_UINT8: return opOf<uint8_t>(*t);
+      case GLX_INT32: return opOf<int32_t>(*t);
+      case GLX_INT64: return opOf<int64_t>(*t);
+      case GLX_UINT64: return opOf<uint64_t>(*t);
+      case GLX_FLOAT32: return opOf<float>(*t);
+      case GLX_FLOAT64: return opOf<double>(*t);
+      case GLX_FLOAT16: return opOf<float16>(*t);
+      case GLX_BFLOAT16: return opOf<bfloat16>(*t);
     }
     return -1;
   }
+  // glx_reduce_fn -> the caller's Func; the first exception it throws is
+  // kept (never unwound through the C ABI) and rethrown by allreduce()
+  struct HostCall {
+    const Func* fn;
+    std::exception_ptr error;
+    static void trampoline(void* user, void* c, const void* a, const void* b, size_t n) {
+      HostCall* call = static_cast<HostCall*>(user);
+      if (call->error) return;
+      try {
+        (*call->fn)(c, a, b, n);
+      } catch (...) {
+        call->error = std::current_exception();
+      }
+    }
+  };
 
   std::shared_ptr<Context> context_;
   int algorithm_ = UNSPECIFIED;
   std::vector<void*> in_, out_;
   size_t elements_ = 0;
+  size_t elementSize_ = 0;
   int dtype_ = -1;
   Func fn_ = nullptr;
   int op_ = -1;
@@ -618,9 +716,22 @@ class AllreduceOptions {
 inline void allreduce(const AllreduceOptions& opts) {
   const int op = opts.resolveOp();
   if (op < 0) {
-    throw EnforceNotMet(
-        "allreduce: only the gloo/math.h reductions (sum, product, max, min of the "
-        "buffers' type) run on the device");
+    // a host Func: host buffers, no stream (glx_allreduce_host_fn refuses
+    // device buffers with a message)
+    if (opts.stream_ != nullptr) {
+      throw EnforceNotMet("allreduce: a caller's reduce function runs on the host, with "
+                          "host buffers; there is no stream to order it on");
+    }
+    AllreduceOptions::HostCall call{&opts.fn_, nullptr};
+    const int rc = glx_allreduce_host_fn(
+        opts.context_->handle(), opts.algorithm_, opts.elementSize_,
+        &AllreduceOptions::HostCall::trampoline, &call,
+        opts.in_.empty() ? nullptr : opts.in_.data(), (int)opts.in_.size(), opts.out_.data(),
+        (int)opts.out_.size(), opts.elements_, opts.tag_, opts.maxSegmentSize_,
+        (int64_t)opts.timeout_.count());
+    if (call.error) std::rethrow_exception(call.error);
+    check(rc, "allreduce");
+    return;
   }
   check(glx_allreduce(opts.context_->handle(), opts.algorithm_, opts.dtype_, op,
                       opts.in_.data(), (int)opts.in_.size(), opts.out_.data(),

@@ -13,7 +13,11 @@
 //                   &sum<uint64_t>, in place or not, maxSegmentSize 128
 //                   (gloo/test/allreduce_test.cc:306-378); TestTimeout (:386-402)
 //
-// Exit status 0 = all passed.  Needs a GPU (all ranks share device 0).
+//   --host-fn       gloo::allreduce(opts) with a caller's Func on host
+//                   buffers (no GPU needed)
+//
+// Exit status 0 = all passed.  Needs a GPU (all ranks share device 0), except
+// --host-fn.
 #include <hip/hip_runtime_api.h>
 
 #include <cmath>
@@ -398,6 +402,158 @@ void streamsAndEvents(int P, int N) {
   });
 }
 
+// gloo::allreduce(opts) with a caller's Func (gloo/allreduce.h:36,69) on HOST
+// buffers through the header: a capturing lambda c = a | b over 32-bit words
+// (order-independent, so the expected value is plain), inputs or in place,
+// several outputs, RING and BCUBE, two calls; a throwing Func comes back out
+// of allreduce() on every rank; a stream is refused.  Needs no GPU.
+int hostFn() {
+  for (auto algo : {gloo_amd::AllreduceOptions::RING, gloo_amd::AllreduceOptions::BCUBE}) {
+    for (int P : {1, 3, 4}) {
+      for (int nin : {0, 2}) {
+        const size_t N = 4099;
+        gloo_amd::rendezvous::HashStore store;
+        std::vector<std::thread> ts;
+        std::vector<std::string> errs(P);
+        std::vector<std::vector<uint32_t>> outs(P);
+        auto in = [](int r, int i, size_t j) { return (uint32_t)(1u << ((r * 3 + i + j) % 31)); };
+        for (int r = 0; r < P; r++) {
+          ts.emplace_back([&, r] {
+            try {
+              auto ctx = std::make_shared<gloo_amd::Context>(r, P, -1);
+              if (P > 1) ctx->connectFullMesh(store);
+              const uint32_t mask = 0xffffffffu;  // captured state: a std::function, not a pointer
+              for (int call = 0; call < 2; call++) {
+                std::vector<std::vector<uint32_t>> ins(nin, std::vector<uint32_t>(N));
+                for (int i = 0; i < nin; i++) {
+                  for (size_t j = 0; j < N; j++) ins[i][j] = in(r, i, j);
+                }
+                std::vector<uint32_t> o0(N), o1(N, 7);
+                for (size_t j = 0; j < N; j++) o0[j] = nin ? 0 : in(r, 0, j);
+                std::vector<uint32_t*> ip, op{o0.data(), o1.data()};
+                for (auto& v : ins) ip.push_back(v.data());
+                gloo_amd::AllreduceOptions opts(ctx);
+                opts.setAlgorithm(algo);
+                if (nin) opts.setInputs(ip, N);
+                opts.setOutputs(op, N);
+                opts.setReduceFunction([mask](void* c, const void* a, const void* b, size_t n) {
+                  const uint32_t* x = static_cast<const uint32_t*>(a);
+                  const uint32_t* y = static_cast<const uint32_t*>(b);
+                  uint32_t* z = static_cast<uint32_t*>(c);
+                  for (size_t i = 0; i < n; i++) z[i] = (x[i] | y[i]) & mask;
+                });
+                gloo_amd::allreduce(opts);
+                outs[r] = o1;
+                if (std::memcmp(o0.data(), o1.data(), N * 4) != 0) errs[r] = "outputs differ";
+              }
+            } catch (const std::exception& e) {
+              errs[r] = e.what();
+            }
+          });
+        }
+        for (auto& t : ts) t.join();
+        size_t bad = 0;
+        for (int r = 0; r < P; r++) {
+          EXPECT(errs[r].empty(), "host Func P=%d nin=%d rank %d: %s", P, nin, r, errs[r].c_str());
+          for (size_t j = 0; j < N; j++) {
+            uint32_t e = 0;
+            for (int q = 0; q < P; q++) {
+              if (nin) {
+                for (int i = 0; i < nin; i++) e |= in(q, i, j);
+              } else {  // no inputs: every output's old contents are reduced (o1 holds 7)
+                e |= in(q, 0, j) | 7u;
+              }
+            }
+            bad += outs[r][j] != e;
+          }
+        }
+        EXPECT(bad == 0, "host Func P=%d nin=%d: %zu wrong elements", P, nin, bad);
+      }
+    }
+  }
+  // the ring-chunked and halving-doubling classes with a CUSTOM
+  // ReductionFunction (x |= y) on host buffers, two pointers, two runs
+  static const gloo_amd::ReductionFunction<int32_t> orFn(
+      gloo_amd::CUSTOM, [](int32_t* x, const int32_t* y, size_t n) {
+        for (size_t i = 0; i < n; i++) x[i] |= y[i];
+      });
+  for (bool hd : {false, true}) {
+    for (int P : {1, 3, 5}) {
+      const int N = 1000;
+      gloo_amd::rendezvous::HashStore store;
+      std::vector<std::thread> ts;
+      std::vector<std::string> errs(P);
+      std::vector<std::vector<std::vector<int32_t>>> bufs(P);
+      auto v = [](int r, int i, int j) { return (int32_t)(1u << ((r * 5 + i * 3 + j) % 31)); };
+      for (int r = 0; r < P; r++) {
+        ts.emplace_back([&, r] {
+          try {
+            auto ctx = std::make_shared<gloo_amd::Context>(r, P, -1);
+            if (P > 1) ctx->connectFullMesh(store);
+            bufs[r].assign(2, std::vector<int32_t>(N));
+            std::vector<int32_t*> ptrs{bufs[r][0].data(), bufs[r][1].data()};
+            std::unique_ptr<gloo_amd::Algorithm> a;
+            if (hd) {
+              a.reset(new gloo_amd::HipAllreduceHalvingDoubling<int32_t>(ctx, ptrs, N, {}, &orFn));
+            } else {
+              a.reset(new gloo_amd::HipAllreduceRingChunked<int32_t>(ctx, ptrs, N, {}, &orFn));
+            }
+            for (int run = 0; run < 2; run++) {
+              for (int i = 0; i < 2; i++) {
+                for (int j = 0; j < N; j++) bufs[r][i][j] = v(r, i, j);
+              }
+              a->run();
+            }
+          } catch (const std::exception& e) {
+            errs[r] = e.what();
+          }
+        });
+      }
+      for (auto& t : ts) t.join();
+      size_t bad = 0;
+      for (int r = 0; r < P; r++) {
+        EXPECT(errs[r].empty(), "CUSTOM class %s P=%d rank %d: %s", hd ? "hd" : "ring", P, r,
+               errs[r].c_str());
+        if (!errs[r].empty()) continue;
+        for (int i = 0; i < 2; i++) {
+          for (int j = 0; j < N; j++) {
+            int32_t e = 0;
+            for (int q = 0; q < P; q++) e |= v(q, 0, j) | v(q, 1, j);
+            bad += bufs[r][i][j] != e;
+          }
+        }
+      }
+      EXPECT(bad == 0, "CUSTOM class %s P=%d: %zu wrong elements", hd ? "hd" : "ring", P, bad);
+    }
+  }
+  {  // a throwing Func, and a stream, with one rank
+    auto ctx = std::make_shared<gloo_amd::Context>(0, 1, -1);
+    std::vector<int32_t> a(8, 1), b(8, 2);
+    gloo_amd::AllreduceOptions opts(ctx);
+    opts.setOutputs(std::vector<int32_t*>{a.data(), b.data()}, 8);
+    opts.setReduceFunction([](void*, const void*, const void*, size_t) {
+      throw std::runtime_error("boom");
+    });
+    bool thrown = false;
+    try {
+      gloo_amd::allreduce(opts);
+    } catch (const std::runtime_error& e) {
+      thrown = std::string(e.what()) == "boom";
+    }
+    EXPECT(thrown, "the Func's exception must come back out of allreduce()");
+    opts.setStream(reinterpret_cast<glx_stream_t>(1));
+    bool refused = false;
+    try {
+      gloo_amd::allreduce(opts);
+    } catch (const gloo_amd::EnforceNotMet&) {
+      refused = true;
+    }
+    EXPECT(refused, "a host Func with a stream must be refused");
+  }
+  if (g_failures == 0) std::printf("dropin_test --host-fn: all passed\n");
+  return g_failures == 0 ? 0 : 1;
+}
+
 }  // namespace
 
 // The SURVEY 8 contract's cases by default; `--widening`: only the round-4
@@ -424,6 +580,7 @@ int widening(int argc, char** argv) {
 
 int main(int argc, char** argv) {
   if (argc > 1 && std::strcmp(argv[1], "--widening") == 0) return widening(argc, argv);
+  if (argc > 1 && std::strcmp(argv[1], "--host-fn") == 0) return hostFn();
   for (int P : {1, 2, 4}) streamsAndEvents(P, 100003);
   for (int P = 1; P <= 8; P++) {
     for (int N : {0, 4, 100, 1000, 10000}) {

@@ -21,6 +21,16 @@ def test_dropin_header_compiles(tmp_path):
     build(str(tmp_path / "dropin_test"))
 
 
+def test_dropin_host_function_allreduce(tmp_path):
+    """gloo_amd::allreduce(opts) with a capturing lambda on host buffers
+    (glx_allreduce_host_fn through the header): no GPU needed."""
+    exe = str(tmp_path / "dropin_test")
+    build(exe)
+    p = subprocess.run([exe, "--host-fn"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "all passed" in p.stdout
+
+
 @pytest.mark.gpu
 def test_dropin_reference_cases_on_gpu(tmp_path):
     exe = str(tmp_path / "dropin_test")
