@@ -135,8 +135,8 @@ STORE_SET_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_char_p,
                                 ctypes.c_void_p, ctypes.c_size_t)
 STORE_GET_FN = ctypes.CFUNCTYPE(ctypes.c_int64, ctypes.c_void_p, ctypes.c_char_p,
                                 ctypes.c_void_p, ctypes.c_size_t)
-# glx_reduce_fn: (user, c, a, b, n)
-REDUCE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+# glx_reduce_fn: (user, c, a, b, n) -> 0, or nonzero when the function failed
+REDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                              ctypes.c_void_p, ctypes.c_size_t)
 
 # status codes (glx_status), and GLX_NOT_READY of glx_event_query

@@ -209,11 +209,13 @@ class Algorithm:
 
         def trampoline(user, c, a, b, n):
             if errors:
-                return
+                return 1
             try:
                 fn.call(c, b, n)  # c == a: x = f(x, y)
             except BaseException as e:  # noqa: BLE001 - re-raised by run()
                 errors.append(e)
+                return 1  # the run stops here (glx.h glx_reduce_fn)
+            return 0
         self._hostfn = (_lib.REDUCE_FN(trampoline), errors)
         self._h = check_handle(
             lib.glx_allreduce_create_host_fn(

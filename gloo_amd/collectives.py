@@ -192,10 +192,14 @@ def _allreduce_host_fn(opts):
     errors = []
 
     def tramp(_user, c, a, b, n):
+        if errors:
+            return 1
         try:
             user_fn(c, a, b, n)
         except BaseException as e:  # noqa: BLE001 - re-raised after the call
             errors.append(e)
+            return 1  # the call stops here (glx.h glx_reduce_fn)
+        return 0
     cb = _REDUCE_FN(tramp)
     iarr, ni = opts._in_ptrs if opts._inputs else ((ctypes.c_void_p * 1)(), 0)
     oarr, no = opts._out_ptrs

@@ -12,6 +12,7 @@
 #include <cerrno>
 #include <cstdio>
 #include <cstring>
+#include <stdexcept>
 #include <thread>
 
 #include "common.h"
@@ -268,6 +269,14 @@ void HostFnExecutor::call(HostReduceFn fn, void* user, const std::vector<const v
   GLX_ENFORCE(fn != nullptr, "host-fn allreduce: null reduction function");
   GLX_ENFORCE(!out.empty(), "host-fn allreduce: at least one output is required");
   if (elements_ == 0) return;
+  // every call of the caller's function; a failure stops this rank's call
+  // here (its peers then time out waiting, as in the reference)
+  auto f = [&](void* c, const void* a, const void* b, size_t n) {
+    if (fn(user, c, a, b, n) != 0) {
+      broken_ = true;
+      throw std::invalid_argument("allreduce: the reduction function failed");
+    }
+  };
   const size_t bytes = elements_ * es_;
   char* out0 = static_cast<char*>(out[0]);
   // local reduction of the inputs into out[0] (gloo/allreduce.cc:44-82),
@@ -276,10 +285,10 @@ void HostFnExecutor::call(HostReduceFn fn, void* user, const std::vector<const v
   if (in.size() == 1) {
     if (in[0] != out0) std::memcpy(out0, in[0], bytes);
   } else if (in.size() >= 2) {
-    fn(user, out0, in[0], in[1], elements_);
-    for (size_t i = 2; i < in.size(); i++) fn(user, out0, out0, in[i], elements_);
+    f(out0, in[0], in[1], elements_);
+    for (size_t i = 2; i < in.size(); i++) f(out0, out0, in[i], elements_);
   } else {
-    for (size_t i = 1; i < out.size(); i++) fn(user, out0, out0, out[i], elements_);
+    for (size_t i = 1; i < out.size(); i++) f(out0, out0, out[i], elements_);
   }
   if (contextSize_ > 1) {
     const auto wait = timeout.count() > 0 ? timeout : context_->getTimeout();
@@ -314,7 +323,7 @@ void HostFnExecutor::call(HostReduceFn fn, void* user, const std::vector<const v
           break;
         }
         case glx::REDUCE:  // out = f(out, tmp) (:292-296, :586-592)
-          fn(user, dst, dst, region_ + (size_t)s.boff * es_, (size_t)s.len);
+          f(dst, dst, region_ + (size_t)s.boff * es_, (size_t)s.len);
           break;
         case glx::COPY:
           std::memcpy(dst, region_ + (size_t)s.boff * es_, len);
@@ -328,9 +337,9 @@ void HostFnExecutor::call(HostReduceFn fn, void* user, const std::vector<const v
           const bool left = (s.flags & glx::kFoldLeft) != 0;
           for (size_t k = 1; k < srcs.size(); k++) {
             if (left) {
-              fn(user, dst, dst, src(srcs[k]), (size_t)s.len);
+              f(dst, dst, src(srcs[k]), (size_t)s.len);
             } else {
-              fn(user, dst, src(srcs[k]), dst, (size_t)s.len);
+              f(dst, src(srcs[k]), dst, (size_t)s.len);
             }
           }
           break;

@@ -37,8 +37,9 @@
 
 namespace gloo {
 
-// c = f(a, b) over n elements, as the reference's Func; `user` passed through.
-using HostReduceFn = void (*)(void* user, void* c, const void* a, const void* b, size_t n);
+// c = f(a, b) over n elements, as the reference's Func; `user` passed through;
+// nonzero = the function failed (glx.h glx_reduce_fn): the call stops.
+using HostReduceFn = int (*)(void* user, void* c, const void* a, const void* b, size_t n);
 
 class HostFnExecutor : public Algorithm {
  public:

@@ -362,14 +362,16 @@ class DeviceAllreduce : public Algorithm {
   struct CustomCall {
     const ReductionFunction<T>* fn;
     std::exception_ptr error;
-    static void trampoline(void* user, void* c, const void*, const void* b, size_t n) {
+    static int trampoline(void* user, void* c, const void*, const void* b, size_t n) {
       CustomCall* call = static_cast<CustomCall*>(user);
-      if (call->error) return;
+      if (call->error) return 1;
       try {
         call->fn->call(static_cast<T*>(c), static_cast<const T*>(b), n);
       } catch (...) {
         call->error = std::current_exception();
+        return 1;
       }
+      return 0;
     }
   };
   glx_algorithm* a_ = nullptr;
@@ -685,14 +687,16 @@ class AllreduceOptions {
   struct HostCall {
     const Func* fn;
     std::exception_ptr error;
-    static void trampoline(void* user, void* c, const void* a, const void* b, size_t n) {
+    static int trampoline(void* user, void* c, const void* a, const void* b, size_t n) {
       HostCall* call = static_cast<HostCall*>(user);
-      if (call->error) return;
+      if (call->error) return 1;
       try {
         (*call->fn)(c, a, b, n);
       } catch (...) {
         call->error = std::current_exception();
+        return 1;
       }
+      return 0;
     }
   };
 

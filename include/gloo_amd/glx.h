@@ -411,7 +411,12 @@ int glx_allreduce(glx_context* ctx, int algorithm, int dtype, int op,
  * reference's AllreduceOptions::Func (gloo/allreduce.h:36,69,171), which may
  * be any host std::function (bitwise ops, user types, non-commutative ops);
  * `user` is passed through. */
-typedef void (*glx_reduce_fn)(void* user, void* c, const void* a, const void* b, size_t n);
+typedef int (*glx_reduce_fn)(void* user, void* c, const void* a, const void* b, size_t n);
+/* It returns 0, or nonzero when it failed (a C++ wrapper caught an exception
+ * it must not unwind through this ABI): the call then stops at once with
+ * GLX_ERR_INVALID on that rank and reduces nothing more -- its peers wait
+ * for messages that never come and fail with GLX_ERR_TIMEOUT, as the
+ * reference's ranks do when one rank's Func throws. */
 /* gloo::allreduce(opts) with such a function, on HOST buffers: the same step
  * program as glx_allreduce (RING, or BCUBE; UNSPECIFIED = RING) run on the
  * host -- messages through shared memory, every reduction a call of `fn` in

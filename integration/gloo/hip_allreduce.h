@@ -409,14 +409,16 @@ template <typename T>
 struct ClassFnCall {
   const ReductionFunction<T>* fn;
   std::exception_ptr error;
-  static void trampoline(void* user, void* c, const void* /*a == c*/, const void* b, size_t n) {
+  static int trampoline(void* user, void* c, const void* /*a == c*/, const void* b, size_t n) {
     ClassFnCall* call = static_cast<ClassFnCall*>(user);
-    if (call->error) return;
+    if (call->error) return 1;
     try {
       call->fn->call(static_cast<T*>(c), static_cast<const T*>(b), n);
     } catch (...) {
       call->error = std::current_exception();
+      return 1;
     }
+    return 0;
   }
 };
 
@@ -537,14 +539,16 @@ inline size_t glxElementSize(int dtype) {
 struct HostFnCall {
   const AllreduceOptions::Func* fn;
   std::exception_ptr error;
-  static void trampoline(void* user, void* c, const void* a, const void* b, size_t n) {
+  static int trampoline(void* user, void* c, const void* a, const void* b, size_t n) {
     HostFnCall* call = static_cast<HostFnCall*>(user);
-    if (call->error) return;
+    if (call->error) return 1;
     try {
       (*call->fn)(c, a, b, n);
     } catch (...) {
       call->error = std::current_exception();
+      return 1;
     }
+    return 0;
   }
 };
 

@@ -146,6 +146,39 @@ def test_custom_function_exception_propagates():
         gloo_amd.allreduce(opts)
 
 
+def test_a_failing_function_stops_the_call_and_its_peers_time_out():
+    """Rank 0's function raises on its first call: rank 0's allreduce stops
+    there and raises that exception; rank 1, whose function is fine, gets
+    no result built from rank 0's unreduced data -- it waits for a message
+    that never comes and raises IoException ("Timed out ..."), as the
+    reference's ranks do when one rank's Func throws."""
+    P = 2
+    store = gloo_amd.rendezvous.HashStore()
+    got = [None] * P
+
+    def body(r):
+        def fn(c, a, b, n):
+            if r == 0:
+                raise ValueError("rank 0 fails")
+            custom_fn(OR)(c, a, b, n)
+        try:
+            ctx = gloo_amd.rendezvous.Context(r, P)
+            ctx.setTimeout(2)
+            ctx.connectFullMesh(store)
+            opts = gloo_amd.AllreduceOptions(ctx)
+            opts.setOutputs([np.arange(4096, dtype=np.int32)])
+            opts.setReduceFunction(fn)
+            gloo_amd.allreduce(opts)
+            got[r] = "returned"
+        except BaseException as e:  # noqa: BLE001
+            got[r] = e
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(P)]
+    [t.start() for t in ts]
+    [t.join(60) for t in ts]
+    assert isinstance(got[0], ValueError) and "rank 0 fails" in str(got[0]), got
+    assert isinstance(got[1], gloo_amd.IoException) and "Timed out" in str(got[1]), got
+
+
 @pytest.mark.parametrize("P", [3, pytest.param(2, marks=pytest.mark.gpu),
                                pytest.param(4, marks=pytest.mark.gpu)])
 def test_custom_function_one_process_per_rank(P):
