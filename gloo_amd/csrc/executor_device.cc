@@ -389,10 +389,6 @@ void HipPlanExecutor::setupDevSteps() {
   GLX_HIP_CHECK(hipMemcpy(devSegs_, segs.data(), segs.size() * sizeof(glx::DevSegment),
                           hipMemcpyHostToDevice));
   pk_.segs = devSegs_;
-  {  // GLOO_AMD_POLL=load: flag polls by loads (an A/B switch; default cas)
-    const char* e = std::getenv("GLOO_AMD_POLL");
-    pk_.pollLoad = e != nullptr && std::string(e) == "load" ? 1 : 0;
-  }
   for (size_t k = 0; k < in_.size(); k++) in_[k].deliveryWord = (uint32_t)k;
   for (size_t k = 0; k < out_.size(); k++) out_[k].creditWord = (uint32_t)(in_.size() + k);
   const size_t rows = std::max<size_t>(1, in_.size() + out_.size());

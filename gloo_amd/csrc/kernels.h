@@ -208,8 +208,6 @@ struct PlanKernelParams {
   int* claim;
   int narrow;                  // 1: narrow release / acquire around flags (below)
   int flagStore;               // 1: write peers' flags with stores (Context::flagStores)
-  int pollLoad;                // 1: poll flags with system-scope loads instead of
-                               // compare-exchanges (GLOO_AMD_POLL=load; an A/B switch)
   int fast;                    // 1: nontemporal loads, write-through stores (plan kernel only;
                                // every span's stores stay below kWtMaxStream: setupDevSteps)
   // diagnostics (GLOO_AMD_DEVTRACE=1): [G][2 * nsteps + 1] s_memrealtime

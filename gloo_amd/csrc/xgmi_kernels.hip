@@ -350,12 +350,6 @@ __device__ __forceinline__ uint64_t get_flag(const uint64_t* word) {
   return v;
 }
 
-// A poll by a system-scope load: the flag block is uncached (MTYPE UC), so
-// the load goes to memory like the compare-exchange, as a read request.
-__device__ __forceinline__ uint64_t load_flag(const uint64_t* word) {
-  return __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 __device__ __forceinline__ uint64_t* flag_at(uint64_t* row, int w) {
   return row + (size_t)w * kFlagStride;
 }
@@ -459,13 +453,12 @@ __device__ __forceinline__ void report_timeout(int* status, int* claim, int code
 __device__ __forceinline__ bool wait_flag(const uint64_t* word, uint64_t epoch, int peer,
                                           uint64_t start, uint64_t timeoutTicks, int* status,
                                           int* claim, int* s_ok, int sync, bool acquire = true,
-                                          int where = 0, uint32_t* polls = nullptr,
-                                          bool loadPoll = false) {
+                                          int where = 0, uint32_t* polls = nullptr) {
   if (threadIdx.x == 0) {
     int ok = 1;
     uint64_t v;
     uint32_t spin = 1;
-    for (; (v = loadPoll ? load_flag(word) : get_flag(word)) < epoch; spin++) {
+    for (; (v = get_flag(word)) < epoch; spin++) {
       if (__builtin_amdgcn_s_memrealtime() - start > timeoutTicks) {
         ok = 0;
         report_timeout(status, claim, 1 + peer + 256 * where, v, epoch);
@@ -745,7 +738,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
         if (seq > (uint64_t)p.slots &&
             !wait_flag(flag_at(st.credit, w), seq - p.slots, st.peer,
                        __builtin_amdgcn_s_memrealtime(), p.timeoutTicks, p.status, p.claim,
-                       &s_ok, sync, /*acquire=*/false, 1 + i, &polls, p.pollLoad != 0)) {
+                       &s_ok, sync, /*acquire=*/false, 1 + i, &polls)) {
           return;
         }
         stamp(2 * i + 1);
@@ -782,7 +775,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
         if (seq > (uint64_t)p.slots &&
             !wait_flag(flag_at(st.credit, w), seq - p.slots, st.peer,
                        __builtin_amdgcn_s_memrealtime(), p.timeoutTicks, p.status, p.claim,
-                       &s_ok, sync, /*acquire=*/false, 1 + i, &polls, p.pollLoad != 0)) {
+                       &s_ok, sync, /*acquire=*/false, 1 + i, &polls)) {
           return;
         }
         stamp(2 * i + 1);
@@ -818,8 +811,7 @@ __device__ __forceinline__ void plan_body(const PlanKernelParams& p) {
       }
       case 1:  // RECV
         if (!wait_flag(flag_at(st.flag, w), seq, st.peer, __builtin_amdgcn_s_memrealtime(),
-                       p.timeoutTicks, p.status, p.claim, &s_ok, sync, true, 1 + i, &polls,
-                       p.pollLoad != 0)) {
+                       p.timeoutTicks, p.status, p.claim, &s_ok, sync, true, 1 + i, &polls)) {
           return;
         }
         stamp(2 * i + 1);
