@@ -1212,8 +1212,14 @@ def run_soak(store_dir, rank, size, runs, uneven="", n=1 << 20):
         g.manual_seed(1000003 * it + r)
         return torch.randint(-64, 64, (n,), generator=g, device=dev, dtype=torch.int32)
 
-    bufs = {k: torch.empty(n, dtype=torch.float32, device=dev)
-            for k in ("ring", "hd", "mesh", "repl", "ring_host", "ring_dma", "hd_dma")}
+    # above 32 MiB per rank the automatic choice for processes sharing a GPU
+    # runs the ring on host-issued steps (executor_device.cc kDevStepsMaxBytes):
+    # "ring_dev" keeps the plan kernel there too (the north star's engine at
+    # its own size, e.g. the release-side control at 2^26)
+    big = n * 4 > (32 << 20)
+    keys = ("ring", "hd", "mesh", "repl", "ring_host", "ring_dma", "hd_dma") + (
+        ("ring_dev",) if big else ())
+    bufs = {k: torch.empty(n, dtype=torch.float32, device=dev) for k in keys}
     algs = {
         "ring": gloo_amd.AllreduceRingChunked(ctx, [bufs["ring"]], schedule="ring"),
         "hd": gloo_amd.AllreduceHalvingDoubling(ctx, [bufs["hd"]]),
@@ -1236,6 +1242,13 @@ def run_soak(store_dir, rank, size, runs, uneven="", n=1 << 20):
         algs["hd_dma"] = gloo_amd.AllreduceHalvingDoubling(ctx, [bufs["hd_dma"]])
     finally:
         gloo_amd.set_steps_engine("auto")
+    if big:
+        gloo_amd.set_steps_engine("device")
+        try:
+            algs["ring_dev"] = gloo_amd.AllreduceRingChunked(ctx, [bufs["ring_dev"]],
+                                                             schedule="ring")
+        finally:
+            gloo_amd.set_steps_engine("auto")
     engines = {k: a.engine() for k, a in algs.items()}
     rng = random.Random(rank)
     side = torch.cuda.Stream() if uneven == "uneven" and rank == 0 else None

@@ -20,7 +20,11 @@ the checks catch on one GPU:
   wave of the workgroup and the flag can overtake the other waves' stores:
   the two-shot mesh wrong in 91-100 of 100 runs on every rank at P = 4 and 8
   (the plan kernel's ring and halving-doubling in 0-2; 16 M elements: the
-  mesh in 25-46; profiles/round6/sync_control_release_1M_16M.json).
+  mesh in 25-46; profiles/round6/sync_control_release_1M_16M.json);
+* at the north-star size (2^26 elements per rank) the plan kernel's own ring
+  -- the north star's engine -- is wrong in 29-30 of 30 runs on every rank
+  without the release, and exact with it (profiles/round6/
+  sync_control_release_64M_plan_kernel.json).
 """
 import os
 import re
@@ -35,6 +39,7 @@ from helpers import rank_env
 WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "mp_worker.py")
 SMALL = 4096
 LARGE = 1 << 20
+NORTH_STAR = 1 << 26  # 256 MiB fp32 per rank
 
 
 def small_soak(P, runs, sync, n=SMALL):
@@ -111,3 +116,18 @@ def test_large_buffer_soak_catches_a_missing_release(P):
     assert all(rc != 0 for rc in rcs), rcs
     for r, b in enumerate(bad):
         assert b.get("mesh", 0) >= runs // 2, (r, b)
+
+
+@pytest.mark.gpu
+def test_north_star_size_plan_kernel_exact_and_catches_a_missing_release():
+    """At the north star's 256 MiB per rank, P = 4: the plan kernel's ring
+    (mp_worker.py soak "ring_dev") exact under the product sync, and wrong in
+    (nearly) every run on every rank once the release is dropped."""
+    runs = 6
+    rcs, bad, eng, outs = small_soak(4, runs, "narrow", NORTH_STAR)
+    assert "'ring_dev': 'devsteps'" in eng, eng
+    assert rcs == [0] * 4 and all(b == {} for b in bad), (rcs, bad, outs[0][-2000:])
+    rcs, bad, eng, _ = small_soak(4, runs, "unsafe_norelease", NORTH_STAR)
+    assert all(rc != 0 for rc in rcs), rcs
+    for r, b in enumerate(bad):
+        assert b.get("ring_dev", 0) >= runs // 2, (r, b)
